@@ -1,0 +1,336 @@
+/*
+ * rpgpu.h — C-ABI boundary of the MI355X record-batch validation/decode engine.
+ *
+ * This is the drop-in boundary for Redpanda's batch hot path.
+ * Every entry point below replaces one reference interface; the reference
+ * file:line it stands in for is cited next to it (paths relative to
+ * /root/reference/src/v).  Plain pointers and sizes only — no HIP, torch or
+ * C++ types cross this boundary, and no exception ever does: every call
+ * returns an int status (0 = ok, <0 = rpgpu_status).
+ *
+ * Layouts of the per-batch result, the per-record index and the segment
+ * summary are part of the contract: the CPU oracle (oracle/) emits the same
+ * structs, so parity is a memcmp.
+ */
+#ifndef RPGPU_H_
+#define RPGPU_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ------------------------------------------------------------------------ */
+/* Constants                                                                 */
+/* ------------------------------------------------------------------------ */
+
+/* model::packed_record_batch_header_size (model/record.h:473-487): the
+ * comment there says 57 but the fields sum to 61. */
+#define RPGPU_HEADER_SIZE 61u
+/* kafka::internal::kafka_header_size (kafka/protocol/kafka_batch_adapter.h:25-37) */
+#define RPGPU_KAFKA_HEADER_SIZE 61u
+/* bytes of the Kafka CRC prefix rebuilt big-endian from the header
+ * (model/record_utils.cc:68-80: attrs..record_count) */
+#define RPGPU_CRC_PREFIX_SIZE 40u
+
+/* model::compression (model/compression.h:35-48) */
+enum rpgpu_codec {
+    RPGPU_CODEC_NONE = 0,
+    RPGPU_CODEC_GZIP = 1,
+    RPGPU_CODEC_SNAPPY = 2, /* snappy-java framing, falls back to raw snappy */
+    RPGPU_CODEC_LZ4 = 3,    /* LZ4 frame */
+    RPGPU_CODEC_ZSTD = 4,
+};
+
+/* storage::parser_errc (storage/parser_errc.h:18-25), same numbering. */
+enum rpgpu_parser_errc {
+    RPGPU_ERRC_NONE = 0,
+    RPGPU_ERRC_END_OF_STREAM = 1,
+    RPGPU_ERRC_HEADER_ONLY_CRC_MISSMATCH = 2,
+    RPGPU_ERRC_INPUT_STREAM_NOT_ENOUGH_BYTES = 3,
+    RPGPU_ERRC_FALLOCATED_FILE_READ_ZERO_BYTES_FOR_HEADER = 4,
+    RPGPU_ERRC_NOT_ENOUGH_BYTES_IN_PARSER_FOR_ONE_RECORD = 5,
+};
+
+/* Library status codes (return values). */
+enum rpgpu_status {
+    RPGPU_OK = 0,
+    RPGPU_E_INVALID = -1,      /* bad argument */
+    RPGPU_E_NO_DEVICE = -2,    /* no HIP device / HIP call failed */
+    RPGPU_E_NOMEM = -3,        /* device or host allocation failed */
+    RPGPU_E_OVERFLOW = -4,     /* caller-provided output capacity too small */
+    RPGPU_E_CODEC = -5,        /* uncompress failed (maps to std::runtime_error) */
+    RPGPU_E_UNSUPPORTED = -6,  /* codec not decoded by this engine (gzip/zstd) */
+    RPGPU_E_HIP = -7,          /* kernel launch / runtime error */
+};
+
+/* ------------------------------------------------------------------------ */
+/* Per-batch verdict flags (rpgpu_batch_result.flags).  Each bit is pinned    */
+/* to one reference function ("composite verdict").         */
+/* ------------------------------------------------------------------------ */
+#define RPGPU_F_HEADER_OK (1u << 0)      /* read_header_impl accepted: header_crc != 0 and == internal_header_only_crc (storage/parser.cc:139-176) */
+#define RPGPU_F_COMPLETE (1u << 1)       /* size_bytes-61 payload bytes present (storage/parser.cc:206-216) */
+#define RPGPU_F_CRC_OK (1u << 2)         /* (uint32)hdr.crc == crc32c(BE hdr40 ++ stored payload) (storage/log_replayer.cc:62-79, model/record_utils.cc:68-91) */
+#define RPGPU_F_COMPRESSED (1u << 3)     /* attrs codec != none */
+#define RPGPU_F_CODEC_INVALID (1u << 4)  /* codec value 5..7: record_batch_attributes::compression() throws (model/record.h:283-300) */
+#define RPGPU_F_CODEC_UNSUPPORTED (1u << 5) /* gzip/zstd: not decoded here (CPU fallback behind compressor::uncompress) */
+#define RPGPU_F_CODEC_OK (1u << 6)       /* compressor::uncompress succeeded (compression/compression.cc:34-55) */
+#define RPGPU_F_PARSED (1u << 7)         /* a record walk was run over the (decoded) payload */
+#define RPGPU_F_PARSE_ASYNC_OK (1u << 8) /* model::for_each_record completed without throwing (model/record.h:680-697) */
+#define RPGPU_F_PARSE_OK (1u << 9)       /* record_batch::for_each_record: no throw AND no trailing bytes (model/record.h:616-627) */
+#define RPGPU_F_INDEX_WRITTEN (1u << 10) /* record index entries [index_base, index_base+records_parsed) are valid */
+#define RPGPU_F_WIRE_V2 (1u << 11)       /* wire layout: magic == 2 (kafka/protocol/kafka_batch_adapter.cc:39-43) */
+#define RPGPU_F_DECODE_OVERFLOW (1u << 12) /* decoded bytes did not fit the reserved arena slot */
+
+/* rpgpu_batch_result.parse_err: why the record walk stopped (0 = no error). */
+enum rpgpu_parse_err {
+    RPGPU_PARSE_ERR_NONE = 0,
+    RPGPU_PARSE_ERR_ATTR_EOF = 1,        /* consume_type<int8_t> out_of_range (bytes/details/io_iterator_consumer.h:64-84) */
+    RPGPU_PARSE_ERR_COPY_NEGATIVE = 2,   /* iobuf_copy with (int)len < 0 -> bad_alloc (bytes/iobuf.cc:133-157) */
+    RPGPU_PARSE_ERR_HEADER_RESERVE = 3,  /* headers.reserve(count) throws (model/record_utils.cc:99) */
+    RPGPU_PARSE_ERR_TRAILING = 4,        /* sync for_each_record: bytes left after record_count records */
+    RPGPU_PARSE_ERR_INDEX_CAPACITY = 5,  /* more records than the reserved index slots (record_count > payload) */
+};
+
+/* Reference-environment limit for headers.reserve(header_count): libstdc++
+ * throws length_error above max_size() and Seastar throws bad_alloc when the
+ * shard cannot allocate count*sizeof(record_header) (=64 B).  The latter is
+ * environment dependent; this engine pins it at 2 GiB of reservation. */
+#define RPGPU_MAX_HEADER_RESERVE (1ll << 25)
+
+/* ------------------------------------------------------------------------ */
+/* Output layouts                                                            */
+/* ------------------------------------------------------------------------ */
+
+/* One entry per batch reached by the continuous_batch_parser chain whose
+ * header passed read_header_impl (storage/parser.cc:139-176), in chain order.
+ * 128 bytes. */
+typedef struct rpgpu_batch_result {
+    uint64_t file_pos;            /* physical offset of the header in its segment */
+    int64_t base_offset;          /* record_batch_header fields as decoded by   */
+    int64_t first_timestamp;      /* storage::header_from_iobuf                 */
+    int64_t max_timestamp;        /* (storage/parser.cc:36-76)                  */
+    int64_t producer_id;
+    int32_t size_bytes;           /* stored size (header + payload) */
+    int32_t record_count;
+    int32_t last_offset_delta;
+    int32_t base_sequence;
+    uint32_t header_crc;          /* stored header_crc */
+    uint32_t crc;                 /* stored crc (as uint32) */
+    uint32_t crc_computed;        /* crc32c(BE hdr40 ++ stored payload) */
+    uint32_t header_crc_computed; /* internal_header_only_crc(header) */
+    uint32_t flags;               /* RPGPU_F_* */
+    uint32_t segment;             /* segment index within the job */
+    uint64_t index_base;          /* first record-index slot of this batch */
+    uint64_t decoded_off;         /* offset of the decoded payload in the decoded arena (compressed batches) */
+    uint32_t records_parsed;      /* records fully parsed before stop */
+    uint32_t decoded_len;         /* decoded payload bytes (== stored payload len when not compressed) */
+    uint32_t decoded_crc;         /* reset_size_checksum_metadata: new crc over decoded payload (storage/parser_utils.cc:114-120) */
+    uint32_t decoded_header_crc;  /* reset_size_checksum_metadata: new header_crc */
+    int16_t attrs;
+    int16_t producer_epoch;
+    int8_t type;
+    uint8_t parse_err;            /* rpgpu_parse_err */
+    uint16_t reserved0;
+    uint64_t reserved1;
+} rpgpu_batch_result;
+
+/* One entry per parsed record (model/record_utils.cc:94-181).  Positions are
+ * byte offsets inside the batch's (decoded) payload.  64 bytes. */
+typedef struct rpgpu_record_index {
+    uint32_t batch;               /* job-wide batch ordinal */
+    uint32_t rec_pos;             /* offset of the record's length varint */
+    int64_t ts_delta;             /* timestamp_delta */
+    int32_t length;               /* record::size_bytes (length varint, int32) */
+    int32_t offset_delta;         /* static_cast<int32_t>(offset delta varint) */
+    int32_t key_len;              /* key_length as stored by model::record (int32) */
+    uint32_t key_pos;             /* first key byte */
+    int32_t val_len;
+    uint32_t val_pos;
+    int32_t hdr_count;            /* number of record headers */
+    uint32_t hdr_pos;             /* first byte after the header-count varint */
+    uint32_t end_pos;             /* first byte after this record */
+    int8_t attrs;                 /* record attributes byte */
+    uint8_t pad[3];
+    uint32_t reserved[2];
+} rpgpu_record_index;
+
+/* Per segment: where and why the parser chain stopped, and the
+ * log_replayer checkpoint (storage/log_replayer.cc:62-79, log_replayer.h:159-165). */
+typedef struct rpgpu_segment_summary {
+    uint64_t first_batch;         /* job-wide ordinal of the segment's first batch */
+    uint64_t n_batches;           /* batches with a valid header on the chain */
+    uint64_t terminal_pos;        /* file position where the chain stopped */
+    uint64_t bytes_consumed;      /* continuous_batch_parser::_bytes_consumed */
+    int32_t terminal_errc;        /* rpgpu_parser_errc that ended the chain */
+    int32_t terminal_eof;         /* 1 if the stop came from a short read (input_stream::eof()) */
+    int32_t has_checkpoint;       /* checkpoint fields valid */
+    uint32_t first_bad;           /* chain ordinal of the first batch failing crc (== n_batches if none) */
+    int64_t ckpt_last_offset;     /* checkpoint.last_offset */
+    uint64_t ckpt_truncate_pos;   /* checkpoint.truncate_file_pos */
+    uint64_t n_records;           /* index slots reserved for this segment */
+    uint64_t reserved[2];
+} rpgpu_segment_summary;
+
+/* Whole-job totals, written by the device. */
+typedef struct rpgpu_job_totals {
+    uint64_t n_batches;
+    uint64_t n_records;           /* index slots used */
+    uint64_t decoded_bytes;       /* arena bytes reserved */
+    uint64_t batch_capacity_needed;
+    uint64_t record_capacity_needed;
+    uint64_t decoded_capacity_needed;
+    uint32_t overflow;            /* nonzero: an output capacity was too small */
+    uint32_t n_rewalks;           /* discovery chunks whose speculative entry had to be re-walked */
+    uint64_t reserved[2];
+} rpgpu_job_totals;
+
+/* ------------------------------------------------------------------------ */
+/* Context / memory                                                          */
+/* ------------------------------------------------------------------------ */
+
+typedef struct rpgpu_ctx rpgpu_ctx;
+
+/* Number of visible HIP devices (0 when none). */
+int rpgpu_device_count(void);
+/* One context per host thread or Seastar shard (ownership
+ * row): it owns a HIP stream pair and device scratch.  Not thread-safe. */
+int rpgpu_create(int device, rpgpu_ctx** out);
+int rpgpu_destroy(rpgpu_ctx* ctx);
+const char* rpgpu_strerror(int status);
+const char* rpgpu_last_error(rpgpu_ctx* ctx);
+
+int rpgpu_dev_alloc(rpgpu_ctx* ctx, size_t bytes, void** out);
+int rpgpu_dev_free(rpgpu_ctx* ctx, void* p);
+/* pinned host memory for the double-buffered H2D staging */
+int rpgpu_host_alloc(rpgpu_ctx* ctx, size_t bytes, void** out);
+int rpgpu_host_free(rpgpu_ctx* ctx, void* p);
+int rpgpu_memcpy_h2d(rpgpu_ctx* ctx, void* dst, const void* src, size_t n, void* stream);
+int rpgpu_memcpy_d2h(rpgpu_ctx* ctx, void* dst, const void* src, size_t n, void* stream);
+int rpgpu_memset(rpgpu_ctx* ctx, void* dst, int value, size_t n, void* stream);
+int rpgpu_sync(rpgpu_ctx* ctx, void* stream);
+
+/* ------------------------------------------------------------------------ */
+/* crc::crc32c (hashing/crc32c.h:19-40)                                      */
+/* ------------------------------------------------------------------------ */
+
+/* google crc32c::Extend(crc, p, n) semantics: Extend(0, p, n) is the standard
+ * CRC32C (Castagnoli, reflected 0x82F63B78, init/xorout ~0).  Host-side
+ * (SSE4.2) for the small per-call sizes crc::crc32c sees; bulk segment CRC
+ * runs on the GPU through rpgpu_submit. Pure, thread-safe, no allocation. */
+uint32_t rpgpu_crc32c_extend(uint32_t crc, const uint8_t* p, size_t n);
+
+/* ------------------------------------------------------------------------ */
+/* Segment engine (new; replaces the per-batch loops of                      */
+/* storage::continuous_batch_parser::consume (storage/parser.cc:218-254),    */
+/* log_replayer::recover_in_thread (storage/log_replayer.cc:95-114),         */
+/* storage::internal::decompress_batch (storage/parser_utils.cc:43-60) and   */
+/* kafka_batch_adapter::adapt (kafka/protocol/kafka_batch_adapter.cc:126)).  */
+/* ------------------------------------------------------------------------ */
+
+enum rpgpu_layout {
+    RPGPU_LAYOUT_DISK = 0, /* Redpanda on-disk: 61-byte LE header (storage/segment_appender_utils.cc:28-54) */
+    RPGPU_LAYOUT_WIRE = 1, /* Kafka v2 wire: BE header (kafka/protocol/kafka_batch_adapter.cc:32-91) */
+};
+
+#define RPGPU_JOB_CRC (1u << 0)     /* compute the payload crc (always on in recovery) */
+#define RPGPU_JOB_PARSE (1u << 1)   /* walk records into the index */
+#define RPGPU_JOB_DECODE (1u << 2)  /* uncompress lz4/snappy payloads into the arena */
+
+/* All pointers are DEVICE pointers, caller-owned.  Segments are concatenated
+ * in d_data; segment s spans [d_seg_offsets[s], d_seg_offsets[s+1]). */
+typedef struct rpgpu_job {
+    const uint8_t* d_data;
+    const uint64_t* d_seg_offsets;   /* n_segments + 1 entries */
+    uint32_t n_segments;
+    uint32_t layout;                 /* rpgpu_layout */
+    uint32_t flags;                  /* RPGPU_JOB_* */
+    uint32_t chunk_bytes;            /* discovery chunk size (0 = default 256 KiB) */
+    rpgpu_batch_result* d_batches;   /* capacity batch_capacity */
+    uint64_t batch_capacity;
+    rpgpu_record_index* d_records;   /* capacity record_capacity (may be NULL if !PARSE) */
+    uint64_t record_capacity;
+    uint8_t* d_decoded;              /* decoded arena (may be NULL if !DECODE) */
+    uint64_t decoded_capacity;
+    rpgpu_segment_summary* d_summaries; /* n_segments entries */
+    rpgpu_job_totals* d_totals;      /* one entry */
+    uint64_t* d_valid_bitmap;        /* optional: 1 bit per batch, set = crc_ok && header_ok (&& parse_ok if PARSE) */
+} rpgpu_job;
+
+/* Enqueue the whole pipeline (discover -> resolve -> plan -> validate/decode)
+ * on `stream` (hipStream_t, NULL = the context's stream).  Asynchronous:
+ * results are valid after rpgpu_sync / an event on that stream.  Capacity
+ * overflow is reported in d_totals (overflow != 0), never by writing out of
+ * bounds. */
+int rpgpu_submit(rpgpu_ctx* ctx, const rpgpu_job* job, void* stream);
+
+/* Device-time of the kernels of the last rpgpu_submit on this context,
+ * measured with HIP events on the launch stream (milliseconds).  Indices:
+ * 0 = whole pipeline, 1 = discover, 2 = resolve+plan, 3 = validate. */
+int rpgpu_last_timings(rpgpu_ctx* ctx, float* ms, int n);
+/* Enable/disable per-kernel event timing (off by default). */
+int rpgpu_set_timing(rpgpu_ctx* ctx, int enable);
+
+/* ------------------------------------------------------------------------ */
+/* compression::compressor::uncompress (compression/compression.h:21-24)     */
+/* ------------------------------------------------------------------------ */
+
+/* Decode one payload (host pointers) on the device.  *out_len receives the
+ * decoded size; returns RPGPU_E_CODEC where the reference throws
+ * std::runtime_error, RPGPU_E_OVERFLOW if cap is too small (out_len then
+ * holds the size needed when known). */
+int rpgpu_uncompress(rpgpu_ctx* ctx, int codec, const void* in, size_t n,
+                     void* out, size_t cap, size_t* out_len);
+
+/* ------------------------------------------------------------------------ */
+/* Host segment path: pinned, double-buffered H2D of host-resident segments  */
+/* (log_replayer over files).  Segments are copied in chunks on a copy       */
+/* stream while the previous chunk validates.  Outputs are HOST pointers.    */
+/* ------------------------------------------------------------------------ */
+typedef struct rpgpu_host_job {
+    const uint8_t* const* segments;  /* host pointers (pinned or pageable) */
+    const uint64_t* seg_sizes;
+    uint32_t n_segments;
+    uint32_t layout;
+    uint32_t flags;
+    uint32_t reserved;
+    rpgpu_batch_result* batches;     /* host, capacity batch_capacity */
+    uint64_t batch_capacity;
+    rpgpu_segment_summary* summaries; /* host, n_segments */
+    rpgpu_job_totals* totals;        /* host */
+} rpgpu_host_job;
+
+int rpgpu_validate_host(rpgpu_ctx* ctx, const rpgpu_host_job* job);
+
+/* ------------------------------------------------------------------------ */
+/* Synthetic workload (storage/tests/utils/random_batch.cc:50-154 recipe,    */
+/* seeded mt19937_64 so runs reproduce).  Host-side generator.               */
+/* ------------------------------------------------------------------------ */
+typedef struct rpgpu_gen_spec {
+    uint64_t seed;
+    uint64_t segment_bytes;          /* exact bytes per segment */
+    uint32_t batch_bytes;            /* target size_bytes per batch (0 = variable, see min/max) */
+    uint32_t min_batch_bytes;        /* variable mode: log-uniform in [min, max] */
+    uint32_t max_batch_bytes;
+    uint32_t value_bytes;            /* approximate record value size */
+    uint32_t key_bytes;
+    uint32_t headers_per_record;
+    uint32_t codec_mix;              /* 0 = none only; bitmask of codecs allowed (1<<codec) */
+    uint32_t corrupt_ppm_payload;    /* payload bit flips per million batches */
+    uint32_t corrupt_ppm_header;     /* header bit flips per million batches */
+    uint32_t corrupt_ppm_zero;       /* zeroed headers per million batches */
+    uint32_t threads;                /* 0 = all cores */
+    int64_t base_offset;
+} rpgpu_gen_spec;
+
+/* Fill `out` (segment_bytes) with one segment; returns number of batches or
+ * <0.  The tail that cannot hold another batch is zero-filled (fallocated). */
+int64_t rpgpu_gen_segment(const rpgpu_gen_spec* spec, uint32_t segment_index, uint8_t* out);
+
+#ifdef __cplusplus
+} /* extern "C" */
+#endif
+
+#endif /* RPGPU_H_ */

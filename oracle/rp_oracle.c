@@ -1,0 +1,1131 @@
+/*
+ * rp_oracle.c — CPU restatement of the reference's record-batch hot path.
+ *
+ * TEST INFRASTRUCTURE ONLY (see rp_oracle.h).  Never linked into the product.
+ * Written for clarity over speed (bytewise CRC, scalar decoders), except the
+ * SSE4.2 CRC used as the timed CPU baseline.
+ */
+#define _GNU_SOURCE
+#include "rp_oracle.h"
+
+#include <pthread.h>
+#include <stdlib.h>
+#include <string.h>
+#include <time.h>
+
+#if defined(__x86_64__)
+#include <nmmintrin.h>
+#endif
+
+/* ======================================================================== */
+/* CRC32C — google crc32c::Extend semantics (hashing/crc32c.h:27 calls       */
+/* ::crc32c::Extend(_crc, data, size); crc32c @47b40d22, cmake/oss.cmake.in:195-197). */
+/* ======================================================================== */
+#define RPO_CRC32C_POLY 0x82F63B78u
+
+static uint32_t g_crc_table[256];
+static int g_crc_init = 0;
+
+static void crc_init(void) {
+    if (g_crc_init) return;
+    for (uint32_t i = 0; i < 256; i++) {
+        uint32_t c = i;
+        for (int k = 0; k < 8; k++) c = (c & 1) ? (c >> 1) ^ RPO_CRC32C_POLY : c >> 1;
+        g_crc_table[i] = c;
+    }
+    g_crc_init = 1;
+}
+
+uint32_t rpo_crc32c_extend(uint32_t crc, const uint8_t* p, size_t n) {
+    crc_init();
+    uint32_t l = crc ^ 0xFFFFFFFFu; /* kCRC32Xor */
+    for (size_t i = 0; i < n; i++) l = g_crc_table[(l ^ p[i]) & 0xFF] ^ (l >> 8);
+    return l ^ 0xFFFFFFFFu;
+}
+
+/* GF(2) multiply of two reflected polynomials mod P (zlib multmodp shape). */
+static uint32_t gf_mulmod(uint32_t a, uint32_t b) {
+    uint32_t m = 1u << 31, p = 0;
+    for (;;) {
+        if (a & m) {
+            p ^= b;
+            if ((a & (m - 1)) == 0) break;
+        }
+        m >>= 1;
+        b = (b & 1) ? (b >> 1) ^ RPO_CRC32C_POLY : b >> 1;
+    }
+    return p;
+}
+
+/* x^(8*len) mod P in the reflected domain. */
+static uint32_t x8n_mod(uint64_t len) {
+    uint32_t r = 1u << 31;       /* x^0 */
+    uint32_t sq = 1u << 23;      /* x^8 (reflected: bit 31-8) */
+    while (len) {
+        if (len & 1) r = gf_mulmod(r, sq);
+        sq = gf_mulmod(sq, sq);
+        len >>= 1;
+    }
+    return r;
+}
+
+uint32_t rpo_crc32c_combine(uint32_t crc_a, uint32_t crc_b, uint64_t len_b) {
+    return gf_mulmod(x8n_mod(len_b), crc_a) ^ crc_b;
+}
+
+#if defined(__x86_64__)
+__attribute__((target("sse4.2")))
+static uint32_t hw_raw(uint32_t l, const uint8_t* p, size_t n) {
+    while (n && ((uintptr_t)p & 7)) { l = _mm_crc32_u8(l, *p++); n--; }
+    /* three interleaved streams of `blk` bytes, merged by x^(8*blk) shifts */
+    const size_t blk = 4096;
+    static uint32_t k1 = 0, k2 = 0;
+    if (!k1) { k1 = x8n_mod(blk); k2 = x8n_mod(2 * blk); }
+    while (n >= 3 * blk) {
+        uint64_t a = l, b = 0, c = 0;
+        const uint64_t* q = (const uint64_t*)p;
+        for (size_t i = 0; i < blk / 8; i++) {
+            a = _mm_crc32_u64(a, q[i]);
+            b = _mm_crc32_u64(b, q[i + blk / 8]);
+            c = _mm_crc32_u64(c, q[i + 2 * blk / 8]);
+        }
+        l = gf_mulmod(k2, (uint32_t)a) ^ gf_mulmod(k1, (uint32_t)b) ^ (uint32_t)c;
+        p += 3 * blk;
+        n -= 3 * blk;
+    }
+    uint64_t v = l;
+    while (n >= 8) { v = _mm_crc32_u64(v, *(const uint64_t*)p); p += 8; n -= 8; }
+    l = (uint32_t)v;
+    while (n) { l = _mm_crc32_u8(l, *p++); n--; }
+    return l;
+}
+uint32_t rpo_crc32c_extend_hw(uint32_t crc, const uint8_t* p, size_t n) {
+    crc_init();
+    return hw_raw(crc ^ 0xFFFFFFFFu, p, n) ^ 0xFFFFFFFFu;
+}
+#else
+uint32_t rpo_crc32c_extend_hw(uint32_t crc, const uint8_t* p, size_t n) { return rpo_crc32c_extend(crc, p, n); }
+#endif
+
+/* ======================================================================== */
+/* XXH32 (lz4 1.9.3 lib/xxhash.c, XXH32())                                  */
+/* ======================================================================== */
+#define XP1 0x9E3779B1u
+#define XP2 0x85EBCA77u
+#define XP3 0xC2B2AE3Du
+#define XP4 0x27D4EB2Fu
+#define XP5 0x165667B1u
+static inline uint32_t rotl32(uint32_t x, int r) { return (x << r) | (x >> (32 - r)); }
+static inline uint32_t rd32(const uint8_t* p) { return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24); }
+static inline uint64_t rd64(const uint8_t* p) { return (uint64_t)rd32(p) | ((uint64_t)rd32(p + 4) << 32); }
+static inline uint16_t rd16(const uint8_t* p) { return (uint16_t)(p[0] | (p[1] << 8)); }
+
+uint32_t rpo_xxh32(const uint8_t* p, size_t n, uint32_t seed) {
+    const uint8_t* end = p + n;
+    uint32_t h;
+    if (n >= 16) {
+        uint32_t v1 = seed + XP1 + XP2, v2 = seed + XP2, v3 = seed, v4 = seed - XP1;
+        const uint8_t* lim = end - 16;
+        do {
+            v1 = rotl32(v1 + rd32(p) * XP2, 13) * XP1; p += 4;
+            v2 = rotl32(v2 + rd32(p) * XP2, 13) * XP1; p += 4;
+            v3 = rotl32(v3 + rd32(p) * XP2, 13) * XP1; p += 4;
+            v4 = rotl32(v4 + rd32(p) * XP2, 13) * XP1; p += 4;
+        } while (p <= lim);
+        h = rotl32(v1, 1) + rotl32(v2, 7) + rotl32(v3, 12) + rotl32(v4, 18);
+    } else {
+        h = seed + XP5;
+    }
+    h += (uint32_t)n;
+    while (p + 4 <= end) { h += rd32(p) * XP3; h = rotl32(h, 17) * XP4; p += 4; }
+    while (p < end) { h += (*p) * XP5; h = rotl32(h, 11) * XP1; p++; }
+    h ^= h >> 15; h *= XP2; h ^= h >> 13; h *= XP3; h ^= h >> 16;
+    return h;
+}
+
+/* ======================================================================== */
+/* vint (utils/vint.h)                                                       */
+/* ======================================================================== */
+int64_t rpo_vint_deserialize(const uint8_t* p, size_t avail, size_t* bytes_read) {
+    /* utils/vint.h:82-98: stops after shift 63 (10 bytes) even if the
+     * continuation bit is set; at end of input returns what it has. */
+    uint64_t result = 0, shift = 0;
+    size_t br = 0;
+    for (size_t i = 0; shift <= 63 && i < avail; i++) {
+        uint64_t byte = p[i];
+        br++;
+        if (byte & 128) {
+            result |= ((byte & 127) << shift);
+        } else {
+            result |= byte << shift;
+            break;
+        }
+        shift += 7;
+    }
+    *bytes_read = br;
+    /* decode_zigzag (utils/vint.h:37-39) */
+    return (int64_t)((result >> 1) ^ (~(result & 1) + 1));
+}
+
+size_t rpo_vint_serialize(int64_t x, uint8_t* out) {
+    uint64_t v = ((uint64_t)x << 1) ^ (uint64_t)(x >> 63);
+    size_t n = 0;
+    while (v >= 0x80) { out[n++] = (uint8_t)(v | 0x80); v >>= 7; }
+    out[n++] = (uint8_t)v;
+    return n;
+}
+
+/* ======================================================================== */
+/* Headers and CRCs                                                          */
+/* ======================================================================== */
+void rpo_header_from_disk(const uint8_t* p, rpo_header* h) {
+    /* storage/parser.cc:36-76, reflection::adl little endian */
+    h->header_crc = rd32(p + 0);
+    h->size_bytes = (int32_t)rd32(p + 4);
+    h->base_offset = (int64_t)rd64(p + 8);
+    h->type = (int8_t)p[16];
+    h->crc = (int32_t)rd32(p + 17);
+    h->attrs = (int16_t)rd16(p + 21);
+    h->last_offset_delta = (int32_t)rd32(p + 23);
+    h->first_timestamp = (int64_t)rd64(p + 27);
+    h->max_timestamp = (int64_t)rd64(p + 35);
+    h->producer_id = (int64_t)rd64(p + 43);
+    h->producer_epoch = (int16_t)rd16(p + 51);
+    h->base_sequence = (int32_t)rd32(p + 53);
+    h->record_count = (int32_t)rd32(p + 57);
+}
+
+static void wr_le(uint8_t* p, uint64_t v, int n) { for (int i = 0; i < n; i++) p[i] = (uint8_t)(v >> (8 * i)); }
+static void wr_be(uint8_t* p, uint64_t v, int n) { for (int i = 0; i < n; i++) p[i] = (uint8_t)(v >> (8 * (n - 1 - i))); }
+
+void rpo_header_to_disk(const rpo_header* h, uint8_t* o) {
+    wr_le(o + 0, h->header_crc, 4);
+    wr_le(o + 4, (uint32_t)h->size_bytes, 4);
+    wr_le(o + 8, (uint64_t)h->base_offset, 8);
+    o[16] = (uint8_t)h->type;
+    wr_le(o + 17, (uint32_t)h->crc, 4);
+    wr_le(o + 21, (uint16_t)h->attrs, 2);
+    wr_le(o + 23, (uint32_t)h->last_offset_delta, 4);
+    wr_le(o + 27, (uint64_t)h->first_timestamp, 8);
+    wr_le(o + 35, (uint64_t)h->max_timestamp, 8);
+    wr_le(o + 43, (uint64_t)h->producer_id, 8);
+    wr_le(o + 51, (uint16_t)h->producer_epoch, 2);
+    wr_le(o + 53, (uint32_t)h->base_sequence, 4);
+    wr_le(o + 57, (uint32_t)h->record_count, 4);
+}
+
+uint32_t rpo_internal_header_only_crc(const rpo_header* h) {
+    /* model/record_utils.cc:34-55: the 57 bytes after header_crc, LE */
+    uint8_t b[61];
+    rpo_header_to_disk(h, b);
+    return rpo_crc32c_extend(0, b + 4, 57);
+}
+
+static void be_prefix(const rpo_header* h, uint8_t* o) {
+    /* model/record_utils.cc:68-80: attrs..record_count, big endian (40 B) */
+    wr_be(o + 0, (uint16_t)h->attrs, 2);
+    wr_be(o + 2, (uint32_t)h->last_offset_delta, 4);
+    wr_be(o + 6, (uint64_t)h->first_timestamp, 8);
+    wr_be(o + 14, (uint64_t)h->max_timestamp, 8);
+    wr_be(o + 22, (uint64_t)h->producer_id, 8);
+    wr_be(o + 30, (uint16_t)h->producer_epoch, 2);
+    wr_be(o + 32, (uint32_t)h->base_sequence, 4);
+    wr_be(o + 36, (uint32_t)h->record_count, 4);
+}
+
+uint32_t rpo_crc_record_batch(const rpo_header* h, const uint8_t* payload, size_t n) {
+    uint8_t pre[40];
+    be_prefix(h, pre);
+    uint32_t c = rpo_crc32c_extend(0, pre, 40);
+    return rpo_crc32c_extend(c, payload, n);
+}
+
+static uint32_t crc_record_batch_hw(const rpo_header* h, const uint8_t* payload, size_t n) {
+    uint8_t pre[40];
+    be_prefix(h, pre);
+    uint32_t c = rpo_crc32c_extend_hw(0, pre, 40);
+    return rpo_crc32c_extend_hw(c, payload, n);
+}
+
+/* ======================================================================== */
+/* Record walk                                                               */
+/* ======================================================================== */
+typedef struct walk_cur {
+    const uint8_t* p;
+    uint64_t n;
+    uint64_t pos;
+} walk_cur;
+
+/* iobuf_parser_base::read_varlong (bytes/iobuf_parser.h:48-52): deserialize
+ * then skip(bytes_read) — never throws (bytes_read <= available). */
+static int64_t rd_varlong(walk_cur* c) {
+    size_t br;
+    int64_t v = rpo_vint_deserialize(c->p + c->pos, c->n - c->pos, &br);
+    c->pos += br;
+    return v;
+}
+
+/* iobuf_const_parser::copy(len) -> iobuf_copy (bytes/iobuf.cc:133-157):
+ * `int bytes_left = len` truncates; a negative int reaches
+ * ss_next_allocation_size((size_t)neg) -> 2^63-byte temporary_buffer ->
+ * bad_alloc; zero copies nothing; positive copies min(len, available) and
+ * never throws. Returns 0 or -1 (throw). */
+static int copy_bytes(walk_cur* c, int64_t len) {
+    int32_t bl = (int32_t)(uint32_t)(uint64_t)len;
+    if (bl < 0) return -1;
+    uint64_t left = c->n - c->pos;
+    c->pos += ((uint64_t)bl < left) ? (uint64_t)bl : left;
+    return 0;
+}
+
+uint32_t rpo_walk_records(const uint8_t* payload, size_t n, int32_t record_count,
+                          uint32_t batch_ordinal, rpgpu_record_index* index,
+                          uint64_t index_cap, uint8_t* parse_err, uint64_t* trailing) {
+    walk_cur c = {payload, n, 0};
+    uint32_t parsed = 0;
+    *parse_err = RPGPU_PARSE_ERR_NONE;
+    *trailing = 0;
+    /* model/record.h:619: for (auto i = 0; i < record_count; i++) */
+    for (int32_t i = 0; i < record_count; i++) {
+        rpgpu_record_index e;
+        memset(&e, 0, sizeof e);
+        e.batch = batch_ordinal;
+        e.rec_pos = (uint32_t)c.pos;
+        /* parse_record_meta_from_buffer (model/record_utils.cc:147-160) */
+        int64_t record_size = rd_varlong(&c);
+        if (c.pos >= c.n) { *parse_err = RPGPU_PARSE_ERR_ATTR_EOF; return parsed; }
+        int8_t attr = (int8_t)c.p[c.pos++];
+        /* do_parse_one_record_from_buffer (model/record_utils.cc:116-145) */
+        int64_t ts = rd_varlong(&c);
+        int64_t off = rd_varlong(&c);
+        int64_t klen = rd_varlong(&c);
+        e.key_pos = (uint32_t)c.pos;
+        if (klen > 0 && copy_bytes(&c, klen)) { *parse_err = RPGPU_PARSE_ERR_COPY_NEGATIVE; return parsed; }
+        int64_t vlen = rd_varlong(&c);
+        e.val_pos = (uint32_t)c.pos;
+        if (vlen > 0 && copy_bytes(&c, vlen)) { *parse_err = RPGPU_PARSE_ERR_COPY_NEGATIVE; return parsed; }
+        /* parse_record_headers (model/record_utils.cc:94-114) */
+        int64_t hcount = rd_varlong(&c);
+        e.hdr_pos = (uint32_t)c.pos;
+        /* headers.reserve(header_count): length_error for negative counts,
+         * bad_alloc above the pinned reservation limit */
+        if (hcount < 0 || hcount > RPGPU_MAX_HEADER_RESERVE) { *parse_err = RPGPU_PARSE_ERR_HEADER_RESERVE; return parsed; }
+        for (int64_t h = 0; h < hcount; h++) {
+            if (c.pos >= c.n) break; /* remaining iterations read {0,0}: no-ops */
+            int64_t hk = rd_varlong(&c);
+            if (hk > 0 && copy_bytes(&c, hk)) { *parse_err = RPGPU_PARSE_ERR_COPY_NEGATIVE; return parsed; }
+            int64_t hv = rd_varlong(&c);
+            if (hv > 0 && copy_bytes(&c, hv)) { *parse_err = RPGPU_PARSE_ERR_COPY_NEGATIVE; return parsed; }
+        }
+        e.length = (int32_t)record_size;
+        e.attrs = attr;
+        e.ts_delta = ts;
+        e.offset_delta = (int32_t)off;
+        e.key_len = (int32_t)klen;
+        e.val_len = (int32_t)vlen;
+        e.hdr_count = (int32_t)hcount;
+        e.end_pos = (uint32_t)c.pos;
+        if (index && (uint64_t)parsed < index_cap) index[parsed] = e;
+        parsed++;
+    }
+    *trailing = c.n - c.pos;
+    return parsed;
+}
+
+/* ======================================================================== */
+/* LZ4 block decode — restates lz4 1.9.3 LZ4_decompress_generic for         */
+/* LZ4_decompress_safe_usingDict (endOnInputSize, decode_full_block,         */
+/* LZ4_FAST_DEC_LOOP on x86-64).  Control flow and every acceptance check    */
+/* are kept; copies use canonical forward-copy semantics (offset 0 -> zeros, */
+/* as LZ4_memcpy_using_offset_base / the safe loop's write32(op,0) produce). */
+/* ======================================================================== */
+#define LZ_MINMATCH 4
+#define LZ_LASTLITERALS 5
+#define LZ_MFLIMIT 12
+#define LZ_FASTLOOP_SAFE_DISTANCE 64
+
+/* read_variable_length: returns added length; *err: 0 ok, 1 initial, 2 loop */
+static uint32_t lz_read_var(const uint8_t* s, int64_t* ip, int64_t lencheck, int loop_check,
+                            int initial_check, int* err) {
+    uint32_t length = 0, b;
+    *err = 0;
+    if (initial_check && *ip >= lencheck) { *err = 1; return length; }
+    do {
+        b = s[*ip];
+        (*ip)++;
+        length += b;
+        if (loop_check && *ip >= lencheck) { *err = 2; return length; }
+    } while (b == 255);
+    return length;
+}
+
+static void lz_match_copy(uint8_t* dst, int64_t op, int64_t offset, int64_t length) {
+    if (offset == 0) {
+        memset(dst + op, 0, (size_t)length);
+        return;
+    }
+    for (int64_t i = 0; i < length; i++) dst[op + i] = dst[op + i - offset];
+}
+
+int rpo_lz4_block_decode(const uint8_t* src, size_t n, uint8_t* dst, size_t dst_cap,
+                         size_t history) {
+    const int64_t iend = (int64_t)n, oend = (int64_t)dst_cap;
+    int64_t ip = 0, op = 0;
+    const int64_t H = (int64_t)history;
+    const int64_t shortiend = iend - 14 - 2, shortoend = oend - 14 - 18;
+    uint32_t token;
+    int64_t length, offset, cpy;
+    int err;
+
+    if (oend == 0) return (n == 1 && src[0] == 0) ? 0 : -1;
+    if (n == 0) return -1;
+
+    if (oend - op < LZ_FASTLOOP_SAFE_DISTANCE) goto safe_decode;
+    for (;;) {
+        token = src[ip++];
+        length = token >> 4;
+        if (length == 15) {
+            length += lz_read_var(src, &ip, iend - 15, 1, 1, &err);
+            if (err == 1) return -1;
+            cpy = op + length;
+            if (cpy > oend - 32 || ip + length > iend - 32) goto safe_literal_copy;
+            memcpy(dst + op, src + ip, (size_t)length);
+            ip += length;
+            op = cpy;
+        } else {
+            cpy = op + length;
+            if (ip > iend - (16 + 1)) goto safe_literal_copy;
+            memcpy(dst + op, src + ip, (size_t)length);
+            ip += length;
+            op = cpy;
+        }
+        offset = rd16(src + ip);
+        ip += 2;
+        length = token & 15;
+        if (length == 15) {
+            if (offset > op + H) return -1;
+            length += lz_read_var(src, &ip, iend - LZ_LASTLITERALS + 1, 1, 0, &err);
+            if (err) return -1;
+            length += LZ_MINMATCH;
+            if (op + length >= oend - LZ_FASTLOOP_SAFE_DISTANCE) goto safe_match_copy;
+        } else {
+            length += LZ_MINMATCH;
+            if (op + length >= oend - LZ_FASTLOOP_SAFE_DISTANCE) goto safe_match_copy;
+            if (offset <= op + H && offset >= 8) {
+                lz_match_copy(dst, op, offset, length);
+                op += length;
+                continue;
+            }
+        }
+        if (offset > op + H) return -1;
+        /* external-dictionary end-of-block rule cannot trigger here
+         * (op + length < oend - 64) */
+        lz_match_copy(dst, op, offset, length);
+        op += length;
+    }
+
+safe_decode:
+    for (;;) {
+        token = src[ip++];
+        length = token >> 4;
+        if (length != 15 && ip < shortiend && op <= shortoend) {
+            memcpy(dst + op, src + ip, (size_t)length);
+            op += length;
+            ip += length;
+            length = token & 15;
+            offset = rd16(src + ip);
+            ip += 2;
+            if (length != 15 && offset >= 8 && offset <= op + H) {
+                lz_match_copy(dst, op, offset, length + LZ_MINMATCH);
+                op += length + LZ_MINMATCH;
+                continue;
+            }
+            goto copy_match;
+        }
+        if (length == 15) {
+            length += lz_read_var(src, &ip, iend - 15, 1, 1, &err);
+            if (err == 1) return -1;
+        }
+        cpy = op + length;
+    safe_literal_copy:
+        if (cpy > oend - LZ_MFLIMIT || ip + length > iend - (2 + 1 + LZ_LASTLITERALS)) {
+            if (ip + length != iend || cpy > oend) return -1;
+            memmove(dst + op, src + ip, (size_t)length);
+            ip += length;
+            op += length;
+            break;
+        }
+        memcpy(dst + op, src + ip, (size_t)length);
+        ip += length;
+        op = cpy;
+        offset = rd16(src + ip);
+        ip += 2;
+        length = token & 15;
+    copy_match:
+        if (length == 15) {
+            length += lz_read_var(src, &ip, iend - LZ_LASTLITERALS + 1, 1, 0, &err);
+            if (err) return -1;
+        }
+        length += LZ_MINMATCH;
+    safe_match_copy:
+        if (offset > op + H) return -1;
+        if (offset > op) {
+            /* match starts in the history (external dictionary or prefix):
+             * LZ4_decompress_generic rejects op+length > oend-LASTLITERALS in
+             * extDict mode; the in-block rule below rejects the same ends. */
+            if (op + length > oend - LZ_LASTLITERALS) return -1;
+            lz_match_copy(dst, op, offset, length);
+            op += length;
+            continue;
+        }
+        cpy = op + length;
+        if (cpy > oend - LZ_MFLIMIT) {
+            if (cpy > oend - LZ_LASTLITERALS) return -1;
+        }
+        lz_match_copy(dst, op, offset, length);
+        op = cpy;
+    }
+    return (int)op;
+}
+
+/* ======================================================================== */
+/* LZ4 frame — restates compression/internal/lz4_frame_compressor.cc:115-200 */
+/* (do_uncompressed: LZ4F_getFrameInfo + LZ4F_decompress loop until code==0,  */
+/* throw if input remains) over lz4 1.9.3 lz4frame.c's state machine.        */
+/* Running out of input before the end mark is NOT an error there: the loop  */
+/* exits with bytes_remaining == src_size and the partial output is returned. */
+/* ======================================================================== */
+static size_t lz4f_block_max(unsigned id) {
+    switch (id) {
+    case 4: return 64u << 10;
+    case 5: return 256u << 10;
+    case 6: return 1u << 20;
+    case 7: return 4u << 20;
+    }
+    return 0;
+}
+
+/* Parses the frame header (LZ4F_headerSize + LZ4F_decodeHeader via
+ * LZ4F_getFrameInfo).  Returns header bytes consumed, 0 for a skippable frame
+ * (4 bytes consumed), -1 on error. */
+typedef struct lz4f_info {
+    int skippable;
+    unsigned block_linked, block_checksum, content_checksum, content_size_flag;
+    uint64_t content_size;
+    size_t block_max;
+} lz4f_info;
+
+static int64_t lz4f_parse_header(const uint8_t* s, size_t n, lz4f_info* fi) {
+    memset(fi, 0, sizeof *fi);
+    if (n < 7) return -1;                                  /* frameHeader_incomplete */
+    uint32_t magic = rd32(s);
+    if ((magic & 0xFFFFFFF0u) == 0x184D2A50u) {            /* skippable */
+        if (n < 8) return -1;
+        fi->skippable = 1;
+        return 4;
+    }
+    if (magic != 0x184D2204u) return -1;                   /* frameType_unknown */
+    uint8_t flg = s[4];
+    size_t hsize = 7 + ((flg >> 3) & 1 ? 8 : 0) + ((flg & 1) ? 4 : 0);
+    if (n < hsize) return -1;                              /* frameHeader_incomplete */
+    if ((flg >> 1) & 1) return -1;                         /* reservedFlag_set */
+    if (((flg >> 6) & 3) != 1) return -1;                  /* headerVersion_wrong */
+    uint8_t bd = s[5];
+    if ((bd >> 7) & 1) return -1;
+    unsigned bsid = (bd >> 4) & 7;
+    if (bsid < 4) return -1;                               /* maxBlockSize_invalid */
+    if (bd & 15) return -1;
+    uint8_t hc = (uint8_t)((rpo_xxh32(s + 4, hsize - 5, 0) >> 8) & 0xFF);
+    if (hc != s[hsize - 1]) return -1;                     /* headerChecksum_invalid */
+    fi->block_linked = !((flg >> 5) & 1);
+    fi->block_checksum = (flg >> 4) & 1;
+    fi->content_checksum = (flg >> 2) & 1;
+    fi->content_size_flag = (flg >> 3) & 1;
+    if (fi->content_size_flag) fi->content_size = rd64(s + 6);
+    fi->block_max = lz4f_block_max(bsid);
+    return (int64_t)hsize;
+}
+
+/* do_uncompressed drives LZ4F_decompress with an output buffer of
+ * `est` bytes (contentSize, or 4x the input when unknown / >255x), growing it
+ * to 1 KiB + 1.5x whenever a call returns with the buffer exactly full, and
+ * stops calling as soon as all input has been handed over.  A compressed
+ * block is decoded straight into the buffer only when at least maxBlockSize
+ * bytes of room remain; otherwise liblz4 decodes it into its tmpOut and
+ * flushes what fits, returning early.  If the input is exhausted at that
+ * point (a frame truncated right after such a block), the unflushed tail is
+ * never delivered — the reference returns the flushed prefix.  This
+ * restatement tracks est/consumed to reproduce that exactly. */
+int rpo_lz4f_uncompress(const uint8_t* s, size_t n, uint8_t* dst, size_t cap, size_t* out_len) {
+    lz4f_info fi;
+    *out_len = 0;
+    int64_t h = lz4f_parse_header(s, n, &fi);
+    if (h < 0) return -1;
+    size_t pos = (size_t)h, out = 0;
+    if (fi.skippable) {
+        /* dstage_getSFrameSize / dstage_skipSkippable */
+        if (n - pos < 4) return 0;
+        uint32_t sz = rd32(s + pos);
+        pos += 4;
+        if (n - pos < sz) return 0;        /* still skipping: input exhausted, no error */
+        pos += sz;
+        return pos < n ? -1 : 0;           /* frame done (code 0), input left -> throw */
+    }
+    /* compute_frame_uncompressed_size (lz4_frame_compressor.cc:115-121) */
+    uint64_t est = (fi.content_size == 0 || fi.content_size > (uint64_t)n * 255) ? (uint64_t)n * 4 : fi.content_size;
+#define LZ4F_GROW() (est = 1024 + ((est * 3) + 1) / 2)
+    uint64_t remaining = fi.content_size; /* frameRemainingSize */
+    for (;;) {
+        if (n - pos < 4) return (*out_len = out, 0);      /* waiting for block header */
+        uint32_t bh = rd32(s + pos);
+        pos += 4;
+        if (bh == 0) break;                                /* end mark -> dstage_getSuffix */
+        size_t bsz = bh & 0x7FFFFFFFu;
+        if (bsz > fi.block_max) return -1;                 /* maxBlockSize_invalid */
+        if (bh & 0x80000000u) {
+            /* dstage_copyDirect: streamed, partial data is emitted */
+            size_t left = bsz;
+            const uint8_t* blk = s + pos;
+            for (;;) {
+                size_t space = (size_t)(est - out), avail = n - pos;
+                size_t k = left < avail ? left : avail;
+                if (k > space) k = space;
+                if (out + k > cap) return -2;
+                memcpy(dst + out, s + pos, k);
+                out += k;
+                pos += k;
+                left -= k;
+                if (fi.content_size) remaining -= k;
+                if (left == 0) break;
+                if (out == est) LZ4F_GROW();               /* call returned, buffer full */
+                if (pos == n) return (*out_len = out, 0);  /* input exhausted */
+            }
+            if (fi.block_checksum) {
+                if (n - pos < 4) return (*out_len = out, 0);
+                if (rd32(s + pos) != rpo_xxh32(blk, bsz, 0)) return -1;
+                pos += 4;
+            }
+            continue;
+        }
+        /* compressed block header read: the call returns if dst is full or
+         * the input is exhausted (dstage_getBlockHeader) */
+        if (out == est) LZ4F_GROW();
+        if (pos == n) return (*out_len = out, 0);
+        size_t need = bsz + (fi.block_checksum ? 4 : 0);
+        if (n - pos < need) return (*out_len = out, 0);  /* dstage_storeCBlock: wait */
+        if (fi.block_checksum && rd32(s + pos + bsz) != rpo_xxh32(s + pos, bsz, 0)) return -1;
+        size_t hist = fi.block_linked ? out : 0;
+        if (out + fi.block_max > cap) {
+            /* decode into a bounded scratch so an overflow is reported, not written */
+            size_t hk = hist < 65536 ? hist : 65536;
+            uint8_t* tmp = (uint8_t*)malloc(fi.block_max + 65536);
+            memcpy(tmp, dst + out - hk, hk);
+            int d = rpo_lz4_block_decode(s + pos, bsz, tmp + hk, fi.block_max, hk);
+            if (d < 0) { free(tmp); return -1; }
+            if (out + (size_t)d > cap) { free(tmp); return -2; }
+            memcpy(dst + out, tmp + hk, (size_t)d);
+            free(tmp);
+            pos += need;
+            if (fi.content_size) remaining -= (uint64_t)d;
+            size_t space = (size_t)(est - out);
+            if (space >= fi.block_max || (size_t)d <= space) { out += (size_t)d; continue; }
+            /* tmpOut flush path: same bookkeeping as below */
+            size_t pending = (size_t)d - space;
+            out += space;
+            while (pending) {
+                if (out == est) LZ4F_GROW();
+                if (pos == n) return (*out_len = out, 0);
+                size_t sp = (size_t)(est - out), f = pending < sp ? pending : sp;
+                out += f;
+                pending -= f;
+            }
+            continue;
+        }
+        int d = rpo_lz4_block_decode(s + pos, bsz, dst + out, fi.block_max, hist);
+        if (d < 0) return -1;                              /* decompressionFailed */
+        pos += need;
+        if (fi.content_size) remaining -= (uint64_t)d;
+        size_t space = (size_t)(est - out);
+        if (space >= fi.block_max || (size_t)d <= space) {
+            out += (size_t)d;                              /* direct, or fully flushed */
+            continue;
+        }
+        /* decoded into tmpOut: `space` bytes flushed now, the rest on later
+         * calls — which only happen while input remains */
+        size_t pending = (size_t)d - space;
+        out += space;
+        while (pending) {
+            if (out == est) LZ4F_GROW();
+            if (pos == n) return (*out_len = out, 0);      /* tail never flushed */
+            size_t sp = (size_t)(est - out), f = pending < sp ? pending : sp;
+            out += f;
+            pending -= f;
+        }
+    }
+#undef LZ4F_GROW
+    /* dstage_getSuffix */
+    if (remaining) return -1;                              /* frameSize_wrong */
+    if (fi.content_checksum) {
+        if (n - pos < 4) return (*out_len = out, 0);       /* storeSuffix: wait */
+        if (rd32(s + pos) != rpo_xxh32(dst, out, 0)) return -1;
+        pos += 4;
+    }
+    *out_len = out;
+    return pos < n ? -1 : 0; /* "could not consume all input bytes" */
+}
+
+/* ======================================================================== */
+/* snappy 1.1.8 raw decode (snappy.cc: GetUncompressedLength ->              */
+/* Varint::Parse32WithLimit; RawUncompress -> SnappyDecompressor::            */
+/* DecompressAllTags into SnappyArrayWriter).                                 */
+/* ======================================================================== */
+static int snappy_varint32(const uint8_t* s, size_t n, uint32_t* v, size_t* used) {
+    uint32_t r = 0;
+    for (size_t i = 0; i < 5; i++) {
+        if (i >= n) return -1;
+        uint32_t b = s[i];
+        if (i < 4) {
+            r |= (b & 127) << (7 * i);
+            if (b < 128) { *v = r; *used = i + 1; return 0; }
+        } else {
+            r |= (b & 127) << 28;
+            if (b < 16) { *v = r; *used = 5; return 0; }
+            return -1;
+        }
+    }
+    return -1;
+}
+
+/* DecompressAllTags restated over one contiguous input.  Succeeds iff the
+ * tags end exactly at the end of input and exactly ulen bytes come out. */
+static int snappy_decode_tags(const uint8_t* s, size_t n, size_t ip, uint8_t* dst, size_t ulen) {
+    size_t op = 0;
+    while (ip < n) {
+        uint8_t c = s[ip];
+        size_t extra;
+        if ((c & 3) == 0) extra = ((c >> 2) >= 60) ? (size_t)((c >> 2) - 59) : 0;
+        else if ((c & 3) == 1) extra = 1;
+        else if ((c & 3) == 2) extra = 2;
+        else extra = 4;
+        if (n - ip < 1 + extra) return -1; /* RefillTag cannot stitch the tag */
+        ip++;
+        if ((c & 3) == 0) {
+            size_t lit = (size_t)(c >> 2) + 1;
+            if (lit >= 61) {
+                size_t ll = lit - 60;
+                uint32_t v = 0;
+                for (size_t k = 0; k < ll; k++) v |= (uint32_t)s[ip + k] << (8 * k);
+                lit = (size_t)v + 1;
+                ip += ll;
+            }
+            if (n - ip < lit) return -1;   /* premature end of input */
+            if (ulen - op < lit) return -1; /* SnappyArrayWriter::Append overflow */
+            memcpy(dst + op, s + ip, lit);
+            op += lit;
+            ip += lit;
+        } else {
+            size_t len, off;
+            if ((c & 3) == 1) {
+                len = 4 + ((c >> 2) & 7);
+                off = ((size_t)(c >> 5) << 8) | s[ip];
+            } else if ((c & 3) == 2) {
+                len = (size_t)(c >> 2) + 1;
+                off = rd16(s + ip);
+            } else {
+                len = (size_t)(c >> 2) + 1;
+                off = rd32(s + ip);
+            }
+            ip += extra;
+            /* AppendFromSelf: Produced() <= offset - 1u || op_end > op_limit_ */
+            if (off == 0 || op < off || ulen - op < len) return -1;
+            for (size_t k = 0; k < len; k++) dst[op + k] = dst[op + k - off];
+            op += len;
+        }
+    }
+    return op == ulen ? 0 : -1; /* decompressor->eof() && writer->CheckLength() */
+}
+
+/* snappy::RawUncompress on one buffer (length varint + tags) */
+static int snappy_raw_checked(const uint8_t* s, size_t n, uint8_t* dst, size_t cap, size_t* out_len) {
+    uint32_t ulen;
+    size_t used;
+    if (snappy_varint32(s, n, &ulen, &used)) return -1;
+    /* no tag sequence expands more than 64/3 per input byte: a longer
+     * declared length can never be produced exactly -> RawUncompress fails */
+    if ((uint64_t)ulen > 22ull * (uint64_t)n + 64) return -1;
+    if (ulen > cap) return -2;
+    if (snappy_decode_tags(s, n, used, dst, ulen)) return -1;
+    *out_len = ulen;
+    return 0;
+}
+
+int rpo_snappy_raw_uncompress(const uint8_t* s, size_t n, uint8_t* dst, size_t cap, size_t* out_len) {
+    /* compression/snappy_standard_compressor.cc:43-65 (do_uncompressed) */
+    uint32_t ulen;
+    size_t used;
+    *out_len = 0;
+    if (snappy_varint32(s, n, &ulen, &used)) return -1;
+    if (ulen == 0) return 0; /* "empty frame": RawUncompress is not called */
+    return snappy_raw_checked(s, n, dst, cap, out_len);
+}
+
+static const uint8_t k_snappy_java_magic[8] = {0x82, 'S', 'N', 'A', 'P', 'P', 'Y', 0};
+
+int rpo_snappy_java_uncompress(const uint8_t* s, size_t n, uint8_t* dst, size_t cap, size_t* out_len) {
+    /* compression/internal/snappy_java_compressor.cc:76-129 */
+    *out_len = 0;
+    if (n < 16) return rpo_snappy_raw_uncompress(s, n, dst, cap, out_len);
+    if (memcmp(s, k_snappy_java_magic, 8) != 0) return rpo_snappy_raw_uncompress(s, n, dst, cap, out_len);
+    int32_t min_version = (int32_t)rd32(s + 12); /* native little endian */
+    if (min_version < 1) return -1;
+    size_t pos = 16, out = 0;
+    while (pos != n) {
+        if (n - pos < 4) return -1;                       /* consume_be_type out_of_range */
+        int32_t clen = (int32_t)(((uint32_t)s[pos] << 24) | ((uint32_t)s[pos + 1] << 16) |
+                                 ((uint32_t)s[pos + 2] << 8) | s[pos + 3]);
+        pos += 4;
+        if (clen < 0) return -1;                          /* sstring overflow */
+        if (n - pos < (size_t)clen) return -1;            /* consume_to out_of_range */
+        size_t got = 0;
+        int r = snappy_raw_checked(s + pos, (size_t)clen, dst + out, cap - out, &got);
+        if (r) return r;
+        out += got;
+        pos += (size_t)clen;
+    }
+    *out_len = out;
+    return 0;
+}
+
+int rpo_uncompress(int codec, const uint8_t* s, size_t n, uint8_t* dst, size_t cap, size_t* out_len) {
+    /* compression/compression.cc:34-55 */
+    *out_len = 0;
+    if (n == 0) return -1;
+    switch (codec) {
+    case RPGPU_CODEC_SNAPPY: return rpo_snappy_java_uncompress(s, n, dst, cap, out_len);
+    case RPGPU_CODEC_LZ4: return rpo_lz4f_uncompress(s, n, dst, cap, out_len);
+    default: return -1;
+    }
+}
+
+uint64_t rpo_decode_capacity(int codec, const uint8_t* s, size_t n) {
+    if (n == 0) return 0;
+    if (codec == RPGPU_CODEC_LZ4) {
+        lz4f_info fi;
+        int64_t h = lz4f_parse_header(s, n, &fi);
+        if (h < 0 || fi.skippable) return 0;
+        uint64_t cap = 0;
+        size_t pos = (size_t)h;
+        while (n - pos >= 4) {
+            uint32_t bh = rd32(s + pos);
+            if (bh == 0) break;
+            size_t bsz = bh & 0x7FFFFFFFu;
+            if (bsz > fi.block_max) break;
+            cap += (bh & 0x80000000u) ? bsz : fi.block_max;
+            pos += 4;
+            size_t adv = bsz + (fi.block_checksum ? 4 : 0);
+            if (n - pos < adv) break;
+            pos += adv;
+        }
+        return cap;
+    }
+    if (codec == RPGPU_CODEC_SNAPPY) {
+        uint32_t ulen;
+        size_t used;
+        if (n < 16 || memcmp(s, k_snappy_java_magic, 8) != 0) {
+            if (snappy_varint32(s, n, &ulen, &used)) return 0;
+            return ((uint64_t)ulen <= 22ull * n + 64) ? ulen : 0;
+        }
+        uint64_t cap = 0;
+        size_t pos = 16;
+        while (n - pos >= 4) {
+            int32_t clen = (int32_t)(((uint32_t)s[pos] << 24) | ((uint32_t)s[pos + 1] << 16) |
+                                     ((uint32_t)s[pos + 2] << 8) | s[pos + 3]);
+            if (clen <= 0 || n - pos - 4 < (size_t)clen) break;
+            if (snappy_varint32(s + pos + 4, (size_t)clen, &ulen, &used)) break;
+            if ((uint64_t)ulen > 22ull * (uint64_t)clen + 64) break;
+            cap += ulen;
+            pos += 4 + (size_t)clen;
+        }
+        return cap;
+    }
+    return 0;
+}
+
+/* ======================================================================== */
+/* Segment pipeline                                                          */
+/* ======================================================================== */
+int rpo_batch_valid(const rpgpu_batch_result* b, uint32_t job_flags) {
+    (void)job_flags;
+    uint32_t f = b->flags;
+    if (!(f & RPGPU_F_HEADER_OK) || !(f & RPGPU_F_COMPLETE) || !(f & RPGPU_F_CRC_OK)) return 0;
+    if (f & RPGPU_F_CODEC_INVALID) return 0;
+    if ((f & RPGPU_F_COMPRESSED) && (job_flags & RPGPU_JOB_DECODE) &&
+        !(f & RPGPU_F_CODEC_UNSUPPORTED) && !(f & RPGPU_F_CODEC_OK)) return 0;
+    if ((f & RPGPU_F_PARSED) && !(f & RPGPU_F_PARSE_OK)) return 0;
+    return 1;
+}
+
+static void fill_result_header(rpgpu_batch_result* r, const rpo_header* h) {
+    r->base_offset = h->base_offset;
+    r->first_timestamp = h->first_timestamp;
+    r->max_timestamp = h->max_timestamp;
+    r->producer_id = h->producer_id;
+    r->size_bytes = h->size_bytes;
+    r->record_count = h->record_count;
+    r->last_offset_delta = h->last_offset_delta;
+    r->base_sequence = h->base_sequence;
+    r->header_crc = h->header_crc;
+    r->crc = (uint32_t)h->crc;
+    r->attrs = h->attrs;
+    r->producer_epoch = h->producer_epoch;
+    r->type = h->type;
+}
+
+int64_t rpo_scan_segment(const uint8_t* seg, uint64_t len, uint32_t segment, uint32_t job_flags,
+                         rpgpu_batch_result* batches, uint64_t batch_cap,
+                         rpgpu_record_index* index, uint64_t index_cap,
+                         uint8_t* decoded, uint64_t decoded_cap,
+                         rpgpu_segment_summary* sm, rpo_job_state* st) {
+    memset(sm, 0, sizeof *sm);
+    sm->first_batch = st->batch_base;
+    uint64_t pos = 0, phys = 0;
+    uint64_t nb = 0;
+    int64_t first_bad = -1;
+    uint64_t seg_records = 0;
+    for (;;) {
+        /* read_header_impl (storage/parser.cc:139-176) */
+        uint64_t rem = len - pos;
+        if (rem == 0) { sm->terminal_errc = RPGPU_ERRC_END_OF_STREAM; sm->terminal_eof = 1; break; }
+        if (rem < RPGPU_HEADER_SIZE) { sm->terminal_errc = RPGPU_ERRC_INPUT_STREAM_NOT_ENOUGH_BYTES; sm->terminal_eof = 1; break; }
+        rpo_header h;
+        rpo_header_from_disk(seg + pos, &h);
+        if (h.header_crc == 0) { sm->terminal_errc = RPGPU_ERRC_FALLOCATED_FILE_READ_ZERO_BYTES_FOR_HEADER; break; }
+        uint32_t hc = rpo_internal_header_only_crc(&h);
+        if (hc != h.header_crc) { sm->terminal_errc = RPGPU_ERRC_HEADER_ONLY_CRC_MISSMATCH; break; }
+        if (st->batch_base + nb >= batch_cap) { st->overflow |= 1; sm->terminal_errc = RPGPU_ERRC_NONE; break; }
+        rpgpu_batch_result* r = &batches[st->batch_base + nb];
+        memset(r, 0, sizeof *r);
+        r->file_pos = pos;
+        r->segment = segment;
+        fill_result_header(r, &h);
+        r->header_crc_computed = hc;
+        r->flags = RPGPU_F_HEADER_OK;
+        /* consume_records: size_bytes - 61 computed unsigned (storage/parser.cc:207) */
+        uint64_t need = (uint32_t)((uint32_t)h.size_bytes - RPGPU_HEADER_SIZE);
+        const uint8_t* payload = seg + pos + RPGPU_HEADER_SIZE;
+        uint32_t codec = (uint16_t)h.attrs & 7;
+        if (rem - RPGPU_HEADER_SIZE < need) {
+            /* short read -> input_stream_not_enough_bytes with eof() set */
+            r->index_base = st->index_base;
+            r->decoded_off = st->decoded_base;
+            if (codec) r->flags |= RPGPU_F_COMPRESSED;
+            if (codec >= 5) r->flags |= RPGPU_F_CODEC_INVALID;
+            nb++;
+            if (first_bad < 0) first_bad = (int64_t)nb - 1;
+            sm->terminal_errc = RPGPU_ERRC_INPUT_STREAM_NOT_ENOUGH_BYTES;
+            sm->terminal_eof = 1;
+            sm->terminal_pos = pos;
+            phys += (uint64_t)(int64_t)h.size_bytes;
+            goto done;
+        }
+        r->flags |= RPGPU_F_COMPLETE;
+        r->crc_computed = rpo_crc_record_batch(&h, payload, need);
+        if (r->crc_computed == (uint32_t)h.crc) r->flags |= RPGPU_F_CRC_OK;
+        else if (first_bad < 0) first_bad = (int64_t)nb;
+        if (codec) r->flags |= RPGPU_F_COMPRESSED;
+        if (codec >= 5) r->flags |= RPGPU_F_CODEC_INVALID;
+        if (codec == RPGPU_CODEC_GZIP || codec == RPGPU_CODEC_ZSTD) r->flags |= RPGPU_F_CODEC_UNSUPPORTED;
+
+        r->index_base = st->index_base;
+        r->decoded_off = st->decoded_base;
+        const uint8_t* walk = NULL;
+        uint64_t walk_len = 0, limit = 0;
+        int do_walk = 0;
+        if (codec == 0) {
+            r->decoded_len = (uint32_t)need;
+            walk = payload;
+            walk_len = need;
+            limit = need;
+            do_walk = (job_flags & RPGPU_JOB_PARSE) != 0;
+        } else if ((codec == RPGPU_CODEC_LZ4 || codec == RPGPU_CODEC_SNAPPY) && (job_flags & RPGPU_JOB_DECODE)) {
+            uint64_t cap = rpo_decode_capacity((int)codec, payload, need);
+            if (st->decoded_base + cap > decoded_cap) {
+                st->overflow |= 4;
+                r->flags |= RPGPU_F_DECODE_OVERFLOW;
+            } else {
+                size_t got = 0;
+                int rc = rpo_uncompress((int)codec, payload, need, decoded + st->decoded_base, cap, &got);
+                if (rc == -2) {
+                    r->flags |= RPGPU_F_DECODE_OVERFLOW;
+                } else if (rc == 0) {
+                    r->flags |= RPGPU_F_CODEC_OK;
+                    r->decoded_len = (uint32_t)got;
+                    /* reset_size_checksum_metadata (storage/parser_utils.cc:114-120) */
+                    rpo_header nh = h;
+                    nh.attrs = (int16_t)((uint16_t)nh.attrs & ~7u);
+                    nh.size_bytes = (int32_t)(RPGPU_HEADER_SIZE + got);
+                    nh.crc = (int32_t)rpo_crc_record_batch(&nh, decoded + st->decoded_base, got);
+                    nh.header_crc = rpo_internal_header_only_crc(&nh);
+                    r->decoded_crc = (uint32_t)nh.crc;
+                    r->decoded_header_crc = nh.header_crc;
+                    walk = decoded + st->decoded_base;
+                    walk_len = got;
+                    do_walk = (job_flags & RPGPU_JOB_PARSE) != 0;
+                }
+                st->decoded_base += cap;
+                limit = cap;
+            }
+        }
+        if (do_walk) {
+            uint64_t slots = (h.record_count > 0 && (uint64_t)h.record_count <= limit) ? (uint64_t)h.record_count : 0;
+            uint64_t base = st->index_base;
+            int idx_ok = 1;
+            if (base + slots > index_cap) { st->overflow |= 2; idx_ok = 0; }
+            uint8_t perr;
+            uint64_t trailing;
+            r->records_parsed = rpo_walk_records(walk, walk_len, h.record_count, (uint32_t)(st->batch_base + nb),
+                                                 idx_ok ? index + base : NULL, idx_ok ? slots : 0, &perr, &trailing);
+            r->flags |= RPGPU_F_PARSED;
+            r->parse_err = perr;
+            if (perr == RPGPU_PARSE_ERR_NONE) {
+                r->flags |= RPGPU_F_PARSE_ASYNC_OK;
+                if (trailing == 0) r->flags |= RPGPU_F_PARSE_OK;
+                else r->parse_err = RPGPU_PARSE_ERR_TRAILING;
+            }
+            if ((r->flags & RPGPU_F_PARSE_OK) && idx_ok) r->flags |= RPGPU_F_INDEX_WRITTEN;
+            else if (!idx_ok) r->parse_err = r->parse_err ? r->parse_err : RPGPU_PARSE_ERR_INDEX_CAPACITY;
+            st->index_base += slots;
+            seg_records += slots;
+        }
+        nb++;
+        phys += (uint64_t)(int64_t)h.size_bytes;
+        pos += RPGPU_HEADER_SIZE + need;
+        if (pos > len) pos = len; /* cannot happen: need <= rem - 61 */
+    }
+    sm->terminal_pos = pos;
+done:
+    sm->n_batches = nb;
+    sm->n_records = seg_records;
+    /* checksumming_consumer checkpoint (storage/log_replayer.cc:62-79) */
+    uint64_t good = (first_bad < 0) ? nb : (uint64_t)first_bad;
+    sm->first_bad = (uint32_t)good;
+    sm->bytes_consumed = 0;
+    uint64_t upto = (first_bad < 0) ? nb : (uint64_t)first_bad + 1;
+    for (uint64_t i = 0; i < upto; i++)
+        sm->bytes_consumed += (uint64_t)(int64_t)batches[st->batch_base + i].size_bytes;
+    if (good > 0) {
+        const rpgpu_batch_result* g = &batches[st->batch_base + good - 1];
+        sm->has_checkpoint = 1;
+        sm->ckpt_last_offset = (int64_t)((uint64_t)g->base_offset + (uint64_t)(int64_t)g->last_offset_delta);
+        /* _file_pos_to_end_of_batch = size_on_disk + physical_base_offset,
+         * physical offsets accumulate size_bytes (storage/parser.cc:118-128) */
+        uint64_t ph = 0;
+        for (uint64_t i = 0; i < good - 1; i++) ph += (uint64_t)(int64_t)batches[st->batch_base + i].size_bytes;
+        sm->ckpt_truncate_pos = ph + (uint64_t)(int64_t)g->size_bytes;
+    }
+    (void)phys;
+    st->batch_base += nb;
+    return (int64_t)nb;
+}
+
+int rpo_run_job(const uint8_t* data, const uint64_t* seg_offsets, uint32_t n_segments,
+                uint32_t job_flags, rpgpu_batch_result* batches, uint64_t batch_cap,
+                rpgpu_record_index* index, uint64_t index_cap, uint8_t* decoded,
+                uint64_t decoded_cap, rpgpu_segment_summary* summaries,
+                rpgpu_job_totals* totals, uint64_t* valid_bitmap) {
+    rpo_job_state st = {0, 0, 0, 0};
+    for (uint32_t s = 0; s < n_segments; s++) {
+        rpo_scan_segment(data + seg_offsets[s], seg_offsets[s + 1] - seg_offsets[s], s, job_flags, batches,
+                         batch_cap, index, index_cap, decoded, decoded_cap, &summaries[s], &st);
+    }
+    memset(totals, 0, sizeof *totals);
+    totals->n_batches = st.batch_base;
+    totals->n_records = st.index_base;
+    totals->decoded_bytes = st.decoded_base;
+    totals->overflow = st.overflow;
+    if (valid_bitmap) {
+        for (uint64_t i = 0; i < st.batch_base; i++) {
+            if (rpo_batch_valid(&batches[i], job_flags)) valid_bitmap[i >> 6] |= 1ull << (i & 63);
+            else valid_bitmap[i >> 6] &= ~(1ull << (i & 63));
+        }
+    }
+    return 0;
+}
+
+/* ======================================================================== */
+/* CPU baseline (timed on the GPU box's host cores by bench.py)              */
+/* ======================================================================== */
+typedef struct base_task {
+    const uint8_t* data;
+    const uint64_t* seg_offsets;
+    uint32_t seg_lo, seg_hi;
+    int hw;
+    int64_t batches;
+    uint64_t bytes;
+} base_task;
+
+static void* base_worker(void* arg) {
+    base_task* t = (base_task*)arg;
+    rpgpu_record_index* scratch = (rpgpu_record_index*)malloc(sizeof(rpgpu_record_index) * 65536);
+    for (uint32_t s = t->seg_lo; s < t->seg_hi; s++) {
+        const uint8_t* seg = t->data + t->seg_offsets[s];
+        uint64_t len = t->seg_offsets[s + 1] - t->seg_offsets[s], pos = 0;
+        while (len - pos >= RPGPU_HEADER_SIZE) {
+            rpo_header h;
+            rpo_header_from_disk(seg + pos, &h);
+            if (h.header_crc == 0) break;
+            uint8_t b[61];
+            memcpy(b, seg + pos, 61);
+            uint32_t hc = t->hw ? rpo_crc32c_extend_hw(0, b + 4, 57) : rpo_crc32c_extend(0, b + 4, 57);
+            if (hc != h.header_crc) break;
+            uint64_t need = (uint32_t)((uint32_t)h.size_bytes - RPGPU_HEADER_SIZE);
+            if (len - pos - RPGPU_HEADER_SIZE < need) break;
+            const uint8_t* payload = seg + pos + RPGPU_HEADER_SIZE;
+            uint32_t c = t->hw ? crc_record_batch_hw(&h, payload, need) : rpo_crc_record_batch(&h, payload, need);
+            if (c != (uint32_t)h.crc) break;
+            if (((uint16_t)h.attrs & 7) == 0) {
+                uint8_t perr;
+                uint64_t trailing;
+                rpo_walk_records(payload, need, h.record_count, 0, scratch, 65536, &perr, &trailing);
+            }
+            t->batches++;
+            t->bytes += RPGPU_HEADER_SIZE + need;
+            pos += RPGPU_HEADER_SIZE + need;
+        }
+    }
+    free(scratch);
+    return NULL;
+}
+
+int64_t rpo_baseline_validate(const uint8_t* data, const uint64_t* seg_offsets,
+                              uint32_t n_segments, int threads, int use_hw_crc,
+                              double* seconds, uint64_t* bytes) {
+    if (threads < 1) threads = 1;
+    if ((uint32_t)threads > n_segments) threads = (int)n_segments;
+    base_task* tasks = (base_task*)calloc((size_t)threads, sizeof(base_task));
+    pthread_t* th = (pthread_t*)calloc((size_t)threads, sizeof(pthread_t));
+    crc_init();
+    struct timespec t0, t1;
+    clock_gettime(CLOCK_MONOTONIC, &t0);
+    for (int i = 0; i < threads; i++) {
+        tasks[i].data = data;
+        tasks[i].seg_offsets = seg_offsets;
+        tasks[i].seg_lo = (uint32_t)((uint64_t)n_segments * (uint64_t)i / (uint64_t)threads);
+        tasks[i].seg_hi = (uint32_t)((uint64_t)n_segments * (uint64_t)(i + 1) / (uint64_t)threads);
+        tasks[i].hw = use_hw_crc;
+        pthread_create(&th[i], NULL, base_worker, &tasks[i]);
+    }
+    int64_t nb = 0;
+    uint64_t by = 0;
+    for (int i = 0; i < threads; i++) {
+        pthread_join(th[i], NULL);
+        nb += tasks[i].batches;
+        by += tasks[i].bytes;
+    }
+    clock_gettime(CLOCK_MONOTONIC, &t1);
+    *seconds = (double)(t1.tv_sec - t0.tv_sec) + 1e-9 * (double)(t1.tv_nsec - t0.tv_nsec);
+    *bytes = by;
+    free(tasks);
+    free(th);
+    return nb;
+}
