@@ -244,6 +244,7 @@ enum rpgpu_layout {
 typedef struct rpgpu_job {
     const uint8_t* d_data;
     const uint64_t* d_seg_offsets;   /* n_segments + 1 entries */
+    const uint64_t* h_seg_offsets;   /* HOST copy of the same offsets (sizes the launch grids) */
     uint32_t n_segments;
     uint32_t layout;                 /* rpgpu_layout */
     uint32_t flags;                  /* RPGPU_JOB_* */

@@ -936,27 +936,46 @@ int64_t rpo_scan_segment(const uint8_t* seg, uint64_t len, uint32_t segment, uin
         if (codec >= 5) r->flags |= RPGPU_F_CODEC_INVALID;
         if (codec == RPGPU_CODEC_GZIP || codec == RPGPU_CODEC_ZSTD) r->flags |= RPGPU_F_CODEC_UNSUPPORTED;
 
+        /* Plan (engine rule, see DESIGN.md "index and arena planning"): the
+         * record-index slots and decode-arena bytes of a batch are reserved
+         * from its header and payload structure alone, before any decode, so
+         * the GPU can assign them with prefix sums.  Reservations never depend
+         * on whether the decode or the walk later succeed. */
+        uint64_t slots = 0, cap = 0;
+        int decodable = (codec == RPGPU_CODEC_LZ4 || codec == RPGPU_CODEC_SNAPPY) && (job_flags & RPGPU_JOB_DECODE);
+        if (codec == 0) {
+            if ((job_flags & RPGPU_JOB_PARSE) && h.record_count > 0 && (uint64_t)h.record_count <= need)
+                slots = (uint64_t)h.record_count;
+        } else if (decodable) {
+            cap = rpo_decode_capacity((int)codec, payload, need);
+            if ((job_flags & RPGPU_JOB_PARSE) && h.record_count > 0 && (uint64_t)h.record_count <= cap)
+                slots = (uint64_t)h.record_count;
+        }
         r->index_base = st->index_base;
         r->decoded_off = st->decoded_base;
+        st->index_base += slots;
+        st->decoded_base += cap;
+        seg_records += slots;
+        int idx_ok = r->index_base + slots <= index_cap;
+        if (!idx_ok) st->overflow |= 2;
+
         const uint8_t* walk = NULL;
-        uint64_t walk_len = 0, limit = 0;
+        uint64_t walk_len = 0;
         int do_walk = 0;
         if (codec == 0) {
             r->decoded_len = (uint32_t)need;
             walk = payload;
             walk_len = need;
-            limit = need;
             do_walk = (job_flags & RPGPU_JOB_PARSE) != 0;
-        } else if ((codec == RPGPU_CODEC_LZ4 || codec == RPGPU_CODEC_SNAPPY) && (job_flags & RPGPU_JOB_DECODE)) {
-            uint64_t cap = rpo_decode_capacity((int)codec, payload, need);
-            if (st->decoded_base + cap > decoded_cap) {
+        } else if (decodable) {
+            if (r->decoded_off + cap > decoded_cap) {
                 st->overflow |= 4;
                 r->flags |= RPGPU_F_DECODE_OVERFLOW;
             } else {
                 size_t got = 0;
-                int rc = rpo_uncompress((int)codec, payload, need, decoded + st->decoded_base, cap, &got);
+                int rc = rpo_uncompress((int)codec, payload, need, decoded + r->decoded_off, cap, &got);
                 if (rc == -2) {
-                    r->flags |= RPGPU_F_DECODE_OVERFLOW;
+                    r->flags |= RPGPU_F_DECODE_OVERFLOW; /* cannot happen with the planned cap */
                 } else if (rc == 0) {
                     r->flags |= RPGPU_F_CODEC_OK;
                     r->decoded_len = (uint32_t)got;
@@ -964,27 +983,21 @@ int64_t rpo_scan_segment(const uint8_t* seg, uint64_t len, uint32_t segment, uin
                     rpo_header nh = h;
                     nh.attrs = (int16_t)((uint16_t)nh.attrs & ~7u);
                     nh.size_bytes = (int32_t)(RPGPU_HEADER_SIZE + got);
-                    nh.crc = (int32_t)rpo_crc_record_batch(&nh, decoded + st->decoded_base, got);
+                    nh.crc = (int32_t)rpo_crc_record_batch(&nh, decoded + r->decoded_off, got);
                     nh.header_crc = rpo_internal_header_only_crc(&nh);
                     r->decoded_crc = (uint32_t)nh.crc;
                     r->decoded_header_crc = nh.header_crc;
-                    walk = decoded + st->decoded_base;
+                    walk = decoded + r->decoded_off;
                     walk_len = got;
                     do_walk = (job_flags & RPGPU_JOB_PARSE) != 0;
                 }
-                st->decoded_base += cap;
-                limit = cap;
             }
         }
         if (do_walk) {
-            uint64_t slots = (h.record_count > 0 && (uint64_t)h.record_count <= limit) ? (uint64_t)h.record_count : 0;
-            uint64_t base = st->index_base;
-            int idx_ok = 1;
-            if (base + slots > index_cap) { st->overflow |= 2; idx_ok = 0; }
             uint8_t perr;
             uint64_t trailing;
             r->records_parsed = rpo_walk_records(walk, walk_len, h.record_count, (uint32_t)(st->batch_base + nb),
-                                                 idx_ok ? index + base : NULL, idx_ok ? slots : 0, &perr, &trailing);
+                                                 idx_ok ? index + r->index_base : NULL, idx_ok ? slots : 0, &perr, &trailing);
             r->flags |= RPGPU_F_PARSED;
             r->parse_err = perr;
             if (perr == RPGPU_PARSE_ERR_NONE) {
@@ -992,10 +1005,10 @@ int64_t rpo_scan_segment(const uint8_t* seg, uint64_t len, uint32_t segment, uin
                 if (trailing == 0) r->flags |= RPGPU_F_PARSE_OK;
                 else r->parse_err = RPGPU_PARSE_ERR_TRAILING;
             }
-            if ((r->flags & RPGPU_F_PARSE_OK) && idx_ok) r->flags |= RPGPU_F_INDEX_WRITTEN;
-            else if (!idx_ok) r->parse_err = r->parse_err ? r->parse_err : RPGPU_PARSE_ERR_INDEX_CAPACITY;
-            st->index_base += slots;
-            seg_records += slots;
+            if (r->flags & RPGPU_F_PARSE_OK) {
+                if (idx_ok) r->flags |= RPGPU_F_INDEX_WRITTEN;
+                else r->parse_err = RPGPU_PARSE_ERR_INDEX_CAPACITY;
+            }
         }
         nb++;
         phys += (uint64_t)(int64_t)h.size_bytes;

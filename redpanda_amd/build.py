@@ -1,0 +1,81 @@
+"""Builds librpgpu.so in-tree: hand-written gfx950 kernels + the C-ABI host
+runtime (hipcc), the host generator (g++), linked into one shared library.
+
+No JIT, no torch extension: the .so lives next to this file so it travels to
+the GPU box with the repo snapshot.
+"""
+from __future__ import annotations
+
+import os
+import shutil
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+CSRC = os.path.join(HERE, "csrc")
+INC = os.path.join(ROOT, "include")
+OUT = os.path.join(HERE, "librpgpu.so")
+BUILD = os.path.join(HERE, "_build")
+ARCH = os.environ.get("RPGPU_ARCH", "gfx950")
+
+HIP_SOURCES = ["rp_kernels.hip", "rp_runtime.hip"]
+CXX_SOURCES = ["rp_gen.cpp"]
+
+
+def _hipcc():
+    for c in (os.environ.get("HIPCC"), "/opt/rocm/bin/hipcc", shutil.which("hipcc")):
+        if c and os.path.exists(c):
+            return c
+    raise RuntimeError("hipcc not found")
+
+
+def _run(cmd):
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        sys.stderr.write(" ".join(cmd) + "\n" + r.stdout + r.stderr)
+        raise RuntimeError(f"build step failed: {cmd[0]} ({r.returncode})")
+    return r
+
+
+def _stale(obj, srcs):
+    if not os.path.exists(obj):
+        return True
+    t = os.path.getmtime(obj)
+    return any(os.path.getmtime(s) > t for s in srcs)
+
+
+def build(force: bool = False, verbose: bool = False) -> str:
+    os.makedirs(BUILD, exist_ok=True)
+    hipcc = _hipcc()
+    headers = [os.path.join(INC, "rpgpu.h"), os.path.join(CSRC, "rp_internal.h")]
+    objs = []
+    for src in HIP_SOURCES:
+        s = os.path.join(CSRC, src)
+        o = os.path.join(BUILD, src + ".o")
+        if force or _stale(o, [s] + headers):
+            cmd = [hipcc, f"--offload-arch={ARCH}", "-O3", "-fPIC", "-std=c++17", "-I", INC, "-I", CSRC,
+                   "-Wall", "-Wno-unused-function", "-Wno-unused-variable", "-c", s, "-o", o]
+            if verbose:
+                print(" ".join(cmd))
+            _run(cmd)
+        objs.append(o)
+    for src in CXX_SOURCES:
+        s = os.path.join(CSRC, src)
+        o = os.path.join(BUILD, src + ".o")
+        if force or _stale(o, [s] + headers):
+            cmd = ["g++", "-O2", "-fPIC", "-std=c++17", "-I", INC, "-Wall", "-c", s, "-o", o]
+            if verbose:
+                print(" ".join(cmd))
+            _run(cmd)
+        objs.append(o)
+    if force or _stale(OUT, objs):
+        cmd = [hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", OUT] + objs + ["-ldl", "-lpthread"]
+        if verbose:
+            print(" ".join(cmd))
+        _run(cmd)
+    return OUT
+
+
+if __name__ == "__main__":
+    print(build(force="--force" in sys.argv, verbose=True))

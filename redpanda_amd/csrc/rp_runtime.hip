@@ -1,0 +1,372 @@
+// rp_runtime.hip — host side of the C-ABI (include/rpgpu.h): contexts,
+// constant tables, the submit pipeline, memory helpers, the host CRC32C
+// behind crc::crc32c and the synthetic segment generator.
+#include <hip/hip_runtime.h>
+#include <nmmintrin.h>
+
+#include <algorithm>
+#include <atomic>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <mutex>
+#include <random>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "rp_internal.h"
+
+namespace rp {
+
+// ---------------------------------------------------------------------------
+// GF(2) helpers for the CRC tables (reflected CRC32C)
+// ---------------------------------------------------------------------------
+static uint32_t raw_step_zero(uint32_t c, const uint32_t* t0) { return t0[c & 0xFF] ^ (c >> 8); }
+
+static void build_tables(Tables* T) {
+    uint32_t t0[256];
+    for (uint32_t i = 0; i < 256; i++) {
+        uint32_t c = i;
+        for (int k = 0; k < 8; k++) c = (c & 1) ? (c >> 1) ^ kCrcPoly : c >> 1;
+        t0[i] = c;
+    }
+    // T_d[b]: raw CRC of byte b followed by d zero bytes
+    for (uint32_t b = 0; b < 256; b++) {
+        uint32_t c = t0[b];
+        for (uint32_t d = 0; d < 57; d++) {
+            T->hdr[d][b] = c;
+            if (d < 4) T->slice[d][b] = c;
+            c = raw_step_zero(c, t0);
+        }
+    }
+    // shift tables: state byte j (value b << 8j) advanced over kStream*2^l zero bytes
+    for (uint32_t l = 0; l < kCombineLevels; l++) {
+        const uint64_t n = (uint64_t)kStream << l;
+        for (uint32_t j = 0; j < 4; j++) {
+            for (uint32_t b = 0; b < 256; b++) {
+                uint32_t c = b << (8 * j);
+                for (uint64_t z = 0; z < n; z++) c = raw_step_zero(c, t0);
+                T->comb[l][j][b] = c;
+            }
+        }
+    }
+    uint32_t c = 0xFFFFFFFFu;
+    for (int z = 0; z < 40; z++) c = raw_step_zero(c, t0);
+    T->c40 = c;
+    for (int z = 40; z < 57; z++) c = raw_step_zero(c, t0);
+    T->c57 = c;
+    T->pad[0] = T->pad[1] = 0;
+}
+
+// the combine tables take ~2^13 * 1024 zero-steps; build them once per process
+static const Tables* host_tables() {
+    static Tables* T = nullptr;
+    static std::once_flag once;
+    std::call_once(once, [] {
+        T = new Tables;
+        build_tables(T);
+    });
+    return T;
+}
+
+}  // namespace rp
+
+using namespace rp;
+
+struct rpgpu_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    Tables* d_tables = nullptr;
+    // growable device workspace
+    void* ws = nullptr;
+    size_t ws_bytes = 0;
+    // pinned staging for small host->device uploads
+    void* pin = nullptr;
+    size_t pin_bytes = 0;
+    bool timing = false;
+    hipEvent_t ev[6] = {};
+    float last_ms[4] = {0, 0, 0, 0};
+    bool have_timing = false;
+    uint32_t cu_count = 256;
+    std::string err;
+};
+
+namespace {
+
+int fail(rpgpu_ctx* c, int code, const char* what, hipError_t e = hipSuccess) {
+    if (c) {
+        c->err = what;
+        if (e != hipSuccess) {
+            c->err += ": ";
+            c->err += hipGetErrorString(e);
+        }
+    }
+    return code;
+}
+
+#define HIPCHK(ctx, call)                                                   \
+    do {                                                                    \
+        hipError_t _e = (call);                                             \
+        if (_e != hipSuccess) return fail((ctx), RPGPU_E_HIP, #call, _e);   \
+    } while (0)
+
+size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
+
+}  // namespace
+
+extern "C" {
+
+int rpgpu_device_count(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
+int rpgpu_create(int device, rpgpu_ctx** out) {
+    if (!out) return RPGPU_E_INVALID;
+    *out = nullptr;
+    int n = rpgpu_device_count();
+    if (n <= 0 || device < 0 || device >= n) return RPGPU_E_NO_DEVICE;
+    rpgpu_ctx* c = new rpgpu_ctx;
+    c->device = device;
+    if (hipSetDevice(device) != hipSuccess) { delete c; return RPGPU_E_NO_DEVICE; }
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0)
+        c->cu_count = (uint32_t)prop.multiProcessorCount;
+    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) { delete c; return RPGPU_E_HIP; }
+    if (hipMalloc(&c->d_tables, sizeof(Tables)) != hipSuccess) { delete c; return RPGPU_E_NOMEM; }
+    if (hipMemcpy(c->d_tables, host_tables(), sizeof(Tables), hipMemcpyHostToDevice) != hipSuccess) {
+        hipFree(c->d_tables);
+        delete c;
+        return RPGPU_E_HIP;
+    }
+    for (auto& e : c->ev) hipEventCreate(&e);
+    *out = c;
+    return RPGPU_OK;
+}
+
+int rpgpu_destroy(rpgpu_ctx* c) {
+    if (!c) return RPGPU_E_INVALID;
+    hipSetDevice(c->device);
+    if (c->stream) hipStreamSynchronize(c->stream);
+    if (c->ws) hipFree(c->ws);
+    if (c->pin) hipHostFree(c->pin);
+    if (c->d_tables) hipFree(c->d_tables);
+    for (auto& e : c->ev)
+        if (e) hipEventDestroy(e);
+    if (c->stream) hipStreamDestroy(c->stream);
+    delete c;
+    return RPGPU_OK;
+}
+
+const char* rpgpu_strerror(int s) {
+    switch (s) {
+    case RPGPU_OK: return "ok";
+    case RPGPU_E_INVALID: return "invalid argument";
+    case RPGPU_E_NO_DEVICE: return "no HIP device";
+    case RPGPU_E_NOMEM: return "out of memory";
+    case RPGPU_E_OVERFLOW: return "output capacity too small";
+    case RPGPU_E_CODEC: return "uncompress failed";
+    case RPGPU_E_UNSUPPORTED: return "codec not supported by the engine";
+    case RPGPU_E_HIP: return "HIP runtime error";
+    }
+    return "unknown";
+}
+
+const char* rpgpu_last_error(rpgpu_ctx* c) { return c ? c->err.c_str() : ""; }
+
+int rpgpu_dev_alloc(rpgpu_ctx* c, size_t bytes, void** out) {
+    if (!c || !out) return RPGPU_E_INVALID;
+    hipSetDevice(c->device);
+    if (hipMalloc(out, bytes ? bytes : 1) != hipSuccess) return fail(c, RPGPU_E_NOMEM, "hipMalloc");
+    return RPGPU_OK;
+}
+int rpgpu_dev_free(rpgpu_ctx* c, void* p) {
+    if (!c) return RPGPU_E_INVALID;
+    hipSetDevice(c->device);
+    HIPCHK(c, hipFree(p));
+    return RPGPU_OK;
+}
+int rpgpu_host_alloc(rpgpu_ctx* c, size_t bytes, void** out) {
+    if (!c || !out) return RPGPU_E_INVALID;
+    if (hipHostMalloc(out, bytes ? bytes : 1, hipHostMallocDefault) != hipSuccess) return fail(c, RPGPU_E_NOMEM, "hipHostMalloc");
+    return RPGPU_OK;
+}
+int rpgpu_host_free(rpgpu_ctx* c, void* p) {
+    if (!c) return RPGPU_E_INVALID;
+    HIPCHK(c, hipHostFree(p));
+    return RPGPU_OK;
+}
+static hipStream_t pick(rpgpu_ctx* c, void* s) { return s ? (hipStream_t)s : c->stream; }
+int rpgpu_memcpy_h2d(rpgpu_ctx* c, void* dst, const void* src, size_t n, void* s) {
+    if (!c) return RPGPU_E_INVALID;
+    HIPCHK(c, hipMemcpyAsync(dst, src, n, hipMemcpyHostToDevice, pick(c, s)));
+    return RPGPU_OK;
+}
+int rpgpu_memcpy_d2h(rpgpu_ctx* c, void* dst, const void* src, size_t n, void* s) {
+    if (!c) return RPGPU_E_INVALID;
+    HIPCHK(c, hipMemcpyAsync(dst, src, n, hipMemcpyDeviceToHost, pick(c, s)));
+    return RPGPU_OK;
+}
+int rpgpu_memset(rpgpu_ctx* c, void* dst, int v, size_t n, void* s) {
+    if (!c) return RPGPU_E_INVALID;
+    HIPCHK(c, hipMemsetAsync(dst, v, n, pick(c, s)));
+    return RPGPU_OK;
+}
+int rpgpu_sync(rpgpu_ctx* c, void* s) {
+    if (!c) return RPGPU_E_INVALID;
+    HIPCHK(c, hipStreamSynchronize(pick(c, s)));
+    return RPGPU_OK;
+}
+
+int rpgpu_set_timing(rpgpu_ctx* c, int enable) {
+    if (!c) return RPGPU_E_INVALID;
+    c->timing = enable != 0;
+    return RPGPU_OK;
+}
+
+int rpgpu_last_timings(rpgpu_ctx* c, float* ms, int n) {
+    if (!c || !ms) return RPGPU_E_INVALID;
+    if (!c->have_timing) return RPGPU_E_INVALID;
+    // events are resolved lazily so the submit stays asynchronous
+    HIPCHK(c, hipEventSynchronize(c->ev[5]));
+    float t[4] = {0, 0, 0, 0};
+    hipEventElapsedTime(&t[0], c->ev[0], c->ev[5]);
+    hipEventElapsedTime(&t[1], c->ev[0], c->ev[1]);
+    hipEventElapsedTime(&t[2], c->ev[1], c->ev[3]);
+    hipEventElapsedTime(&t[3], c->ev[3], c->ev[4]);
+    for (int i = 0; i < n && i < 4; i++) ms[i] = t[i];
+    return RPGPU_OK;
+}
+
+// ---------------------------------------------------------------------------
+// submit
+// ---------------------------------------------------------------------------
+int rpgpu_submit(rpgpu_ctx* c, const rpgpu_job* job, void* stream) {
+    if (!c || !job || !job->d_data || !job->d_seg_offsets || !job->h_seg_offsets || job->n_segments == 0 ||
+        !job->d_batches || !job->d_summaries || !job->d_totals)
+        return fail(c, RPGPU_E_INVALID, "rpgpu_submit: missing argument");
+    if (((uintptr_t)job->d_data & 15) != 0) return fail(c, RPGPU_E_INVALID, "rpgpu_submit: d_data must be 16-byte aligned");
+    if (job->layout != RPGPU_LAYOUT_DISK) return fail(c, RPGPU_E_UNSUPPORTED, "rpgpu_submit: only the disk layout is wired up");
+    if ((job->flags & RPGPU_JOB_PARSE) && !job->d_records && job->record_capacity)
+        return fail(c, RPGPU_E_INVALID, "rpgpu_submit: PARSE needs d_records");
+    hipSetDevice(c->device);
+    hipStream_t s = pick(c, stream);
+    const uint32_t nseg = job->n_segments;
+    const uint32_t cs = job->chunk_bytes ? job->chunk_bytes : (256u << 10);
+    // chunk table from the host offsets
+    uint64_t tc = 0;
+    for (uint32_t i = 0; i < nseg; i++) {
+        const uint64_t len = job->h_seg_offsets[i + 1] - job->h_seg_offsets[i];
+        uint64_t nc = (len + cs - 1) / cs;
+        tc += nc ? nc : 1;
+    }
+    if (tc > 0xFFFFFFF0ull) return fail(c, RPGPU_E_INVALID, "rpgpu_submit: too many chunks");
+    const uint64_t bcap = job->batch_capacity;
+    // workspace layout
+    size_t off = 0;
+    auto take = [&](size_t bytes) { size_t o = off; off = align_up(off + bytes, 256); return o; };
+    const size_t o_cbase = take((nseg + 1) * 8);
+    const size_t o_chunks = take(tc * sizeof(ChunkRec));
+    const size_t o_ccount = take((tc + 1) * 8);
+    const size_t o_centry = take(tc * 8);
+    const size_t o_segterm = take(nseg * sizeof(SegTerm));
+    const size_t o_slots = take((bcap + 1) * 8);
+    const size_t o_dcap = take((bcap + 1) * 8);
+    const size_t o_counters = take(16);
+    const size_t o_scan = take(scan_temp_bytes(std::max<uint64_t>(tc, bcap)) + 64);
+    const size_t need = off;
+    if (need > c->ws_bytes) {
+        if (c->ws) { hipStreamSynchronize(s); hipFree(c->ws); c->ws = nullptr; }
+        if (hipMalloc(&c->ws, need) != hipSuccess) { c->ws_bytes = 0; return fail(c, RPGPU_E_NOMEM, "workspace"); }
+        c->ws_bytes = need;
+    }
+    uint8_t* ws = (uint8_t*)c->ws;
+
+    DeviceJob j;
+    j.data = job->d_data;
+    j.seg_off = job->d_seg_offsets;
+    j.chunk_base = (const uint64_t*)(ws + o_cbase);
+    j.n_segments = nseg;
+    j.flags = job->flags;
+    j.chunk_bytes = cs;
+    j.total_chunks = (uint32_t)tc;
+    j.chunks = (ChunkRec*)(ws + o_chunks);
+    j.chunk_count = (uint64_t*)(ws + o_ccount);
+    j.chunk_entry = (uint64_t*)(ws + o_centry);
+    j.seg_term = (SegTerm*)(ws + o_segterm);
+    j.batches = job->d_batches;
+    j.batch_capacity = bcap;
+    j.slots = (uint64_t*)(ws + o_slots);
+    j.dcap = (uint64_t*)(ws + o_dcap);
+    j.records = job->d_records;
+    j.record_capacity = job->d_records ? job->record_capacity : 0;
+    j.decoded = job->d_decoded;
+    j.decoded_capacity = job->d_decoded ? job->decoded_capacity : 0;
+    j.summaries = job->d_summaries;
+    j.totals = job->d_totals;
+    j.bitmap = job->d_valid_bitmap;
+    j.tables = c->d_tables;
+    j.counters = (uint32_t*)(ws + o_counters);
+    uint64_t* scan_tmp = (uint64_t*)(ws + o_scan);
+
+    const bool tm = c->timing;
+    if (tm) HIPCHK(c, hipEventRecord(c->ev[0], s));
+    HIPCHK(c, launch_chunk_base(j, s));
+    HIPCHK(c, hipMemsetAsync(j.counters, 0, 16, s));
+    HIPCHK(c, launch_discover(j, s));
+    if (tm) HIPCHK(c, hipEventRecord(c->ev[1], s));
+    HIPCHK(c, launch_resolve(j, s));
+    HIPCHK(c, scan_exclusive_u64(j.chunk_count, tc, scan_tmp, 0, s));
+    HIPCHK(c, launch_emit(j, s));
+    const uint64_t* d_nb = j.chunk_count + tc;
+    HIPCHK(c, scan_exclusive_u64_devn(j.slots, d_nb, bcap, scan_tmp, s));
+    HIPCHK(c, scan_exclusive_u64_devn(j.dcap, d_nb, bcap, scan_tmp, s));
+    if (tm) HIPCHK(c, hipEventRecord(c->ev[3], s));
+    HIPCHK(c, launch_validate(j, s, c->cu_count));
+    if (tm) HIPCHK(c, hipEventRecord(c->ev[4], s));
+    HIPCHK(c, launch_finalize(j, s));
+    if (tm) HIPCHK(c, hipEventRecord(c->ev[5], s));
+    c->have_timing = tm;
+    return RPGPU_OK;
+}
+
+// ---------------------------------------------------------------------------
+// crc::crc32c host path (hashing/crc32c.h:19-40).  SSE4.2 crc32 instructions,
+// the same arithmetic google crc32c's x86 path uses.
+// ---------------------------------------------------------------------------
+__attribute__((target("sse4.2"))) uint32_t rpgpu_crc32c_extend(uint32_t crc, const uint8_t* p, size_t n) {
+    uint64_t l = crc ^ 0xFFFFFFFFu;
+    while (n && ((uintptr_t)p & 7)) { l = _mm_crc32_u8((uint32_t)l, *p++); n--; }
+    while (n >= 8) {
+        uint64_t v;
+        std::memcpy(&v, p, 8);
+        l = _mm_crc32_u64(l, v);
+        p += 8;
+        n -= 8;
+    }
+    uint32_t s = (uint32_t)l;
+    while (n) { s = _mm_crc32_u8(s, *p++); n--; }
+    return s ^ 0xFFFFFFFFu;
+}
+
+}  // extern "C"
+
+extern "C" {
+
+// Implemented with the decode kernels (rp_codec.hip); until then the engine
+// reports the codec as unsupported rather than decoding on the CPU.
+__attribute__((weak)) int rpgpu_uncompress(rpgpu_ctx* c, int codec, const void* in, size_t n, void* out, size_t cap,
+                                           size_t* out_len) {
+    (void)codec; (void)in; (void)n; (void)out; (void)cap;
+    if (out_len) *out_len = 0;
+    return fail(c, RPGPU_E_UNSUPPORTED, "rpgpu_uncompress: decode kernels not built");
+}
+
+__attribute__((weak)) int rpgpu_validate_host(rpgpu_ctx* c, const rpgpu_host_job* job) {
+    (void)job;
+    return fail(c, RPGPU_E_UNSUPPORTED, "rpgpu_validate_host: not built");
+}
+
+}  // extern "C"

@@ -1,0 +1,154 @@
+"""Host-side segment engine over the C-ABI.
+
+`Engine` owns one rpgpu context (one per host thread / shard, as the
+reference's shard-per-core ownership requires: SURVEY.md §8(b)).  Device
+buffers are torch tensors — torch is plumbing here (HIP allocation, streams,
+torch.distributed for the final gather); all compute is in librpgpu.so.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass
+
+import numpy as np
+
+from . import abi
+from ._lib import JobC, RpgpuError, check, load
+
+
+def _torch():
+    import torch
+    return torch
+
+
+@dataclass
+class DeviceResult:
+    batches: "object"     # torch uint8 tensor viewed as abi.BATCH_RESULT on the host
+    records: "object"
+    decoded: "object"
+    summaries: "object"
+    totals: "object"
+    bitmap: "object"
+    n_segments: int
+
+    def totals_host(self):
+        return np.frombuffer(self.totals.cpu().numpy().tobytes(), dtype=abi.JOB_TOTALS)[0]
+
+    def to_host(self):
+        t = self.totals_host()
+        nb = int(min(t["n_batches"], self.batches.numel() // abi.BATCH_RESULT.itemsize))
+        nr = int(min(t["n_records"], self.records.numel() // abi.RECORD_INDEX.itemsize))
+        nd = int(min(t["decoded_bytes"], self.decoded.numel()))
+        b = np.frombuffer(self.batches[: nb * abi.BATCH_RESULT.itemsize].cpu().numpy().tobytes(), dtype=abi.BATCH_RESULT)
+        r = np.frombuffer(self.records[: nr * abi.RECORD_INDEX.itemsize].cpu().numpy().tobytes(), dtype=abi.RECORD_INDEX)
+        d = self.decoded[:nd].cpu().numpy()
+        s = np.frombuffer(self.summaries.cpu().numpy().tobytes(), dtype=abi.SEGMENT_SUMMARY)[: self.n_segments]
+        bm = self.bitmap[: (nb + 63) // 64 * 8].cpu().numpy().view(np.uint64) if self.bitmap is not None else None
+        return HostResult(b, r, d, s, t, bm)
+
+
+@dataclass
+class HostResult:
+    batches: np.ndarray
+    records: np.ndarray
+    decoded: np.ndarray
+    summaries: np.ndarray
+    totals: np.void
+    bitmap: np.ndarray
+
+
+class Engine:
+    """One rpgpu context on one device."""
+
+    def __init__(self, device: int = 0):
+        torch = _torch()
+        if not torch.cuda.is_available():
+            raise RpgpuError("no GPU visible: the engine has no CPU fallback")
+        self.L = load()
+        self.device = device
+        torch.cuda.set_device(device)
+        ctx = C.c_void_p()
+        check(self.L.rpgpu_create(device, C.byref(ctx)), None, "rpgpu_create")
+        self.ctx = ctx
+
+    def close(self):
+        if getattr(self, "ctx", None):
+            self.L.rpgpu_destroy(self.ctx)
+            self.ctx = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def set_timing(self, on: bool = True):
+        check(self.L.rpgpu_set_timing(self.ctx, 1 if on else 0), self.ctx, "rpgpu_set_timing")
+
+    def last_timings(self):
+        ms = (C.c_float * 4)()
+        check(self.L.rpgpu_last_timings(self.ctx, ms, 4), self.ctx, "rpgpu_last_timings")
+        return {"total": ms[0], "discover": ms[1], "resolve_plan": ms[2], "validate": ms[3]}
+
+    def alloc_outputs(self, n_segments: int, batch_capacity: int, record_capacity: int,
+                      decoded_capacity: int, bitmap: bool = True):
+        torch = _torch()
+        dev = torch.device("cuda", self.device)
+        u8 = torch.uint8
+        return DeviceResult(
+            batches=torch.zeros(max(batch_capacity, 1) * abi.BATCH_RESULT.itemsize, dtype=u8, device=dev),
+            records=torch.zeros(max(record_capacity, 1) * abi.RECORD_INDEX.itemsize, dtype=u8, device=dev),
+            decoded=torch.zeros(max(decoded_capacity, 1), dtype=u8, device=dev),
+            summaries=torch.zeros(max(n_segments, 1) * abi.SEGMENT_SUMMARY.itemsize, dtype=u8, device=dev),
+            totals=torch.zeros(abi.JOB_TOTALS.itemsize, dtype=u8, device=dev),
+            bitmap=torch.zeros(((max(batch_capacity, 1) + 63) // 64) * 8, dtype=u8, device=dev) if bitmap else None,
+            n_segments=n_segments,
+        )
+
+    def submit(self, data, seg_offsets, out: DeviceResult, flags: int = abi.JOB_CRC | abi.JOB_PARSE,
+               chunk_bytes: int = 0, stream=None, d_seg_offsets=None):
+        """Enqueue one job on `stream` (default: torch's current stream).
+        `data` is a torch uint8 CUDA tensor holding the concatenated segments."""
+        torch = _torch()
+        h_off = np.ascontiguousarray(np.asarray(seg_offsets, dtype=np.uint64))
+        if d_seg_offsets is None:
+            d_seg_offsets = torch.from_numpy(h_off.view(np.int64)).to(data.device)
+        self._keep = (h_off, d_seg_offsets)
+        job = JobC()
+        job.d_data = data.data_ptr()
+        job.d_seg_offsets = d_seg_offsets.data_ptr()
+        job.h_seg_offsets = h_off.ctypes.data
+        job.n_segments = h_off.size - 1
+        job.layout = abi.LAYOUT_DISK
+        job.flags = flags
+        job.chunk_bytes = chunk_bytes
+        job.d_batches = out.batches.data_ptr()
+        job.batch_capacity = out.batches.numel() // abi.BATCH_RESULT.itemsize
+        job.d_records = out.records.data_ptr()
+        job.record_capacity = out.records.numel() // abi.RECORD_INDEX.itemsize
+        job.d_decoded = out.decoded.data_ptr()
+        job.decoded_capacity = out.decoded.numel()
+        job.d_summaries = out.summaries.data_ptr()
+        job.d_totals = out.totals.data_ptr()
+        job.d_valid_bitmap = out.bitmap.data_ptr() if out.bitmap is not None else 0
+        s = stream if stream is not None else torch.cuda.current_stream(data.device)
+        check(self.L.rpgpu_submit(self.ctx, C.byref(job), C.c_void_p(s.cuda_stream)), self.ctx, "rpgpu_submit")
+        return out
+
+    def validate(self, data, seg_offsets, flags: int = abi.JOB_CRC | abi.JOB_PARSE, batch_capacity=None,
+                 record_capacity=None, decoded_capacity=None, chunk_bytes: int = 0) -> HostResult:
+        """Convenience: allocate outputs, run, synchronize, copy back."""
+        torch = _torch()
+        offs = np.asarray(seg_offsets, dtype=np.uint64)
+        total = int(offs[-1])
+        nseg = offs.size - 1
+        if batch_capacity is None:
+            batch_capacity = total // abi.HEADER_SIZE + nseg + 1
+        if record_capacity is None:
+            record_capacity = max(total // 4, 64)
+        if decoded_capacity is None:
+            decoded_capacity = max(total * 8, 1 << 16) if flags & abi.JOB_DECODE else 1
+        out = self.alloc_outputs(nseg, batch_capacity, record_capacity, decoded_capacity)
+        self.submit(data, offs, out, flags, chunk_bytes)
+        torch.cuda.synchronize(data.device)
+        return out.to_host()
