@@ -267,9 +267,10 @@ typedef struct rpgpu_job {
  * bounds. */
 int rpgpu_submit(rpgpu_ctx* ctx, const rpgpu_job* job, void* stream);
 
-/* Device-time of the kernels of the last rpgpu_submit on this context,
- * measured with HIP events on the launch stream (milliseconds).  Indices:
- * 0 = whole pipeline, 1 = discover, 2 = resolve+plan, 3 = validate. */
+/* Device time of the pipeline stages, measured with HIP events recorded on
+ * the launch stream, averaged over every timed rpgpu_submit since the
+ * previous call (milliseconds; the call resets the average).  Indices:
+ * 0 = whole pipeline, 1 = discover, 2 = resolve+emit+plan, 3 = validate. */
 int rpgpu_last_timings(rpgpu_ctx* ctx, float* ms, int n);
 /* Enable/disable per-kernel event timing (off by default). */
 int rpgpu_set_timing(rpgpu_ctx* ctx, int enable);

@@ -62,9 +62,12 @@ def load():
         import torch  # noqa: F401  (one HIP runtime per process)
     except Exception:
         pass
-    if not os.path.exists(LIB_PATH):
-        raise RpgpuError(f"{LIB_PATH} missing: run `python -m redpanda_amd.build` (no CPU fallback exists)")
-    L = C.CDLL(LIB_PATH)
+    path = LIB_PATH
+    if os.environ.get("RPGPU_CHECKED") == "1":
+        path = os.path.join(HERE, "librpgpu_checked.so")
+    if not os.path.exists(path):
+        raise RpgpuError(f"{path} missing: run `python -m redpanda_amd.build` (no CPU fallback exists)")
+    L = C.CDLL(path)
     vp, i32, u32, u64, sz = C.c_void_p, C.c_int, C.c_uint32, C.c_uint64, C.c_size_t
     sig = {
         "rpgpu_device_count": (i32, []),

@@ -45,37 +45,41 @@ def _stale(obj, srcs):
     return any(os.path.getmtime(s) > t for s in srcs)
 
 
-def build(force: bool = False, verbose: bool = False) -> str:
-    os.makedirs(BUILD, exist_ok=True)
+def build(force: bool = False, verbose: bool = False, checked: bool = False) -> str:
+    """checked=True builds librpgpu_checked.so (bounds-checked kernels)."""
+    out = OUT if not checked else os.path.join(HERE, "librpgpu_checked.so")
+    bdir = BUILD if not checked else BUILD + "_checked"
+    extra = [] if not checked else ["-DRPGPU_CHECKED"]
+    os.makedirs(bdir, exist_ok=True)
     hipcc = _hipcc()
     headers = [os.path.join(INC, "rpgpu.h"), os.path.join(CSRC, "rp_internal.h")]
     objs = []
     for src in HIP_SOURCES:
         s = os.path.join(CSRC, src)
-        o = os.path.join(BUILD, src + ".o")
+        o = os.path.join(bdir, src + ".o")
         if force or _stale(o, [s] + headers):
             cmd = [hipcc, f"--offload-arch={ARCH}", "-O3", "-fPIC", "-std=c++17", "-I", INC, "-I", CSRC,
-                   "-Wall", "-Wno-unused-function", "-Wno-unused-variable", "-c", s, "-o", o]
+                   "-Wall", "-Wno-unused-function", "-Wno-unused-variable", "-Wno-unused-label"] + extra + ["-c", s, "-o", o]
             if verbose:
                 print(" ".join(cmd))
             _run(cmd)
         objs.append(o)
     for src in CXX_SOURCES:
         s = os.path.join(CSRC, src)
-        o = os.path.join(BUILD, src + ".o")
+        o = os.path.join(bdir, src + ".o")
         if force or _stale(o, [s] + headers):
             cmd = ["g++", "-O2", "-fPIC", "-std=c++17", "-I", INC, "-Wall", "-c", s, "-o", o]
             if verbose:
                 print(" ".join(cmd))
             _run(cmd)
         objs.append(o)
-    if force or _stale(OUT, objs):
-        cmd = [hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", OUT] + objs + ["-ldl", "-lpthread"]
+    if force or _stale(out, objs):
+        cmd = [hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", out] + objs + ["-ldl", "-lpthread"]
         if verbose:
             print(" ".join(cmd))
         _run(cmd)
-    return OUT
+    return out
 
 
 if __name__ == "__main__":
-    print(build(force="--force" in sys.argv, verbose=True))
+    print(build(force="--force" in sys.argv, verbose=True, checked="--checked" in sys.argv))

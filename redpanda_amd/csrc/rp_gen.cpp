@@ -173,32 +173,29 @@ int encode_records(Rng& rng, std::vector<uint8_t>& out, size_t target, const rpg
         // one as the last record and pad its value to hit the target exactly
         RecSpec minr = r;
         minr.vlen = 0;
-        if (left < full + rec_total(idx + 1, minr, nh) + 8) {
+        if (left < full + rec_total(idx + 1, minr, nh) + 64) {
+            // last record: search key/header-value padding and the value
+            // length for an exact fit (varint widths make some totals
+            // unreachable with the value alone)
+            bool found = false;
             RecSpec last = r;
-            last.vlen = 0;
-            size_t base = rec_total(idx, last, nh);
-            if (base > left) {
-                // cannot fit even a minimal record: shrink the key
-                last.klen = 0;
-                base = rec_total(idx, last, nh);
-                if (base > left) break;
+            for (int dk = 0; dk < 4 && !found; dk++) {
+                for (int dh = 0; dh < 10 && !found; dh++) {
+                    RecSpec t = r;
+                    t.klen = r.klen + dk;
+                    if (nh > 0) t.hv[0] = r.hv[0] + dh;
+                    t.vlen = 0;
+                    const size_t base = rec_total(idx, t, nh);
+                    if (base > left) continue;
+                    int32_t v = (int32_t)(left - base);
+                    while (v > 0 && rec_total(idx, RecSpec{t.klen, v, {t.hk[0], t.hk[1]}, {t.hv[0], t.hv[1]}}, nh) > left) v--;
+                    t.vlen = v;
+                    if (rec_total(idx, t, nh) == left) { last = t; found = true; }
+                }
             }
-            int32_t v = (int32_t)(left - base);
-            // varint widths grow with v; step down until the total matches
-            while (v > 0 && rec_total(idx, RecSpec{last.klen, v, {last.hk[0], last.hk[1]}, {last.hv[0], last.hv[1]}}, nh) > left) v--;
-            last.vlen = v;
-            size_t tot = rec_total(idx, last, nh);
-            if (tot != left && last.klen > 0) {
-                // one byte short because a varint shrank: absorb it in the key
-                last.klen += (int32_t)(left - tot);
-                tot = rec_total(idx, last, nh);
-            }
-            if (tot != left) {
-                // fall back: grow the first header value byte by byte
-                while (tot < left) { last.hv[0]++; tot = rec_total(idx, last, nh); }
-            }
+            if (!found) break;
             specs.push_back(last);
-            used += tot;
+            used += left;
             idx++;
             break;
         }

@@ -56,6 +56,7 @@ struct SegTerm {
 
 struct DeviceJob {
     const uint8_t* data;
+    uint64_t data_len;            // bytes of d_data (= h_seg_offsets[n_segments])
     const uint64_t* seg_off;      // n_segments + 1
     const uint64_t* chunk_base;   // n_segments + 1 : first global chunk index of each segment
     uint32_t n_segments;

@@ -17,6 +17,20 @@ namespace rp {
 
 #define DEV __device__ __forceinline__
 
+// Bounds-checked build (-DRPGPU_CHECKED, librpgpu_checked.so): every data
+// access of k_validate is checked against the allocation and reported with
+// printf instead of faulting.  Fault localisation only; never benchmarked.
+#ifdef RPGPU_CHECKED
+#include <cstdio>
+#define RP_CHECK(flag, cond, fmt, ...)                                               \
+    do {                                                                            \
+        if (!(cond)) {                                                              \
+            if (__lane_id() == 0) printf("RPGPU_CHECK %d " fmt "\n", __LINE__, __VA_ARGS__); \
+            flag = true;                                                            \
+        }                                                                           \
+    } while (0)
+#endif
+
 DEV uint32_t lane() { return __lane_id(); }
 
 DEV uint32_t wave_xor(uint32_t v) {
@@ -29,12 +43,13 @@ DEV uint32_t wave_or(uint32_t v) {
     for (int o = 32; o > 0; o >>= 1) v |= __shfl_xor(v, o, 64);
     return v;
 }
-DEV uint32_t rl(uint32_t v, int l) { return __builtin_amdgcn_readlane(v, l); }
+DEV uint32_t rl(uint32_t v, int l) { return (uint32_t)__builtin_amdgcn_readlane((int)v, l); }
+// readfirstlane/readlane return int: go through uint32_t so the low half is
+// never sign-extended into the high half (positions >= 2 GiB).
+DEV uint32_t uni32(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); }
 DEV uint64_t uni64(uint64_t v) {
-    return (uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)v) |
-           ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(v >> 32)) << 32);
+    return (uint64_t)uni32((uint32_t)v) | ((uint64_t)uni32((uint32_t)(v >> 32)) << 32);
 }
-DEV uint32_t uni32(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
 
 // byte k (0..60) of a header whose bytes are spread one per lane
 DEV uint32_t hb(uint32_t b, int k) { return rl(b, k); }
@@ -456,6 +471,15 @@ __global__ __launch_bounds__(256) void k_emit(DeviceJob j) {
     const uint32_t l = lane();
     uint64_t p = j.chunk_entry[g];
     for (uint64_t i = 0; i < cnt; i++) {
+#ifdef RPGPU_CHECKED
+        {
+            bool bad = false;
+            RP_CHECK(bad, p < len, "emit g=%llu i=%llu cnt=%llu p=%llu len=%llu entry=%llu", (unsigned long long)g,
+                     (unsigned long long)i, (unsigned long long)cnt, (unsigned long long)p, (unsigned long long)len,
+                     (unsigned long long)j.chunk_entry[g]);
+            if (bad) break;
+        }
+#endif
         Hdr h = wave_header(seg, len, p, T);  // known valid (resolved chain)
         const uint64_t ord = base_ord + i;
         const bool complete = (len - p - RPGPU_HEADER_SIZE) >= h.need;
@@ -628,7 +652,6 @@ DEV uint32_t shift_lvl(const uint8_t* lds, uint32_t s, uint32_t lvl) {
     return t[s & 0xFF] ^ t[256 + ((s >> 8) & 0xFF)] ^ t[512 + ((s >> 16) & 0xFF)] ^ t[768 + (s >> 24)];
 }
 
-typedef uint32_t u32x4a __attribute__((ext_vector_type(4), aligned(4)));
 
 // 16 bytes at an arbitrary address, zero past `lim` (exclusive, absolute).
 DEV void load16u(const uint8_t* p, const uint8_t* lim, uint32_t& r0, uint32_t& r1, uint32_t& r2, uint32_t& r3) {
@@ -784,6 +807,9 @@ DEV WalkResult walk_records(const uint8_t* base, uint64_t n, int32_t rc, uint32_
         const uint64_t errs = __ballot(act && l < exact && r.err != 0);
         const uint32_t nok = errs ? (uint32_t)__builtin_ctzll(errs) : exact;  // records parsed OK
         if (l < nok && done + l < out_cap) {
+#ifdef RPGPU_CHECKED
+            if (my_start >= n) printf("RPGPU_CHECK walk start %llu n %llu\n", (unsigned long long)my_start, (unsigned long long)n);
+#endif
             rpgpu_record_index e;
             e.batch = batch_ord;
             e.rec_pos = (uint32_t)my_start;
@@ -855,19 +881,40 @@ __global__ __launch_bounds__(1024) void k_validate(DeviceJob j) {
         const uint64_t n = uni32((uint32_t)(R->size_bytes - (int32_t)RPGPU_HEADER_SIZE));
         const uint64_t E = S + n;
         const uint8_t* data = j.data;
+#ifdef RPGPU_CHECKED
+        {
+            bool bad = false;
+            RP_CHECK(bad, segi < j.n_segments, "b=%llu segi=%u flags=%u", (unsigned long long)b, segi, flags0);
+            if (bad) continue;
+            const uint64_t slen = j.seg_off[segi + 1] - j.seg_off[segi];
+            RP_CHECK(bad, segi < j.n_segments && uni64(R->file_pos) + RPGPU_HEADER_SIZE + n <= slen && E <= j.data_len,
+                     "b=%llu seg=%u file_pos=%llu n=%llu slen=%llu E=%llu data_len=%llu", (unsigned long long)b, segi,
+                     (unsigned long long)R->file_pos, (unsigned long long)n, (unsigned long long)slen,
+                     (unsigned long long)E, (unsigned long long)j.data_len);
+            const uint64_t ib0 = j.slots[b], ib1 = j.slots[b + 1];
+            RP_CHECK(bad, ib0 <= ib1 && ib1 <= j.slots[nb], "b=%llu slots %llu %llu total %llu", (unsigned long long)b,
+                     (unsigned long long)ib0, (unsigned long long)ib1, (unsigned long long)j.slots[nb]);
+            if (bad) continue;
+        }
+#endif
         // CRC state after the BE40 prefix with init ~0: c40 ^ raw contribution
         // of the prefix bytes (computed by k_emit, parked in reserved1)
         uint32_t Tst = uni32((uint32_t)R->reserved1) ^ T->c40;
 
-        if (n > 0) {
-            const uint64_t Ntot = (n + kStream - 1) / kStream;
+        // Lane regions are anchored at E16 = E rounded down to 16 bytes so
+        // every vector load is an aligned 16-byte load; chunk c spans
+        // [E16 - kStream*(Ntot-c), +kStream), chunk 0 is clipped at S, and
+        // the <16-byte tail [E16, E) is folded in after the rounds.
+        const uint64_t E16 = (E & ~(uint64_t)15) > S ? (E & ~(uint64_t)15) : S;
+        const uint64_t n16 = E16 - S;
+        if (n16 > 0) {
+            const uint64_t Ntot = (n16 + kStream - 1) / kStream;
             const uint64_t R_ = (Ntot + 127) / 128;
             for (uint64_t r = 0; r < R_; r++) {
-                // first chunk of this round; chunk c spans [E - kStream*(Ntot-c), +kStream)
                 const int64_t c0 = (int64_t)Ntot - (int64_t)(128 * (R_ - r));
                 const int64_t ca = c0 + 2 * (int64_t)l;
                 // lane region start (bytes), may lie before S in round 0
-                const int64_t a = (int64_t)E - (int64_t)kStream * ((int64_t)Ntot - ca);
+                const int64_t a = (int64_t)E16 - (int64_t)kStream * ((int64_t)Ntot - ca);
                 uint32_t sA = 0, sB = 0;
                 if (r == 0) {
                     // the lane holding chunk 0 starts from the prefix state
@@ -876,37 +923,27 @@ __global__ __launch_bounds__(1024) void k_validate(DeviceJob j) {
                 } else if (l == 0) {
                     sA = Tst;
                 }
-                const uint8_t* pa = data + a;
                 if (a >= (int64_t)S) {
-                    // full 256-byte region: 65 dwords from a 4-aligned base
-                    const uintptr_t ad = (uintptr_t)pa;
-                    const u32x4a* q = (const u32x4a*)(ad & ~(uintptr_t)3);
-                    const uint32_t sh = (uint32_t)(ad & 3);
-                    u32x4a v[17];
+                    // full 256-byte region, 16-byte aligned
+#ifdef RPGPU_CHECKED
+                    if (!(a + 256 <= (int64_t)E16 && (a & 15) == 0))
+                        printf("RPGPU_CHECK region b=%llu a=%lld E16=%llu S=%llu\n", (unsigned long long)b, (long long)a,
+                               (unsigned long long)E16, (unsigned long long)S);
+#endif
+                    const uint4* q = (const uint4*)(data + a);
+                    uint4 v[16];
 #pragma unroll
                     for (int k = 0; k < 16; k++) v[k] = q[k];
-                    // the 65th dword is only needed when misaligned; it then
-                    // holds the region's last byte, so it is always in bounds
-                    v[16].x = 0u;
-                    if (sh) v[16].x = ((const uint32_t*)(q + 16))[0];
 #pragma unroll
                     for (int k = 0; k < 8; k++) {
-                        const uint32_t wa0 = __builtin_amdgcn_alignbyte(v[k].y, v[k].x, sh);
-                        const uint32_t wa1 = __builtin_amdgcn_alignbyte(v[k].z, v[k].y, sh);
-                        const uint32_t wa2 = __builtin_amdgcn_alignbyte(v[k].w, v[k].z, sh);
-                        const uint32_t wa3 = __builtin_amdgcn_alignbyte(v[k + 1].x, v[k].w, sh);
-                        const uint32_t wb0 = __builtin_amdgcn_alignbyte(v[k + 8].y, v[k + 8].x, sh);
-                        const uint32_t wb1 = __builtin_amdgcn_alignbyte(v[k + 8].z, v[k + 8].y, sh);
-                        const uint32_t wb2 = __builtin_amdgcn_alignbyte(v[k + 8].w, v[k + 8].z, sh);
-                        const uint32_t wb3 = __builtin_amdgcn_alignbyte(v[k + 9].x, v[k + 8].w, sh);
-                        sA = step4(lds, K, sA, wa0);
-                        sB = step4(lds, K, sB, wb0);
-                        sA = step4(lds, K, sA, wa1);
-                        sB = step4(lds, K, sB, wb1);
-                        sA = step4(lds, K, sA, wa2);
-                        sB = step4(lds, K, sB, wb2);
-                        sA = step4(lds, K, sA, wa3);
-                        sB = step4(lds, K, sB, wb3);
+                        sA = step4(lds, K, sA, v[k].x);
+                        sB = step4(lds, K, sB, v[k + 8].x);
+                        sA = step4(lds, K, sA, v[k].y);
+                        sB = step4(lds, K, sB, v[k + 8].y);
+                        sA = step4(lds, K, sA, v[k].z);
+                        sB = step4(lds, K, sB, v[k + 8].z);
+                        sA = step4(lds, K, sA, v[k].w);
+                        sB = step4(lds, K, sB, v[k + 8].w);
                     }
                 } else if (a + (int64_t)kLaneBytes > (int64_t)S) {
                     // region straddles the payload start (round 0 only): bytes
@@ -917,8 +954,6 @@ __global__ __launch_bounds__(1024) void k_validate(DeviceJob j) {
                         if (se <= (int64_t)S) continue;
                         uint32_t sv = st ? sB : sA;
                         int64_t x = sa > (int64_t)S ? sa : (int64_t)S;
-                        // bytewise up to a 4-byte boundary of the stream end,
-                        // then whole words
                         for (; ((se - x) & 3) != 0; x++) sv = step1(lds, K, sv, data[x]);
                         for (; x < se; x += 4) sv = step4(lds, K, sv, ldu32(data + x));
                         if (st) sB = sv; else sA = sv;
@@ -935,6 +970,8 @@ __global__ __launch_bounds__(1024) void k_validate(DeviceJob j) {
                 Tst = uni32(sv);  // lane 0 holds the state after this round
             }
         }
+        // tail bytes [E16, E): fewer than 16, uniform
+        for (uint64_t x = E16; x < E; x++) Tst = uni32(step1(lds, K, Tst, data[x]));
         const uint32_t crc = ~Tst;
         uint32_t f = flags0;
         if (crc == uni32(R->crc)) f |= RPGPU_F_CRC_OK;

@@ -5,6 +5,7 @@
 #include <nmmintrin.h>
 
 #include <algorithm>
+#include <array>
 #include <atomic>
 #include <cstdio>
 #include <cstdlib>
@@ -85,9 +86,10 @@ struct rpgpu_ctx {
     void* pin = nullptr;
     size_t pin_bytes = 0;
     bool timing = false;
-    hipEvent_t ev[6] = {};
-    float last_ms[4] = {0, 0, 0, 0};
-    bool have_timing = false;
+    // one event set per timed submit: start, discover done, plan done,
+    // validate done, end; resolved lazily by rpgpu_last_timings
+    std::vector<std::array<hipEvent_t, 5>> ev_sets;
+    size_t ev_used = 0;
     uint32_t cu_count = 256;
     std::string err;
 };
@@ -141,7 +143,6 @@ int rpgpu_create(int device, rpgpu_ctx** out) {
         delete c;
         return RPGPU_E_HIP;
     }
-    for (auto& e : c->ev) hipEventCreate(&e);
     *out = c;
     return RPGPU_OK;
 }
@@ -153,8 +154,8 @@ int rpgpu_destroy(rpgpu_ctx* c) {
     if (c->ws) hipFree(c->ws);
     if (c->pin) hipHostFree(c->pin);
     if (c->d_tables) hipFree(c->d_tables);
-    for (auto& e : c->ev)
-        if (e) hipEventDestroy(e);
+    for (auto& set : c->ev_sets)
+        for (auto& e : set) hipEventDestroy(e);
     if (c->stream) hipStreamDestroy(c->stream);
     delete c;
     return RPGPU_OK;
@@ -226,17 +227,22 @@ int rpgpu_set_timing(rpgpu_ctx* c, int enable) {
     return RPGPU_OK;
 }
 
+// Averages over every timed submit since the previous call (then resets).
 int rpgpu_last_timings(rpgpu_ctx* c, float* ms, int n) {
     if (!c || !ms) return RPGPU_E_INVALID;
-    if (!c->have_timing) return RPGPU_E_INVALID;
-    // events are resolved lazily so the submit stays asynchronous
-    HIPCHK(c, hipEventSynchronize(c->ev[5]));
-    float t[4] = {0, 0, 0, 0};
-    hipEventElapsedTime(&t[0], c->ev[0], c->ev[5]);
-    hipEventElapsedTime(&t[1], c->ev[0], c->ev[1]);
-    hipEventElapsedTime(&t[2], c->ev[1], c->ev[3]);
-    hipEventElapsedTime(&t[3], c->ev[3], c->ev[4]);
-    for (int i = 0; i < n && i < 4; i++) ms[i] = t[i];
+    if (c->ev_used == 0) return fail(c, RPGPU_E_INVALID, "rpgpu_last_timings: no timed submit");
+    double acc[4] = {0, 0, 0, 0};
+    for (size_t i = 0; i < c->ev_used; i++) {
+        auto& e = c->ev_sets[i];
+        HIPCHK(c, hipEventSynchronize(e[4]));
+        float t;
+        hipEventElapsedTime(&t, e[0], e[4]); acc[0] += t;
+        hipEventElapsedTime(&t, e[0], e[1]); acc[1] += t;
+        hipEventElapsedTime(&t, e[1], e[2]); acc[2] += t;
+        hipEventElapsedTime(&t, e[2], e[3]); acc[3] += t;
+    }
+    for (int i = 0; i < n && i < 4; i++) ms[i] = (float)(acc[i] / (double)c->ev_used);
+    c->ev_used = 0;
     return RPGPU_OK;
 }
 
@@ -286,6 +292,7 @@ int rpgpu_submit(rpgpu_ctx* c, const rpgpu_job* job, void* stream) {
 
     DeviceJob j;
     j.data = job->d_data;
+    j.data_len = job->h_seg_offsets[nseg];
     j.seg_off = job->d_seg_offsets;
     j.chunk_base = (const uint64_t*)(ws + o_cbase);
     j.n_segments = nseg;
@@ -311,24 +318,44 @@ int rpgpu_submit(rpgpu_ctx* c, const rpgpu_job* job, void* stream) {
     j.counters = (uint32_t*)(ws + o_counters);
     uint64_t* scan_tmp = (uint64_t*)(ws + o_scan);
 
+    // RPGPU_DEBUG_SYNC=1: synchronize after every stage and name the stage
+    // that failed (fault localisation; never set in measured runs)
+    static const bool dbg = [] { const char* e = getenv("RPGPU_DEBUG_SYNC"); return e && *e == '1'; }();
+#define STAGE(name, call)                                                                  \
+    do {                                                                                   \
+        HIPCHK(c, (call));                                                                 \
+        if (dbg) {                                                                         \
+            hipError_t _e = hipStreamSynchronize(s);                                       \
+            if (_e != hipSuccess) return fail(c, RPGPU_E_HIP, "stage " name " failed", _e); \
+        }                                                                                  \
+    } while (0)
     const bool tm = c->timing;
-    if (tm) HIPCHK(c, hipEventRecord(c->ev[0], s));
-    HIPCHK(c, launch_chunk_base(j, s));
+    hipEvent_t* ev = nullptr;
+    if (tm) {
+        if (c->ev_used == c->ev_sets.size()) {
+            std::array<hipEvent_t, 5> set;
+            for (auto& e : set) HIPCHK(c, hipEventCreate(&e));
+            c->ev_sets.push_back(set);
+        }
+        ev = c->ev_sets[c->ev_used++].data();
+        HIPCHK(c, hipEventRecord(ev[0], s));
+    }
+    STAGE("chunk_base", launch_chunk_base(j, s));
     HIPCHK(c, hipMemsetAsync(j.counters, 0, 16, s));
-    HIPCHK(c, launch_discover(j, s));
-    if (tm) HIPCHK(c, hipEventRecord(c->ev[1], s));
-    HIPCHK(c, launch_resolve(j, s));
-    HIPCHK(c, scan_exclusive_u64(j.chunk_count, tc, scan_tmp, 0, s));
-    HIPCHK(c, launch_emit(j, s));
+    STAGE("discover", launch_discover(j, s));
+    if (tm) HIPCHK(c, hipEventRecord(ev[1], s));
+    STAGE("resolve", launch_resolve(j, s));
+    STAGE("scan_chunks", scan_exclusive_u64(j.chunk_count, tc, scan_tmp, 0, s));
+    STAGE("emit", launch_emit(j, s));
     const uint64_t* d_nb = j.chunk_count + tc;
-    HIPCHK(c, scan_exclusive_u64_devn(j.slots, d_nb, bcap, scan_tmp, s));
-    HIPCHK(c, scan_exclusive_u64_devn(j.dcap, d_nb, bcap, scan_tmp, s));
-    if (tm) HIPCHK(c, hipEventRecord(c->ev[3], s));
-    HIPCHK(c, launch_validate(j, s, c->cu_count));
-    if (tm) HIPCHK(c, hipEventRecord(c->ev[4], s));
-    HIPCHK(c, launch_finalize(j, s));
-    if (tm) HIPCHK(c, hipEventRecord(c->ev[5], s));
-    c->have_timing = tm;
+    STAGE("scan_slots", scan_exclusive_u64_devn(j.slots, d_nb, bcap, scan_tmp, s));
+    STAGE("scan_dcap", scan_exclusive_u64_devn(j.dcap, d_nb, bcap, scan_tmp, s));
+    if (tm) HIPCHK(c, hipEventRecord(ev[2], s));
+    STAGE("validate", launch_validate(j, s, c->cu_count));
+    if (tm) HIPCHK(c, hipEventRecord(ev[3], s));
+    STAGE("finalize", launch_finalize(j, s));
+    if (tm) HIPCHK(c, hipEventRecord(ev[4], s));
+#undef STAGE
     return RPGPU_OK;
 }
 
