@@ -107,6 +107,7 @@ def main():
     ap.add_argument("--chunk-kib", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--gather", choices=["bitmap", "index"], default="bitmap")
+    ap.add_argument("--no-parse", action="store_true", help="CRC only (diagnostic; not the headline workload)")
     args = ap.parse_args()
 
     import torch
@@ -130,7 +131,7 @@ def main():
     log(f"[rank {rank}] generated {len(parts)} x {seg_bytes >> 20} MiB, {n_batches} batches in {time.time() - t0:.1f}s")
 
     eng = Engine(local)
-    flags = abi.JOB_CRC | abi.JOB_PARSE
+    flags = abi.JOB_CRC | (0 if args.no_parse else abi.JOB_PARSE)
     rec_per_batch = 32
     out = eng.alloc_outputs(len(parts), n_batches + 16, n_batches * rec_per_batch, 1)
     d_offs = torch.from_numpy(offs.view(np.int64)).to(device)
@@ -156,7 +157,7 @@ def main():
     # correctness of the measured workload (size-independent properties)
     h = out.to_host()
     nb = len(h.batches)
-    all_ok = bool(nb == n_batches and np.all(h.batches["flags"] & abi.F_PARSE_OK)
+    all_ok = bool(nb == n_batches and (args.no_parse or np.all(h.batches["flags"] & abi.F_PARSE_OK))
                   and np.all(h.batches["flags"] & abi.F_CRC_OK) and h.totals["overflow"] == 0)
     bm_ok = bool(np.all(h.bitmap[: nb // 64] == np.uint64(0xFFFFFFFFFFFFFFFF)))
     n_records = int(h.totals["n_records"])

@@ -65,6 +65,8 @@ def load():
     path = LIB_PATH
     if os.environ.get("RPGPU_CHECKED") == "1":
         path = os.path.join(HERE, "librpgpu_checked.so")
+    elif os.environ.get("RPGPU_STAMPS") == "1":
+        path = os.path.join(HERE, "librpgpu_stamps.so")
     if not os.path.exists(path):
         raise RpgpuError(f"{path} missing: run `python -m redpanda_amd.build` (no CPU fallback exists)")
     L = C.CDLL(path)

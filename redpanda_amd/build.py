@@ -19,7 +19,7 @@ OUT = os.path.join(HERE, "librpgpu.so")
 BUILD = os.path.join(HERE, "_build")
 ARCH = os.environ.get("RPGPU_ARCH", "gfx950")
 
-HIP_SOURCES = ["rp_kernels.hip", "rp_runtime.hip"]
+HIP_SOURCES = ["rp_kernels.hip", "rp_validate.hip", "rp_codec.hip", "rp_runtime.hip"]
 CXX_SOURCES = ["rp_gen.cpp"]
 
 
@@ -45,14 +45,23 @@ def _stale(obj, srcs):
     return any(os.path.getmtime(s) > t for s in srcs)
 
 
-def build(force: bool = False, verbose: bool = False, checked: bool = False) -> str:
-    """checked=True builds librpgpu_checked.so (bounds-checked kernels)."""
-    out = OUT if not checked else os.path.join(HERE, "librpgpu_checked.so")
-    bdir = BUILD if not checked else BUILD + "_checked"
-    extra = [] if not checked else ["-DRPGPU_CHECKED"]
+VARIANTS = {
+    # name: (library, build dir, extra flags)
+    "": (OUT, BUILD, []),
+    "checked": (os.path.join(HERE, "librpgpu_checked.so"), BUILD + "_checked", ["-DRPGPU_CHECKED"]),
+    "stamps": (os.path.join(HERE, "librpgpu_stamps.so"), BUILD + "_stamps", ["-DRPGPU_STAMPS"]),
+}
+
+
+def build(force: bool = False, verbose: bool = False, checked: bool = False, variant: str = "") -> str:
+    """checked=True builds librpgpu_checked.so (bounds-checked kernels);
+    variant="stamps" builds librpgpu_stamps.so (per-phase cycle stamps)."""
+    if checked:
+        variant = "checked"
+    out, bdir, extra = VARIANTS[variant]
     os.makedirs(bdir, exist_ok=True)
     hipcc = _hipcc()
-    headers = [os.path.join(INC, "rpgpu.h"), os.path.join(CSRC, "rp_internal.h")]
+    headers = [os.path.join(INC, "rpgpu.h"), os.path.join(CSRC, "rp_internal.h"), os.path.join(CSRC, "rp_device.h")]
     objs = []
     for src in HIP_SOURCES:
         s = os.path.join(CSRC, src)
@@ -82,4 +91,5 @@ def build(force: bool = False, verbose: bool = False, checked: bool = False) -> 
 
 
 if __name__ == "__main__":
-    print(build(force="--force" in sys.argv, verbose=True, checked="--checked" in sys.argv))
+    v = "checked" if "--checked" in sys.argv else "stamps" if "--stamps" in sys.argv else ""
+    print(build(force="--force" in sys.argv, verbose=True, variant=v))

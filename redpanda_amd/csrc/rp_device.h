@@ -1,0 +1,207 @@
+// rp_device.h — device helpers shared by the kernel translation units
+// (rp_kernels.hip, rp_validate.hip, rp_codec.hip).  Wave64 idioms only.
+#pragma once
+
+#include "rp_internal.h"
+
+namespace rp {
+
+#define DEV __device__ __forceinline__
+
+DEV uint32_t lane() { return __lane_id(); }
+
+DEV uint32_t wave_xor(uint32_t v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v ^= __shfl_xor(v, o, 64);
+    return v;
+}
+DEV uint32_t wave_or(uint32_t v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v |= __shfl_xor(v, o, 64);
+    return v;
+}
+DEV uint32_t rl(uint32_t v, int l) { return (uint32_t)__builtin_amdgcn_readlane((int)v, l); }
+// readfirstlane/readlane return int: go through uint32_t so the low half is
+// never sign-extended into the high half (positions >= 2 GiB).
+DEV uint32_t uni32(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); }
+DEV uint64_t uni64(uint64_t v) {
+    return (uint64_t)uni32((uint32_t)v) | ((uint64_t)uni32((uint32_t)(v >> 32)) << 32);
+}
+
+// byte k (0..60) of a header whose bytes are spread one per lane
+DEV uint32_t hb(uint32_t b, int k) { return rl(b, k); }
+DEV uint32_t h32(uint32_t b, int k) { return hb(b, k) | (hb(b, k + 1) << 8) | (hb(b, k + 2) << 16) | (hb(b, k + 3) << 24); }
+DEV uint64_t h64(uint32_t b, int k) { return (uint64_t)h32(b, k) | ((uint64_t)h32(b, k + 4) << 32); }
+DEV uint32_t h16(uint32_t b, int k) { return hb(b, k) | (hb(b, k + 1) << 8); }
+
+// ---------------------------------------------------------------------------
+// Wave-cooperative header read: read_header_impl (storage/parser.cc:139-176).
+// Lane l holds header byte l; internal_header_only_crc (model/record_utils.cc:
+// 34-55) is computed in parallel: byte l at distance 60-l from the end
+// contributes T_{60-l}[b] (raw CRC), the ~0 init contributes c57.
+// ---------------------------------------------------------------------------
+struct Hdr {
+    int32_t status;   // -1 ok, else parser errc
+    int32_t eof;
+    uint32_t hcrc, computed;
+    int32_t size;
+    uint64_t need;    // (uint32_t)(size - 61)
+    uint32_t b;       // this lane's header byte
+};
+
+DEV Hdr wave_header(const uint8_t* __restrict__ seg, uint64_t len, uint64_t p, const Tables* __restrict__ T) {
+    Hdr h;
+    h.eof = 0;
+    h.b = 0;
+    h.hcrc = h.computed = 0;
+    h.size = 0;
+    h.need = 0;
+    const uint64_t rem = len - p;
+    if (rem == 0) { h.status = RPGPU_ERRC_END_OF_STREAM; h.eof = 1; return h; }
+    if (rem < RPGPU_HEADER_SIZE) { h.status = RPGPU_ERRC_INPUT_STREAM_NOT_ENOUGH_BYTES; h.eof = 1; return h; }
+    const uint32_t l = lane();
+    uint32_t b = (l < RPGPU_HEADER_SIZE) ? (uint32_t)seg[p + l] : 0u;
+    uint32_t contrib = (l >= 4 && l < RPGPU_HEADER_SIZE) ? T->hdr[60 - l][b] : 0u;
+    uint32_t raw = wave_xor(contrib);
+    h.b = b;
+    h.computed = ~(T->c57 ^ raw);
+    h.hcrc = h32(b, 0);
+    h.size = (int32_t)h32(b, 4);
+    h.need = (uint32_t)((uint32_t)h.size - RPGPU_HEADER_SIZE);
+    if (h.hcrc == 0) { h.status = RPGPU_ERRC_FALLOCATED_FILE_READ_ZERO_BYTES_FOR_HEADER; return h; }
+    if (h.hcrc != h.computed) { h.status = RPGPU_ERRC_HEADER_ONLY_CRC_MISSMATCH; return h; }
+    h.status = -1;
+    return h;
+}
+
+// 4 bytes at an arbitrary byte address, from the aligned dwords around it.
+// The second dword is only touched when the bytes straddle it, so the read
+// never goes past the last byte asked for.
+DEV uint32_t ldu32(const uint8_t* p) {
+    uintptr_t a = (uintptr_t)p;
+    const uint32_t* q = (const uint32_t*)(a & ~(uintptr_t)3);
+    const uint32_t sh = (uint32_t)(a & 3);
+    uint32_t hi = 0;
+    if (sh) hi = q[1];
+    return __builtin_amdgcn_alignbyte(hi, q[0], sh);
+}
+
+// BE40 prefix position of disk header byte l (21..60): fields are reversed
+// byte-wise (model/record_utils.cc:68-80).
+DEV int be_index(uint32_t l) {
+    // field starts on disk and lengths: attrs 21/2, lod 23/4, first_ts 27/8,
+    // max_ts 35/8, pid 43/8, epoch 51/2, base_seq 53/4, record_count 57/4
+    int fs, fl;
+    if (l < 23) { fs = 21; fl = 2; }
+    else if (l < 27) { fs = 23; fl = 4; }
+    else if (l < 35) { fs = 27; fl = 8; }
+    else if (l < 43) { fs = 35; fl = 8; }
+    else if (l < 51) { fs = 43; fl = 8; }
+    else if (l < 53) { fs = 51; fl = 2; }
+    else if (l < 57) { fs = 53; fl = 4; }
+    else { fs = 57; fl = 4; }
+    return (fs - 21) + (fl - 1 - ((int)l - fs));
+}
+
+#define HD __host__ __device__ inline
+
+HD uint32_t rd32h(const uint8_t* p) { return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24); }
+
+// ---------------------------------------------------------------------------
+// Decode-arena plan rule (engine rule, restated by the oracle as
+// rpo_decode_capacity): bytes reserved for one compressed payload, from its
+// frame structure alone, before any decode.  Shared by k_emit and the
+// rpgpu_uncompress host path.
+// ---------------------------------------------------------------------------
+HD uint32_t xxh32_small(const uint8_t* p, uint32_t n) {
+    // XXH32 for n < 16 (the LZ4F header checksum input is <= 14 bytes)
+    const uint32_t P1 = 0x9E3779B1u, P3 = 0xC2B2AE3Du, P4 = 0x27D4EB2Fu, P5 = 0x165667B1u, P2 = 0x85EBCA77u;
+    uint32_t h = P5 + n;
+    uint32_t i = 0;
+    for (; i + 4 <= n; i += 4) {
+        uint32_t v = (uint32_t)p[i] | ((uint32_t)p[i + 1] << 8) | ((uint32_t)p[i + 2] << 16) | ((uint32_t)p[i + 3] << 24);
+        h += v * P3;
+        h = ((h << 17) | (h >> 15)) * P4;
+    }
+    for (; i < n; i++) { h += p[i] * P5; h = ((h << 11) | (h >> 21)) * P1; }
+    h ^= h >> 15; h *= P2; h ^= h >> 13; h *= P3; h ^= h >> 16;
+    return h;
+}
+
+
+HD int snappy_varint32_dev(const uint8_t* s, uint64_t n, uint32_t* v) {
+    uint32_t r = 0;
+    for (uint32_t i = 0; i < 5; i++) {
+        if (i >= n) return -1;
+        uint32_t b = s[i];
+        if (i < 4) {
+            r |= (b & 127) << (7 * i);
+            if (b < 128) { *v = r; return (int)i + 1; }
+        } else {
+            r |= (b & 127) << 28;
+            if (b < 16) { *v = r; return 5; }
+            return -1;
+        }
+    }
+    return -1;
+}
+
+// Same rule as the oracle's rpo_decode_capacity (engine plan rule).
+HD uint64_t decode_capacity_dev(int codec, const uint8_t* s, uint64_t n) {
+    if (n == 0) return 0;
+    if (codec == RPGPU_CODEC_LZ4) {
+        if (n < 7) return 0;
+        uint32_t magic = rd32h(s);
+        if ((magic & 0xFFFFFFF0u) == 0x184D2A50u || magic != 0x184D2204u) return 0;
+        uint32_t flg = s[4];
+        uint64_t hs = 7 + (((flg >> 3) & 1) ? 8 : 0) + ((flg & 1) ? 4 : 0);
+        if (n < hs) return 0;
+        if ((flg >> 1) & 1) return 0;
+        if (((flg >> 6) & 3) != 1) return 0;
+        uint32_t bd = s[5];
+        if ((bd >> 7) & 1) return 0;
+        uint32_t bsid = (bd >> 4) & 7;
+        if (bsid < 4 || (bd & 15)) return 0;
+        if (((xxh32_small(s + 4, (uint32_t)(hs - 5)) >> 8) & 0xFF) != s[hs - 1]) return 0;
+        const uint64_t bmax = bsid == 4 ? (64u << 10) : bsid == 5 ? (256u << 10) : bsid == 6 ? (1u << 20) : (4u << 20);
+        const uint32_t bcs = (flg >> 4) & 1;
+        uint64_t cap = 0, pos = hs;
+        while (n - pos >= 4) {
+            uint32_t bh = rd32h(s + pos);
+            if (bh == 0) break;
+            uint64_t bsz = bh & 0x7FFFFFFFu;
+            if (bsz > bmax) break;
+            cap += (bh & 0x80000000u) ? bsz : bmax;
+            pos += 4;
+            uint64_t adv = bsz + (bcs ? 4 : 0);
+            if (n - pos < adv) break;
+            pos += adv;
+        }
+        return cap;
+    }
+    if (codec == RPGPU_CODEC_SNAPPY) {
+        const uint8_t magic[8] = {0x82, 'S', 'N', 'A', 'P', 'P', 'Y', 0};
+        bool java = n >= 16;
+        for (int i = 0; i < 8 && java; i++) java = s[i] == magic[i];
+        uint32_t ulen;
+        if (!java) {
+            if (snappy_varint32_dev(s, n, &ulen) < 0) return 0;
+            return ((uint64_t)ulen <= 22ull * n + 64) ? ulen : 0;
+        }
+        uint64_t cap = 0, pos = 16;
+        while (n - pos >= 4) {
+            int32_t clen = (int32_t)(((uint32_t)s[pos] << 24) | ((uint32_t)s[pos + 1] << 16) |
+                                     ((uint32_t)s[pos + 2] << 8) | s[pos + 3]);
+            if (clen <= 0 || n - pos - 4 < (uint64_t)clen) break;
+            if (snappy_varint32_dev(s + pos + 4, (uint64_t)clen, &ulen) < 0) break;
+            if ((uint64_t)ulen > 22ull * (uint64_t)clen + 64) break;
+            cap += ulen;
+            pos += 4 + (uint64_t)clen;
+        }
+        return cap;
+    }
+    return 0;
+}
+
+
+}  // namespace rp

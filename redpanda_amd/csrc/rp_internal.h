@@ -12,21 +12,28 @@ namespace rp {
 constexpr uint64_t kNone = ~0ull;
 constexpr uint32_t kCrcPoly = 0x82F63B78u;
 
-// CRC chunking of the validate kernel: every lane owns two consecutive
-// streams of kStream bytes; a wave round covers 64 * 2 * kStream bytes.
+// Combine tables: shift a raw CRC state over kStream * 2^l zero bytes.
 constexpr uint32_t kStream = 128;
-constexpr uint32_t kLaneBytes = 2 * kStream;       // 256
-constexpr uint32_t kRoundBytes = 64 * kLaneBytes;  // 16 KiB
-constexpr uint32_t kCombineLevels = 7;             // shift by kStream * 2^l, l = 0..6
+constexpr uint32_t kCombineLevels = 7;             // l = 0..6 (128 B .. 8 KiB)
 
-// LDS image of the validate kernel (bytes).
-//  [0, 128 KiB): slice-by-4 CRC tables replicated 32x so lane L always hits
-//                bank L%32 (2 tables per 256-byte row: see rp_kernels.hip)
-//  [128 KiB, 156 KiB): combine tables, 7 levels x 4 byte-tables x 256
-constexpr uint32_t kLdsSliceBytes = 128u << 10;
-constexpr uint32_t kLdsCombineOff = kLdsSliceBytes;
-constexpr uint32_t kLdsCombineBytes = kCombineLevels * 4 * 256 * 4;
-constexpr uint32_t kLdsValidateBytes = kLdsCombineOff + kLdsCombineBytes;
+// Validate kernel (rp_validate.hip): one wave per batch, 16 waves per
+// workgroup (4 per SIMD), one workgroup per CU.  A payload is processed in
+// 16 KiB windows: lane l holds bytes [256 l, 256 l + 256) of the window.
+constexpr uint32_t kVWaves = 16;
+constexpr uint32_t kWinBytes = 16384;
+// LDS image of the validate kernel (bytes):
+//  [0, 128 KiB)    braid tables T15..T12 (byte followed by 15..12 zero bytes),
+//                  32 copies so lane L always hits bank L % 32: two 64 KiB
+//                  row-sets, entry e row = 256 B, table A at [0,128) and
+//                  table B at [128,256), copy c at 4c
+//  [128, 132 KiB)  slice tables T3..T0 (single copy): word/byte steps
+//  [132, 156 KiB)  shift tables: 6 levels, shift by 256 << k bytes
+constexpr uint32_t kLdsBraidOff = 0;
+constexpr uint32_t kLdsSlice4Off = 131072;
+constexpr uint32_t kLdsShiftOff = kLdsSlice4Off + 4096;
+constexpr uint32_t kShiftLevels = 6;
+constexpr uint32_t kLdsValidateBytes = kLdsShiftOff + kShiftLevels * 4096;
+static_assert(kLdsValidateBytes <= 160u * 1024u, "validate LDS image exceeds 160 KiB");
 
 // Constant tables, built on the host once per context.
 struct Tables {
@@ -79,7 +86,9 @@ struct DeviceJob {
     rpgpu_job_totals* totals;
     uint64_t* bitmap;
     const Tables* tables;
-    uint32_t* counters;           // [0]: rewalks, [1]: overflow bits
+    uint32_t* counters;           // [0] rewalks, [1] overflow bits, [2] decode items, [3] decode cursor
+    uint32_t* decode_list;        // batch_capacity: ordinals of batches to uncompress
+    uint32_t* seg_first_bad;      // n_segments: first chain ordinal failing complete && crc_ok (atomicMin)
 };
 
 // kernel launchers (rp_kernels.hip)
@@ -87,7 +96,11 @@ hipError_t launch_chunk_base(const DeviceJob& j, hipStream_t s);
 hipError_t launch_discover(const DeviceJob& j, hipStream_t s);
 hipError_t launch_resolve(const DeviceJob& j, hipStream_t s);
 hipError_t launch_emit(const DeviceJob& j, hipStream_t s);
-hipError_t launch_validate(const DeviceJob& j, hipStream_t s, uint32_t grid);
+hipError_t launch_validate(const DeviceJob& j, hipStream_t s, uint32_t grid);  // rp_validate.hip
+hipError_t launch_decode(const DeviceJob& j, hipStream_t s, uint32_t grid);    // rp_codec.hip
+// one payload, one wave (rpgpu_uncompress); res[0] = rc (0 / -1 / -2), res[1] = out_len
+hipError_t launch_uncompress_one(int codec, const uint8_t* src, uint64_t n, uint8_t* dst, uint64_t cap,
+                                 int64_t* res, hipStream_t s);
 hipError_t launch_finalize(const DeviceJob& j, hipStream_t s);
 hipError_t scan_exclusive_u64(uint64_t* data, uint64_t n, void* temp, size_t temp_bytes, hipStream_t s);
 // n = min(*d_n, n_cap), read on the device

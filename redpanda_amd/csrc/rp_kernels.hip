@@ -11,11 +11,10 @@
 //
 // Integer/byte work only: HBM-bound, no MFMA.  The CRC runs from LDS tables
 // replicated 32x so every lane reads its own bank (conflict-free ds_read_b32).
-#include "rp_internal.h"
+#include "rp_device.h"
 
 namespace rp {
 
-#define DEV __device__ __forceinline__
 
 // Bounds-checked build (-DRPGPU_CHECKED, librpgpu_checked.so): every data
 // access of k_validate is checked against the allocation and reported with
@@ -30,84 +29,6 @@ namespace rp {
         }                                                                           \
     } while (0)
 #endif
-
-DEV uint32_t lane() { return __lane_id(); }
-
-DEV uint32_t wave_xor(uint32_t v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v ^= __shfl_xor(v, o, 64);
-    return v;
-}
-DEV uint32_t wave_or(uint32_t v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v |= __shfl_xor(v, o, 64);
-    return v;
-}
-DEV uint32_t rl(uint32_t v, int l) { return (uint32_t)__builtin_amdgcn_readlane((int)v, l); }
-// readfirstlane/readlane return int: go through uint32_t so the low half is
-// never sign-extended into the high half (positions >= 2 GiB).
-DEV uint32_t uni32(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); }
-DEV uint64_t uni64(uint64_t v) {
-    return (uint64_t)uni32((uint32_t)v) | ((uint64_t)uni32((uint32_t)(v >> 32)) << 32);
-}
-
-// byte k (0..60) of a header whose bytes are spread one per lane
-DEV uint32_t hb(uint32_t b, int k) { return rl(b, k); }
-DEV uint32_t h32(uint32_t b, int k) { return hb(b, k) | (hb(b, k + 1) << 8) | (hb(b, k + 2) << 16) | (hb(b, k + 3) << 24); }
-DEV uint64_t h64(uint32_t b, int k) { return (uint64_t)h32(b, k) | ((uint64_t)h32(b, k + 4) << 32); }
-DEV uint32_t h16(uint32_t b, int k) { return hb(b, k) | (hb(b, k + 1) << 8); }
-
-// ---------------------------------------------------------------------------
-// Wave-cooperative header read: read_header_impl (storage/parser.cc:139-176).
-// Lane l holds header byte l; internal_header_only_crc (model/record_utils.cc:
-// 34-55) is computed in parallel: byte l at distance 60-l from the end
-// contributes T_{60-l}[b] (raw CRC), the ~0 init contributes c57.
-// ---------------------------------------------------------------------------
-struct Hdr {
-    int32_t status;   // -1 ok, else parser errc
-    int32_t eof;
-    uint32_t hcrc, computed;
-    int32_t size;
-    uint64_t need;    // (uint32_t)(size - 61)
-    uint32_t b;       // this lane's header byte
-};
-
-DEV Hdr wave_header(const uint8_t* __restrict__ seg, uint64_t len, uint64_t p, const Tables* __restrict__ T) {
-    Hdr h;
-    h.eof = 0;
-    h.b = 0;
-    h.hcrc = h.computed = 0;
-    h.size = 0;
-    h.need = 0;
-    const uint64_t rem = len - p;
-    if (rem == 0) { h.status = RPGPU_ERRC_END_OF_STREAM; h.eof = 1; return h; }
-    if (rem < RPGPU_HEADER_SIZE) { h.status = RPGPU_ERRC_INPUT_STREAM_NOT_ENOUGH_BYTES; h.eof = 1; return h; }
-    const uint32_t l = lane();
-    uint32_t b = (l < RPGPU_HEADER_SIZE) ? (uint32_t)seg[p + l] : 0u;
-    uint32_t contrib = (l >= 4 && l < RPGPU_HEADER_SIZE) ? T->hdr[60 - l][b] : 0u;
-    uint32_t raw = wave_xor(contrib);
-    h.b = b;
-    h.computed = ~(T->c57 ^ raw);
-    h.hcrc = h32(b, 0);
-    h.size = (int32_t)h32(b, 4);
-    h.need = (uint32_t)((uint32_t)h.size - RPGPU_HEADER_SIZE);
-    if (h.hcrc == 0) { h.status = RPGPU_ERRC_FALLOCATED_FILE_READ_ZERO_BYTES_FOR_HEADER; return h; }
-    if (h.hcrc != h.computed) { h.status = RPGPU_ERRC_HEADER_ONLY_CRC_MISSMATCH; return h; }
-    h.status = -1;
-    return h;
-}
-
-// 4 bytes at an arbitrary byte address, from the aligned dwords around it.
-// The second dword is only touched when the bytes straddle it, so the read
-// never goes past the last byte asked for.
-DEV uint32_t ldu32(const uint8_t* p) {
-    uintptr_t a = (uintptr_t)p;
-    const uint32_t* q = (const uint32_t*)(a & ~(uintptr_t)3);
-    const uint32_t sh = (uint32_t)(a & 3);
-    uint32_t hi = 0;
-    if (sh) hi = q[1];
-    return __builtin_amdgcn_alignbyte(hi, q[0], sh);
-}
 
 // ---------------------------------------------------------------------------
 // Discovery
@@ -350,114 +271,6 @@ __global__ __launch_bounds__(256) void k_resolve(DeviceJob j) {
 // Emit: walk each chunk again from its resolved entry; write the decoded
 // header (storage/parser.cc:36-76) and plan index slots / decode bytes.
 // ---------------------------------------------------------------------------
-DEV uint32_t xxh32_small(const uint8_t* p, uint32_t n) {
-    // XXH32 for n < 16 (the LZ4F header checksum input is <= 14 bytes)
-    const uint32_t P1 = 0x9E3779B1u, P3 = 0xC2B2AE3Du, P4 = 0x27D4EB2Fu, P5 = 0x165667B1u, P2 = 0x85EBCA77u;
-    uint32_t h = P5 + n;
-    uint32_t i = 0;
-    for (; i + 4 <= n; i += 4) {
-        uint32_t v = (uint32_t)p[i] | ((uint32_t)p[i + 1] << 8) | ((uint32_t)p[i + 2] << 16) | ((uint32_t)p[i + 3] << 24);
-        h += v * P3;
-        h = ((h << 17) | (h >> 15)) * P4;
-    }
-    for (; i < n; i++) { h += p[i] * P5; h = ((h << 11) | (h >> 21)) * P1; }
-    h ^= h >> 15; h *= P2; h ^= h >> 13; h *= P3; h ^= h >> 16;
-    return h;
-}
-
-DEV uint32_t rd32b(const uint8_t* p) { return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24); }
-
-DEV int snappy_varint32_dev(const uint8_t* s, uint64_t n, uint32_t* v) {
-    uint32_t r = 0;
-    for (uint32_t i = 0; i < 5; i++) {
-        if (i >= n) return -1;
-        uint32_t b = s[i];
-        if (i < 4) {
-            r |= (b & 127) << (7 * i);
-            if (b < 128) { *v = r; return (int)i + 1; }
-        } else {
-            r |= (b & 127) << 28;
-            if (b < 16) { *v = r; return 5; }
-            return -1;
-        }
-    }
-    return -1;
-}
-
-// Same rule as the oracle's rpo_decode_capacity (engine plan rule).
-DEV uint64_t decode_capacity_dev(int codec, const uint8_t* s, uint64_t n) {
-    if (n == 0) return 0;
-    if (codec == RPGPU_CODEC_LZ4) {
-        if (n < 7) return 0;
-        uint32_t magic = rd32b(s);
-        if ((magic & 0xFFFFFFF0u) == 0x184D2A50u || magic != 0x184D2204u) return 0;
-        uint32_t flg = s[4];
-        uint64_t hs = 7 + (((flg >> 3) & 1) ? 8 : 0) + ((flg & 1) ? 4 : 0);
-        if (n < hs) return 0;
-        if ((flg >> 1) & 1) return 0;
-        if (((flg >> 6) & 3) != 1) return 0;
-        uint32_t bd = s[5];
-        if ((bd >> 7) & 1) return 0;
-        uint32_t bsid = (bd >> 4) & 7;
-        if (bsid < 4 || (bd & 15)) return 0;
-        if (((xxh32_small(s + 4, (uint32_t)(hs - 5)) >> 8) & 0xFF) != s[hs - 1]) return 0;
-        const uint64_t bmax = bsid == 4 ? (64u << 10) : bsid == 5 ? (256u << 10) : bsid == 6 ? (1u << 20) : (4u << 20);
-        const uint32_t bcs = (flg >> 4) & 1;
-        uint64_t cap = 0, pos = hs;
-        while (n - pos >= 4) {
-            uint32_t bh = rd32b(s + pos);
-            if (bh == 0) break;
-            uint64_t bsz = bh & 0x7FFFFFFFu;
-            if (bsz > bmax) break;
-            cap += (bh & 0x80000000u) ? bsz : bmax;
-            pos += 4;
-            uint64_t adv = bsz + (bcs ? 4 : 0);
-            if (n - pos < adv) break;
-            pos += adv;
-        }
-        return cap;
-    }
-    if (codec == RPGPU_CODEC_SNAPPY) {
-        static const uint8_t magic[8] = {0x82, 'S', 'N', 'A', 'P', 'P', 'Y', 0};
-        bool java = n >= 16;
-        for (int i = 0; i < 8 && java; i++) java = s[i] == magic[i];
-        uint32_t ulen;
-        if (!java) {
-            if (snappy_varint32_dev(s, n, &ulen) < 0) return 0;
-            return ((uint64_t)ulen <= 22ull * n + 64) ? ulen : 0;
-        }
-        uint64_t cap = 0, pos = 16;
-        while (n - pos >= 4) {
-            int32_t clen = (int32_t)(((uint32_t)s[pos] << 24) | ((uint32_t)s[pos + 1] << 16) |
-                                     ((uint32_t)s[pos + 2] << 8) | s[pos + 3]);
-            if (clen <= 0 || n - pos - 4 < (uint64_t)clen) break;
-            if (snappy_varint32_dev(s + pos + 4, (uint64_t)clen, &ulen) < 0) break;
-            if ((uint64_t)ulen > 22ull * (uint64_t)clen + 64) break;
-            cap += ulen;
-            pos += 4 + (uint64_t)clen;
-        }
-        return cap;
-    }
-    return 0;
-}
-
-// BE40 prefix position of disk header byte l (21..60): fields are reversed
-// byte-wise (model/record_utils.cc:68-80).
-DEV int be_index(uint32_t l) {
-    // field starts on disk and lengths: attrs 21/2, lod 23/4, first_ts 27/8,
-    // max_ts 35/8, pid 43/8, epoch 51/2, base_seq 53/4, record_count 57/4
-    int fs, fl;
-    if (l < 23) { fs = 21; fl = 2; }
-    else if (l < 27) { fs = 23; fl = 4; }
-    else if (l < 35) { fs = 27; fl = 8; }
-    else if (l < 43) { fs = 35; fl = 8; }
-    else if (l < 51) { fs = 43; fl = 8; }
-    else if (l < 53) { fs = 51; fl = 2; }
-    else if (l < 57) { fs = 53; fl = 4; }
-    else { fs = 57; fl = 4; }
-    return (fs - 21) + (fl - 1 - ((int)l - fs));
-}
-
 __global__ __launch_bounds__(256) void k_emit(DeviceJob j) {
     const uint64_t g = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
     if (g >= j.total_chunks) return;
@@ -521,7 +334,9 @@ __global__ __launch_bounds__(256) void k_emit(DeviceJob j) {
             if (complete && (codec == RPGPU_CODEC_GZIP || codec == RPGPU_CODEC_ZSTD)) f |= RPGPU_F_CODEC_UNSUPPORTED;
             r.flags = f;
             r.segment = s;
-            r.index_base = 0;
+            // scratch for k_validate: absolute payload start (overwritten with
+            // the record-index base there)
+            r.index_base = off + p + RPGPU_HEADER_SIZE;
             r.decoded_off = 0;
             r.records_parsed = 0;
             r.decoded_len = (complete && codec == 0) ? (uint32_t)h.need : 0;
@@ -537,6 +352,9 @@ __global__ __launch_bounds__(256) void k_emit(DeviceJob j) {
             j.batches[ord] = r;
             j.slots[ord] = slots;
             j.dcap[ord] = cap;
+            // decode work list for k_decode (order is irrelevant: every item
+            // writes only its own batch and its own reserved arena slot)
+            if (complete && decodable) j.decode_list[atomicAdd(&j.counters[2], 1u)] = (uint32_t)ord;
         }
         if (!complete) break;
         p += RPGPU_HEADER_SIZE + h.need;
@@ -614,437 +432,51 @@ __global__ __launch_bounds__(256) void k_scan_add(uint64_t* data, const uint64_t
 }
 
 // ---------------------------------------------------------------------------
-// Validate: CRC32C over BE40 prefix ++ payload, record walk.
-// ---------------------------------------------------------------------------
-
-// LDS address of T_k[e] in the replicated image:
-//   row-set rs (64 KiB) holds two tables, A at bytes [0,128) of each 256-byte
-//   row and B at [128,256); copy c of entry e sits at e*256 + slot*128 + 4c,
-//   i.e. bank c: lane L reads copy L%32 and never conflicts.
-// v_perm_b32 assembles {key.b0, x.b_j, key.b2, 0} = address in one op.
-constexpr uint32_t kSel0 = 0x0C020400u;  // x byte 0
-constexpr uint32_t kSel1 = 0x0C020500u;  // x byte 1
-constexpr uint32_t kSel2 = 0x0C020600u;  // x byte 2
-constexpr uint32_t kSel3 = 0x0C020700u;  // x byte 3
-
-struct Keys {
-    uint32_t k3, k2, k1, k0;  // keys of T3, T2, T1, T0
-};
-
-DEV uint32_t lds32(const uint8_t* lds, uint32_t addr) { return *(const uint32_t*)(lds + addr); }
-
-DEV uint32_t step4(const uint8_t* lds, const Keys& K, uint32_t s, uint32_t w) {
-    const uint32_t x = s ^ w;
-    const uint32_t a = lds32(lds, __builtin_amdgcn_perm(x, K.k3, kSel0));
-    const uint32_t b = lds32(lds, __builtin_amdgcn_perm(x, K.k2, kSel1));
-    const uint32_t c = lds32(lds, __builtin_amdgcn_perm(x, K.k1, kSel2));
-    const uint32_t d = lds32(lds, __builtin_amdgcn_perm(x, K.k0, kSel3));
-    return (a ^ b) ^ (c ^ d);
-}
-
-DEV uint32_t step1(const uint8_t* lds, const Keys& K, uint32_t s, uint32_t byte) {
-    return lds32(lds, __builtin_amdgcn_perm(s ^ byte, K.k0, kSel0)) ^ (s >> 8);
-}
-
-// shift a raw CRC state forward over kStream*2^lvl zero bytes
-DEV uint32_t shift_lvl(const uint8_t* lds, uint32_t s, uint32_t lvl) {
-    const uint32_t* t = (const uint32_t*)(lds + kLdsCombineOff) + lvl * 1024;
-    return t[s & 0xFF] ^ t[256 + ((s >> 8) & 0xFF)] ^ t[512 + ((s >> 16) & 0xFF)] ^ t[768 + (s >> 24)];
-}
-
-
-// 16 bytes at an arbitrary address, zero past `lim` (exclusive, absolute).
-DEV void load16u(const uint8_t* p, const uint8_t* lim, uint32_t& r0, uint32_t& r1, uint32_t& r2, uint32_t& r3) {
-    const uintptr_t a = (uintptr_t)p;
-    const uint32_t* q = (const uint32_t*)(a & ~(uintptr_t)3);
-    const uint32_t sh = (uint32_t)(a & 3);
-    const uintptr_t L = (uintptr_t)lim;
-    uint32_t d0 = ((uintptr_t)(q + 0) < L) ? q[0] : 0;
-    uint32_t d1 = ((uintptr_t)(q + 1) < L) ? q[1] : 0;
-    uint32_t d2 = ((uintptr_t)(q + 2) < L) ? q[2] : 0;
-    uint32_t d3 = ((uintptr_t)(q + 3) < L) ? q[3] : 0;
-    uint32_t d4 = ((uintptr_t)(q + 4) < L) ? q[4] : 0;
-    r0 = __builtin_amdgcn_alignbyte(d1, d0, sh);
-    r1 = __builtin_amdgcn_alignbyte(d2, d1, sh);
-    r2 = __builtin_amdgcn_alignbyte(d3, d2, sh);
-    r3 = __builtin_amdgcn_alignbyte(d4, d3, sh);
-}
-
-// vint::deserialize (utils/vint.h:82-98) over at most `avail` bytes.
-DEV int64_t varint16(uint32_t r0, uint32_t r1, uint32_t r2, uint32_t r3, uint64_t avail, uint32_t& br) {
-    const uint64_t lo = (uint64_t)r0 | ((uint64_t)r1 << 32);
-    const uint64_t hi = (uint64_t)r2 | ((uint64_t)r3 << 32);
-    uint64_t res = 0;
-    uint32_t n = 0;
-    const uint32_t lim = avail < 10 ? (uint32_t)avail : 10u;
-    for (uint32_t i = 0; i < lim; i++) {
-        const uint64_t byte = (i < 8 ? (lo >> (8 * i)) : (hi >> (8 * (i - 8)))) & 0xFF;
-        n++;
-        res |= (byte & 127) << (7 * i);
-        if (!(byte & 128)) break;
-    }
-    br = n;
-    return (int64_t)((res >> 1) ^ (~(res & 1) + 1));
-}
-
-struct Reader {
-    const uint8_t* base;  // payload start
-    const uint8_t* lim;   // payload end (absolute)
-    uint64_t n;
-    uint64_t pos;
-};
-
-DEV int64_t rd_varlong(Reader& c) {
-    uint32_t r0, r1, r2, r3, br;
-    load16u(c.base + c.pos, c.lim, r0, r1, r2, r3);
-    int64_t v = varint16(r0, r1, r2, r3, c.n - c.pos, br);
-    c.pos += br;
-    return v;
-}
-
-// iobuf_copy (bytes/iobuf.cc:133-157): -1 when (int)len < 0 (bad_alloc)
-DEV int copy_bytes(Reader& c, int64_t len) {
-    const int32_t bl = (int32_t)(uint32_t)(uint64_t)len;
-    if (bl < 0) return -1;
-    const uint64_t left = c.n - c.pos;
-    c.pos += ((uint64_t)bl < left) ? (uint64_t)bl : left;
-    return 0;
-}
-
-struct Rec {
-    uint32_t err;   // rpgpu_parse_err
-    uint64_t end;
-    int64_t ts;
-    int32_t length, off, klen, vlen, hcount;
-    uint32_t key_pos, val_pos, hdr_pos;
-    int32_t attr;
-};
-
-// parse_one_record_copy_from_buffer (model/record_utils.cc:170-177)
-DEV Rec parse_record(const uint8_t* base, const uint8_t* lim, uint64_t n, uint64_t start) {
-    Rec r;
-    Reader c{base, lim, n, start};
-    r.err = 0;
-    r.key_pos = r.val_pos = r.hdr_pos = 0;
-    r.ts = 0; r.length = r.off = r.klen = r.vlen = r.hcount = 0; r.attr = 0;
-    const int64_t rsz = rd_varlong(c);
-    if (c.pos >= n) { r.err = RPGPU_PARSE_ERR_ATTR_EOF; r.end = c.pos; return r; }
-    r.attr = (int8_t)base[c.pos];
-    c.pos++;
-    r.ts = rd_varlong(c);
-    const int64_t off = rd_varlong(c);
-    const int64_t kl = rd_varlong(c);
-    r.key_pos = (uint32_t)c.pos;
-    if (kl > 0 && copy_bytes(c, kl)) { r.err = RPGPU_PARSE_ERR_COPY_NEGATIVE; r.end = c.pos; return r; }
-    const int64_t vl = rd_varlong(c);
-    r.val_pos = (uint32_t)c.pos;
-    if (vl > 0 && copy_bytes(c, vl)) { r.err = RPGPU_PARSE_ERR_COPY_NEGATIVE; r.end = c.pos; return r; }
-    const int64_t hc = rd_varlong(c);
-    r.hdr_pos = (uint32_t)c.pos;
-    if (hc < 0 || hc > RPGPU_MAX_HEADER_RESERVE) { r.err = RPGPU_PARSE_ERR_HEADER_RESERVE; r.end = c.pos; return r; }
-    for (int64_t h = 0; h < hc; h++) {
-        if (c.pos >= n) break;
-        const int64_t hk = rd_varlong(c);
-        if (hk > 0 && copy_bytes(c, hk)) { r.err = RPGPU_PARSE_ERR_COPY_NEGATIVE; r.end = c.pos; return r; }
-        const int64_t hv = rd_varlong(c);
-        if (hv > 0 && copy_bytes(c, hv)) { r.err = RPGPU_PARSE_ERR_COPY_NEGATIVE; r.end = c.pos; return r; }
-    }
-    r.length = (int32_t)rsz;
-    r.off = (int32_t)off;
-    r.klen = (int32_t)kl;
-    r.vlen = (int32_t)vl;
-    r.hcount = (int32_t)hc;
-    r.end = c.pos;
-    return r;
-}
-
-struct WalkResult {
-    uint32_t parsed;
-    uint32_t err;
-    uint64_t trailing;
-};
-
-// record_batch::for_each_record (model/record.h:616-627) with speculative
-// lane-parallel records: a scalar chain over the length varints guesses where
-// records start, lanes parse one record each, and only the prefix whose
-// starts are confirmed by the previous record's exact end is committed.
-DEV WalkResult walk_records(const uint8_t* base, uint64_t n, int32_t rc, uint32_t batch_ord,
-                            rpgpu_record_index* out, uint64_t out_cap) {
-    WalkResult wr;
-    wr.parsed = 0;
-    wr.err = 0;
-    wr.trailing = 0;
-    const uint32_t l = lane();
-    const uint8_t* lim = base + n;
-    uint64_t start = 0;
-    uint32_t done = 0;
-    while (done < (uint32_t)(rc > 0 ? rc : 0)) {
-        const uint32_t want = ((uint32_t)rc - done) < 64u ? ((uint32_t)rc - done) : 64u;
-        // speculative starts (uniform chain on the length varint)
-        uint64_t my_start = kNone;
-        uint64_t p = start;
-        uint32_t m = 0;
-        for (; m < want; m++) {
-            if (l == m) my_start = p;
-            if (p >= n) { m++; break; }
-            uint32_t r0, r1, r2, r3, br;
-            load16u(base + p, lim, r0, r1, r2, r3);
-            r0 = uni32(r0); r1 = uni32(r1); r2 = uni32(r2); r3 = uni32(r3);
-            const int64_t len = varint16(r0, r1, r2, r3, n - p, br);
-            if (len < 0 || (uint64_t)len > n) { m++; break; }
-            p = p + br + (uint64_t)len;
-        }
-        // each lane parses its record exactly
-        Rec r;
-        const bool act = l < m;
-        if (act) r = parse_record(base, lim, n, my_start);
-        else { r.err = 0; r.end = kNone; }
-        const uint64_t prev_end = __shfl_up(r.end, 1, 64);
-        const uint32_t prev_err = __shfl_up(r.err, 1, 64);
-        const bool match = (l == 0) || (prev_err == 0 && prev_end == my_start);
-        const uint64_t bad = __ballot(act && !match);
-        const uint32_t exact = bad ? (uint32_t)__builtin_ctzll(bad) : m;  // lanes [0, exact) are exact
-        const uint64_t errs = __ballot(act && l < exact && r.err != 0);
-        const uint32_t nok = errs ? (uint32_t)__builtin_ctzll(errs) : exact;  // records parsed OK
-        if (l < nok && done + l < out_cap) {
-#ifdef RPGPU_CHECKED
-            if (my_start >= n) printf("RPGPU_CHECK walk start %llu n %llu\n", (unsigned long long)my_start, (unsigned long long)n);
-#endif
-            rpgpu_record_index e;
-            e.batch = batch_ord;
-            e.rec_pos = (uint32_t)my_start;
-            e.ts_delta = r.ts;
-            e.length = r.length;
-            e.offset_delta = r.off;
-            e.key_len = r.klen;
-            e.key_pos = r.key_pos;
-            e.val_len = r.vlen;
-            e.val_pos = r.val_pos;
-            e.hdr_count = r.hcount;
-            e.hdr_pos = r.hdr_pos;
-            e.end_pos = (uint32_t)r.end;
-            e.attrs = (int8_t)r.attr;
-            e.pad[0] = e.pad[1] = e.pad[2] = 0;
-            e.reserved[0] = e.reserved[1] = 0;
-            out[done + l] = e;
-        }
-        if (errs) {
-            wr.parsed = done + nok;
-            wr.err = uni32(__shfl(r.err, nok, 64));
-            return wr;
-        }
-        start = uni64(__shfl(r.end, exact - 1, 64));
-        done += exact;
-    }
-    wr.parsed = done;
-    wr.trailing = n - start;
-    return wr;
-}
-
-__global__ __launch_bounds__(1024) void k_validate(DeviceJob j) {
-    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-    const Tables* T = j.tables;
-    // replicated slice tables: word i -> rs = i>>14, e = (i>>6)&255, slot = (i>>5)&1, copy = i&31
-    for (uint32_t i = threadIdx.x; i < kLdsSliceBytes / 4; i += blockDim.x) {
-        const uint32_t rs = i >> 14, e = (i >> 6) & 255, slot = (i >> 5) & 1;
-        const uint32_t k = 3 - (rs * 2 + slot);  // A0 = T3, B0 = T2, A1 = T1, B1 = T0
-        ((uint32_t*)lds)[i] = T->slice[k][e];
-    }
-    for (uint32_t i = threadIdx.x; i < kLdsCombineBytes / 4; i += blockDim.x)
-        ((uint32_t*)(lds + kLdsCombineOff))[i] = ((const uint32_t*)T->comb)[i];
-    __syncthreads();
-
-    const uint32_t l = lane();
-    const uint32_t bank = (l & 31) * 4;
-    Keys K;
-    K.k3 = (0u << 16) | (0u + bank);
-    K.k2 = (0u << 16) | (128u + bank);
-    K.k1 = (1u << 16) | (0u + bank);
-    K.k0 = (1u << 16) | (128u + bank);
-
-    const uint64_t nb_total = j.chunk_count[j.total_chunks];
-    const uint64_t nb = nb_total < j.batch_capacity ? nb_total : j.batch_capacity;
-    const uint32_t waves_per_block = blockDim.x >> 6;
-    const uint64_t nwaves = (uint64_t)gridDim.x * waves_per_block;
-    const uint64_t gw = (uint64_t)blockIdx.x * waves_per_block + (threadIdx.x >> 6);
-
-    for (uint64_t b = gw; b < nb; b += nwaves) {
-        rpgpu_batch_result* R = &j.batches[b];
-        const uint32_t flags0 = uni32(R->flags);
-        if (!(flags0 & RPGPU_F_COMPLETE)) {
-            if (l == 0) { R->index_base = j.slots[b]; R->decoded_off = j.dcap[b]; R->reserved1 = 0; }
-            continue;
-        }
-        const uint32_t segi = uni32(R->segment);
-        const uint64_t seg_base = uni64(j.seg_off[segi]);
-        const uint64_t S = seg_base + uni64(R->file_pos) + RPGPU_HEADER_SIZE;
-        const uint64_t n = uni32((uint32_t)(R->size_bytes - (int32_t)RPGPU_HEADER_SIZE));
-        const uint64_t E = S + n;
-        const uint8_t* data = j.data;
-#ifdef RPGPU_CHECKED
-        {
-            bool bad = false;
-            RP_CHECK(bad, segi < j.n_segments, "b=%llu segi=%u flags=%u", (unsigned long long)b, segi, flags0);
-            if (bad) continue;
-            const uint64_t slen = j.seg_off[segi + 1] - j.seg_off[segi];
-            RP_CHECK(bad, segi < j.n_segments && uni64(R->file_pos) + RPGPU_HEADER_SIZE + n <= slen && E <= j.data_len,
-                     "b=%llu seg=%u file_pos=%llu n=%llu slen=%llu E=%llu data_len=%llu", (unsigned long long)b, segi,
-                     (unsigned long long)R->file_pos, (unsigned long long)n, (unsigned long long)slen,
-                     (unsigned long long)E, (unsigned long long)j.data_len);
-            const uint64_t ib0 = j.slots[b], ib1 = j.slots[b + 1];
-            RP_CHECK(bad, ib0 <= ib1 && ib1 <= j.slots[nb], "b=%llu slots %llu %llu total %llu", (unsigned long long)b,
-                     (unsigned long long)ib0, (unsigned long long)ib1, (unsigned long long)j.slots[nb]);
-            if (bad) continue;
-        }
-#endif
-        // CRC state after the BE40 prefix with init ~0: c40 ^ raw contribution
-        // of the prefix bytes (computed by k_emit, parked in reserved1)
-        uint32_t Tst = uni32((uint32_t)R->reserved1) ^ T->c40;
-
-        // Lane regions are anchored at E16 = E rounded down to 16 bytes so
-        // every vector load is an aligned 16-byte load; chunk c spans
-        // [E16 - kStream*(Ntot-c), +kStream), chunk 0 is clipped at S, and
-        // the <16-byte tail [E16, E) is folded in after the rounds.
-        const uint64_t E16 = (E & ~(uint64_t)15) > S ? (E & ~(uint64_t)15) : S;
-        const uint64_t n16 = E16 - S;
-        if (n16 > 0) {
-            const uint64_t Ntot = (n16 + kStream - 1) / kStream;
-            const uint64_t R_ = (Ntot + 127) / 128;
-            for (uint64_t r = 0; r < R_; r++) {
-                const int64_t c0 = (int64_t)Ntot - (int64_t)(128 * (R_ - r));
-                const int64_t ca = c0 + 2 * (int64_t)l;
-                // lane region start (bytes), may lie before S in round 0
-                const int64_t a = (int64_t)E16 - (int64_t)kStream * ((int64_t)Ntot - ca);
-                uint32_t sA = 0, sB = 0;
-                if (r == 0) {
-                    // the lane holding chunk 0 starts from the prefix state
-                    if (ca == 0) sA = Tst;
-                    else if (ca + 1 == 0) sB = Tst;
-                } else if (l == 0) {
-                    sA = Tst;
-                }
-                if (a >= (int64_t)S) {
-                    // full 256-byte region, 16-byte aligned
-#ifdef RPGPU_CHECKED
-                    if (!(a + 256 <= (int64_t)E16 && (a & 15) == 0))
-                        printf("RPGPU_CHECK region b=%llu a=%lld E16=%llu S=%llu\n", (unsigned long long)b, (long long)a,
-                               (unsigned long long)E16, (unsigned long long)S);
-#endif
-                    const uint4* q = (const uint4*)(data + a);
-                    uint4 v[16];
-#pragma unroll
-                    for (int k = 0; k < 16; k++) v[k] = q[k];
-#pragma unroll
-                    for (int k = 0; k < 8; k++) {
-                        sA = step4(lds, K, sA, v[k].x);
-                        sB = step4(lds, K, sB, v[k + 8].x);
-                        sA = step4(lds, K, sA, v[k].y);
-                        sB = step4(lds, K, sB, v[k + 8].y);
-                        sA = step4(lds, K, sA, v[k].z);
-                        sB = step4(lds, K, sB, v[k + 8].z);
-                        sA = step4(lds, K, sA, v[k].w);
-                        sB = step4(lds, K, sB, v[k + 8].w);
-                    }
-                } else if (a + (int64_t)kLaneBytes > (int64_t)S) {
-                    // region straddles the payload start (round 0 only): bytes
-                    // before S are skipped; stream A covers [a, a+128)
-                    for (int st = 0; st < 2; st++) {
-                        const int64_t sa = a + st * (int64_t)kStream;
-                        const int64_t se = sa + (int64_t)kStream;
-                        if (se <= (int64_t)S) continue;
-                        uint32_t sv = st ? sB : sA;
-                        int64_t x = sa > (int64_t)S ? sa : (int64_t)S;
-                        for (; ((se - x) & 3) != 0; x++) sv = step1(lds, K, sv, data[x]);
-                        for (; x < se; x += 4) sv = step4(lds, K, sv, ldu32(data + x));
-                        if (st) sB = sv; else sA = sv;
-                    }
-                }
-                // combine: s = shift(sA, kStream) ^ sB, then a tree over lanes
-                uint32_t sv = shift_lvl(lds, sA, 0) ^ sB;
-#pragma unroll
-                for (uint32_t lv = 1; lv < kCombineLevels; lv++) {
-                    const uint32_t d = 1u << (lv - 1);
-                    const uint32_t other = __shfl_down(sv, d, 64);
-                    sv = shift_lvl(lds, sv, lv) ^ other;
-                }
-                Tst = uni32(sv);  // lane 0 holds the state after this round
-            }
-        }
-        // tail bytes [E16, E): fewer than 16, uniform
-        for (uint64_t x = E16; x < E; x++) Tst = uni32(step1(lds, K, Tst, data[x]));
-        const uint32_t crc = ~Tst;
-        uint32_t f = flags0;
-        if (crc == uni32(R->crc)) f |= RPGPU_F_CRC_OK;
-
-        // plan results
-        const uint64_t ib = j.slots[b];
-        const uint64_t islots = j.slots[b + 1] - ib;
-        const uint32_t codec = (uint32_t)(uint16_t)R->attrs & 7;
-        uint32_t parsed = 0, perr = 0;
-        if (codec == 0 && (j.flags & RPGPU_JOB_PARSE)) {
-            const bool idx_ok = ib + islots <= j.record_capacity;
-            WalkResult w = walk_records(data + S, n, R->record_count, (uint32_t)b,
-                                        idx_ok ? j.records + ib : nullptr, idx_ok ? islots : 0);
-            parsed = w.parsed;
-            perr = w.err;
-            f |= RPGPU_F_PARSED;
-            if (perr == 0) {
-                f |= RPGPU_F_PARSE_ASYNC_OK;
-                if (w.trailing == 0) f |= RPGPU_F_PARSE_OK;
-                else perr = RPGPU_PARSE_ERR_TRAILING;
-            }
-            if (f & RPGPU_F_PARSE_OK) {
-                if (idx_ok) f |= RPGPU_F_INDEX_WRITTEN;
-                else { perr = RPGPU_PARSE_ERR_INDEX_CAPACITY; if (l == 0) atomicOr(&j.counters[1], 2u); }
-            }
-        }
-        if (l == 0) {
-            R->crc_computed = crc;
-            R->flags = f;
-            R->index_base = ib;
-            R->decoded_off = j.dcap[b];
-            R->records_parsed = parsed;
-            R->parse_err = (uint8_t)perr;
-            R->reserved1 = 0;
-        }
-    }
-}
-
-// ---------------------------------------------------------------------------
-// Finalize: per-segment checkpoint (storage/log_replayer.cc:62-79), bytes
-// consumed (storage/parser.cc:183-254), bitmap and totals.
+// Finalize: per-segment checkpoint (storage/log_replayer.cc:62-79) and bytes
+// consumed (storage/parser.cc:183-254).  The first batch failing
+// complete && crc_ok was recorded by k_validate with atomicMin; positions
+// accumulate size_bytes (storage/parser.cc:118-128), so the sums are the end
+// position of one batch — except in segments >= 4 GiB, where a header with
+// size_bytes < 61 can still chain (need wraps as uint32) and the sums are
+// taken explicitly.
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void k_finalize_segments(DeviceJob j) {
     const uint32_t s = blockIdx.x;
     const uint32_t tid = threadIdx.x;
-    const uint64_t nb_total = j.chunk_count[j.total_chunks];
     const uint64_t first = j.chunk_count[j.chunk_base[s]];
     const uint64_t last = j.chunk_count[j.chunk_base[s + 1]];
     const uint64_t cnt = last - first;
-    __shared__ uint64_t s_bad;
-    __shared__ uint64_t s_bytes, s_phys, s_rec;
-    if (tid == 0) { s_bad = cnt; s_bytes = 0; s_phys = 0; s_rec = 0; }
-    __syncthreads();
     const bool fits = last <= j.batch_capacity;
-    if (fits) {
-        for (uint64_t i = tid; i < cnt; i += 256) {
-            const uint32_t f = j.batches[first + i].flags;
-            if (!((f & RPGPU_F_COMPLETE) && (f & RPGPU_F_CRC_OK))) atomicMin((unsigned long long*)&s_bad, (unsigned long long)i);
-        }
-    }
-    __syncthreads();
-    const uint64_t bad = s_bad;
+    const uint64_t fb = j.seg_first_bad[s];
+    const uint64_t bad = (fits && fb < cnt) ? fb : cnt;
     const uint64_t upto = bad < cnt ? bad + 1 : cnt;
-    uint64_t bytes = 0, phys = 0;
+    const uint64_t seg_len = j.seg_off[s + 1] - j.seg_off[s];
+    __shared__ unsigned long long s_bytes, s_phys;
+    if (tid == 0) { s_bytes = 0; s_phys = 0; }
+    __syncthreads();
     if (fits) {
-        for (uint64_t i = tid; i < cnt; i += 256) {
-            const uint64_t sz = (uint64_t)(int64_t)j.batches[first + i].size_bytes;
-            if (i < upto) bytes += sz;
-            if (i < bad) phys += sz;
+        if (seg_len < (1ull << 32)) {
+            if (tid == 0) {
+                if (upto > 0) {
+                    const rpgpu_batch_result& g = j.batches[first + upto - 1];
+                    s_bytes = g.file_pos + (uint64_t)(int64_t)g.size_bytes;
+                }
+                if (bad > 0) {
+                    const rpgpu_batch_result& g = j.batches[first + bad - 1];
+                    s_phys = g.file_pos + (uint64_t)(int64_t)g.size_bytes;
+                }
+            }
+        } else {
+            uint64_t bytes = 0, phys = 0;
+            for (uint64_t i = tid; i < upto; i += 256) {
+                const uint64_t sz = (uint64_t)(int64_t)j.batches[first + i].size_bytes;
+                bytes += sz;
+                if (i < bad) phys += sz;
+            }
+            atomicAdd(&s_bytes, (unsigned long long)bytes);
+            atomicAdd(&s_phys, (unsigned long long)phys);
         }
     }
-    atomicAdd((unsigned long long*)&s_bytes, (unsigned long long)bytes);
-    atomicAdd((unsigned long long*)&s_phys, (unsigned long long)phys);
     __syncthreads();
     if (tid == 0) {
         rpgpu_segment_summary sm;
@@ -1070,7 +502,6 @@ __global__ __launch_bounds__(256) void k_finalize_segments(DeviceJob j) {
         sm.n_records = j.slots[sl] - j.slots[sf];
         sm.reserved[0] = sm.reserved[1] = 0;
         j.summaries[s] = sm;
-        (void)nb_total;
     }
 }
 
@@ -1168,15 +599,6 @@ hipError_t launch_resolve(const DeviceJob& j, hipStream_t s) {
 hipError_t launch_emit(const DeviceJob& j, hipStream_t s) {
     const uint32_t grid = (j.total_chunks + 3) / 4;
     hipLaunchKernelGGL(k_emit, dim3(grid), dim3(256), 0, s, j);
-    return hipGetLastError();
-}
-hipError_t launch_validate(const DeviceJob& j, hipStream_t s, uint32_t grid) {
-    static bool attr = false;
-    if (!attr) {
-        hipFuncSetAttribute((const void*)k_validate, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsValidateBytes);
-        attr = true;
-    }
-    hipLaunchKernelGGL(k_validate, dim3(grid), dim3(1024), kLdsValidateBytes, s, j);
     return hipGetLastError();
 }
 hipError_t launch_finalize(const DeviceJob& j, hipStream_t s) {

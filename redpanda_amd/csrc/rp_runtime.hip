@@ -16,7 +16,7 @@
 #include <thread>
 #include <vector>
 
-#include "rp_internal.h"
+#include "rp_device.h"
 
 namespace rp {
 
@@ -87,8 +87,11 @@ struct rpgpu_ctx {
     size_t pin_bytes = 0;
     bool timing = false;
     // one event set per timed submit: start, discover done, plan done,
-    // validate done, end; resolved lazily by rpgpu_last_timings
-    std::vector<std::array<hipEvent_t, 5>> ev_sets;
+    // decode done, validate done, end; resolved lazily by rpgpu_last_timings
+    std::vector<std::array<hipEvent_t, 6>> ev_sets;
+    // rpgpu_uncompress staging (device)
+    void* uws = nullptr;
+    size_t uws_bytes = 0;
     size_t ev_used = 0;
     uint32_t cu_count = 256;
     std::string err;
@@ -152,6 +155,7 @@ int rpgpu_destroy(rpgpu_ctx* c) {
     hipSetDevice(c->device);
     if (c->stream) hipStreamSynchronize(c->stream);
     if (c->ws) hipFree(c->ws);
+    if (c->uws) hipFree(c->uws);
     if (c->pin) hipHostFree(c->pin);
     if (c->d_tables) hipFree(c->d_tables);
     for (auto& set : c->ev_sets)
@@ -228,20 +232,23 @@ int rpgpu_set_timing(rpgpu_ctx* c, int enable) {
 }
 
 // Averages over every timed submit since the previous call (then resets).
+// ms[0] whole pipeline, [1] discover, [2] resolve+emit+plan, [3] validate,
+// [4] decode.
 int rpgpu_last_timings(rpgpu_ctx* c, float* ms, int n) {
     if (!c || !ms) return RPGPU_E_INVALID;
     if (c->ev_used == 0) return fail(c, RPGPU_E_INVALID, "rpgpu_last_timings: no timed submit");
-    double acc[4] = {0, 0, 0, 0};
+    double acc[5] = {0, 0, 0, 0, 0};
     for (size_t i = 0; i < c->ev_used; i++) {
         auto& e = c->ev_sets[i];
-        HIPCHK(c, hipEventSynchronize(e[4]));
+        HIPCHK(c, hipEventSynchronize(e[5]));
         float t;
-        hipEventElapsedTime(&t, e[0], e[4]); acc[0] += t;
+        hipEventElapsedTime(&t, e[0], e[5]); acc[0] += t;
         hipEventElapsedTime(&t, e[0], e[1]); acc[1] += t;
         hipEventElapsedTime(&t, e[1], e[2]); acc[2] += t;
-        hipEventElapsedTime(&t, e[2], e[3]); acc[3] += t;
+        hipEventElapsedTime(&t, e[3], e[4]); acc[3] += t;
+        hipEventElapsedTime(&t, e[2], e[3]); acc[4] += t;
     }
-    for (int i = 0; i < n && i < 4; i++) ms[i] = (float)(acc[i] / (double)c->ev_used);
+    for (int i = 0; i < n && i < 5; i++) ms[i] = (float)(acc[i] / (double)c->ev_used);
     c->ev_used = 0;
     return RPGPU_OK;
 }
@@ -280,7 +287,9 @@ int rpgpu_submit(rpgpu_ctx* c, const rpgpu_job* job, void* stream) {
     const size_t o_segterm = take(nseg * sizeof(SegTerm));
     const size_t o_slots = take((bcap + 1) * 8);
     const size_t o_dcap = take((bcap + 1) * 8);
-    const size_t o_counters = take(16);
+    const size_t o_counters = take(32);
+    const size_t o_dlist = take((bcap + 1) * 4);
+    const size_t o_fbad = take((size_t)nseg * 4);
     const size_t o_scan = take(scan_temp_bytes(std::max<uint64_t>(tc, bcap)) + 64);
     const size_t need = off;
     if (need > c->ws_bytes) {
@@ -316,6 +325,9 @@ int rpgpu_submit(rpgpu_ctx* c, const rpgpu_job* job, void* stream) {
     j.bitmap = job->d_valid_bitmap;
     j.tables = c->d_tables;
     j.counters = (uint32_t*)(ws + o_counters);
+    j.decode_list = (uint32_t*)(ws + o_dlist);
+    j.seg_first_bad = (uint32_t*)(ws + o_fbad);
+    if (((uintptr_t)job->d_decoded & 15) != 0) return fail(c, RPGPU_E_INVALID, "rpgpu_submit: d_decoded must be 16-byte aligned");
     uint64_t* scan_tmp = (uint64_t*)(ws + o_scan);
 
     // RPGPU_DEBUG_SYNC=1: synchronize after every stage and name the stage
@@ -333,7 +345,7 @@ int rpgpu_submit(rpgpu_ctx* c, const rpgpu_job* job, void* stream) {
     hipEvent_t* ev = nullptr;
     if (tm) {
         if (c->ev_used == c->ev_sets.size()) {
-            std::array<hipEvent_t, 5> set;
+            std::array<hipEvent_t, 6> set;
             for (auto& e : set) HIPCHK(c, hipEventCreate(&e));
             c->ev_sets.push_back(set);
         }
@@ -341,7 +353,8 @@ int rpgpu_submit(rpgpu_ctx* c, const rpgpu_job* job, void* stream) {
         HIPCHK(c, hipEventRecord(ev[0], s));
     }
     STAGE("chunk_base", launch_chunk_base(j, s));
-    HIPCHK(c, hipMemsetAsync(j.counters, 0, 16, s));
+    HIPCHK(c, hipMemsetAsync(j.counters, 0, 32, s));
+    HIPCHK(c, hipMemsetAsync(j.seg_first_bad, 0xFF, (size_t)nseg * 4, s));
     STAGE("discover", launch_discover(j, s));
     if (tm) HIPCHK(c, hipEventRecord(ev[1], s));
     STAGE("resolve", launch_resolve(j, s));
@@ -351,10 +364,13 @@ int rpgpu_submit(rpgpu_ctx* c, const rpgpu_job* job, void* stream) {
     STAGE("scan_slots", scan_exclusive_u64_devn(j.slots, d_nb, bcap, scan_tmp, s));
     STAGE("scan_dcap", scan_exclusive_u64_devn(j.dcap, d_nb, bcap, scan_tmp, s));
     if (tm) HIPCHK(c, hipEventRecord(ev[2], s));
-    STAGE("validate", launch_validate(j, s, c->cu_count));
+    // decode first: k_validate checksums and walks the decoded payloads
+    if ((job->flags & RPGPU_JOB_DECODE) && j.decoded) STAGE("decode", launch_decode(j, s, c->cu_count * 8));
     if (tm) HIPCHK(c, hipEventRecord(ev[3], s));
-    STAGE("finalize", launch_finalize(j, s));
+    STAGE("validate", launch_validate(j, s, c->cu_count));
     if (tm) HIPCHK(c, hipEventRecord(ev[4], s));
+    STAGE("finalize", launch_finalize(j, s));
+    if (tm) HIPCHK(c, hipEventRecord(ev[5], s));
 #undef STAGE
     return RPGPU_OK;
 }
@@ -382,13 +398,40 @@ __attribute__((target("sse4.2"))) uint32_t rpgpu_crc32c_extend(uint32_t crc, con
 
 extern "C" {
 
-// Implemented with the decode kernels (rp_codec.hip); until then the engine
-// reports the codec as unsupported rather than decoding on the CPU.
-__attribute__((weak)) int rpgpu_uncompress(rpgpu_ctx* c, int codec, const void* in, size_t n, void* out, size_t cap,
-                                           size_t* out_len) {
-    (void)codec; (void)in; (void)n; (void)out; (void)cap;
-    if (out_len) *out_len = 0;
-    return fail(c, RPGPU_E_UNSUPPORTED, "rpgpu_uncompress: decode kernels not built");
+// compression::compressor::uncompress (compression/compression.h:21-24) for
+// one payload: staged to the device, decoded by one wave (rp_codec.hip).
+// The reference throws std::runtime_error on empty input, on `none` and on
+// any decode failure -> RPGPU_E_CODEC; gzip/zstd are not decoded here.
+int rpgpu_uncompress(rpgpu_ctx* c, int codec, const void* in, size_t n, void* out, size_t cap, size_t* out_len) {
+    if (!c || (!in && n) || !out_len) return RPGPU_E_INVALID;
+    *out_len = 0;
+    if (codec < 0 || codec > RPGPU_CODEC_ZSTD) return fail(c, RPGPU_E_INVALID, "rpgpu_uncompress: unknown codec");
+    if (codec == RPGPU_CODEC_GZIP || codec == RPGPU_CODEC_ZSTD)
+        return fail(c, RPGPU_E_UNSUPPORTED, "rpgpu_uncompress: gzip/zstd are not decoded by the engine");
+    if (n == 0 || codec == RPGPU_CODEC_NONE) return fail(c, RPGPU_E_CODEC, "rpgpu_uncompress: empty input or codec none");
+    hipSetDevice(c->device);
+    const uint64_t dcap = decode_capacity_dev(codec, (const uint8_t*)in, n);
+    const size_t in_sz = align_up(n + 16, 256), out_sz = align_up(dcap + 16, 256);
+    const size_t need = in_sz + out_sz + 256;
+    if (need > c->uws_bytes) {
+        if (c->uws) { hipStreamSynchronize(c->stream); hipFree(c->uws); c->uws = nullptr; }
+        if (hipMalloc(&c->uws, need) != hipSuccess) { c->uws_bytes = 0; return fail(c, RPGPU_E_NOMEM, "uncompress workspace"); }
+        c->uws_bytes = need;
+    }
+    uint8_t* d_in = (uint8_t*)c->uws;
+    uint8_t* d_out = d_in + in_sz;
+    int64_t* d_res = (int64_t*)(d_out + out_sz);
+    HIPCHK(c, hipMemsetAsync(d_in + n, 0, in_sz - n, c->stream));
+    HIPCHK(c, hipMemcpyAsync(d_in, in, n, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, launch_uncompress_one(codec, d_in, n, d_out, dcap, d_res, c->stream));
+    int64_t res[2] = {0, 0};
+    HIPCHK(c, hipMemcpyAsync(res, d_res, sizeof res, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    if (res[0] != 0) return fail(c, RPGPU_E_CODEC, "rpgpu_uncompress: payload rejected");
+    *out_len = (size_t)res[1];
+    if ((size_t)res[1] > cap) return fail(c, RPGPU_E_OVERFLOW, "rpgpu_uncompress: output capacity too small");
+    if (res[1]) HIPCHK(c, hipMemcpy(out, d_out, (size_t)res[1], hipMemcpyDeviceToHost));
+    return RPGPU_OK;
 }
 
 __attribute__((weak)) int rpgpu_validate_host(rpgpu_ctx* c, const rpgpu_host_job* job) {

@@ -1,0 +1,653 @@
+// rp_validate.hip — k_validate: the batch CRC32C (model/record_utils.cc:68-91
+// as checked by storage/log_replayer.cc:48-79), reset_size_checksum_metadata
+// over decoded payloads (storage/parser_utils.cc:114-120) and the record walk
+// into the offset index (model/record.h:616-627, model/record_utils.cc:94-181).
+//
+// One wave per batch, 16 waves per CU (4 per SIMD, so LDS and memory latency
+// of one wave hide behind the others), persistent grid of one workgroup per
+// CU.  A payload is processed in 16 KiB windows; lane l loads the contiguous
+// 256-byte region [256 l, +256) of the window into 16 VGPR quads and runs a
+// 4-braid slice-by-4 CRC over it (braid k = dword k of each 16-byte row: four
+// independent chains per lane; tables T15..T12 replicated 32x in LDS so every
+// lookup is bank-conflict-free).  The 64 lane states are merged with GF(2)
+// shift tables over a shuffle tree (shift by 256 << k bytes, k = 0..5).
+//
+// The record walk: a uniform chain over the record length varints, then one
+// record per lane, both reading L2 (the wave has just streamed these bytes)
+// through 32-byte per-lane caches; the other 15 waves of the CU cover the
+// latency.  Integer/byte work only: HBM-bound, no MFMA.
+#include "rp_device.h"
+
+namespace rp {
+
+// Diagnostic build (-DRPGPU_STAMPS, librpgpu_stamps.so): per-phase s_memtime
+// cycle totals summed over all waves, printed by k_print_stamps.  Never
+// benchmarked.
+#ifdef RPGPU_STAMPS
+__device__ unsigned long long g_stamps[8];
+__shared__ unsigned long long s_stamps[kVWaves][8];  // per-wave, flushed once at the end
+#define STAMP(v) const uint64_t v = __builtin_amdgcn_s_memtime()
+#define STAMP_ADD(i, d) do { if (lane() == 0) s_stamps[threadIdx.x >> 6][i] += (unsigned long long)(d); } while (0)
+#else
+#define STAMP(v)
+#define STAMP_ADD(i, d)
+#endif
+
+DEV uint32_t L32(const uint8_t* lds, uint32_t a) { return *(const uint32_t*)(lds + a); }
+
+// LDS address keys of the four braid tables for this lane's copy:
+// {slot * 128 + 4 c, -, row-set, -}; v_perm inserts the entry byte.
+struct Keys {
+    uint32_t k15, k14, k13, k12;
+};
+constexpr uint32_t kSel0 = 0x0C020400u;  // {key.b0, x.b0, key.b2, 0}
+constexpr uint32_t kSel1 = 0x0C020500u;  // x byte 1
+constexpr uint32_t kSel2 = 0x0C020600u;  // x byte 2
+constexpr uint32_t kSel3 = 0x0C020700u;  // x byte 3
+
+// s' = T15[x0] ^ T14[x1] ^ T13[x2] ^ T12[x3], x = s ^ w: the CRC of the word
+// followed by the 12 bytes of the three other braids.
+DEV uint32_t braid_step(const uint8_t* lds, const Keys& K, uint32_t s, uint32_t w) {
+    const uint32_t x = s ^ w;
+    const uint32_t a = L32(lds, __builtin_amdgcn_perm(x, K.k15, kSel0));
+    const uint32_t b = L32(lds, __builtin_amdgcn_perm(x, K.k14, kSel1));
+    const uint32_t c = L32(lds, __builtin_amdgcn_perm(x, K.k13, kSel2));
+    const uint32_t d = L32(lds, __builtin_amdgcn_perm(x, K.k12, kSel3));
+    return (a ^ b) ^ (c ^ d);
+}
+
+// slice-by-4 word step (T3..T0, single copy)
+DEV uint32_t word_step(const uint8_t* lds, uint32_t s, uint32_t w) {
+    const uint32_t x = s ^ w;
+    return (L32(lds, kLdsSlice4Off + ((x & 0xFFu) << 2)) ^ L32(lds, kLdsSlice4Off + 1024u + ((x >> 6) & 0x3FCu))) ^
+           (L32(lds, kLdsSlice4Off + 2048u + ((x >> 14) & 0x3FCu)) ^ L32(lds, kLdsSlice4Off + 3072u + ((x >> 22) & 0x3FCu)));
+}
+
+DEV uint32_t byte_step(const uint8_t* lds, uint32_t s, uint32_t b) {
+    return L32(lds, kLdsSlice4Off + 3072u + (((s ^ b) & 0xFFu) << 2)) ^ (s >> 8);
+}
+
+// advance a raw CRC state over 256 << k zero bytes
+DEV uint32_t shift_k(const uint8_t* lds, uint32_t s, uint32_t k) {
+    const uint32_t base = kLdsShiftOff + k * 4096u;
+    return (L32(lds, base + ((s & 0xFFu) << 2)) ^ L32(lds, base + 1024u + ((s >> 6) & 0x3FCu))) ^
+           (L32(lds, base + 2048u + ((s >> 14) & 0x3FCu)) ^ L32(lds, base + 3072u + ((s >> 22) & 0x3FCu)));
+}
+
+// select a dword by index from values (never from addresses: a select of
+// pointers would pin the register arrays in scratch)
+DEV uint32_t pick4(uint4 v, uint32_t k) {
+    const uint32_t x = v.x, y = v.y, z = v.z, w = v.w;
+    const uint32_t lo = (k & 1u) ? y : x, hi = (k & 1u) ? w : z;
+    return (k & 2u) ? hi : lo;
+}
+
+// Bytes [S, E) of src (offsets from a 16-byte aligned base).  E16 = E rounded
+// down to 16.  When E16 > S, windows are anchored at E16: window r covers
+// [E16 - 16K (R - r), +16K) (window 0 may start before S) and the < 16-byte
+// tail [E16, E) is folded in after them; otherwise the whole payload lies in
+// the 16-byte row at E16 and is all tail.
+struct Stream {
+    const uint8_t* src;
+    uint64_t S, E, E16, R;
+};
+
+DEV Stream make_stream(const uint8_t* src, uint64_t S, uint64_t E) {
+    Stream st;
+    st.src = src;
+    st.S = S;
+    st.E = E;
+    st.E16 = E & ~15ull;
+    st.R = st.E16 > S ? (st.E16 - S + kWinBytes - 1) / kWinBytes : 0;
+    return st;
+}
+
+DEV int64_t win_base(const Stream& st, uint64_t r) {
+    return (int64_t)st.E16 - (int64_t)kWinBytes * (int64_t)(st.R - r);
+}
+
+// this lane's 16 rows of window r (rows wholly outside [S, E16) are zero)
+DEV void load_region(const Stream& st, uint64_t r, uint4 (&d)[16]) {
+    const int64_t a = win_base(st, r) + 256 * (int64_t)lane();
+#pragma unroll
+    for (int i = 0; i < 16; i++) {
+        const int64_t q = a + 16 * i;
+        if (q + 16 > (int64_t)st.S && q < (int64_t)st.E16) d[i] = *(const uint4*)(st.src + q);
+        else d[i] = make_uint4(0u, 0u, 0u, 0u);
+    }
+}
+
+// the 16-byte row at E16 holding the tail (uniform)
+DEV uint4 load_tail(const Stream& st) {
+    uint4 t = make_uint4(0u, 0u, 0u, 0u);
+    if (st.E > st.E16) t = *(const uint4*)(st.src + st.E16);
+    return t;
+}
+
+// CRC of one window from registers: the state at W0 + 16K from the incoming
+// state Tin at Sr (Sr = S in window 0, W0 afterwards).
+DEV uint32_t crc_window(const uint8_t* lds, const Keys& K, uint4 (&d)[16], int64_t W0, uint64_t Sr, uint32_t Tin) {
+    const uint32_t l = lane();
+    const int64_t a = W0 + 256 * (int64_t)l;
+    const int64_t sp = a > (int64_t)Sr ? a : (int64_t)Sr;
+    const bool has = sp < a + 256;
+    // The lane holding Sr starts from Tin; a partial first row is consumed
+    // sequentially.  cc is then the state at the start of row rb; rows before
+    // rb feed zero words into zero braid states (a no-op), so the braid loop
+    // is straight-line for every lane and the four chains interleave.
+    uint32_t cc = 0, rb = 16;
+    if (has) {
+        cc = (sp == (int64_t)Sr) ? Tin : 0u;
+        uint32_t x = (uint32_t)(sp - a);
+        if (x & 15u) {
+            const uint32_t rp = x >> 4;
+            uint32_t px = d[0].x, py = d[0].y, pz = d[0].z, pw = d[0].w;
+#pragma unroll
+            for (int i = 1; i < 16; i++) {
+                const bool h = (uint32_t)i == rp;
+                px = h ? d[i].x : px;
+                py = h ? d[i].y : py;
+                pz = h ? d[i].z : pz;
+                pw = h ? d[i].w : pw;
+            }
+            const uint4 pr = make_uint4(px, py, pz, pw);
+            for (; (x & 3u) && (x & 15u); x++) cc = byte_step(lds, cc, (pick4(pr, (x >> 2) & 3u) >> (8 * (x & 3u))) & 0xFFu);
+            for (; x & 15u; x += 4) cc = word_step(lds, cc, pick4(pr, (x >> 2) & 3u));
+        }
+        rb = x >> 4;
+    }
+    uint32_t s0 = 0, s1 = 0, s2 = 0, s3 = 0;
+#pragma unroll
+    for (int i = 0; i < 15; i++) {
+        // rows before rb are zeroed in place (no second copy of the window)
+        const bool on = (uint32_t)i >= rb;
+        d[i].x = on ? d[i].x : 0u;
+        d[i].y = on ? d[i].y : 0u;
+        d[i].z = on ? d[i].z : 0u;
+        d[i].w = on ? d[i].w : 0u;
+        s0 ^= ((uint32_t)i == rb) ? cc : 0u;
+        s0 = braid_step(lds, K, s0, d[i].x);
+        s1 = braid_step(lds, K, s1, d[i].y);
+        s2 = braid_step(lds, K, s2, d[i].z);
+        s3 = braid_step(lds, K, s3, d[i].w);
+    }
+    // last row: fold the braids back into one state (s_k sits 4k bytes into
+    // row 15) with plain word steps
+    s0 ^= (rb == 15) ? cc : 0u;
+    const bool on15 = rb <= 15;
+    d[15].x = on15 ? d[15].x : 0u;
+    d[15].y = on15 ? d[15].y : 0u;
+    d[15].z = on15 ? d[15].z : 0u;
+    d[15].w = on15 ? d[15].w : 0u;
+    uint32_t m = word_step(lds, s0, d[15].x) ^ s1;
+    m = word_step(lds, m, d[15].y) ^ s2;
+    m = word_step(lds, m, d[15].z) ^ s3;
+    m = word_step(lds, m, d[15].w);
+    uint32_t sv = (rb == 16) ? cc : m;
+    // lane l's state sits at the end of its region: shift-and-xor tree
+#pragma unroll
+    for (uint32_t k = 0; k < kShiftLevels; k++) {
+        const uint32_t other = __shfl_down(sv, 1u << k, 64);
+        sv = shift_k(lds, sv, k) ^ other;
+    }
+    return uni32(sv);
+}
+
+// fold the tail bytes [max(S, E16), E) held in gt into the state (uniform)
+DEV uint32_t crc_tail(const uint8_t* lds, const Stream& st, const uint4& gt, uint32_t Tst) {
+    if (st.E <= st.E16) return Tst;
+    uint32_t x = (uint32_t)((st.S > st.E16 ? st.S : st.E16) - st.E16);
+    const uint32_t nt = (uint32_t)(st.E - st.E16);
+    const uint4 t = make_uint4(uni32(gt.x), uni32(gt.y), uni32(gt.z), uni32(gt.w));
+    for (; (x & 3u) && x < nt; x++) Tst = byte_step(lds, Tst, (pick4(t, x >> 2) >> (8 * (x & 3u))) & 0xFFu);
+    for (; x + 4 <= nt; x += 4) Tst = word_step(lds, Tst, pick4(t, x >> 2));
+    for (; x < nt; x++) Tst = byte_step(lds, Tst, (pick4(t, x >> 2) >> (8 * (x & 3u))) & 0xFFu);
+    return uni32(Tst);
+}
+
+// CRC state after [S, E) from the state Tst at S.  d holds window 0 (or the
+// only window) on entry and the last window on exit; gt the tail row.
+DEV uint32_t crc_stream(const uint8_t* lds, const Keys& K, const Stream& st, uint4 (&d)[16], const uint4& gt,
+                        uint32_t Tst) {
+    for (uint64_t r = 0; r < st.R; r++) {
+        if (r) load_region(st, r, d);
+        const int64_t W0 = win_base(st, r);
+        Tst = crc_window(lds, K, d, W0, r == 0 ? st.S : (uint64_t)W0, Tst);
+    }
+    return crc_tail(lds, st, gt, Tst);
+}
+
+// ---------------------------------------------------------------------------
+// Record walk
+// ---------------------------------------------------------------------------
+
+// Per-lane 32-byte read cache over global memory (L2-resident payload).
+// Positions are 32-bit offsets from the payload start p0 (a wave-uniform
+// pointer, so addresses are SGPR base + VGPR offset).  16-byte rows starting
+// at or past n read as zero; a row may run up to 15 bytes past the payload
+// (buffers are readable to a 16-byte boundary past their end).
+struct GCache {
+    uint32_t base;   // payload offset of lo (base + p0 is 16-byte aligned)
+    uint4 lo, hi;
+};
+
+// p0 is 16-byte aligned minus `mis` (= p0 & 15): row starts are kept on the
+// absolute 16-byte grid so every load is one aligned dwordx4
+DEV void gc12(const uint8_t* p0, uint32_t mis, uint32_t n, GCache& C, uint32_t q, uint32_t& r0, uint32_t& r1,
+              uint32_t& r2) {
+    // cache coordinates are absolute-grid offsets: g = q + mis
+    const uint32_t g = q + mis;
+    if (!(g >= C.base && g + 12 <= C.base + 32)) {
+        C.base = g & ~15u;
+        C.lo = make_uint4(0u, 0u, 0u, 0u);
+        C.hi = make_uint4(0u, 0u, 0u, 0u);
+        const uint8_t* row = p0 - mis + C.base;
+        if (C.base < n + mis) C.lo = *(const uint4*)row;
+        if (C.base + 16 < n + mis) C.hi = *(const uint4*)(row + 16);
+    }
+    const uint32_t o = g - C.base;
+    const uint32_t k = o >> 2, sh = o & 3u;
+    uint32_t w[4];
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        const uint32_t kk = k + (uint32_t)i;  // 0..7
+        w[i] = kk < 4 ? pick4(C.lo, kk) : pick4(C.hi, kk - 4);
+    }
+    r0 = __builtin_amdgcn_alignbyte(w[1], w[0], sh);
+    r1 = __builtin_amdgcn_alignbyte(w[2], w[1], sh);
+    r2 = __builtin_amdgcn_alignbyte(w[3], w[2], sh);
+}
+
+// vint::deserialize (utils/vint.h:82-98) over at most `avail` bytes: LEB128
+// stopping after 10 bytes, or at the end of input with the partial value.
+// One- and two-byte varints (almost every length/delta) take a short path.
+DEV int64_t varint12(uint32_t r0, uint32_t r1, uint32_t r2, uint32_t avail, uint32_t& br) {
+    uint64_t res;
+    if (avail >= 2 && (r0 & 0x8080u) != 0x8080u) {
+        const uint32_t b0 = r0 & 0xFFu;
+        if (!(b0 & 0x80u)) { br = 1; res = b0; }
+        else { br = 2; res = (b0 & 0x7Fu) | (((r0 >> 8) & 0x7Fu) << 7); }
+    } else {
+        const uint64_t lo = (uint64_t)r0 | ((uint64_t)r1 << 32);
+        res = 0;
+        uint32_t cnt = 0;
+        const uint32_t lim = avail < 10 ? avail : 10u;
+        for (uint32_t i = 0; i < lim; i++) {
+            const uint64_t byte = (i < 8 ? (lo >> (8 * i)) : (r2 >> (8 * (i - 8)))) & 0xFF;
+            cnt++;
+            res |= (byte & 127) << (7 * i);
+            if (!(byte & 128)) break;
+        }
+        br = cnt;
+    }
+    return (int64_t)((res >> 1) ^ (~(res & 1) + 1));
+}
+
+struct Reader {
+    const uint8_t* p0;  // payload start (wave-uniform)
+    uint32_t mis;       // p0 & 15
+    uint32_t n;
+    uint32_t pos;
+    GCache C;
+
+    // iobuf_parser_base::read_varlong (bytes/iobuf_parser.h:48-52)
+    DEV int64_t varlong() {
+        uint32_t r0, r1, r2, br;
+        gc12(p0, mis, n, C, pos, r0, r1, r2);
+        const int64_t x = varint12(r0, r1, r2, n - pos, br);
+        pos += br;
+        return x;
+    }
+    DEV uint32_t byte() {
+        uint32_t r0, r1, r2;
+        gc12(p0, mis, n, C, pos, r0, r1, r2);
+        return r0 & 0xFFu;
+    }
+};
+
+// iobuf_copy (bytes/iobuf.cc:133-157): -1 when (int)len < 0 (bad_alloc);
+// a length past the end copies what is there, silently
+DEV int copy_bytes(Reader& c, int64_t len) {
+    const int32_t bl = (int32_t)(uint32_t)(uint64_t)len;
+    if (bl < 0) return -1;
+    const uint32_t left = c.n - c.pos;
+    c.pos += ((uint32_t)bl < left) ? (uint32_t)bl : left;
+    return 0;
+}
+
+struct Rec {
+    uint32_t err;   // rpgpu_parse_err
+    uint32_t end;
+    int64_t ts;
+    int32_t length, off, klen, vlen, hcount;
+    uint32_t key_pos, val_pos, hdr_pos;
+    int32_t attr;
+};
+
+// parse_one_record_copy_from_buffer (model/record_utils.cc:170-177) over
+// parse_record_meta_from_buffer / do_parse_one_record_from_buffer /
+// parse_record_headers (:94-160)
+DEV Rec parse_record(const uint8_t* p0, uint32_t mis, uint32_t n, uint32_t start) {
+    Rec r;
+    Reader c;
+    c.p0 = p0;
+    c.mis = mis;
+    c.n = n;
+    c.pos = start;
+    c.C.base = 0xFFFFFFF0u;
+    r.err = 0;
+    r.key_pos = r.val_pos = r.hdr_pos = 0;
+    r.ts = 0; r.length = r.off = r.klen = r.vlen = r.hcount = 0; r.attr = 0;
+    const int64_t rsz = c.varlong();
+    // consume_type<int8_t>: the only read that throws on short input
+    if (c.pos >= n) { r.err = RPGPU_PARSE_ERR_ATTR_EOF; r.end = c.pos; return r; }
+    r.attr = (int8_t)c.byte();
+    c.pos++;
+    r.ts = c.varlong();
+    const int64_t off = c.varlong();
+    const int64_t kl = c.varlong();
+    r.key_pos = c.pos;
+    if (kl > 0 && copy_bytes(c, kl)) { r.err = RPGPU_PARSE_ERR_COPY_NEGATIVE; r.end = c.pos; return r; }
+    const int64_t vl = c.varlong();
+    r.val_pos = c.pos;
+    if (vl > 0 && copy_bytes(c, vl)) { r.err = RPGPU_PARSE_ERR_COPY_NEGATIVE; r.end = c.pos; return r; }
+    const int64_t hc = c.varlong();
+    r.hdr_pos = c.pos;
+    // headers.reserve(count) throws for count < 0 or beyond the limit
+    if (hc < 0 || hc > RPGPU_MAX_HEADER_RESERVE) { r.err = RPGPU_PARSE_ERR_HEADER_RESERVE; r.end = c.pos; return r; }
+    for (int32_t h = 0; h < (int32_t)hc; h++) {
+        if (c.pos >= n) break;
+        const int64_t hk = c.varlong();
+        if (hk > 0 && copy_bytes(c, hk)) { r.err = RPGPU_PARSE_ERR_COPY_NEGATIVE; r.end = c.pos; return r; }
+        const int64_t hv = c.varlong();
+        if (hv > 0 && copy_bytes(c, hv)) { r.err = RPGPU_PARSE_ERR_COPY_NEGATIVE; r.end = c.pos; return r; }
+    }
+    r.length = (int32_t)rsz;
+    r.off = (int32_t)off;
+    r.klen = (int32_t)kl;
+    r.vlen = (int32_t)vl;
+    r.hcount = (int32_t)hc;
+    r.end = c.pos;
+    return r;
+}
+
+struct WalkResult {
+    uint32_t parsed;
+    uint32_t err;
+    uint32_t trailing;
+};
+
+// record_batch::for_each_record (model/record.h:616-627) with speculative
+// lane-parallel records: a uniform chain over the length varints guesses
+// where records start, lanes parse one record each, and only the prefix
+// whose starts are confirmed by the previous record's exact end is committed.
+// The chain reads through the same 32-byte cache as the lanes (uniform
+// address: one L2 line per step).
+DEV WalkResult walk_records(const uint8_t* p0, uint32_t n, int32_t rc, uint32_t batch_ord, rpgpu_record_index* out,
+                            uint64_t out_cap) {
+    WalkResult wr;
+    wr.parsed = 0;
+    wr.err = 0;
+    wr.trailing = 0;
+    const uint32_t l = lane();
+    const uint32_t mis = (uint32_t)((uintptr_t)p0 & 15);
+    GCache cc;
+    cc.base = 0xFFFFFFF0u;
+    uint32_t start = 0;
+    uint32_t done = 0;
+    const uint32_t total = (uint32_t)(rc > 0 ? rc : 0);
+    while (done < total) {
+        const uint32_t want = (total - done) < 64u ? (total - done) : 64u;
+        uint32_t my_start = 0xFFFFFFFFu;
+        uint32_t p = start;
+        uint32_t m = 0;
+        for (; m < want; m++) {
+            if (l == m) my_start = p;
+            if (p >= n) { m++; break; }
+            uint32_t r0, r1, r2, br;
+            gc12(p0, mis, n, cc, p, r0, r1, r2);
+            r0 = uni32(r0); r1 = uni32(r1); r2 = uni32(r2);
+            const int64_t len = varint12(r0, r1, r2, n - p, br);
+            if (len < 0 || (uint64_t)len > n) { m++; break; }
+            p = p + br + (uint32_t)len;
+        }
+        Rec r;
+        const bool act = l < m;
+        if (act) r = parse_record(p0, mis, n, my_start);
+        else { r.err = 0; r.end = 0xFFFFFFFFu; }
+        const uint32_t prev_end = __shfl_up(r.end, 1, 64);
+        const uint32_t prev_err = __shfl_up(r.err, 1, 64);
+        const bool match = (l == 0) || (prev_err == 0 && prev_end == my_start);
+        const uint64_t bad = __ballot(act && !match);
+        const uint32_t exact = bad ? (uint32_t)__builtin_ctzll(bad) : m;  // lanes [0, exact) are exact
+        const uint64_t errs = __ballot(act && l < exact && r.err != 0);
+        const uint32_t nok = errs ? (uint32_t)__builtin_ctzll(errs) : exact;  // records parsed OK
+        if (l < nok && done + l < out_cap) {
+            rpgpu_record_index e;
+            e.batch = batch_ord;
+            e.rec_pos = my_start;
+            e.ts_delta = r.ts;
+            e.length = r.length;
+            e.offset_delta = r.off;
+            e.key_len = r.klen;
+            e.key_pos = r.key_pos;
+            e.val_len = r.vlen;
+            e.val_pos = r.val_pos;
+            e.hdr_count = r.hcount;
+            e.hdr_pos = r.hdr_pos;
+            e.end_pos = r.end;
+            e.attrs = (int8_t)r.attr;
+            e.pad[0] = e.pad[1] = e.pad[2] = 0;
+            e.reserved[0] = e.reserved[1] = 0;
+            out[done + l] = e;
+        }
+        if (errs) {
+            wr.parsed = done + nok;
+            wr.err = uni32(__shfl(r.err, nok, 64));
+            return wr;
+        }
+        start = uni32(__shfl(r.end, exact - 1, 64));
+        done += exact;
+    }
+    wr.parsed = done;
+    wr.trailing = n - start;
+    return wr;
+}
+
+// internal_header_only_crc (model/record_utils.cc:34-55) of the header that
+// reset_size_checksum_metadata produces: codec bits cleared, size_bytes =
+// 61 + decoded, crc = the decoded crc (storage/parser_utils.cc:53-56, 114-120)
+DEV uint32_t decoded_header_crc(const Tables* T, const uint8_t* hdr, uint32_t new_size, uint32_t new_crc) {
+    const uint32_t l = lane();
+    uint32_t b = (l < RPGPU_HEADER_SIZE) ? (uint32_t)hdr[l] : 0u;
+    if (l >= 4 && l < 8) b = (new_size >> (8 * (l - 4))) & 0xFFu;
+    if (l >= 17 && l < 21) b = (new_crc >> (8 * (l - 17))) & 0xFFu;
+    if (l == 21) b &= ~7u;
+    const uint32_t contrib = (l >= 4 && l < RPGPU_HEADER_SIZE) ? T->hdr[60 - l][b] : 0u;
+    return ~(T->c57 ^ wave_xor(contrib));
+}
+
+// first batch of segment s failing complete && crc_ok (log_replayer
+// checkpoint, storage/log_replayer.cc:62-79); resolved by k_finalize_segments
+DEV void note_bad(const DeviceJob& j, uint32_t seg, uint64_t b) {
+    if (lane() == 0) {
+        const uint64_t first = j.chunk_count[j.chunk_base[seg]];
+        atomicMin(&j.seg_first_bad[seg], (uint32_t)(b - first));
+    }
+}
+
+// Per-batch descriptor (uniform).  index_base carries the absolute payload
+// start from k_emit (scratch, overwritten here).
+struct Desc {
+    uint32_t flags, crc, praw, codec, seg;
+    uint64_t S, n, ib, islots, doff;
+    int32_t rc;
+};
+
+DEV Desc load_desc(const DeviceJob& j, uint64_t b) {
+    const rpgpu_batch_result* R = &j.batches[b];
+    Desc d;
+    d.flags = uni32(R->flags);
+    d.crc = uni32(R->crc);
+    d.praw = uni32((uint32_t)R->reserved1);
+    d.S = uni64(R->index_base);
+    d.n = uni32((uint32_t)R->size_bytes - RPGPU_HEADER_SIZE);
+    d.rc = (int32_t)uni32((uint32_t)R->record_count);
+    d.codec = uni32((uint32_t)(uint16_t)R->attrs) & 7u;
+    d.seg = uni32(R->segment);
+    d.ib = uni64(j.slots[b]);
+    d.islots = uni64(j.slots[b + 1]) - d.ib;
+    d.doff = uni64(j.dcap[b]);
+    return d;
+}
+
+// CRC + (optional) walk of one stream; d/gt hold its first window and tail
+DEV uint32_t stream_crc_walk(const DeviceJob& j, const uint8_t* lds, const Keys& K, const Stream& st, uint4 (&d)[16],
+                             const uint4& gt, uint32_t Tst, bool walk, const Desc& ds, uint64_t b, WalkResult& w,
+                             bool& idx_ok) {
+    STAMP(t0);
+    const uint32_t crc = ~crc_stream(lds, K, st, d, gt, Tst);
+    STAMP(t1);
+    STAMP_ADD(0, t1 - t0);
+    if (walk) {
+        idx_ok = ds.ib + ds.islots <= j.record_capacity;
+        rpgpu_record_index* out = idx_ok ? j.records + ds.ib : nullptr;
+        const uint64_t cap = idx_ok ? ds.islots : 0;
+        w = walk_records(st.src + st.S, (uint32_t)(st.E - st.S), ds.rc, (uint32_t)b, out, cap);
+        STAMP(t2);
+        STAMP_ADD(1, t2 - t1);
+    }
+    return crc;
+}
+
+__global__ __launch_bounds__(1024) void k_validate(DeviceJob j) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    const Tables* T = j.tables;
+    const uint32_t tid = threadIdx.x;
+    // braid tables: word i -> row-set rs = i >> 14, entry e = (i >> 6) & 255,
+    // slot = (i >> 5) & 1, copy = i & 31; (rs, slot) = (0,0) T15, (0,1) T14,
+    // (1,0) T13, (1,1) T12
+    for (uint32_t i = tid; i < 32768u; i += blockDim.x)
+        ((uint32_t*)(lds + kLdsBraidOff))[i] = T->hdr[15 - (((i >> 14) << 1) | ((i >> 5) & 1u))][(i >> 6) & 255u];
+    // slice tables: T3, T2, T1, T0
+    for (uint32_t i = tid; i < 1024u; i += blockDim.x) ((uint32_t*)(lds + kLdsSlice4Off))[i] = T->hdr[3 - (i >> 8)][i & 255u];
+    // shift tables: comb[1..6] (256 .. 8192 bytes)
+    for (uint32_t i = tid; i < kShiftLevels * 1024u; i += blockDim.x)
+        ((uint32_t*)(lds + kLdsShiftOff))[i] = ((const uint32_t*)T->comb[1])[i];
+    __syncthreads();
+
+    const uint32_t l = lane();
+    const uint32_t bank = (l & 31u) * 4u;
+    Keys K;
+    K.k15 = (0u << 16) | (0u + bank);
+    K.k14 = (0u << 16) | (128u + bank);
+    K.k13 = (1u << 16) | (0u + bank);
+    K.k12 = (1u << 16) | (128u + bank);
+    const uint32_t c40 = uni32(T->c40);
+
+    const uint64_t nb_total = j.chunk_count[j.total_chunks];
+    const uint64_t nb = nb_total < j.batch_capacity ? nb_total : j.batch_capacity;
+    const uint64_t nw = (uint64_t)gridDim.x * kVWaves;
+#ifdef RPGPU_STAMPS
+    if (l == 0)
+        for (int i = 0; i < 8; i++) s_stamps[tid >> 6][i] = 0;
+#endif
+    STAMP(tk0);
+    for (uint64_t b = (uint64_t)blockIdx.x * kVWaves + (tid >> 6); b < nb; b += nw) {
+        rpgpu_batch_result* R = &j.batches[b];
+        const Desc d = load_desc(j, b);
+        if (!(d.flags & RPGPU_F_COMPLETE)) {
+            if (l == 0) { R->index_base = d.ib; R->decoded_off = d.doff; R->reserved1 = 0; }
+            note_bad(j, d.seg, b);
+            continue;
+        }
+        uint32_t f = d.flags;
+        uint32_t parsed = 0, perr = 0, dcrc = 0, dhcrc = 0;
+        WalkResult w;
+        bool walked = false, idx_ok = false;
+        uint32_t crc;
+        {
+            // stored payload: batch crc (+ walk when uncompressed).  CRC state
+            // after the BE40 prefix with init ~0 = c40 ^ the prefix's raw
+            // contribution (computed by k_emit)
+            const Stream st = make_stream(j.data, d.S, d.S + d.n);
+            uint4 v[16];
+            load_region(st, 0, v);  // unconditional: an array left undefined on one path is pinned in scratch
+            const uint4 gt = load_tail(st);
+            walked = d.codec == 0 && (j.flags & RPGPU_JOB_PARSE);
+            crc = stream_crc_walk(j, lds, K, st, v, gt, d.praw ^ c40, walked, d, b, w, idx_ok);
+        }
+        if (crc == d.crc) f |= RPGPU_F_CRC_OK;
+        else note_bad(j, d.seg, b);
+        if (d.codec != 0 && (f & RPGPU_F_CODEC_OK)) {
+            // reset_size_checksum_metadata over the decoded payload: the prefix
+            // differs only in the codec bits of attrs (BE40 byte 1)
+            const uint64_t dl = uni32(R->decoded_len);
+            const Stream ds = make_stream(j.decoded, d.doff, d.doff + dl);
+            uint4 v[16];
+            load_region(ds, 0, v);
+            const uint4 gt = load_tail(ds);
+            walked = (j.flags & RPGPU_JOB_PARSE) != 0;
+            dcrc = stream_crc_walk(j, lds, K, ds, v, gt, d.praw ^ T->hdr[38][d.codec] ^ c40, walked, d, b, w, idx_ok);
+            dhcrc = decoded_header_crc(T, j.data + d.S - RPGPU_HEADER_SIZE, (uint32_t)(RPGPU_HEADER_SIZE + dl), dcrc);
+        }
+        if (walked) {
+            parsed = w.parsed;
+            perr = w.err;
+            f |= RPGPU_F_PARSED;
+            if (perr == 0) {
+                f |= RPGPU_F_PARSE_ASYNC_OK;
+                if (w.trailing == 0) f |= RPGPU_F_PARSE_OK;
+                else perr = RPGPU_PARSE_ERR_TRAILING;
+            }
+            if (f & RPGPU_F_PARSE_OK) {
+                if (idx_ok) f |= RPGPU_F_INDEX_WRITTEN;
+                else { perr = RPGPU_PARSE_ERR_INDEX_CAPACITY; if (l == 0) atomicOr(&j.counters[1], 2u); }
+            }
+        }
+        if (l == 0) {
+            R->crc_computed = crc;
+            R->flags = f;
+            R->index_base = d.ib;
+            R->decoded_off = d.doff;
+            R->records_parsed = parsed;
+            R->parse_err = (uint8_t)perr;
+            if (d.codec != 0 && (f & RPGPU_F_CODEC_OK)) {
+                R->decoded_crc = dcrc;
+                R->decoded_header_crc = dhcrc;
+            }
+            R->reserved1 = 0;
+        }
+        STAMP_ADD(3, 1);
+    }
+    STAMP(tk1);
+    STAMP_ADD(4, tk1 - tk0);
+#ifdef RPGPU_STAMPS
+    if (l == 0)
+        for (int i = 0; i < 8; i++) atomicAdd(&g_stamps[i], s_stamps[tid >> 6][i]);
+#endif
+}
+
+#ifdef RPGPU_STAMPS
+__global__ void k_print_stamps() {
+    const double n = (double)g_stamps[3];
+    printf("RPGPU_STAMPS batches=%.0f cycles/batch/wave: crc(+loads)=%.0f walk=%.0f total=%.0f\n", n,
+           g_stamps[0] / n, g_stamps[1] / n, g_stamps[4] / n);
+    for (int i = 0; i < 8; i++) g_stamps[i] = 0;
+}
+#endif
+
+hipError_t launch_validate(const DeviceJob& j, hipStream_t s, uint32_t grid) {
+    static bool attr = false;
+    if (!attr) {
+        (void)hipFuncSetAttribute((const void*)k_validate, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsValidateBytes);
+        attr = true;
+    }
+    hipLaunchKernelGGL(k_validate, dim3(grid), dim3(64 * kVWaves), kLdsValidateBytes, s, j);
+#ifdef RPGPU_STAMPS
+    hipLaunchKernelGGL(k_print_stamps, dim3(1), dim3(1), 0, s);
+#endif
+    return hipGetLastError();
+}
+
+}  // namespace rp

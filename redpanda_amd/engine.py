@@ -86,9 +86,9 @@ class Engine:
         check(self.L.rpgpu_set_timing(self.ctx, 1 if on else 0), self.ctx, "rpgpu_set_timing")
 
     def last_timings(self):
-        ms = (C.c_float * 4)()
-        check(self.L.rpgpu_last_timings(self.ctx, ms, 4), self.ctx, "rpgpu_last_timings")
-        return {"total": ms[0], "discover": ms[1], "resolve_plan": ms[2], "validate": ms[3]}
+        ms = (C.c_float * 5)()
+        check(self.L.rpgpu_last_timings(self.ctx, ms, 5), self.ctx, "rpgpu_last_timings")
+        return {"total": ms[0], "discover": ms[1], "resolve_plan": ms[2], "validate": ms[3], "decode": ms[4]}
 
     def alloc_outputs(self, n_segments: int, batch_capacity: int, record_capacity: int,
                       decoded_capacity: int, bitmap: bool = True):
@@ -134,6 +134,20 @@ class Engine:
         s = stream if stream is not None else torch.cuda.current_stream(data.device)
         check(self.L.rpgpu_submit(self.ctx, C.byref(job), C.c_void_p(s.cuda_stream)), self.ctx, "rpgpu_submit")
         return out
+
+    def uncompress(self, codec: int, payload: bytes, cap: int = None):
+        """compression::compressor::uncompress for one payload on the device.
+        Returns the decoded bytes; raises RpgpuError (RPGPU_E_CODEC) where the
+        reference throws std::runtime_error."""
+        src = np.frombuffer(bytes(payload), dtype=np.uint8)
+        if cap is None:
+            cap = max(len(payload) * 300, 1 << 20)
+        out = np.zeros(max(cap, 1), dtype=np.uint8)
+        n = C.c_size_t(0)
+        rc = self.L.rpgpu_uncompress(self.ctx, codec, src.ctypes.data_as(C.c_void_p), src.nbytes,
+                                     out.ctypes.data_as(C.c_void_p), cap, C.byref(n))
+        check(rc, self.ctx, "rpgpu_uncompress")
+        return out[: n.value].tobytes()
 
     def validate(self, data, seg_offsets, flags: int = abi.JOB_CRC | abi.JOB_PARSE, batch_capacity=None,
                  record_capacity=None, decoded_capacity=None, chunk_bytes: int = 0) -> HostResult:
