@@ -12,26 +12,30 @@ namespace rp {
 constexpr uint64_t kNone = ~0ull;
 constexpr uint32_t kCrcPoly = 0x82F63B78u;
 
-// Combine tables: shift a raw CRC state over kStream * 2^l zero bytes.
-constexpr uint32_t kStream = 128;
-constexpr uint32_t kCombineLevels = 7;             // l = 0..6 (128 B .. 8 KiB)
+// Shift tables: advance a raw CRC state over 16 << m zero bytes (m = 0..5):
+// the cross-lane merge tree of the validate kernel.
+constexpr uint32_t kShiftLevels = 6;
+// Braid stride of the validate kernel: lane l's 16 bytes of window row i sit
+// at 1024 i + 16 l, so a braid word is followed by 1020 bytes of other braids.
+constexpr uint32_t kBraidSkip = 1020;
 
 // Validate kernel (rp_validate.hip): one wave per batch, 16 waves per
 // workgroup (4 per SIMD), one workgroup per CU.  A payload is processed in
-// 16 KiB windows: lane l holds bytes [256 l, 256 l + 256) of the window.
+// 16 KiB windows of 16 rows of 1 KiB: lane l holds bytes [1024 i + 16 l, +16)
+// of every row i (one coalesced dwordx4 load per row).
 constexpr uint32_t kVWaves = 16;
 constexpr uint32_t kWinBytes = 16384;
 // LDS image of the validate kernel (bytes):
-//  [0, 128 KiB)    braid tables T15..T12 (byte followed by 15..12 zero bytes),
+//  [0, 128 KiB)    braid tables T1023..T1020 (byte followed by 1023..1020
+//                  zero bytes),
 //                  32 copies so lane L always hits bank L % 32: two 64 KiB
 //                  row-sets, entry e row = 256 B, table A at [0,128) and
 //                  table B at [128,256), copy c at 4c
 //  [128, 132 KiB)  slice tables T3..T0 (single copy): word/byte steps
-//  [132, 156 KiB)  shift tables: 6 levels, shift by 256 << k bytes
+//  [132, 156 KiB)  shift tables: 6 levels, shift by 16 << m bytes
 constexpr uint32_t kLdsBraidOff = 0;
 constexpr uint32_t kLdsSlice4Off = 131072;
 constexpr uint32_t kLdsShiftOff = kLdsSlice4Off + 4096;
-constexpr uint32_t kShiftLevels = 6;
 constexpr uint32_t kLdsValidateBytes = kLdsShiftOff + kShiftLevels * 4096;
 static_assert(kLdsValidateBytes <= 160u * 1024u, "validate LDS image exceeds 160 KiB");
 
@@ -39,7 +43,8 @@ static_assert(kLdsValidateBytes <= 160u * 1024u, "validate LDS image exceeds 160
 struct Tables {
     uint32_t slice[4][256];          // T_k[b]: byte b followed by k zero bytes (raw CRC)
     uint32_t hdr[57][256];           // T_d for d = 0..56 (parallel header CRC)
-    uint32_t comb[kCombineLevels][4][256]; // shift by kStream*2^l bytes, per state byte
+    uint32_t braid[4][256];          // T_{1023-t}[b]: byte b followed by 1023 - t zero bytes
+    uint32_t shift[kShiftLevels][4][256]; // state byte j (value b << 8j) over 16 << m zero bytes
     uint32_t c57;                    // state 0xFFFFFFFF advanced over 57 zero bytes
     uint32_t c40;                    // state 0xFFFFFFFF advanced over 40 zero bytes
     uint32_t pad[2];

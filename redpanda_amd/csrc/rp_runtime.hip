@@ -41,14 +41,23 @@ static void build_tables(Tables* T) {
             c = raw_step_zero(c, t0);
         }
     }
-    // shift tables: state byte j (value b << 8j) advanced over kStream*2^l zero bytes
-    for (uint32_t l = 0; l < kCombineLevels; l++) {
-        const uint64_t n = (uint64_t)kStream << l;
+    // braid tables: byte b followed by 1023 - t zero bytes
+    for (uint32_t b = 0; b < 256; b++) {
+        uint32_t c = t0[b];
+        for (uint32_t z = 0; z < kBraidSkip; z++) c = raw_step_zero(c, t0);
+        for (int t = 3; t >= 0; t--) {
+            T->braid[t][b] = c;  // t = 3: 1020 zeros ... t = 0: 1023 zeros
+            c = raw_step_zero(c, t0);
+        }
+    }
+    // shift tables: state byte j (value b << 8j) advanced over 16 << m zero bytes
+    for (uint32_t m = 0; m < kShiftLevels; m++) {
+        const uint64_t n = 16ull << m;
         for (uint32_t j = 0; j < 4; j++) {
             for (uint32_t b = 0; b < 256; b++) {
                 uint32_t c = b << (8 * j);
                 for (uint64_t z = 0; z < n; z++) c = raw_step_zero(c, t0);
-                T->comb[l][j][b] = c;
+                T->shift[m][j][b] = c;
             }
         }
     }

@@ -5,17 +5,21 @@
 //
 // One wave per batch, 16 waves per CU (4 per SIMD, so LDS and memory latency
 // of one wave hide behind the others), persistent grid of one workgroup per
-// CU.  A payload is processed in 16 KiB windows; lane l loads the contiguous
-// 256-byte region [256 l, +256) of the window into 16 VGPR quads and runs a
-// 4-braid slice-by-4 CRC over it (braid k = dword k of each 16-byte row: four
-// independent chains per lane; tables T15..T12 replicated 32x in LDS so every
-// lookup is bank-conflict-free).  The 64 lane states are merged with GF(2)
-// shift tables over a shuffle tree (shift by 256 << k bytes, k = 0..5).
+// CU.  A payload is processed in 16 KiB windows of 16 rows of 1 KiB; lane l
+// loads bytes [1024 i + 16 l, +16) of each row i (one fully coalesced
+// dwordx4 per row) and runs 4 braided CRC chains over them: braid (l, k) is
+// dword k of the lane's 16 bytes in every row, so one step covers the word
+// plus the 1020 bytes of the other 255 braids (tables T1023..T1020,
+// replicated 32x in LDS: every lookup bank-conflict-free).  Row 15 folds the
+// lane's four braids back into one state with plain word steps, and the 64
+// lane states are merged with GF(2) shift tables over a shuffle tree (shift
+// by 16 << m bytes, m = 0..5).
 //
-// The record walk: a uniform chain over the record length varints, then one
-// record per lane, both reading L2 (the wave has just streamed these bytes)
-// through 32-byte per-lane caches; the other 15 waves of the CU cover the
-// latency.  Integer/byte work only: HBM-bound, no MFMA.
+// The record walk: a uniform chain over the record length varints read
+// through the scalar cache, then one record per lane read from L2 (the wave
+// has just streamed these bytes) through 32-byte per-lane caches; the other
+// 15 waves of the CU cover the latency.  Integer/byte work only: HBM-bound,
+// no MFMA.
 #include "rp_device.h"
 
 namespace rp {
@@ -35,6 +39,10 @@ __shared__ unsigned long long s_stamps[kVWaves][8];  // per-wave, flushed once a
 
 DEV uint32_t L32(const uint8_t* lds, uint32_t a) { return *(const uint32_t*)(lds + a); }
 
+// constant address space: wave-uniform loads through it become s_load (the
+// scalar cache), off the vector-memory queue the window stream keeps busy
+typedef const __attribute__((address_space(4))) uint32_t cu32;
+
 // LDS address keys of the four braid tables for this lane's copy:
 // {slot * 128 + 4 c, -, row-set, -}; v_perm inserts the entry byte.
 struct Keys {
@@ -45,8 +53,8 @@ constexpr uint32_t kSel1 = 0x0C020500u;  // x byte 1
 constexpr uint32_t kSel2 = 0x0C020600u;  // x byte 2
 constexpr uint32_t kSel3 = 0x0C020700u;  // x byte 3
 
-// s' = T15[x0] ^ T14[x1] ^ T13[x2] ^ T12[x3], x = s ^ w: the CRC of the word
-// followed by the 12 bytes of the three other braids.
+// s' = T1023[x0] ^ T1022[x1] ^ T1021[x2] ^ T1020[x3], x = s ^ w: the CRC of
+// the word followed by the 1020 bytes of the other braids.
 DEV uint32_t braid_step(const uint8_t* lds, const Keys& K, uint32_t s, uint32_t w) {
     const uint32_t x = s ^ w;
     const uint32_t a = L32(lds, __builtin_amdgcn_perm(x, K.k15, kSel0));
@@ -67,7 +75,7 @@ DEV uint32_t byte_step(const uint8_t* lds, uint32_t s, uint32_t b) {
     return L32(lds, kLdsSlice4Off + 3072u + (((s ^ b) & 0xFFu) << 2)) ^ (s >> 8);
 }
 
-// advance a raw CRC state over 256 << k zero bytes
+// advance a raw CRC state over 16 << k zero bytes
 DEV uint32_t shift_k(const uint8_t* lds, uint32_t s, uint32_t k) {
     const uint32_t base = kLdsShiftOff + k * 4096u;
     return (L32(lds, base + ((s & 0xFFu) << 2)) ^ L32(lds, base + 1024u + ((s >> 6) & 0x3FCu))) ^
@@ -81,6 +89,12 @@ DEV uint32_t pick4(uint4 v, uint32_t k) {
     const uint32_t lo = (k & 1u) ? y : x, hi = (k & 1u) ? w : z;
     return (k & 2u) ? hi : lo;
 }
+
+// A lane's share of the current window: dword k of row i in d[i] (rows
+// 0..15, 16 bytes at 1024 i + 16 l).
+struct Win {
+    uint4 r[16];
+};
 
 // Bytes [S, E) of src (offsets from a 16-byte aligned base).  E16 = E rounded
 // down to 16.  When E16 > S, windows are anchored at E16: window r covers
@@ -106,14 +120,16 @@ DEV int64_t win_base(const Stream& st, uint64_t r) {
     return (int64_t)st.E16 - (int64_t)kWinBytes * (int64_t)(st.R - r);
 }
 
-// this lane's 16 rows of window r (rows wholly outside [S, E16) are zero)
-DEV void load_region(const Stream& st, uint64_t r, uint4 (&d)[16]) {
-    const int64_t a = win_base(st, r) + 256 * (int64_t)lane();
+// window r, coalesced: row i of every lane is one 1 KiB wave load (rows
+// wholly outside [S, E16) are zero)
+DEV void load_window(const Stream& st, uint64_t r, Win& w) {
+    const int64_t a = win_base(st, r) + 16 * (int64_t)lane();
 #pragma unroll
     for (int i = 0; i < 16; i++) {
-        const int64_t q = a + 16 * i;
-        if (q + 16 > (int64_t)st.S && q < (int64_t)st.E16) d[i] = *(const uint4*)(st.src + q);
-        else d[i] = make_uint4(0u, 0u, 0u, 0u);
+        const int64_t q = a + 1024 * i;
+        uint4 t = make_uint4(0u, 0u, 0u, 0u);
+        if (q + 16 > (int64_t)st.S && q < (int64_t)st.E16) t = *(const uint4*)(st.src + q);
+        w.r[i] = t;
     }
 }
 
@@ -124,71 +140,45 @@ DEV uint4 load_tail(const Stream& st) {
     return t;
 }
 
-// CRC of one window from registers: the state at W0 + 16K from the incoming
-// state Tin at Sr (Sr = S in window 0, W0 afterwards).
-DEV uint32_t crc_window(const uint8_t* lds, const Keys& K, uint4 (&d)[16], int64_t W0, uint64_t Sr, uint32_t Tin) {
+// CRC of one window from registers: the state at W0 + 16K.  Words before
+// window offset o4 (4-aligned) are not part of the stream (read as zero);
+// the state Tinj is injected at o4.
+DEV uint32_t crc_window(const uint8_t* lds, const Keys& K, const Win& d, uint32_t o4, uint32_t Tinj) {
     const uint32_t l = lane();
-    const int64_t a = W0 + 256 * (int64_t)l;
-    const int64_t sp = a > (int64_t)Sr ? a : (int64_t)Sr;
-    const bool has = sp < a + 256;
-    // The lane holding Sr starts from Tin; a partial first row is consumed
-    // sequentially.  cc is then the state at the start of row rb; rows before
-    // rb feed zero words into zero braid states (a no-op), so the braid loop
-    // is straight-line for every lane and the four chains interleave.
-    uint32_t cc = 0, rb = 16;
-    if (has) {
-        cc = (sp == (int64_t)Sr) ? Tin : 0u;
-        uint32_t x = (uint32_t)(sp - a);
-        if (x & 15u) {
-            const uint32_t rp = x >> 4;
-            uint32_t px = d[0].x, py = d[0].y, pz = d[0].z, pw = d[0].w;
+    const uint32_t i4 = o4 >> 10, l4 = (o4 >> 4) & 63u, k4 = (o4 >> 2) & 3u;
+    const uint32_t lo = 16u * l;  // this lane's offset within a row
+    uint32_t s[4] = {0u, 0u, 0u, 0u};
 #pragma unroll
-            for (int i = 1; i < 16; i++) {
-                const bool h = (uint32_t)i == rp;
-                px = h ? d[i].x : px;
-                py = h ? d[i].y : py;
-                pz = h ? d[i].z : pz;
-                pw = h ? d[i].w : pw;
+    for (int i = 0; i < 16; i++) {
+        uint32_t w[4] = {d.r[i].x, d.r[i].y, d.r[i].z, d.r[i].w};
+        if ((uint32_t)i <= i4) {
+            // the row holding o4 (and any before it): mask words before o4,
+            // inject at o4 (uniform branch; rows after it take neither)
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                const uint32_t off = 1024u * (uint32_t)i + lo + 4u * (uint32_t)k;
+                w[k] = off >= o4 ? w[k] : 0u;
+                s[k] ^= (off == o4) ? Tinj : 0u;
             }
-            const uint4 pr = make_uint4(px, py, pz, pw);
-            for (; (x & 3u) && (x & 15u); x++) cc = byte_step(lds, cc, (pick4(pr, (x >> 2) & 3u) >> (8 * (x & 3u))) & 0xFFu);
-            for (; x & 15u; x += 4) cc = word_step(lds, cc, pick4(pr, (x >> 2) & 3u));
         }
-        rb = x >> 4;
-    }
-    uint32_t s0 = 0, s1 = 0, s2 = 0, s3 = 0;
+        if (i < 15) {
 #pragma unroll
-    for (int i = 0; i < 15; i++) {
-        // rows before rb are zeroed in place (no second copy of the window)
-        const bool on = (uint32_t)i >= rb;
-        d[i].x = on ? d[i].x : 0u;
-        d[i].y = on ? d[i].y : 0u;
-        d[i].z = on ? d[i].z : 0u;
-        d[i].w = on ? d[i].w : 0u;
-        s0 ^= ((uint32_t)i == rb) ? cc : 0u;
-        s0 = braid_step(lds, K, s0, d[i].x);
-        s1 = braid_step(lds, K, s1, d[i].y);
-        s2 = braid_step(lds, K, s2, d[i].z);
-        s3 = braid_step(lds, K, s3, d[i].w);
+            for (int k = 0; k < 4; k++) s[k] = braid_step(lds, K, s[k], w[k]);
+        } else {
+            // row 15: fold the braids (s_k sits at word k) with word steps
+            uint32_t c = word_step(lds, s[0], w[0]) ^ s[1];
+            c = word_step(lds, c, w[1]) ^ s[2];
+            c = word_step(lds, c, w[2]) ^ s[3];
+            s[0] = word_step(lds, c, w[3]);
+        }
     }
-    // last row: fold the braids back into one state (s_k sits 4k bytes into
-    // row 15) with plain word steps
-    s0 ^= (rb == 15) ? cc : 0u;
-    const bool on15 = rb <= 15;
-    d[15].x = on15 ? d[15].x : 0u;
-    d[15].y = on15 ? d[15].y : 0u;
-    d[15].z = on15 ? d[15].z : 0u;
-    d[15].w = on15 ? d[15].w : 0u;
-    uint32_t m = word_step(lds, s0, d[15].x) ^ s1;
-    m = word_step(lds, m, d[15].y) ^ s2;
-    m = word_step(lds, m, d[15].z) ^ s3;
-    m = word_step(lds, m, d[15].w);
-    uint32_t sv = (rb == 16) ? cc : m;
-    // lane l's state sits at the end of its region: shift-and-xor tree
+    // lane l's state sits 16 (63 - l) bytes before the window end:
+    // shift-and-xor tree
+    uint32_t sv = s[0];
 #pragma unroll
-    for (uint32_t k = 0; k < kShiftLevels; k++) {
-        const uint32_t other = __shfl_down(sv, 1u << k, 64);
-        sv = shift_k(lds, sv, k) ^ other;
+    for (uint32_t m = 0; m < kShiftLevels; m++) {
+        const uint32_t other = __shfl_down(sv, 1u << m, 64);
+        sv = shift_k(lds, sv, m) ^ other;
     }
     return uni32(sv);
 }
@@ -205,14 +195,26 @@ DEV uint32_t crc_tail(const uint8_t* lds, const Stream& st, const uint4& gt, uin
     return uni32(Tst);
 }
 
-// CRC state after [S, E) from the state Tst at S.  d holds window 0 (or the
-// only window) on entry and the last window on exit; gt the tail row.
-DEV uint32_t crc_stream(const uint8_t* lds, const Keys& K, const Stream& st, uint4 (&d)[16], const uint4& gt,
-                        uint32_t Tst) {
-    for (uint64_t r = 0; r < st.R; r++) {
-        if (r) load_region(st, r, d);
-        const int64_t W0 = win_base(st, r);
-        Tst = crc_window(lds, K, d, W0, r == 0 ? st.S : (uint64_t)W0, Tst);
+// CRC state after [S, E) from the state Tst at S.  d holds window 0 on entry
+// (issued by the caller); gt the tail row.  The < 4 bytes up to the first
+// 4-aligned position are folded in first (scalar load), so the window only
+// injects at a word boundary.
+DEV uint32_t crc_stream(const uint8_t* lds, const Keys& K, const Stream& st, Win& d, const uint4& gt, uint32_t Tst) {
+    if (st.R) {
+        const uint64_t S4 = (st.S + 3) & ~3ull;
+        if (S4 != st.S) {
+            const uint32_t w = *(cu32*)(st.src + (st.S & ~3ull));
+            for (uint64_t x = st.S; x < S4; x++) Tst = byte_step(lds, Tst, (w >> (8 * (uint32_t)(x & 3))) & 0xFFu);
+            Tst = uni32(Tst);
+        }
+        for (uint64_t r = 0; r < st.R; r++) {
+            if (r) load_window(st, r, d);
+            const int64_t W0 = win_base(st, r);
+            const uint32_t o4 = r == 0 ? (uint32_t)((int64_t)S4 - W0) : 0u;
+            // S4 can sit exactly at the end of window 0 (S within 3 bytes of
+            // it): that window holds no stream bytes and the state passes on
+            if (o4 < kWinBytes) Tst = crc_window(lds, K, d, o4, Tst);
+        }
     }
     return crc_tail(lds, st, gt, Tst);
 }
@@ -220,6 +222,22 @@ DEV uint32_t crc_stream(const uint8_t* lds, const Keys& K, const Stream& st, uin
 // ---------------------------------------------------------------------------
 // Record walk
 // ---------------------------------------------------------------------------
+
+// 12 bytes at payload offset q (wave-uniform) through the scalar cache:
+// the constant address space makes these s_load_dwordx4, which bypass the
+// vector-memory queue the window stream keeps full (and its in-order vmcnt).
+// The payload is read-only for the whole kernel.  Bytes past the payload are
+// whatever follows it (readable to a 16-byte boundary); callers bound every
+// use by the bytes available.
+DEV void s12(const uint8_t* p0, uint32_t q, uint32_t& r0, uint32_t& r1, uint32_t& r2) {
+    const uintptr_t a = (uintptr_t)(p0 + q);
+    cu32* c = (cu32*)(a & ~(uintptr_t)3);
+    const uint32_t sh = (uint32_t)(a & 3);
+    const uint32_t w0 = c[0], w1 = c[1], w2 = c[2], w3 = c[3];
+    r0 = __builtin_amdgcn_alignbyte(w1, w0, sh);
+    r1 = __builtin_amdgcn_alignbyte(w2, w1, sh);
+    r2 = __builtin_amdgcn_alignbyte(w3, w2, sh);
+}
 
 // Per-lane 32-byte read cache over global memory (L2-resident payload).
 // Positions are 32-bit offsets from the payload start p0 (a wave-uniform
@@ -377,77 +395,89 @@ struct WalkResult {
     uint32_t trailing;
 };
 
+// Speculative record starts for records [done, done + want): a uniform chain
+// over the length varints from `start` (scalar loads).  Lane m gets the
+// start of record done + m; returns how many lanes got one.
+DEV uint32_t chain_starts(const uint8_t* p0, uint32_t n, uint32_t start, uint32_t want, uint32_t& my_start) {
+    const uint32_t l = lane();
+    my_start = 0xFFFFFFFFu;
+    uint32_t p = start;
+    uint32_t m = 0;
+    for (; m < want; m++) {
+        if (l == m) my_start = p;
+        if (p >= n) { m++; break; }
+        uint32_t r0, r1, r2, br;
+        s12(p0, p, r0, r1, r2);
+        const int64_t len = varint12(r0, r1, r2, n - p, br);
+        if (len < 0 || (uint64_t)len > n) { m++; break; }
+        p = uni32(p + br + (uint32_t)len);
+    }
+    return m;
+}
+
+// Lanes [0, m) parse one record each from their speculative starts; the
+// prefix whose starts are confirmed by the previous record's exact end is
+// committed to the index.  Returns false when a record failed (wr filled).
+DEV bool parse_group(const uint8_t* p0, uint32_t mis, uint32_t n, uint32_t m, uint32_t my_start, uint32_t batch_ord,
+                     rpgpu_record_index* out, uint64_t out_cap, uint32_t& done, uint32_t& start, WalkResult& wr) {
+    const uint32_t l = lane();
+    Rec r;
+    const bool act = l < m;
+    if (act) r = parse_record(p0, mis, n, my_start);
+    else { r.err = 0; r.end = 0xFFFFFFFFu; }
+    const uint32_t prev_end = __shfl_up(r.end, 1, 64);
+    const uint32_t prev_err = __shfl_up(r.err, 1, 64);
+    const bool match = (l == 0) || (prev_err == 0 && prev_end == my_start);
+    const uint64_t bad = __ballot(act && !match);
+    const uint32_t exact = bad ? (uint32_t)__builtin_ctzll(bad) : m;  // lanes [0, exact) are exact
+    const uint64_t errs = __ballot(act && l < exact && r.err != 0);
+    const uint32_t nok = errs ? (uint32_t)__builtin_ctzll(errs) : exact;  // records parsed OK
+    if (l < nok && done + l < out_cap) {
+        rpgpu_record_index e;
+        e.batch = batch_ord;
+        e.rec_pos = my_start;
+        e.ts_delta = r.ts;
+        e.length = r.length;
+        e.offset_delta = r.off;
+        e.key_len = r.klen;
+        e.key_pos = r.key_pos;
+        e.val_len = r.vlen;
+        e.val_pos = r.val_pos;
+        e.hdr_count = r.hcount;
+        e.hdr_pos = r.hdr_pos;
+        e.end_pos = r.end;
+        e.attrs = (int8_t)r.attr;
+        e.pad[0] = e.pad[1] = e.pad[2] = 0;
+        e.reserved[0] = e.reserved[1] = 0;
+        out[done + l] = e;
+    }
+    if (errs) {
+        wr.parsed = done + nok;
+        wr.err = uni32(__shfl(r.err, nok, 64));
+        return false;
+    }
+    start = uni32(__shfl(r.end, exact - 1, 64));
+    done += exact;
+    return true;
+}
+
 // record_batch::for_each_record (model/record.h:616-627) with speculative
-// lane-parallel records: a uniform chain over the length varints guesses
-// where records start, lanes parse one record each, and only the prefix
-// whose starts are confirmed by the previous record's exact end is committed.
-// The chain reads through the same 32-byte cache as the lanes (uniform
-// address: one L2 line per step).
+// lane-parallel records: chain_starts guesses 64 record starts at a time,
+// parse_group parses and commits the confirmed prefix.
 DEV WalkResult walk_records(const uint8_t* p0, uint32_t n, int32_t rc, uint32_t batch_ord, rpgpu_record_index* out,
                             uint64_t out_cap) {
     WalkResult wr;
     wr.parsed = 0;
     wr.err = 0;
     wr.trailing = 0;
-    const uint32_t l = lane();
     const uint32_t mis = (uint32_t)((uintptr_t)p0 & 15);
-    GCache cc;
-    cc.base = 0xFFFFFFF0u;
-    uint32_t start = 0;
-    uint32_t done = 0;
     const uint32_t total = (uint32_t)(rc > 0 ? rc : 0);
+    uint32_t start = 0, done = 0;
     while (done < total) {
+        uint32_t my_start;
         const uint32_t want = (total - done) < 64u ? (total - done) : 64u;
-        uint32_t my_start = 0xFFFFFFFFu;
-        uint32_t p = start;
-        uint32_t m = 0;
-        for (; m < want; m++) {
-            if (l == m) my_start = p;
-            if (p >= n) { m++; break; }
-            uint32_t r0, r1, r2, br;
-            gc12(p0, mis, n, cc, p, r0, r1, r2);
-            r0 = uni32(r0); r1 = uni32(r1); r2 = uni32(r2);
-            const int64_t len = varint12(r0, r1, r2, n - p, br);
-            if (len < 0 || (uint64_t)len > n) { m++; break; }
-            p = p + br + (uint32_t)len;
-        }
-        Rec r;
-        const bool act = l < m;
-        if (act) r = parse_record(p0, mis, n, my_start);
-        else { r.err = 0; r.end = 0xFFFFFFFFu; }
-        const uint32_t prev_end = __shfl_up(r.end, 1, 64);
-        const uint32_t prev_err = __shfl_up(r.err, 1, 64);
-        const bool match = (l == 0) || (prev_err == 0 && prev_end == my_start);
-        const uint64_t bad = __ballot(act && !match);
-        const uint32_t exact = bad ? (uint32_t)__builtin_ctzll(bad) : m;  // lanes [0, exact) are exact
-        const uint64_t errs = __ballot(act && l < exact && r.err != 0);
-        const uint32_t nok = errs ? (uint32_t)__builtin_ctzll(errs) : exact;  // records parsed OK
-        if (l < nok && done + l < out_cap) {
-            rpgpu_record_index e;
-            e.batch = batch_ord;
-            e.rec_pos = my_start;
-            e.ts_delta = r.ts;
-            e.length = r.length;
-            e.offset_delta = r.off;
-            e.key_len = r.klen;
-            e.key_pos = r.key_pos;
-            e.val_len = r.vlen;
-            e.val_pos = r.val_pos;
-            e.hdr_count = r.hcount;
-            e.hdr_pos = r.hdr_pos;
-            e.end_pos = r.end;
-            e.attrs = (int8_t)r.attr;
-            e.pad[0] = e.pad[1] = e.pad[2] = 0;
-            e.reserved[0] = e.reserved[1] = 0;
-            out[done + l] = e;
-        }
-        if (errs) {
-            wr.parsed = done + nok;
-            wr.err = uni32(__shfl(r.err, nok, 64));
-            return wr;
-        }
-        start = uni32(__shfl(r.end, exact - 1, 64));
-        done += exact;
+        const uint32_t m = chain_starts(p0, n, start, want, my_start);
+        if (!parse_group(p0, mis, n, m, my_start, batch_ord, out, out_cap, done, start, wr)) return wr;
     }
     wr.parsed = done;
     wr.trailing = n - start;
@@ -502,7 +532,7 @@ DEV Desc load_desc(const DeviceJob& j, uint64_t b) {
 }
 
 // CRC + (optional) walk of one stream; d/gt hold its first window and tail
-DEV uint32_t stream_crc_walk(const DeviceJob& j, const uint8_t* lds, const Keys& K, const Stream& st, uint4 (&d)[16],
+DEV uint32_t stream_crc_walk(const DeviceJob& j, const uint8_t* lds, const Keys& K, const Stream& st, Win& d,
                              const uint4& gt, uint32_t Tst, bool walk, const Desc& ds, uint64_t b, WalkResult& w,
                              bool& idx_ok) {
     STAMP(t0);
@@ -525,15 +555,15 @@ __global__ __launch_bounds__(1024) void k_validate(DeviceJob j) {
     const Tables* T = j.tables;
     const uint32_t tid = threadIdx.x;
     // braid tables: word i -> row-set rs = i >> 14, entry e = (i >> 6) & 255,
-    // slot = (i >> 5) & 1, copy = i & 31; (rs, slot) = (0,0) T15, (0,1) T14,
-    // (1,0) T13, (1,1) T12
+    // slot = (i >> 5) & 1, copy = i & 31; (rs, slot) = (0,0) T1023, (0,1)
+    // T1022, (1,0) T1021, (1,1) T1020
     for (uint32_t i = tid; i < 32768u; i += blockDim.x)
-        ((uint32_t*)(lds + kLdsBraidOff))[i] = T->hdr[15 - (((i >> 14) << 1) | ((i >> 5) & 1u))][(i >> 6) & 255u];
+        ((uint32_t*)(lds + kLdsBraidOff))[i] = T->braid[((i >> 14) << 1) | ((i >> 5) & 1u)][(i >> 6) & 255u];
     // slice tables: T3, T2, T1, T0
     for (uint32_t i = tid; i < 1024u; i += blockDim.x) ((uint32_t*)(lds + kLdsSlice4Off))[i] = T->hdr[3 - (i >> 8)][i & 255u];
-    // shift tables: comb[1..6] (256 .. 8192 bytes)
+    // shift tables: 16 << m bytes, m = 0..5
     for (uint32_t i = tid; i < kShiftLevels * 1024u; i += blockDim.x)
-        ((uint32_t*)(lds + kLdsShiftOff))[i] = ((const uint32_t*)T->comb[1])[i];
+        ((uint32_t*)(lds + kLdsShiftOff))[i] = ((const uint32_t*)T->shift)[i];
     __syncthreads();
 
     const uint32_t l = lane();
@@ -555,7 +585,13 @@ __global__ __launch_bounds__(1024) void k_validate(DeviceJob j) {
     STAMP(tk0);
     for (uint64_t b = (uint64_t)blockIdx.x * kVWaves + (tid >> 6); b < nb; b += nw) {
         rpgpu_batch_result* R = &j.batches[b];
+        STAMP(ta);
         const Desc d = load_desc(j, b);
+#ifdef RPGPU_STAMPS
+        { const uint32_t z = d.flags ^ d.crc; if (z == 0x9e3779b9u) g_stamps[7]++; }
+#endif
+        STAMP(tb);
+        STAMP_ADD(2, tb - ta);
         if (!(d.flags & RPGPU_F_COMPLETE)) {
             if (l == 0) { R->index_base = d.ib; R->decoded_off = d.doff; R->reserved1 = 0; }
             note_bad(j, d.seg, b);
@@ -571,8 +607,8 @@ __global__ __launch_bounds__(1024) void k_validate(DeviceJob j) {
             // after the BE40 prefix with init ~0 = c40 ^ the prefix's raw
             // contribution (computed by k_emit)
             const Stream st = make_stream(j.data, d.S, d.S + d.n);
-            uint4 v[16];
-            load_region(st, 0, v);  // unconditional: an array left undefined on one path is pinned in scratch
+            Win v;
+            load_window(st, 0, v);  // unconditional: a window left undefined on one path is pinned in scratch
             const uint4 gt = load_tail(st);
             walked = d.codec == 0 && (j.flags & RPGPU_JOB_PARSE);
             crc = stream_crc_walk(j, lds, K, st, v, gt, d.praw ^ c40, walked, d, b, w, idx_ok);
@@ -584,8 +620,8 @@ __global__ __launch_bounds__(1024) void k_validate(DeviceJob j) {
             // differs only in the codec bits of attrs (BE40 byte 1)
             const uint64_t dl = uni32(R->decoded_len);
             const Stream ds = make_stream(j.decoded, d.doff, d.doff + dl);
-            uint4 v[16];
-            load_region(ds, 0, v);
+            Win v;
+            load_window(ds, 0, v);
             const uint4 gt = load_tail(ds);
             walked = (j.flags & RPGPU_JOB_PARSE) != 0;
             dcrc = stream_crc_walk(j, lds, K, ds, v, gt, d.praw ^ T->hdr[38][d.codec] ^ c40, walked, d, b, w, idx_ok);
@@ -605,6 +641,7 @@ __global__ __launch_bounds__(1024) void k_validate(DeviceJob j) {
                 else { perr = RPGPU_PARSE_ERR_INDEX_CAPACITY; if (l == 0) atomicOr(&j.counters[1], 2u); }
             }
         }
+        STAMP(tc);
         if (l == 0) {
             R->crc_computed = crc;
             R->flags = f;
@@ -618,6 +655,8 @@ __global__ __launch_bounds__(1024) void k_validate(DeviceJob j) {
             }
             R->reserved1 = 0;
         }
+        STAMP(td);
+        STAMP_ADD(5, td - tc);
         STAMP_ADD(3, 1);
     }
     STAMP(tk1);
@@ -631,8 +670,8 @@ __global__ __launch_bounds__(1024) void k_validate(DeviceJob j) {
 #ifdef RPGPU_STAMPS
 __global__ void k_print_stamps() {
     const double n = (double)g_stamps[3];
-    printf("RPGPU_STAMPS batches=%.0f cycles/batch/wave: crc(+loads)=%.0f walk=%.0f total=%.0f\n", n,
-           g_stamps[0] / n, g_stamps[1] / n, g_stamps[4] / n);
+    printf("RPGPU_STAMPS batches=%.0f cycles/batch/wave: desc=%.0f crc(+loads)=%.0f walk=%.0f stores=%.0f total=%.0f\n",
+           n, g_stamps[2] / n, g_stamps[0] / n, g_stamps[1] / n, g_stamps[5] / n, g_stamps[4] / n);
     for (int i = 0; i < 8; i++) g_stamps[i] = 0;
 }
 #endif
