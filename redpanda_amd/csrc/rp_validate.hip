@@ -223,20 +223,21 @@ DEV uint32_t crc_stream(const uint8_t* lds, const Keys& K, const Stream& st, Win
 // Record walk
 // ---------------------------------------------------------------------------
 
-// 12 bytes at payload offset q (wave-uniform) through the scalar cache:
+// 16 bytes at payload offset q (wave-uniform) through the scalar cache:
 // the constant address space makes these s_load_dwordx4, which bypass the
 // vector-memory queue the window stream keeps full (and its in-order vmcnt).
 // The payload is read-only for the whole kernel.  Bytes past the payload are
 // whatever follows it (readable to a 16-byte boundary); callers bound every
 // use by the bytes available.
-DEV void s12(const uint8_t* p0, uint32_t q, uint32_t& r0, uint32_t& r1, uint32_t& r2) {
+DEV void s16(const uint8_t* p0, uint32_t q, uint32_t& r0, uint32_t& r1, uint32_t& r2, uint32_t& r3) {
     const uintptr_t a = (uintptr_t)(p0 + q);
     cu32* c = (cu32*)(a & ~(uintptr_t)3);
     const uint32_t sh = (uint32_t)(a & 3);
-    const uint32_t w0 = c[0], w1 = c[1], w2 = c[2], w3 = c[3];
+    const uint32_t w0 = c[0], w1 = c[1], w2 = c[2], w3 = c[3], w4 = c[4];
     r0 = __builtin_amdgcn_alignbyte(w1, w0, sh);
     r1 = __builtin_amdgcn_alignbyte(w2, w1, sh);
     r2 = __builtin_amdgcn_alignbyte(w3, w2, sh);
+    r3 = __builtin_amdgcn_alignbyte(w4, w3, sh);
 }
 
 // Per-lane 32-byte read cache over global memory (L2-resident payload).
@@ -306,17 +307,34 @@ struct Reader {
     uint32_t mis;       // p0 & 15
     uint32_t n;
     uint32_t pos;
+    uint32_t hs;        // payload offset of head (the 16 bytes the chain handed over)
+    uint4 head;
     GCache C;
 
-    // iobuf_parser_base::read_varlong (bytes/iobuf_parser.h:48-52)
+    DEV uint32_t head_dword(uint32_t k) const { return k < 4u ? pick4(head, k) : 0u; }
+
+    // iobuf_parser_base::read_varlong (bytes/iobuf_parser.h:48-52).  One- and
+    // two-byte varints inside the head are decoded without a load.
     DEV int64_t varlong() {
         uint32_t r0, r1, r2, br;
+        const uint32_t o = pos - hs;  // huge when pos < hs
+        const uint32_t avail = n - pos;
+        if (o <= 12u) {
+            r0 = __builtin_amdgcn_alignbyte(head_dword((o >> 2) + 1), head_dword(o >> 2), o & 3u);
+            if (avail < 2 || (r0 & 0x8080u) != 0x8080u) {
+                const int64_t x = varint12(r0, 0u, 0u, avail, br);
+                pos += br;
+                return x;
+            }
+        }
         gc12(p0, mis, n, C, pos, r0, r1, r2);
-        const int64_t x = varint12(r0, r1, r2, n - pos, br);
+        const int64_t x = varint12(r0, r1, r2, avail, br);
         pos += br;
         return x;
     }
     DEV uint32_t byte() {
+        const uint32_t o = pos - hs;
+        if (o <= 15u) return (head_dword(o >> 2) >> (8 * (o & 3u))) & 0xFFu;
         uint32_t r0, r1, r2;
         gc12(p0, mis, n, C, pos, r0, r1, r2);
         return r0 & 0xFFu;
@@ -345,13 +363,15 @@ struct Rec {
 // parse_one_record_copy_from_buffer (model/record_utils.cc:170-177) over
 // parse_record_meta_from_buffer / do_parse_one_record_from_buffer /
 // parse_record_headers (:94-160)
-DEV Rec parse_record(const uint8_t* p0, uint32_t mis, uint32_t n, uint32_t start) {
+DEV Rec parse_record(const uint8_t* p0, uint32_t mis, uint32_t n, uint32_t start, const uint4& head) {
     Rec r;
     Reader c;
     c.p0 = p0;
     c.mis = mis;
     c.n = n;
     c.pos = start;
+    c.hs = start;
+    c.head = head;
     c.C.base = 0xFFFFFFF0u;
     r.err = 0;
     r.key_pos = r.val_pos = r.hdr_pos = 0;
@@ -397,17 +417,21 @@ struct WalkResult {
 
 // Speculative record starts for records [done, done + want): a uniform chain
 // over the length varints from `start` (scalar loads).  Lane m gets the
-// start of record done + m; returns how many lanes got one.
-DEV uint32_t chain_starts(const uint8_t* p0, uint32_t n, uint32_t start, uint32_t want, uint32_t& my_start) {
+// start of record done + m and the 16 bytes there (its parse starts from
+// them); returns how many lanes got one.
+DEV uint32_t chain_starts(const uint8_t* p0, uint32_t n, uint32_t start, uint32_t want, uint32_t& my_start,
+                          uint4& head) {
     const uint32_t l = lane();
     my_start = 0xFFFFFFFFu;
+    head = make_uint4(0u, 0u, 0u, 0u);
     uint32_t p = start;
     uint32_t m = 0;
     for (; m < want; m++) {
         if (l == m) my_start = p;
         if (p >= n) { m++; break; }
-        uint32_t r0, r1, r2, br;
-        s12(p0, p, r0, r1, r2);
+        uint32_t r0, r1, r2, r3, br;
+        s16(p0, p, r0, r1, r2, r3);
+        if (l == m) head = make_uint4(r0, r1, r2, r3);
         const int64_t len = varint12(r0, r1, r2, n - p, br);
         if (len < 0 || (uint64_t)len > n) { m++; break; }
         p = uni32(p + br + (uint32_t)len);
@@ -418,12 +442,13 @@ DEV uint32_t chain_starts(const uint8_t* p0, uint32_t n, uint32_t start, uint32_
 // Lanes [0, m) parse one record each from their speculative starts; the
 // prefix whose starts are confirmed by the previous record's exact end is
 // committed to the index.  Returns false when a record failed (wr filled).
-DEV bool parse_group(const uint8_t* p0, uint32_t mis, uint32_t n, uint32_t m, uint32_t my_start, uint32_t batch_ord,
+DEV bool parse_group(const uint8_t* p0, uint32_t mis, uint32_t n, uint32_t m, uint32_t my_start, const uint4& head,
+                     uint32_t batch_ord,
                      rpgpu_record_index* out, uint64_t out_cap, uint32_t& done, uint32_t& start, WalkResult& wr) {
     const uint32_t l = lane();
     Rec r;
     const bool act = l < m;
-    if (act) r = parse_record(p0, mis, n, my_start);
+    if (act) r = parse_record(p0, mis, n, my_start, head);
     else { r.err = 0; r.end = 0xFFFFFFFFu; }
     const uint32_t prev_end = __shfl_up(r.end, 1, 64);
     const uint32_t prev_err = __shfl_up(r.err, 1, 64);
@@ -475,9 +500,13 @@ DEV WalkResult walk_records(const uint8_t* p0, uint32_t n, int32_t rc, uint32_t 
     uint32_t start = 0, done = 0;
     while (done < total) {
         uint32_t my_start;
+        uint4 head;
         const uint32_t want = (total - done) < 64u ? (total - done) : 64u;
-        const uint32_t m = chain_starts(p0, n, start, want, my_start);
-        if (!parse_group(p0, mis, n, m, my_start, batch_ord, out, out_cap, done, start, wr)) return wr;
+        STAMP(w0);
+        const uint32_t m = chain_starts(p0, n, start, want, my_start, head);
+        STAMP(w1);
+        STAMP_ADD(6, w1 - w0);
+        if (!parse_group(p0, mis, n, m, my_start, head, batch_ord, out, out_cap, done, start, wr)) return wr;
     }
     wr.parsed = done;
     wr.trailing = n - start;
@@ -670,8 +699,9 @@ __global__ __launch_bounds__(1024) void k_validate(DeviceJob j) {
 #ifdef RPGPU_STAMPS
 __global__ void k_print_stamps() {
     const double n = (double)g_stamps[3];
-    printf("RPGPU_STAMPS batches=%.0f cycles/batch/wave: desc=%.0f crc(+loads)=%.0f walk=%.0f stores=%.0f total=%.0f\n",
-           n, g_stamps[2] / n, g_stamps[0] / n, g_stamps[1] / n, g_stamps[5] / n, g_stamps[4] / n);
+    printf("RPGPU_STAMPS batches=%.0f cycles/batch/wave: desc=%.0f crc(+loads)=%.0f walk=%.0f (chain %.0f) stores=%.0f "
+           "total=%.0f\n",
+           n, g_stamps[2] / n, g_stamps[0] / n, g_stamps[1] / n, g_stamps[6] / n, g_stamps[5] / n, g_stamps[4] / n);
     for (int i = 0; i < 8; i++) g_stamps[i] = 0;
 }
 #endif
