@@ -114,6 +114,7 @@ def main():
     import torch.distributed as dist
     from redpanda_amd import abi
     from redpanda_amd.engine import Engine
+    from redpanda_amd.shard import as_bytes, gather_bytes, gather_job_verdicts, partitions_for_rank
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -124,7 +125,7 @@ def main():
     torch.cuda.set_device(device)
 
     seg_bytes = int(args.seg_gib * (1 << 30)) // BATCH_BYTES * BATCH_BYTES
-    parts = [p for p in range(args.partitions * world) if p % world == rank]
+    parts = partitions_for_rank(args.partitions * world, world, rank)
     t0 = time.time()
     data, offs, counts, host_first = gen_partitions(parts, seg_bytes, BATCH_BYTES, torch, device)
     n_batches = int(sum(counts))
@@ -145,11 +146,7 @@ def main():
             if args.gather == "index":
                 payload.append(out.batches)
             for t in payload:
-                if rank == 0:
-                    bufs = [torch.empty_like(t) for _ in range(world)]
-                    dist.gather(t, bufs, dst=0)
-                else:
-                    dist.gather(t, None, dst=0)
+                gather_bytes(as_bytes(t), rank, world, dist)
 
     for _ in range(args.warmup):
         step()
@@ -161,6 +158,12 @@ def main():
                   and np.all(h.batches["flags"] & abi.F_CRC_OK) and h.totals["overflow"] == 0)
     bm_ok = bool(np.all(h.bitmap[: nb // 64] == np.uint64(0xFFFFFFFFFFFFFFFF)))
     n_records = int(h.totals["n_records"])
+    if world > 1:
+        # the gathered job picture on rank 0: every partition checkpointed at its end
+        g = gather_job_verdicts(out.summaries, out.bitmap, nb, parts, rank, world, dist)
+        if rank == 0:
+            all_ok = bool(all_ok and np.all(g["summaries"]["has_checkpoint"] == 1)
+                          and np.all(g["summaries"]["first_bad"] == g["summaries"]["n_batches"]))
     payload_bytes = int(np.sum(h.batches["size_bytes"].astype(np.int64) - abi.HEADER_SIZE))
     seg_total = int(np.sum(h.batches["size_bytes"].astype(np.int64)))
     del h

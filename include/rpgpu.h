@@ -270,7 +270,8 @@ int rpgpu_submit(rpgpu_ctx* ctx, const rpgpu_job* job, void* stream);
 /* Device time of the pipeline stages, measured with HIP events recorded on
  * the launch stream, averaged over every timed rpgpu_submit since the
  * previous call (milliseconds; the call resets the average).  Indices:
- * 0 = whole pipeline, 1 = discover, 2 = resolve+emit+plan, 3 = validate. */
+ * 0 = whole pipeline, 1 = discover, 2 = resolve+emit+plan, 3 = validate,
+ * 4 = decode (0 when the job has no RPGPU_JOB_DECODE). */
 int rpgpu_last_timings(rpgpu_ctx* ctx, float* ms, int n);
 /* Enable/disable per-kernel event timing (off by default). */
 int rpgpu_set_timing(rpgpu_ctx* ctx, int enable);

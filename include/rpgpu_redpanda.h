@@ -1,0 +1,517 @@
+/*
+ * rpgpu_redpanda.h — the reference's hot-path surfaces, re-declared in C++17
+ * over the C-ABI in rpgpu.h, so a caller of Redpanda's batch path swaps the
+ * include and keeps its code:
+ *
+ *   crc::crc32c                           hashing/crc32c.h:19-40
+ *   model::record_batch_attributes        model/record.h:255-351
+ *   model::record_batch_header            model/record.h:354-417
+ *   model::internal_header_only_crc,
+ *   model::crc_record_batch_header,
+ *   model::crc_record_batch               model/record_utils.h:23-35 (.cc:34-91)
+ *   storage::parser_errc                  storage/parser_errc.h:18-25
+ *   storage::batch_consumer               storage/parser.h:32-87
+ *   storage::continuous_batch_parser      storage/parser.h:94-136 (parser.cc:96-254)
+ *   storage::log_replayer                 storage/log_replayer.h/.cc:27-114
+ *   compression::compressor::uncompress   compression/compression.h:21-24
+ *
+ * Differences forced by leaving Seastar: futures become synchronous calls,
+ * ss::input_stream becomes a byte span of a whole segment, iobuf a
+ * contiguous byte buffer.  The parser validates the whole segment on the GPU
+ * in one rpgpu_submit, then replays the per-batch verdicts into the consumer
+ * in chain order, so accept / skip / stop decisions and byte accounting
+ * follow continuous_batch_parser::consume exactly.  No exception crosses the
+ * C-ABI; these wrappers rethrow where the reference throws.
+ */
+#ifndef RPGPU_REDPANDA_H_
+#define RPGPU_REDPANDA_H_
+
+#include <cstddef>
+#include <cstdint>
+#include <cstring>
+#include <memory>
+#include <optional>
+#include <ostream>
+#include <stdexcept>
+#include <string>
+#include <type_traits>
+#include <vector>
+
+#include "rpgpu.h"
+
+namespace rpgpu {
+
+// Contiguous byte buffer standing in for iobuf (bytes/iobuf.h).
+class iobuf {
+public:
+    iobuf() = default;
+    iobuf(const uint8_t* p, size_t n) : _b(p, p + n) {}
+    explicit iobuf(std::vector<uint8_t> b) : _b(std::move(b)) {}
+    size_t size_bytes() const { return _b.size(); }
+    bool empty() const { return _b.empty(); }
+    const uint8_t* data() const { return _b.data(); }
+    uint8_t* data() { return _b.data(); }
+    const std::vector<uint8_t>& bytes() const { return _b; }
+
+private:
+    std::vector<uint8_t> _b;
+};
+
+// One rpgpu context (HIP stream + device scratch) on one device; one per
+// host thread / shard, as the reference's shard-per-core ownership requires.
+class engine {
+public:
+    explicit engine(int device = 0) {
+        const int rc = rpgpu_create(device, &_ctx);
+        if (rc != RPGPU_OK) throw std::runtime_error(std::string("rpgpu_create: ") + rpgpu_strerror(rc));
+    }
+    engine(const engine&) = delete;
+    engine& operator=(const engine&) = delete;
+    ~engine() {
+        if (_ctx) rpgpu_destroy(_ctx);
+    }
+    rpgpu_ctx* ctx() const { return _ctx; }
+    void check(int rc, const char* what) const {
+        if (rc != RPGPU_OK)
+            throw std::runtime_error(std::string(what) + ": " + rpgpu_strerror(rc) + " (" + rpgpu_last_error(_ctx) + ")");
+    }
+
+    // The engine used by the surfaces below when none is passed explicitly.
+    static engine& local() {
+        thread_local engine e(0);
+        return e;
+    }
+
+private:
+    rpgpu_ctx* _ctx = nullptr;
+};
+
+// RAII device buffer
+class dev_buffer {
+public:
+    dev_buffer(engine& e, size_t bytes) : _e(e) { _e.check(rpgpu_dev_alloc(_e.ctx(), bytes, &_p), "rpgpu_dev_alloc"); }
+    dev_buffer(const dev_buffer&) = delete;
+    dev_buffer& operator=(const dev_buffer&) = delete;
+    ~dev_buffer() {
+        if (_p) rpgpu_dev_free(_e.ctx(), _p);
+    }
+    void* get() const { return _p; }
+
+private:
+    engine& _e;
+    void* _p = nullptr;
+};
+
+}  // namespace rpgpu
+
+// ---------------------------------------------------------------------------
+// crc::crc32c — hashing/crc32c.h:19-40 (google crc32c::Extend semantics)
+// ---------------------------------------------------------------------------
+namespace crc {
+class crc32c {
+public:
+    template <typename T, typename = std::enable_if_t<std::is_integral_v<T>, T>>
+    void extend(T num) noexcept {
+        extend(reinterpret_cast<const uint8_t*>(&num), sizeof(T));
+    }
+    void extend(const uint8_t* data, size_t size) { _crc = rpgpu_crc32c_extend(_crc, data, size); }
+    void extend(const char* data, size_t size) { extend(reinterpret_cast<const uint8_t*>(data), size); }
+    uint32_t value() const { return _crc; }
+
+private:
+    uint32_t _crc = 0;
+};
+}  // namespace crc
+
+// ---------------------------------------------------------------------------
+// model — record batch types and CRC helpers
+// ---------------------------------------------------------------------------
+namespace model {
+
+// model/compression.h:35-48
+enum class compression : uint8_t { none = 0, gzip = 1, snappy = 2, lz4 = 3, zstd = 4 };
+
+// model/record.h:255-351
+class record_batch_attributes final {
+public:
+    static constexpr uint16_t compression_mask = 0x7;
+    static constexpr uint16_t timestamp_type_mask = 0x8;
+    static constexpr uint16_t transactional_mask = 0x10;
+    static constexpr uint16_t control_mask = 0x20;
+    using type = int16_t;
+
+    record_batch_attributes() noexcept = default;
+    explicit record_batch_attributes(type v) noexcept : _a((uint16_t)v) {}
+    type value() const { return (type)_a; }
+    bool is_control() const { return _a & control_mask; }
+    bool is_transactional() const { return _a & transactional_mask; }
+    bool is_valid_compression() const { return (_a & compression_mask) <= 4; }
+    // throws for codec values 5..7, as the reference does
+    model::compression compression() const {
+        const uint16_t v = _a & compression_mask;
+        if (v > 4) throw std::runtime_error("Unknown compression value: " + std::to_string(v));
+        return (model::compression)v;
+    }
+    void remove_compression() { _a &= (uint16_t)~compression_mask; }
+    record_batch_attributes& operator|=(model::compression c) {
+        _a |= (uint16_t)((uint16_t)c & compression_mask);
+        return *this;
+    }
+    bool operator==(const record_batch_attributes& o) const { return _a == o._a; }
+    bool operator!=(const record_batch_attributes& o) const { return _a != o._a; }
+
+private:
+    uint16_t _a = 0;
+};
+
+// model/record.h:473-487 (the comment there says 57; the fields sum to 61)
+constexpr size_t packed_record_batch_header_size = RPGPU_HEADER_SIZE;
+
+// model/record.h:354-417 (context fields dropped: not serialized)
+struct record_batch_header {
+    uint32_t header_crc{0};
+    int32_t size_bytes{0};
+    int64_t base_offset{0};
+    int8_t type{0};
+    int32_t crc{0};
+    record_batch_attributes attrs;
+    int32_t last_offset_delta{0};
+    int64_t first_timestamp{0};
+    int64_t max_timestamp{0};
+    int64_t producer_id{0};
+    int16_t producer_epoch{0};
+    int32_t base_sequence{0};
+    int32_t record_count{0};
+
+    int64_t last_offset() const { return base_offset + last_offset_delta; }
+    bool operator==(const record_batch_header& o) const {
+        return size_bytes == o.size_bytes && base_offset == o.base_offset && crc == o.crc && attrs == o.attrs &&
+               last_offset_delta == o.last_offset_delta && first_timestamp == o.first_timestamp &&
+               max_timestamp == o.max_timestamp && record_count == o.record_count;
+    }
+    bool operator!=(const record_batch_header& o) const { return !(*this == o); }
+
+    // from an engine verdict (the fields storage::header_from_iobuf decodes)
+    static record_batch_header from(const rpgpu_batch_result& r) {
+        record_batch_header h;
+        h.header_crc = r.header_crc;
+        h.size_bytes = r.size_bytes;
+        h.base_offset = r.base_offset;
+        h.type = r.type;
+        h.crc = (int32_t)r.crc;
+        h.attrs = record_batch_attributes(r.attrs);
+        h.last_offset_delta = r.last_offset_delta;
+        h.first_timestamp = r.first_timestamp;
+        h.max_timestamp = r.max_timestamp;
+        h.producer_id = r.producer_id;
+        h.producer_epoch = r.producer_epoch;
+        h.base_sequence = r.base_sequence;
+        h.record_count = r.record_count;
+        return h;
+    }
+};
+
+namespace detail {
+template <typename T>
+inline void put_be(uint8_t*& p, T v) {
+    using U = std::make_unsigned_t<T>;
+    U u = (U)v;
+    for (int i = (int)sizeof(T) - 1; i >= 0; i--) *p++ = (uint8_t)(u >> (8 * i));
+}
+}  // namespace detail
+
+// model/record_utils.cc:34-55: fields hashed in native (little-endian) order
+inline uint32_t internal_header_only_crc(const record_batch_header& h) {
+    crc::crc32c c;
+    c.extend(h.size_bytes);
+    c.extend(h.base_offset);
+    c.extend(h.type);
+    c.extend(h.crc);
+    c.extend(h.attrs.value());
+    c.extend(h.last_offset_delta);
+    c.extend(h.first_timestamp);
+    c.extend(h.max_timestamp);
+    c.extend(h.producer_id);
+    c.extend(h.producer_epoch);
+    c.extend(h.base_sequence);
+    c.extend(h.record_count);
+    return c.value();
+}
+
+// model/record_utils.cc:68-80: the Kafka crc prefix, big-endian
+inline void crc_record_batch_header(crc::crc32c& c, const record_batch_header& h) {
+    uint8_t b[RPGPU_CRC_PREFIX_SIZE];
+    uint8_t* p = b;
+    detail::put_be(p, h.attrs.value());
+    detail::put_be(p, h.last_offset_delta);
+    detail::put_be(p, h.first_timestamp);
+    detail::put_be(p, h.max_timestamp);
+    detail::put_be(p, h.producer_id);
+    detail::put_be(p, h.producer_epoch);
+    detail::put_be(p, h.base_sequence);
+    detail::put_be(p, h.record_count);
+    c.extend(b, sizeof b);
+}
+
+// model/record_utils.cc:82-91
+inline int32_t crc_record_batch(const record_batch_header& h, const rpgpu::iobuf& records) {
+    crc::crc32c c;
+    crc_record_batch_header(c, h);
+    c.extend(records.data(), records.size_bytes());
+    return (int32_t)c.value();
+}
+
+}  // namespace model
+
+// ---------------------------------------------------------------------------
+// compression::compressor::uncompress — compression/compression.h:21-24
+// (lz4 and snappy decoded on the GPU; throws std::runtime_error where the
+// reference throws; gzip/zstd are not decoded by this engine)
+// ---------------------------------------------------------------------------
+namespace compression {
+using type = model::compression;
+struct compressor {
+    static rpgpu::iobuf uncompress(const rpgpu::iobuf& in, type t, rpgpu::engine& e = rpgpu::engine::local()) {
+        size_t cap = in.size_bytes() * 8 + 4096, got = 0;
+        for (;;) {
+            std::vector<uint8_t> out(cap);
+            const int rc = rpgpu_uncompress(e.ctx(), (int)t, in.data(), in.size_bytes(), out.data(), cap, &got);
+            if (rc == RPGPU_OK) {
+                out.resize(got);
+                return rpgpu::iobuf(std::move(out));
+            }
+            if (rc == RPGPU_E_OVERFLOW && got > cap) {
+                cap = got;
+                continue;
+            }
+            if (rc == RPGPU_E_UNSUPPORTED) throw std::logic_error(rpgpu_last_error(e.ctx()));
+            throw std::runtime_error(rpgpu_last_error(e.ctx()));
+        }
+    }
+};
+}  // namespace compression
+
+// ---------------------------------------------------------------------------
+// storage — parser surfaces
+// ---------------------------------------------------------------------------
+namespace storage {
+
+// storage/parser_errc.h:18-25
+enum class parser_errc : int {
+    none = RPGPU_ERRC_NONE,
+    end_of_stream = RPGPU_ERRC_END_OF_STREAM,
+    header_only_crc_missmatch = RPGPU_ERRC_HEADER_ONLY_CRC_MISSMATCH,
+    input_stream_not_enough_bytes = RPGPU_ERRC_INPUT_STREAM_NOT_ENOUGH_BYTES,
+    fallocated_file_read_zero_bytes_for_header = RPGPU_ERRC_FALLOCATED_FILE_READ_ZERO_BYTES_FOR_HEADER,
+    not_enough_bytes_in_parser_for_one_record = RPGPU_ERRC_NOT_ENOUGH_BYTES_IN_PARSER_FOR_ONE_RECORD,
+};
+
+// outcome::result<size_t, parser_errc>
+struct parse_result {
+    size_t value{0};
+    std::optional<parser_errc> error;
+    explicit operator bool() const { return !error.has_value(); }
+};
+
+// storage/parser.h:32-87
+class batch_consumer {
+public:
+    using stop_parser = bool;  // ss::bool_class<stop_parser_tag>
+    enum class consume_result : int8_t { accept_batch, stop_parser, skip_batch };
+
+    batch_consumer() noexcept = default;
+    virtual ~batch_consumer() noexcept = default;
+    virtual consume_result accept_batch_start(const model::record_batch_header&) const = 0;
+    virtual void consume_batch_start(model::record_batch_header, size_t physical_base_offset, size_t size_on_disk) = 0;
+    virtual void skip_batch_start(model::record_batch_header, size_t physical_base_offset, size_t size_on_disk) = 0;
+    virtual void consume_records(rpgpu::iobuf&&) = 0;
+    virtual stop_parser consume_batch_end() = 0;
+    virtual void print(std::ostream&) const = 0;
+};
+
+inline std::ostream& operator<<(std::ostream& os, const batch_consumer& c) {
+    c.print(os);
+    return os;
+}
+
+namespace detail {
+// One disk-layout segment validated on the GPU (chain discovery, header_crc,
+// batch crc): the per-batch verdicts in chain order and the segment summary.
+struct segment_scan {
+    std::vector<rpgpu_batch_result> batches;
+    rpgpu_segment_summary summary{};
+};
+
+inline segment_scan scan_segment(rpgpu::engine& e, const uint8_t* seg, size_t len) {
+    segment_scan out;
+    const size_t cap = len / RPGPU_HEADER_SIZE + 2;
+    const size_t padded = ((len + 15) / 16 + 1) * 16;
+    rpgpu::dev_buffer d_data(e, padded), d_offs(e, 16), d_b(e, cap * sizeof(rpgpu_batch_result)),
+        d_s(e, sizeof(rpgpu_segment_summary)), d_t(e, sizeof(rpgpu_job_totals));
+    const uint64_t offs[2] = {0, (uint64_t)len};
+    e.check(rpgpu_memset(e.ctx(), d_data.get(), 0, padded, nullptr), "rpgpu_memset");
+    if (len) e.check(rpgpu_memcpy_h2d(e.ctx(), d_data.get(), seg, len, nullptr), "rpgpu_memcpy_h2d");
+    e.check(rpgpu_memcpy_h2d(e.ctx(), d_offs.get(), offs, sizeof offs, nullptr), "rpgpu_memcpy_h2d");
+    rpgpu_job j{};
+    j.d_data = (const uint8_t*)d_data.get();
+    j.d_seg_offsets = (const uint64_t*)d_offs.get();
+    j.h_seg_offsets = offs;
+    j.n_segments = 1;
+    j.layout = RPGPU_LAYOUT_DISK;
+    j.flags = RPGPU_JOB_CRC;
+    j.d_batches = (rpgpu_batch_result*)d_b.get();
+    j.batch_capacity = cap;
+    j.d_summaries = (rpgpu_segment_summary*)d_s.get();
+    j.d_totals = (rpgpu_job_totals*)d_t.get();
+    e.check(rpgpu_submit(e.ctx(), &j, nullptr), "rpgpu_submit");
+    rpgpu_job_totals t{};
+    e.check(rpgpu_memcpy_d2h(e.ctx(), &t, d_t.get(), sizeof t, nullptr), "rpgpu_memcpy_d2h");
+    e.check(rpgpu_memcpy_d2h(e.ctx(), &out.summary, d_s.get(), sizeof out.summary, nullptr), "rpgpu_memcpy_d2h");
+    e.check(rpgpu_sync(e.ctx(), nullptr), "rpgpu_sync");
+    out.batches.resize((size_t)t.n_batches);
+    if (t.n_batches)
+        e.check(rpgpu_memcpy_d2h(e.ctx(), out.batches.data(), d_b.get(), t.n_batches * sizeof(rpgpu_batch_result), nullptr),
+                "rpgpu_memcpy_d2h");
+    e.check(rpgpu_sync(e.ctx(), nullptr), "rpgpu_sync");
+    return out;
+}
+}  // namespace detail
+
+// storage/parser.h:94-136.  The input stream is one whole segment in host
+// memory (a file's bytes from position 0, as log_replayer reads it).
+class continuous_batch_parser {
+public:
+    continuous_batch_parser(std::unique_ptr<batch_consumer> consumer, const uint8_t* segment, size_t len,
+                            rpgpu::engine& e = rpgpu::engine::local()) noexcept
+      : _consumer(std::move(consumer)), _seg(segment), _len(len), _e(e) {}
+    continuous_batch_parser(const continuous_batch_parser&) = delete;
+    continuous_batch_parser& operator=(const continuous_batch_parser&) = delete;
+
+    // continuous_batch_parser::consume (storage/parser.cc:218-254) over the
+    // GPU's verdicts.  The segment is validated on the first call; later
+    // calls resume where the previous one stopped.
+    parse_result consume() {
+        if (_err != parser_errc::none) return {0, _err};
+        if (!_scan) _scan = detail::scan_segment(_e, _seg, _len);
+        for (;;) {
+            const step s = consume_one();
+            if (_eof) break;
+            if (s.err != parser_errc::none) {
+                _err = s.err;
+                break;
+            }
+            if (s.stop) break;
+        }
+        if (_bytes_consumed) return {_bytes_consumed, std::nullopt};  // partial reads
+        if (_err == parser_errc::none || _err == parser_errc::end_of_stream ||
+            _err == parser_errc::fallocated_file_read_zero_bytes_for_header)
+            return {_bytes_consumed, std::nullopt};
+        return {0, _err};
+    }
+
+    void close() {}
+
+private:
+    struct step {
+        parser_errc err = parser_errc::none;
+        bool stop = false;
+    };
+
+    // consume_one (storage/parser.cc:178-190) = consume_header + consume_records
+    step consume_one() {
+        const detail::segment_scan& sc = *_scan;
+        for (;;) {
+            if (!_pending) {
+                // read_header_impl (storage/parser.cc:139-176): the chain's
+                // next header, or the verdict that ended the chain.  A read
+                // past the end of the data is an empty read: end_of_stream.
+                if (_i >= sc.batches.size()) {
+                    if (_eof) return {parser_errc::end_of_stream, false};
+                    if (sc.summary.terminal_eof) _eof = true;
+                    return {(parser_errc)sc.summary.terminal_errc, false};
+                }
+                _pending = true;
+            }
+            const rpgpu_batch_result& r = sc.batches[_i];
+            const model::record_batch_header h = model::record_batch_header::from(r);
+            const bool complete = (r.flags & RPGPU_F_COMPLETE) != 0;
+            const size_t size = (size_t)(int64_t)h.size_bytes;
+            switch (_consumer->accept_batch_start(h)) {
+            case batch_consumer::consume_result::stop_parser:
+                return {parser_errc::none, true};  // the header stays pending
+            case batch_consumer::consume_result::skip_batch:
+                _consumer->skip_batch_start(h, _physical_base_offset, size);
+                _physical_base_offset += size;
+                // verify_read_iobuf: a short read sets eof and returns before
+                // add_bytes_and_reset, so the header stays pending
+                if (!complete) {
+                    _eof = true;
+                    return {parser_errc::input_stream_not_enough_bytes, false};
+                }
+                add_bytes_and_reset(size);
+                continue;
+            case batch_consumer::consume_result::accept_batch:
+                break;
+            }
+            _consumer->consume_batch_start(h, _physical_base_offset, size);
+            _physical_base_offset += size;
+            // consume_records: add_bytes_and_reset runs whether or not the
+            // payload could be read
+            step out;
+            if (!complete) {
+                _eof = true;
+                out.err = parser_errc::input_stream_not_enough_bytes;
+            } else {
+                const uint8_t* payload = _seg + r.file_pos + RPGPU_HEADER_SIZE;
+                _consumer->consume_records(
+                  rpgpu::iobuf(payload, (uint32_t)(r.size_bytes - (int32_t)RPGPU_HEADER_SIZE)));
+                out.stop = _consumer->consume_batch_end();
+            }
+            add_bytes_and_reset(size);
+            return out;
+        }
+    }
+
+    void add_bytes_and_reset(size_t size) {
+        _bytes_consumed += size;
+        _pending = false;
+        _i++;
+    }
+
+    std::unique_ptr<batch_consumer> _consumer;
+    const uint8_t* _seg;
+    size_t _len;
+    rpgpu::engine& _e;
+    std::optional<detail::segment_scan> _scan;
+    size_t _i = 0;         // chain ordinal of the next (or pending) header
+    bool _pending = false; // _header is set
+    bool _eof = false;     // _input.eof()
+    parser_errc _err = parser_errc::none;
+    size_t _bytes_consumed{0};
+    size_t _physical_base_offset{0};
+};
+
+// storage/log_replayer.h:159-165 + log_replayer.cc:95-114: recover a segment
+// from file position 0; the checkpoint is the last batch whose crc matched
+// before the first one that did not.  Computed on the GPU in one submit.
+class log_replayer {
+public:
+    struct checkpoint {
+        std::optional<int64_t> last_offset;
+        std::optional<size_t> truncate_file_pos;
+    };
+
+    static checkpoint recover(const uint8_t* segment, size_t len, rpgpu::engine& e = rpgpu::engine::local()) {
+        const detail::segment_scan sc = detail::scan_segment(e, segment, len);
+        checkpoint c;
+        if (sc.summary.has_checkpoint) {
+            c.last_offset = sc.summary.ckpt_last_offset;
+            c.truncate_file_pos = (size_t)sc.summary.ckpt_truncate_pos;
+        }
+        return c;
+    }
+};
+
+}  // namespace storage
+
+#endif  // RPGPU_REDPANDA_H_

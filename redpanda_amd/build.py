@@ -90,6 +90,23 @@ def build(force: bool = False, verbose: bool = False, checked: bool = False, var
     return out
 
 
+SURFACES_SRC = os.path.join(ROOT, "tests", "cpp", "surfaces_main.cpp")
+SURFACES_BIN = os.path.join(ROOT, "tests", "cpp", "_bin", "surfaces_test")
+
+
+def build_surfaces_test(force: bool = False) -> str:
+    """Host-only driver of include/rpgpu_redpanda.h (the C++ drop-in
+    surfaces), linked against librpgpu.so by a relative runpath so the built
+    binary travels with the tree."""
+    lib = build()
+    hdrs = [os.path.join(INC, "rpgpu.h"), os.path.join(INC, "rpgpu_redpanda.h")]
+    if force or _stale(SURFACES_BIN, [SURFACES_SRC, lib] + hdrs):
+        os.makedirs(os.path.dirname(SURFACES_BIN), exist_ok=True)
+        _run(["g++", "-O2", "-std=c++17", "-Wall", "-Wextra", "-I", INC, SURFACES_SRC, "-o", SURFACES_BIN, "-L", HERE, "-l:librpgpu.so",
+              "-Wl,-rpath,$ORIGIN/../../../redpanda_amd"])
+    return SURFACES_BIN
+
+
 if __name__ == "__main__":
     v = "checked" if "--checked" in sys.argv else "stamps" if "--stamps" in sys.argv else ""
     print(build(force="--force" in sys.argv, verbose=True, variant=v))

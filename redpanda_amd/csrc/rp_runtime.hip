@@ -415,9 +415,12 @@ int rpgpu_uncompress(rpgpu_ctx* c, int codec, const void* in, size_t n, void* ou
     if (!c || (!in && n) || !out_len) return RPGPU_E_INVALID;
     *out_len = 0;
     if (codec < 0 || codec > RPGPU_CODEC_ZSTD) return fail(c, RPGPU_E_INVALID, "rpgpu_uncompress: unknown codec");
+    // compressor::uncompress (compression/compression.cc:34-53): an empty
+    // buffer throws before the codec dispatch
+    if (n == 0) return fail(c, RPGPU_E_CODEC, "rpgpu_uncompress: asked to decompress an empty buffer");
+    if (codec == RPGPU_CODEC_NONE) return fail(c, RPGPU_E_CODEC, "compressor: nothing to uncompress for 'none'");
     if (codec == RPGPU_CODEC_GZIP || codec == RPGPU_CODEC_ZSTD)
         return fail(c, RPGPU_E_UNSUPPORTED, "rpgpu_uncompress: gzip/zstd are not decoded by the engine");
-    if (n == 0 || codec == RPGPU_CODEC_NONE) return fail(c, RPGPU_E_CODEC, "rpgpu_uncompress: empty input or codec none");
     hipSetDevice(c->device);
     const uint64_t dcap = decode_capacity_dev(codec, (const uint8_t*)in, n);
     const size_t in_sz = align_up(n + 16, 256), out_sz = align_up(dcap + 16, 256);

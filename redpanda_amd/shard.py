@@ -1,0 +1,85 @@
+"""Multi-GPU sharding of a recovery / validation job.
+
+Partitions are independent: partition p is owned by rank p % world (the
+reference's shard-per-core ownership, cluster/partition_manager, lifted to
+one process per GPU).  Each rank validates its own segments with no
+data-path collective; the one exchange is a gather of the per-segment
+summaries (checkpoints) and validity bitmaps to rank 0, where a caller such
+as log recovery wants the whole job's picture.
+
+Everything here takes `dist` (torch.distributed) and works with the nccl
+(RCCL) backend on device tensors and with gloo on host tensors.
+"""
+from __future__ import annotations
+
+from typing import List, Sequence
+
+import numpy as np
+
+
+def partitions_for_rank(n_partitions: int, world: int, rank: int) -> List[int]:
+    """Global partition ids owned by `rank` (p % world == rank)."""
+    if not (0 <= rank < world):
+        raise ValueError(f"rank {rank} outside world {world}")
+    return [p for p in range(n_partitions) if p % world == rank]
+
+
+def gather_bytes(t, rank: int, world: int, dist, dst: int = 0):
+    """Gather a 1-D uint8 tensor of any per-rank length to `dst`.  Returns the
+    list of per-rank tensors on dst, None elsewhere.  One small all_gather of
+    the lengths, then one gather of equal-size (padded) buffers."""
+    import torch
+    n = torch.tensor([t.numel()], dtype=torch.int64, device=t.device)
+    sizes = [torch.zeros_like(n) for _ in range(world)]
+    dist.all_gather(sizes, n)
+    sizes = [int(s.item()) for s in sizes]
+    m = max(sizes) if sizes else 0
+    buf = t
+    if t.numel() < m:
+        buf = torch.zeros(m, dtype=t.dtype, device=t.device)
+        buf[: t.numel()] = t
+    if m == 0:
+        return [t[:0] for _ in range(world)] if rank == dst else None
+    if rank == dst:
+        bufs = [torch.empty(m, dtype=t.dtype, device=t.device) for _ in range(world)]
+        dist.gather(buf, bufs, dst=dst)
+        return [b[:s] for b, s in zip(bufs, sizes)]
+    dist.gather(buf, None, dst=dst)
+    return None
+
+
+def as_bytes(t):
+    """View a contiguous tensor as flat uint8 (the gather payload)."""
+    import torch
+    return t.contiguous().view(torch.uint8).reshape(-1)
+
+
+def gather_job_verdicts(summaries, bitmap, n_batches: int, parts: Sequence[int], rank: int, world: int, dist):
+    """Gather each rank's segment summaries (rpgpu_segment_summary[len(parts)])
+    and its validity bitmap (first n_batches bits) to rank 0.
+
+    Returns on rank 0 a dict with `summaries`: a numpy structured array of
+    all partitions in global partition order, and `bitmaps`: {partition
+    rank's parts tuple: bits} per rank; None on other ranks."""
+    import torch
+    from . import abi
+    meta = torch.tensor(list(parts) + [n_batches], dtype=torch.int64, device=summaries.device)
+    got_meta = gather_bytes(as_bytes(meta), rank, world, dist)
+    got_s = gather_bytes(as_bytes(summaries), rank, world, dist)
+    got_b = gather_bytes(as_bytes(bitmap), rank, world, dist)
+    if rank != 0:
+        return None
+    total = sum(len(m.cpu().numpy().view(np.int64)) - 1 for m in got_meta)
+    out = np.zeros(total, dtype=abi.SEGMENT_SUMMARY)
+    bits = {}
+    for r in range(world):
+        m = got_meta[r].cpu().numpy().view(np.int64)
+        rp, nb = [int(x) for x in m[:-1]], int(m[-1])
+        s = got_s[r].cpu().numpy().view(abi.SEGMENT_SUMMARY)
+        if len(s) != len(rp):
+            raise RuntimeError(f"rank {r}: {len(s)} summaries for {len(rp)} partitions")
+        for i, p in enumerate(rp):
+            out[p] = s[i]
+        b = np.unpackbits(got_b[r].cpu().numpy(), bitorder="little")[:nb]
+        bits[tuple(rp)] = b
+    return {"summaries": out, "bitmaps": bits}

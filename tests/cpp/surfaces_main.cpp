@@ -1,0 +1,197 @@
+// Driver for the C++ drop-in surfaces in include/rpgpu_redpanda.h, used by
+// tests/test_cpp_surfaces.py.  Each mode prints one event per line; the
+// Python side compares the events with a restatement of the reference's
+// loops over the same bytes.
+//
+//   surfaces_test cpu <segment>                 host walk: model:: crc helpers
+//   surfaces_test parse <segment> M R S E       continuous_batch_parser replay
+//   surfaces_test recover <segment>             log_replayer checkpoint
+//   surfaces_test uncompress <codec> <in> <out> compressor::uncompress
+#include <cstdio>
+#include <cstdlib>
+#include <fstream>
+#include <iostream>
+#include <iterator>
+#include <sstream>
+
+#include "rpgpu_redpanda.h"
+
+static std::vector<uint8_t> slurp(const char* path) {
+    std::ifstream f(path, std::ios::binary);
+    if (!f) { std::fprintf(stderr, "cannot open %s\n", path); std::exit(2); }
+    return std::vector<uint8_t>(std::istreambuf_iterator<char>(f), {});
+}
+
+template <typename T>
+static T le(const uint8_t* p) {
+    T v;
+    std::memcpy(&v, p, sizeof v);
+    return v;
+}
+
+// storage::header_from_iobuf (storage/parser.cc:36-76): the disk header is
+// little-endian, in declaration order
+static model::record_batch_header header_at(const uint8_t* p) {
+    model::record_batch_header h;
+    h.header_crc = le<uint32_t>(p + 0);
+    h.size_bytes = le<int32_t>(p + 4);
+    h.base_offset = le<int64_t>(p + 8);
+    h.type = (int8_t)p[16];
+    h.crc = le<int32_t>(p + 17);
+    h.attrs = model::record_batch_attributes(le<int16_t>(p + 21));
+    h.last_offset_delta = le<int32_t>(p + 23);
+    h.first_timestamp = le<int64_t>(p + 27);
+    h.max_timestamp = le<int64_t>(p + 35);
+    h.producer_id = le<int64_t>(p + 43);
+    h.producer_epoch = le<int16_t>(p + 51);
+    h.base_sequence = le<int32_t>(p + 53);
+    h.record_count = le<int32_t>(p + 57);
+    return h;
+}
+
+static int self_checks() {
+    // crc::crc32c: the standard check value, and extend() composes
+    const char* s = "123456789";
+    crc::crc32c a;
+    a.extend(s, 9);
+    crc::crc32c b;
+    b.extend(s, 4);
+    b.extend(s + 4, 5);
+    if (a.value() != 0xE3069283u || b.value() != a.value()) return 1;
+    crc::crc32c c;
+    c.extend((int32_t)0x01020304);
+    const uint8_t le4[4] = {4, 3, 2, 1};
+    if (c.value() != rpgpu_crc32c_extend(0, le4, 4)) return 2;
+    // attributes: codec bits, control / transactional bits, invalid codecs throw
+    model::record_batch_attributes at(0x33);
+    if (at.compression() != model::compression::lz4 || !at.is_control() || !at.is_transactional()) return 3;
+    bool threw = false;
+    try {
+        (void)model::record_batch_attributes(0x6).compression();
+    } catch (const std::runtime_error&) {
+        threw = true;
+    }
+    if (!threw) return 4;
+    model::record_batch_attributes at2(0x12);
+    at2.remove_compression();
+    at2 |= model::compression::snappy;
+    if (at2.value() != 0x12) return 5;
+    return 0;
+}
+
+static int mode_cpu(const std::vector<uint8_t>& seg) {
+    const int sc = self_checks();
+    std::printf("SELF %d\n", sc);
+    // a log_replayer-style host walk (storage/log_replayer.cc:62-79) using
+    // only the model:: surfaces
+    size_t pos = 0;
+    while (seg.size() - pos >= model::packed_record_batch_header_size) {
+        const model::record_batch_header h = header_at(seg.data() + pos);
+        if (h.header_crc == 0) break;
+        const bool hok = model::internal_header_only_crc(h) == h.header_crc;
+        if (!hok) break;
+        const size_t size = (size_t)(int64_t)h.size_bytes;
+        if (size < model::packed_record_batch_header_size || seg.size() - pos < size) break;
+        rpgpu::iobuf rec(seg.data() + pos + model::packed_record_batch_header_size,
+                         size - model::packed_record_batch_header_size);
+        const bool cok = model::crc_record_batch(h, rec) == h.crc;
+        std::printf("B %zu %d %lld %d %d %d\n", pos, h.size_bytes, (long long)h.base_offset, (int)hok, (int)cok,
+                    (int)h.attrs.value());
+        pos += size;
+    }
+    return sc;
+}
+
+// Consumer with scripted decisions by chain ordinal k: skip when k % M == R,
+// stop_parser once at k == S, consume_batch_end() returns stop at k == E.
+class scripted_consumer final : public storage::batch_consumer {
+public:
+    scripted_consumer(int m, int r, int s, int e) : _m(m), _r(r), _s(s), _e(e) {}
+    consume_result accept_batch_start(const model::record_batch_header& h) const override {
+        std::printf("ASK %d %lld\n", _k, (long long)h.base_offset);
+        if (_k == _s && !_stopped) {
+            _stopped = true;
+            return consume_result::stop_parser;
+        }
+        if (_m > 0 && _k % _m == _r) return consume_result::skip_batch;
+        return consume_result::accept_batch;
+    }
+    void consume_batch_start(model::record_batch_header h, size_t phys, size_t size) override {
+        std::printf("START %d %lld %zu %zu %d\n", _k, (long long)h.base_offset, phys, size, h.record_count);
+    }
+    void skip_batch_start(model::record_batch_header h, size_t phys, size_t size) override {
+        std::printf("SKIP %d %lld %zu %zu\n", _k, (long long)h.base_offset, phys, size);
+        _k++;
+    }
+    void consume_records(rpgpu::iobuf&& b) override {
+        crc::crc32c c;
+        c.extend(b.data(), b.size_bytes());
+        std::printf("RECORDS %d %zu %u\n", _k, b.size_bytes(), c.value());
+    }
+    stop_parser consume_batch_end() override {
+        const bool stop = _k == _e;
+        std::printf("END %d %d\n", _k, (int)stop);
+        _k++;
+        return stop;
+    }
+    void print(std::ostream& os) const override { os << "scripted_consumer{" << _k << "}"; }
+
+private:
+    int _m, _r, _s, _e;
+    int _k = 0;
+    mutable bool _stopped = false;
+};
+
+static void print_result(const storage::parse_result& r) {
+    if (r) std::printf("RESULT ok %zu\n", r.value);
+    else std::printf("RESULT err %d\n", (int)*r.error);
+}
+
+int main(int argc, char** argv) {
+    if (argc < 3) { std::fprintf(stderr, "usage: surfaces_test <mode> ...\n"); return 2; }
+    const std::string mode = argv[1];
+    try {
+        if (mode == "cpu") return mode_cpu(slurp(argv[2]));
+        if (mode == "parse" && argc == 7) {
+            const std::vector<uint8_t> seg = slurp(argv[2]);
+            storage::continuous_batch_parser p(
+              std::make_unique<scripted_consumer>(std::atoi(argv[3]), std::atoi(argv[4]), std::atoi(argv[5]),
+                                                  std::atoi(argv[6])),
+              seg.data(), seg.size());
+            // a stop ends one consume(); the caller resumes, as the
+            // reference's readers do after a stop_parser
+            for (int call = 0; call < 3; call++) {
+                print_result(p.consume());
+            }
+            p.close();
+            return 0;
+        }
+        if (mode == "recover") {
+            const std::vector<uint8_t> seg = slurp(argv[2]);
+            const storage::log_replayer::checkpoint c = storage::log_replayer::recover(seg.data(), seg.size());
+            if (c.last_offset) std::printf("CKPT 1 %lld %zu\n", (long long)*c.last_offset, *c.truncate_file_pos);
+            else std::printf("CKPT 0\n");
+            return 0;
+        }
+        if (mode == "uncompress" && argc == 5) {
+            const std::vector<uint8_t> in = slurp(argv[3]);
+            try {
+                const rpgpu::iobuf out = compression::compressor::uncompress(
+                  rpgpu::iobuf(in.data(), in.size()), (compression::type)std::atoi(argv[2]));
+                std::ofstream f(argv[4], std::ios::binary);
+                f.write((const char*)out.data(), (std::streamsize)out.size_bytes());
+                std::printf("U ok %zu\n", out.size_bytes());
+            } catch (const std::logic_error& e) {
+                std::printf("U logic_error\n");
+            } catch (const std::runtime_error& e) {
+                std::printf("U runtime_error\n");
+            }
+            return 0;
+        }
+    } catch (const std::exception& e) {
+        std::fprintf(stderr, "exception: %s\n", e.what());
+        return 3;
+    }
+    std::fprintf(stderr, "bad arguments\n");
+    return 2;
+}

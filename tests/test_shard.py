@@ -1,0 +1,97 @@
+"""Multi-rank path (redpanda_amd/shard.py) with gloo, world_size 2, on CPU.
+
+Each rank owns partitions p % world == rank and runs the oracle over them in
+place of the device engine (this test covers sharding and the gather, not
+the kernels); rank 0 must end with every partition's summary in global
+order and each rank's validity bits, equal to a single-process run.
+"""
+import json
+import os
+import socket
+
+import numpy as np
+import pytest
+
+from redpanda_amd import abi
+from redpanda_amd.shard import partitions_for_rank
+
+N_PARTS = 5
+SEG = 300_000
+KW = dict(seed=0xE5, batch_bytes=0, min_batch=300, max_batch=40_000, corrupt_payload_ppm=80_000)
+SUMMARY_FIELDS = ["n_batches", "terminal_pos", "bytes_consumed", "terminal_errc", "terminal_eof", "has_checkpoint",
+                  "first_bad", "ckpt_last_offset", "ckpt_truncate_pos", "n_records"]
+
+
+def _segments(parts):
+    from redpanda_amd import _lib
+    segs = []
+    for p in parts:
+        a = np.zeros(SEG + 997 * p, dtype=np.uint8)  # ragged per-partition sizes
+        _lib.gen_segment(a, p, **KW)
+        segs.append(a)
+    return segs
+
+
+def _oracle_job(segs):
+    from oracle import oracle as O
+    offs = np.cumsum([0] + [s.size for s in segs]).astype(np.uint64)
+    data = np.concatenate(segs) if segs else np.zeros(0, np.uint8)
+    return O.run_job(data, offs, abi.JOB_CRC | abi.JOB_PARSE)
+
+
+def _worker(rank, world, port, out_path):
+    import torch
+    import torch.distributed as dist
+    from redpanda_amd.shard import gather_job_verdicts
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        parts = partitions_for_rank(N_PARTS, world, rank)
+        res = _oracle_job(_segments(parts))
+        summaries = torch.from_numpy(res.summaries.copy().view(np.uint8))
+        bitmap = torch.from_numpy(res.bitmap.copy().view(np.uint8))
+        got = gather_job_verdicts(summaries, bitmap, len(res.batches), parts, rank, world, dist)
+        if rank == 0:
+            s = got["summaries"]
+            json.dump({"summaries": {f: s[f].tolist() for f in SUMMARY_FIELDS},
+                       "bitmaps": {",".join(map(str, k)): v.tolist() for k, v in got["bitmaps"].items()}},
+                      open(out_path, "w"))
+        else:
+            assert got is None
+    finally:
+        dist.destroy_process_group()
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def test_partition_ownership():
+    for world in (1, 2, 3, 8):
+        owned = [partitions_for_rank(17, world, r) for r in range(world)]
+        assert sorted(p for o in owned for p in o) == list(range(17))
+        assert all(p % world == r for r, o in enumerate(owned) for p in o)
+    with pytest.raises(ValueError):
+        partitions_for_rank(4, 2, 2)
+
+
+def test_gloo_world2_gather_matches_single_process(rplib, oracle, tmp_path):
+    import torch.multiprocessing as mp
+    out = str(tmp_path / "rank0.json")
+    mp.spawn(_worker, args=(2, _free_port(), out), nprocs=2, join=True)
+    got = json.load(open(out))
+    # single-process reference: every partition on its own
+    for p in range(N_PARTS):
+        ref = _oracle_job(_segments([p]))
+        for f in SUMMARY_FIELDS:
+            assert got["summaries"][f][p] == ref.summaries[f][0].item(), (p, f)
+    assert any(v == 0 for b in got["bitmaps"].values() for v in b), "corruption should clear some bits"
+    for r in range(2):
+        parts = partitions_for_rank(N_PARTS, 2, r)
+        want = np.concatenate([np.unpackbits(_oracle_job(_segments([p])).bitmap.view(np.uint8),
+                                             bitorder="little")[: len(_oracle_job(_segments([p])).batches)]
+                               for p in parts])
+        assert got["bitmaps"][",".join(map(str, parts))] == want.tolist()
