@@ -67,6 +67,9 @@ def load():
         path = os.path.join(HERE, "librpgpu_checked.so")
     elif os.environ.get("RPGPU_STAMPS") == "1":
         path = os.path.join(HERE, "librpgpu_stamps.so")
+    elif os.environ.get("RPGPU_VARIANT"):
+        # experiment builds (scripts/build_exp.py): librpgpu_<variant>.so
+        path = os.path.join(HERE, f"librpgpu_{os.environ['RPGPU_VARIANT']}.so")
     if not os.path.exists(path):
         raise RpgpuError(f"{path} missing: run `python -m redpanda_amd.build` (no CPU fallback exists)")
     L = C.CDLL(path)

@@ -133,11 +133,32 @@ DEV void load_window(const Stream& st, uint64_t r, Win& w) {
     }
 }
 
+// rows [I0, I1) of window 0 only (the software pipeline issues a batch's
+// window in two parts)
+template <int I0, int I1>
+DEV void load_rows(const Stream& st, Win& w) {
+    const int64_t a = win_base(st, 0) + 16 * (int64_t)lane();
+#pragma unroll
+    for (int i = I0; i < I1; i++) {
+        const int64_t q = a + 1024 * i;
+        uint4 t = make_uint4(0u, 0u, 0u, 0u);
+        if (q + 16 > (int64_t)st.S && q < (int64_t)st.E16) t = *(const uint4*)(st.src + q);
+        w.r[i] = t;
+    }
+}
+
 // the 16-byte row at E16 holding the tail (uniform)
 DEV uint4 load_tail(const Stream& st) {
     uint4 t = make_uint4(0u, 0u, 0u, 0u);
     if (st.E > st.E16) t = *(const uint4*)(st.src + st.E16);
     return t;
+}
+
+// lane l ^ X's value within 32-lane halves (ds_swizzle bit mode: and 0x1F,
+// xor X; an immediate pattern, so no address VGPR stays live)
+template <uint32_t X>
+DEV uint32_t swz_xor(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_ds_swizzle((int)v, (int)(0x1Fu | (X << 10)));
 }
 
 // CRC of one window from registers: the state at W0 + 16K.  Words before
@@ -153,12 +174,15 @@ DEV uint32_t crc_window(const uint8_t* lds, const Keys& K, const Win& d, uint32_
         uint32_t w[4] = {d.r[i].x, d.r[i].y, d.r[i].z, d.r[i].w};
         if ((uint32_t)i <= i4) {
             // the row holding o4 (and any before it): mask words before o4,
-            // inject at o4 (uniform branch; rows after it take neither)
+            // inject at o4 (uniform branch; rows after it take neither).  The
+            // lane's row offsets lo + 4k against the uniform row threshold:
+            // no per-row constants stay live across the batch loop
+            const int32_t t = (int32_t)o4 - 1024 * i;
 #pragma unroll
             for (int k = 0; k < 4; k++) {
-                const uint32_t off = 1024u * (uint32_t)i + lo + 4u * (uint32_t)k;
-                w[k] = off >= o4 ? w[k] : 0u;
-                s[k] ^= (off == o4) ? Tinj : 0u;
+                const int32_t off = (int32_t)(lo + 4u * (uint32_t)k);
+                w[k] = off >= t ? w[k] : 0u;
+                s[k] ^= (off == t) ? Tinj : 0u;
             }
         }
         if (i < 15) {
@@ -173,14 +197,18 @@ DEV uint32_t crc_window(const uint8_t* lds, const Keys& K, const Win& d, uint32_
         }
     }
     // lane l's state sits 16 (63 - l) bytes before the window end:
-    // shift-and-xor tree
+    // shift-and-xor tree into lane 0.  At level m only lanes that are
+    // multiples of 2^(m+1) matter, and for them l ^ 2^m = l + 2^m, so the
+    // exchange is an xor swizzle (immediate pattern, no address VGPR) and the
+    // last level a readlane of lane 32.
+    static_assert(kShiftLevels == 6, "shift tree is written out for 64 lanes");
     uint32_t sv = s[0];
-#pragma unroll
-    for (uint32_t m = 0; m < kShiftLevels; m++) {
-        const uint32_t other = __shfl_down(sv, 1u << m, 64);
-        sv = shift_k(lds, sv, m) ^ other;
-    }
-    return uni32(sv);
+    sv = shift_k(lds, sv, 0) ^ swz_xor<1>(sv);
+    sv = shift_k(lds, sv, 1) ^ swz_xor<2>(sv);
+    sv = shift_k(lds, sv, 2) ^ swz_xor<4>(sv);
+    sv = shift_k(lds, sv, 3) ^ swz_xor<8>(sv);
+    sv = shift_k(lds, sv, 4) ^ swz_xor<16>(sv);
+    return shift_k(lds, uni32(sv), 5) ^ rl(sv, 32);
 }
 
 // fold the tail bytes [max(S, E16), E) held in gt into the state (uniform)
@@ -450,8 +478,9 @@ DEV bool parse_group(const uint8_t* p0, uint32_t mis, uint32_t n, uint32_t m, ui
     const bool act = l < m;
     if (act) r = parse_record(p0, mis, n, my_start, head);
     else { r.err = 0; r.end = 0xFFFFFFFFu; }
-    const uint32_t prev_end = __shfl_up(r.end, 1, 64);
-    const uint32_t prev_err = __shfl_up(r.err, 1, 64);
+    // lane l - 1's values (DPP wave_shr:1; lane 0 ignores them)
+    const uint32_t prev_end = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)r.end, 0x138, 0xF, 0xF, false);
+    const uint32_t prev_err = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)r.err, 0x138, 0xF, 0xF, false);
     const bool match = (l == 0) || (prev_err == 0 && prev_end == my_start);
     const uint64_t bad = __ballot(act && !match);
     const uint32_t exact = bad ? (uint32_t)__builtin_ctzll(bad) : m;  // lanes [0, exact) are exact
@@ -478,10 +507,10 @@ DEV bool parse_group(const uint8_t* p0, uint32_t mis, uint32_t n, uint32_t m, ui
     }
     if (errs) {
         wr.parsed = done + nok;
-        wr.err = uni32(__shfl(r.err, nok, 64));
+        wr.err = rl(r.err, (int)nok);
         return false;
     }
-    start = uni32(__shfl(r.end, exact - 1, 64));
+    start = rl(r.end, (int)(exact - 1));
     done += exact;
     return true;
 }
@@ -535,57 +564,73 @@ DEV void note_bad(const DeviceJob& j, uint32_t seg, uint64_t b) {
     }
 }
 
-// Per-batch descriptor (uniform).  index_base carries the absolute payload
-// start from k_emit (scratch, overwritten here).
+// Per-batch descriptor, loaded one iteration ahead as ONE VGPR: lane i < 32
+// holds dword i of the batch result, lanes 32..37 the index-slot and
+// decode-arena words; the fields are read out with v_readlane when the batch
+// is reached.  index_base carries the absolute payload start from k_emit
+// (scratch, overwritten here), reserved1 the raw BE40 prefix CRC contribution.
+constexpr int kDwSize = offsetof(rpgpu_batch_result, size_bytes) / 4;
+constexpr int kDwCount = offsetof(rpgpu_batch_result, record_count) / 4;
+constexpr int kDwCrc = offsetof(rpgpu_batch_result, crc) / 4;
+constexpr int kDwFlags = offsetof(rpgpu_batch_result, flags) / 4;
+constexpr int kDwSeg = offsetof(rpgpu_batch_result, segment) / 4;
+constexpr int kDwBase = offsetof(rpgpu_batch_result, index_base) / 4;
+constexpr int kDwDlen = offsetof(rpgpu_batch_result, decoded_len) / 4;
+constexpr int kDwAttrs = offsetof(rpgpu_batch_result, attrs) / 4;
+constexpr int kDwPraw = offsetof(rpgpu_batch_result, reserved1) / 4;
+static_assert(sizeof(rpgpu_batch_result) == 128 && offsetof(rpgpu_batch_result, attrs) % 4 == 0, "desc layout");
+
+DEV uint32_t load_desc_raw(const DeviceJob& j, uint64_t b) {
+    const uint32_t l = lane();
+    const uint32_t* p = l < 32u ? (const uint32_t*)&j.batches[b] + l
+                      : l < 34u ? (const uint32_t*)&j.slots[b] + (l - 32u)
+                      : l < 36u ? (const uint32_t*)&j.slots[b + 1] + (l - 34u)
+                                : (const uint32_t*)&j.dcap[b] + (l & 1u);
+    return l < 38u ? *p : 0u;
+}
+
 struct Desc {
-    uint32_t flags, crc, praw, codec, seg;
+    uint32_t flags, crc, praw, codec, seg, dlen;
     uint64_t S, n, ib, islots, doff;
     int32_t rc;
 };
 
-DEV Desc load_desc(const DeviceJob& j, uint64_t b) {
-    const rpgpu_batch_result* R = &j.batches[b];
+DEV Desc desc_of(uint32_t raw) {
     Desc d;
-    d.flags = uni32(R->flags);
-    d.crc = uni32(R->crc);
-    d.praw = uni32((uint32_t)R->reserved1);
-    d.S = uni64(R->index_base);
-    d.n = uni32((uint32_t)R->size_bytes - RPGPU_HEADER_SIZE);
-    d.rc = (int32_t)uni32((uint32_t)R->record_count);
-    d.codec = uni32((uint32_t)(uint16_t)R->attrs) & 7u;
-    d.seg = uni32(R->segment);
-    d.ib = uni64(j.slots[b]);
-    d.islots = uni64(j.slots[b + 1]) - d.ib;
-    d.doff = uni64(j.dcap[b]);
+    d.flags = rl(raw, kDwFlags);
+    d.crc = rl(raw, kDwCrc);
+    d.praw = rl(raw, kDwPraw);
+    d.S = (uint64_t)rl(raw, kDwBase) | ((uint64_t)rl(raw, kDwBase + 1) << 32);
+    d.n = rl(raw, kDwSize) - RPGPU_HEADER_SIZE;
+    d.rc = (int32_t)rl(raw, kDwCount);
+    d.codec = rl(raw, kDwAttrs) & 7u;
+    d.seg = rl(raw, kDwSeg);
+    d.dlen = rl(raw, kDwDlen);
+    d.ib = (uint64_t)rl(raw, 32) | ((uint64_t)rl(raw, 33) << 32);
+    d.islots = ((uint64_t)rl(raw, 34) | ((uint64_t)rl(raw, 35) << 32)) - d.ib;
+    d.doff = (uint64_t)rl(raw, 36) | ((uint64_t)rl(raw, 37) << 32);
     return d;
 }
 
-// CRC + (optional) walk of one stream; d/gt hold its first window and tail
-DEV uint32_t stream_crc_walk(const DeviceJob& j, const uint8_t* lds, const Keys& K, const Stream& st, Win& d,
-                             const uint4& gt, uint32_t Tst, bool walk, const Desc& ds, uint64_t b, WalkResult& w,
-                             bool& idx_ok) {
-    STAMP(t0);
-    const uint32_t crc = ~crc_stream(lds, K, st, d, gt, Tst);
-    STAMP(t1);
-    STAMP_ADD(0, t1 - t0);
-    if (walk) {
-        idx_ok = ds.ib + ds.islots <= j.record_capacity;
-        rpgpu_record_index* out = idx_ok ? j.records + ds.ib : nullptr;
-        const uint64_t cap = idx_ok ? ds.islots : 0;
-        w = walk_records(st.src + st.S, (uint32_t)(st.E - st.S), ds.rc, (uint32_t)b, out, cap);
-        STAMP(t2);
-        STAMP_ADD(1, t2 - t1);
-    }
-    return crc;
+// the stored payload of a batch as a stream (empty when there is none)
+DEV Stream stored_stream(const DeviceJob& j, const Desc& d, bool valid) {
+    return (valid && (d.flags & RPGPU_F_COMPLETE)) ? make_stream(j.data, d.S, d.S + d.n) : make_stream(j.data, 0, 0);
 }
 
-__global__ __launch_bounds__(1024) void k_validate(DeviceJob j) {
-    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-    const Tables* T = j.tables;
+// the record walk of one payload into the batch's index slots
+DEV WalkResult walk_batch(const DeviceJob& j, const Desc& ds, const uint8_t* p0, uint32_t n, uint64_t b, bool& idx_ok) {
+    idx_ok = ds.ib + ds.islots <= j.record_capacity;
+    rpgpu_record_index* out = idx_ok ? j.records + ds.ib : nullptr;
+    const uint64_t cap = idx_ok ? ds.islots : 0;
+    return walk_records(p0, n, ds.rc, (uint32_t)b, out, cap);
+}
+
+// LDS image of the CRC tables (every workgroup of the validate kernels).
+// braid tables: word i -> row-set rs = i >> 14, entry e = (i >> 6) & 255,
+// slot = (i >> 5) & 1, copy = i & 31; (rs, slot) = (0,0) T1023, (0,1)
+// T1022, (1,0) T1021, (1,1) T1020
+DEV void init_lds_tables(uint8_t* lds, const Tables* T) {
     const uint32_t tid = threadIdx.x;
-    // braid tables: word i -> row-set rs = i >> 14, entry e = (i >> 6) & 255,
-    // slot = (i >> 5) & 1, copy = i & 31; (rs, slot) = (0,0) T1023, (0,1)
-    // T1022, (1,0) T1021, (1,1) T1020
     for (uint32_t i = tid; i < 32768u; i += blockDim.x)
         ((uint32_t*)(lds + kLdsBraidOff))[i] = T->braid[((i >> 14) << 1) | ((i >> 5) & 1u)][(i >> 6) & 255u];
     // slice tables: T3, T2, T1, T0
@@ -594,14 +639,49 @@ __global__ __launch_bounds__(1024) void k_validate(DeviceJob j) {
     for (uint32_t i = tid; i < kShiftLevels * 1024u; i += blockDim.x)
         ((uint32_t*)(lds + kLdsShiftOff))[i] = ((const uint32_t*)T->shift)[i];
     __syncthreads();
+}
 
-    const uint32_t l = lane();
-    const uint32_t bank = (l & 31u) * 4u;
+// this lane's copy of the four braid tables
+DEV Keys make_keys() {
+    const uint32_t bank = (lane() & 31u) * 4u;
     Keys K;
     K.k15 = (0u << 16) | (0u + bank);
     K.k14 = (0u << 16) | (128u + bank);
     K.k13 = (1u << 16) | (0u + bank);
     K.k12 = (1u << 16) | (128u + bank);
+    return K;
+}
+
+// Walk result -> verdict bits (model/record.h:616-627 sync, :680-697 async)
+DEV uint32_t walk_flags(const DeviceJob& j, const WalkResult& w, bool idx_ok, uint32_t& perr) {
+    uint32_t f = RPGPU_F_PARSED;
+    perr = w.err;
+    if (perr == 0) {
+        f |= RPGPU_F_PARSE_ASYNC_OK;
+        if (w.trailing == 0) f |= RPGPU_F_PARSE_OK;
+        else perr = RPGPU_PARSE_ERR_TRAILING;
+    }
+    if (f & RPGPU_F_PARSE_OK) {
+        if (idx_ok) f |= RPGPU_F_INDEX_WRITTEN;
+        else { perr = RPGPU_PARSE_ERR_INDEX_CAPACITY; if (lane() == 0) atomicOr(&j.counters[1], 2u); }
+    }
+    return f;
+}
+
+// Rows of a batch's window that may be issued one iteration ahead, before
+// the previous batch's walk (whose chain reads through the scalar cache, so
+// it never waits on them).  Measured on the C1 workload: 0, 4, 8 and 10 rows
+// within 1% of each other (the walk, not the window latency, is exposed), so
+// only the descriptor is prefetched.
+constexpr int kPreRows = 0;
+
+__global__ __launch_bounds__(1024) void k_validate(DeviceJob j) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    const Tables* T = j.tables;
+    const uint32_t tid = threadIdx.x;
+    init_lds_tables(lds, T);
+    const uint32_t l = lane();
+    const Keys K = make_keys();
     const uint32_t c40 = uni32(T->c40);
 
     const uint64_t nb_total = j.chunk_count[j.total_chunks];
@@ -612,81 +692,69 @@ __global__ __launch_bounds__(1024) void k_validate(DeviceJob j) {
         for (int i = 0; i < 8; i++) s_stamps[tid >> 6][i] = 0;
 #endif
     STAMP(tk0);
-    for (uint64_t b = (uint64_t)blockIdx.x * kVWaves + (tid >> 6); b < nb; b += nw) {
-        rpgpu_batch_result* R = &j.batches[b];
-        STAMP(ta);
-        const Desc d = load_desc(j, b);
-#ifdef RPGPU_STAMPS
-        { const uint32_t z = d.flags ^ d.crc; if (z == 0x9e3779b9u) g_stamps[7]++; }
-#endif
-        STAMP(tb);
-        STAMP_ADD(2, tb - ta);
-        if (!(d.flags & RPGPU_F_COMPLETE)) {
-            if (l == 0) { R->index_base = d.ib; R->decoded_off = d.doff; R->reserved1 = 0; }
-            note_bad(j, d.seg, b);
-            continue;
-        }
-        uint32_t f = d.flags;
-        uint32_t parsed = 0, perr = 0, dcrc = 0, dhcrc = 0;
-        WalkResult w;
-        bool walked = false, idx_ok = false;
-        uint32_t crc;
-        {
-            // stored payload: batch crc (+ walk when uncompressed).  CRC state
-            // after the BE40 prefix with init ~0 = c40 ^ the prefix's raw
-            // contribution (computed by k_emit)
-            const Stream st = make_stream(j.data, d.S, d.S + d.n);
-            Win v;
-            load_window(st, 0, v);  // unconditional: a window left undefined on one path is pinned in scratch
+    uint64_t b = (uint64_t)blockIdx.x * kVWaves + (tid >> 6);
+    if (b < nb) {
+        uint32_t raw = load_desc_raw(j, b);
+        Desc dn = desc_of(raw);
+        Stream sn = stored_stream(j, dn, true);
+        Win v;
+        load_rows<0, kPreRows>(sn, v);
+        for (; b < nb; b += nw) {
+            const Desc d = dn;
+            const Stream st = sn;
+            const uint64_t bn = b + nw;
+            const bool more = bn < nb;
+            raw = load_desc_raw(j, more ? bn : b);
+            load_rows<kPreRows, 16>(st, v);  // the rest of this batch's window
             const uint4 gt = load_tail(st);
-            walked = d.codec == 0 && (j.flags & RPGPU_JOB_PARSE);
-            crc = stream_crc_walk(j, lds, K, st, v, gt, d.praw ^ c40, walked, d, b, w, idx_ok);
-        }
-        if (crc == d.crc) f |= RPGPU_F_CRC_OK;
-        else note_bad(j, d.seg, b);
-        if (d.codec != 0 && (f & RPGPU_F_CODEC_OK)) {
-            // reset_size_checksum_metadata over the decoded payload: the prefix
-            // differs only in the codec bits of attrs (BE40 byte 1)
-            const uint64_t dl = uni32(R->decoded_len);
-            const Stream ds = make_stream(j.decoded, d.doff, d.doff + dl);
-            Win v;
-            load_window(ds, 0, v);
-            const uint4 gt = load_tail(ds);
-            walked = (j.flags & RPGPU_JOB_PARSE) != 0;
-            dcrc = stream_crc_walk(j, lds, K, ds, v, gt, d.praw ^ T->hdr[38][d.codec] ^ c40, walked, d, b, w, idx_ok);
-            dhcrc = decoded_header_crc(T, j.data + d.S - RPGPU_HEADER_SIZE, (uint32_t)(RPGPU_HEADER_SIZE + dl), dcrc);
-        }
-        if (walked) {
-            parsed = w.parsed;
-            perr = w.err;
-            f |= RPGPU_F_PARSED;
-            if (perr == 0) {
-                f |= RPGPU_F_PARSE_ASYNC_OK;
-                if (w.trailing == 0) f |= RPGPU_F_PARSE_OK;
-                else perr = RPGPU_PARSE_ERR_TRAILING;
+            // the next batch's descriptor and first rows (into the rows the
+            // CRC has consumed)
+            auto prefetch = [&]() __attribute__((always_inline)) {
+                dn = desc_of(raw);
+                sn = stored_stream(j, dn, more);
+                load_rows<0, kPreRows>(sn, v);
+            };
+            rpgpu_batch_result* R = &j.batches[b];
+            STAMP(ta);
+            if (!(d.flags & RPGPU_F_COMPLETE)) {
+                if (l == 0) { R->index_base = d.ib; R->decoded_off = d.doff; R->reserved1 = 0; }
+                note_bad(j, d.seg, b);
+                prefetch();
+                continue;
             }
-            if (f & RPGPU_F_PARSE_OK) {
-                if (idx_ok) f |= RPGPU_F_INDEX_WRITTEN;
-                else { perr = RPGPU_PARSE_ERR_INDEX_CAPACITY; if (l == 0) atomicOr(&j.counters[1], 2u); }
+            uint32_t f = d.flags;
+            uint32_t parsed = 0, perr = 0;
+            // stored payload: batch crc.  CRC state after the BE40 prefix with
+            // init ~0 = c40 ^ the prefix's raw contribution (from k_emit)
+            const uint32_t crc = ~crc_stream(lds, K, st, v, gt, d.praw ^ c40);
+            STAMP(tb);
+            STAMP_ADD(0, tb - ta);
+            if (crc == d.crc) f |= RPGPU_F_CRC_OK;
+            else note_bad(j, d.seg, b);
+            prefetch();
+            if (d.codec == 0 && (j.flags & RPGPU_JOB_PARSE)) {
+                bool idx_ok;
+                const WalkResult w = walk_batch(j, d, j.data + d.S, (uint32_t)d.n, b, idx_ok);
+                f |= walk_flags(j, w, idx_ok, perr);
+                parsed = w.parsed;
             }
-        }
-        STAMP(tc);
-        if (l == 0) {
-            R->crc_computed = crc;
-            R->flags = f;
-            R->index_base = d.ib;
-            R->decoded_off = d.doff;
-            R->records_parsed = parsed;
-            R->parse_err = (uint8_t)perr;
-            if (d.codec != 0 && (f & RPGPU_F_CODEC_OK)) {
-                R->decoded_crc = dcrc;
-                R->decoded_header_crc = dhcrc;
+            STAMP(tc);
+            STAMP_ADD(1, tc - tb);
+            if (l == 0) {
+                R->crc_computed = crc;
+                R->flags = f;
+                R->index_base = d.ib;
+                R->decoded_off = d.doff;
+                R->records_parsed = parsed;
+                R->parse_err = (uint8_t)perr;
+                // a decoded payload is finished by k_validate_decoded, which
+                // still needs the prefix contribution
+                if (!(d.codec != 0 && (f & RPGPU_F_CODEC_OK))) R->reserved1 = 0;
             }
-            R->reserved1 = 0;
+            STAMP(td);
+            STAMP_ADD(5, td - tc);
+            STAMP_ADD(3, 1);
         }
-        STAMP(td);
-        STAMP_ADD(5, td - tc);
-        STAMP_ADD(3, 1);
     }
     STAMP(tk1);
     STAMP_ADD(4, tk1 - tk0);
@@ -706,16 +774,68 @@ __global__ void k_print_stamps() {
 }
 #endif
 
+// reset_size_checksum_metadata (storage/parser_utils.cc:114-120) and the
+// record walk over every payload k_decode uncompressed: one wave per
+// worklist item, after k_validate has written the stored-payload verdict.
+// The new crc covers the BE40 prefix with the codec bits of attrs cleared
+// (BE40 byte 1) followed by the decoded bytes.
+__global__ __launch_bounds__(1024) void k_validate_decoded(DeviceJob j) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    const uint32_t count = j.counters[2];
+    if (count == 0) return;
+    const Tables* T = j.tables;
+    init_lds_tables(lds, T);
+    const uint32_t l = lane();
+    const Keys K = make_keys();
+    const uint32_t c40 = uni32(T->c40);
+    const uint64_t nw = (uint64_t)gridDim.x * kVWaves;
+    for (uint64_t i = (uint64_t)blockIdx.x * kVWaves + (threadIdx.x >> 6); i < count; i += nw) {
+        const uint64_t b = uni32(j.decode_list[i]);
+        rpgpu_batch_result* R = &j.batches[b];
+        Desc d = desc_of(load_desc_raw(j, b));
+        if (!(d.flags & RPGPU_F_CODEC_OK)) continue;
+        // k_validate replaced index_base (the payload start) by the index
+        // slot; the header sits at file_pos in its segment
+        const uint64_t hdr = uni64(R->file_pos) + uni64(j.seg_off[d.seg]);
+        const uint64_t dl = d.dlen;
+        const Stream ds = make_stream(j.decoded, d.doff, d.doff + dl);
+        Win dv;
+        load_window(ds, 0, dv);
+        const uint4 dgt = load_tail(ds);
+        const uint32_t dcrc = ~crc_stream(lds, K, ds, dv, dgt, d.praw ^ T->hdr[38][d.codec] ^ c40);
+        const uint32_t dhcrc = decoded_header_crc(T, j.data + hdr, (uint32_t)(RPGPU_HEADER_SIZE + dl), dcrc);
+        uint32_t f = d.flags, perr = 0, parsed = 0;
+        if (j.flags & RPGPU_JOB_PARSE) {
+            bool idx_ok;
+            const WalkResult w = walk_batch(j, d, j.decoded + d.doff, (uint32_t)dl, b, idx_ok);
+            f |= walk_flags(j, w, idx_ok, perr);
+            parsed = w.parsed;
+        }
+        if (l == 0) {
+            R->flags = f;
+            R->records_parsed = parsed;
+            R->parse_err = (uint8_t)perr;
+            R->decoded_crc = dcrc;
+            R->decoded_header_crc = dhcrc;
+            R->reserved1 = 0;
+        }
+    }
+}
+
 hipError_t launch_validate(const DeviceJob& j, hipStream_t s, uint32_t grid) {
     static bool attr = false;
     if (!attr) {
         (void)hipFuncSetAttribute((const void*)k_validate, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsValidateBytes);
+        (void)hipFuncSetAttribute((const void*)k_validate_decoded, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  kLdsValidateBytes);
         attr = true;
     }
     hipLaunchKernelGGL(k_validate, dim3(grid), dim3(64 * kVWaves), kLdsValidateBytes, s, j);
 #ifdef RPGPU_STAMPS
     hipLaunchKernelGGL(k_print_stamps, dim3(1), dim3(1), 0, s);
 #endif
+    if ((j.flags & RPGPU_JOB_DECODE) && j.decoded)
+        hipLaunchKernelGGL(k_validate_decoded, dim3(grid), dim3(64 * kVWaves), kLdsValidateBytes, s, j);
     return hipGetLastError();
 }
 

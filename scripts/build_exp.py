@@ -1,0 +1,30 @@
+"""Build experiment variants of librpgpu.so: redpanda_amd/librpgpu_<name>.so
+with an alternate k_validate source and/or extra defines; the other objects
+come from the main build.  Usage:
+  python scripts/build_exp.py NAME [--src path/to/rp_validate.hip] [-DFOO ...]
+Load with RPGPU_VARIANT=NAME.  Diagnostics only, never the product."""
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+from redpanda_amd import build as B  # noqa: E402
+
+name = sys.argv[1]
+args = sys.argv[2:]
+src = os.path.join(B.CSRC, "rp_validate.hip")
+if "--src" in args:
+    i = args.index("--src")
+    src = os.path.abspath(args[i + 1])
+    del args[i:i + 2]
+defs = [a for a in args if a.startswith("-D")]
+B.build()
+bdir = os.path.join(B.HERE, "_build_exp_" + name)
+os.makedirs(bdir, exist_ok=True)
+obj = os.path.join(bdir, "rp_validate.hip.o")
+B._run([B._hipcc(), f"--offload-arch={B.ARCH}", "-O3", "-fPIC", "-std=c++17", "-I", B.INC, "-I", B.CSRC,
+        "-Wno-unused-function", "-Wno-unused-variable"] + defs + ["-c", src, "-o", obj])
+objs = [os.path.join(B.BUILD, s + ".o") for s in B.HIP_SOURCES + B.CXX_SOURCES if s != "rp_validate.hip"] + [obj]
+out = os.path.join(B.HERE, f"librpgpu_{name}.so")
+B._run([B._hipcc(), f"--offload-arch={B.ARCH}", "-shared", "-fPIC", "-o", out] + objs + ["-ldl", "-lpthread"])
+print(out)
