@@ -517,9 +517,16 @@ DEV bool parse_group(const uint8_t* p0, uint32_t mis, uint32_t n, uint32_t m, ui
 
 // record_batch::for_each_record (model/record.h:616-627) with speculative
 // lane-parallel records: chain_starts guesses 64 record starts at a time,
-// parse_group parses and commits the confirmed prefix.
+// parse_group parses and commits the confirmed prefix.  first: the first
+// group's chain already ran (m0 lanes, my_start0 / head0).
+struct Group {
+    bool first;
+    uint32_t m, my_start;
+    uint4 head;
+};
+
 DEV WalkResult walk_records(const uint8_t* p0, uint32_t n, int32_t rc, uint32_t batch_ord, rpgpu_record_index* out,
-                            uint64_t out_cap) {
+                            uint64_t out_cap, const Group& g0) {
     WalkResult wr;
     wr.parsed = 0;
     wr.err = 0;
@@ -528,13 +535,19 @@ DEV WalkResult walk_records(const uint8_t* p0, uint32_t n, int32_t rc, uint32_t 
     const uint32_t total = (uint32_t)(rc > 0 ? rc : 0);
     uint32_t start = 0, done = 0;
     while (done < total) {
-        uint32_t my_start;
+        uint32_t my_start, m;
         uint4 head;
-        const uint32_t want = (total - done) < 64u ? (total - done) : 64u;
-        STAMP(w0);
-        const uint32_t m = chain_starts(p0, n, start, want, my_start, head);
-        STAMP(w1);
-        STAMP_ADD(6, w1 - w0);
+        if (done == 0 && g0.first) {
+            m = g0.m;
+            my_start = g0.my_start;
+            head = g0.head;
+        } else {
+            const uint32_t want = (total - done) < 64u ? (total - done) : 64u;
+            STAMP(w0);
+            m = chain_starts(p0, n, start, want, my_start, head);
+            STAMP(w1);
+            STAMP_ADD(6, w1 - w0);
+        }
         if (!parse_group(p0, mis, n, m, my_start, head, batch_ord, out, out_cap, done, start, wr)) return wr;
     }
     wr.parsed = done;
@@ -618,11 +631,12 @@ DEV Stream stored_stream(const DeviceJob& j, const Desc& d, bool valid) {
 }
 
 // the record walk of one payload into the batch's index slots
-DEV WalkResult walk_batch(const DeviceJob& j, const Desc& ds, const uint8_t* p0, uint32_t n, uint64_t b, bool& idx_ok) {
+DEV WalkResult walk_batch(const DeviceJob& j, const Desc& ds, const uint8_t* p0, uint32_t n, uint64_t b, bool& idx_ok,
+                          const Group& g0) {
     idx_ok = ds.ib + ds.islots <= j.record_capacity;
     rpgpu_record_index* out = idx_ok ? j.records + ds.ib : nullptr;
     const uint64_t cap = idx_ok ? ds.islots : 0;
-    return walk_records(p0, n, ds.rc, (uint32_t)b, out, cap);
+    return walk_records(p0, n, ds.rc, (uint32_t)b, out, cap, g0);
 }
 
 // LDS image of the CRC tables (every workgroup of the validate kernels).
@@ -724,22 +738,37 @@ __global__ __launch_bounds__(1024) void k_validate(DeviceJob j) {
             }
             uint32_t f = d.flags;
             uint32_t parsed = 0, perr = 0;
+            // uncompressed: the first record chain runs now, while the
+            // window's lines are arriving in L2 (its scalar loads hit or merge
+            // with them; after the CRC they would be evicted again)
+            const bool walk = d.codec == 0 && (j.flags & RPGPU_JOB_PARSE);
+            Group g0;
+            g0.first = walk && d.rc > 0;
+            g0.m = 0;
+            g0.my_start = 0xFFFFFFFFu;
+            g0.head = make_uint4(0u, 0u, 0u, 0u);
+            if (g0.first) {
+                const uint32_t total = (uint32_t)d.rc;
+                g0.m = chain_starts(j.data + d.S, (uint32_t)d.n, 0u, total < 64u ? total : 64u, g0.my_start, g0.head);
+            }
+            STAMP(tb);
+            STAMP_ADD(6, tb - ta);
             // stored payload: batch crc.  CRC state after the BE40 prefix with
             // init ~0 = c40 ^ the prefix's raw contribution (from k_emit)
             const uint32_t crc = ~crc_stream(lds, K, st, v, gt, d.praw ^ c40);
-            STAMP(tb);
-            STAMP_ADD(0, tb - ta);
+            STAMP(tb2);
+            STAMP_ADD(0, tb2 - tb);
             if (crc == d.crc) f |= RPGPU_F_CRC_OK;
             else note_bad(j, d.seg, b);
             prefetch();
-            if (d.codec == 0 && (j.flags & RPGPU_JOB_PARSE)) {
+            if (walk) {
                 bool idx_ok;
-                const WalkResult w = walk_batch(j, d, j.data + d.S, (uint32_t)d.n, b, idx_ok);
+                const WalkResult w = walk_batch(j, d, j.data + d.S, (uint32_t)d.n, b, idx_ok, g0);
                 f |= walk_flags(j, w, idx_ok, perr);
                 parsed = w.parsed;
             }
             STAMP(tc);
-            STAMP_ADD(1, tc - tb);
+            STAMP_ADD(1, tc - tb2);
             if (l == 0) {
                 R->crc_computed = crc;
                 R->flags = f;
@@ -807,7 +836,12 @@ __global__ __launch_bounds__(1024) void k_validate_decoded(DeviceJob j) {
         uint32_t f = d.flags, perr = 0, parsed = 0;
         if (j.flags & RPGPU_JOB_PARSE) {
             bool idx_ok;
-            const WalkResult w = walk_batch(j, d, j.decoded + d.doff, (uint32_t)dl, b, idx_ok);
+            Group g0;
+            g0.first = false;
+            g0.m = 0;
+            g0.my_start = 0xFFFFFFFFu;
+            g0.head = make_uint4(0u, 0u, 0u, 0u);
+            const WalkResult w = walk_batch(j, d, j.decoded + d.doff, (uint32_t)dl, b, idx_ok, g0);
             f |= walk_flags(j, w, idx_ok, perr);
             parsed = w.parsed;
         }
