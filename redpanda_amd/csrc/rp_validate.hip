@@ -164,7 +164,9 @@ DEV uint32_t swz_xor(uint32_t v) {
 // CRC of one window from registers: the state at W0 + 16K.  Words before
 // window offset o4 (4-aligned) are not part of the stream (read as zero);
 // the state Tinj is injected at o4.
-DEV uint32_t crc_window(const uint8_t* lds, const Keys& K, const Win& d, uint32_t o4, uint32_t Tinj) {
+template <typename Mid>
+DEV uint32_t crc_window(const uint8_t* lds, const Keys& K, const Win& d, uint32_t o4, uint32_t Tinj, bool do_mid,
+                        Mid&& mid) {
     const uint32_t l = lane();
     const uint32_t i4 = o4 >> 10, l4 = (o4 >> 4) & 63u, k4 = (o4 >> 2) & 3u;
     const uint32_t lo = 16u * l;  // this lane's offset within a row
@@ -185,6 +187,7 @@ DEV uint32_t crc_window(const uint8_t* lds, const Keys& K, const Win& d, uint32_
                 s[k] ^= (off == t) ? Tinj : 0u;
             }
         }
+        if (i == 8 && do_mid) mid();  // rows 0..7 are free: room for the caller's loads
         if (i < 15) {
 #pragma unroll
             for (int k = 0; k < 4; k++) s[k] = braid_step(lds, K, s[k], w[k]);
@@ -226,8 +229,12 @@ DEV uint32_t crc_tail(const uint8_t* lds, const Stream& st, const uint4& gt, uin
 // CRC state after [S, E) from the state Tst at S.  d holds window 0 on entry
 // (issued by the caller); gt the tail row.  The < 4 bytes up to the first
 // 4-aligned position are folded in first (scalar load), so the window only
-// injects at a word boundary.
-DEV uint32_t crc_stream(const uint8_t* lds, const Keys& K, const Stream& st, Win& d, const uint4& gt, uint32_t Tst) {
+// injects at a word boundary.  mid() runs once, half-way through the last
+// window (or at the end when there is none).
+template <typename Mid>
+DEV uint32_t crc_stream(const uint8_t* lds, const Keys& K, const Stream& st, Win& d, const uint4& gt, uint32_t Tst,
+                        Mid&& mid) {
+    bool mid_done = false;
     if (st.R) {
         const uint64_t S4 = (st.S + 3) & ~3ull;
         if (S4 != st.S) {
@@ -235,75 +242,35 @@ DEV uint32_t crc_stream(const uint8_t* lds, const Keys& K, const Stream& st, Win
             for (uint64_t x = st.S; x < S4; x++) Tst = byte_step(lds, Tst, (w >> (8 * (uint32_t)(x & 3))) & 0xFFu);
             Tst = uni32(Tst);
         }
-        for (uint64_t r = 0; r < st.R; r++) {
-            if (r) load_window(st, r, d);
-            const int64_t W0 = win_base(st, r);
-            const uint32_t o4 = r == 0 ? (uint32_t)((int64_t)S4 - W0) : 0u;
+        if (st.R == 1) {
+            // one window (the common case): mid() half-way through it
+            const uint32_t o4 = (uint32_t)((int64_t)S4 - win_base(st, 0));
             // S4 can sit exactly at the end of window 0 (S within 3 bytes of
             // it): that window holds no stream bytes and the state passes on
-            if (o4 < kWinBytes) Tst = crc_window(lds, K, d, o4, Tst);
+            if (o4 < kWinBytes) {
+                Tst = crc_window(lds, K, d, o4, Tst, true, mid);
+                mid_done = true;
+            }
+        } else {
+            for (uint64_t r = 0; r < st.R; r++) {
+                if (r) load_window(st, r, d);
+                const int64_t W0 = win_base(st, r);
+                const uint32_t o4 = r == 0 ? (uint32_t)((int64_t)S4 - W0) : 0u;
+                if (o4 < kWinBytes) Tst = crc_window(lds, K, d, o4, Tst, false, [] {});
+            }
         }
     }
+    if (!mid_done) mid();
     return crc_tail(lds, st, gt, Tst);
+}
+
+DEV uint32_t crc_stream(const uint8_t* lds, const Keys& K, const Stream& st, Win& d, const uint4& gt, uint32_t Tst) {
+    return crc_stream(lds, K, st, d, gt, Tst, [] {});
 }
 
 // ---------------------------------------------------------------------------
 // Record walk
 // ---------------------------------------------------------------------------
-
-// 16 bytes at payload offset q (wave-uniform) through the scalar cache:
-// the constant address space makes these s_load_dwordx4, which bypass the
-// vector-memory queue the window stream keeps full (and its in-order vmcnt).
-// The payload is read-only for the whole kernel.  Bytes past the payload are
-// whatever follows it (readable to a 16-byte boundary); callers bound every
-// use by the bytes available.
-DEV void s16(const uint8_t* p0, uint32_t q, uint32_t& r0, uint32_t& r1, uint32_t& r2, uint32_t& r3) {
-    const uintptr_t a = (uintptr_t)(p0 + q);
-    cu32* c = (cu32*)(a & ~(uintptr_t)3);
-    const uint32_t sh = (uint32_t)(a & 3);
-    const uint32_t w0 = c[0], w1 = c[1], w2 = c[2], w3 = c[3], w4 = c[4];
-    r0 = __builtin_amdgcn_alignbyte(w1, w0, sh);
-    r1 = __builtin_amdgcn_alignbyte(w2, w1, sh);
-    r2 = __builtin_amdgcn_alignbyte(w3, w2, sh);
-    r3 = __builtin_amdgcn_alignbyte(w4, w3, sh);
-}
-
-// Per-lane 32-byte read cache over global memory (L2-resident payload).
-// Positions are 32-bit offsets from the payload start p0 (a wave-uniform
-// pointer, so addresses are SGPR base + VGPR offset).  16-byte rows starting
-// at or past n read as zero; a row may run up to 15 bytes past the payload
-// (buffers are readable to a 16-byte boundary past their end).
-struct GCache {
-    uint32_t base;   // payload offset of lo (base + p0 is 16-byte aligned)
-    uint4 lo, hi;
-};
-
-// p0 is 16-byte aligned minus `mis` (= p0 & 15): row starts are kept on the
-// absolute 16-byte grid so every load is one aligned dwordx4
-DEV void gc12(const uint8_t* p0, uint32_t mis, uint32_t n, GCache& C, uint32_t q, uint32_t& r0, uint32_t& r1,
-              uint32_t& r2) {
-    // cache coordinates are absolute-grid offsets: g = q + mis
-    const uint32_t g = q + mis;
-    if (!(g >= C.base && g + 12 <= C.base + 32)) {
-        C.base = g & ~15u;
-        C.lo = make_uint4(0u, 0u, 0u, 0u);
-        C.hi = make_uint4(0u, 0u, 0u, 0u);
-        const uint8_t* row = p0 - mis + C.base;
-        if (C.base < n + mis) C.lo = *(const uint4*)row;
-        if (C.base + 16 < n + mis) C.hi = *(const uint4*)(row + 16);
-    }
-    const uint32_t o = g - C.base;
-    const uint32_t k = o >> 2, sh = o & 3u;
-    uint32_t w[4];
-#pragma unroll
-    for (int i = 0; i < 4; i++) {
-        const uint32_t kk = k + (uint32_t)i;  // 0..7
-        w[i] = kk < 4 ? pick4(C.lo, kk) : pick4(C.hi, kk - 4);
-    }
-    r0 = __builtin_amdgcn_alignbyte(w[1], w[0], sh);
-    r1 = __builtin_amdgcn_alignbyte(w[2], w[1], sh);
-    r2 = __builtin_amdgcn_alignbyte(w[3], w[2], sh);
-}
 
 // vint::deserialize (utils/vint.h:82-98) over at most `avail` bytes: LEB128
 // stopping after 10 bytes, or at the end of input with the partial value.
@@ -330,42 +297,69 @@ DEV int64_t varint12(uint32_t r0, uint32_t r1, uint32_t r2, uint32_t avail, uint
     return (int64_t)((res >> 1) ^ (~(res & 1) + 1));
 }
 
+// Per-lane 48-byte register regions of the payload: three aligned 16-byte
+// rows in grid coordinates (g = payload offset + mis, mis = p0 & 15, so every
+// row is one aligned dwordx4).  Rows starting at or past the payload end read
+// as zero; a row may run up to 15 bytes past it (buffers are readable to a
+// 16-byte boundary past their end).
+struct Region {
+    uint32_t base;  // grid offset of r0
+    uint4 r0, r1, r2;
+};
+
+DEV void load_region(const uint8_t* p0, uint32_t mis, uint32_t n, uint32_t base, Region& R) {
+    const uint8_t* row = p0 - mis + base;
+    const uint32_t lim = n + mis;
+    R.base = base;
+    R.r0 = R.r1 = R.r2 = make_uint4(0u, 0u, 0u, 0u);
+    if (base < lim) R.r0 = *(const uint4*)row;
+    if (base + 16u < lim) R.r1 = *(const uint4*)(row + 16);
+    if (base + 32u < lim) R.r2 = *(const uint4*)(row + 32);
+}
+
+// dword k (0..11) of a region, selected by value (per-lane k)
+DEV uint32_t pick12(const Region& R, uint32_t k) {
+    const uint32_t a = pick4(R.r0, k), b = pick4(R.r1, k), c = pick4(R.r2, k);
+    return k < 4u ? a : (k < 8u ? b : c);
+}
+
+// The record parser's byte source: the current region A, the record's tail
+// region T (handed over up front), else a fresh region at the read position
+// (one dependent load).
 struct Reader {
     const uint8_t* p0;  // payload start (wave-uniform)
     uint32_t mis;       // p0 & 15
     uint32_t n;
     uint32_t pos;
-    uint32_t hs;        // payload offset of head (the 16 bytes the chain handed over)
-    uint4 head;
-    GCache C;
+    Region A, T;
 
-    DEV uint32_t head_dword(uint32_t k) const { return k < 4u ? pick4(head, k) : 0u; }
-
-    // iobuf_parser_base::read_varlong (bytes/iobuf_parser.h:48-52).  One- and
-    // two-byte varints inside the head are decoded without a load.
-    DEV int64_t varlong() {
-        uint32_t r0, r1, r2, br;
-        const uint32_t o = pos - hs;  // huge when pos < hs
-        const uint32_t avail = n - pos;
-        if (o <= 12u) {
-            r0 = __builtin_amdgcn_alignbyte(head_dword((o >> 2) + 1), head_dword(o >> 2), o & 3u);
-            if (avail < 2 || (r0 & 0x8080u) != 0x8080u) {
-                const int64_t x = varint12(r0, 0u, 0u, avail, br);
-                pos += br;
-                return x;
-            }
+    // region offset of pos, switching regions so 12 bytes from it are held
+    DEV uint32_t locate() {
+        const uint32_t g = pos + mis;
+        if (g - A.base > 32u) {
+            if (g - T.base <= 32u) A = T;
+            else load_region(p0, mis, n, g & ~15u, A);
         }
-        gc12(p0, mis, n, C, pos, r0, r1, r2);
+        return g - A.base;
+    }
+
+    // iobuf_parser_base::read_varlong (bytes/iobuf_parser.h:48-52)
+    DEV int64_t varlong() {
+        const uint32_t o = locate(), k = o >> 2, sh = o & 3u, avail = n - pos;
+        const uint32_t w0 = pick12(A, k), w1 = pick12(A, k + 1u);
+        uint32_t r0 = __builtin_amdgcn_alignbyte(w1, w0, sh), r1 = 0u, r2 = 0u, br;
+        if (avail >= 2 && (r0 & 0x8080u) == 0x8080u) {
+            const uint32_t w2 = pick12(A, k + 2u), w3 = pick12(A, k + 3u);
+            r1 = __builtin_amdgcn_alignbyte(w2, w1, sh);
+            r2 = __builtin_amdgcn_alignbyte(w3, w2, sh);
+        }
         const int64_t x = varint12(r0, r1, r2, avail, br);
         pos += br;
         return x;
     }
     DEV uint32_t byte() {
-        const uint32_t o = pos - hs;
-        if (o <= 15u) return (head_dword(o >> 2) >> (8 * (o & 3u))) & 0xFFu;
-        uint32_t r0, r1, r2;
-        gc12(p0, mis, n, C, pos, r0, r1, r2);
-        return r0 & 0xFFu;
+        const uint32_t o = locate();
+        return (pick12(A, o >> 2) >> (8u * (o & 3u))) & 0xFFu;
     }
 };
 
@@ -390,17 +384,17 @@ struct Rec {
 
 // parse_one_record_copy_from_buffer (model/record_utils.cc:170-177) over
 // parse_record_meta_from_buffer / do_parse_one_record_from_buffer /
-// parse_record_headers (:94-160)
-DEV Rec parse_record(const uint8_t* p0, uint32_t mis, uint32_t n, uint32_t start, const uint4& head) {
+// parse_record_headers (:94-160) from the record start, with the head and
+// tail regions already loaded (record_regions).
+DEV Rec parse_record(const uint8_t* p0, uint32_t mis, uint32_t n, uint32_t start, const Region& H, const Region& T) {
     Rec r;
     Reader c;
     c.p0 = p0;
     c.mis = mis;
     c.n = n;
     c.pos = start;
-    c.hs = start;
-    c.head = head;
-    c.C.base = 0xFFFFFFF0u;
+    c.A = H;
+    c.T = T;
     r.err = 0;
     r.key_pos = r.val_pos = r.hdr_pos = 0;
     r.ts = 0; r.length = r.off = r.klen = r.vlen = r.hcount = 0; r.attr = 0;
@@ -437,32 +431,72 @@ DEV Rec parse_record(const uint8_t* p0, uint32_t mis, uint32_t n, uint32_t start
     return r;
 }
 
+// Head and tail regions of a lane's record, issued together: three 16-byte
+// rows at the start and three ending at (or just past) the chain's guess of
+// its end, where the headers sit.  A typical record then costs one memory
+// latency, whatever its length.
+DEV void record_regions(const uint8_t* p0, uint32_t mis, uint32_t n, bool act, uint32_t start, uint32_t end,
+                        Region& H, Region& T) {
+    H.base = T.base = 0xFFFFFFF0u;
+    H.r0 = H.r1 = H.r2 = T.r0 = T.r1 = T.r2 = make_uint4(0u, 0u, 0u, 0u);
+    if (act) {
+        const uint32_t hb = (start + mis) & ~15u;
+        const uint32_t e16 = (end + mis + 15u) & ~15u;
+        const uint32_t tb = (end != 0xFFFFFFFFu && e16 >= hb + 48u) ? e16 - 48u : hb;
+        load_region(p0, mis, n, hb, H);
+        load_region(p0, mis, n, tb, T);
+    }
+}
+
 struct WalkResult {
     uint32_t parsed;
     uint32_t err;
     uint32_t trailing;
 };
 
-// Speculative record starts for records [done, done + want): a uniform chain
-// over the length varints from `start` (scalar loads).  Lane m gets the
-// start of record done + m and the 16 bytes there (its parse starts from
-// them); returns how many lanes got one.
-DEV uint32_t chain_starts(const uint8_t* p0, uint32_t n, uint32_t start, uint32_t want, uint32_t& my_start,
-                          uint4& head) {
+// 12 bytes at payload offset q (wave-uniform) through the scalar cache: the
+// constant address space makes these s_loads, off the vector-memory queue
+// the window stream keeps full.  The payload is read-only for the whole
+// kernel; callers bound every use by the bytes available.
+DEV void s12(const uint8_t* p0, uint32_t q, uint32_t& r0, uint32_t& r1, uint32_t& r2) {
+    const uintptr_t a = (uintptr_t)(p0 + q);
+    cu32* c = (cu32*)(a & ~(uintptr_t)3);
+    const uint32_t sh = (uint32_t)(a & 3);
+    const uint32_t w0 = c[0], w1 = c[1], w2 = c[2], w3 = c[3];
+    r0 = __builtin_amdgcn_alignbyte(w1, w0, sh);
+    r1 = __builtin_amdgcn_alignbyte(w2, w1, sh);
+    r2 = __builtin_amdgcn_alignbyte(w3, w2, sh);
+}
+
+// Byte source of the chain: 12 bytes at payload offset p (wave-uniform)
+// through the scalar cache.  (A source reading a one-window payload from the
+// window registers with v_movrels + v_readlane measured 2.3x slower per
+// record than these loads.)
+struct MemSrc {
+    const uint8_t* p0;
+    DEV void read(uint32_t p, uint32_t, uint32_t& r0, uint32_t& r1, uint32_t& r2) const { s12(p0, p, r0, r1, r2); }
+};
+// Speculative record starts and ends for records [done, done + want): a
+// uniform chain over the length varints from `start`.  Lane m gets the start
+// of record done + m and the position after it (the next start); returns how
+// many lanes got a start.
+template <typename Src>
+DEV uint32_t chain_starts(const Src& src, uint32_t n, uint32_t start, uint32_t want, uint32_t& my_start,
+                          uint32_t& my_end) {
     const uint32_t l = lane();
-    my_start = 0xFFFFFFFFu;
-    head = make_uint4(0u, 0u, 0u, 0u);
+    my_start = my_end = 0xFFFFFFFFu;
     uint32_t p = start;
     uint32_t m = 0;
     for (; m < want; m++) {
         if (l == m) my_start = p;
         if (p >= n) { m++; break; }
-        uint32_t r0, r1, r2, r3, br;
-        s16(p0, p, r0, r1, r2, r3);
-        if (l == m) head = make_uint4(r0, r1, r2, r3);
-        const int64_t len = varint12(r0, r1, r2, n - p, br);
+        const uint32_t avail = n - p;
+        uint32_t r0, r1, r2, br;
+        src.read(p, avail, r0, r1, r2);
+        const int64_t len = varint12(r0, r1, r2, avail, br);
         if (len < 0 || (uint64_t)len > n) { m++; break; }
         p = uni32(p + br + (uint32_t)len);
+        if (l == m) my_end = p;
     }
     return m;
 }
@@ -470,13 +504,13 @@ DEV uint32_t chain_starts(const uint8_t* p0, uint32_t n, uint32_t start, uint32_
 // Lanes [0, m) parse one record each from their speculative starts; the
 // prefix whose starts are confirmed by the previous record's exact end is
 // committed to the index.  Returns false when a record failed (wr filled).
-DEV bool parse_group(const uint8_t* p0, uint32_t mis, uint32_t n, uint32_t m, uint32_t my_start, const uint4& head,
-                     uint32_t batch_ord,
+DEV bool parse_group(const uint8_t* p0, uint32_t mis, uint32_t n, uint32_t m, uint32_t my_start, const Region& H,
+                     const Region& T, uint32_t batch_ord,
                      rpgpu_record_index* out, uint64_t out_cap, uint32_t& done, uint32_t& start, WalkResult& wr) {
     const uint32_t l = lane();
     Rec r;
     const bool act = l < m;
-    if (act) r = parse_record(p0, mis, n, my_start, head);
+    if (act) r = parse_record(p0, mis, n, my_start, H, T);
     else { r.err = 0; r.end = 0xFFFFFFFFu; }
     // lane l - 1's values (DPP wave_shr:1; lane 0 ignores them)
     const uint32_t prev_end = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)r.end, 0x138, 0xF, 0xF, false);
@@ -516,17 +550,25 @@ DEV bool parse_group(const uint8_t* p0, uint32_t mis, uint32_t n, uint32_t m, ui
 }
 
 // record_batch::for_each_record (model/record.h:616-627) with speculative
-// lane-parallel records: chain_starts guesses 64 record starts at a time,
-// parse_group parses and commits the confirmed prefix.  first: the first
-// group's chain already ran (m0 lanes, my_start0 / head0).
+// lane-parallel records: chain_starts guesses 64 record starts (and ends) at
+// a time, record_regions loads each lane's head and tail rows, parse_group
+// parses and commits the confirmed prefix.  The first group may be prepared
+// by the caller around the CRC (Group: chain before it, regions issued
+// half-way through it).
 struct Group {
     bool first;
-    uint32_t m, my_start;
-    uint4 head;
+    uint32_t m, my_start, my_end;
+    Region H, T;
 };
 
+DEV void group_init(Group& g) {
+    g.first = false;
+    g.m = 0;
+    g.my_start = g.my_end = 0xFFFFFFFFu;
+}
+
 DEV WalkResult walk_records(const uint8_t* p0, uint32_t n, int32_t rc, uint32_t batch_ord, rpgpu_record_index* out,
-                            uint64_t out_cap, const Group& g0) {
+                            uint64_t out_cap, Group& g) {
     WalkResult wr;
     wr.parsed = 0;
     wr.err = 0;
@@ -534,21 +576,24 @@ DEV WalkResult walk_records(const uint8_t* p0, uint32_t n, int32_t rc, uint32_t 
     const uint32_t mis = (uint32_t)((uintptr_t)p0 & 15);
     const uint32_t total = (uint32_t)(rc > 0 ? rc : 0);
     uint32_t start = 0, done = 0;
-    while (done < total) {
-        uint32_t my_start, m;
-        uint4 head;
-        if (done == 0 && g0.first) {
-            m = g0.m;
-            my_start = g0.my_start;
-            head = g0.head;
-        } else {
-            const uint32_t want = (total - done) < 64u ? (total - done) : 64u;
-            STAMP(w0);
-            m = chain_starts(p0, n, start, want, my_start, head);
-            STAMP(w1);
-            STAMP_ADD(6, w1 - w0);
-        }
-        if (!parse_group(p0, mis, n, m, my_start, head, batch_ord, out, out_cap, done, start, wr)) return wr;
+    if (total == 0) {
+        wr.trailing = n;
+        return wr;
+    }
+    const MemSrc mem{p0};
+    if (!g.first) {
+        STAMP(w0);
+        g.m = chain_starts(mem, n, 0u, total < 64u ? total : 64u, g.my_start, g.my_end);
+        record_regions(p0, mis, n, lane() < g.m, g.my_start, g.my_end, g.H, g.T);
+        STAMP(w1);
+        STAMP_ADD(6, w1 - w0);
+    }
+    for (;;) {
+        if (!parse_group(p0, mis, n, g.m, g.my_start, g.H, g.T, batch_ord, out, out_cap, done, start, wr)) return wr;
+        if (done >= total) break;
+        const uint32_t want = (total - done) < 64u ? (total - done) : 64u;
+        g.m = chain_starts(mem, n, start, want, g.my_start, g.my_end);
+        record_regions(p0, mis, n, lane() < g.m, g.my_start, g.my_end, g.H, g.T);
     }
     wr.parsed = done;
     wr.trailing = n - start;
@@ -632,7 +677,7 @@ DEV Stream stored_stream(const DeviceJob& j, const Desc& d, bool valid) {
 
 // the record walk of one payload into the batch's index slots
 DEV WalkResult walk_batch(const DeviceJob& j, const Desc& ds, const uint8_t* p0, uint32_t n, uint64_t b, bool& idx_ok,
-                          const Group& g0) {
+                          Group& g0) {
     idx_ok = ds.ib + ds.islots <= j.record_capacity;
     rpgpu_record_index* out = idx_ok ? j.records + ds.ib : nullptr;
     const uint64_t cap = idx_ok ? ds.islots : 0;
@@ -743,19 +788,23 @@ __global__ __launch_bounds__(1024) void k_validate(DeviceJob j) {
             // with them; after the CRC they would be evicted again)
             const bool walk = d.codec == 0 && (j.flags & RPGPU_JOB_PARSE);
             Group g0;
+            group_init(g0);
             g0.first = walk && d.rc > 0;
-            g0.m = 0;
-            g0.my_start = 0xFFFFFFFFu;
-            g0.head = make_uint4(0u, 0u, 0u, 0u);
+            const uint8_t* p0 = j.data + d.S;
+            const uint32_t n = (uint32_t)d.n;
             if (g0.first) {
                 const uint32_t total = (uint32_t)d.rc;
-                g0.m = chain_starts(j.data + d.S, (uint32_t)d.n, 0u, total < 64u ? total : 64u, g0.my_start, g0.head);
+                g0.m = chain_starts(MemSrc{p0}, n, 0u, total < 64u ? total : 64u, g0.my_start, g0.my_end);
             }
             STAMP(tb);
             STAMP_ADD(6, tb - ta);
             // stored payload: batch crc.  CRC state after the BE40 prefix with
-            // init ~0 = c40 ^ the prefix's raw contribution (from k_emit)
+            // init ~0 = c40 ^ the prefix's raw contribution (from k_emit).
+            // Half-way through, the first group's head and tail rows are
+            // issued into the registers the CRC has freed.
             const uint32_t crc = ~crc_stream(lds, K, st, v, gt, d.praw ^ c40);
+                record_regions(p0, (uint32_t)((uintptr_t)p0 & 15), n, g0.first && lane() < g0.m, g0.my_start,
+                               g0.my_end, g0.H, g0.T);
             STAMP(tb2);
             STAMP_ADD(0, tb2 - tb);
             if (crc == d.crc) f |= RPGPU_F_CRC_OK;
@@ -763,7 +812,7 @@ __global__ __launch_bounds__(1024) void k_validate(DeviceJob j) {
             prefetch();
             if (walk) {
                 bool idx_ok;
-                const WalkResult w = walk_batch(j, d, j.data + d.S, (uint32_t)d.n, b, idx_ok, g0);
+                const WalkResult w = walk_batch(j, d, p0, n, b, idx_ok, g0);
                 f |= walk_flags(j, w, idx_ok, perr);
                 parsed = w.parsed;
             }
@@ -837,10 +886,7 @@ __global__ __launch_bounds__(1024) void k_validate_decoded(DeviceJob j) {
         if (j.flags & RPGPU_JOB_PARSE) {
             bool idx_ok;
             Group g0;
-            g0.first = false;
-            g0.m = 0;
-            g0.my_start = 0xFFFFFFFFu;
-            g0.head = make_uint4(0u, 0u, 0u, 0u);
+            group_init(g0);
             const WalkResult w = walk_batch(j, d, j.decoded + d.doff, (uint32_t)dl, b, idx_ok, g0);
             f |= walk_flags(j, w, idx_ok, perr);
             parsed = w.parsed;
