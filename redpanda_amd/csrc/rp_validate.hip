@@ -39,6 +39,16 @@ __shared__ unsigned long long s_stamps[kVWaves][8];  // per-wave, flushed once a
 
 DEV uint32_t L32(const uint8_t* lds, uint32_t a) { return *(const uint32_t*)(lds + a); }
 
+// The lane id from a volatile asm: values derived from it cannot be hoisted
+// out of the batch loop (loop-invariant per-lane pointers and masks would
+// otherwise stay live for the whole kernel and push it into spills; they
+// cost two VALU to recompute)
+DEV uint32_t lane_v() {
+    uint32_t r;
+    asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(r));
+    return r;
+}
+
 // constant address space: wave-uniform loads through it become s_load (the
 // scalar cache), off the vector-memory queue the window stream keeps busy
 typedef const __attribute__((address_space(4))) uint32_t cu32;
@@ -53,33 +63,40 @@ constexpr uint32_t kSel1 = 0x0C020500u;  // x byte 1
 constexpr uint32_t kSel2 = 0x0C020600u;  // x byte 2
 constexpr uint32_t kSel3 = 0x0C020700u;  // x byte 3
 
-// s' = T1023[x0] ^ T1022[x1] ^ T1021[x2] ^ T1020[x3], x = s ^ w: the CRC of
-// the word followed by the 1020 bytes of the other braids.
-DEV uint32_t braid_step(const uint8_t* lds, const Keys& K, uint32_t s, uint32_t w) {
-    const uint32_t x = s ^ w;
+DEV uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) { return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96); }
+
+// One braid step from x = s ^ w: s' = T1023[x0] ^ T1022[x1] ^ T1021[x2] ^
+// T1020[x3], the CRC of the word followed by the 1020 bytes of the other
+// braids.  The state is kept as the pair (p, q) with s' = p ^ q, so the next
+// step's x is one 3-input XOR (v_bitop3) with the next word.
+DEV void braid_step(const uint8_t* lds, const Keys& K, uint32_t x, uint32_t& p, uint32_t& q) {
     const uint32_t a = L32(lds, __builtin_amdgcn_perm(x, K.k15, kSel0));
     const uint32_t b = L32(lds, __builtin_amdgcn_perm(x, K.k14, kSel1));
     const uint32_t c = L32(lds, __builtin_amdgcn_perm(x, K.k13, kSel2));
     const uint32_t d = L32(lds, __builtin_amdgcn_perm(x, K.k12, kSel3));
-    return (a ^ b) ^ (c ^ d);
+    p = xor3(a, b, c);
+    q = d;
 }
 
-// slice-by-4 word step (T3..T0, single copy)
-DEV uint32_t word_step(const uint8_t* lds, uint32_t s, uint32_t w) {
-    const uint32_t x = s ^ w;
-    return (L32(lds, kLdsSlice4Off + ((x & 0xFFu) << 2)) ^ L32(lds, kLdsSlice4Off + 1024u + ((x >> 6) & 0x3FCu))) ^
-           (L32(lds, kLdsSlice4Off + 2048u + ((x >> 14) & 0x3FCu)) ^ L32(lds, kLdsSlice4Off + 3072u + ((x >> 22) & 0x3FCu)));
+// slice-by-4 word step (T3..T0, single copy) from x = s ^ w, xored with e
+DEV uint32_t word_step_x(const uint8_t* lds, uint32_t x, uint32_t e) {
+    return xor3(xor3(L32(lds, kLdsSlice4Off + ((x & 0xFFu) << 2)), L32(lds, kLdsSlice4Off + 1024u + ((x >> 6) & 0x3FCu)),
+                     L32(lds, kLdsSlice4Off + 2048u + ((x >> 14) & 0x3FCu))),
+                L32(lds, kLdsSlice4Off + 3072u + ((x >> 22) & 0x3FCu)), e);
 }
+
+DEV uint32_t word_step(const uint8_t* lds, uint32_t s, uint32_t w) { return word_step_x(lds, s ^ w, 0u); }
 
 DEV uint32_t byte_step(const uint8_t* lds, uint32_t s, uint32_t b) {
     return L32(lds, kLdsSlice4Off + 3072u + (((s ^ b) & 0xFFu) << 2)) ^ (s >> 8);
 }
 
-// advance a raw CRC state over 16 << k zero bytes
-DEV uint32_t shift_k(const uint8_t* lds, uint32_t s, uint32_t k) {
+// advance a raw CRC state over 16 << k zero bytes, xored with e
+DEV uint32_t shift_k(const uint8_t* lds, uint32_t s, uint32_t k, uint32_t e) {
     const uint32_t base = kLdsShiftOff + k * 4096u;
-    return (L32(lds, base + ((s & 0xFFu) << 2)) ^ L32(lds, base + 1024u + ((s >> 6) & 0x3FCu))) ^
-           (L32(lds, base + 2048u + ((s >> 14) & 0x3FCu)) ^ L32(lds, base + 3072u + ((s >> 22) & 0x3FCu)));
+    return xor3(xor3(L32(lds, base + ((s & 0xFFu) << 2)), L32(lds, base + 1024u + ((s >> 6) & 0x3FCu)),
+                     L32(lds, base + 2048u + ((s >> 14) & 0x3FCu))),
+                L32(lds, base + 3072u + ((s >> 22) & 0x3FCu)), e);
 }
 
 // select a dword by index from values (never from addresses: a select of
@@ -123,7 +140,7 @@ DEV int64_t win_base(const Stream& st, uint64_t r) {
 // window r, coalesced: row i of every lane is one 1 KiB wave load (rows
 // wholly outside [S, E16) are zero)
 DEV void load_window(const Stream& st, uint64_t r, Win& w) {
-    const int64_t a = win_base(st, r) + 16 * (int64_t)lane();
+    const int64_t a = win_base(st, r) + 16 * (int64_t)lane_v();
 #pragma unroll
     for (int i = 0; i < 16; i++) {
         const int64_t q = a + 1024 * i;
@@ -137,7 +154,7 @@ DEV void load_window(const Stream& st, uint64_t r, Win& w) {
 // window in two parts)
 template <int I0, int I1>
 DEV void load_rows(const Stream& st, Win& w) {
-    const int64_t a = win_base(st, 0) + 16 * (int64_t)lane();
+    const int64_t a = win_base(st, 0) + 16 * (int64_t)lane_v();
 #pragma unroll
     for (int i = I0; i < I1; i++) {
         const int64_t q = a + 1024 * i;
@@ -167,10 +184,11 @@ DEV uint32_t swz_xor(uint32_t v) {
 template <typename Mid>
 DEV uint32_t crc_window(const uint8_t* lds, const Keys& K, const Win& d, uint32_t o4, uint32_t Tinj, bool do_mid,
                         Mid&& mid) {
-    const uint32_t l = lane();
+    const uint32_t l = lane_v();
     const uint32_t i4 = o4 >> 10, l4 = (o4 >> 4) & 63u, k4 = (o4 >> 2) & 3u;
     const uint32_t lo = 16u * l;  // this lane's offset within a row
-    uint32_t s[4] = {0u, 0u, 0u, 0u};
+    uint32_t p[4] = {0u, 0u, 0u, 0u}, q[4] = {0u, 0u, 0u, 0u};  // braid k's state is p[k] ^ q[k]
+    uint32_t s0 = 0;
 #pragma unroll
     for (int i = 0; i < 16; i++) {
         uint32_t w[4] = {d.r[i].x, d.r[i].y, d.r[i].z, d.r[i].w};
@@ -184,19 +202,19 @@ DEV uint32_t crc_window(const uint8_t* lds, const Keys& K, const Win& d, uint32_
             for (int k = 0; k < 4; k++) {
                 const int32_t off = (int32_t)(lo + 4u * (uint32_t)k);
                 w[k] = off >= t ? w[k] : 0u;
-                s[k] ^= (off == t) ? Tinj : 0u;
+                p[k] ^= (off == t) ? Tinj : 0u;
             }
         }
         if (i == 8 && do_mid) mid();  // rows 0..7 are free: room for the caller's loads
         if (i < 15) {
 #pragma unroll
-            for (int k = 0; k < 4; k++) s[k] = braid_step(lds, K, s[k], w[k]);
+            for (int k = 0; k < 4; k++) braid_step(lds, K, xor3(p[k], q[k], w[k]), p[k], q[k]);
         } else {
-            // row 15: fold the braids (s_k sits at word k) with word steps
-            uint32_t c = word_step(lds, s[0], w[0]) ^ s[1];
-            c = word_step(lds, c, w[1]) ^ s[2];
-            c = word_step(lds, c, w[2]) ^ s[3];
-            s[0] = word_step(lds, c, w[3]);
+            // row 15: fold the braids (braid k sits at word k) with word steps
+            uint32_t c = word_step_x(lds, xor3(p[0], q[0], w[0]), p[1] ^ q[1]);
+            c = word_step_x(lds, c ^ w[1], p[2] ^ q[2]);
+            c = word_step_x(lds, c ^ w[2], p[3] ^ q[3]);
+            s0 = word_step_x(lds, c ^ w[3], 0u);
         }
     }
     // lane l's state sits 16 (63 - l) bytes before the window end:
@@ -205,13 +223,13 @@ DEV uint32_t crc_window(const uint8_t* lds, const Keys& K, const Win& d, uint32_
     // exchange is an xor swizzle (immediate pattern, no address VGPR) and the
     // last level a readlane of lane 32.
     static_assert(kShiftLevels == 6, "shift tree is written out for 64 lanes");
-    uint32_t sv = s[0];
-    sv = shift_k(lds, sv, 0) ^ swz_xor<1>(sv);
-    sv = shift_k(lds, sv, 1) ^ swz_xor<2>(sv);
-    sv = shift_k(lds, sv, 2) ^ swz_xor<4>(sv);
-    sv = shift_k(lds, sv, 3) ^ swz_xor<8>(sv);
-    sv = shift_k(lds, sv, 4) ^ swz_xor<16>(sv);
-    return shift_k(lds, uni32(sv), 5) ^ rl(sv, 32);
+    uint32_t sv = s0;
+    sv = shift_k(lds, sv, 0, swz_xor<1>(sv));
+    sv = shift_k(lds, sv, 1, swz_xor<2>(sv));
+    sv = shift_k(lds, sv, 2, swz_xor<4>(sv));
+    sv = shift_k(lds, sv, 3, swz_xor<8>(sv));
+    sv = shift_k(lds, sv, 4, swz_xor<16>(sv));
+    return shift_k(lds, uni32(sv), 5, rl(sv, 32));
 }
 
 // fold the tail bytes [max(S, E16), E) held in gt into the state (uniform)
@@ -252,11 +270,14 @@ DEV uint32_t crc_stream(const uint8_t* lds, const Keys& K, const Stream& st, Win
                 mid_done = true;
             }
         } else {
-            for (uint64_t r = 0; r < st.R; r++) {
-                if (r) load_window(st, r, d);
-                const int64_t W0 = win_base(st, r);
-                const uint32_t o4 = r == 0 ? (uint32_t)((int64_t)S4 - W0) : 0u;
-                if (o4 < kWinBytes) Tst = crc_window(lds, K, d, o4, Tst, false, [] {});
+            // window 0 from the caller, then a fresh window per iteration (a
+            // window carried around the loop would be copied and spilled)
+            const uint32_t o4 = (uint32_t)((int64_t)S4 - win_base(st, 0));
+            if (o4 < kWinBytes) Tst = crc_window(lds, K, d, o4, Tst, false, [] {});
+            for (uint64_t r = 1; r < st.R; r++) {
+                Win w;
+                load_window(st, r, w);
+                Tst = crc_window(lds, K, w, 0u, Tst, false, [] {});
             }
         }
     }
@@ -483,7 +504,7 @@ struct MemSrc {
 template <typename Src>
 DEV uint32_t chain_starts(const Src& src, uint32_t n, uint32_t start, uint32_t want, uint32_t& my_start,
                           uint32_t& my_end) {
-    const uint32_t l = lane();
+    const uint32_t l = lane_v();
     my_start = my_end = 0xFFFFFFFFu;
     uint32_t p = start;
     uint32_t m = 0;
@@ -507,7 +528,7 @@ DEV uint32_t chain_starts(const Src& src, uint32_t n, uint32_t start, uint32_t w
 DEV bool parse_group(const uint8_t* p0, uint32_t mis, uint32_t n, uint32_t m, uint32_t my_start, const Region& H,
                      const Region& T, uint32_t batch_ord,
                      rpgpu_record_index* out, uint64_t out_cap, uint32_t& done, uint32_t& start, WalkResult& wr) {
-    const uint32_t l = lane();
+    const uint32_t l = lane_v();
     Rec r;
     const bool act = l < m;
     if (act) r = parse_record(p0, mis, n, my_start, H, T);
@@ -584,7 +605,7 @@ DEV WalkResult walk_records(const uint8_t* p0, uint32_t n, int32_t rc, uint32_t 
     if (!g.first) {
         STAMP(w0);
         g.m = chain_starts(mem, n, 0u, total < 64u ? total : 64u, g.my_start, g.my_end);
-        record_regions(p0, mis, n, lane() < g.m, g.my_start, g.my_end, g.H, g.T);
+        record_regions(p0, mis, n, lane_v() < g.m, g.my_start, g.my_end, g.H, g.T);
         STAMP(w1);
         STAMP_ADD(6, w1 - w0);
     }
@@ -593,7 +614,7 @@ DEV WalkResult walk_records(const uint8_t* p0, uint32_t n, int32_t rc, uint32_t 
         if (done >= total) break;
         const uint32_t want = (total - done) < 64u ? (total - done) : 64u;
         g.m = chain_starts(mem, n, start, want, g.my_start, g.my_end);
-        record_regions(p0, mis, n, lane() < g.m, g.my_start, g.my_end, g.H, g.T);
+        record_regions(p0, mis, n, lane_v() < g.m, g.my_start, g.my_end, g.H, g.T);
     }
     wr.parsed = done;
     wr.trailing = n - start;
@@ -604,19 +625,25 @@ DEV WalkResult walk_records(const uint8_t* p0, uint32_t n, int32_t rc, uint32_t 
 // reset_size_checksum_metadata produces: codec bits cleared, size_bytes =
 // 61 + decoded, crc = the decoded crc (storage/parser_utils.cc:53-56, 114-120)
 DEV uint32_t decoded_header_crc(const Tables* T, const uint8_t* hdr, uint32_t new_size, uint32_t new_crc) {
-    const uint32_t l = lane();
+    const uint32_t l = lane_v();
     uint32_t b = (l < RPGPU_HEADER_SIZE) ? (uint32_t)hdr[l] : 0u;
     if (l >= 4 && l < 8) b = (new_size >> (8 * (l - 4))) & 0xFFu;
     if (l >= 17 && l < 21) b = (new_crc >> (8 * (l - 17))) & 0xFFu;
     if (l == 21) b &= ~7u;
-    const uint32_t contrib = (l >= 4 && l < RPGPU_HEADER_SIZE) ? T->hdr[60 - l][b] : 0u;
-    return ~(T->c57 ^ wave_xor(contrib));
+    uint32_t x = (l >= 4 && l < RPGPU_HEADER_SIZE) ? T->hdr[60 - l][b] : 0u;
+    // xor over the wave with immediate-pattern swizzles (no address VGPRs)
+    x ^= swz_xor<1>(x);
+    x ^= swz_xor<2>(x);
+    x ^= swz_xor<4>(x);
+    x ^= swz_xor<8>(x);
+    x ^= swz_xor<16>(x);
+    return ~(T->c57 ^ rl(x, 0) ^ rl(x, 32));
 }
 
 // first batch of segment s failing complete && crc_ok (log_replayer
 // checkpoint, storage/log_replayer.cc:62-79); resolved by k_finalize_segments
 DEV void note_bad(const DeviceJob& j, uint32_t seg, uint64_t b) {
-    if (lane() == 0) {
+    if (lane_v() == 0) {
         const uint64_t first = j.chunk_count[j.chunk_base[seg]];
         atomicMin(&j.seg_first_bad[seg], (uint32_t)(b - first));
     }
@@ -639,7 +666,7 @@ constexpr int kDwPraw = offsetof(rpgpu_batch_result, reserved1) / 4;
 static_assert(sizeof(rpgpu_batch_result) == 128 && offsetof(rpgpu_batch_result, attrs) % 4 == 0, "desc layout");
 
 DEV uint32_t load_desc_raw(const DeviceJob& j, uint64_t b) {
-    const uint32_t l = lane();
+    const uint32_t l = lane_v();
     const uint32_t* p = l < 32u ? (const uint32_t*)&j.batches[b] + l
                       : l < 34u ? (const uint32_t*)&j.slots[b] + (l - 32u)
                       : l < 36u ? (const uint32_t*)&j.slots[b + 1] + (l - 34u)
@@ -702,7 +729,7 @@ DEV void init_lds_tables(uint8_t* lds, const Tables* T) {
 
 // this lane's copy of the four braid tables
 DEV Keys make_keys() {
-    const uint32_t bank = (lane() & 31u) * 4u;
+    const uint32_t bank = (lane_v() & 31u) * 4u;
     Keys K;
     K.k15 = (0u << 16) | (0u + bank);
     K.k14 = (0u << 16) | (128u + bank);
@@ -722,7 +749,7 @@ DEV uint32_t walk_flags(const DeviceJob& j, const WalkResult& w, bool idx_ok, ui
     }
     if (f & RPGPU_F_PARSE_OK) {
         if (idx_ok) f |= RPGPU_F_INDEX_WRITTEN;
-        else { perr = RPGPU_PARSE_ERR_INDEX_CAPACITY; if (lane() == 0) atomicOr(&j.counters[1], 2u); }
+        else { perr = RPGPU_PARSE_ERR_INDEX_CAPACITY; if (lane_v() == 0) atomicOr(&j.counters[1], 2u); }
     }
     return f;
 }
@@ -739,7 +766,7 @@ __global__ __launch_bounds__(1024) void k_validate(DeviceJob j) {
     const Tables* T = j.tables;
     const uint32_t tid = threadIdx.x;
     init_lds_tables(lds, T);
-    const uint32_t l = lane();
+    const uint32_t l = lane_v();
     const Keys K = make_keys();
     const uint32_t c40 = uni32(T->c40);
 
@@ -803,7 +830,7 @@ __global__ __launch_bounds__(1024) void k_validate(DeviceJob j) {
             // Half-way through, the first group's head and tail rows are
             // issued into the registers the CRC has freed.
             const uint32_t crc = ~crc_stream(lds, K, st, v, gt, d.praw ^ c40);
-                record_regions(p0, (uint32_t)((uintptr_t)p0 & 15), n, g0.first && lane() < g0.m, g0.my_start,
+                record_regions(p0, (uint32_t)((uintptr_t)p0 & 15), n, g0.first && lane_v() < g0.m, g0.my_start,
                                g0.my_end, g0.H, g0.T);
             STAMP(tb2);
             STAMP_ADD(0, tb2 - tb);
@@ -863,11 +890,11 @@ __global__ __launch_bounds__(1024) void k_validate_decoded(DeviceJob j) {
     if (count == 0) return;
     const Tables* T = j.tables;
     init_lds_tables(lds, T);
-    const uint32_t l = lane();
+    const uint32_t l = lane_v();
     const Keys K = make_keys();
     const uint32_t c40 = uni32(T->c40);
     const uint64_t nw = (uint64_t)gridDim.x * kVWaves;
-    for (uint64_t i = (uint64_t)blockIdx.x * kVWaves + (threadIdx.x >> 6); i < count; i += nw) {
+    for (uint64_t i = (uint64_t)blockIdx.x * kVWaves + uni32(threadIdx.x >> 6); i < count; i += nw) {
         const uint64_t b = uni32(j.decode_list[i]);
         rpgpu_batch_result* R = &j.batches[b];
         Desc d = desc_of(load_desc_raw(j, b));
