@@ -66,6 +66,10 @@ def lib():
         L.rpo_run_job.argtypes = [C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32, C.c_void_p,
                                   C.c_uint64, C.c_void_p, C.c_uint64, C.c_void_p, C.c_uint64,
                                   C.c_void_p, C.c_void_p, C.c_void_p]
+        L.rpo_run_job_layout.restype = C.c_int
+        L.rpo_run_job_layout.argtypes = [C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint32, C.c_void_p,
+                                         C.c_uint64, C.c_void_p, C.c_uint64, C.c_void_p, C.c_uint64,
+                                         C.c_void_p, C.c_void_p, C.c_void_p]
         L.rpo_batch_valid.restype = C.c_int
         L.rpo_batch_valid.argtypes = [C.c_void_p, C.c_uint32]
         L.rpo_baseline_validate.restype = C.c_int64
@@ -207,8 +211,9 @@ class JobResult:
 
 
 def run_job(data: np.ndarray, seg_offsets, flags=abi.JOB_CRC | abi.JOB_PARSE | abi.JOB_DECODE,
-            batch_cap=None, record_cap=None, decoded_cap=None) -> JobResult:
-    """Oracle run of the rpgpu_job contract over host-resident segments."""
+            batch_cap=None, record_cap=None, decoded_cap=None, layout: int = abi.LAYOUT_DISK) -> JobResult:
+    """Oracle run of the rpgpu_job contract over host-resident segments
+    (layout: abi.LAYOUT_DISK segments or abi.LAYOUT_WIRE Kafka record sets)."""
     data = np.ascontiguousarray(data, dtype=np.uint8)
     offs = np.ascontiguousarray(np.asarray(seg_offsets, dtype=np.uint64))
     nseg = offs.size - 1
@@ -227,7 +232,7 @@ def run_job(data: np.ndarray, seg_offsets, flags=abi.JOB_CRC | abi.JOB_PARSE | a
     bitmap = np.zeros(batch_cap // 64 + 1, dtype=np.uint64)
     pad = np.zeros(data.size + 64, dtype=np.uint8)
     pad[: data.size] = data
-    lib().rpo_run_job(pad.ctypes.data_as(C.c_void_p), offs.ctypes.data_as(C.c_void_p), nseg, flags,
+    lib().rpo_run_job_layout(pad.ctypes.data_as(C.c_void_p), offs.ctypes.data_as(C.c_void_p), nseg, flags, layout,
                       batches.ctypes.data_as(C.c_void_p), batch_cap,
                       records.ctypes.data_as(C.c_void_p), record_cap,
                       decoded.ctypes.data_as(C.c_void_p), decoded_cap,

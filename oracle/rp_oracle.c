@@ -195,6 +195,33 @@ void rpo_header_from_disk(const uint8_t* p, rpo_header* h) {
     h->record_count = (int32_t)rd32(p + 57);
 }
 
+static inline uint64_t be_n(const uint8_t* p, int n) {
+    uint64_t v = 0;
+    for (int i = 0; i < n; i++) v = (v << 8) | p[i];
+    return v;
+}
+
+/* kafka_batch_adapter::read_header (kafka/protocol/kafka_batch_adapter.cc:
+ * 32-91): big-endian v2 header; size_bytes = batch_length + 12 (int32
+ * arithmetic, :57-63), type raft_data, partition_leader_epoch ignored.
+ * Returns the magic byte. */
+int rpo_header_from_wire(const uint8_t* p, rpo_header* h) {
+    h->header_crc = 0;
+    h->base_offset = (int64_t)be_n(p, 8);
+    h->size_bytes = (int32_t)((uint32_t)be_n(p + 8, 4) + 12u);
+    h->type = 1;
+    h->crc = (int32_t)(uint32_t)be_n(p + 17, 4);
+    h->attrs = (int16_t)(uint16_t)be_n(p + 21, 2);
+    h->last_offset_delta = (int32_t)(uint32_t)be_n(p + 23, 4);
+    h->first_timestamp = (int64_t)be_n(p + 27, 8);
+    h->max_timestamp = (int64_t)be_n(p + 35, 8);
+    h->producer_id = (int64_t)be_n(p + 43, 8);
+    h->producer_epoch = (int16_t)(uint16_t)be_n(p + 51, 2);
+    h->base_sequence = (int32_t)(uint32_t)be_n(p + 53, 4);
+    h->record_count = (int32_t)(uint32_t)be_n(p + 57, 4);
+    return (int8_t)p[16];
+}
+
 static void wr_le(uint8_t* p, uint64_t v, int n) { for (int i = 0; i < n; i++) p[i] = (uint8_t)(v >> (8 * i)); }
 static void wr_be(uint8_t* p, uint64_t v, int n) { for (int i = 0; i < n; i++) p[i] = (uint8_t)(v >> (8 * (n - 1 - i))); }
 
@@ -854,8 +881,12 @@ uint64_t rpo_decode_capacity(int codec, const uint8_t* s, size_t n) {
 /* ======================================================================== */
 /* Segment pipeline                                                          */
 /* ======================================================================== */
+int rpo_batch_valid_layout(const rpgpu_batch_result* b, uint32_t job_flags, uint32_t layout) {
+    if (layout == RPGPU_LAYOUT_WIRE && !(b->flags & RPGPU_F_WIRE_V2)) return 0;
+    return rpo_batch_valid(b, job_flags);
+}
+
 int rpo_batch_valid(const rpgpu_batch_result* b, uint32_t job_flags) {
-    (void)job_flags;
     uint32_t f = b->flags;
     if (!(f & RPGPU_F_HEADER_OK) || !(f & RPGPU_F_COMPLETE) || !(f & RPGPU_F_CRC_OK)) return 0;
     if (f & RPGPU_F_CODEC_INVALID) return 0;
@@ -881,11 +912,20 @@ static void fill_result_header(rpgpu_batch_result* r, const rpo_header* h) {
     r->type = h->type;
 }
 
-int64_t rpo_scan_segment(const uint8_t* seg, uint64_t len, uint32_t segment, uint32_t job_flags,
-                         rpgpu_batch_result* batches, uint64_t batch_cap,
-                         rpgpu_record_index* index, uint64_t index_cap,
-                         uint8_t* decoded, uint64_t decoded_cap,
-                         rpgpu_segment_summary* sm, rpo_job_state* st) {
+/* One segment.  Disk layout: continuous_batch_parser + checksumming_consumer
+ * (storage/parser.cc:96-254, storage/log_replayer.cc:27-114).  Wire layout:
+ * kafka::batch_reader over one record set (kafka/protocol/batch_reader.cc:
+ * 50-156) adapting each batch with kafka_batch_adapter::adapt
+ * (kafka_batch_adapter.cc:126-188): the chain is structural (batch_length +
+ * 12 per batch); first_bad is the first batch do_load_slice would reject
+ * (not v2, crc mismatch, codec bits 5-7 -- compressed() throws --, or a sync
+ * record parse failure of an uncompressed batch). */
+int64_t rpo_scan_segment_layout(const uint8_t* seg, uint64_t len, uint32_t segment, uint32_t job_flags,
+                                uint32_t layout, rpgpu_batch_result* batches, uint64_t batch_cap,
+                                rpgpu_record_index* index, uint64_t index_cap,
+                                uint8_t* decoded, uint64_t decoded_cap,
+                                rpgpu_segment_summary* sm, rpo_job_state* st) {
+    const int wire = layout == RPGPU_LAYOUT_WIRE;
     memset(sm, 0, sizeof *sm);
     sm->first_batch = st->batch_base;
     uint64_t pos = 0, phys = 0;
@@ -898,10 +938,24 @@ int64_t rpo_scan_segment(const uint8_t* seg, uint64_t len, uint32_t segment, uin
         if (rem == 0) { sm->terminal_errc = RPGPU_ERRC_END_OF_STREAM; sm->terminal_eof = 1; break; }
         if (rem < RPGPU_HEADER_SIZE) { sm->terminal_errc = RPGPU_ERRC_INPUT_STREAM_NOT_ENOUGH_BYTES; sm->terminal_eof = 1; break; }
         rpo_header h;
-        rpo_header_from_disk(seg + pos, &h);
-        if (h.header_crc == 0) { sm->terminal_errc = RPGPU_ERRC_FALLOCATED_FILE_READ_ZERO_BYTES_FOR_HEADER; break; }
-        uint32_t hc = rpo_internal_header_only_crc(&h);
-        if (hc != h.header_crc) { sm->terminal_errc = RPGPU_ERRC_HEADER_ONLY_CRC_MISSMATCH; break; }
+        int v2 = 0;
+        uint32_t hc;
+        if (wire) {
+            /* read_record_batch_info (batch_reader.cc:50-88) needs 61 bytes;
+             * adapt() then reads the 61-byte header out of the batch's own
+             * batch_length + 12 bytes: a smaller batch throws */
+            v2 = rpo_header_from_wire(seg + pos, &h) == 2;
+            if ((int64_t)(int32_t)be_n(seg + pos + 8, 4) + 12 < (int64_t)RPGPU_HEADER_SIZE) {
+                sm->terminal_errc = RPGPU_ERRC_INPUT_STREAM_NOT_ENOUGH_BYTES;
+                break;
+            }
+            hc = rpo_internal_header_only_crc(&h); /* the header_crc the batch gets on disk */
+        } else {
+            rpo_header_from_disk(seg + pos, &h);
+            if (h.header_crc == 0) { sm->terminal_errc = RPGPU_ERRC_FALLOCATED_FILE_READ_ZERO_BYTES_FOR_HEADER; break; }
+            hc = rpo_internal_header_only_crc(&h);
+            if (hc != h.header_crc) { sm->terminal_errc = RPGPU_ERRC_HEADER_ONLY_CRC_MISSMATCH; break; }
+        }
         if (st->batch_base + nb >= batch_cap) { st->overflow |= 1; sm->terminal_errc = RPGPU_ERRC_NONE; break; }
         rpgpu_batch_result* r = &batches[st->batch_base + nb];
         memset(r, 0, sizeof *r);
@@ -910,6 +964,7 @@ int64_t rpo_scan_segment(const uint8_t* seg, uint64_t len, uint32_t segment, uin
         fill_result_header(r, &h);
         r->header_crc_computed = hc;
         r->flags = RPGPU_F_HEADER_OK;
+        if (wire && v2) r->flags |= RPGPU_F_WIRE_V2;
         /* consume_records: size_bytes - 61 computed unsigned (storage/parser.cc:207) */
         uint64_t need = (uint32_t)((uint32_t)h.size_bytes - RPGPU_HEADER_SIZE);
         const uint8_t* payload = seg + pos + RPGPU_HEADER_SIZE;
@@ -929,9 +984,14 @@ int64_t rpo_scan_segment(const uint8_t* seg, uint64_t len, uint32_t segment, uin
             goto done;
         }
         r->flags |= RPGPU_F_COMPLETE;
+        /* the BE40 prefix is wire bytes [21, 61) as they stand: on the wire
+         * this is CRC32C(wire[21..end)) (kafka_batch_adapter.cc:94-124); there
+         * valid_crc is only computed for v2 batches */
         r->crc_computed = rpo_crc_record_batch(&h, payload, need);
-        if (r->crc_computed == (uint32_t)h.crc) r->flags |= RPGPU_F_CRC_OK;
-        else if (first_bad < 0) first_bad = (int64_t)nb;
+        if (r->crc_computed == (uint32_t)h.crc && (!wire || v2)) r->flags |= RPGPU_F_CRC_OK;
+        else if (!wire && first_bad < 0) first_bad = (int64_t)nb;
+        /* adapt() parses records only after the v2 and crc checks */
+        const int may_walk = !wire || (r->flags & RPGPU_F_CRC_OK);
         if (codec) r->flags |= RPGPU_F_COMPRESSED;
         if (codec >= 5) r->flags |= RPGPU_F_CODEC_INVALID;
         if (codec == RPGPU_CODEC_GZIP || codec == RPGPU_CODEC_ZSTD) r->flags |= RPGPU_F_CODEC_UNSUPPORTED;
@@ -966,7 +1026,7 @@ int64_t rpo_scan_segment(const uint8_t* seg, uint64_t len, uint32_t segment, uin
             r->decoded_len = (uint32_t)need;
             walk = payload;
             walk_len = need;
-            do_walk = (job_flags & RPGPU_JOB_PARSE) != 0;
+            do_walk = (job_flags & RPGPU_JOB_PARSE) && may_walk;
         } else if (decodable) {
             if (r->decoded_off + cap > decoded_cap) {
                 st->overflow |= 4;
@@ -989,7 +1049,7 @@ int64_t rpo_scan_segment(const uint8_t* seg, uint64_t len, uint32_t segment, uin
                     r->decoded_header_crc = nh.header_crc;
                     walk = decoded + r->decoded_off;
                     walk_len = got;
-                    do_walk = (job_flags & RPGPU_JOB_PARSE) != 0;
+                    do_walk = (job_flags & RPGPU_JOB_PARSE) && may_walk;
                 }
             }
         }
@@ -1010,6 +1070,12 @@ int64_t rpo_scan_segment(const uint8_t* seg, uint64_t len, uint32_t segment, uin
                 else r->parse_err = RPGPU_PARSE_ERR_INDEX_CAPACITY;
             }
         }
+        if (wire && first_bad < 0) {
+            const uint32_t f = r->flags;
+            const int accepted = (f & RPGPU_F_CRC_OK) && !(f & RPGPU_F_CODEC_INVALID) &&
+                                 !(codec == 0 && (f & RPGPU_F_PARSED) && !(f & RPGPU_F_PARSE_OK));
+            if (!accepted) first_bad = (int64_t)nb;
+        }
         nb++;
         phys += (uint64_t)(int64_t)h.size_bytes;
         pos += RPGPU_HEADER_SIZE + need;
@@ -1023,7 +1089,9 @@ done:
     uint64_t good = (first_bad < 0) ? nb : (uint64_t)first_bad;
     sm->first_bad = (uint32_t)good;
     sm->bytes_consumed = 0;
-    uint64_t upto = (first_bad < 0) ? nb : (uint64_t)first_bad + 1;
+    /* disk: continuous_batch_parser also counts the batch it stopped in;
+     * wire: batch_reader consumed the accepted prefix */
+    uint64_t upto = (first_bad < 0) ? nb : (uint64_t)first_bad + (wire ? 0 : 1);
     for (uint64_t i = 0; i < upto; i++)
         sm->bytes_consumed += (uint64_t)(int64_t)batches[st->batch_base + i].size_bytes;
     if (good > 0) {
@@ -1041,15 +1109,33 @@ done:
     return (int64_t)nb;
 }
 
+int64_t rpo_scan_segment(const uint8_t* seg, uint64_t len, uint32_t segment, uint32_t job_flags,
+                         rpgpu_batch_result* batches, uint64_t batch_cap,
+                         rpgpu_record_index* index, uint64_t index_cap,
+                         uint8_t* decoded, uint64_t decoded_cap,
+                         rpgpu_segment_summary* sm, rpo_job_state* st) {
+    return rpo_scan_segment_layout(seg, len, segment, job_flags, RPGPU_LAYOUT_DISK, batches, batch_cap, index,
+                                   index_cap, decoded, decoded_cap, sm, st);
+}
+
 int rpo_run_job(const uint8_t* data, const uint64_t* seg_offsets, uint32_t n_segments,
                 uint32_t job_flags, rpgpu_batch_result* batches, uint64_t batch_cap,
                 rpgpu_record_index* index, uint64_t index_cap, uint8_t* decoded,
                 uint64_t decoded_cap, rpgpu_segment_summary* summaries,
                 rpgpu_job_totals* totals, uint64_t* valid_bitmap) {
+    return rpo_run_job_layout(data, seg_offsets, n_segments, job_flags, RPGPU_LAYOUT_DISK, batches, batch_cap, index,
+                              index_cap, decoded, decoded_cap, summaries, totals, valid_bitmap);
+}
+
+int rpo_run_job_layout(const uint8_t* data, const uint64_t* seg_offsets, uint32_t n_segments,
+                       uint32_t job_flags, uint32_t layout, rpgpu_batch_result* batches, uint64_t batch_cap,
+                       rpgpu_record_index* index, uint64_t index_cap, uint8_t* decoded,
+                       uint64_t decoded_cap, rpgpu_segment_summary* summaries,
+                       rpgpu_job_totals* totals, uint64_t* valid_bitmap) {
     rpo_job_state st = {0, 0, 0, 0};
     for (uint32_t s = 0; s < n_segments; s++) {
-        rpo_scan_segment(data + seg_offsets[s], seg_offsets[s + 1] - seg_offsets[s], s, job_flags, batches,
-                         batch_cap, index, index_cap, decoded, decoded_cap, &summaries[s], &st);
+        rpo_scan_segment_layout(data + seg_offsets[s], seg_offsets[s + 1] - seg_offsets[s], s, job_flags, layout,
+                                batches, batch_cap, index, index_cap, decoded, decoded_cap, &summaries[s], &st);
     }
     memset(totals, 0, sizeof *totals);
     totals->n_batches = st.batch_base;
@@ -1058,7 +1144,7 @@ int rpo_run_job(const uint8_t* data, const uint64_t* seg_offsets, uint32_t n_seg
     totals->overflow = st.overflow;
     if (valid_bitmap) {
         for (uint64_t i = 0; i < st.batch_base; i++) {
-            if (rpo_batch_valid(&batches[i], job_flags)) valid_bitmap[i >> 6] |= 1ull << (i & 63);
+            if (rpo_batch_valid_layout(&batches[i], job_flags, layout)) valid_bitmap[i >> 6] |= 1ull << (i & 63);
             else valid_bitmap[i >> 6] &= ~(1ull << (i & 63));
         }
     }

@@ -62,6 +62,9 @@ typedef struct rpo_header {
 
 /* storage/parser.cc:36-76 (header_from_iobuf, little endian) */
 void rpo_header_from_disk(const uint8_t* p, rpo_header* h);
+/* kafka/protocol/kafka_batch_adapter.cc:32-91 (read_header, big endian);
+ * returns the magic byte */
+int rpo_header_from_wire(const uint8_t* p, rpo_header* h);
 /* storage/segment_appender_utils.cc:28-54 (disk_header_to_iobuf) */
 void rpo_header_to_disk(const rpo_header* h, uint8_t* out61);
 /* model/record_utils.cc:34-55 */
@@ -122,6 +125,17 @@ int rpo_run_job(const uint8_t* data, const uint64_t* seg_offsets, uint32_t n_seg
 
 /* validity rule behind rpgpu_job.d_valid_bitmap */
 int rpo_batch_valid(const rpgpu_batch_result* b, uint32_t job_flags);
+int rpo_batch_valid_layout(const rpgpu_batch_result* b, uint32_t job_flags, uint32_t layout);
+int64_t rpo_scan_segment_layout(const uint8_t* seg, uint64_t len, uint32_t segment, uint32_t job_flags,
+                                uint32_t layout, rpgpu_batch_result* batches, uint64_t batch_cap,
+                                rpgpu_record_index* index, uint64_t index_cap,
+                                uint8_t* decoded, uint64_t decoded_cap,
+                                rpgpu_segment_summary* sm, rpo_job_state* st);
+int rpo_run_job_layout(const uint8_t* data, const uint64_t* seg_offsets, uint32_t n_segments,
+                       uint32_t job_flags, uint32_t layout, rpgpu_batch_result* batches, uint64_t batch_cap,
+                       rpgpu_record_index* index, uint64_t index_cap, uint8_t* decoded,
+                       uint64_t decoded_cap, rpgpu_segment_summary* summaries,
+                       rpgpu_job_totals* totals, uint64_t* valid_bitmap);
 
 /* CPU baseline: validate (crc + header crc + record walk) a segment set with
  * `threads` workers, one segment-slice per worker (Seastar shard-per-core);

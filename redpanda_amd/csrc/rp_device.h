@@ -103,6 +103,59 @@ DEV int be_index(uint32_t l) {
     return (fs - 21) + (fl - 1 - ((int)l - fs));
 }
 
+// big-endian fields of a header spread one byte per lane
+DEV uint32_t hbe16(uint32_t b, int k) { return (hb(b, k) << 8) | hb(b, k + 1); }
+DEV uint32_t hbe32(uint32_t b, int k) { return (hbe16(b, k) << 16) | hbe16(b, k + 2); }
+DEV uint64_t hbe64(uint32_t b, int k) { return ((uint64_t)hbe32(b, k) << 32) | hbe32(b, k + 4); }
+
+// ---------------------------------------------------------------------------
+// Wave-cooperative Kafka v2 wire header: batch_reader::read_record_batch_info
+// (kafka/protocol/batch_reader.cc:50-88) + kafka_batch_adapter::read_header
+// (kafka/protocol/kafka_batch_adapter.cc:32-91).  Lane l holds wire byte l.
+// The chain is structural: size = batch_length + 12; a size below 61 cannot
+// hold the header adapt() reads (it throws).  There is no header_crc on the
+// wire: `computed` is internal_header_only_crc of the adapted header (the
+// value the batch carries on disk), from disk byte l = wire byte src(l).
+// ---------------------------------------------------------------------------
+DEV Hdr wave_header_wire(const uint8_t* __restrict__ seg, uint64_t len, uint64_t p, const Tables* __restrict__ T) {
+    Hdr h;
+    h.eof = 0;
+    h.b = 0;
+    h.hcrc = h.computed = 0;
+    h.size = 0;
+    h.need = 0;
+    const uint64_t rem = len - p;
+    if (rem == 0) { h.status = RPGPU_ERRC_END_OF_STREAM; h.eof = 1; return h; }
+    if (rem < RPGPU_HEADER_SIZE) { h.status = RPGPU_ERRC_INPUT_STREAM_NOT_ENOUGH_BYTES; h.eof = 1; return h; }
+    const uint32_t l = lane();
+    const uint32_t b = (l < RPGPU_HEADER_SIZE) ? (uint32_t)seg[p + l] : 0u;
+    h.b = b;
+    const uint32_t bl = hbe32(b, 8);
+    if ((int64_t)(int32_t)bl + 12 < (int64_t)RPGPU_HEADER_SIZE) { h.status = RPGPU_ERRC_INPUT_STREAM_NOT_ENOUGH_BYTES; return h; }
+    h.size = (int32_t)(bl + 12u);
+    h.need = (uint32_t)((uint32_t)h.size - RPGPU_HEADER_SIZE);
+    // adapted (disk, little-endian) byte l: size_bytes 4..7, base_offset
+    // 8..15 (wire 7..0), type 16 (raft_data), then every field byte-reversed
+    // in place (the BE40 prefix is wire[21..61))
+    int src = 0;
+    if (l >= 8 && l < 16) src = 15 - (int)l;
+    else if (l >= 17 && l < 21) src = 37 - (int)l;
+    else if (l >= 21 && l < RPGPU_HEADER_SIZE) src = 21 + be_index(l);
+    const uint32_t moved = (uint32_t)__shfl((int)b, src, 64);
+    uint32_t d = moved;
+    if (l >= 4 && l < 8) d = ((uint32_t)h.size >> (8 * (l - 4))) & 0xFFu;
+    if (l == 16) d = 1u;
+    const uint32_t contrib = (l >= 4 && l < RPGPU_HEADER_SIZE) ? T->hdr[60 - l][d] : 0u;
+    h.computed = ~(T->c57 ^ wave_xor(contrib));
+    h.status = -1;
+    return h;
+}
+
+DEV Hdr wave_header_of(uint32_t layout, const uint8_t* __restrict__ seg, uint64_t len, uint64_t p,
+                       const Tables* __restrict__ T) {
+    return layout == RPGPU_LAYOUT_WIRE ? wave_header_wire(seg, len, p, T) : wave_header(seg, len, p, T);
+}
+
 #define HD __host__ __device__ inline
 
 HD uint32_t rd32h(const uint8_t* p) { return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24); }

@@ -73,6 +73,7 @@ struct DeviceJob {
     const uint64_t* chunk_base;   // n_segments + 1 : first global chunk index of each segment
     uint32_t n_segments;
     uint32_t flags;
+    uint32_t layout;              // rpgpu_layout
     uint32_t chunk_bytes;
     uint32_t total_chunks;
     ChunkRec* chunks;

@@ -60,6 +60,17 @@ DEV bool prefilter(const uint8_t* __restrict__ seg, uint64_t len, uint64_t q) {
     return true;
 }
 
+// wire layout: a v2 header whose batch_length fits the segment
+DEV bool prefilter_wire(const uint8_t* __restrict__ seg, uint64_t len, uint64_t q) {
+    if (len - q < RPGPU_HEADER_SIZE) return false;
+    const uint8_t* h = seg + q;
+    const int64_t size = (int64_t)(int32_t)((uint32_t)h[8] << 24 | (uint32_t)h[9] << 16 | (uint32_t)h[10] << 8 | h[11]) + 12;
+    if (size < (int64_t)RPGPU_HEADER_SIZE || (uint64_t)size > len - q) return false;
+    if (h[16] != 2 || (h[22] & 7) > 4) return false;
+    const int32_t rc = (int32_t)((uint32_t)h[57] << 24 | (uint32_t)h[58] << 16 | (uint32_t)h[59] << 8 | h[60]);
+    return rc >= 0 && rc <= size;
+}
+
 struct WalkOut {
     uint64_t exit;
     uint64_t tpos;
@@ -68,13 +79,14 @@ struct WalkOut {
 };
 
 // Follow the chain from p while headers start before ce.
-DEV WalkOut wave_walk(const uint8_t* __restrict__ seg, uint64_t len, uint64_t p, uint64_t ce, const Tables* __restrict__ T) {
+DEV WalkOut wave_walk(uint32_t layout, const uint8_t* __restrict__ seg, uint64_t len, uint64_t p, uint64_t ce,
+                      const Tables* __restrict__ T) {
     WalkOut w;
     w.count = 0;
     w.term = -1;
     w.tpos = 0;
     while (p < ce) {
-        Hdr h = wave_header(seg, len, p, T);
+        Hdr h = wave_header_of(layout, seg, len, p, T);
         if (h.status >= 0) { w.term = h.status | (h.eof << 8); w.tpos = p; break; }
         if (len - p - RPGPU_HEADER_SIZE < h.need) {
             w.count++;
@@ -104,13 +116,13 @@ __global__ __launch_bounds__(256) void k_discover(DeviceJob j) {
     } else {
         for (uint64_t q0 = cs; q0 < ce && entry == kNone; q0 += 64) {
             const uint64_t q = q0 + lane();
-            bool cand = (q < ce) && prefilter(seg, len, q);
+            bool cand = (q < ce) && (j.layout == RPGPU_LAYOUT_WIRE ? prefilter_wire(seg, len, q) : prefilter(seg, len, q));
             uint64_t mask = __ballot(cand);
             while (mask) {
                 const uint32_t bit = __builtin_ctzll(mask);
                 mask &= mask - 1;
                 const uint64_t qc = q0 + bit;
-                Hdr h = wave_header(seg, len, qc, j.tables);
+                Hdr h = wave_header_of(j.layout, seg, len, qc, j.tables);
                 if (h.status < 0 && len - qc - RPGPU_HEADER_SIZE >= h.need) { entry = qc; break; }
             }
         }
@@ -119,7 +131,7 @@ __global__ __launch_bounds__(256) void k_discover(DeviceJob j) {
     if (entry == kNone) {
         o.exit = kNone; o.count = 0; o.term = -1; o.tpos = 0;
     } else {
-        o = wave_walk(seg, len, entry, ce, j.tables);
+        o = wave_walk(j.layout, seg, len, entry, ce, j.tables);
     }
     if (lane() == 0) {
         ChunkRec r;
@@ -235,7 +247,7 @@ __global__ __launch_bounds__(256) void k_resolve(DeviceJob j) {
                 o.exit = P; o.count = 0; o.term = -1; o.tpos = 0;
             } else {
                 entry = P;
-                o = wave_walk(seg, len, P, ce2, j.tables);
+                o = wave_walk(j.layout, seg, len, P, ce2, j.tables);
             }
             if (tid == 0) {
                 ChunkRec nr;
@@ -293,14 +305,17 @@ __global__ __launch_bounds__(256) void k_emit(DeviceJob j) {
             if (bad) break;
         }
 #endif
-        Hdr h = wave_header(seg, len, p, T);  // known valid (resolved chain)
+        Hdr h = wave_header_of(j.layout, seg, len, p, T);  // known valid (resolved chain)
+        const bool wire = j.layout == RPGPU_LAYOUT_WIRE;
         const uint64_t ord = base_ord + i;
         const bool complete = (len - p - RPGPU_HEADER_SIZE) >= h.need;
         // prefix state of the batch crc: CRC over the BE40 prefix, init ~0
-        uint32_t pc = (l >= 21 && l < RPGPU_HEADER_SIZE) ? T->hdr[39 - be_index(l)][h.b] : 0u;
+        // (on the wire the prefix is bytes [21, 61) as they stand)
+        const uint32_t pe = wire ? (uint32_t)(l - 21) : (uint32_t)be_index(l);
+        uint32_t pc = (l >= 21 && l < RPGPU_HEADER_SIZE) ? T->hdr[39 - pe][h.b] : 0u;
         uint32_t praw = wave_xor(pc);
-        const uint32_t attrs = h16(h.b, 21);
-        const int32_t rc = (int32_t)h32(h.b, 57);
+        const uint32_t attrs = wire ? hbe16(h.b, 21) : h16(h.b, 21);
+        const int32_t rc = (int32_t)(wire ? hbe32(h.b, 57) : h32(h.b, 57));
         const uint32_t codec = attrs & 7;
         uint64_t slots = 0, cap = 0;
         const bool decodable = (codec == RPGPU_CODEC_LZ4 || codec == RPGPU_CODEC_SNAPPY) && (j.flags & RPGPU_JOB_DECODE);
@@ -315,19 +330,36 @@ __global__ __launch_bounds__(256) void k_emit(DeviceJob j) {
         if (l == 0 && ord < j.batch_capacity) {
             rpgpu_batch_result r;
             r.file_pos = p;
-            r.base_offset = (int64_t)h64(h.b, 8);
-            r.first_timestamp = (int64_t)h64(h.b, 27);
-            r.max_timestamp = (int64_t)h64(h.b, 35);
-            r.producer_id = (int64_t)h64(h.b, 43);
+            uint32_t f = RPGPU_F_HEADER_OK;
+            if (wire) {
+                // kafka_batch_adapter::read_header (kafka_batch_adapter.cc:32-91)
+                r.base_offset = (int64_t)hbe64(h.b, 0);
+                r.first_timestamp = (int64_t)hbe64(h.b, 27);
+                r.max_timestamp = (int64_t)hbe64(h.b, 35);
+                r.producer_id = (int64_t)hbe64(h.b, 43);
+                r.last_offset_delta = (int32_t)hbe32(h.b, 23);
+                r.base_sequence = (int32_t)hbe32(h.b, 53);
+                r.header_crc = 0;
+                r.crc = hbe32(h.b, 17);
+                r.producer_epoch = (int16_t)hbe16(h.b, 51);
+                r.type = 1;  // record_batch_type::raft_data
+                if (hb(h.b, 16) == 2) f |= RPGPU_F_WIRE_V2;
+            } else {
+                r.base_offset = (int64_t)h64(h.b, 8);
+                r.first_timestamp = (int64_t)h64(h.b, 27);
+                r.max_timestamp = (int64_t)h64(h.b, 35);
+                r.producer_id = (int64_t)h64(h.b, 43);
+                r.last_offset_delta = (int32_t)h32(h.b, 23);
+                r.base_sequence = (int32_t)h32(h.b, 53);
+                r.header_crc = h.hcrc;
+                r.crc = h32(h.b, 17);
+                r.producer_epoch = (int16_t)h16(h.b, 51);
+                r.type = (int8_t)hb(h.b, 16);
+            }
             r.size_bytes = h.size;
             r.record_count = rc;
-            r.last_offset_delta = (int32_t)h32(h.b, 23);
-            r.base_sequence = (int32_t)h32(h.b, 53);
-            r.header_crc = h.hcrc;
-            r.crc = h32(h.b, 17);
             r.crc_computed = 0;
             r.header_crc_computed = h.computed;
-            uint32_t f = RPGPU_F_HEADER_OK;
             if (complete) f |= RPGPU_F_COMPLETE;
             if (codec) f |= RPGPU_F_COMPRESSED;
             if (codec >= 5) f |= RPGPU_F_CODEC_INVALID;
@@ -343,8 +375,6 @@ __global__ __launch_bounds__(256) void k_emit(DeviceJob j) {
             r.decoded_crc = 0;
             r.decoded_header_crc = 0;
             r.attrs = (int16_t)attrs;
-            r.producer_epoch = (int16_t)h16(h.b, 51);
-            r.type = (int8_t)hb(h.b, 16);
             r.parse_err = 0;
             r.reserved0 = 0;
             // scratch for k_validate: raw CRC contribution of the BE prefix
@@ -449,7 +479,10 @@ __global__ __launch_bounds__(256) void k_finalize_segments(DeviceJob j) {
     const bool fits = last <= j.batch_capacity;
     const uint64_t fb = j.seg_first_bad[s];
     const uint64_t bad = (fits && fb < cnt) ? fb : cnt;
-    const uint64_t upto = bad < cnt ? bad + 1 : cnt;
+    // disk: continuous_batch_parser also counts the batch it stopped in
+    // (storage/parser.cc:178-190); wire: batch_reader consumed the accepted
+    // prefix (kafka/protocol/batch_reader.cc:122-156)
+    const uint64_t upto = bad < cnt ? bad + (j.layout == RPGPU_LAYOUT_WIRE ? 0 : 1) : cnt;
     const uint64_t seg_len = j.seg_off[s + 1] - j.seg_off[s];
     __shared__ unsigned long long s_bytes, s_phys;
     if (tid == 0) { s_bytes = 0; s_phys = 0; }
@@ -505,7 +538,8 @@ __global__ __launch_bounds__(256) void k_finalize_segments(DeviceJob j) {
     }
 }
 
-DEV bool batch_valid(uint32_t f, uint32_t job_flags) {
+DEV bool batch_valid(uint32_t f, uint32_t job_flags, uint32_t layout) {
+    if (layout == RPGPU_LAYOUT_WIRE && !(f & RPGPU_F_WIRE_V2)) return false;
     if (!(f & RPGPU_F_HEADER_OK) || !(f & RPGPU_F_COMPLETE) || !(f & RPGPU_F_CRC_OK)) return false;
     if (f & RPGPU_F_CODEC_INVALID) return false;
     if ((f & RPGPU_F_COMPRESSED) && (job_flags & RPGPU_JOB_DECODE) && !(f & RPGPU_F_CODEC_UNSUPPORTED) &&
@@ -523,7 +557,7 @@ __global__ __launch_bounds__(256) void k_finalize_bitmap(DeviceJob j) {
     uint64_t word = 0;
     for (uint32_t i = 0; i < 64; i++) {
         const uint64_t b = w * 64 + i;
-        if (b < nb && batch_valid(j.batches[b].flags, j.flags)) word |= 1ull << i;
+        if (b < nb && batch_valid(j.batches[b].flags, j.flags, j.layout)) word |= 1ull << i;
     }
     j.bitmap[w] = word;
 }

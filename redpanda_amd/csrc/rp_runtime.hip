@@ -270,7 +270,8 @@ int rpgpu_submit(rpgpu_ctx* c, const rpgpu_job* job, void* stream) {
         !job->d_batches || !job->d_summaries || !job->d_totals)
         return fail(c, RPGPU_E_INVALID, "rpgpu_submit: missing argument");
     if (((uintptr_t)job->d_data & 15) != 0) return fail(c, RPGPU_E_INVALID, "rpgpu_submit: d_data must be 16-byte aligned");
-    if (job->layout != RPGPU_LAYOUT_DISK) return fail(c, RPGPU_E_UNSUPPORTED, "rpgpu_submit: only the disk layout is wired up");
+    if (job->layout != RPGPU_LAYOUT_DISK && job->layout != RPGPU_LAYOUT_WIRE)
+        return fail(c, RPGPU_E_INVALID, "rpgpu_submit: unknown layout");
     if ((job->flags & RPGPU_JOB_PARSE) && !job->d_records && job->record_capacity)
         return fail(c, RPGPU_E_INVALID, "rpgpu_submit: PARSE needs d_records");
     hipSetDevice(c->device);
@@ -315,6 +316,7 @@ int rpgpu_submit(rpgpu_ctx* c, const rpgpu_job* job, void* stream) {
     j.chunk_base = (const uint64_t*)(ws + o_cbase);
     j.n_segments = nseg;
     j.flags = job->flags;
+    j.layout = job->layout;
     j.chunk_bytes = cs;
     j.total_chunks = (uint32_t)tc;
     j.chunks = (ChunkRec*)(ws + o_chunks);

@@ -813,6 +813,7 @@ __global__ __launch_bounds__(1024) void k_validate(DeviceJob j) {
             // uncompressed: the first record chain runs now, while the
             // window's lines are arriving in L2 (its scalar loads hit or merge
             // with them; after the CRC they would be evicted again)
+            const bool wire = j.layout == RPGPU_LAYOUT_WIRE;
             const bool walk = d.codec == 0 && (j.flags & RPGPU_JOB_PARSE);
             Group g0;
             group_init(g0);
@@ -834,15 +835,24 @@ __global__ __launch_bounds__(1024) void k_validate(DeviceJob j) {
                                g0.my_end, g0.H, g0.T);
             STAMP(tb2);
             STAMP_ADD(0, tb2 - tb);
-            if (crc == d.crc) f |= RPGPU_F_CRC_OK;
-            else note_bad(j, d.seg, b);
+            // on the wire valid_crc is only computed for v2 batches, and
+            // adapt() parses records only after both checks passed
+            // (kafka/protocol/kafka_batch_adapter.cc:157-181)
+            if (crc == d.crc && (!wire || (f & RPGPU_F_WIRE_V2))) f |= RPGPU_F_CRC_OK;
+            else if (!wire) note_bad(j, d.seg, b);
             prefetch();
-            if (walk) {
+            if (walk && (!wire || (f & RPGPU_F_CRC_OK))) {
                 bool idx_ok;
                 const WalkResult w = walk_batch(j, d, p0, n, b, idx_ok, g0);
                 f |= walk_flags(j, w, idx_ok, perr);
                 parsed = w.parsed;
             }
+            // wire: the first batch batch_reader::do_load_slice rejects
+            // (kafka/protocol/batch_reader.cc:129-151): not v2 / bad crc, codec
+            // bits 5-7 (compressed() throws), or a failed sync record parse
+            if (wire && (!(f & RPGPU_F_CRC_OK) || (f & RPGPU_F_CODEC_INVALID) ||
+                         ((f & RPGPU_F_PARSED) && !(f & RPGPU_F_PARSE_OK))))
+                note_bad(j, d.seg, b);
             STAMP(tc);
             STAMP_ADD(1, tc - tb2);
             if (l == 0) {
@@ -910,7 +920,7 @@ __global__ __launch_bounds__(1024) void k_validate_decoded(DeviceJob j) {
         const uint32_t dcrc = ~crc_stream(lds, K, ds, dv, dgt, d.praw ^ T->hdr[38][d.codec] ^ c40);
         const uint32_t dhcrc = decoded_header_crc(T, j.data + hdr, (uint32_t)(RPGPU_HEADER_SIZE + dl), dcrc);
         uint32_t f = d.flags, perr = 0, parsed = 0;
-        if (j.flags & RPGPU_JOB_PARSE) {
+        if ((j.flags & RPGPU_JOB_PARSE) && (j.layout != RPGPU_LAYOUT_WIRE || (d.flags & RPGPU_F_CRC_OK))) {
             bool idx_ok;
             Group g0;
             group_init(g0);

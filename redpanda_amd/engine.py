@@ -106,9 +106,11 @@ class Engine:
         )
 
     def submit(self, data, seg_offsets, out: DeviceResult, flags: int = abi.JOB_CRC | abi.JOB_PARSE,
-               chunk_bytes: int = 0, stream=None, d_seg_offsets=None):
+               chunk_bytes: int = 0, stream=None, d_seg_offsets=None, layout: int = abi.LAYOUT_DISK):
         """Enqueue one job on `stream` (default: torch's current stream).
-        `data` is a torch uint8 CUDA tensor holding the concatenated segments."""
+        `data` is a torch uint8 CUDA tensor holding the concatenated segments
+        (abi.LAYOUT_DISK: Redpanda log segments; abi.LAYOUT_WIRE: Kafka v2
+        record sets as a produce request carries them)."""
         torch = _torch()
         h_off = np.ascontiguousarray(np.asarray(seg_offsets, dtype=np.uint64))
         if d_seg_offsets is None:
@@ -119,7 +121,7 @@ class Engine:
         job.d_seg_offsets = d_seg_offsets.data_ptr()
         job.h_seg_offsets = h_off.ctypes.data
         job.n_segments = h_off.size - 1
-        job.layout = abi.LAYOUT_DISK
+        job.layout = layout
         job.flags = flags
         job.chunk_bytes = chunk_bytes
         job.d_batches = out.batches.data_ptr()
@@ -150,7 +152,8 @@ class Engine:
         return out[: n.value].tobytes()
 
     def validate(self, data, seg_offsets, flags: int = abi.JOB_CRC | abi.JOB_PARSE, batch_capacity=None,
-                 record_capacity=None, decoded_capacity=None, chunk_bytes: int = 0) -> HostResult:
+                 record_capacity=None, decoded_capacity=None, chunk_bytes: int = 0,
+                 layout: int = abi.LAYOUT_DISK) -> HostResult:
         """Convenience: allocate outputs, run, synchronize, copy back."""
         torch = _torch()
         offs = np.asarray(seg_offsets, dtype=np.uint64)
@@ -163,6 +166,6 @@ class Engine:
         if decoded_capacity is None:
             decoded_capacity = max(total * 8, 1 << 16) if flags & abi.JOB_DECODE else 1
         out = self.alloc_outputs(nseg, batch_capacity, record_capacity, decoded_capacity)
-        self.submit(data, offs, out, flags, chunk_bytes)
+        self.submit(data, offs, out, flags, chunk_bytes, layout=layout)
         torch.cuda.synchronize(data.device)
         return out.to_host()

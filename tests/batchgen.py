@@ -106,3 +106,37 @@ def simple_records(n: int, vlen: int = 40, klen: int = 8, headers: int = 2, seed
                bytes(rnd.choice(alnum) for _ in range(rnd.randint(1, 10)))) for _ in range(headers)]
         out += record(i, k, v, hs)
     return bytes(out)
+
+
+DISK_HDR = struct.Struct("<Iiqbihiqqqhii")   # storage/segment_appender_utils.cc:28-54
+WIRE_HDR = struct.Struct(">qiibihiqqqhii")   # kafka/protocol/response_writer.h:241-276
+
+
+def disk_to_wire(seg: bytes, stop_at_bad_header: bool = True) -> bytes:
+    """writer_serialize_batch (kafka/protocol/response_writer.h:241-276) over
+    every complete batch of a disk segment: the Kafka v2 record set the
+    produce path receives (batch_length = size_bytes - 12, leader epoch 0,
+    magic 2; the crc and payload are unchanged).  Stops at the first
+    fallocated / incomplete batch."""
+    out = bytearray()
+    pos = 0
+    while len(seg) - pos >= 61:
+        (hcrc, size, base, typ, crc, attrs, lod, first, mx, pid, epoch, seq, rc) = DISK_HDR.unpack_from(seg, pos)
+        if hcrc == 0 or size < 61 or pos + size > len(seg):
+            break
+        if stop_at_bad_header and crc32c(bytes(seg[pos + 4:pos + 61])) != hcrc:
+            break
+        out += WIRE_HDR.pack(base, size - 12, 0, 2, crc, attrs, lod, first, mx, pid, epoch, seq, rc)
+        out += seg[pos + 61:pos + size]
+        pos += size
+    return bytes(out)
+
+
+def wire_batches(rs: bytes):
+    """(offset, size) of each batch of a well-formed record set."""
+    pos, out = 0, []
+    while len(rs) - pos >= 61:
+        size = struct.unpack_from(">i", rs, pos + 8)[0] + 12
+        out.append((pos, size))
+        pos += size
+    return out

@@ -41,14 +41,14 @@ def assert_same(got, ref, flags=0):
         np.testing.assert_array_equal(gb, rb, err_msg="valid bitmap")
 
 
-def run_both(engine, oracle, segs, flags=FLAGS, chunk=0):  # noqa: D103
+def run_both(engine, oracle, segs, flags=FLAGS, chunk=0, layout=abi.LAYOUT_DISK):  # noqa: D103
     import torch
     offs = np.cumsum([0] + [s.size for s in segs]).astype(np.uint64)
     data = np.concatenate(segs) if segs else np.zeros(0, np.uint8)
-    ref = oracle.run_job(data, offs, flags)
+    ref = oracle.run_job(data, offs, flags, layout=layout)
     d = torch.from_numpy(np.concatenate([data, np.zeros(16, np.uint8)])).cuda()[: data.size] if data.size else \
         torch.zeros(16, dtype=torch.uint8, device="cuda")
-    got = engine.validate(d, offs, flags, chunk_bytes=chunk)
+    got = engine.validate(d, offs, flags, chunk_bytes=chunk, layout=layout)
     return got, ref
 
 
@@ -157,3 +157,52 @@ def test_uncompress_fixture(engine, oracle, ent):
         grc, got = -1, b""
     assert grc == (0 if rc == 0 else -1) == ent["rc"]
     assert got == want
+
+
+# ---------------------------------------------------------------------------
+# Kafka v2 wire layout (kafka_batch_adapter / batch_reader), SURVEY §8(a) a8
+# ---------------------------------------------------------------------------
+def wire_sets(rplib, seed, n=4, nbytes=1 << 20, **kw):
+    from tests import batchgen as bg
+    out = []
+    for i in range(n):
+        seg = gen(rplib, nbytes, i, seed=seed, batch_bytes=0, min_batch=200, max_batch=200000, **kw)
+        out.append(np.frombuffer(bg.disk_to_wire(seg.tobytes()), dtype=np.uint8).copy())
+    return out
+
+
+def wire_corruptions(rs: np.ndarray):
+    """The reference test's corruptions (batch_reader_test.cc): magic, crc,
+    lod decremented as native int32, plus a truncated tail and a short
+    header, each applied to a copy."""
+    import struct
+    from tests import batchgen as bg
+    raw = rs.tobytes()
+    batches = bg.wire_batches(raw)
+    out = []
+    for off in (16, 17, 23):
+        b = bytearray(raw)
+        p = batches[min(2, len(batches) - 1)][0] + off
+        v = struct.unpack_from("<i", b, p)[0]
+        struct.pack_into("<i", b, p, (v - 1 + 2**31) % 2**32 - 2**31)
+        out.append(np.frombuffer(bytes(b), dtype=np.uint8).copy())
+    p3, s3 = batches[min(3, len(batches) - 1)]
+    out.append(np.frombuffer(raw[: p3 + s3 - 7], dtype=np.uint8).copy())
+    out.append(np.frombuffer(raw[:58], dtype=np.uint8).copy())
+    return out
+
+
+@pytest.mark.parametrize("chunk", [0, 4096, 65536])
+def test_wire_layout(engine, oracle, rplib, chunk):
+    sets = wire_sets(rplib, 0xA8, corrupt_payload_ppm=20000)
+    sets += wire_corruptions(sets[0])
+    got, ref = run_both(engine, oracle, sets, chunk=chunk, layout=abi.LAYOUT_WIRE)
+    assert np.any(got.batches["flags"] & abi.F_WIRE_V2)
+    assert_same(got, ref)
+
+
+def test_wire_layout_codec_mix(engine, oracle, rplib):
+    sets = wire_sets(rplib, 0xA9, n=3, codec_mix=MIX, corrupt_payload_ppm=20000)
+    got, ref = run_both(engine, oracle, sets, flags=DFLAGS, chunk=64 << 10, layout=abi.LAYOUT_WIRE)
+    assert np.any(got.batches["flags"] & abi.F_CODEC_OK)
+    assert_same(got, ref, DFLAGS)
