@@ -624,9 +624,20 @@ DEV WalkResult walk_records(const uint8_t* p0, uint32_t n, int32_t rc, uint32_t 
 // internal_header_only_crc (model/record_utils.cc:34-55) of the header that
 // reset_size_checksum_metadata produces: codec bits cleared, size_bytes =
 // 61 + decoded, crc = the decoded crc (storage/parser_utils.cc:53-56, 114-120)
-DEV uint32_t decoded_header_crc(const Tables* T, const uint8_t* hdr, uint32_t new_size, uint32_t new_crc) {
+DEV uint32_t decoded_header_crc(const Tables* T, const uint8_t* hdr, uint32_t new_size, uint32_t new_crc,
+                                bool wire) {
     const uint32_t l = lane_v();
     uint32_t b = (l < RPGPU_HEADER_SIZE) ? (uint32_t)hdr[l] : 0u;
+    if (wire) {
+        // the adapted (disk) header: byte l from wire byte src(l), as in
+        // wave_header_wire; type raft_data
+        int src = 0;
+        if (l >= 8 && l < 16) src = 15 - (int)l;
+        else if (l >= 17 && l < 21) src = 37 - (int)l;
+        else if (l >= 21 && l < RPGPU_HEADER_SIZE) src = 21 + be_index(l);
+        b = (uint32_t)__shfl((int)b, src, 64);
+        if (l == 16) b = 1u;
+    }
     if (l >= 4 && l < 8) b = (new_size >> (8 * (l - 4))) & 0xFFu;
     if (l >= 17 && l < 21) b = (new_crc >> (8 * (l - 17))) & 0xFFu;
     if (l == 21) b &= ~7u;
@@ -918,7 +929,8 @@ __global__ __launch_bounds__(1024) void k_validate_decoded(DeviceJob j) {
         load_window(ds, 0, dv);
         const uint4 dgt = load_tail(ds);
         const uint32_t dcrc = ~crc_stream(lds, K, ds, dv, dgt, d.praw ^ T->hdr[38][d.codec] ^ c40);
-        const uint32_t dhcrc = decoded_header_crc(T, j.data + hdr, (uint32_t)(RPGPU_HEADER_SIZE + dl), dcrc);
+        const uint32_t dhcrc = decoded_header_crc(T, j.data + hdr, (uint32_t)(RPGPU_HEADER_SIZE + dl), dcrc,
+                                                  j.layout == RPGPU_LAYOUT_WIRE);
         uint32_t f = d.flags, perr = 0, parsed = 0;
         if ((j.flags & RPGPU_JOB_PARSE) && (j.layout != RPGPU_LAYOUT_WIRE || (d.flags & RPGPU_F_CRC_OK))) {
             bool idx_ok;
