@@ -14,6 +14,9 @@
  *   storage::continuous_batch_parser      storage/parser.h:94-136 (parser.cc:96-254)
  *   storage::log_replayer                 storage/log_replayer.h/.cc:27-114
  *   compression::compressor::uncompress   compression/compression.h:21-24
+ *   kafka::batch_reader,
+ *   kafka::kafka_batch_adapter            kafka/protocol/batch_reader.h, batch_reader.cc:50-156,
+ *                                         kafka/protocol/kafka_batch_adapter.h:60-76 (.cc:126-188)
  *
  * Differences forced by leaving Seastar: futures become synchronous calls,
  * ss::input_stream becomes a byte span of a whole segment, iobuf a
@@ -342,12 +345,15 @@ struct segment_scan {
     rpgpu_segment_summary summary{};
 };
 
-inline segment_scan scan_segment(rpgpu::engine& e, const uint8_t* seg, size_t len) {
+inline segment_scan scan_segment(rpgpu::engine& e, const uint8_t* seg, size_t len,
+                                 uint32_t layout = RPGPU_LAYOUT_DISK, uint32_t flags = RPGPU_JOB_CRC) {
     segment_scan out;
     const size_t cap = len / RPGPU_HEADER_SIZE + 2;
+    const size_t rcap = (flags & RPGPU_JOB_PARSE) ? len / 4 + 64 : 1;
     const size_t padded = ((len + 15) / 16 + 1) * 16;
     rpgpu::dev_buffer d_data(e, padded), d_offs(e, 16), d_b(e, cap * sizeof(rpgpu_batch_result)),
-        d_s(e, sizeof(rpgpu_segment_summary)), d_t(e, sizeof(rpgpu_job_totals));
+        d_s(e, sizeof(rpgpu_segment_summary)), d_t(e, sizeof(rpgpu_job_totals)),
+        d_r(e, rcap * sizeof(rpgpu_record_index));
     const uint64_t offs[2] = {0, (uint64_t)len};
     e.check(rpgpu_memset(e.ctx(), d_data.get(), 0, padded, nullptr), "rpgpu_memset");
     if (len) e.check(rpgpu_memcpy_h2d(e.ctx(), d_data.get(), seg, len, nullptr), "rpgpu_memcpy_h2d");
@@ -357,8 +363,10 @@ inline segment_scan scan_segment(rpgpu::engine& e, const uint8_t* seg, size_t le
     j.d_seg_offsets = (const uint64_t*)d_offs.get();
     j.h_seg_offsets = offs;
     j.n_segments = 1;
-    j.layout = RPGPU_LAYOUT_DISK;
-    j.flags = RPGPU_JOB_CRC;
+    j.layout = layout;
+    j.flags = flags;
+    j.d_records = (rpgpu_record_index*)d_r.get();
+    j.record_capacity = rcap;
     j.d_batches = (rpgpu_batch_result*)d_b.get();
     j.batch_capacity = cap;
     j.d_summaries = (rpgpu_segment_summary*)d_s.get();
@@ -513,5 +521,103 @@ public:
 };
 
 }  // namespace storage
+
+// ---------------------------------------------------------------------------
+// kafka — the produce path's record-set reader over the wire layout
+// ---------------------------------------------------------------------------
+namespace kafka {
+
+// kafka/protocol/errors.h (the one code this path raises)
+enum class error_code : int16_t { none = 0, corrupt_message = 2 };
+
+// kafka/protocol/exceptions.h
+struct exception : std::runtime_error {
+    exception(error_code e, const std::string& msg) : std::runtime_error(msg), error(e) {}
+    error_code error;
+};
+
+// kafka/protocol/kafka_batch_adapter.h:60-76: the verdict of adapt() on one
+// wire batch.  `batch` holds the adapted header (size_bytes = batch_length
+// + 12, type raft_data) when the batch was accepted; `records` its payload.
+struct kafka_batch_adapter {
+    bool v2_format{false};
+    bool valid_crc{false};
+    std::optional<model::record_batch_header> batch;
+    rpgpu::iobuf records;
+};
+
+// kafka/protocol/batch_reader.h: a Kafka v2 record set as a produce request
+// carries it.  The whole set is validated on the GPU in one rpgpu_submit
+// (layout RPGPU_LAYOUT_WIRE: CRC, record parse), then consumed batch by
+// batch with the reference's verdicts and exceptions.
+class batch_reader {
+public:
+    batch_reader(const uint8_t* record_set, size_t len, rpgpu::engine& e = rpgpu::engine::local())
+      : _buf(record_set), _len(len),
+        _scan(storage::detail::scan_segment(e, record_set, len, RPGPU_LAYOUT_WIRE, RPGPU_JOB_CRC | RPGPU_JOB_PARSE)) {}
+
+    bool empty() const { return _pos >= _len; }
+    size_t size_bytes() const { return _len - _pos; }
+
+    // batch_reader::last_offset (batch_reader.cc:92-103): last_offset of the
+    // final batch, structurally; a short header throws corrupt_message and a
+    // batch running past the end (or shorter than its own header) makes the
+    // parser's skip throw std::out_of_range
+    int64_t last_offset() const {
+        int64_t last = 0;
+        for (size_t i = _i; i < _scan.batches.size(); i++) {
+            const rpgpu_batch_result& r = _scan.batches[i];
+            if (!(r.flags & RPGPU_F_COMPLETE)) throw std::out_of_range("batch_reader: batch past the end");
+            last = (int64_t)((uint64_t)r.base_offset + (uint64_t)(int64_t)r.last_offset_delta);
+        }
+        check_terminal();
+        return last;
+    }
+
+    // batch_reader::consume_batch (batch_reader.cc:112-121) + adapt()
+    // (kafka_batch_adapter.cc:126-188)
+    kafka_batch_adapter consume_batch() {
+        if (_i >= _scan.batches.size()) {
+            check_terminal();
+            throw exception(error_code::corrupt_message, "Invalid kafka header parsing: no batch left");
+        }
+        const rpgpu_batch_result& r = _scan.batches[_i];
+        if (!(r.flags & RPGPU_F_COMPLETE)) throw std::out_of_range("batch_reader: batch past the end");
+        kafka_batch_adapter kba;
+        kba.v2_format = (r.flags & RPGPU_F_WIRE_V2) != 0;
+        kba.valid_crc = kba.v2_format && (r.flags & RPGPU_F_CRC_OK);
+        _i++;
+        _pos = (size_t)r.file_pos + (size_t)(int64_t)r.size_bytes;
+        if (!kba.valid_crc) return kba;
+        // record_batch::compressed() -> attributes::compression() throws for
+        // codec values 5..7, out of adapt()
+        if (r.flags & RPGPU_F_CODEC_INVALID)
+            throw std::runtime_error("Unknown compression value: " + std::to_string(r.attrs & 7));
+        if (!(r.flags & RPGPU_F_COMPRESSED) && !(r.flags & RPGPU_F_PARSE_OK)) return kba;  // for_each_record threw
+        kba.batch = model::record_batch_header::from(r);
+        kba.records = rpgpu::iobuf(_buf + r.file_pos + RPGPU_HEADER_SIZE,
+                                   (size_t)((int64_t)r.size_bytes - (int64_t)RPGPU_HEADER_SIZE));
+        return kba;
+    }
+
+private:
+    void check_terminal() const {
+        const rpgpu_segment_summary& sm = _scan.summary;
+        if (sm.terminal_errc == RPGPU_ERRC_INPUT_STREAM_NOT_ENOUGH_BYTES) {
+            // fewer than 61 bytes left: read_record_batch_info throws; a
+            // batch_length too small for the header makes the skip throw
+            if (sm.terminal_eof) throw exception(error_code::corrupt_message, "Invalid kafka header parsing");
+            throw std::out_of_range("batch_reader: batch shorter than its header");
+        }
+    }
+
+    const uint8_t* _buf;
+    size_t _len;
+    storage::detail::segment_scan _scan;
+    size_t _i = 0;
+    size_t _pos = 0;
+};
+
+}  // namespace kafka
 
 #endif  // RPGPU_REDPANDA_H_

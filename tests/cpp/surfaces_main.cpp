@@ -7,6 +7,7 @@
 //   surfaces_test parse <segment> M R S E       continuous_batch_parser replay
 //   surfaces_test recover <segment>             log_replayer checkpoint
 //   surfaces_test uncompress <codec> <in> <out> compressor::uncompress
+//   surfaces_test wire <record_set>             kafka::batch_reader
 #include <cstdio>
 #include <cstdlib>
 #include <fstream>
@@ -171,6 +172,44 @@ int main(int argc, char** argv) {
             const storage::log_replayer::checkpoint c = storage::log_replayer::recover(seg.data(), seg.size());
             if (c.last_offset) std::printf("CKPT 1 %lld %zu\n", (long long)*c.last_offset, *c.truncate_file_pos);
             else std::printf("CKPT 0\n");
+            return 0;
+        }
+        if (mode == "wire") {
+            const std::vector<uint8_t> rs = slurp(argv[2]);
+            {
+                kafka::batch_reader r(rs.data(), rs.size());
+                try {
+                    std::printf("L %lld\n", (long long)r.last_offset());
+                } catch (const kafka::exception&) {
+                    std::printf("L corrupt\n");
+                } catch (const std::out_of_range&) {
+                    std::printf("L out_of_range\n");
+                }
+            }
+            kafka::batch_reader r(rs.data(), rs.size());
+            while (!r.empty()) {
+                try {
+                    const kafka::kafka_batch_adapter kba = r.consume_batch();
+                    if (kba.batch) {
+                        crc::crc32c c;
+                        c.extend(kba.records.data(), kba.records.size_bytes());
+                        std::printf("B %d %d 1 %lld %d %zu %u\n", (int)kba.v2_format, (int)kba.valid_crc,
+                                    (long long)kba.batch->base_offset, kba.batch->size_bytes, kba.records.size_bytes(),
+                                    c.value());
+                    } else {
+                        std::printf("B %d %d 0\n", (int)kba.v2_format, (int)(kba.v2_format && kba.valid_crc));
+                    }
+                } catch (const kafka::exception&) {
+                    std::printf("X corrupt\n");
+                    break;
+                } catch (const std::out_of_range&) {
+                    std::printf("X out_of_range\n");
+                    break;
+                } catch (const std::runtime_error&) {
+                    std::printf("X runtime_error\n");
+                    break;
+                }
+            }
             return 0;
         }
         if (mode == "uncompress" && argc == 5) {

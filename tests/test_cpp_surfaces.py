@@ -20,6 +20,7 @@ import numpy as np
 import pytest
 
 from redpanda_amd import abi
+from tests import batchgen as bg
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 G = os.path.join(HERE, "golden")
@@ -258,3 +259,81 @@ def test_compressor_uncompress(driver, oracle, engine, tmp_path):
     assert run(driver, "uncompress", abi.CODEC_NONE, one, out) == ["U runtime_error"]
     assert run(driver, "uncompress", abi.CODEC_GZIP, one, out) == ["U logic_error"]
     assert run(driver, "uncompress", abi.CODEC_ZSTD, one, out) == ["U logic_error"]
+
+
+# ---------------------------------------------------------------------------
+# GPU: kafka::batch_reader (wire layout)
+# ---------------------------------------------------------------------------
+
+def ref_batch_reader(rs: bytes, oracle):
+    """kafka::batch_reader + kafka_batch_adapter::adapt over raw bytes
+    (kafka/protocol/batch_reader.cc:50-156, kafka_batch_adapter.cc:32-188):
+    the events surfaces_main.cpp prints."""
+    def last_offset():
+        pos, last = 0, 0
+        while len(rs) - pos:
+            if len(rs) - pos < 61:
+                return "L corrupt"
+            size = struct.unpack_from(">i", rs, pos + 8)[0] + 12
+            if size < 61 or pos + size > len(rs):
+                return "L out_of_range"
+            base = struct.unpack_from(">q", rs, pos)[0]
+            lod = struct.unpack_from(">i", rs, pos + 23)[0]
+            last = base + lod
+            pos += size
+        return f"L {last}"
+
+    ev = [last_offset()]
+    pos = 0
+    while len(rs) - pos:
+        if len(rs) - pos < 61:
+            ev.append("X corrupt")
+            break
+        size = struct.unpack_from(">i", rs, pos + 8)[0] + 12
+        if size < 61 or pos + size > len(rs):
+            ev.append("X out_of_range")
+            break
+        b = rs[pos:pos + size]
+        v2 = b[16] == 2
+        crc_ok = v2 and oracle.crc32c(b[21:]) == struct.unpack_from(">I", b, 17)[0]
+        pos += size
+        if not crc_ok:
+            ev.append(f"B {int(v2)} 0 0")
+            continue
+        codec = struct.unpack_from(">h", b, 21)[0] & 7
+        if codec > 4:
+            ev.append("X runtime_error")
+            break
+        if codec == 0:
+            rc = struct.unpack_from(">i", b, 57)[0]
+            _, perr, trailing, _ = oracle.walk_records(b[61:], rc)
+            if perr != 0 or trailing != 0:
+                ev.append(f"B 1 1 0")
+                continue
+        base = struct.unpack_from(">q", b, 0)[0]
+        ev.append(f"B 1 1 1 {base} {size} {size - 61} {oracle.crc32c(b[61:])}")
+    return ev
+
+
+@pytest.mark.gpu
+def test_kafka_batch_reader(driver, rplib, oracle, engine, tmp_path):
+    seg = gen(rplib, 300_000, 3, seed=0x5A, batch_bytes=0, min_batch=200, max_batch=30_000, corrupt_payload_ppm=100_000)
+    rs = bg.disk_to_wire(seg.tobytes())
+    cases = {"clean": rs}
+    b = bytearray(rs)
+    b[16 + bg.wire_batches(rs)[1][0]] = 1  # magic of batch 1
+    cases["magic"] = bytes(b)
+    p3, s3 = bg.wire_batches(rs)[3]
+    cases["truncated"] = rs[: p3 + s3 - 9]
+    cases["short_tail"] = rs[: p3 + s3 + 40]
+    b = bytearray(rs)
+    struct.pack_into(">i", b, p3 + 8, 10)
+    cases["small_length"] = bytes(b)
+    b = bytearray(rs)
+    b[p3 + 22] = (b[p3 + 22] & ~7) | 5
+    struct.pack_into(">I", b, p3 + 17, bg.crc32c(bytes(b[p3 + 21:p3 + s3])))
+    cases["codec5"] = bytes(b)
+    cases["empty"] = b""
+    for name, data in cases.items():
+        got = run(driver, "wire", write(tmp_path, name, data))
+        assert got == ref_batch_reader(data, oracle), name
