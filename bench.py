@@ -201,7 +201,7 @@ def main():
     v_ms = tm["validate"]
     achieved = alg / (v_ms * 1e-3) / 1e9
     traffic = None
-    tfile = os.path.join(ROOT, "profiles", "r01_validate_traffic.json")
+    tfile = os.path.join(ROOT, "profiles", "validate_traffic.json")  # refreshed by scripts/parse_profile.py
     if os.path.exists(tfile):
         try:
             traffic = json.load(open(tfile)).get("bytes_per_launch")

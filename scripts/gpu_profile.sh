@@ -1,5 +1,5 @@
-# rocprofv3 kernel trace + two PMC passes (FETCH_SIZE, WRITE_SIZE) of the
-# headline bench; each pass is its own bounded run (no trace domains beside --pmc)
+# rocprofv3 kernel trace + PMC passes of the headline bench; each pass is its
+# own bounded run (--pmc alone, no trace domains beside it)
 set -e
 cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
@@ -10,4 +10,5 @@ timeout -s KILL 240 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_fetch_$TAG -o f
 echo "fetch ok"
 timeout -s KILL 240 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc_write_$TAG -o write --output-format csv -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline > gpurun_out/pmc_write_$TAG.log 2>&1
 echo "write ok"
-find gpurun_out/prof_$TAG gpurun_out/pmc_fetch_$TAG gpurun_out/pmc_write_$TAG -name "*.csv" | head -20
+timeout -s KILL 240 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_fetchnp_$TAG -o fetchnp --output-format csv -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-parse > gpurun_out/pmc_fetchnp_$TAG.log 2>&1
+echo "fetch crc-only ok"

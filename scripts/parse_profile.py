@@ -40,9 +40,13 @@ def pmc(sub, name):
 
 fetch = pmc(f"pmc_fetch_{tag}", "FETCH_SIZE")
 write = pmc(f"pmc_write_{tag}", "WRITE_SIZE")
-res = {"kernel": "k_validate", "fetch_size_kib": fetch, "write_size_kib": write,
-       "correction": "FETCH_SIZE x2 (gfx950 counts half of a wide coalesced read), WRITE_SIZE x1; KiB -> bytes"}
+fetch_np = pmc(f"pmc_fetchnp_{tag}", "FETCH_SIZE")  # CRC-only run (calibration), when collected
+res = {"tag": tag, "kernel": "k_validate", "fetch_size_kib": fetch, "write_size_kib": write,
+       "fetch_size_kib_crc_only": fetch_np,
+       "correction": "FETCH_SIZE x2 (gfx950 counts half of a wide coalesced read; calibrated on the CRC-only run, "
+                     "whose traffic is the dwordx4 window stream alone), WRITE_SIZE x1; KiB -> bytes"}
 if fetch is not None and write is not None:
     res["bytes_per_launch"] = int(fetch * 1024 * 2 + write * 1024)
-json.dump(res, open(os.path.join(prof, f"{tag}_validate_traffic.json"), "w"), indent=1)
+for name in (f"{tag}_validate_traffic.json", "validate_traffic.json"):
+    json.dump(res, open(os.path.join(prof, name), "w"), indent=1)
 print(json.dumps(res))
