@@ -253,7 +253,9 @@ typedef struct rpgpu_job {
     uint64_t batch_capacity;
     rpgpu_record_index* d_records;   /* capacity record_capacity (may be NULL if !PARSE) */
     uint64_t record_capacity;
-    uint8_t* d_decoded;              /* decoded arena (may be NULL if !DECODE) */
+    uint8_t* d_decoded;              /* decoded arena (may be NULL if !DECODE); bytes are defined only at
+                                        [decoded_off, +decoded_len) of batches with RPGPU_F_CODEC_OK (the
+                                        reference throws and keeps nothing for the others); 16-B aligned */
     uint64_t decoded_capacity;
     rpgpu_segment_summary* d_summaries; /* n_segments entries */
     rpgpu_job_totals* d_totals;      /* one entry */

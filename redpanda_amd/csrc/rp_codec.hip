@@ -17,6 +17,9 @@
 // release/acquire fence makes those stores visible first, issued only when
 // the match source overlaps output written since the last fence.
 #include "rp_device.h"
+#ifdef RPGPU_CHECKED
+#include <cstdio>
+#endif
 
 namespace rp {
 
@@ -66,6 +69,23 @@ DEV void vis_fence() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
 }
 
+// Loads of output this wave wrote: agent-scope relaxed loads (sc1) skip the
+// vector L1, which may hold a copy of the line taken by another wave of the
+// CU before these bytes were stored (arena slots and blocks are adjacent;
+// the workgroup-scope acquire does not invalidate L1).  The release in
+// vis_fence has put the stores in L2 first.
+DEV uint32_t ld_out8(const uint8_t* p) {
+    return __hip_atomic_load(const_cast<uint8_t*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+DEV uint32_t ld_out32(const uint8_t* p) {  // 4 bytes at any address
+    const uintptr_t a = (uintptr_t)p;
+    uint32_t* q = (uint32_t*)(a & ~(uintptr_t)3);
+    const uint32_t sh = (uint32_t)(a & 3);
+    const uint32_t lo = __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint32_t hi = sh ? __hip_atomic_load(q + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
+    return __builtin_amdgcn_alignbyte(hi, lo, sh);
+}
+
 DEV void copy_lit(uint8_t* dst, int64_t op, const uint8_t* src, int64_t ip, int64_t len) {
     for (int64_t k = lane(); k < len; k += 64) dst[op + k] = src[ip + k];
 }
@@ -87,34 +107,41 @@ DEV void copy_match(uint8_t* dst, int64_t op, int64_t off, int64_t len, int64_t&
         fenced = op;
     }
     if (off >= len) {
-        for (int64_t k = lane(); k < len; k += 64) dst[op + k] = dst[s0 + k];
+        for (int64_t k = lane(); k < len; k += 64) dst[op + k] = (uint8_t)ld_out8(dst + s0 + k);
     } else {
         const uint32_t uo = (uint32_t)off;
-        for (int64_t k = lane(); k < len; k += 64) dst[op + k] = dst[s0 + (int64_t)((uint32_t)k % uo)];
+        for (int64_t k = lane(); k < len; k += 64) dst[op + k] = (uint8_t)ld_out8(dst + s0 + (int64_t)((uint32_t)k % uo));
     }
 }
 
 // XXH32 (lz4 1.9.3 xxhash.c), uniform over global memory
 DEV uint32_t rotl32(uint32_t x, int r) { return (x << r) | (x >> (32 - r)); }
-DEV uint32_t xxh32_dev(const uint8_t* p, int64_t n, uint32_t seed) {
+template <bool OUT>
+DEV uint32_t xxh32_t(const uint8_t* p, int64_t n, uint32_t seed);
+DEV uint32_t xxh32_dev(const uint8_t* p, int64_t n, uint32_t seed) { return xxh32_t<false>(p, n, seed); }
+DEV uint32_t xxh32_out(const uint8_t* p, int64_t n, uint32_t seed) { return xxh32_t<true>(p, n, seed); }
+
+// OUT: p is output this wave (or this kernel) wrote: L1-bypassing loads
+template <bool OUT>
+DEV uint32_t xxh32_t(const uint8_t* p, int64_t n, uint32_t seed) {
     const uint32_t P1 = 0x9E3779B1u, P2 = 0x85EBCA77u, P3 = 0xC2B2AE3Du, P4 = 0x27D4EB2Fu, P5 = 0x165667B1u;
     int64_t i = 0;
     uint32_t h;
     if (n >= 16) {
         uint32_t v1 = seed + P1 + P2, v2 = seed + P2, v3 = seed, v4 = seed - P1;
         for (; i + 16 <= n; i += 16) {
-            v1 = rotl32(v1 + ldu32(p + i) * P2, 13) * P1;
-            v2 = rotl32(v2 + ldu32(p + i + 4) * P2, 13) * P1;
-            v3 = rotl32(v3 + ldu32(p + i + 8) * P2, 13) * P1;
-            v4 = rotl32(v4 + ldu32(p + i + 12) * P2, 13) * P1;
+            v1 = rotl32(v1 + (OUT ? ld_out32(p + i) : ldu32(p + i)) * P2, 13) * P1;
+            v2 = rotl32(v2 + (OUT ? ld_out32(p + i + 4) : ldu32(p + i + 4)) * P2, 13) * P1;
+            v3 = rotl32(v3 + (OUT ? ld_out32(p + i + 8) : ldu32(p + i + 8)) * P2, 13) * P1;
+            v4 = rotl32(v4 + (OUT ? ld_out32(p + i + 12) : ldu32(p + i + 12)) * P2, 13) * P1;
         }
         h = rotl32(v1, 1) + rotl32(v2, 7) + rotl32(v3, 12) + rotl32(v4, 18);
     } else {
         h = seed + P5;
     }
     h += (uint32_t)n;
-    for (; i + 4 <= n; i += 4) h = rotl32(h + ldu32(p + i) * P3, 17) * P4;
-    for (; i < n; i++) h = rotl32(h + p[i] * P5, 11) * P1;
+    for (; i + 4 <= n; i += 4) h = rotl32(h + (OUT ? ld_out32(p + i) : ldu32(p + i)) * P3, 17) * P4;
+    for (; i < n; i++) h = rotl32(h + (OUT ? ld_out8(p + i) : (uint32_t)p[i]) * P5, 11) * P1;
     h ^= h >> 15;
     h *= P2;
     h ^= h >> 13;
@@ -374,7 +401,7 @@ DEV int lz4f_decode(In& in, const uint8_t* s, int64_t n, uint8_t* dst, int64_t& 
     if (ccs) {
         if (n - pos < 4) { out_len = out; return 0; }
         vis_fence();
-        if (in_le32(in, pos) != xxh32_dev(dst, out, 0)) return -1;
+        if (in_le32(in, pos) != xxh32_out(dst, out, 0)) return -1;
         pos += 4;
     }
     out_len = out;
@@ -510,9 +537,156 @@ DEV int decode_payload(int codec, const uint8_t* s, int64_t n, uint8_t* dst, int
 }
 
 // ---------------------------------------------------------------------------
+// Block-parallel decode.  A payload whose pieces are independent and whose
+// frame is structurally complete decodes to the concatenation of its pieces
+// (or fails when any piece fails): that is the sequential decoder's result
+// for such frames, since every flush of do_uncompressed happens while input
+// remains.  Those frames are split into BlockItems at the plan rule's
+// positions (decode_capacity_dev); everything else (linked LZ4 blocks,
+// truncated or malformed frames, raw snappy) takes the sequential path.
+// ---------------------------------------------------------------------------
+
+// reserve `nb` items (wave-uniform); UINT32_MAX when the list is full
+DEV uint32_t reserve_blocks(const DeviceJob& j, uint32_t nb) {
+    uint32_t first = 0;
+    if (lane() == 0) first = atomicAdd(&j.counters[4], nb);
+    first = rl(first, 0);
+    return ((uint64_t)first + nb <= j.block_capacity) ? first : 0xFFFFFFFFu;
+}
+
+// LZ4F frame of independent blocks (lz4_frame_compressor.cc:115-200 over
+// lz4 1.9.3): returns true and fills the plan when eligible
+DEV bool plan_lz4f(const DeviceJob& j, In& in, int64_t n, uint64_t src_abs, uint64_t dst_abs, FramePlan& fp) {
+    if (n < 7) return false;
+    if (in_le32(in, 0) != 0x184D2204u) return false;
+    const uint32_t flg = in_byte(in, 4);
+    const int64_t hsize = 7 + (((flg >> 3) & 1) ? 8 : 0) + ((flg & 1) ? 4 : 0);
+    if (n < hsize || ((flg >> 1) & 1) || ((flg >> 6) & 3) != 1) return false;
+    if (!((flg >> 5) & 1)) return false;  // linked blocks: sequential
+    const uint32_t bd = in_byte(in, 5);
+    const uint32_t bsid = (bd >> 4) & 7;
+    if (((bd >> 7) & 1) || bsid < 4 || (bd & 15)) return false;
+    if (((xxh32_dev(in.src + 4, hsize - 5, 0) >> 8) & 0xFFu) != in_byte(in, hsize - 1)) return false;
+    const bool bcs = (flg >> 4) & 1, ccs = (flg >> 2) & 1, csf = (flg >> 3) & 1;
+    const int64_t bmax = bsid == 4 ? (64 << 10) : bsid == 5 ? (256 << 10) : bsid == 6 ? (1 << 20) : (4 << 20);
+    // structure: every block present, the end mark, the content checksum,
+    // and nothing after it
+    int64_t pos = hsize;
+    uint32_t nb = 0;
+    bool end = false;
+    while (n - pos >= 4) {
+        const uint32_t bh = in_le32(in, pos);
+        pos += 4;
+        if (bh == 0) { end = true; break; }
+        const int64_t bsz = bh & 0x7FFFFFFFu;
+        if (bsz > bmax) return false;
+        const int64_t need = bsz + (bcs ? 4 : 0);
+        if (n - pos < need) return false;
+        pos += need;
+        nb++;
+    }
+    if (!end) return false;
+    uint32_t ccs_val = 0;
+    if (ccs) {
+        if (n - pos < 4) return false;
+        ccs_val = in_le32(in, pos);
+        pos += 4;
+    }
+    if (pos != n || nb == 0) return false;
+    const uint32_t first = reserve_blocks(j, nb);
+    if (first == 0xFFFFFFFFu) return false;
+    pos = hsize;
+    uint64_t plan = 0;
+    for (uint32_t k = 0; k < nb; k++) {
+        const uint32_t bh = in_le32(in, pos);
+        const int64_t bsz = bh & 0x7FFFFFFFu;
+        const bool raw = (bh & 0x80000000u) != 0;
+        if (lane() == 0) {
+            BlockItem it;
+            it.src = src_abs + (uint64_t)pos + 4;
+            it.dst = dst_abs + plan;
+            it.csize = (uint32_t)bsz;
+            it.kind = (raw ? kBlkRaw : 0u) | (bcs ? kBlkChecksum : 0u);
+            it.out = -1;
+            it.cap = raw ? (uint32_t)bsz : (uint32_t)bmax;
+            j.blocks[first + k] = it;
+        }
+        plan += raw ? (uint64_t)bsz : (uint64_t)bmax;
+        pos += 4 + bsz + (bcs ? 4 : 0);
+    }
+    fp.mode = 1;
+    fp.first = first;
+    fp.nb = nb;
+    fp.ccs = ccs;
+    fp.ccs_val = ccs_val;
+    fp.csf = csf;
+    fp.content_size = csf ? ((uint64_t)in_le32(in, 6) | ((uint64_t)in_le32(in, 10) << 32)) : 0;
+    return true;
+}
+
+// snappy-java stream (snappy_java_compressor.cc:76-129): chunks are
+// independent raw snappy blocks at exact offsets (their length varints)
+DEV bool plan_snappy_java(const DeviceJob& j, In& in, int64_t n, uint64_t src_abs, uint64_t dst_abs, FramePlan& fp) {
+    const uint8_t magic[8] = {0x82, 'S', 'N', 'A', 'P', 'P', 'Y', 0};
+    if (n < 16) return false;
+    for (int i = 0; i < 8; i++)
+        if (in_byte(in, i) != magic[i]) return false;
+    if ((int32_t)in_le32(in, 12) < 1) return false;
+    int64_t pos = 16;
+    uint32_t nb = 0;
+    while (pos != n) {
+        if (n - pos < 4) return false;
+        const int32_t clen = (int32_t)((in_byte(in, pos) << 24) | (in_byte(in, pos + 1) << 16) |
+                                       (in_byte(in, pos + 2) << 8) | in_byte(in, pos + 3));
+        pos += 4;
+        if (clen < 0 || n - pos < (int64_t)clen) return false;
+        uint32_t ulen;
+        int64_t used;
+        if (snappy_varint_in(in, pos, clen, ulen, used)) return false;
+        if ((uint64_t)ulen > 22ull * (uint64_t)clen + 64) return false;
+        pos += clen;
+        nb++;
+    }
+    if (nb == 0) return false;
+    const uint32_t first = reserve_blocks(j, nb);
+    if (first == 0xFFFFFFFFu) return false;
+    pos = 16;
+    uint64_t plan = 0;
+    for (uint32_t k = 0; k < nb; k++) {
+        const int32_t clen = (int32_t)((in_byte(in, pos) << 24) | (in_byte(in, pos + 1) << 16) |
+                                       (in_byte(in, pos + 2) << 8) | in_byte(in, pos + 3));
+        pos += 4;
+        uint32_t ulen;
+        int64_t used;
+        snappy_varint_in(in, pos, clen, ulen, used);
+        if (lane() == 0) {
+            BlockItem it;
+            it.src = src_abs + (uint64_t)pos;
+            it.dst = dst_abs + plan;
+            it.csize = (uint32_t)clen;
+            it.kind = kBlkSnappy;
+            it.out = -1;
+            it.cap = ulen;
+            j.blocks[first + k] = it;
+        }
+        plan += ulen;
+        pos += clen;
+    }
+    fp.mode = 2;
+    fp.first = first;
+    fp.nb = nb;
+    fp.ccs = 0;
+    fp.ccs_val = 0;
+    fp.csf = 0;
+    fp.content_size = 0;
+    return true;
+}
+
+// ---------------------------------------------------------------------------
 // k_decode: one wave per compressed batch of the job (work list built by
-// k_emit), claimed dynamically so 64 KiB and 1 MiB payloads balance.  Each
-// item writes only its own batch result and its own planned arena slot.
+// k_emit), claimed dynamically.  Block-parallel frames are only planned here;
+// the rest are decoded on the spot.  Each item writes only its own batch
+// result, its own plan and its own planned arena slot.
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void k_decode(DeviceJob j) {
     const uint32_t count = j.counters[2];
@@ -530,18 +704,137 @@ __global__ __launch_bounds__(256) void k_decode(DeviceJob j) {
         const uint64_t doff = uni64(j.dcap[b]);
         const uint64_t cap = uni64(j.dcap[b + 1]) - doff;
         uint32_t addf = 0, dl = 0;
+        FramePlan fp;
+        fp.mode = 0;
         if (doff + cap > j.decoded_capacity) {
             addf = RPGPU_F_DECODE_OVERFLOW;
         } else {
-            int64_t got = 0;
-            if (decode_payload(codec, j.data + S, n, j.decoded + doff, got) == 0) {
-                addf = RPGPU_F_CODEC_OK;
-                dl = (uint32_t)got;
+            In in;
+            in_init(in, j.data + S, n);
+            bool planned = false;
+            if (n > 0 && j.block_capacity) {
+                if (codec == RPGPU_CODEC_LZ4) planned = plan_lz4f(j, in, n, S, doff, fp);
+                else if (codec == RPGPU_CODEC_SNAPPY) planned = plan_snappy_java(j, in, n, S, doff, fp);
+            }
+            if (!planned) {
+                fp.mode = 0;
+                int64_t got = 0;
+                if (decode_payload(codec, j.data + S, n, j.decoded + doff, got) == 0) {
+                    addf = RPGPU_F_CODEC_OK;
+                    dl = (uint32_t)got;
+                }
             }
         }
-        if (lane() == 0 && addf) {
-            R->flags = R->flags | addf;
-            if (addf & RPGPU_F_CODEC_OK) R->decoded_len = dl;
+        if (lane() == 0) {
+            if (j.block_capacity) j.plans[item] = fp;
+            if (addf) {
+                R->flags = R->flags | addf;
+                if (addf & RPGPU_F_CODEC_OK) R->decoded_len = dl;
+            }
+        }
+    }
+}
+
+// one wave per BlockItem, wave-strided (a dynamic lane-0 atomic claim here
+// compiled to a loop that never terminated on gfx950)
+__global__ __launch_bounds__(256) void k_decode_blocks(DeviceJob j) {
+    const uint32_t reserved = j.counters[4];
+    const uint32_t count = reserved < j.block_capacity ? reserved : j.block_capacity;
+#ifdef RPGPU_CHECKED
+    const uint64_t t_start = __builtin_amdgcn_s_memtime();
+    if (blockIdx.x == 0 && threadIdx.x == 0) printf("RPGPU_CHECK blocks reserved=%u cap=%u\n", reserved, j.block_capacity);
+#endif
+    const uint32_t nw = gridDim.x * (blockDim.x >> 6);
+    for (uint32_t item = blockIdx.x * (blockDim.x >> 6) + uni32(threadIdx.x >> 6); item < count; item += nw) {
+#ifdef RPGPU_CHECKED
+        if (__builtin_amdgcn_s_memtime() - t_start > 20000000000ull) {
+            if (lane() == 0) printf("RPGPU_CHECK blocks timeout at item %u\n", item);
+            break;
+        }
+#endif
+        const BlockItem it = j.blocks[item];
+        const uint64_t srcp = uni64(it.src), dstp = uni64(it.dst);
+        const uint32_t csize = uni32(it.csize), kind = uni32(it.kind), bcap = uni32(it.cap);
+#ifdef RPGPU_CHECKED
+        if (lane() == 0)
+            printf("RPGPU_CHECK block %u src=%llu dst=%llu csize=%u kind=%u cap=%u dlen=%llu dcap=%llu\n", item,
+                   (unsigned long long)srcp, (unsigned long long)dstp, csize, kind, bcap,
+                   (unsigned long long)j.data_len, (unsigned long long)j.decoded_capacity);
+#endif
+        const uint8_t* src = j.data + srcp;
+        uint8_t* dst = j.decoded + dstp;
+        int64_t out = -1;
+        In in;
+        in_init(in, src, csize);
+        if (kind & kBlkSnappy) {
+            int64_t got = 0;
+            if (snappy_raw_checked(in, src, csize, dst, got) == 0) out = got;
+        } else {
+            // dstage_getBlockChecksum before the block is used
+            bool ok = true;
+            if (kind & kBlkChecksum) {
+                In cin;
+                in_init(cin, src + csize, 4);
+                ok = in_le32(cin, 0) == xxh32_dev(src, csize, 0);
+            }
+            if (ok) {
+                if (kind & kBlkRaw) {
+                    copy_lit(dst, 0, src, 0, csize);
+                    out = csize;
+                } else {
+                    int64_t fenced = 0;
+                    out = lz4_block(in, src, csize, dst, bcap, 0, fenced);
+                }
+            }
+        }
+        if (lane() == 0) j.blocks[item].out = (int32_t)(out < 0 ? -1 : out);
+    }
+}
+
+// one wave per block-parallel frame: all pieces decoded, moved together
+// when an earlier one came out short, content size / checksum checked
+__global__ __launch_bounds__(256) void k_decode_finish(DeviceJob j) {
+    const uint32_t count = j.counters[2];
+    const uint32_t nw = gridDim.x * (blockDim.x >> 6);
+    for (uint32_t item = blockIdx.x * (blockDim.x >> 6) + uni32(threadIdx.x >> 6); item < count; item += nw) {
+        const FramePlan fp = j.plans[item];
+        if (uni32(fp.mode) == 0) continue;
+        const uint32_t first = uni32(fp.first), nb = uni32(fp.nb);
+        const uint64_t b = j.decode_list[item];
+        rpgpu_batch_result* R = &j.batches[b];
+        const uint64_t d0 = uni64(j.dcap[b]);
+        bool ok = true;
+        uint64_t run = d0;  // where the next piece belongs
+        for (uint32_t k = 0; k < nb; k++) {
+            const BlockItem it = j.blocks[first + k];
+            const int32_t out = (int32_t)uni32((uint32_t)it.out);
+            if (out < 0) { ok = false; break; }
+            const uint64_t at = uni64(it.dst);
+            if (at != run) {
+                // forward move to a lower address, 64 bytes per step: each
+                // step loads before it stores
+                uint8_t* d = j.decoded;
+                for (int64_t o = 0; o < out; o += 64) {
+                    const int64_t k2 = o + lane();
+                    uint8_t v = 0;
+                    if (k2 < out) v = (uint8_t)ld_out8(d + at + k2);
+                    __builtin_amdgcn_s_waitcnt(0);
+                    if (k2 < out) d[run + k2] = v;
+                }
+            }
+            run += (uint64_t)out;
+        }
+        const uint64_t total = run - d0;
+        if (ok && uni32(fp.mode) == 1) {
+            if (uni32(fp.csf) && total != uni64(fp.content_size)) ok = false;  // frameSize_wrong
+            if (ok && uni32(fp.ccs)) {
+                vis_fence();
+                if (xxh32_out(j.decoded + d0, (int64_t)total, 0) != uni32(fp.ccs_val)) ok = false;
+            }
+        }
+        if (lane() == 0 && ok) {
+            R->flags = R->flags | RPGPU_F_CODEC_OK;
+            R->decoded_len = (uint32_t)total;
         }
     }
 }
@@ -558,6 +851,16 @@ __global__ __launch_bounds__(64) void k_uncompress_one(int codec, const uint8_t*
 
 hipError_t launch_decode(const DeviceJob& j, hipStream_t s, uint32_t grid) {
     hipLaunchKernelGGL(k_decode, dim3(grid), dim3(256), 0, s, j);
+    return hipGetLastError();
+}
+
+hipError_t launch_decode_blocks(const DeviceJob& j, hipStream_t s, uint32_t grid) {
+    if (j.block_capacity) hipLaunchKernelGGL(k_decode_blocks, dim3(grid), dim3(256), 0, s, j);
+    return hipGetLastError();
+}
+
+hipError_t launch_decode_finish(const DeviceJob& j, hipStream_t s, uint32_t grid) {
+    if (j.block_capacity) hipLaunchKernelGGL(k_decode_finish, dim3(grid), dim3(256), 0, s, j);
     return hipGetLastError();
 }
 

@@ -66,6 +66,30 @@ struct SegTerm {
     int32_t eof;
 };
 
+// One independently decodable piece of a compressed payload (an LZ4F block
+// of a block-independent frame, or a snappy-java chunk), decoded by its own
+// wave into its planned arena position.
+struct BlockItem {
+    uint64_t src;    // absolute offset of the block data in the job's data
+    uint64_t dst;    // absolute offset in the decoded arena (planned)
+    uint32_t csize;  // block data bytes
+    uint32_t kind;   // kBlk* bits
+    int32_t out;     // decoded bytes, -1 on failure (written by k_decode_blocks)
+    uint32_t cap;    // bytes reserved at dst
+};
+constexpr uint32_t kBlkRaw = 1, kBlkChecksum = 2, kBlkSnappy = 4;
+
+// Per decode item: how its payload is being decoded
+struct FramePlan {
+    uint32_t mode;   // 0 decoded sequentially by k_decode, 1 LZ4F blocks, 2 snappy-java chunks
+    uint32_t first;  // first BlockItem
+    uint32_t nb;     // number of BlockItems
+    uint32_t ccs;    // LZ4F: content checksum present
+    uint64_t content_size;  // LZ4F: content size (0 = absent)
+    uint32_t ccs_val;       // LZ4F: stored content checksum
+    uint32_t csf;           // LZ4F: content size present
+};
+
 struct DeviceJob {
     const uint8_t* data;
     uint64_t data_len;            // bytes of d_data (= h_seg_offsets[n_segments])
@@ -92,8 +116,12 @@ struct DeviceJob {
     rpgpu_job_totals* totals;
     uint64_t* bitmap;
     const Tables* tables;
-    uint32_t* counters;           // [0] rewalks, [1] overflow bits, [2] decode items, [3] decode cursor
+    uint32_t* counters;           // [0] rewalks, [1] overflow bits, [2] decode items, [3] decode cursor,
+                                  // [4] block items reserved
     uint32_t* decode_list;        // batch_capacity: ordinals of batches to uncompress
+    BlockItem* blocks;            // block work list ([4] items reserved, [5] claim cursor)
+    uint32_t block_capacity;
+    FramePlan* plans;             // one per decode item
     uint32_t* seg_first_bad;      // n_segments: first chain ordinal failing complete && crc_ok (atomicMin)
 };
 
@@ -104,6 +132,8 @@ hipError_t launch_resolve(const DeviceJob& j, hipStream_t s);
 hipError_t launch_emit(const DeviceJob& j, hipStream_t s);
 hipError_t launch_validate(const DeviceJob& j, hipStream_t s, uint32_t grid);  // rp_validate.hip
 hipError_t launch_decode(const DeviceJob& j, hipStream_t s, uint32_t grid);    // rp_codec.hip
+hipError_t launch_decode_blocks(const DeviceJob& j, hipStream_t s, uint32_t grid);
+hipError_t launch_decode_finish(const DeviceJob& j, hipStream_t s, uint32_t grid);
 // one payload, one wave (rpgpu_uncompress); res[0] = rc (0 / -1 / -2), res[1] = out_len
 hipError_t launch_uncompress_one(int codec, const uint8_t* src, uint64_t n, uint8_t* dst, uint64_t cap,
                                  int64_t* res, hipStream_t s);

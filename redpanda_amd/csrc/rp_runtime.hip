@@ -300,6 +300,12 @@ int rpgpu_submit(rpgpu_ctx* c, const rpgpu_job* job, void* stream) {
     const size_t o_counters = take(32);
     const size_t o_dlist = take((bcap + 1) * 4);
     const size_t o_fbad = take((size_t)nseg * 4);
+    // block-parallel decode: one item per LZ4F block / snappy-java chunk
+    const bool dec = (job->flags & RPGPU_JOB_DECODE) && job->d_decoded;
+    const uint64_t data_len = job->h_seg_offsets[nseg];
+    const uint64_t bl_cap64 = dec ? std::min<uint64_t>(data_len / 16384 + 2 * bcap + 64, 0x7FFFFFFFull) : 0;
+    const size_t o_blocks = take(bl_cap64 * sizeof(BlockItem));
+    const size_t o_plans = take(dec ? (bcap + 1) * sizeof(FramePlan) : 0);
     const size_t o_scan = take(scan_temp_bytes(std::max<uint64_t>(tc, bcap)) + 64);
     const size_t need = off;
     if (need > c->ws_bytes) {
@@ -338,6 +344,9 @@ int rpgpu_submit(rpgpu_ctx* c, const rpgpu_job* job, void* stream) {
     j.counters = (uint32_t*)(ws + o_counters);
     j.decode_list = (uint32_t*)(ws + o_dlist);
     j.seg_first_bad = (uint32_t*)(ws + o_fbad);
+    j.blocks = (BlockItem*)(ws + o_blocks);
+    j.block_capacity = (uint32_t)bl_cap64;
+    j.plans = (FramePlan*)(ws + o_plans);
     if (((uintptr_t)job->d_decoded & 15) != 0) return fail(c, RPGPU_E_INVALID, "rpgpu_submit: d_decoded must be 16-byte aligned");
     uint64_t* scan_tmp = (uint64_t*)(ws + o_scan);
 
@@ -348,6 +357,8 @@ int rpgpu_submit(rpgpu_ctx* c, const rpgpu_job* job, void* stream) {
     do {                                                                                   \
         HIPCHK(c, (call));                                                                 \
         if (dbg) {                                                                         \
+            fprintf(stderr, "[rpgpu] stage %s\n", name);                                   \
+            fflush(stderr);                                                                \
             hipError_t _e = hipStreamSynchronize(s);                                       \
             if (_e != hipSuccess) return fail(c, RPGPU_E_HIP, "stage " name " failed", _e); \
         }                                                                                  \
@@ -376,7 +387,11 @@ int rpgpu_submit(rpgpu_ctx* c, const rpgpu_job* job, void* stream) {
     STAGE("scan_dcap", scan_exclusive_u64_devn(j.dcap, d_nb, bcap, scan_tmp, s));
     if (tm) HIPCHK(c, hipEventRecord(ev[2], s));
     // decode first: k_validate checksums and walks the decoded payloads
-    if ((job->flags & RPGPU_JOB_DECODE) && j.decoded) STAGE("decode", launch_decode(j, s, c->cu_count * 8));
+    if ((job->flags & RPGPU_JOB_DECODE) && j.decoded) {
+        STAGE("decode", launch_decode(j, s, c->cu_count * 8));
+        STAGE("decode_blocks", launch_decode_blocks(j, s, c->cu_count * 8));
+        STAGE("decode_finish", launch_decode_finish(j, s, c->cu_count * 8));
+    }
     if (tm) HIPCHK(c, hipEventRecord(ev[3], s));
     STAGE("validate", launch_validate(j, s, c->cu_count));
     if (tm) HIPCHK(c, hipEventRecord(ev[4], s));
