@@ -194,17 +194,24 @@ def main():
     ms_per_step = elapsed / args.steps * 1e3
     value = job_bytes * args.steps / elapsed / 1e9
 
-    # roofline of the dominant kernel (k_validate): algorithmic bytes per
-    # launch = payload read once + 64 B per record index entry written +
-    # 128 B per batch result (read + write of the verdict struct counted once)
-    alg = payload_bytes + 64 * n_records + 128 * n_batches
+    # roofline of the dominant kernel (k_validate: CRC32C of every stored
+    # payload): algorithmic bytes per launch = payload read once + 128 B per
+    # batch result (descriptor read + verdict written, counted once).  The
+    # record walk runs in k_walk (index writes: 64 B per record + the result
+    # struct), reported beside it.
+    alg = payload_bytes + 128 * n_batches
     v_ms = tm["validate"]
     achieved = alg / (v_ms * 1e-3) / 1e9
+    walk_alg = 64 * n_records + 128 * n_batches
+    w_ms = tm.get("walk", 0.0)
     traffic = None
     tfile = os.path.join(ROOT, "profiles", "validate_traffic.json")  # refreshed by scripts/parse_profile.py
     if os.path.exists(tfile):
         try:
-            traffic = json.load(open(tfile)).get("bytes_per_launch")
+            tj = json.load(open(tfile))
+            # only a profile of the same kernel split counts
+            if tj.get("alg_def") == "payload+128B/batch":
+                traffic = tj.get("bytes_per_launch")
         except Exception:
             traffic = None
 
@@ -249,6 +256,8 @@ def main():
                 "traffic": traffic,
                 "alg_bytes_per_launch": alg,
                 "kernel_ms": round(v_ms, 4),
+                "walk": {"kernel": "k_walk", "kernel_ms": round(w_ms, 4), "alg_bytes_per_launch": walk_alg,
+                         "achieved": round(walk_alg / (w_ms * 1e-3) / 1e9, 1) if w_ms > 0 else None},
             },
             "cpu_baseline": cpu,
         }

@@ -273,7 +273,8 @@ int rpgpu_submit(rpgpu_ctx* ctx, const rpgpu_job* job, void* stream);
  * the launch stream, averaged over every timed rpgpu_submit since the
  * previous call (milliseconds; the call resets the average).  Indices:
  * 0 = whole pipeline, 1 = discover, 2 = resolve+emit+plan, 3 = validate,
- * 4 = decode (0 when the job has no RPGPU_JOB_DECODE). */
+ * 4 = decode (0 when the job has no RPGPU_JOB_DECODE), 5 = lane record walk
+ * of stored payloads (k_walk; 0 without RPGPU_JOB_PARSE). */
 int rpgpu_last_timings(rpgpu_ctx* ctx, float* ms, int n);
 /* Enable/disable per-kernel event timing (off by default). */
 int rpgpu_set_timing(rpgpu_ctx* ctx, int enable);

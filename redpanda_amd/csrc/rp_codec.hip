@@ -86,31 +86,94 @@ DEV uint32_t ld_out32(const uint8_t* p) {  // 4 bytes at any address
     return __builtin_amdgcn_alignbyte(hi, lo, sh);
 }
 
-DEV void copy_lit(uint8_t* dst, int64_t op, const uint8_t* src, int64_t ip, int64_t len) {
-    for (int64_t k = lane(); k < len; k += 64) dst[op + k] = src[ip + k];
+// Output of one decode: the arena, plus an optional per-wave LDS ring of the
+// last kRing output bytes.  Near matches (offset + length <= kRing) read the
+// ring: LDS is in order within a wave, so no fence and no round trip through
+// L2.  Far matches read the arena behind a fence with L1-bypassing loads.
+typedef __attribute__((address_space(3))) uint8_t lds_u8;
+#ifndef RPGPU_RING_BYTES
+#define RPGPU_RING_BYTES 8192
+#endif
+constexpr int64_t kRing = RPGPU_RING_BYTES > 0 ? RPGPU_RING_BYTES : 1;  // 0: no ring
+constexpr uint32_t kRingWaves = 4;  // waves per workgroup of the decode kernels
+
+struct Out {
+    uint8_t* dst;
+    lds_u8* ring;    // nullptr: no ring
+    int64_t fenced;  // arena bytes below this are visible to loads
+};
+
+DEV void out_init(Out& o, uint8_t* dst, lds_u8* ring) {
+    o.dst = dst;
+    o.ring = ring;
+    o.fenced = 0;
 }
 
-// forward copy dst[op + k] = dst[op + k - off] (k < len): with off < len the
+DEV void put(Out& o, int64_t at, uint32_t v, bool valid) {
+    if (valid) {
+        o.dst[at] = (uint8_t)v;
+        if (o.ring) o.ring[at & (kRing - 1)] = (uint8_t)v;
+    }
+}
+
+// literals: src[ip, ip + len) -> out[op, ...).  Bytes inside the 256-byte
+// input window come from its registers (ds_bpermute), the rest from memory.
+DEV void copy_lit(Out& o, int64_t op, In& in, const uint8_t* src, int64_t ip, int64_t len) {
+    if (len <= 0) return;
+    if (ip < in.base || ip >= in.base + 192) in_load(in, ip);
+    for (int64_t c = 0; c < len; c += 64) {
+        const int64_t k = c + (int64_t)lane();
+        const bool valid = k < len;
+        const int64_t w = ip + k - in.base;
+        const bool inwin = w >= 0 && w < 256;
+        const uint32_t word = (uint32_t)__shfl((int)in.w, (int)((w >> 2) & 63), 64);
+        uint32_t v = (word >> (8 * (uint32_t)(w & 3))) & 0xFFu;
+        if (valid && !inwin) v = src[ip + k];
+        put(o, op + k, v, valid);
+    }
+}
+
+// raw bytes straight from memory (stored LZ4 blocks)
+DEV void copy_raw(Out& o, int64_t op, const uint8_t* src, int64_t ip, int64_t len) {
+    for (int64_t c = 0; c < len; c += 64) {
+        const int64_t k = c + (int64_t)lane();
+        const bool valid = k < len;
+        put(o, op + k, valid ? (uint32_t)src[ip + k] : 0u, valid);
+    }
+}
+
+// forward copy out[op + k] = out[op + k - off] (k < len): with off < len the
 // source repeats with period off; off == 0 writes zeros (as liblz4's
-// write32(op, 0) / LZ4_memcpy_using_offset_base produce).  `fenced`: output
-// positions below it are visible to loads.
-DEV void copy_match(uint8_t* dst, int64_t op, int64_t off, int64_t len, int64_t& fenced) {
+// write32(op, 0) / LZ4_memcpy_using_offset_base produce)
+DEV void copy_match(Out& o, int64_t op, int64_t off, int64_t len) {
     if (len <= 0) return;
     if (off == 0) {
-        for (int64_t k = lane(); k < len; k += 64) dst[op + k] = 0;
+        for (int64_t c = 0; c < len; c += 64) put(o, op + c + lane(), 0u, c + (int64_t)lane() < len);
         return;
     }
     const int64_t s0 = op - off;
-    const int64_t span = off < len ? off : len;
-    if (s0 + span > fenced) {
-        vis_fence();
-        fenced = op;
+    if (o.ring && off + len <= kRing) {
+        // every source byte is below op and within the ring
+        for (int64_t c = 0; c < len; c += 64) {
+            const int64_t k = c + (int64_t)lane();
+            const bool valid = k < len;
+            const int64_t sk = off >= len ? k : (int64_t)((uint32_t)k % (uint32_t)off);
+            const uint32_t v = valid ? (uint32_t)o.ring[(s0 + sk) & (kRing - 1)] : 0u;
+            put(o, op + k, v, valid);
+        }
+        return;
     }
-    if (off >= len) {
-        for (int64_t k = lane(); k < len; k += 64) dst[op + k] = (uint8_t)ld_out8(dst + s0 + k);
-    } else {
-        const uint32_t uo = (uint32_t)off;
-        for (int64_t k = lane(); k < len; k += 64) dst[op + k] = (uint8_t)ld_out8(dst + s0 + (int64_t)((uint32_t)k % uo));
+    const int64_t span = off < len ? off : len;
+    if (s0 + span > o.fenced) {
+        vis_fence();
+        o.fenced = op;
+    }
+    for (int64_t c = 0; c < len; c += 64) {
+        const int64_t k = c + (int64_t)lane();
+        const bool valid = k < len;
+        const int64_t sk = off >= len ? k : (int64_t)((uint32_t)k % (uint32_t)off);
+        const uint32_t v = valid ? ld_out8(o.dst + s0 + sk) : 0u;
+        put(o, op + k, v, valid);
     }
 }
 
@@ -176,7 +239,7 @@ DEV uint32_t lz_read_var(In& in, int64_t& ip, int64_t lencheck, bool loop_check,
     return length;
 }
 
-DEV int64_t lz4_block(In& in, const uint8_t* src, int64_t n, uint8_t* dst, int64_t oend, int64_t H, int64_t& fenced) {
+DEV int64_t lz4_block(In& in, const uint8_t* src, int64_t n, Out& o, int64_t obase, int64_t oend, int64_t H) {
     const int64_t iend = n;
     int64_t ip = 0, op = 0;
     const int64_t shortiend = iend - 14 - 2, shortoend = oend - 14 - 18;
@@ -196,13 +259,13 @@ DEV int64_t lz4_block(In& in, const uint8_t* src, int64_t n, uint8_t* dst, int64
             if (err == 1) return -1;
             cpy = op + length;
             if (cpy > oend - 32 || ip + length > iend - 32) goto safe_literal_copy;
-            copy_lit(dst, op, src, ip, length);
+            copy_lit(o, obase + op, in, src, ip, length);
             ip += length;
             op = cpy;
         } else {
             cpy = op + length;
             if (ip > iend - (16 + 1)) goto safe_literal_copy;
-            copy_lit(dst, op, src, ip, length);
+            copy_lit(o, obase + op, in, src, ip, length);
             ip += length;
             op = cpy;
         }
@@ -219,13 +282,13 @@ DEV int64_t lz4_block(In& in, const uint8_t* src, int64_t n, uint8_t* dst, int64
             length += kMinMatch;
             if (op + length >= oend - kFastSafeDistance) goto safe_match_copy;
             if (offset <= op + H && offset >= 8) {
-                copy_match(dst, op, offset, length, fenced);
+                copy_match(o, obase + op, offset, length);
                 op += length;
                 continue;
             }
         }
         if (offset > op + H) return -1;
-        copy_match(dst, op, offset, length, fenced);
+        copy_match(o, obase + op, offset, length);
         op += length;
     }
 
@@ -234,14 +297,14 @@ safe_decode:
         token = in_byte(in, ip++);
         length = token >> 4;
         if (length != 15 && ip < shortiend && op <= shortoend) {
-            copy_lit(dst, op, src, ip, length);
+            copy_lit(o, obase + op, in, src, ip, length);
             op += length;
             ip += length;
             length = token & 15;
             offset = in_le16(in, ip);
             ip += 2;
             if (length != 15 && offset >= 8 && offset <= op + H) {
-                copy_match(dst, op, offset, length + kMinMatch, fenced);
+                copy_match(o, obase + op, offset, length + kMinMatch);
                 op += length + kMinMatch;
                 continue;
             }
@@ -255,12 +318,12 @@ safe_decode:
     safe_literal_copy:
         if (cpy > oend - kMfLimit || ip + length > iend - (2 + 1 + kLastLiterals)) {
             if (ip + length != iend || cpy > oend) return -1;
-            copy_lit(dst, op, src, ip, length);
+            copy_lit(o, obase + op, in, src, ip, length);
             ip += length;
             op += length;
             break;
         }
-        copy_lit(dst, op, src, ip, length);
+        copy_lit(o, obase + op, in, src, ip, length);
         ip += length;
         op = cpy;
         offset = in_le16(in, ip);
@@ -277,7 +340,7 @@ safe_decode:
         if (offset > op) {
             // match starts in the history (prefix / external dictionary)
             if (op + length > oend - kLastLiterals) return -1;
-            copy_match(dst, op, offset, length, fenced);
+            copy_match(o, obase + op, offset, length);
             op += length;
             continue;
         }
@@ -285,7 +348,7 @@ safe_decode:
         if (cpy > oend - kMfLimit) {
             if (cpy > oend - kLastLiterals) return -1;
         }
-        copy_match(dst, op, offset, length, fenced);
+        copy_match(o, obase + op, offset, length);
         op = cpy;
     }
     return op;
@@ -299,7 +362,7 @@ safe_decode:
 // returned.  dst has room for the planned capacity (decode_capacity_dev).
 // Returns 0 (out_len set) or -1 where the reference throws.
 // ---------------------------------------------------------------------------
-DEV int lz4f_decode(In& in, const uint8_t* s, int64_t n, uint8_t* dst, int64_t& out_len) {
+DEV int lz4f_decode(In& in, const uint8_t* s, int64_t n, Out& o, int64_t& out_len) {
     out_len = 0;
     if (n < 7) return -1;                                        // frameHeader_incomplete
     const uint32_t magic = in_le32(in, 0);
@@ -337,7 +400,6 @@ DEV int lz4f_decode(In& in, const uint8_t* s, int64_t n, uint8_t* dst, int64_t& 
     uint64_t est = (content_size == 0 || content_size > (uint64_t)n * 255) ? (uint64_t)n * 4 : content_size;
     uint64_t remaining = content_size;
     int64_t out = 0;
-    int64_t fenced = 0;
     for (;;) {
         if (n - pos < 4) { out_len = out; return 0; }            // waiting for a block header
         const uint32_t bh = in_le32(in, pos);
@@ -353,7 +415,7 @@ DEV int lz4f_decode(In& in, const uint8_t* s, int64_t n, uint8_t* dst, int64_t& 
                 const int64_t space = (int64_t)(est - (uint64_t)out), avail = n - pos;
                 int64_t k = left < avail ? left : avail;
                 if (k > space) k = space;
-                copy_lit(dst, out, s, pos, k);
+                copy_raw(o, out, s, pos, k);
                 out += k;
                 pos += k;
                 left -= k;
@@ -374,12 +436,9 @@ DEV int lz4f_decode(In& in, const uint8_t* s, int64_t n, uint8_t* dst, int64_t& 
         const int64_t need = bsz + (bcs ? 4 : 0);
         if (n - pos < need) { out_len = out; return 0; }         // dstage_storeCBlock: wait
         if (bcs && in_le32(in, pos + bsz) != xxh32_dev(s + pos, bsz, 0)) return -1;
-        // earlier blocks (the linked history) must be visible to matches
-        vis_fence();
-        fenced = 0;
         In bin;
         in_init(bin, s + pos, bsz);
-        const int64_t d = lz4_block(bin, s + pos, bsz, dst + out, bmax, linked ? out : 0, fenced);
+        const int64_t d = lz4_block(bin, s + pos, bsz, o, out, bmax, linked ? out : 0);
         if (d < 0) return -1;                                    // decompressionFailed
         pos += need;
         if (content_size) remaining -= (uint64_t)d;
@@ -401,7 +460,7 @@ DEV int lz4f_decode(In& in, const uint8_t* s, int64_t n, uint8_t* dst, int64_t& 
     if (ccs) {
         if (n - pos < 4) { out_len = out; return 0; }
         vis_fence();
-        if (in_le32(in, pos) != xxh32_out(dst, out, 0)) return -1;
+        if (in_le32(in, pos) != xxh32_out(o.dst, out, 0)) return -1;
         pos += 4;
     }
     out_len = out;
@@ -431,8 +490,8 @@ DEV int snappy_varint_in(In& in, int64_t pos, int64_t n, uint32_t& v, int64_t& u
 
 // DecompressAllTags over [ip, n): succeeds iff the tags end exactly at n and
 // exactly ulen bytes come out
-DEV int snappy_tags(In& in, const uint8_t* s, int64_t n, int64_t ip, uint8_t* dst, int64_t ulen) {
-    int64_t op = 0, fenced = 0;
+DEV int snappy_tags(In& in, const uint8_t* s, int64_t n, int64_t ip, Out& o, int64_t obase, int64_t ulen) {
+    int64_t op = 0;
     while (ip < n) {
         const uint32_t c = in_byte(in, ip);
         int64_t extra;
@@ -453,7 +512,7 @@ DEV int snappy_tags(In& in, const uint8_t* s, int64_t n, int64_t ip, uint8_t* ds
             }
             if (n - ip < lit) return -1;       // premature end of input
             if (ulen - op < lit) return -1;    // SnappyArrayWriter::Append overflow
-            copy_lit(dst, op, s, ip, lit);
+            copy_lit(o, obase + op, in, s, ip, lit);
             op += lit;
             ip += lit;
         } else {
@@ -471,39 +530,39 @@ DEV int snappy_tags(In& in, const uint8_t* s, int64_t n, int64_t ip, uint8_t* ds
             ip += extra;
             // AppendFromSelf: Produced() <= offset - 1u || op_end > op_limit_
             if (off == 0 || op < off || ulen - op < len) return -1;
-            copy_match(dst, op, off, len, fenced);
+            copy_match(o, obase + op, off, len);
             op += len;
         }
     }
     return op == ulen ? 0 : -1;
 }
 
-DEV int snappy_raw_checked(In& in, const uint8_t* s, int64_t n, uint8_t* dst, int64_t& out_len) {
+DEV int snappy_raw_checked(In& in, const uint8_t* s, int64_t n, Out& o, int64_t obase, int64_t& out_len) {
     uint32_t ulen;
     int64_t used;
     if (snappy_varint_in(in, 0, n, ulen, used)) return -1;
     // no tag sequence expands more than 64/3 per input byte
     if ((uint64_t)ulen > 22ull * (uint64_t)n + 64) return -1;
-    if (snappy_tags(in, s, n, used, dst, ulen)) return -1;
+    if (snappy_tags(in, s, n, used, o, obase, ulen)) return -1;
     out_len = ulen;
     return 0;
 }
 
-DEV int snappy_raw(In& in, const uint8_t* s, int64_t n, uint8_t* dst, int64_t& out_len) {
+DEV int snappy_raw(In& in, const uint8_t* s, int64_t n, Out& o, int64_t& out_len) {
     uint32_t ulen;
     int64_t used;
     out_len = 0;
     if (snappy_varint_in(in, 0, n, ulen, used)) return -1;
     if (ulen == 0) return 0;  // "empty frame": RawUncompress is not called
-    return snappy_raw_checked(in, s, n, dst, out_len);
+    return snappy_raw_checked(in, s, n, o, 0, out_len);
 }
 
-DEV int snappy_java(In& in, const uint8_t* s, int64_t n, uint8_t* dst, int64_t& out_len) {
+DEV int snappy_java(In& in, const uint8_t* s, int64_t n, Out& o, int64_t& out_len) {
     out_len = 0;
     const uint8_t magic[8] = {0x82, 'S', 'N', 'A', 'P', 'P', 'Y', 0};
     bool java = n >= 16;
     for (int i = 0; i < 8 && java; i++) java = in_byte(in, i) == magic[i];
-    if (!java) return snappy_raw(in, s, n, dst, out_len);
+    if (!java) return snappy_raw(in, s, n, o, out_len);
     const int32_t min_version = (int32_t)in_le32(in, 12);  // native little endian
     if (min_version < 1) return -1;
     int64_t pos = 16, out = 0;
@@ -517,7 +576,7 @@ DEV int snappy_java(In& in, const uint8_t* s, int64_t n, uint8_t* dst, int64_t& 
         In cin;
         in_init(cin, s + pos, clen);
         int64_t got = 0;
-        if (snappy_raw_checked(cin, s + pos, clen, dst + out, got)) return -1;
+        if (snappy_raw_checked(cin, s + pos, clen, o, out, got)) return -1;
         out += got;
         pos += clen;
     }
@@ -526,13 +585,15 @@ DEV int snappy_java(In& in, const uint8_t* s, int64_t n, uint8_t* dst, int64_t& 
 }
 
 // compression::compressor::uncompress dispatch (compression/compression.cc:34-55)
-DEV int decode_payload(int codec, const uint8_t* s, int64_t n, uint8_t* dst, int64_t& out_len) {
+DEV int decode_payload(int codec, const uint8_t* s, int64_t n, uint8_t* dst, lds_u8* ring, int64_t& out_len) {
     out_len = 0;
     if (n == 0) return -1;
     In in;
     in_init(in, s, n);
-    if (codec == RPGPU_CODEC_SNAPPY) return snappy_java(in, s, n, dst, out_len);
-    if (codec == RPGPU_CODEC_LZ4) return lz4f_decode(in, s, n, dst, out_len);
+    Out o;
+    out_init(o, dst, ring);
+    if (codec == RPGPU_CODEC_SNAPPY) return snappy_java(in, s, n, o, out_len);
+    if (codec == RPGPU_CODEC_LZ4) return lz4f_decode(in, s, n, o, out_len);
     return -1;
 }
 
@@ -688,7 +749,16 @@ DEV bool plan_snappy_java(const DeviceJob& j, In& in, int64_t n, uint64_t src_ab
 // the rest are decoded on the spot.  Each item writes only its own batch
 // result, its own plan and its own planned arena slot.
 // ---------------------------------------------------------------------------
+#if RPGPU_RING_BYTES > 0
+#define RP_WAVE_RING(name)                              \
+    __shared__ uint8_t name##_lds[kRingWaves * kRing]; \
+    lds_u8* name = (lds_u8*)(name##_lds + (threadIdx.x >> 6) * kRing)
+#else
+#define RP_WAVE_RING(name) lds_u8* name = nullptr
+#endif
+
 __global__ __launch_bounds__(256) void k_decode(DeviceJob j) {
+    RP_WAVE_RING(ring);
     const uint32_t count = j.counters[2];
     for (;;) {
         uint32_t item = 0;
@@ -719,7 +789,7 @@ __global__ __launch_bounds__(256) void k_decode(DeviceJob j) {
             if (!planned) {
                 fp.mode = 0;
                 int64_t got = 0;
-                if (decode_payload(codec, j.data + S, n, j.decoded + doff, got) == 0) {
+                if (decode_payload(codec, j.data + S, n, j.decoded + doff, ring, got) == 0) {
                     addf = RPGPU_F_CODEC_OK;
                     dl = (uint32_t)got;
                 }
@@ -738,6 +808,7 @@ __global__ __launch_bounds__(256) void k_decode(DeviceJob j) {
 // one wave per BlockItem, wave-strided (a dynamic lane-0 atomic claim here
 // compiled to a loop that never terminated on gfx950)
 __global__ __launch_bounds__(256) void k_decode_blocks(DeviceJob j) {
+    RP_WAVE_RING(ring);
     const uint32_t reserved = j.counters[4];
     const uint32_t count = reserved < j.block_capacity ? reserved : j.block_capacity;
 #ifdef RPGPU_CHECKED
@@ -766,9 +837,11 @@ __global__ __launch_bounds__(256) void k_decode_blocks(DeviceJob j) {
         int64_t out = -1;
         In in;
         in_init(in, src, csize);
+        Out o;
+        out_init(o, dst, ring);
         if (kind & kBlkSnappy) {
             int64_t got = 0;
-            if (snappy_raw_checked(in, src, csize, dst, got) == 0) out = got;
+            if (snappy_raw_checked(in, src, csize, o, 0, got) == 0) out = got;
         } else {
             // dstage_getBlockChecksum before the block is used
             bool ok = true;
@@ -779,11 +852,10 @@ __global__ __launch_bounds__(256) void k_decode_blocks(DeviceJob j) {
             }
             if (ok) {
                 if (kind & kBlkRaw) {
-                    copy_lit(dst, 0, src, 0, csize);
+                    copy_raw(o, 0, src, 0, csize);
                     out = csize;
                 } else {
-                    int64_t fenced = 0;
-                    out = lz4_block(in, src, csize, dst, bcap, 0, fenced);
+                    out = lz4_block(in, src, csize, o, 0, bcap, 0);
                 }
             }
         }
@@ -841,8 +913,9 @@ __global__ __launch_bounds__(256) void k_decode_finish(DeviceJob j) {
 
 __global__ __launch_bounds__(64) void k_uncompress_one(int codec, const uint8_t* src, uint64_t n, uint8_t* dst,
                                                        int64_t* res) {
+    RP_WAVE_RING(ring);
     int64_t got = 0;
-    const int rc = decode_payload(codec, src, (int64_t)n, dst, got);
+    const int rc = decode_payload(codec, src, (int64_t)n, dst, ring, got);
     if (lane() == 0) {
         res[0] = rc;
         res[1] = got;

@@ -131,6 +131,7 @@ hipError_t launch_discover(const DeviceJob& j, hipStream_t s);
 hipError_t launch_resolve(const DeviceJob& j, hipStream_t s);
 hipError_t launch_emit(const DeviceJob& j, hipStream_t s);
 hipError_t launch_validate(const DeviceJob& j, hipStream_t s, uint32_t grid);  // rp_validate.hip
+hipError_t launch_walk(const DeviceJob& j, hipStream_t s, uint32_t grid);
 hipError_t launch_decode(const DeviceJob& j, hipStream_t s, uint32_t grid);    // rp_codec.hip
 hipError_t launch_decode_blocks(const DeviceJob& j, hipStream_t s, uint32_t grid);
 hipError_t launch_decode_finish(const DeviceJob& j, hipStream_t s, uint32_t grid);

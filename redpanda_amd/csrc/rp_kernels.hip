@@ -42,35 +42,6 @@ DEV uint32_t find_segment(const uint64_t* __restrict__ chunk_base, uint32_t nseg
     return lo;
 }
 
-// Cheap plausibility test of a candidate header at q (speculation only: a
-// wrong guess is caught by k_resolve, so this never decides a verdict).
-DEV bool prefilter(const uint8_t* __restrict__ seg, uint64_t len, uint64_t q) {
-    if (len - q < RPGPU_HEADER_SIZE) return false;
-    uint32_t hcrc = ldu32(seg + q);
-    int32_t size = (int32_t)ldu32(seg + q + 4);
-    if (hcrc == 0 || size < (int32_t)RPGPU_HEADER_SIZE) return false;
-    if ((uint64_t)size > len - q) return false;
-    uint32_t t = ldu32(seg + q + 16);
-    int8_t type = (int8_t)(t & 0xFF);
-    if (type < 1 || type > 32) return false;
-    uint32_t attrs = (ldu32(seg + q + 21) & 0xFFFF);
-    if ((attrs & 7) > 4) return false;
-    int32_t rc = (int32_t)ldu32(seg + q + 57);
-    if (rc < 0 || rc > size) return false;
-    return true;
-}
-
-// wire layout: a v2 header whose batch_length fits the segment
-DEV bool prefilter_wire(const uint8_t* __restrict__ seg, uint64_t len, uint64_t q) {
-    if (len - q < RPGPU_HEADER_SIZE) return false;
-    const uint8_t* h = seg + q;
-    const int64_t size = (int64_t)(int32_t)((uint32_t)h[8] << 24 | (uint32_t)h[9] << 16 | (uint32_t)h[10] << 8 | h[11]) + 12;
-    if (size < (int64_t)RPGPU_HEADER_SIZE || (uint64_t)size > len - q) return false;
-    if (h[16] != 2 || (h[22] & 7) > 4) return false;
-    const int32_t rc = (int32_t)((uint32_t)h[57] << 24 | (uint32_t)h[58] << 16 | (uint32_t)h[59] << 8 | h[60]);
-    return rc >= 0 && rc <= size;
-}
-
 struct WalkOut {
     uint64_t exit;
     uint64_t tpos;
@@ -101,6 +72,92 @@ DEV WalkOut wave_walk(uint32_t layout, const uint8_t* __restrict__ seg, uint64_t
     return w;
 }
 
+// Discovery scan (speculation only: a wrong guess is caught by k_resolve,
+// so none of this decides a verdict).  A 1 KiB step covers positions
+// a + 16 l + i (a 16-aligned, lane l, i < 16) from five coalesced 16-byte
+// loads per lane that hold every field a header check reads (bytes i .. i +
+// 60); the next step's loads are in flight while a step is tested.
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+struct ScanWin {
+    uint32_t w[20];
+};
+
+DEV void scan_load(const uint8_t* __restrict__ data, uint64_t data_len, uint64_t a, ScanWin& sw) {
+    const uint64_t la = a + 16ull * lane();
+#pragma unroll
+    for (int k = 0; k < 5; k++) {
+        const uint64_t x = la + 16ull * k;
+        u32x4 v = {0, 0, 0, 0};
+        if (x + 16 <= data_len) v = __builtin_nontemporal_load((const u32x4*)(data + x));
+        sw.w[4 * k] = v.x; sw.w[4 * k + 1] = v.y; sw.w[4 * k + 2] = v.z; sw.w[4 * k + 3] = v.w;
+    }
+}
+
+// Plausible header fields (disk or wire) given the 61 header bytes through
+// W32(o) / B(o); `rem` = bytes from the header to the segment end.  The
+// base_offset sign bit must be clear (offsets are never negative in a real
+// log; a real header this misses only costs a re-walk in k_resolve).
+#define RP_PLAUSIBLE(layout, W32, B, rem, size_out)                                                          \
+    ((layout) == RPGPU_LAYOUT_WIRE                                                                           \
+         ? ((size_out) = (int32_t)__builtin_bswap32(W32(8)) + 12,                                            \
+            (B(0) & 0x80u) == 0 && (int32_t)__builtin_bswap32(W32(8)) >= (int32_t)RPGPU_HEADER_SIZE - 12 &&  \
+                (uint32_t)(size_out) <= (rem) && B(16) == 2u && (B(22) & 7u) <= 4u &&                       \
+                (int32_t)__builtin_bswap32(W32(57)) >= 0 && (int32_t)__builtin_bswap32(W32(57)) <= (size_out)) \
+         : ((size_out) = (int32_t)W32(4),                                                                    \
+            W32(0) != 0u && (size_out) >= (int32_t)RPGPU_HEADER_SIZE && (uint32_t)(size_out) <= (rem) &&     \
+                (B(15) & 0x80u) == 0 && B(16) - 1u < 32u && (B(21) & 7u) <= 4u && (int32_t)W32(57) >= 0 &&  \
+                (int32_t)W32(57) <= (size_out)))
+
+// the header a candidate's size points at must be plausible too (or lie in
+// the last 61 bytes of the segment): random payload bytes pass the field
+// checks about once per KiB, both checks about once per GiB
+DEV bool follow_ok(uint32_t layout, const uint8_t* __restrict__ seg, uint64_t len, uint64_t q) {
+    if (len - q < RPGPU_HEADER_SIZE) return true;
+    const uint8_t* h = seg + q;
+    const uint32_t f0 = ldu32(h), f4 = ldu32(h + 4), f8 = ldu32(h + 8), f12 = ldu32(h + 12), f16 = ldu32(h + 16),
+                   f21 = ldu32(h + 21), f57 = ldu32(h + 57);
+#define RP_W32(o) ((o) == 0 ? f0 : (o) == 4 ? f4 : (o) == 8 ? f8 : (o) == 21 ? f21 : f57)
+#define RP_B(o) ((o) == 0 ? (f0 & 0xFFu) : (o) == 15 ? (f12 >> 24) : (o) == 16 ? (f16 & 0xFFu) : (o) == 21 ? (f21 & 0xFFu) : ((f21 >> 8) & 0xFFu))
+    const uint64_t rem64 = len - q;
+    const uint32_t rem = rem64 > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)rem64;
+    int32_t size;
+    const bool ok = RP_PLAUSIBLE(layout, RP_W32, RP_B, rem, size);
+#undef RP_W32
+#undef RP_B
+    return ok;
+}
+
+// candidate bits of a step (bit i = position a + 16 l + i), with the first
+// candidate's follow-up header also checked
+DEV uint32_t scan_step(uint32_t layout, const uint8_t* __restrict__ seg, const ScanWin& sw, uint64_t a, uint64_t off,
+                       uint64_t len, uint64_t cs, uint64_t ce) {
+    const uint64_t la = a + 16ull * lane();
+    // 32-bit bounds relative to this lane's first position r = la - off:
+    // position i is inside the chunk iff lo <= i < hi, and a size fits iff
+    // size <= rem - i (size >= 61 > 0)
+    const int64_t r = (int64_t)(la - off);
+    const int64_t lo64 = (int64_t)cs - r, hi64 = (int64_t)ce - r, rem64 = (int64_t)len - r;
+    const int32_t lo = lo64 < 0 ? 0 : lo64 > 16 ? 16 : (int32_t)lo64;
+    const int32_t hi = hi64 < 0 ? 0 : hi64 > 16 ? 16 : (int32_t)hi64;
+    const uint32_t rem = rem64 < 0 ? 0u : rem64 > 0xFFFFFFFFll ? 0xFFFFFFFFu : (uint32_t)rem64;
+    uint32_t m = 0, fi = 16, fsize = 0;
+#pragma unroll
+    for (int i = 0; i < 16; i++) {
+#define RP_W32(o) __builtin_amdgcn_alignbyte(sw.w[((i) + (o)) / 4 + 1], sw.w[((i) + (o)) / 4], ((i) + (o)) & 3)
+#define RP_B(o) ((sw.w[((i) + (o)) / 4] >> (8 * (((i) + (o)) & 3))) & 0xFFu)
+        const bool in = i >= lo && i < hi && (uint32_t)i + RPGPU_HEADER_SIZE <= rem;
+        int32_t size;
+        const bool pass = RP_PLAUSIBLE(layout, RP_W32, RP_B, rem - (uint32_t)i, size);
+#undef RP_W32
+#undef RP_B
+        const bool c = in && pass;
+        if (c && fi == 16) { fi = i; fsize = (uint32_t)size; }
+        m |= (uint32_t)c << i;
+    }
+    if (fi < 16 && !follow_ok(layout, seg, len, (uint64_t)r + fi + fsize)) m &= ~(1u << fi);
+    return m;
+}
+
 __global__ __launch_bounds__(256) void k_discover(DeviceJob j) {
     const uint64_t g = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
     if (g >= j.total_chunks) return;
@@ -114,17 +171,28 @@ __global__ __launch_bounds__(256) void k_discover(DeviceJob j) {
     if (w == 0) {
         entry = 0;
     } else {
-        for (uint64_t q0 = cs; q0 < ce && entry == kNone; q0 += 64) {
-            const uint64_t q = q0 + lane();
-            bool cand = (q < ce) && (j.layout == RPGPU_LAYOUT_WIRE ? prefilter_wire(seg, len, q) : prefilter(seg, len, q));
-            uint64_t mask = __ballot(cand);
-            while (mask) {
-                const uint32_t bit = __builtin_ctzll(mask);
-                mask &= mask - 1;
-                const uint64_t qc = q0 + bit;
-                Hdr h = wave_header_of(j.layout, seg, len, qc, j.tables);
-                if (h.status < 0 && len - qc - RPGPU_HEADER_SIZE >= h.need) { entry = qc; break; }
+        // candidates in ascending order: lanes cover consecutive 16-byte
+        // spans, bits ascend within a lane
+        uint64_t a = (off + cs) & ~15ull;
+        ScanWin cur, nxt;
+        scan_load(j.data, j.data_len, a, cur);
+        for (; a < off + ce && entry == kNone; a += 1024) {
+            if (a + 1024 < off + ce) scan_load(j.data, j.data_len, a + 1024, nxt);
+            const uint32_t m = scan_step(j.layout, seg, cur, a, off, len, cs, ce);
+            uint64_t lanes = __ballot(m != 0);
+            while (lanes && entry == kNone) {
+                const uint32_t l = __builtin_ctzll(lanes);
+                lanes &= lanes - 1;
+                uint32_t bits = rl(m, (int)l);
+                while (bits) {
+                    const uint32_t i = __builtin_ctz(bits);
+                    bits &= bits - 1;
+                    const uint64_t qc = a + 16ull * l + i - off;
+                    Hdr h = wave_header_of(j.layout, seg, len, qc, j.tables);
+                    if (h.status < 0 && len - qc - RPGPU_HEADER_SIZE >= h.need) { entry = qc; break; }
+                }
             }
+            cur = nxt;
         }
     }
     WalkOut o;

@@ -96,8 +96,9 @@ struct rpgpu_ctx {
     size_t pin_bytes = 0;
     bool timing = false;
     // one event set per timed submit: start, discover done, plan done,
-    // decode done, validate done, end; resolved lazily by rpgpu_last_timings
-    std::vector<std::array<hipEvent_t, 6>> ev_sets;
+    // decode done, validate done, walk done, end; resolved lazily by
+    // rpgpu_last_timings
+    std::vector<std::array<hipEvent_t, 7>> ev_sets;
     // rpgpu_uncompress staging (device)
     void* uws = nullptr;
     size_t uws_bytes = 0;
@@ -242,22 +243,23 @@ int rpgpu_set_timing(rpgpu_ctx* c, int enable) {
 
 // Averages over every timed submit since the previous call (then resets).
 // ms[0] whole pipeline, [1] discover, [2] resolve+emit+plan, [3] validate,
-// [4] decode.
+// [4] decode, [5] lane record walk.
 int rpgpu_last_timings(rpgpu_ctx* c, float* ms, int n) {
     if (!c || !ms) return RPGPU_E_INVALID;
     if (c->ev_used == 0) return fail(c, RPGPU_E_INVALID, "rpgpu_last_timings: no timed submit");
-    double acc[5] = {0, 0, 0, 0, 0};
+    double acc[6] = {0, 0, 0, 0, 0, 0};
     for (size_t i = 0; i < c->ev_used; i++) {
         auto& e = c->ev_sets[i];
-        HIPCHK(c, hipEventSynchronize(e[5]));
+        HIPCHK(c, hipEventSynchronize(e[6]));
         float t;
-        hipEventElapsedTime(&t, e[0], e[5]); acc[0] += t;
+        hipEventElapsedTime(&t, e[0], e[6]); acc[0] += t;
         hipEventElapsedTime(&t, e[0], e[1]); acc[1] += t;
         hipEventElapsedTime(&t, e[1], e[2]); acc[2] += t;
         hipEventElapsedTime(&t, e[3], e[4]); acc[3] += t;
         hipEventElapsedTime(&t, e[2], e[3]); acc[4] += t;
+        hipEventElapsedTime(&t, e[4], e[5]); acc[5] += t;
     }
-    for (int i = 0; i < n && i < 5; i++) ms[i] = (float)(acc[i] / (double)c->ev_used);
+    for (int i = 0; i < n && i < 6; i++) ms[i] = (float)(acc[i] / (double)c->ev_used);
     c->ev_used = 0;
     return RPGPU_OK;
 }
@@ -367,7 +369,7 @@ int rpgpu_submit(rpgpu_ctx* c, const rpgpu_job* job, void* stream) {
     hipEvent_t* ev = nullptr;
     if (tm) {
         if (c->ev_used == c->ev_sets.size()) {
-            std::array<hipEvent_t, 6> set;
+            std::array<hipEvent_t, 7> set;
             for (auto& e : set) HIPCHK(c, hipEventCreate(&e));
             c->ev_sets.push_back(set);
         }
@@ -395,8 +397,10 @@ int rpgpu_submit(rpgpu_ctx* c, const rpgpu_job* job, void* stream) {
     if (tm) HIPCHK(c, hipEventRecord(ev[3], s));
     STAGE("validate", launch_validate(j, s, c->cu_count));
     if (tm) HIPCHK(c, hipEventRecord(ev[4], s));
-    STAGE("finalize", launch_finalize(j, s));
+    STAGE("walk", launch_walk(j, s, c->cu_count * 8));
     if (tm) HIPCHK(c, hipEventRecord(ev[5], s));
+    STAGE("finalize", launch_finalize(j, s));
+    if (tm) HIPCHK(c, hipEventRecord(ev[6], s));
 #undef STAGE
     return RPGPU_OK;
 }

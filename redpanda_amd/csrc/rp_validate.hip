@@ -660,6 +660,14 @@ DEV void note_bad(const DeviceJob& j, uint32_t seg, uint64_t b) {
     }
 }
 
+// Stored payloads with at most kLaneWalkMax records are walked one lane per
+// batch by k_walk; k_validate walks the rest (and decoded payloads) with the
+// wave-parallel walk.
+constexpr int32_t kLaneWalkMax = 256;
+DEV bool lane_walked(uint32_t flags, uint32_t codec, int32_t rc) {
+    return (flags & RPGPU_F_COMPLETE) && codec == 0 && rc <= kLaneWalkMax;
+}
+
 // Per-batch descriptor, loaded one iteration ahead as ONE VGPR: lane i < 32
 // holds dword i of the batch result, lanes 32..37 the index-slot and
 // decode-arena words; the fields are read out with v_readlane when the batch
@@ -825,7 +833,7 @@ __global__ __launch_bounds__(1024) void k_validate(DeviceJob j) {
             // window's lines are arriving in L2 (its scalar loads hit or merge
             // with them; after the CRC they would be evicted again)
             const bool wire = j.layout == RPGPU_LAYOUT_WIRE;
-            const bool walk = d.codec == 0 && (j.flags & RPGPU_JOB_PARSE);
+            const bool walk = d.codec == 0 && (j.flags & RPGPU_JOB_PARSE) && !lane_walked(f, d.codec, d.rc);
             Group g0;
             group_init(g0);
             g0.first = walk && d.rc > 0;
@@ -949,6 +957,134 @@ __global__ __launch_bounds__(1024) void k_validate_decoded(DeviceJob j) {
             R->reserved1 = 0;
         }
     }
+}
+
+// ---------------------------------------------------------------------------
+// k_walk: the record walk of stored (uncompressed) payloads with at most
+// kLaneWalkMax records, one LANE per batch, after k_validate has written the
+// CRC verdicts.  record_batch::for_each_record (model/record.h:616-627) is
+// sequential by nature: record k + 1 starts where record k's parse ended
+// (parse_record: model/record_utils.cc:94-181, the same code as the wave
+// walk).  A lane loads the tail of record k (where its headers sit, guessed
+// from the length varint) together with the head of record k + 1 (at that
+// same guess), so a typical record costs one memory latency; 64 batches per
+// wave walk at once and the whole job is in flight together.  Batches with
+// more records are walked by the wave-parallel walk inside k_validate.
+// ---------------------------------------------------------------------------
+DEV void note_bad_lane(const DeviceJob& j, uint32_t seg, uint64_t b) {
+    const uint64_t first = j.chunk_count[j.chunk_base[seg]];
+    atomicMin(&j.seg_first_bad[seg], (uint32_t)(b - first));
+}
+
+DEV WalkResult walk_lane(const uint8_t* p0, uint32_t n, int32_t rc, uint32_t batch_ord, rpgpu_record_index* out,
+                         uint64_t out_cap) {
+    WalkResult wr;
+    wr.parsed = 0;
+    wr.err = 0;
+    wr.trailing = 0;
+    const uint32_t mis = (uint32_t)((uintptr_t)p0 & 15);
+    const uint32_t total = (uint32_t)(rc > 0 ? rc : 0);
+    if (total == 0) {
+        wr.trailing = n;
+        return wr;
+    }
+    uint32_t start = 0, done = 0;
+    Region H, T, N;
+    load_region(p0, mis, n, mis & ~15u, H);
+    for (;;) {
+        // the length varint at start (H holds the 12 bytes after it)
+        uint32_t guess = 0xFFFFFFFFu;
+        if (start < n) {
+            const uint32_t o = start + mis - H.base, k = o >> 2, sh = o & 3u;
+            const uint32_t w0 = pick12(H, k), w1 = pick12(H, k + 1u), w2 = pick12(H, k + 2u), w3 = pick12(H, k + 3u);
+            uint32_t br;
+            const int64_t len = varint12(__builtin_amdgcn_alignbyte(w1, w0, sh), __builtin_amdgcn_alignbyte(w2, w1, sh),
+                                         __builtin_amdgcn_alignbyte(w3, w2, sh), n - start, br);
+            if (len >= 0 && (uint64_t)len <= n) guess = start + br + (uint32_t)len;
+        }
+        // tail rows of this record and head rows of the next, together
+        const uint32_t hb = H.base;
+        const uint32_t e16 = (guess + mis + 15u) & ~15u;
+        const uint32_t tb = (guess != 0xFFFFFFFFu && e16 >= hb + 48u) ? e16 - 48u : hb;
+        load_region(p0, mis, n, tb, T);
+        const bool ahead = guess != 0xFFFFFFFFu && guess < n && done + 1u < total;
+        if (ahead) load_region(p0, mis, n, (guess + mis) & ~15u, N);
+        const Rec r = parse_record(p0, mis, n, start, H, T);
+        if (r.err) {
+            wr.parsed = done;
+            wr.err = r.err;
+            return wr;
+        }
+        if (done < out_cap) {
+            rpgpu_record_index e;
+            e.batch = batch_ord;
+            e.rec_pos = start;
+            e.ts_delta = r.ts;
+            e.length = r.length;
+            e.offset_delta = r.off;
+            e.key_len = r.klen;
+            e.key_pos = r.key_pos;
+            e.val_len = r.vlen;
+            e.val_pos = r.val_pos;
+            e.hdr_count = r.hcount;
+            e.hdr_pos = r.hdr_pos;
+            e.end_pos = r.end;
+            e.attrs = (int8_t)r.attr;
+            e.pad[0] = e.pad[1] = e.pad[2] = 0;
+            e.reserved[0] = e.reserved[1] = 0;
+            out[done] = e;
+        }
+        done++;
+        start = r.end;
+        if (done >= total) break;
+        if (ahead && start == guess) H = N;
+        else load_region(p0, mis, n, (start + mis) & ~15u, H);
+    }
+    wr.parsed = done;
+    wr.trailing = n - start;
+    return wr;
+}
+
+__global__ __launch_bounds__(256) void k_walk(DeviceJob j) {
+    const uint64_t nb_total = j.chunk_count[j.total_chunks];
+    const uint64_t nb = nb_total < j.batch_capacity ? nb_total : j.batch_capacity;
+    const bool wire = j.layout == RPGPU_LAYOUT_WIRE;
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t b = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; b < nb; b += stride) {
+        rpgpu_batch_result* R = &j.batches[b];
+        const uint32_t flags = R->flags;
+        const int32_t rc = R->record_count;
+        if (!lane_walked(flags, (uint32_t)R->attrs & 7u, rc)) continue;
+        if (wire && !(flags & RPGPU_F_CRC_OK)) continue;
+        const uint32_t seg = R->segment;
+        const uint64_t S = j.seg_off[seg] + R->file_pos + RPGPU_HEADER_SIZE;
+        const uint32_t n = (uint32_t)(R->size_bytes - (int32_t)RPGPU_HEADER_SIZE);
+        const uint64_t ib = j.slots[b], islots = j.slots[b + 1] - ib;
+        const bool idx_ok = ib + islots <= j.record_capacity;
+        const WalkResult w = walk_lane(j.data + S, n, rc, (uint32_t)b, idx_ok ? j.records + ib : nullptr,
+                                       idx_ok ? islots : 0);
+        uint32_t f = flags | RPGPU_F_PARSED, perr = w.err;
+        if (perr == 0) {
+            f |= RPGPU_F_PARSE_ASYNC_OK;
+            if (w.trailing == 0) f |= RPGPU_F_PARSE_OK;
+            else perr = RPGPU_PARSE_ERR_TRAILING;
+        }
+        if (f & RPGPU_F_PARSE_OK) {
+            if (idx_ok) f |= RPGPU_F_INDEX_WRITTEN;
+            else { perr = RPGPU_PARSE_ERR_INDEX_CAPACITY; atomicOr(&j.counters[1], 2u); }
+        }
+        // wire: a failed sync record parse is the first batch do_load_slice
+        // rejects (kafka/protocol/batch_reader.cc:129-151)
+        if (wire && !(f & RPGPU_F_PARSE_OK)) note_bad_lane(j, seg, b);
+        R->flags = f;
+        R->records_parsed = w.parsed;
+        R->parse_err = (uint8_t)perr;
+    }
+}
+
+hipError_t launch_walk(const DeviceJob& j, hipStream_t s, uint32_t grid) {
+    if (j.flags & RPGPU_JOB_PARSE) hipLaunchKernelGGL(k_walk, dim3(grid), dim3(256), 0, s, j);
+    return hipGetLastError();
 }
 
 hipError_t launch_validate(const DeviceJob& j, hipStream_t s, uint32_t grid) {

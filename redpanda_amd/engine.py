@@ -86,9 +86,10 @@ class Engine:
         check(self.L.rpgpu_set_timing(self.ctx, 1 if on else 0), self.ctx, "rpgpu_set_timing")
 
     def last_timings(self):
-        ms = (C.c_float * 5)()
-        check(self.L.rpgpu_last_timings(self.ctx, ms, 5), self.ctx, "rpgpu_last_timings")
-        return {"total": ms[0], "discover": ms[1], "resolve_plan": ms[2], "validate": ms[3], "decode": ms[4]}
+        ms = (C.c_float * 6)()
+        check(self.L.rpgpu_last_timings(self.ctx, ms, 6), self.ctx, "rpgpu_last_timings")
+        return {"total": ms[0], "discover": ms[1], "resolve_plan": ms[2], "validate": ms[3], "decode": ms[4],
+                "walk": ms[5]}
 
     def alloc_outputs(self, n_segments: int, batch_capacity: int, record_capacity: int,
                       decoded_capacity: int, bitmap: bool = True):

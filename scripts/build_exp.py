@@ -1,5 +1,5 @@
 """Build experiment variants of librpgpu.so: redpanda_amd/librpgpu_<name>.so
-with an alternate k_validate source and/or extra defines; the other objects
+with an alternate kernel source (--unit, default rp_validate.hip) and/or extra defines; the other objects
 come from the main build.  Usage:
   python scripts/build_exp.py NAME [--src path/to/rp_validate.hip] [-DFOO ...]
 Load with RPGPU_VARIANT=NAME.  Diagnostics only, never the product."""
@@ -12,7 +12,12 @@ from redpanda_amd import build as B  # noqa: E402
 
 name = sys.argv[1]
 args = sys.argv[2:]
-src = os.path.join(B.CSRC, "rp_validate.hip")
+unit = "rp_validate.hip"
+if "--unit" in args:  # which translation unit gets the source / defines
+    i = args.index("--unit")
+    unit = args[i + 1]
+    del args[i:i + 2]
+src = os.path.join(B.CSRC, unit)
 if "--src" in args:
     i = args.index("--src")
     src = os.path.abspath(args[i + 1])
@@ -21,10 +26,10 @@ defs = [a for a in args if a.startswith("-D")]
 B.build()
 bdir = os.path.join(B.HERE, "_build_exp_" + name)
 os.makedirs(bdir, exist_ok=True)
-obj = os.path.join(bdir, "rp_validate.hip.o")
+obj = os.path.join(bdir, unit + ".o")
 B._run([B._hipcc(), f"--offload-arch={B.ARCH}", "-O3", "-fPIC", "-std=c++17", "-I", B.INC, "-I", B.CSRC,
         "-Wno-unused-function", "-Wno-unused-variable"] + defs + ["-c", src, "-o", obj])
-objs = [os.path.join(B.BUILD, s + ".o") for s in B.HIP_SOURCES + B.CXX_SOURCES if s != "rp_validate.hip"] + [obj]
+objs = [os.path.join(B.BUILD, s + ".o") for s in B.HIP_SOURCES + B.CXX_SOURCES if s != unit] + [obj]
 out = os.path.join(B.HERE, f"librpgpu_{name}.so")
 B._run([B._hipcc(), f"--offload-arch={B.ARCH}", "-shared", "-fPIC", "-o", out] + objs + ["-ldl", "-lpthread"])
 print(out)

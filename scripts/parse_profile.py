@@ -41,7 +41,7 @@ def pmc(sub, name):
 fetch = pmc(f"pmc_fetch_{tag}", "FETCH_SIZE")
 write = pmc(f"pmc_write_{tag}", "WRITE_SIZE")
 fetch_np = pmc(f"pmc_fetchnp_{tag}", "FETCH_SIZE")  # CRC-only run (calibration), when collected
-res = {"tag": tag, "kernel": "k_validate", "fetch_size_kib": fetch, "write_size_kib": write,
+res = {"tag": tag, "kernel": "k_validate", "alg_def": "payload+128B/batch", "fetch_size_kib": fetch, "write_size_kib": write,
        "fetch_size_kib_crc_only": fetch_np,
        "correction": "FETCH_SIZE x2 (gfx950 counts half of a wide coalesced read; calibrated on the CRC-only run, "
                      "whose traffic is the dwordx4 window stream alone), WRITE_SIZE x1; KiB -> bytes"}
