@@ -27,13 +27,16 @@ if stats:
     shutil.copy(stats, os.path.join(prof, f"{tag}_kernel_stats.csv"))
 
 
-def pmc(sub, name):
+def pmc(sub, name, kernel="k_validate"):
     f = one(f"{sub}/**/*counter_collection.csv")
     vals = []
     if not f:
         return None
     for row in csv.DictReader(open(f)):
-        if "k_validate" in row.get("Kernel_Name", "") and row.get("Counter_Name") == name:
+        kn = row.get("Kernel_Name", "")
+        if (kernel + "(") in kn.replace(" ", "") or kn.split("(")[0].strip().endswith(kernel):
+            if row.get("Counter_Name") != name:
+                continue
             vals.append(float(row["Counter_Value"]))
     return sum(vals) / len(vals) if vals else None
 
@@ -47,6 +50,12 @@ res = {"tag": tag, "kernel": "k_validate", "alg_def": "payload+128B/batch", "fet
                      "whose traffic is the dwordx4 window stream alone), WRITE_SIZE x1; KiB -> bytes"}
 if fetch is not None and write is not None:
     res["bytes_per_launch"] = int(fetch * 1024 * 2 + write * 1024)
+# the record walk (k_walk: per-lane 16-byte loads, so the x2 wide-stream
+# correction is not calibrated for it: raw counter bytes are reported)
+wf, ww = pmc(f"pmc_fetch_{tag}", "FETCH_SIZE", "k_walk"), pmc(f"pmc_write_{tag}", "WRITE_SIZE", "k_walk")
+if wf is not None:
+    res["walk"] = {"kernel": "k_walk", "fetch_size_kib": wf, "write_size_kib": ww,
+                   "note": "raw FETCH_SIZE/WRITE_SIZE (uncalibrated for per-lane scattered 16-B loads)"}
 for name in (f"{tag}_validate_traffic.json", "validate_traffic.json"):
     json.dump(res, open(os.path.join(prof, name), "w"), indent=1)
 print(json.dumps(res))
