@@ -156,6 +156,129 @@ DEV Hdr wave_header_of(uint32_t layout, const uint8_t* __restrict__ seg, uint64_
     return layout == RPGPU_LAYOUT_WIRE ? wave_header_wire(seg, len, p, T) : wave_header(seg, len, p, T);
 }
 
+// ---------------------------------------------------------------------------
+// Lane-private header read: the same verdicts as wave_header_of, one header
+// per LANE, so 64 chains advance per wave instruction.  The 61 bytes arrive
+// in four 16-byte loads (the last at +45, so nothing past byte 60 is read);
+// header_crc is the xor of 57 independent lookups T_{60-k}[byte k] in the LDS
+// image of Tables::hdr (`th`, 57 x 256 words), so its latency is one LDS
+// round, not 57.
+// ---------------------------------------------------------------------------
+struct LHdr {
+    int32_t status;  // -1 ok, else parser errc
+    int32_t eof;
+    uint32_t hcrc, computed;
+    int32_t size;
+    uint64_t need;   // (uint32_t)(size - 61)
+    uint32_t w[16];  // header bytes 0..63 (61..63 zero)
+};
+
+DEV uint4 ld16u(const uint8_t* p) {
+    uint4 v;
+    __builtin_memcpy(&v, p, 16);  // one global_load_dwordx4 (unaligned access is native)
+    return v;
+}
+
+// header bytes [0, 61) of seg + p into w[0..15]
+DEV void lane_header_bytes(const uint8_t* __restrict__ h, uint32_t (&w)[16]) {
+    const uint4 a = ld16u(h), b = ld16u(h + 16), c = ld16u(h + 32), d = ld16u(h + 45);
+    w[0] = a.x; w[1] = a.y; w[2] = a.z; w[3] = a.w;
+    w[4] = b.x; w[5] = b.y; w[6] = b.z; w[7] = b.w;
+    w[8] = c.x; w[9] = c.y; w[10] = c.z; w[11] = c.w;
+    // d holds bytes 45..60: byte 48 + i = d byte 3 + i
+    w[12] = __builtin_amdgcn_alignbyte(d.y, d.x, 3);
+    w[13] = __builtin_amdgcn_alignbyte(d.z, d.y, 3);
+    w[14] = __builtin_amdgcn_alignbyte(d.w, d.z, 3);
+    w[15] = d.w >> 24;
+}
+
+DEV uint32_t lb(const uint32_t (&w)[16], int k) { return (w[k >> 2] >> (8 * (k & 3))) & 0xFFu; }
+DEV uint32_t l32(const uint32_t (&w)[16], int k) {
+    return (k & 3) ? __builtin_amdgcn_alignbyte(w[(k >> 2) + 1], w[k >> 2], k & 3) : w[k >> 2];
+}
+DEV uint64_t l64(const uint32_t (&w)[16], int k) { return (uint64_t)l32(w, k) | ((uint64_t)l32(w, k + 4) << 32); }
+DEV uint32_t l16(const uint32_t (&w)[16], int k) { return l32(w, k) & 0xFFFFu; }
+DEV uint32_t lbe32(const uint32_t (&w)[16], int k) { return __builtin_bswap32(l32(w, k)); }
+DEV uint64_t lbe64(const uint32_t (&w)[16], int k) { return ((uint64_t)lbe32(w, k) << 32) | lbe32(w, k + 4); }
+DEV uint32_t lbe16(const uint32_t (&w)[16], int k) { return (lb(w, k) << 8) | lb(w, k + 1); }
+
+// wire byte the adapted (disk) header byte l comes from (wave_header_wire)
+constexpr int wire_src(int l) {
+    return (l >= 8 && l < 16) ? 15 - l
+         : (l >= 17 && l < 21) ? 37 - l
+         : (l >= 21 && l < 61) ? 21 + ((l < 23 ? 0 : l < 27 ? 2 : l < 35 ? 6 : l < 43 ? 14 : l < 51 ? 22 : l < 53 ? 30
+                                        : l < 57 ? 32 : 36) +
+                                       ((l < 23 ? 2 : l < 27 ? 4 : l < 35 ? 8 : l < 43 ? 8 : l < 51 ? 8 : l < 53 ? 2
+                                        : 4) - 1 - (l - (l < 23 ? 21 : l < 27 ? 23 : l < 35 ? 27 : l < 43 ? 35
+                                                         : l < 51 ? 43 : l < 53 ? 51 : l < 57 ? 53 : 57))))
+         : 0;
+}
+
+DEV LHdr lane_header(uint32_t layout, const uint8_t* __restrict__ seg, uint64_t len, uint64_t p,
+                     const uint32_t* __restrict__ th, uint32_t c57) {
+    LHdr h;
+    h.eof = 0;
+    h.hcrc = h.computed = 0;
+    h.size = 0;
+    h.need = 0;
+#pragma unroll
+    for (int i = 0; i < 16; i++) h.w[i] = 0;
+    const uint64_t rem = len - p;
+    if (rem == 0) { h.status = RPGPU_ERRC_END_OF_STREAM; h.eof = 1; return h; }
+    if (rem < RPGPU_HEADER_SIZE) { h.status = RPGPU_ERRC_INPUT_STREAM_NOT_ENOUGH_BYTES; h.eof = 1; return h; }
+    lane_header_bytes(seg + p, h.w);
+    uint32_t raw = 0;
+    if (layout == RPGPU_LAYOUT_WIRE) {
+        const uint32_t bl = lbe32(h.w, 8);
+        if ((int64_t)(int32_t)bl + 12 < (int64_t)RPGPU_HEADER_SIZE) {
+            h.status = RPGPU_ERRC_INPUT_STREAM_NOT_ENOUGH_BYTES;
+            return h;
+        }
+        h.size = (int32_t)(bl + 12u);
+        h.need = (uint32_t)((uint32_t)h.size - RPGPU_HEADER_SIZE);
+#pragma unroll
+        for (int k = 4; k < 61; k++) {
+            const uint32_t d = (k < 8) ? (((uint32_t)h.size >> (8 * (k - 4))) & 0xFFu) : (k == 16) ? 1u : lb(h.w, wire_src(k));
+            raw ^= th[(60 - k) * 256 + d];
+        }
+        h.computed = ~(c57 ^ raw);
+        h.status = -1;
+        return h;
+    }
+#pragma unroll
+    for (int k = 4; k < 61; k++) raw ^= th[(60 - k) * 256 + lb(h.w, k)];
+    h.computed = ~(c57 ^ raw);
+    h.hcrc = h.w[0];
+    h.size = (int32_t)h.w[1];
+    h.need = (uint32_t)((uint32_t)h.size - RPGPU_HEADER_SIZE);
+    if (h.hcrc == 0) { h.status = RPGPU_ERRC_FALLOCATED_FILE_READ_ZERO_BYTES_FOR_HEADER; return h; }
+    if (h.hcrc != h.computed) { h.status = RPGPU_ERRC_HEADER_ONLY_CRC_MISSMATCH; return h; }
+    h.status = -1;
+    return h;
+}
+
+// raw CRC contribution of the BE40 prefix of the batch crc (model/record_utils.cc:
+// 68-80): disk byte k (21..60) lands at BE position be(k); on the wire the
+// prefix is bytes [21, 61) as they stand
+DEV uint32_t lane_prefix_raw(uint32_t layout, const uint32_t (&w)[16], const uint32_t* __restrict__ th) {
+    uint32_t x = 0;
+    if (layout == RPGPU_LAYOUT_WIRE) {
+#pragma unroll
+        for (int k = 21; k < 61; k++) x ^= th[(39 - (k - 21)) * 256 + lb(w, k)];
+    } else {
+#pragma unroll
+        for (int k = 21; k < 61; k++) x ^= th[(39 - (wire_src(k) - 21)) * 256 + lb(w, k)];
+    }
+    return x;
+}
+
+// the LDS image of Tables::hdr for lane_header (57 KiB)
+constexpr uint32_t kLdsHdrBytes = 57u * 256u * 4u;
+DEV void init_lds_hdr(uint32_t* th, const Tables* T) {
+    for (uint32_t i = threadIdx.x; i < 57u * 256u; i += blockDim.x) th[i] = (&T->hdr[0][0])[i];
+    __syncthreads();
+}
+
 #define HD __host__ __device__ inline
 
 HD uint32_t rd32h(const uint8_t* p) { return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24); }

@@ -195,21 +195,64 @@ __global__ __launch_bounds__(256) void k_discover(DeviceJob j) {
             cur = nxt;
         }
     }
-    WalkOut o;
-    if (entry == kNone) {
-        o.exit = kNone; o.count = 0; o.term = -1; o.tpos = 0;
-    } else {
-        o = wave_walk(j.layout, seg, len, entry, ce, j.tables);
-    }
     if (lane() == 0) {
         ChunkRec r;
         r.entry = entry;
-        r.exit = o.exit;
-        r.count = o.count;
-        r.term = o.term;
-        r.tpos = o.tpos;
+        r.exit = kNone;
+        r.count = 0;
+        r.term = -1;
+        r.tpos = 0;
         j.chunks[g] = r;
     }
+}
+
+// Follow the chain from p while headers start before ce, one chain per lane
+// (wave_walk's semantics with lane_header).
+DEV WalkOut lane_walk(uint32_t layout, const uint8_t* __restrict__ seg, uint64_t len, uint64_t p, uint64_t ce,
+                      const uint32_t* __restrict__ th, uint32_t c57) {
+    WalkOut w;
+    w.count = 0;
+    w.term = -1;
+    w.tpos = 0;
+    while (p < ce) {
+        const LHdr h = lane_header(layout, seg, len, p, th, c57);
+        if (h.status >= 0) { w.term = h.status | (h.eof << 8); w.tpos = p; break; }
+        if (len - p - RPGPU_HEADER_SIZE < h.need) {
+            w.count++;
+            w.term = RPGPU_ERRC_INPUT_STREAM_NOT_ENOUGH_BYTES | (1 << 8);
+            w.tpos = p;
+            break;
+        }
+        w.count++;
+        p += RPGPU_HEADER_SIZE + h.need;
+    }
+    w.exit = p;
+    return w;
+}
+
+// Speculative chain of every chunk from the entry k_discover found, one chunk
+// per LANE: a chunk's headers are a dependent chain, so 64 chains per wave
+// keep 64 header reads in flight where a wave-cooperative walk had one.
+__global__ __launch_bounds__(256) void k_chain(DeviceJob j) {
+    extern __shared__ uint32_t th[];
+    init_lds_hdr(th, j.tables);
+    const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= j.total_chunks) return;
+    const uint64_t entry = j.chunks[g].entry;
+    if (entry == kNone) return;
+    const uint32_t s = find_segment(j.chunk_base, j.n_segments, g);
+    const uint64_t w = g - j.chunk_base[s];
+    const uint64_t off = j.seg_off[s], len = j.seg_off[s + 1] - off;
+    const uint64_t cs = w * j.chunk_bytes;
+    const uint64_t ce = (cs + j.chunk_bytes < len) ? cs + j.chunk_bytes : len;
+    const WalkOut o = lane_walk(j.layout, j.data + off, len, entry, ce, th, j.tables->c57);
+    ChunkRec r;
+    r.entry = entry;
+    r.exit = o.exit;
+    r.count = o.count;
+    r.term = o.term;
+    r.tpos = o.tpos;
+    j.chunks[g] = r;
 }
 
 // ---------------------------------------------------------------------------
@@ -352,7 +395,9 @@ __global__ __launch_bounds__(256) void k_resolve(DeviceJob j) {
 // header (storage/parser.cc:36-76) and plan index slots / decode bytes.
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void k_emit(DeviceJob j) {
-    const uint64_t g = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    extern __shared__ uint32_t th[];
+    init_lds_hdr(th, j.tables);
+    const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (g >= j.total_chunks) return;
     const uint64_t base_ord = j.chunk_count[g];
     const uint64_t cnt = j.chunk_count[g + 1] - base_ord;
@@ -360,30 +405,25 @@ __global__ __launch_bounds__(256) void k_emit(DeviceJob j) {
     const uint32_t s = find_segment(j.chunk_base, j.n_segments, g);
     const uint64_t off = j.seg_off[s], len = j.seg_off[s + 1] - off;
     const uint8_t* seg = j.data + off;
-    const Tables* T = j.tables;
-    const uint32_t l = lane();
+    const uint32_t c57 = j.tables->c57;
+    const bool wire = j.layout == RPGPU_LAYOUT_WIRE;
     uint64_t p = j.chunk_entry[g];
     for (uint64_t i = 0; i < cnt; i++) {
 #ifdef RPGPU_CHECKED
-        {
-            bool bad = false;
-            RP_CHECK(bad, p < len, "emit g=%llu i=%llu cnt=%llu p=%llu len=%llu entry=%llu", (unsigned long long)g,
-                     (unsigned long long)i, (unsigned long long)cnt, (unsigned long long)p, (unsigned long long)len,
-                     (unsigned long long)j.chunk_entry[g]);
-            if (bad) break;
+        if (!(p < len)) {
+            printf("RPGPU_CHECK emit g=%llu i=%llu cnt=%llu p=%llu len=%llu\n", (unsigned long long)g,
+                   (unsigned long long)i, (unsigned long long)cnt, (unsigned long long)p, (unsigned long long)len);
+            break;
         }
 #endif
-        Hdr h = wave_header_of(j.layout, seg, len, p, T);  // known valid (resolved chain)
-        const bool wire = j.layout == RPGPU_LAYOUT_WIRE;
+        const LHdr h = lane_header(j.layout, seg, len, p, th, c57);  // known valid (resolved chain)
         const uint64_t ord = base_ord + i;
         const bool complete = (len - p - RPGPU_HEADER_SIZE) >= h.need;
-        // prefix state of the batch crc: CRC over the BE40 prefix, init ~0
-        // (on the wire the prefix is bytes [21, 61) as they stand)
-        const uint32_t pe = wire ? (uint32_t)(l - 21) : (uint32_t)be_index(l);
-        uint32_t pc = (l >= 21 && l < RPGPU_HEADER_SIZE) ? T->hdr[39 - pe][h.b] : 0u;
-        uint32_t praw = wave_xor(pc);
-        const uint32_t attrs = wire ? hbe16(h.b, 21) : h16(h.b, 21);
-        const int32_t rc = (int32_t)(wire ? hbe32(h.b, 57) : h32(h.b, 57));
+        // prefix state of the batch crc: raw CRC contribution of the BE40
+        // prefix (init ~0 is added by k_validate)
+        const uint32_t praw = lane_prefix_raw(j.layout, h.w, th);
+        const uint32_t attrs = wire ? lbe16(h.w, 21) : l16(h.w, 21);
+        const int32_t rc = (int32_t)(wire ? lbe32(h.w, 57) : l32(h.w, 57));
         const uint32_t codec = attrs & 7;
         uint64_t slots = 0, cap = 0;
         const bool decodable = (codec == RPGPU_CODEC_LZ4 || codec == RPGPU_CODEC_SNAPPY) && (j.flags & RPGPU_JOB_DECODE);
@@ -391,38 +431,39 @@ __global__ __launch_bounds__(256) void k_emit(DeviceJob j) {
             if (codec == 0) {
                 if ((j.flags & RPGPU_JOB_PARSE) && rc > 0 && (uint64_t)rc <= h.need) slots = (uint64_t)rc;
             } else if (decodable) {
-                cap = uni64(decode_capacity_dev((int)codec, seg + p + RPGPU_HEADER_SIZE, h.need));
+                cap = decode_capacity_dev((int)codec, seg + p + RPGPU_HEADER_SIZE, h.need);
                 if ((j.flags & RPGPU_JOB_PARSE) && rc > 0 && (uint64_t)rc <= cap) slots = (uint64_t)rc;
             }
         }
-        if (l == 0 && ord < j.batch_capacity) {
+        if (ord < j.batch_capacity) {
             rpgpu_batch_result r;
             r.file_pos = p;
             uint32_t f = RPGPU_F_HEADER_OK;
             if (wire) {
                 // kafka_batch_adapter::read_header (kafka_batch_adapter.cc:32-91)
-                r.base_offset = (int64_t)hbe64(h.b, 0);
-                r.first_timestamp = (int64_t)hbe64(h.b, 27);
-                r.max_timestamp = (int64_t)hbe64(h.b, 35);
-                r.producer_id = (int64_t)hbe64(h.b, 43);
-                r.last_offset_delta = (int32_t)hbe32(h.b, 23);
-                r.base_sequence = (int32_t)hbe32(h.b, 53);
+                r.base_offset = (int64_t)lbe64(h.w, 0);
+                r.first_timestamp = (int64_t)lbe64(h.w, 27);
+                r.max_timestamp = (int64_t)lbe64(h.w, 35);
+                r.producer_id = (int64_t)lbe64(h.w, 43);
+                r.last_offset_delta = (int32_t)lbe32(h.w, 23);
+                r.base_sequence = (int32_t)lbe32(h.w, 53);
                 r.header_crc = 0;
-                r.crc = hbe32(h.b, 17);
-                r.producer_epoch = (int16_t)hbe16(h.b, 51);
+                r.crc = lbe32(h.w, 17);
+                r.producer_epoch = (int16_t)lbe16(h.w, 51);
                 r.type = 1;  // record_batch_type::raft_data
-                if (hb(h.b, 16) == 2) f |= RPGPU_F_WIRE_V2;
+                if (lb(h.w, 16) == 2) f |= RPGPU_F_WIRE_V2;
             } else {
-                r.base_offset = (int64_t)h64(h.b, 8);
-                r.first_timestamp = (int64_t)h64(h.b, 27);
-                r.max_timestamp = (int64_t)h64(h.b, 35);
-                r.producer_id = (int64_t)h64(h.b, 43);
-                r.last_offset_delta = (int32_t)h32(h.b, 23);
-                r.base_sequence = (int32_t)h32(h.b, 53);
+                // storage::header_from_iobuf (storage/parser.cc:36-76)
+                r.base_offset = (int64_t)l64(h.w, 8);
+                r.first_timestamp = (int64_t)l64(h.w, 27);
+                r.max_timestamp = (int64_t)l64(h.w, 35);
+                r.producer_id = (int64_t)l64(h.w, 43);
+                r.last_offset_delta = (int32_t)l32(h.w, 23);
+                r.base_sequence = (int32_t)l32(h.w, 53);
                 r.header_crc = h.hcrc;
-                r.crc = h32(h.b, 17);
-                r.producer_epoch = (int16_t)h16(h.b, 51);
-                r.type = (int8_t)hb(h.b, 16);
+                r.crc = l32(h.w, 17);
+                r.producer_epoch = (int16_t)l16(h.w, 51);
+                r.type = (int8_t)lb(h.w, 16);
             }
             r.size_bytes = h.size;
             r.record_count = rc;
@@ -692,6 +733,9 @@ hipError_t launch_chunk_base(const DeviceJob& j, hipStream_t s) {
 hipError_t launch_discover(const DeviceJob& j, hipStream_t s) {
     const uint32_t grid = (j.total_chunks + 3) / 4;
     hipLaunchKernelGGL(k_discover, dim3(grid), dim3(256), 0, s, j);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_chain, dim3((j.total_chunks + 255) / 256), dim3(256), kLdsHdrBytes, s, j);
     return hipGetLastError();
 }
 hipError_t launch_resolve(const DeviceJob& j, hipStream_t s) {
@@ -699,8 +743,7 @@ hipError_t launch_resolve(const DeviceJob& j, hipStream_t s) {
     return hipGetLastError();
 }
 hipError_t launch_emit(const DeviceJob& j, hipStream_t s) {
-    const uint32_t grid = (j.total_chunks + 3) / 4;
-    hipLaunchKernelGGL(k_emit, dim3(grid), dim3(256), 0, s, j);
+    hipLaunchKernelGGL(k_emit, dim3((j.total_chunks + 255) / 256), dim3(256), kLdsHdrBytes, s, j);
     return hipGetLastError();
 }
 hipError_t launch_finalize(const DeviceJob& j, hipStream_t s) {
