@@ -386,7 +386,8 @@ struct Reader {
 
 // iobuf_copy (bytes/iobuf.cc:133-157): -1 when (int)len < 0 (bad_alloc);
 // a length past the end copies what is there, silently
-DEV int copy_bytes(Reader& c, int64_t len) {
+template <class Src>
+DEV int copy_bytes(Src& c, int64_t len) {
     const int32_t bl = (int32_t)(uint32_t)(uint64_t)len;
     if (bl < 0) return -1;
     const uint32_t left = c.n - c.pos;
@@ -405,20 +406,16 @@ struct Rec {
 
 // parse_one_record_copy_from_buffer (model/record_utils.cc:170-177) over
 // parse_record_meta_from_buffer / do_parse_one_record_from_buffer /
-// parse_record_headers (:94-160) from the record start, with the head and
-// tail regions already loaded (record_regions).
-DEV Rec parse_record(const uint8_t* p0, uint32_t mis, uint32_t n, uint32_t start, const Region& H, const Region& T) {
+// parse_record_headers (:94-160) from the source's position.  Src provides
+// pos, n, varlong() and byte() (Reader: register regions).
+// lane's LDS slab).
+template <class Src>
+DEV Rec parse_fields(Src& c) {
     Rec r;
-    Reader c;
-    c.p0 = p0;
-    c.mis = mis;
-    c.n = n;
-    c.pos = start;
-    c.A = H;
-    c.T = T;
     r.err = 0;
     r.key_pos = r.val_pos = r.hdr_pos = 0;
     r.ts = 0; r.length = r.off = r.klen = r.vlen = r.hcount = 0; r.attr = 0;
+    const uint32_t n = c.n;
     const int64_t rsz = c.varlong();
     // consume_type<int8_t>: the only read that throws on short input
     if (c.pos >= n) { r.err = RPGPU_PARSE_ERR_ATTR_EOF; r.end = c.pos; return r; }
@@ -450,6 +447,19 @@ DEV Rec parse_record(const uint8_t* p0, uint32_t mis, uint32_t n, uint32_t start
     r.hcount = (int32_t)hc;
     r.end = c.pos;
     return r;
+}
+
+// from the record start, with the head and tail regions already loaded
+// (record_regions)
+DEV Rec parse_record(const uint8_t* p0, uint32_t mis, uint32_t n, uint32_t start, const Region& H, const Region& T) {
+    Reader c;
+    c.p0 = p0;
+    c.mis = mis;
+    c.n = n;
+    c.pos = start;
+    c.A = H;
+    c.T = T;
+    return parse_fields(c);
 }
 
 // Head and tail regions of a lane's record, issued together: three 16-byte
