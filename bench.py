@@ -108,6 +108,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--gather", choices=["bitmap", "index"], default="bitmap")
     ap.add_argument("--no-parse", action="store_true", help="CRC only (diagnostic; not the headline workload)")
+    ap.add_argument("--batch-bytes", type=int, default=BATCH_BYTES,
+                    help="size_bytes per batch (diagnostic; the headline workload is 16 KiB)")
     args = ap.parse_args()
 
     import torch
@@ -127,7 +129,7 @@ def main():
     seg_bytes = int(args.seg_gib * (1 << 30)) // BATCH_BYTES * BATCH_BYTES
     parts = partitions_for_rank(args.partitions * world, world, rank)
     t0 = time.time()
-    data, offs, counts, host_first = gen_partitions(parts, seg_bytes, BATCH_BYTES, torch, device)
+    data, offs, counts, host_first = gen_partitions(parts, seg_bytes, args.batch_bytes, torch, device)
     n_batches = int(sum(counts))
     log(f"[rank {rank}] generated {len(parts)} x {seg_bytes >> 20} MiB, {n_batches} batches in {time.time() - t0:.1f}s")
 
@@ -239,7 +241,7 @@ def main():
                 "partitions_per_gpu": len(parts),
                 "batches_per_gpu": n_batches,
                 "records_per_gpu": n_records,
-                "batch_bytes": BATCH_BYTES,
+                "batch_bytes": args.batch_bytes,
                 "batches_per_s": round(job_batches * args.steps / elapsed, 1),
                 "parallelism": f"partition-sharded x{world}, RCCL gather of bitmaps+summaries",
                 "parity": {"all_batches_valid": all_ok, "bitmap_all_ones": bm_ok},

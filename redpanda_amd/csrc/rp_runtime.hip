@@ -397,7 +397,9 @@ int rpgpu_submit(rpgpu_ctx* c, const rpgpu_job* job, void* stream) {
     if (tm) HIPCHK(c, hipEventRecord(ev[3], s));
     STAGE("validate", launch_validate(j, s, c->cu_count));
     if (tm) HIPCHK(c, hipEventRecord(ev[4], s));
-    STAGE("walk", launch_walk(j, s, c->cu_count * 8));
+    // RPGPU_WALK_WGS: diagnostic override of k_walk's grid (workgroups per CU)
+    static const uint32_t walk_wgs = [] { const char* e = getenv("RPGPU_WALK_WGS"); return e ? (uint32_t)atoi(e) : 8u; }();
+    STAGE("walk", launch_walk(j, s, c->cu_count * walk_wgs));
     if (tm) HIPCHK(c, hipEventRecord(ev[5], s));
     STAGE("finalize", launch_finalize(j, s));
     if (tm) HIPCHK(c, hipEventRecord(ev[6], s));

@@ -790,6 +790,283 @@ DEV uint32_t walk_flags(const DeviceJob& j, const WalkResult& w, bool idx_ok, ui
 // only the descriptor is prefetched.
 constexpr int kPreRows = 0;
 
+// ---------------------------------------------------------------------------
+// k_walk: the record walk of stored (uncompressed) payloads with at most
+// kLaneWalkMax records, one LANE per batch, after k_validate has written the
+// CRC verdicts.  record_batch::for_each_record (model/record.h:616-627) is
+// sequential by nature: record k + 1 starts where record k's parse ended
+// (parse_record: model/record_utils.cc:94-181, the same code as the wave
+// walk).  A lane loads the tail of record k (where its headers sit, guessed
+// from the length varint) together with the head of record k + 1 (at that
+// same guess), so a typical record costs one memory latency; 64 batches per
+// wave walk at once and the whole job is in flight together.  Batches with
+// more records are walked by the wave-parallel walk inside k_validate.
+// ---------------------------------------------------------------------------
+template <class J>
+DEV void note_bad_lane(const J& j, uint32_t seg, uint64_t b) {
+    const uint64_t first = j.chunk_count[j.chunk_base[seg]];
+    atomicMin(&j.seg_first_bad[seg], (uint32_t)(b - first));
+}
+
+// One lane's walk of one stored payload.  The bytes a lane parses sit in
+// LDS slots rather than registers: a region (6 rows of 16 bytes at a 16-byte
+// aligned grid offset) is copied global -> LDS by six global_load_lds, and
+// the parser reads any dword of it with one ds_read at a per-lane address.
+// (Held in registers, every field read was a 12-way select: ~1,200 VALU per
+// record.)  Record k's step loads ONE region, C_k = the 96 bytes around its
+// guessed end: the 48 bytes before it hold record k's headers, the 48 after
+// it record k + 1's length .. key length, key and value length (16-byte
+// keys), so the next step parses its head from C_k with no second load.  Each
+// walk wave owns two slots that alternate by the parity of its step counter
+// (uniform, as global_load_lds writes a wave-uniform LDS base + 16 * lane):
+// H (C_{k-1}, read) and C_k (loaded).
+constexpr uint32_t kRegionRows = 6u;
+constexpr uint32_t kRegionBytes = 16u * kRegionRows;
+constexpr uint32_t kRegionReach = kRegionBytes - 16u;  // a read needs 16 bytes from its offset
+constexpr uint32_t kSlotBytes = kRegionRows * 1024u;
+constexpr uint32_t kWalkLdsWave = 2u * kSlotBytes;
+
+typedef __attribute__((address_space(3))) void lds_void;
+typedef const __attribute__((address_space(1))) void gbl_void;
+
+DEV void wait_vm() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
+// the region at grid offset base (rows at or past the payload end are not
+// loaded: their bytes are never parsed) into the slot whose row 0 is at the
+// wave-uniform LDS address `slot`
+DEV void glds_region(const uint8_t* p0, uint32_t mis, uint32_t n, uint32_t base, uint8_t* slot) {
+    const uint8_t* row = p0 - mis + base;
+    const uint32_t lim = n + mis;
+#pragma unroll
+    for (uint32_t r = 0; r < kRegionRows; r++)
+        if (base + 16u * r < lim)
+            __builtin_amdgcn_global_load_lds((gbl_void*)(row + 16u * r), (lds_void*)(slot + 1024u * r), 16, 0, 0);
+}
+
+// dword at 4-aligned region offset o (< kRegionBytes) of a lane's slot
+DEV uint32_t slot_dw(const uint8_t* lane_slot, uint32_t o) {
+    return *(const uint32_t*)(lane_slot + (o >> 4) * 1024u + (o & 12u));
+}
+
+// The record parser's byte source over LDS slots: the current region A, the
+// tail region T (C_k, the other slot), else a fresh region at the read
+// position (one dependent load, into the H slot: the read position has left
+// H, and C_k must survive as the next step's H).
+struct LdsReader {
+    const uint8_t* p0;  // payload start
+    uint32_t mis;       // p0 & 15
+    uint32_t n;
+    uint32_t pos;
+    const uint8_t* lane;  // wave LDS base + 16 * lane
+    uint8_t* wave;        // wave LDS base
+    uint32_t a_base, a_slot, t_base, t_slot, h_slot;
+
+    DEV uint32_t locate() {
+        const uint32_t g = pos + mis;
+        if (g - a_base > kRegionReach) {
+            if (g - t_base <= kRegionReach) {
+                a_base = t_base;
+                a_slot = t_slot;
+            } else {
+                a_base = g & ~15u;
+                a_slot = h_slot;
+                glds_region(p0, mis, n, a_base, wave + h_slot * kSlotBytes);
+                wait_vm();
+            }
+        }
+        return g - a_base;
+    }
+    // iobuf_parser_base::read_varlong (bytes/iobuf_parser.h:48-52)
+    DEV int64_t varlong() {
+        const uint32_t o = locate(), k = o & ~3u, sh = o & 3u, avail = n - pos;
+        const uint8_t* ls = lane + a_slot * kSlotBytes;
+        const uint32_t w0 = slot_dw(ls, k), w1 = slot_dw(ls, k + 4u);
+        uint32_t r0 = __builtin_amdgcn_alignbyte(w1, w0, sh), r1 = 0u, r2 = 0u, br;
+        if (avail >= 2 && (r0 & 0x8080u) == 0x8080u) {
+            const uint32_t w2 = slot_dw(ls, k + 8u), w3 = slot_dw(ls, k + 12u);
+            r1 = __builtin_amdgcn_alignbyte(w2, w1, sh);
+            r2 = __builtin_amdgcn_alignbyte(w3, w2, sh);
+        }
+        const int64_t x = varint12(r0, r1, r2, avail, br);
+        pos += br;
+        return x;
+    }
+    DEV uint32_t byte() {
+        const uint32_t o = locate();
+        return (slot_dw(lane + a_slot * kSlotBytes, o & ~3u) >> (8u * (o & 3u))) & 0xFFu;
+    }
+};
+
+struct LaneWalk {
+    const uint8_t* p0;
+    rpgpu_record_index* out;  // the batch's index slots (null when they overflow)
+    uint32_t mis, n, total, done, start, cap, ord;
+    uint32_t h_base;  // grid offset of the region holding `start` (in the step's H slot)
+};
+
+// H slot of step `step` (the other one receives C_k)
+DEV uint32_t h_slot_of(uint32_t step) { return step & 1u; }
+
+// set up a lane walk; the first region goes into the H slot of the step that
+// walks the first record
+DEV void lane_walk_begin(LaneWalk& w, const uint8_t* p0, uint32_t n, int32_t rc, uint32_t batch_ord,
+                         rpgpu_record_index* out, uint32_t cap, uint8_t* wave, uint32_t hs) {
+    w.p0 = p0;
+    w.out = out;
+    w.mis = (uint32_t)((uintptr_t)p0 & 15);
+    w.n = n;
+    w.total = (uint32_t)(rc > 0 ? rc : 0);
+    w.done = 0;
+    w.start = 0;
+    w.cap = cap;
+    w.ord = batch_ord;
+    w.h_base = w.mis & ~15u;
+    if (w.total) {
+        glds_region(p0, w.mis, n, w.h_base, wave + hs * kSlotBytes);
+        wait_vm();
+    }
+}
+
+// One record of a lane walk (w.total > 0) with H in slot hs: parse the record
+// at w.start, commit it to the index and move on.  Returns true when the
+// batch is finished (wr filled).  A typical record costs one load latency.
+DEV bool lane_record_step(LaneWalk& w, WalkResult& wr, uint8_t* wave, const uint8_t* lane, uint32_t hs) {
+    const uint32_t cs = 1u - hs;
+    const uint32_t n = w.n, mis = w.mis, start = w.start;
+    // the length varint at start (H holds 16 bytes from it)
+    uint32_t guess = 0xFFFFFFFFu;
+    if (start < n) {
+        const uint8_t* H = lane + hs * kSlotBytes;
+        const uint32_t o = start + mis - w.h_base, k = o & ~3u, sh = o & 3u;
+        const uint32_t w0 = slot_dw(H, k), w1 = slot_dw(H, k + 4u), w2 = slot_dw(H, k + 8u), w3 = slot_dw(H, k + 12u);
+        uint32_t br;
+        const int64_t len = varint12(__builtin_amdgcn_alignbyte(w1, w0, sh), __builtin_amdgcn_alignbyte(w2, w1, sh),
+                                     __builtin_amdgcn_alignbyte(w3, w2, sh), n - start, br);
+        if (len >= 0 && (uint64_t)len <= n) guess = start + br + (uint32_t)len;
+    }
+    // C_k: the record's tail and the next record's head, 48 bytes each side
+    // of the guessed end
+    const uint32_t hb = w.h_base;
+    const uint32_t e16 = (guess + mis + 15u) & ~15u;
+    const uint32_t cb = (guess != 0xFFFFFFFFu && e16 >= hb + kRegionBytes / 2u) ? e16 - kRegionBytes / 2u : hb;
+    glds_region(w.p0, mis, n, cb, wave + cs * kSlotBytes);
+    wait_vm();
+    LdsReader c;
+    c.p0 = w.p0;
+    c.mis = mis;
+    c.n = n;
+    c.pos = start;
+    c.lane = lane;
+    c.wave = wave;
+    c.a_base = hb;
+    c.a_slot = hs;
+    c.t_base = cb;
+    c.t_slot = cs;
+    c.h_slot = hs;
+    const Rec r = parse_fields(c);
+    if (r.err) {
+        wr.parsed = w.done;
+        wr.err = r.err;
+        wr.trailing = 0;
+        return true;
+    }
+    if (w.done < w.cap) {
+        rpgpu_record_index e;
+        e.batch = w.ord;
+        e.rec_pos = start;
+        e.ts_delta = r.ts;
+        e.length = r.length;
+        e.offset_delta = r.off;
+        e.key_len = r.klen;
+        e.key_pos = r.key_pos;
+        e.val_len = r.vlen;
+        e.val_pos = r.val_pos;
+        e.hdr_count = r.hcount;
+        e.hdr_pos = r.hdr_pos;
+        e.end_pos = r.end;
+        e.attrs = (int8_t)r.attr;
+        e.pad[0] = e.pad[1] = e.pad[2] = 0;
+        e.reserved[0] = e.reserved[1] = 0;
+        w.out[w.done] = e;
+    }
+    w.done++;
+    w.start = r.end;
+    if (w.done >= w.total) {
+        wr.parsed = w.done;
+        wr.err = 0;
+        wr.trailing = n - w.start;
+        return true;
+    }
+    // the next record's head: in C_k when the guess held, else loaded into
+    // C_k's slot now
+    const uint32_t g = w.start + mis;
+    if (g - cb <= kRegionReach) w.h_base = cb;
+    else {
+        w.h_base = g & ~15u;
+        glds_region(w.p0, mis, n, w.h_base, wave + cs * kSlotBytes);
+        wait_vm();
+    }
+    return false;
+}
+
+// What a lane walk touches of the job
+struct WalkCtx {
+    const uint8_t* data;
+    const uint64_t* seg_off;
+    rpgpu_batch_result* batches;
+    const uint64_t* slots;
+    rpgpu_record_index* records;
+    uint64_t record_capacity;
+    uint32_t* counters;
+    const uint64_t* chunk_count;  // note_bad (wire only)
+    const uint64_t* chunk_base;
+    uint32_t* seg_first_bad;
+};
+
+DEV WalkCtx walk_ctx(const DeviceJob& j) {
+    return WalkCtx{j.data, j.seg_off, j.batches, j.slots, j.records, j.record_capacity, j.counters,
+                   j.chunk_count, j.chunk_base, j.seg_first_bad};
+}
+
+// A lane-walked batch's descriptor, read by the walking lane itself: the
+// payload, its record count and index slots.  Returns false when the batch
+// is not lane-walked (incomplete, compressed or > kLaneWalkMax records).
+DEV bool lane_walk_setup(const WalkCtx& j, uint64_t b, LaneWalk& w, bool& idx_ok, uint8_t* wave, uint32_t hs) {
+    const rpgpu_batch_result* R = &j.batches[b];
+    const int32_t rc = R->record_count;
+    if (!lane_walked(R->flags, (uint32_t)R->attrs & 7u, rc)) return false;
+    const uint64_t S = j.seg_off[R->segment] + R->file_pos + RPGPU_HEADER_SIZE;
+    const uint32_t n = (uint32_t)(R->size_bytes - (int32_t)RPGPU_HEADER_SIZE);
+    const uint64_t ib = j.slots[b], islots = j.slots[b + 1] - ib;
+    idx_ok = ib + islots <= j.record_capacity;
+    lane_walk_begin(w, j.data + S, n, rc, (uint32_t)b, idx_ok ? j.records + ib : nullptr,
+                    idx_ok ? (uint32_t)islots : 0u, wave, hs);
+    return true;
+}
+
+// A lane walk's verdict bits into the batch result (model/record.h:616-627
+// sync, :680-697 async).  flags is OR-ed: the CRC wave may be writing its
+// own bits into the same word at the same time.
+DEV void lane_walk_finish(const WalkCtx& j, uint64_t b, const WalkResult& w, bool idx_ok, bool wire) {
+    rpgpu_batch_result* R = &j.batches[b];
+    uint32_t f = RPGPU_F_PARSED, perr = w.err;
+    if (perr == 0) {
+        f |= RPGPU_F_PARSE_ASYNC_OK;
+        if (w.trailing == 0) f |= RPGPU_F_PARSE_OK;
+        else perr = RPGPU_PARSE_ERR_TRAILING;
+    }
+    if (f & RPGPU_F_PARSE_OK) {
+        if (idx_ok) f |= RPGPU_F_INDEX_WRITTEN;
+        else { perr = RPGPU_PARSE_ERR_INDEX_CAPACITY; atomicOr(&j.counters[1], 2u); }
+    }
+    // wire: a failed sync record parse is the first batch do_load_slice
+    // rejects (kafka/protocol/batch_reader.cc:129-151)
+    if (wire && !(f & RPGPU_F_PARSE_OK)) note_bad_lane(j, R->segment, b);
+    atomicOr(&R->flags, f);
+    R->records_parsed = w.parsed;
+    R->parse_err = (uint8_t)perr;
+}
+
 __global__ __launch_bounds__(1024) void k_validate(DeviceJob j) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     const Tables* T = j.tables;
@@ -969,131 +1246,32 @@ __global__ __launch_bounds__(1024) void k_validate_decoded(DeviceJob j) {
     }
 }
 
-// ---------------------------------------------------------------------------
-// k_walk: the record walk of stored (uncompressed) payloads with at most
-// kLaneWalkMax records, one LANE per batch, after k_validate has written the
-// CRC verdicts.  record_batch::for_each_record (model/record.h:616-627) is
-// sequential by nature: record k + 1 starts where record k's parse ended
-// (parse_record: model/record_utils.cc:94-181, the same code as the wave
-// walk).  A lane loads the tail of record k (where its headers sit, guessed
-// from the length varint) together with the head of record k + 1 (at that
-// same guess), so a typical record costs one memory latency; 64 batches per
-// wave walk at once and the whole job is in flight together.  Batches with
-// more records are walked by the wave-parallel walk inside k_validate.
-// ---------------------------------------------------------------------------
-DEV void note_bad_lane(const DeviceJob& j, uint32_t seg, uint64_t b) {
-    const uint64_t first = j.chunk_count[j.chunk_base[seg]];
-    atomicMin(&j.seg_first_bad[seg], (uint32_t)(b - first));
-}
-
-DEV WalkResult walk_lane(const uint8_t* p0, uint32_t n, int32_t rc, uint32_t batch_ord, rpgpu_record_index* out,
-                         uint64_t out_cap) {
-    WalkResult wr;
-    wr.parsed = 0;
-    wr.err = 0;
-    wr.trailing = 0;
-    const uint32_t mis = (uint32_t)((uintptr_t)p0 & 15);
-    const uint32_t total = (uint32_t)(rc > 0 ? rc : 0);
-    if (total == 0) {
-        wr.trailing = n;
-        return wr;
-    }
-    uint32_t start = 0, done = 0;
-    Region H, T, N;
-    load_region(p0, mis, n, mis & ~15u, H);
-    for (;;) {
-        // the length varint at start (H holds the 12 bytes after it)
-        uint32_t guess = 0xFFFFFFFFu;
-        if (start < n) {
-            const uint32_t o = start + mis - H.base, k = o >> 2, sh = o & 3u;
-            const uint32_t w0 = pick12(H, k), w1 = pick12(H, k + 1u), w2 = pick12(H, k + 2u), w3 = pick12(H, k + 3u);
-            uint32_t br;
-            const int64_t len = varint12(__builtin_amdgcn_alignbyte(w1, w0, sh), __builtin_amdgcn_alignbyte(w2, w1, sh),
-                                         __builtin_amdgcn_alignbyte(w3, w2, sh), n - start, br);
-            if (len >= 0 && (uint64_t)len <= n) guess = start + br + (uint32_t)len;
-        }
-        // tail rows of this record and head rows of the next, together
-        const uint32_t hb = H.base;
-        const uint32_t e16 = (guess + mis + 15u) & ~15u;
-        const uint32_t tb = (guess != 0xFFFFFFFFu && e16 >= hb + 48u) ? e16 - 48u : hb;
-        load_region(p0, mis, n, tb, T);
-        const bool ahead = guess != 0xFFFFFFFFu && guess < n && done + 1u < total;
-        if (ahead) load_region(p0, mis, n, (guess + mis) & ~15u, N);
-        const Rec r = parse_record(p0, mis, n, start, H, T);
-        if (r.err) {
-            wr.parsed = done;
-            wr.err = r.err;
-            return wr;
-        }
-        if (done < out_cap) {
-            rpgpu_record_index e;
-            e.batch = batch_ord;
-            e.rec_pos = start;
-            e.ts_delta = r.ts;
-            e.length = r.length;
-            e.offset_delta = r.off;
-            e.key_len = r.klen;
-            e.key_pos = r.key_pos;
-            e.val_len = r.vlen;
-            e.val_pos = r.val_pos;
-            e.hdr_count = r.hcount;
-            e.hdr_pos = r.hdr_pos;
-            e.end_pos = r.end;
-            e.attrs = (int8_t)r.attr;
-            e.pad[0] = e.pad[1] = e.pad[2] = 0;
-            e.reserved[0] = e.reserved[1] = 0;
-            out[done] = e;
-        }
-        done++;
-        start = r.end;
-        if (done >= total) break;
-        if (ahead && start == guess) H = N;
-        else load_region(p0, mis, n, (start + mis) & ~15u, H);
-    }
-    wr.parsed = done;
-    wr.trailing = n - start;
-    return wr;
-}
-
 __global__ __launch_bounds__(256) void k_walk(DeviceJob j) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    uint8_t* wave = lds + (threadIdx.x >> 6) * kWalkLdsWave;
+    const uint8_t* lane = wave + 16u * lane_v();
     const uint64_t nb_total = j.chunk_count[j.total_chunks];
     const uint64_t nb = nb_total < j.batch_capacity ? nb_total : j.batch_capacity;
     const bool wire = j.layout == RPGPU_LAYOUT_WIRE;
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    const WalkCtx c = walk_ctx(j);
     for (uint64_t b = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; b < nb; b += stride) {
-        rpgpu_batch_result* R = &j.batches[b];
-        const uint32_t flags = R->flags;
-        const int32_t rc = R->record_count;
-        if (!lane_walked(flags, (uint32_t)R->attrs & 7u, rc)) continue;
-        if (wire && !(flags & RPGPU_F_CRC_OK)) continue;
-        const uint32_t seg = R->segment;
-        const uint64_t S = j.seg_off[seg] + R->file_pos + RPGPU_HEADER_SIZE;
-        const uint32_t n = (uint32_t)(R->size_bytes - (int32_t)RPGPU_HEADER_SIZE);
-        const uint64_t ib = j.slots[b], islots = j.slots[b + 1] - ib;
-        const bool idx_ok = ib + islots <= j.record_capacity;
-        const WalkResult w = walk_lane(j.data + S, n, rc, (uint32_t)b, idx_ok ? j.records + ib : nullptr,
-                                       idx_ok ? islots : 0);
-        uint32_t f = flags | RPGPU_F_PARSED, perr = w.err;
-        if (perr == 0) {
-            f |= RPGPU_F_PARSE_ASYNC_OK;
-            if (w.trailing == 0) f |= RPGPU_F_PARSE_OK;
-            else perr = RPGPU_PARSE_ERR_TRAILING;
-        }
-        if (f & RPGPU_F_PARSE_OK) {
-            if (idx_ok) f |= RPGPU_F_INDEX_WRITTEN;
-            else { perr = RPGPU_PARSE_ERR_INDEX_CAPACITY; atomicOr(&j.counters[1], 2u); }
-        }
-        // wire: a failed sync record parse is the first batch do_load_slice
-        // rejects (kafka/protocol/batch_reader.cc:129-151)
-        if (wire && !(f & RPGPU_F_PARSE_OK)) note_bad_lane(j, seg, b);
-        R->flags = f;
-        R->records_parsed = w.parsed;
-        R->parse_err = (uint8_t)perr;
+        if (wire && !(j.batches[b].flags & RPGPU_F_CRC_OK)) continue;
+        LaneWalk w;
+        bool idx_ok;
+        // every lane of the while loop below is at the same step: the slot
+        // parity is uniform
+        if (!lane_walk_setup(c, b, w, idx_ok, wave, h_slot_of(0))) continue;
+        WalkResult wr;
+        if (w.total == 0) { wr.parsed = 0; wr.err = 0; wr.trailing = w.n; }
+        else for (uint32_t step = 0; !lane_record_step(w, wr, wave, lane, h_slot_of(step)); step++) {}
+        lane_walk_finish(c, b, wr, idx_ok, wire);
     }
 }
 
 hipError_t launch_walk(const DeviceJob& j, hipStream_t s, uint32_t grid) {
-    if (j.flags & RPGPU_JOB_PARSE) hipLaunchKernelGGL(k_walk, dim3(grid), dim3(256), 0, s, j);
+    if (j.flags & RPGPU_JOB_PARSE)
+        hipLaunchKernelGGL(k_walk, dim3(grid), dim3(256), 4 * kWalkLdsWave, s, j);
     return hipGetLastError();
 }
 
