@@ -105,6 +105,28 @@ struct rpgpu_ctx {
     size_t ev_used = 0;
     uint32_t cu_count = 256;
     std::string err;
+    // rpgpu_validate_host: a copy stream and two staging slots (segment
+    // bytes in, per-batch results out), used alternately so the H2D copy of
+    // group g + 1 runs while group g validates
+    hipStream_t copy = nullptr;
+    struct HostSlot {
+        uint8_t* d_data = nullptr;
+        uint64_t data_bytes = 0;
+        uint64_t* d_offs = nullptr;
+        uint64_t offs_n = 0;
+        rpgpu_batch_result* d_batches = nullptr;
+        uint64_t bcap = 0;
+        rpgpu_record_index* d_records = nullptr;
+        uint64_t rcap = 0;
+        uint8_t* d_decoded = nullptr;
+        uint64_t dcap = 0;
+        rpgpu_segment_summary* d_sums = nullptr;
+        uint64_t sums_n = 0;
+        rpgpu_job_totals* d_tot = nullptr;
+        rpgpu_job_totals* h_tot = nullptr;  // pinned
+        hipEvent_t h2d = nullptr, done = nullptr;
+        std::vector<uint64_t> h_offs;
+    } hs[2];
 };
 
 namespace {
@@ -171,6 +193,15 @@ int rpgpu_destroy(rpgpu_ctx* c) {
     for (auto& set : c->ev_sets)
         for (auto& e : set) hipEventDestroy(e);
     if (c->stream) hipStreamDestroy(c->stream);
+    if (c->copy) { (void)hipStreamSynchronize(c->copy); (void)hipStreamDestroy(c->copy); }
+    for (auto& h : c->hs) {
+        (void)hipFree(h.d_data); (void)hipFree(h.d_offs); (void)hipFree(h.d_batches); (void)hipFree(h.d_records);
+        (void)hipFree(h.d_decoded);
+        (void)hipFree(h.d_sums); (void)hipFree(h.d_tot);
+        if (h.h_tot) (void)hipHostFree(h.h_tot);
+        if (h.h2d) hipEventDestroy(h.h2d);
+        if (h.done) hipEventDestroy(h.done);
+    }
     delete c;
     return RPGPU_OK;
 }
@@ -469,9 +500,177 @@ int rpgpu_uncompress(rpgpu_ctx* c, int codec, const void* in, size_t n, void* ou
     return RPGPU_OK;
 }
 
-__attribute__((weak)) int rpgpu_validate_host(rpgpu_ctx* c, const rpgpu_host_job* job) {
-    (void)job;
-    return fail(c, RPGPU_E_UNSUPPORTED, "rpgpu_validate_host: not built");
+// ---------------------------------------------------------------------------
+// Host segment path (log_replayer over files, storage/log_replayer.cc:95-114):
+// host-resident segments are grouped into staging groups of at most
+// kHostGroupBytes (a larger segment is a group of its own), copied H2D with
+// hipMemcpyAsync on the context's copy stream into one of two device slots,
+// and validated by the same pipeline as rpgpu_submit on the compute stream;
+// while group g validates, group g + 1 is being copied and group g - 1's
+// per-batch results come back.  Outputs are the caller's host arrays; the
+// record index and decoded bytes stay on the device (the verdict bits,
+// records_parsed and the decoded crcs are in the batch results).  A group
+// whose device outputs overflowed is re-run with the capacities the device
+// reported, so the host sees the same results as one big rpgpu_submit.
+// ---------------------------------------------------------------------------
+}  // extern "C"
+
+namespace {
+constexpr uint64_t kHostGroupBytes = 256ull << 20;
+
+// RPGPU_HOST_GROUP_KIB: staging-group size override (tests use small groups
+// to exercise the double buffering on small inputs)
+uint64_t host_group_bytes() {
+    const char* e = getenv("RPGPU_HOST_GROUP_KIB");
+    const uint64_t kib = e ? strtoull(e, nullptr, 10) : 0;
+    return kib ? kib << 10 : kHostGroupBytes;
+}
+
+template <class T>
+int grow(rpgpu_ctx* c, T*& p, uint64_t& have, uint64_t need) {
+    if (need <= have && p) return RPGPU_OK;
+    if (p) hipFree(p);
+    p = nullptr;
+    have = 0;
+    if (hipMalloc((void**)&p, (size_t)std::max<uint64_t>(need, 1) * sizeof(T)) != hipSuccess)
+        return fail(c, RPGPU_E_NOMEM, "rpgpu_validate_host: device staging");
+    have = need;
+    return RPGPU_OK;
+}
+
+struct HostGroup {
+    uint32_t seg0, nseg;
+    uint64_t bytes;
+};
+
+// issue group g on slot h: H2D on the copy stream, then the pipeline on the
+// compute stream (after the copy), then the totals back to pinned memory
+int host_issue(rpgpu_ctx* c, rpgpu_ctx::HostSlot& h, const rpgpu_host_job* job, const HostGroup& g) {
+    const uint64_t padded = align_up(g.bytes + 64, 256);
+    if (int rc = grow(c, h.d_data, h.data_bytes, padded)) return rc;
+    if (int rc = grow(c, h.d_offs, h.offs_n, (uint64_t)g.nseg + 1)) return rc;
+    if (int rc = grow(c, h.d_sums, h.sums_n, (uint64_t)g.nseg)) return rc;
+    // first-try capacities: every batch at least a header, every record at
+    // least 7 bytes (length, attributes, three deltas/lengths, header count),
+    // decode up to 4x; a group that overflows is re-run
+    const uint64_t bneed = g.bytes / RPGPU_HEADER_SIZE + 1;
+    if (int rc = grow(c, h.d_batches, h.bcap, bneed)) return rc;
+    if (job->flags & RPGPU_JOB_PARSE)
+        if (int rc = grow(c, h.d_records, h.rcap, g.bytes / 7 + 1)) return rc;
+    if (job->flags & RPGPU_JOB_DECODE)
+        if (int rc = grow(c, h.d_decoded, h.dcap, 4 * g.bytes + 4096)) return rc;
+    h.h_offs.assign(g.nseg + 1, 0);
+    for (uint32_t i = 0; i < g.nseg; i++) h.h_offs[i + 1] = h.h_offs[i] + job->seg_sizes[g.seg0 + i];
+    for (uint32_t i = 0; i < g.nseg; i++)
+        if (job->seg_sizes[g.seg0 + i])
+            HIPCHK(c, hipMemcpyAsync(h.d_data + h.h_offs[i], job->segments[g.seg0 + i], job->seg_sizes[g.seg0 + i],
+                                     hipMemcpyHostToDevice, c->copy));
+    HIPCHK(c, hipMemcpyAsync(h.d_offs, h.h_offs.data(), (g.nseg + 1) * 8, hipMemcpyHostToDevice, c->copy));
+    HIPCHK(c, hipEventRecord(h.h2d, c->copy));
+    HIPCHK(c, hipStreamWaitEvent(c->stream, h.h2d, 0));
+    rpgpu_job j{};
+    j.d_data = h.d_data;
+    j.d_seg_offsets = h.d_offs;
+    j.h_seg_offsets = h.h_offs.data();
+    j.n_segments = g.nseg;
+    j.layout = job->layout;
+    j.flags = job->flags;
+    j.d_batches = h.d_batches;
+    j.batch_capacity = h.bcap;
+    j.d_records = h.d_records;
+    j.record_capacity = (job->flags & RPGPU_JOB_PARSE) ? h.rcap : 0;
+    j.d_decoded = h.d_decoded;
+    j.decoded_capacity = (job->flags & RPGPU_JOB_DECODE) ? h.dcap : 0;
+    j.d_summaries = h.d_sums;
+    j.d_totals = h.d_tot;
+    if (int rc = rpgpu_submit(c, &j, c->stream)) return rc;
+    HIPCHK(c, hipMemcpyAsync(h.h_tot, h.d_tot, sizeof(rpgpu_job_totals), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipEventRecord(h.done, c->stream));
+    return RPGPU_OK;
+}
+}  // namespace
+
+extern "C" {
+
+int rpgpu_validate_host(rpgpu_ctx* c, const rpgpu_host_job* job) {
+    if (!c || !job || (job->n_segments && (!job->segments || !job->seg_sizes)) || !job->totals ||
+        (job->n_segments && !job->summaries) || (job->batch_capacity && !job->batches))
+        return fail(c, RPGPU_E_INVALID, "rpgpu_validate_host: missing argument");
+    if (job->layout != RPGPU_LAYOUT_DISK && job->layout != RPGPU_LAYOUT_WIRE)
+        return fail(c, RPGPU_E_INVALID, "rpgpu_validate_host: unknown layout");
+    hipSetDevice(c->device);
+    std::memset(job->totals, 0, sizeof(rpgpu_job_totals));
+    if (job->n_segments == 0) return RPGPU_OK;
+    if (!c->copy) HIPCHK(c, hipStreamCreateWithFlags(&c->copy, hipStreamNonBlocking));
+    for (auto& h : c->hs) {
+        if (!h.h2d) HIPCHK(c, hipEventCreateWithFlags(&h.h2d, hipEventDisableTiming));
+        if (!h.done) HIPCHK(c, hipEventCreateWithFlags(&h.done, hipEventDisableTiming));
+        if (!h.h_tot) HIPCHK(c, hipHostMalloc((void**)&h.h_tot, sizeof(rpgpu_job_totals), hipHostMallocDefault));
+        if (!h.d_tot) HIPCHK(c, hipMalloc((void**)&h.d_tot, sizeof(rpgpu_job_totals)));
+    }
+    std::vector<HostGroup> groups;
+    const uint64_t gbytes = host_group_bytes();
+    for (uint32_t i = 0; i < job->n_segments; i++) {
+        const uint64_t sz = job->seg_sizes[i];
+        if (!job->segments[i] && sz) return fail(c, RPGPU_E_INVALID, "rpgpu_validate_host: null segment");
+        if (groups.empty() || groups.back().bytes + sz > gbytes) groups.push_back({i, 0, 0});
+        groups.back().nseg++;
+        groups.back().bytes += sz;
+    }
+    rpgpu_job_totals& T = *job->totals;
+    uint64_t out_b = 0;
+    // collect group gi (slot h): its totals, re-run on overflow, then the
+    // batch results and summaries into the caller's arrays
+    auto finish = [&](size_t gi) -> int {
+        auto& h = c->hs[gi & 1];
+        const HostGroup& g = groups[gi];
+        HIPCHK(c, hipEventSynchronize(h.done));
+        for (int tries = 0; h.h_tot->overflow && tries < 2; tries++) {
+            const rpgpu_job_totals t = *h.h_tot;
+            if (int rc = grow(c, h.d_batches, h.bcap, t.batch_capacity_needed)) return rc;
+            if (job->flags & RPGPU_JOB_PARSE)
+                if (int rc = grow(c, h.d_records, h.rcap, t.record_capacity_needed)) return rc;
+            if (job->flags & RPGPU_JOB_DECODE)
+                if (int rc = grow(c, h.d_decoded, h.dcap, t.decoded_capacity_needed)) return rc;
+            if (int rc = host_issue(c, h, job, g)) return rc;
+            HIPCHK(c, hipEventSynchronize(h.done));
+        }
+        const rpgpu_job_totals t = *h.h_tot;
+        const uint64_t nb = t.n_batches;
+        const uint64_t room = job->batch_capacity > out_b ? job->batch_capacity - out_b : 0;
+        const uint64_t take = std::min(nb, room);
+        // results back on the copy stream: the compute stream already holds
+        // the next group's pipeline, which must not be waited for here
+        if (take) {
+            HIPCHK(c, hipMemcpyAsync(job->batches + out_b, h.d_batches, take * sizeof(rpgpu_batch_result),
+                                     hipMemcpyDeviceToHost, c->copy));
+        }
+        HIPCHK(c, hipMemcpyAsync(job->summaries + g.seg0, h.d_sums, g.nseg * sizeof(rpgpu_segment_summary),
+                                 hipMemcpyDeviceToHost, c->copy));
+        HIPCHK(c, hipStreamSynchronize(c->copy));
+        // group-relative -> job-wide ordinals
+        for (uint64_t i = 0; i < take; i++) job->batches[out_b + i].segment += g.seg0;
+        for (uint32_t i = 0; i < g.nseg; i++) job->summaries[g.seg0 + i].first_batch += out_b;
+        T.n_batches += nb;
+        T.n_records += t.n_records;
+        T.decoded_bytes += t.decoded_bytes;
+        T.n_rewalks += t.n_rewalks;
+        T.record_capacity_needed += t.record_capacity_needed;
+        T.decoded_capacity_needed += t.decoded_capacity_needed;
+        T.overflow |= t.overflow;
+        if (nb > room) T.overflow |= 1u;
+        out_b += nb;
+        return RPGPU_OK;
+    };
+    // issue(g) before finish(g - 1): group g's copy and pipeline are queued
+    // while g - 1's results come back; issue(g + 1) reuses g - 1's slot
+    for (size_t gi = 0; gi < groups.size(); gi++) {
+        if (int rc = host_issue(c, c->hs[gi & 1], job, groups[gi])) return rc;
+        if (gi) if (int rc = finish(gi - 1)) return rc;
+    }
+    if (int rc = finish(groups.size() - 1)) return rc;
+    T.batch_capacity_needed = T.n_batches;
+    return RPGPU_OK;
 }
 
 }  // extern "C"

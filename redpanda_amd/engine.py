@@ -170,3 +170,33 @@ class Engine:
         self.submit(data, offs, out, flags, chunk_bytes, layout=layout)
         torch.cuda.synchronize(data.device)
         return out.to_host()
+
+    def validate_host(self, segments, flags: int = abi.JOB_CRC | abi.JOB_PARSE, layout: int = abi.LAYOUT_DISK,
+                      batch_capacity=None):
+        """rpgpu_validate_host: host-resident segments (numpy uint8 arrays,
+        pinned or pageable) copied to the device in double-buffered groups
+        and validated there.  Returns (batches, summaries, totals) as numpy
+        structured arrays; the record index stays on the device."""
+        segs = [np.ascontiguousarray(s, dtype=np.uint8) for s in segments]
+        n = len(segs)
+        if batch_capacity is None:
+            batch_capacity = sum(s.size for s in segs) // abi.HEADER_SIZE + n + 1
+        ptrs = (C.c_void_p * max(n, 1))(*[s.ctypes.data for s in segs])
+        sizes = (C.c_uint64 * max(n, 1))(*[s.size for s in segs])
+        batches = np.zeros(max(batch_capacity, 1), dtype=abi.BATCH_RESULT)
+        sums = np.zeros(max(n, 1), dtype=abi.SEGMENT_SUMMARY)
+        tot = np.zeros(1, dtype=abi.JOB_TOTALS)
+        job = HostJobC(C.cast(ptrs, C.c_void_p), C.cast(sizes, C.c_void_p), n, layout, flags, 0,
+                       batches.ctypes.data, batch_capacity, sums.ctypes.data, tot.ctypes.data)
+        rc = self.L.rpgpu_validate_host(self.ctx, C.byref(job))
+        check(rc, self.ctx, "rpgpu_validate_host")
+        nb = int(min(tot[0]["n_batches"], batch_capacity))
+        return batches[:nb], sums[:n], tot[0]
+
+
+class HostJobC(C.Structure):
+    """rpgpu_host_job (include/rpgpu.h)."""
+    _fields_ = [("segments", C.c_void_p), ("seg_sizes", C.c_void_p), ("n_segments", C.c_uint32),
+                ("layout", C.c_uint32), ("flags", C.c_uint32), ("reserved", C.c_uint32),
+                ("batches", C.c_void_p), ("batch_capacity", C.c_uint64), ("summaries", C.c_void_p),
+                ("totals", C.c_void_p)]

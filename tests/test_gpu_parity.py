@@ -218,3 +218,30 @@ def test_wire_layout_codec_mix(engine, oracle, rplib):
     got, ref = run_both(engine, oracle, sets, flags=DFLAGS, chunk=64 << 10, layout=abi.LAYOUT_WIRE)
     assert np.any(got.batches["flags"] & abi.F_CODEC_OK)
     assert_same(got, ref, DFLAGS)
+
+
+@pytest.mark.parametrize("group_kib", [0, 1024, 3000])
+def test_host_path(engine, oracle, rplib, group_kib, monkeypatch):
+    """rpgpu_validate_host (pinned/pageable host segments, double-buffered
+    H2D groups): per-batch results and summaries equal the oracle's over the
+    same segments.  Small staging groups exercise the slot alternation; the
+    LZ4/snappy mix with DECODE makes groups overflow the first-try decode
+    capacity and re-run."""
+    if group_kib:
+        monkeypatch.setenv("RPGPU_HOST_GROUP_KIB", str(group_kib))
+    segs = [gen(rplib, 2 << 20, i, seed=0xC5, batch_bytes=0, min_batch=200, max_batch=300000, codec_mix=MIX,
+                corrupt_payload_ppm=20000, corrupt_header_ppm=(5000 if i == 2 else 0)) for i in range(5)]
+    segs.append(gen(rplib, 4 << 20, 9, seed=0xC1))
+    offs = np.cumsum([0] + [s.size for s in segs]).astype(np.uint64)
+    ref = oracle.run_job(np.concatenate(segs), offs, DFLAGS)
+    b, s, t = engine.validate_host(segs, DFLAGS)
+    assert len(b) == len(ref.batches)
+    for f in abi.BATCH_COMPARE_FIELDS:
+        if f in ("index_base", "decoded_off"):  # device-side arena positions, per staging group
+            continue
+        np.testing.assert_array_equal(b[f], ref.batches[f], err_msg=f"batches.{f}")
+    for f in abi.SUMMARY_COMPARE_FIELDS:
+        np.testing.assert_array_equal(s[f], ref.summaries[f], err_msg=f"summaries.{f}")
+    for k in ("n_batches", "n_records", "decoded_bytes"):
+        assert int(t[k]) == int(ref.totals[k]), k
+    assert int(t["overflow"]) == 0
