@@ -791,16 +791,7 @@ DEV uint32_t walk_flags(const DeviceJob& j, const WalkResult& w, bool idx_ok, ui
 constexpr int kPreRows = 0;
 
 // ---------------------------------------------------------------------------
-// k_walk: the record walk of stored (uncompressed) payloads with at most
-// kLaneWalkMax records, one LANE per batch, after k_validate has written the
-// CRC verdicts.  record_batch::for_each_record (model/record.h:616-627) is
-// sequential by nature: record k + 1 starts where record k's parse ended
-// (parse_record: model/record_utils.cc:94-181, the same code as the wave
-// walk).  A lane loads the tail of record k (where its headers sit, guessed
-// from the length varint) together with the head of record k + 1 (at that
-// same guess), so a typical record costs one memory latency; 64 batches per
-// wave walk at once and the whole job is in flight together.  Batches with
-// more records are walked by the wave-parallel walk inside k_validate.
+// Lane record walk (k_walk)
 // ---------------------------------------------------------------------------
 template <class J>
 DEV void note_bad_lane(const J& j, uint32_t seg, uint64_t b) {
@@ -809,21 +800,25 @@ DEV void note_bad_lane(const J& j, uint32_t seg, uint64_t b) {
 }
 
 // One lane's walk of one stored payload.  The bytes a lane parses sit in
-// LDS slots rather than registers: a region (6 rows of 16 bytes at a 16-byte
-// aligned grid offset) is copied global -> LDS by six global_load_lds, and
-// the parser reads any dword of it with one ds_read at a per-lane address.
-// (Held in registers, every field read was a 12-way select: ~1,200 VALU per
-// record.)  Record k's step loads ONE region, C_k = the 96 bytes around its
-// guessed end: the 48 bytes before it hold record k's headers, the 48 after
-// it record k + 1's length .. key length, key and value length (16-byte
-// keys), so the next step parses its head from C_k with no second load.  Each
-// walk wave owns two slots that alternate by the parity of its step counter
-// (uniform, as global_load_lds writes a wave-uniform LDS base + 16 * lane):
-// H (C_{k-1}, read) and C_k (loaded).
+// LDS rather than registers (held in registers, every field read was a
+// 12-way select: ~1,200 VALU per record), in regions of 6 rows of 16 bytes
+// at a 16-byte aligned grid offset.  Record k's step needs ONE region, C_k =
+// the 96 bytes around its guessed end: the 48 bytes before it hold record
+// k's headers, the 48 after it record k + 1's length .. key length, key and
+// value length (16-byte keys), so the next step parses its head from C_k.
+//
+// The regions of a wave's 64 lanes are fetched together, cooperatively: the
+// 384 rows are spread over 6 global_load_lds wave-instructions so that each
+// instruction reads ~10 regions' contiguous rows (~17 cache lines) instead
+// of one row from each of 64 regions (64 lines).  The lane-per-region
+// gather was bound by the texture addresser (TA ~86% busy, ~126 cycles per
+// instruction).  Row r of lane w's region lands at slot + 96 w + 16 r.  Two
+// slots per wave alternate by step parity: H (C_{k-1}, the record's head)
+// and C_k (loaded this step).
 constexpr uint32_t kRegionRows = 6u;
 constexpr uint32_t kRegionBytes = 16u * kRegionRows;
 constexpr uint32_t kRegionReach = kRegionBytes - 16u;  // a read needs 16 bytes from its offset
-constexpr uint32_t kSlotBytes = kRegionRows * 1024u;
+constexpr uint32_t kSlotBytes = 64u * kRegionBytes;
 constexpr uint32_t kWalkLdsWave = 2u * kSlotBytes;
 
 typedef __attribute__((address_space(3))) void lds_void;
@@ -831,47 +826,119 @@ typedef const __attribute__((address_space(1))) void gbl_void;
 
 DEV void wait_vm() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
-// the region at grid offset base (rows at or past the payload end are not
-// loaded: their bytes are never parsed) into the slot whose row 0 is at the
-// wave-uniform LDS address `slot`
-DEV void glds_region(const uint8_t* p0, uint32_t mis, uint32_t n, uint32_t base, uint8_t* slot) {
-    const uint8_t* row = p0 - mis + base;
+// Region layout in a slot.  Cooperative fetch (default): lane w's region is
+// contiguous at slot + 96 w.  Per-lane fetch (RPGPU_WALK_COOP_LOAD=0, kept
+// for A/B): each lane issues its own six global_load_lds, which land
+// lane-linear, so row r of lane w sits at slot + 1024 r + 16 w.  Measured on
+// C1: walk 1.36 ms cooperative, 1.45 ms per-lane.
+#ifndef RPGPU_WALK_COOP_LOAD
+#define RPGPU_WALK_COOP_LOAD 1
+#endif
+constexpr bool kCoopLoad = RPGPU_WALK_COOP_LOAD != 0;
+DEV uint32_t region_off(uint32_t o) { return kCoopLoad ? o : (o >> 4) * 1024u + (o & 12u); }
+DEV uint32_t region_lane(uint32_t l) { return kCoopLoad ? kRegionBytes * l : 16u * l; }
+
+// rows of the region at grid offset base that start inside the payload
+// (the others are never parsed and are not loaded)
+DEV uint32_t region_rows(uint32_t n, uint32_t mis, uint32_t base) {
     const uint32_t lim = n + mis;
+    if (base >= lim) return 0u;
+    const uint32_t r = (lim - base + 15u) >> 4;
+    return r < kRegionRows ? r : kRegionRows;
+}
+
+// Wave-cooperative fetch (all 64 lanes active): lane w wants `rows` rows from
+// global address g (16-byte aligned) into its region of the slot at the
+// wave-uniform LDS address `slot`.
+DEV void coop_load(uint8_t* slot, const uint8_t* g, uint32_t rows) {
+    const uint32_t l = lane_v();
+    const uint64_t ga = (uint64_t)(uintptr_t)g;
+    const int lo = (int)(uint32_t)ga, hi = (int)(uint32_t)(ga >> 32), nr = (int)rows;
+#pragma unroll
+    for (uint32_t m = 0; m < kRegionRows; m++) {
+        const uint32_t q = 64u * m + l, w = q / kRegionRows, r = q - w * kRegionRows;
+        const int src = (int)(w * 4u);
+        const uint32_t wlo = (uint32_t)__builtin_amdgcn_ds_bpermute(src, lo);
+        const uint32_t whi = (uint32_t)__builtin_amdgcn_ds_bpermute(src, hi);
+        const uint32_t wnr = (uint32_t)__builtin_amdgcn_ds_bpermute(src, nr);
+        if (r < wnr) {
+            const uint8_t* row = (const uint8_t*)(uintptr_t)(((uint64_t)whi << 32) | wlo) + 16u * r;
+            __builtin_amdgcn_global_load_lds((gbl_void*)row, (lds_void*)(slot + 1024u * m), 16, 0, 0);
+        }
+    }
+}
+
+// Wave-cooperative index store (all 64 lanes active): lane w's 64-byte entry
+// e goes to dst (null: nothing to write).  The entries are staged in LDS
+// (`stage`, 4 KiB, wave-uniform) and written 16 per wave-instruction, each
+// as 4 lanes x 16 contiguous bytes, instead of one 16-byte piece of each of
+// 64 scattered entries per instruction (the index stores were a third of
+// the walk's time).
+DEV void coop_store(uint8_t* stage, const rpgpu_record_index& e, rpgpu_record_index* dst) {
+    static_assert(sizeof(rpgpu_record_index) == 64, "index entry is 4 x 16 bytes");
+    const uint32_t l = lane_v();
+    const uint4* src = (const uint4*)&e;
+    uint4* mine = (uint4*)(stage + 64u * l);
+    if (dst) {
+        mine[0] = src[0];
+        mine[1] = src[1];
+        mine[2] = src[2];
+        mine[3] = src[3];
+    }
+    const uint64_t da = (uint64_t)(uintptr_t)dst;
+    const int lo = (int)(uint32_t)da, hi = (int)(uint32_t)(da >> 32);
+#pragma unroll
+    for (uint32_t m = 0; m < 4u; m++) {
+        const uint32_t w = 16u * m + (l >> 2), qtr = l & 3u;
+        const int src_lane = (int)(w * 4u);
+        const uint32_t wlo = (uint32_t)__builtin_amdgcn_ds_bpermute(src_lane, lo);
+        const uint32_t whi = (uint32_t)__builtin_amdgcn_ds_bpermute(src_lane, hi);
+        if (wlo | whi) {
+            const uint4 v = *(const uint4*)(stage + 64u * w + 16u * qtr);
+            *(uint4*)((uint8_t*)(uintptr_t)(((uint64_t)whi << 32) | wlo) + 16u * qtr) = v;
+        }
+    }
+}
+
+// one lane's own region load (rare: a record the guess did not cover), with
+// plain loads and ds_writes into its region of a slot
+DEV void lane_region_load(const uint8_t* p0, uint32_t mis, uint32_t n, uint32_t base, uint8_t* region) {
+    const uint8_t* row = p0 - mis + base;
+    const uint32_t rows = region_rows(n, mis, base);
 #pragma unroll
     for (uint32_t r = 0; r < kRegionRows; r++)
-        if (base + 16u * r < lim)
-            __builtin_amdgcn_global_load_lds((gbl_void*)(row + 16u * r), (lds_void*)(slot + 1024u * r), 16, 0, 0);
+        if (r < rows) *(uint4*)(region + region_off(16u * r)) = *(const uint4*)(row + 16u * r);
 }
 
-// dword at 4-aligned region offset o (< kRegionBytes) of a lane's slot
-DEV uint32_t slot_dw(const uint8_t* lane_slot, uint32_t o) {
-    return *(const uint32_t*)(lane_slot + (o >> 4) * 1024u + (o & 12u));
+// dword at 4-aligned offset o (< kRegionBytes) of a lane's region
+DEV uint32_t region_dw(const uint8_t* region, uint32_t o) {
+    return *(const uint32_t*)(region + region_off(o));
 }
 
-// The record parser's byte source over LDS slots: the current region A, the
-// tail region T (C_k, the other slot), else a fresh region at the read
-// position (one dependent load, into the H slot: the read position has left
-// H, and C_k must survive as the next step's H).
+// The record parser's byte source over LDS regions: the current region A,
+// the tail region T (C_k), else a fresh region at the read position (one
+// dependent load, into H's region: the read position has left H, and C_k
+// must survive as the next step's H).
 struct LdsReader {
     const uint8_t* p0;  // payload start
     uint32_t mis;       // p0 & 15
     uint32_t n;
     uint32_t pos;
-    const uint8_t* lane;  // wave LDS base + 16 * lane
-    uint8_t* wave;        // wave LDS base
-    uint32_t a_base, a_slot, t_base, t_slot, h_slot;
+    const uint8_t* a;   // region being read (LDS)
+    const uint8_t* t;
+    uint8_t* h;
+    uint32_t a_base, t_base;
 
     DEV uint32_t locate() {
         const uint32_t g = pos + mis;
         if (g - a_base > kRegionReach) {
             if (g - t_base <= kRegionReach) {
                 a_base = t_base;
-                a_slot = t_slot;
+                a = t;
             } else {
                 a_base = g & ~15u;
-                a_slot = h_slot;
-                glds_region(p0, mis, n, a_base, wave + h_slot * kSlotBytes);
-                wait_vm();
+                a = h;
+                lane_region_load(p0, mis, n, a_base, h);
             }
         }
         return g - a_base;
@@ -879,11 +946,10 @@ struct LdsReader {
     // iobuf_parser_base::read_varlong (bytes/iobuf_parser.h:48-52)
     DEV int64_t varlong() {
         const uint32_t o = locate(), k = o & ~3u, sh = o & 3u, avail = n - pos;
-        const uint8_t* ls = lane + a_slot * kSlotBytes;
-        const uint32_t w0 = slot_dw(ls, k), w1 = slot_dw(ls, k + 4u);
+        const uint32_t w0 = region_dw(a, k), w1 = region_dw(a, k + 4u);
         uint32_t r0 = __builtin_amdgcn_alignbyte(w1, w0, sh), r1 = 0u, r2 = 0u, br;
         if (avail >= 2 && (r0 & 0x8080u) == 0x8080u) {
-            const uint32_t w2 = slot_dw(ls, k + 8u), w3 = slot_dw(ls, k + 12u);
+            const uint32_t w2 = region_dw(a, k + 8u), w3 = region_dw(a, k + 12u);
             r1 = __builtin_amdgcn_alignbyte(w2, w1, sh);
             r2 = __builtin_amdgcn_alignbyte(w3, w2, sh);
         }
@@ -893,7 +959,7 @@ struct LdsReader {
     }
     DEV uint32_t byte() {
         const uint32_t o = locate();
-        return (slot_dw(lane + a_slot * kSlotBytes, o & ~3u) >> (8u * (o & 3u))) & 0xFFu;
+        return (region_dw(a, o & ~3u) >> (8u * (o & 3u))) & 0xFFu;
     }
 };
 
@@ -901,16 +967,11 @@ struct LaneWalk {
     const uint8_t* p0;
     rpgpu_record_index* out;  // the batch's index slots (null when they overflow)
     uint32_t mis, n, total, done, start, cap, ord;
-    uint32_t h_base;  // grid offset of the region holding `start` (in the step's H slot)
+    uint32_t h_base;  // grid offset of the region holding `start`
 };
 
-// H slot of step `step` (the other one receives C_k)
-DEV uint32_t h_slot_of(uint32_t step) { return step & 1u; }
-
-// set up a lane walk; the first region goes into the H slot of the step that
-// walks the first record
 DEV void lane_walk_begin(LaneWalk& w, const uint8_t* p0, uint32_t n, int32_t rc, uint32_t batch_ord,
-                         rpgpu_record_index* out, uint32_t cap, uint8_t* wave, uint32_t hs) {
+                         rpgpu_record_index* out, uint32_t cap) {
     w.p0 = p0;
     w.out = out;
     w.mis = (uint32_t)((uintptr_t)p0 & 15);
@@ -921,48 +982,44 @@ DEV void lane_walk_begin(LaneWalk& w, const uint8_t* p0, uint32_t n, int32_t rc,
     w.cap = cap;
     w.ord = batch_ord;
     w.h_base = w.mis & ~15u;
-    if (w.total) {
-        glds_region(p0, w.mis, n, w.h_base, wave + hs * kSlotBytes);
-        wait_vm();
-    }
 }
 
-// One record of a lane walk (w.total > 0) with H in slot hs: parse the record
-// at w.start, commit it to the index and move on.  Returns true when the
-// batch is finished (wr filled).  A typical record costs one load latency.
-DEV bool lane_record_step(LaneWalk& w, WalkResult& wr, uint8_t* wave, const uint8_t* lane, uint32_t hs) {
-    const uint32_t cs = 1u - hs;
+// the guessed end of the record at w.start from its length varint (H holds
+// 16 bytes from it), and C_k's grid offset: 48 bytes each side of it
+DEV uint32_t lane_c_base(const LaneWalk& w, const uint8_t* H) {
     const uint32_t n = w.n, mis = w.mis, start = w.start;
-    // the length varint at start (H holds 16 bytes from it)
     uint32_t guess = 0xFFFFFFFFu;
     if (start < n) {
-        const uint8_t* H = lane + hs * kSlotBytes;
         const uint32_t o = start + mis - w.h_base, k = o & ~3u, sh = o & 3u;
-        const uint32_t w0 = slot_dw(H, k), w1 = slot_dw(H, k + 4u), w2 = slot_dw(H, k + 8u), w3 = slot_dw(H, k + 12u);
+        const uint32_t w0 = region_dw(H, k), w1 = region_dw(H, k + 4u), w2 = region_dw(H, k + 8u),
+                       w3 = region_dw(H, k + 12u);
         uint32_t br;
         const int64_t len = varint12(__builtin_amdgcn_alignbyte(w1, w0, sh), __builtin_amdgcn_alignbyte(w2, w1, sh),
                                      __builtin_amdgcn_alignbyte(w3, w2, sh), n - start, br);
         if (len >= 0 && (uint64_t)len <= n) guess = start + br + (uint32_t)len;
     }
-    // C_k: the record's tail and the next record's head, 48 bytes each side
-    // of the guessed end
-    const uint32_t hb = w.h_base;
     const uint32_t e16 = (guess + mis + 15u) & ~15u;
-    const uint32_t cb = (guess != 0xFFFFFFFFu && e16 >= hb + kRegionBytes / 2u) ? e16 - kRegionBytes / 2u : hb;
-    glds_region(w.p0, mis, n, cb, wave + cs * kSlotBytes);
-    wait_vm();
+    return (guess != 0xFFFFFFFFu && e16 >= w.h_base + kRegionBytes / 2u) ? e16 - kRegionBytes / 2u : w.h_base;
+}
+
+// One record of a lane walk (w.total > 0), H and C_k in LDS: parse the record
+// at w.start, hand its index entry out (e, dst: null when there is none to
+// write) and move on.  Returns true when the batch is finished (wr filled);
+// otherwise `fresh` says whether the next record's head is outside C_k and
+// must be loaded before its step.
+DEV bool lane_record_step(LaneWalk& w, WalkResult& wr, uint8_t* H, const uint8_t* Ck, uint32_t cb, bool& fresh,
+                          rpgpu_record_index& e, rpgpu_record_index*& dst) {
+    const uint32_t n = w.n, mis = w.mis, start = w.start;
     LdsReader c;
     c.p0 = w.p0;
     c.mis = mis;
     c.n = n;
     c.pos = start;
-    c.lane = lane;
-    c.wave = wave;
-    c.a_base = hb;
-    c.a_slot = hs;
+    c.a = H;
+    c.t = Ck;
+    c.h = H;
+    c.a_base = w.h_base;
     c.t_base = cb;
-    c.t_slot = cs;
-    c.h_slot = hs;
     const Rec r = parse_fields(c);
     if (r.err) {
         wr.parsed = w.done;
@@ -970,8 +1027,8 @@ DEV bool lane_record_step(LaneWalk& w, WalkResult& wr, uint8_t* wave, const uint
         wr.trailing = 0;
         return true;
     }
+    // the index entry is written by the wave's cooperative store (coop_store)
     if (w.done < w.cap) {
-        rpgpu_record_index e;
         e.batch = w.ord;
         e.rec_pos = start;
         e.ts_delta = r.ts;
@@ -987,7 +1044,7 @@ DEV bool lane_record_step(LaneWalk& w, WalkResult& wr, uint8_t* wave, const uint
         e.attrs = (int8_t)r.attr;
         e.pad[0] = e.pad[1] = e.pad[2] = 0;
         e.reserved[0] = e.reserved[1] = 0;
-        w.out[w.done] = e;
+        dst = w.out + w.done;
     }
     w.done++;
     w.start = r.end;
@@ -997,15 +1054,10 @@ DEV bool lane_record_step(LaneWalk& w, WalkResult& wr, uint8_t* wave, const uint
         wr.trailing = n - w.start;
         return true;
     }
-    // the next record's head: in C_k when the guess held, else loaded into
-    // C_k's slot now
+    // the next record's head: in C_k when the guess held
     const uint32_t g = w.start + mis;
-    if (g - cb <= kRegionReach) w.h_base = cb;
-    else {
-        w.h_base = g & ~15u;
-        glds_region(w.p0, mis, n, w.h_base, wave + cs * kSlotBytes);
-        wait_vm();
-    }
+    fresh = g - cb > kRegionReach;
+    w.h_base = fresh ? (g & ~15u) : cb;
     return false;
 }
 
@@ -1031,7 +1083,7 @@ DEV WalkCtx walk_ctx(const DeviceJob& j) {
 // A lane-walked batch's descriptor, read by the walking lane itself: the
 // payload, its record count and index slots.  Returns false when the batch
 // is not lane-walked (incomplete, compressed or > kLaneWalkMax records).
-DEV bool lane_walk_setup(const WalkCtx& j, uint64_t b, LaneWalk& w, bool& idx_ok, uint8_t* wave, uint32_t hs) {
+DEV bool lane_walk_setup(const WalkCtx& j, uint64_t b, LaneWalk& w, bool& idx_ok) {
     const rpgpu_batch_result* R = &j.batches[b];
     const int32_t rc = R->record_count;
     if (!lane_walked(R->flags, (uint32_t)R->attrs & 7u, rc)) return false;
@@ -1040,7 +1092,7 @@ DEV bool lane_walk_setup(const WalkCtx& j, uint64_t b, LaneWalk& w, bool& idx_ok
     const uint64_t ib = j.slots[b], islots = j.slots[b + 1] - ib;
     idx_ok = ib + islots <= j.record_capacity;
     lane_walk_begin(w, j.data + S, n, rc, (uint32_t)b, idx_ok ? j.records + ib : nullptr,
-                    idx_ok ? (uint32_t)islots : 0u, wave, hs);
+                    idx_ok ? (uint32_t)islots : 0u);
     return true;
 }
 
@@ -1246,32 +1298,80 @@ __global__ __launch_bounds__(1024) void k_validate_decoded(DeviceJob j) {
     }
 }
 
+// k_walk: the record walk of stored (uncompressed) payloads with at most
+// kLaneWalkMax records, one LANE per batch, after k_validate has written the
+// CRC verdicts.  record_batch::for_each_record (model/record.h:616-627) is
+// sequential by nature: record k + 1 starts where record k's parse ended
+// (parse_fields: model/record_utils.cc:94-181).  Every lane of a wave takes
+// one step per turn of a wave-uniform loop (the cooperative region fetch
+// needs all 64 lanes):
+//   idle  -> take the lane's next batch (grid-stride); its first region is
+//            fetched this turn (state head)
+//   head  -> its region arrived: walk from the next turn
+//   walk  -> fetch C_k, parse record k, commit it
+// Batches with more records are walked by the wave-parallel walk inside
+// k_validate.
 __global__ __launch_bounds__(256) void k_walk(DeviceJob j) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    enum : uint32_t { kIdle = 0, kHead = 1, kWalk = 2, kFin = 3 };
     uint8_t* wave = lds + (threadIdx.x >> 6) * kWalkLdsWave;
-    const uint8_t* lane = wave + 16u * lane_v();
+    const uint32_t l = lane_v();
     const uint64_t nb_total = j.chunk_count[j.total_chunks];
     const uint64_t nb = nb_total < j.batch_capacity ? nb_total : j.batch_capacity;
     const bool wire = j.layout == RPGPU_LAYOUT_WIRE;
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     const WalkCtx c = walk_ctx(j);
-    for (uint64_t b = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; b < nb; b += stride) {
-        if (wire && !(j.batches[b].flags & RPGPU_F_CRC_OK)) continue;
-        LaneWalk w;
-        bool idx_ok;
-        // every lane of the while loop below is at the same step: the slot
-        // parity is uniform
-        if (!lane_walk_setup(c, b, w, idx_ok, wave, h_slot_of(0))) continue;
-        WalkResult wr;
-        if (w.total == 0) { wr.parsed = 0; wr.err = 0; wr.trailing = w.n; }
-        else for (uint32_t step = 0; !lane_record_step(w, wr, wave, lane, h_slot_of(step)); step++) {}
-        lane_walk_finish(c, b, wr, idx_ok, wire);
+    uint64_t b = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    uint32_t st = kIdle;
+    bool first = true, idx_ok = false;
+    LaneWalk w;
+    for (uint32_t step = 0;; step++) {
+        uint8_t* hslot = wave + (step & 1u) * kSlotBytes;   // H of this turn
+        uint8_t* cslot = wave + (~step & 1u) * kSlotBytes;  // fetched this turn
+        if (st == kIdle) {
+            if (!first) b += stride;
+            first = false;
+            if (b >= nb) st = kFin;
+            else if (!(wire && !(j.batches[b].flags & RPGPU_F_CRC_OK)) && lane_walk_setup(c, b, w, idx_ok)) {
+                if (w.total == 0) {
+                    WalkResult wr;
+                    wr.parsed = 0; wr.err = 0; wr.trailing = w.n;
+                    lane_walk_finish(c, b, wr, idx_ok, wire);
+                } else st = kHead;
+            }
+        }
+        uint32_t want = 0, rows = 0;
+        if (st == kWalk) want = lane_c_base(w, hslot + region_lane(l));
+        else if (st == kHead) want = w.h_base;
+        if (st == kWalk || st == kHead) rows = region_rows(w.n, w.mis, want);
+        if (__ballot(st != kFin) == 0) break;
+        if (kCoopLoad) coop_load(cslot, w.p0 - w.mis + want, rows);
+        else {
+            const uint8_t* g = w.p0 - w.mis + want;
+#pragma unroll
+            for (uint32_t r = 0; r < kRegionRows; r++)
+                if (r < rows)
+                    __builtin_amdgcn_global_load_lds((gbl_void*)(g + 16u * r), (lds_void*)(cslot + 1024u * r), 16, 0, 0);
+        }
+        wait_vm();
+        rpgpu_record_index e;
+        rpgpu_record_index* dst = nullptr;
+        if (st == kWalk) {
+            WalkResult wr;
+            bool fresh = false;
+            if (lane_record_step(w, wr, hslot + region_lane(l), cslot + region_lane(l), want, fresh, e, dst)) {
+                lane_walk_finish(c, b, wr, idx_ok, wire);
+                st = kIdle;
+            } else if (fresh) st = kHead;
+        } else if (st == kHead) st = kWalk;
+        // H is spent: its slot stages the entries
+        coop_store(hslot, e, dst);
     }
 }
 
 hipError_t launch_walk(const DeviceJob& j, hipStream_t s, uint32_t grid) {
     if (j.flags & RPGPU_JOB_PARSE)
-        hipLaunchKernelGGL(k_walk, dim3(grid), dim3(256), 4 * kWalkLdsWave, s, j);
+        hipLaunchKernelGGL(k_walk, dim3(grid), dim3(256), 4 * kWalkLdsWave, s, j);  // 48 KiB: 3 per CU
     return hipGetLastError();
 }
 
