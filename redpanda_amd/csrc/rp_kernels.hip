@@ -658,17 +658,14 @@ DEV bool batch_valid(uint32_t f, uint32_t job_flags, uint32_t layout) {
     return true;
 }
 
+// one lane per batch, one wave per bitmap word (a ballot of the lanes)
 __global__ __launch_bounds__(256) void k_finalize_bitmap(DeviceJob j) {
     const uint64_t nb_total = j.chunk_count[j.total_chunks];
     const uint64_t nb = nb_total < j.batch_capacity ? nb_total : j.batch_capacity;
-    const uint64_t w = (uint64_t)blockIdx.x * 256 + threadIdx.x;
-    if (w * 64 >= nb) return;
-    uint64_t word = 0;
-    for (uint32_t i = 0; i < 64; i++) {
-        const uint64_t b = w * 64 + i;
-        if (b < nb && batch_valid(j.batches[b].flags, j.flags, j.layout)) word |= 1ull << i;
-    }
-    j.bitmap[w] = word;
+    const uint64_t b = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if ((b & ~63ull) >= nb) return;  // whole wave past the end
+    const uint64_t word = __ballot(b < nb && batch_valid(j.batches[b].flags, j.flags, j.layout));
+    if ((threadIdx.x & 63) == 0) j.bitmap[b >> 6] = word;
 }
 
 __global__ void k_finalize_totals(DeviceJob j) {
@@ -750,7 +747,7 @@ hipError_t launch_finalize(const DeviceJob& j, hipStream_t s) {
     hipLaunchKernelGGL(k_finalize_segments, dim3(j.n_segments), dim3(256), 0, s, j);
     const uint64_t words = (j.batch_capacity + 63) / 64;
     if (j.bitmap) {
-        const uint32_t grid = (uint32_t)((words + 255) / 256);
+        const uint32_t grid = (uint32_t)((words * 64 + 255) / 256);
         hipLaunchKernelGGL(k_finalize_bitmap, dim3(grid ? grid : 1), dim3(256), 0, s, j);
     }
     hipLaunchKernelGGL(k_finalize_totals, dim3(1), dim3(64), 0, s, j);
