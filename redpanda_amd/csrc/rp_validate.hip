@@ -107,6 +107,23 @@ DEV uint32_t pick4(uint4 v, uint32_t k) {
     return (k & 2u) ? hi : lo;
 }
 
+// One 16-byte row of the payload stream, loaded non-temporal: every byte is
+// read once per launch, and with the default policy the window stream
+// displaced lines other waves were still waiting on (measured on C1:
+// k_validate 3.20 -> 2.96 ms; RPGPU_NT_WINDOW=0 restores the default policy
+// for A/B).
+#ifndef RPGPU_NT_WINDOW
+#define RPGPU_NT_WINDOW 1
+#endif
+DEV uint4 ld_stream(const uint8_t* p) {
+    if (RPGPU_NT_WINDOW) {
+        typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+        const v4u v = __builtin_nontemporal_load((const v4u*)p);
+        return make_uint4(v.x, v.y, v.z, v.w);
+    }
+    return *(const uint4*)p;
+}
+
 // A lane's share of the current window: dword k of row i in d[i] (rows
 // 0..15, 16 bytes at 1024 i + 16 l).
 struct Win {
@@ -145,7 +162,7 @@ DEV void load_window(const Stream& st, uint64_t r, Win& w) {
     for (int i = 0; i < 16; i++) {
         const int64_t q = a + 1024 * i;
         uint4 t = make_uint4(0u, 0u, 0u, 0u);
-        if (q + 16 > (int64_t)st.S && q < (int64_t)st.E16) t = *(const uint4*)(st.src + q);
+        if (q + 16 > (int64_t)st.S && q < (int64_t)st.E16) t = ld_stream(st.src + q);
         w.r[i] = t;
     }
 }
@@ -159,7 +176,7 @@ DEV void load_rows(const Stream& st, Win& w) {
     for (int i = I0; i < I1; i++) {
         const int64_t q = a + 1024 * i;
         uint4 t = make_uint4(0u, 0u, 0u, 0u);
-        if (q + 16 > (int64_t)st.S && q < (int64_t)st.E16) t = *(const uint4*)(st.src + q);
+        if (q + 16 > (int64_t)st.S && q < (int64_t)st.E16) t = ld_stream(st.src + q);
         w.r[i] = t;
     }
 }
@@ -823,6 +840,9 @@ constexpr uint32_t kWalkLdsWave = 2u * kSlotBytes;
 
 typedef __attribute__((address_space(3))) void lds_void;
 typedef const __attribute__((address_space(1))) void gbl_void;
+#ifndef RPGPU_WALK_AUX
+#define RPGPU_WALK_AUX 2  // region fetch non-temporal (measured: walk 1.36 -> 1.30 ms); 0 = default policy
+#endif
 
 DEV void wait_vm() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
@@ -863,7 +883,7 @@ DEV void coop_load(uint8_t* slot, const uint8_t* g, uint32_t rows) {
         const uint32_t wnr = (uint32_t)__builtin_amdgcn_ds_bpermute(src, nr);
         if (r < wnr) {
             const uint8_t* row = (const uint8_t*)(uintptr_t)(((uint64_t)whi << 32) | wlo) + 16u * r;
-            __builtin_amdgcn_global_load_lds((gbl_void*)row, (lds_void*)(slot + 1024u * m), 16, 0, 0);
+            __builtin_amdgcn_global_load_lds((gbl_void*)row, (lds_void*)(slot + 1024u * m), 16, 0, RPGPU_WALK_AUX);
         }
     }
 }
@@ -874,6 +894,9 @@ DEV void coop_load(uint8_t* slot, const uint8_t* g, uint32_t rows) {
 // as 4 lanes x 16 contiguous bytes, instead of one 16-byte piece of each of
 // 64 scattered entries per instruction (the index stores were a third of
 // the walk's time).
+#ifndef RPGPU_NT_INDEX
+#define RPGPU_NT_INDEX 0  // index entries stored non-temporal (A/B knob)
+#endif
 DEV void coop_store(uint8_t* stage, const rpgpu_record_index& e, rpgpu_record_index* dst) {
     static_assert(sizeof(rpgpu_record_index) == 64, "index entry is 4 x 16 bytes");
     const uint32_t l = lane_v();
@@ -895,7 +918,13 @@ DEV void coop_store(uint8_t* stage, const rpgpu_record_index& e, rpgpu_record_in
         const uint32_t whi = (uint32_t)__builtin_amdgcn_ds_bpermute(src_lane, hi);
         if (wlo | whi) {
             const uint4 v = *(const uint4*)(stage + 64u * w + 16u * qtr);
-            *(uint4*)((uint8_t*)(uintptr_t)(((uint64_t)whi << 32) | wlo) + 16u * qtr) = v;
+            uint4* d = (uint4*)((uint8_t*)(uintptr_t)(((uint64_t)whi << 32) | wlo) + 16u * qtr);
+            if (RPGPU_NT_INDEX) {
+                typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+                v4u x;
+                x.x = v.x; x.y = v.y; x.z = v.z; x.w = v.w;
+                __builtin_nontemporal_store(x, (v4u*)d);
+            } else *d = v;
         }
     }
 }
