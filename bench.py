@@ -108,6 +108,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--gather", choices=["bitmap", "index"], default="bitmap")
     ap.add_argument("--no-parse", action="store_true", help="CRC only (diagnostic; not the headline workload)")
+    ap.add_argument("--no-index", action="store_true", help="skip the segment-index rebuild measurement")
     ap.add_argument("--batch-bytes", type=int, default=BATCH_BYTES,
                     help="size_bytes per batch (diagnostic; the headline workload is 16 KiB)")
     args = ap.parse_args()
@@ -217,6 +218,30 @@ def main():
         except Exception:
             traffic = None
 
+    # segment sparse-index rebuild (segment_index::maybe_track over the
+    # recovered batches, §8(f) row 2): timed separately on its own stream,
+    # after the headline region; not part of `value`
+    index = None
+    if not args.no_index:
+        st = torch.cuda.Stream(device)
+        bases = [0] * len(parts)
+        torch.cuda.synchronize(device)
+        with torch.cuda.stream(st):
+            res = eng.segment_index(out, bases, stream=st)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            reps = 5
+            e0.record(st)
+            for _ in range(reps):
+                res = eng.segment_index(out, bases, stream=st)
+            e1.record(st)
+        st.synchronize()
+        ix = eng.index_to_host(*res, n_segments=len(parts))
+        n_entries = int(sum(int(r[0]["n_entries"]) for r in ix))
+        index = {"kernel": "k_segment_index", "ms": round(e0.elapsed_time(e1) / reps, 4), "step": abi.INDEX_DEFAULT_STEP,
+                 "entries": n_entries, "tracked": int(sum(int(r[0]["tracked"]) for r in ix)),
+                 "note": "one wave per segment (serial entry chain), includes 3 output allocations"}
+        del ix, res
+
     cpu = None
     if rank == 0 and not args.no_cpu_baseline and host_first is not None:
         cpu = cpu_baseline(host_first)
@@ -247,6 +272,7 @@ def main():
                 "parity": {"all_batches_valid": all_ok, "bitmap_all_ones": bm_ok},
                 "stage_ms": {k: round(v, 4) for k, v in tm.items()},
                 "hbm_fraction_whole_pipeline": round(value / world / HBM_PEAK_GBS, 4),
+                "segment_index": index,
             },
             "roofline": {
                 "bound": "hbm",

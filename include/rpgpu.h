@@ -280,6 +280,43 @@ int rpgpu_last_timings(rpgpu_ctx* ctx, float* ms, int n);
 int rpgpu_set_timing(rpgpu_ctx* ctx, int enable);
 
 /* ------------------------------------------------------------------------ */
+/* storage::segment_index rebuild during recovery                            */
+/* (checksumming_consumer::consume_batch_end -> segment_index::maybe_track,  */
+/* storage/log_replayer.cc:62-74, storage/segment_index.cc:58-72 ->          */
+/* index_state::maybe_index, storage/index_state.cc:48-95).                  */
+/* ------------------------------------------------------------------------ */
+
+/* segment_index::default_data_buffer_step (storage/segment_index.h:49) */
+#define RPGPU_INDEX_DEFAULT_STEP 32768u
+
+/* Per segment: the index_state header fields (storage/index_state.h:37-65)
+ * after replaying maybe_track over the segment's crc-good batch prefix
+ * [0, summary.first_bad).  64 bytes. */
+typedef struct rpgpu_index_state {
+    int64_t base_offset;          /* IN: the segment's base offset (index_state.base_offset, kept by reset()) */
+    int64_t max_offset;           /* last tracked batch's last_offset */
+    int64_t base_timestamp;       /* first tracked batch's first_timestamp */
+    int64_t max_timestamp;        /* max over tracked batches of max(first_timestamp, max_timestamp) */
+    uint64_t first_entry;         /* entries of this segment live at [first_entry, first_entry + n_entries)
+                                     of the entry arrays (== summary.first_batch) */
+    uint64_t n_entries;           /* relative_offset_index.size() */
+    int64_t assert_batch;         /* -1, or the segment ordinal of the first tracked batch whose
+                                     base_offset < base_offset: the reference vasserts (aborts) there,
+                                     so tracking stops before it */
+    uint64_t tracked;             /* batches replayed through maybe_track */
+} rpgpu_index_state;
+
+/* Device pointers.  d_batches/d_summaries are the outputs of a completed
+ * disk-layout rpgpu_submit (same stream, or synchronised).  d_states has
+ * n_segments entries with base_offset filled in by the caller.  The three
+ * entry arrays (relative_offset_index, relative_time_index, position_index)
+ * need batch_capacity slots each.  step = segment_index::_step. */
+int rpgpu_segment_index(rpgpu_ctx* ctx, const rpgpu_batch_result* d_batches, uint64_t batch_capacity,
+                        const rpgpu_segment_summary* d_summaries, uint32_t n_segments, uint64_t step,
+                        rpgpu_index_state* d_states, uint32_t* d_rel_offset, uint32_t* d_rel_time,
+                        uint64_t* d_position, void* stream);
+
+/* ------------------------------------------------------------------------ */
 /* compression::compressor::uncompress (compression/compression.h:21-24)     */
 /* ------------------------------------------------------------------------ */
 

@@ -33,6 +33,7 @@
 #include <cstdint>
 #include <cstring>
 #include <memory>
+#include <algorithm>
 #include <optional>
 #include <ostream>
 #include <stdexcept>
@@ -343,10 +344,20 @@ namespace detail {
 struct segment_scan {
     std::vector<rpgpu_batch_result> batches;
     rpgpu_segment_summary summary{};
+    // filled when an index rebuild was requested (rpgpu_segment_index)
+    rpgpu_index_state index{};
+    std::vector<uint32_t> rel_offset, rel_time;
+    std::vector<uint64_t> position;
+};
+
+struct index_request {
+    int64_t base_offset;  // the segment's base offset (segment_index / index_state.base_offset)
+    uint64_t step;        // segment_index::_step
 };
 
 inline segment_scan scan_segment(rpgpu::engine& e, const uint8_t* seg, size_t len,
-                                 uint32_t layout = RPGPU_LAYOUT_DISK, uint32_t flags = RPGPU_JOB_CRC) {
+                                 uint32_t layout = RPGPU_LAYOUT_DISK, uint32_t flags = RPGPU_JOB_CRC,
+                                 const index_request* want_index = nullptr) {
     segment_scan out;
     const size_t cap = len / RPGPU_HEADER_SIZE + 2;
     const size_t rcap = (flags & RPGPU_JOB_PARSE) ? len / 4 + 64 : 1;
@@ -372,6 +383,33 @@ inline segment_scan scan_segment(rpgpu::engine& e, const uint8_t* seg, size_t le
     j.d_summaries = (rpgpu_segment_summary*)d_s.get();
     j.d_totals = (rpgpu_job_totals*)d_t.get();
     e.check(rpgpu_submit(e.ctx(), &j, nullptr), "rpgpu_submit");
+    if (want_index) {
+        // segment_index::maybe_track over the crc-good prefix, on the same stream
+        rpgpu::dev_buffer d_st(e, sizeof(rpgpu_index_state)), d_ro(e, cap * 4), d_rt(e, cap * 4), d_ps(e, cap * 8);
+        out.index = rpgpu_index_state{};
+        out.index.base_offset = want_index->base_offset;
+        e.check(rpgpu_memcpy_h2d(e.ctx(), d_st.get(), &out.index, sizeof out.index, nullptr), "rpgpu_memcpy_h2d");
+        e.check(rpgpu_segment_index(e.ctx(), (const rpgpu_batch_result*)d_b.get(), cap,
+                                    (const rpgpu_segment_summary*)d_s.get(), 1, want_index->step,
+                                    (rpgpu_index_state*)d_st.get(), (uint32_t*)d_ro.get(), (uint32_t*)d_rt.get(),
+                                    (uint64_t*)d_ps.get(), nullptr),
+                "rpgpu_segment_index");
+        e.check(rpgpu_memcpy_d2h(e.ctx(), &out.index, d_st.get(), sizeof out.index, nullptr), "rpgpu_memcpy_d2h");
+        e.check(rpgpu_sync(e.ctx(), nullptr), "rpgpu_sync");
+        const size_t n = (size_t)out.index.n_entries;
+        out.rel_offset.resize(n);
+        out.rel_time.resize(n);
+        out.position.resize(n);
+        if (n) {
+            e.check(rpgpu_memcpy_d2h(e.ctx(), out.rel_offset.data(), (uint32_t*)d_ro.get() + out.index.first_entry,
+                                     n * 4, nullptr), "rpgpu_memcpy_d2h");
+            e.check(rpgpu_memcpy_d2h(e.ctx(), out.rel_time.data(), (uint32_t*)d_rt.get() + out.index.first_entry,
+                                     n * 4, nullptr), "rpgpu_memcpy_d2h");
+            e.check(rpgpu_memcpy_d2h(e.ctx(), out.position.data(), (uint64_t*)d_ps.get() + out.index.first_entry,
+                                     n * 8, nullptr), "rpgpu_memcpy_d2h");
+        }
+        e.check(rpgpu_sync(e.ctx(), nullptr), "rpgpu_sync");
+    }
     rpgpu_job_totals t{};
     e.check(rpgpu_memcpy_d2h(e.ctx(), &t, d_t.get(), sizeof t, nullptr), "rpgpu_memcpy_d2h");
     e.check(rpgpu_memcpy_d2h(e.ctx(), &out.summary, d_s.get(), sizeof out.summary, nullptr), "rpgpu_memcpy_d2h");
@@ -499,6 +537,60 @@ private:
     size_t _physical_base_offset{0};
 };
 
+// storage/index_state.h:37-75: the sparse offset/time -> file position index
+// of one segment, as recovery rebuilds it.
+struct index_state {
+    int64_t base_offset{0};
+    int64_t max_offset{0};
+    int64_t base_timestamp{0};
+    int64_t max_timestamp{0};
+    std::vector<uint32_t> relative_offset_index;
+    std::vector<uint32_t> relative_time_index;
+    std::vector<uint64_t> position_index;
+    bool empty() const { return relative_offset_index.empty(); }
+};
+
+// storage/segment_index.h:30-100 (the lookups over a rebuilt index_state)
+class segment_index {
+public:
+    static constexpr size_t default_data_buffer_step = RPGPU_INDEX_DEFAULT_STEP;  // segment_index.h:49
+    struct entry {
+        int64_t offset;
+        int64_t timestamp;
+        size_t filepos;
+    };
+    explicit segment_index(index_state st) : _state(std::move(st)) {}
+    const index_state& state() const { return _state; }
+
+    // segment_index::find_nearest(model::offset) (storage/segment_index.cc:89-107):
+    // the last entry whose offset is <= o
+    std::optional<entry> find_nearest(int64_t o) const {
+        if (o < _state.base_offset || _state.empty()) return std::nullopt;
+        const uint32_t i = (uint32_t)(o - _state.base_offset);
+        const auto& ro = _state.relative_offset_index;
+        auto it = std::upper_bound(ro.begin(), ro.end(), i);
+        if (it == ro.begin()) return std::nullopt;
+        return translate(size_t(std::distance(ro.begin(), it)) - 1);
+    }
+    // segment_index::find_nearest(model::timestamp) (storage/segment_index.cc:74-87):
+    // the first entry whose relative time is >= t
+    std::optional<entry> find_nearest_timestamp(int64_t t) const {
+        if (t < _state.base_timestamp || _state.empty()) return std::nullopt;
+        const uint32_t i = (uint32_t)(t - _state.base_timestamp);
+        const auto& rt = _state.relative_time_index;
+        auto it = std::lower_bound(rt.begin(), rt.end(), i);
+        if (it == rt.end()) return std::nullopt;
+        return translate(size_t(std::distance(rt.begin(), it)));
+    }
+
+private:
+    entry translate(size_t k) const {
+        return entry{_state.base_offset + (int64_t)_state.relative_offset_index[k],
+                     _state.base_timestamp + (int64_t)_state.relative_time_index[k], (size_t)_state.position_index[k]};
+    }
+    index_state _state;
+};
+
 // storage/log_replayer.h:159-165 + log_replayer.cc:95-114: recover a segment
 // from file position 0; the checkpoint is the last batch whose crc matched
 // before the first one that did not.  Computed on the GPU in one submit.
@@ -511,6 +603,32 @@ public:
 
     static checkpoint recover(const uint8_t* segment, size_t len, rpgpu::engine& e = rpgpu::engine::local()) {
         const detail::segment_scan sc = detail::scan_segment(e, segment, len);
+        checkpoint c;
+        if (sc.summary.has_checkpoint) {
+            c.last_offset = sc.summary.ckpt_last_offset;
+            c.truncate_file_pos = (size_t)sc.summary.ckpt_truncate_pos;
+        }
+        return c;
+    }
+
+    // Recovery that also rebuilds the segment's sparse index the way
+    // checksumming_consumer does (log_replayer.cc:62-74 -> segment_index::maybe_track).
+    // Where the reference vasserts (a batch below the index base offset) this
+    // throws std::runtime_error.
+    static checkpoint recover(const uint8_t* segment, size_t len, int64_t base_offset, index_state& idx,
+                              size_t step = segment_index::default_data_buffer_step,
+                              rpgpu::engine& e = rpgpu::engine::local()) {
+        const detail::index_request rq{base_offset, step};
+        detail::segment_scan sc = detail::scan_segment(e, segment, len, RPGPU_LAYOUT_DISK, RPGPU_JOB_CRC, &rq);
+        if (sc.index.assert_batch == -2) throw std::runtime_error("log_replayer: batch capacity overflow");
+        if (sc.index.assert_batch >= 0) throw std::runtime_error("index_state::maybe_index: offset below base_offset");
+        idx.base_offset = sc.index.base_offset;
+        idx.max_offset = sc.index.max_offset;
+        idx.base_timestamp = sc.index.base_timestamp;
+        idx.max_timestamp = sc.index.max_timestamp;
+        idx.relative_offset_index = std::move(sc.rel_offset);
+        idx.relative_time_index = std::move(sc.rel_time);
+        idx.position_index = std::move(sc.position);
         checkpoint c;
         if (sc.summary.has_checkpoint) {
             c.last_offset = sc.summary.ckpt_last_offset;

@@ -75,6 +75,9 @@ def lib():
         L.rpo_baseline_validate.restype = C.c_int64
         L.rpo_baseline_validate.argtypes = [C.c_void_p, C.c_void_p, C.c_uint32, C.c_int, C.c_int,
                                             C.POINTER(C.c_double), C.POINTER(C.c_uint64)]
+        L.rpo_segment_index.restype = C.c_int
+        L.rpo_segment_index.argtypes = [C.c_void_p, C.c_uint64, C.c_void_p, C.c_uint32, C.c_uint64,
+                                        C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]
         _lib = L
     return _lib
 
@@ -253,3 +256,32 @@ def baseline_validate(data: np.ndarray, seg_offsets, threads: int, hw: bool = Tr
                                      offs.size - 1, threads, 1 if hw else 0, C.byref(secs),
                                      C.byref(nbytes))
     return nb, secs.value, nbytes.value
+
+
+def segment_index(batches: np.ndarray, summaries: np.ndarray, base_offsets, step: int = abi.INDEX_DEFAULT_STEP,
+                  batch_cap: int = None):
+    """Oracle: segment_index::maybe_track replayed over each segment's
+    crc-good prefix (storage/log_replayer.cc:62-74, storage/segment_index.cc:58-72,
+    storage/index_state.cc:48-95).  Same per-segment output as
+    Engine.index_to_host: [(index_state row, relative_offset, relative_time, position)]."""
+    batches = np.ascontiguousarray(batches, dtype=abi.BATCH_RESULT)
+    summaries = np.ascontiguousarray(summaries, dtype=abi.SEGMENT_SUMMARY)
+    nseg = summaries.size
+    cap = batches.size if batch_cap is None else batch_cap
+    bb = np.zeros(max(cap, 1), dtype=abi.BATCH_RESULT)
+    bb[: min(cap, batches.size)] = batches[:cap]
+    st = np.zeros(max(nseg, 1), dtype=abi.INDEX_STATE)
+    st["base_offset"][:nseg] = np.asarray(base_offsets, dtype=np.int64)
+    ro = np.zeros(max(cap, 1), dtype=np.uint32)
+    rt = np.zeros(max(cap, 1), dtype=np.uint32)
+    ps = np.zeros(max(cap, 1), dtype=np.uint64)
+    rc = lib().rpo_segment_index(bb.ctypes.data_as(C.c_void_p), cap, summaries.ctypes.data_as(C.c_void_p), nseg,
+                                 step, st.ctypes.data_as(C.c_void_p), ro.ctypes.data_as(C.c_void_p),
+                                 rt.ctypes.data_as(C.c_void_p), ps.ctypes.data_as(C.c_void_p))
+    if rc != 0:
+        raise RuntimeError(f"rpo_segment_index: {rc}")
+    out = []
+    for s in st[:nseg]:
+        a, n = int(s["first_entry"]), int(s["n_entries"])
+        out.append((s, ro[a:a + n].copy(), rt[a:a + n].copy(), ps[a:a + n].copy()))
+    return out

@@ -1228,3 +1228,71 @@ int64_t rpo_baseline_validate(const uint8_t* data, const uint64_t* seg_offsets,
     free(th);
     return nb;
 }
+
+/* ------------------------------------------------------------------------ */
+/* Segment index rebuild (recovery).                                         */
+/* ------------------------------------------------------------------------ */
+
+/* index_state::maybe_index (storage/index_state.cc:48-95) for one batch;
+ * `acc` is segment_index::_acc after `_acc += hdr.size_bytes`
+ * (storage/segment_index.cc:60-61).  Returns 1 when the batch was indexed. */
+static int rpo_maybe_index(rpgpu_index_state* st, uint64_t acc, uint64_t step, uint64_t filepos,
+                           const rpgpu_batch_result* b, uint32_t* rel_offset, uint32_t* rel_time,
+                           uint64_t* position) {
+    const int64_t last_offset = (int64_t)((uint64_t)b->base_offset + (uint64_t)(int64_t)b->last_offset_delta);
+    int retval = 0;
+    if (st->n_entries == 0) { /* empty(): index_state.cc:66-70 */
+        st->base_timestamp = b->first_timestamp;
+        st->max_timestamp = b->first_timestamp;
+        retval = 1;
+    }
+    st->max_offset = last_offset; /* :73 */
+    /* last_timestamp = max(first, last) (:77); max_timestamp = max(...) (:78) */
+    const int64_t last_ts = b->max_timestamp > b->first_timestamp ? b->max_timestamp : b->first_timestamp;
+    if (last_ts > st->max_timestamp) st->max_timestamp = last_ts;
+    if (acc >= step || retval) { /* :80-87, add_entry (index_state.h:70-74) */
+        const uint64_t k = st->first_entry + st->n_entries;
+        rel_offset[k] = (uint32_t)((uint64_t)b->base_offset - (uint64_t)st->base_offset);
+        rel_time[k] = (uint32_t)((uint64_t)last_ts - (uint64_t)st->base_timestamp);
+        position[k] = filepos;
+        st->n_entries++;
+        retval = 1;
+    }
+    return retval;
+}
+
+int rpo_segment_index(const rpgpu_batch_result* batches, uint64_t batch_cap,
+                      const rpgpu_segment_summary* summaries, uint32_t n_segments, uint64_t step,
+                      rpgpu_index_state* states, uint32_t* rel_offset, uint32_t* rel_time,
+                      uint64_t* position) {
+    for (uint32_t s = 0; s < n_segments; s++) {
+        const rpgpu_segment_summary* sm = &summaries[s];
+        rpgpu_index_state* st = &states[s];
+        /* checksumming_consumer's constructor: _seg->index().reset() keeps
+         * only base_offset (storage/segment_index.cc:44-49) */
+        const int64_t base = st->base_offset;
+        memset(st, 0, sizeof(*st));
+        st->base_offset = base;
+        st->first_entry = sm->first_batch;
+        st->assert_batch = -1;
+        uint64_t n = sm->first_bad; /* consume_batch_end tracks only crc-good batches, stops at the first bad */
+        const uint64_t avail = sm->first_batch < batch_cap ? batch_cap - sm->first_batch : 0;
+        if (n > avail) { /* the job overflowed its batch capacity */
+            n = avail;
+            st->assert_batch = -2;
+        }
+        uint64_t acc = 0; /* segment_index::_acc */
+        for (uint64_t i = 0; i < n; i++) {
+            const rpgpu_batch_result* b = &batches[sm->first_batch + i];
+            if (b->base_offset < st->base_offset) { /* vassert (index_state.cc:57-63) */
+                st->assert_batch = (int64_t)i;
+                break;
+            }
+            acc += (uint64_t)(int64_t)b->size_bytes; /* _acc += hdr.size_bytes */
+            /* physical_base_offset = end - size_bytes = the header's position (log_replayer.cc:68-70) */
+            if (rpo_maybe_index(st, acc, step, b->file_pos, b, rel_offset, rel_time, position)) acc = 0;
+            st->tracked++;
+        }
+    }
+    return 0;
+}

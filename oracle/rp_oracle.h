@@ -144,6 +144,17 @@ int64_t rpo_baseline_validate(const uint8_t* data, const uint64_t* seg_offsets,
                               uint32_t n_segments, int threads, int use_hw_crc,
                               double* seconds, uint64_t* bytes);
 
+
+/* --- segment index rebuild: checksumming_consumer::consume_batch_end
+ *     (storage/log_replayer.cc:62-74) -> segment_index::maybe_track
+ *     (storage/segment_index.cc:58-72) -> index_state::maybe_index
+ *     (storage/index_state.cc:48-95), replayed over each segment's crc-good
+ *     prefix of a completed job.  Same contract as rpgpu_segment_index. */
+int rpo_segment_index(const rpgpu_batch_result* batches, uint64_t batch_cap,
+                      const rpgpu_segment_summary* summaries, uint32_t n_segments, uint64_t step,
+                      rpgpu_index_state* states, uint32_t* rel_offset, uint32_t* rel_time,
+                      uint64_t* position);
+
 #ifdef __cplusplus
 }
 #endif

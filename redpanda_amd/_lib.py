@@ -94,6 +94,7 @@ def load():
         "rpgpu_set_timing": (i32, [vp, i32]),
         "rpgpu_uncompress": (i32, [vp, i32, vp, sz, vp, sz, C.POINTER(sz)]),
         "rpgpu_validate_host": (i32, [vp, vp]),
+        "rpgpu_segment_index": (i32, [vp, vp, u64, vp, u32, u64, vp, vp, vp, vp, vp]),
         "rpgpu_gen_segment": (C.c_int64, [C.POINTER(GenSpecC), u32, vp]),
     }
     for name, (res, args) in sig.items():

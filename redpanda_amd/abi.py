@@ -74,6 +74,15 @@ SEGMENT_SUMMARY = np.dtype([
 ])
 assert SEGMENT_SUMMARY.itemsize == 88
 
+# rpgpu_index_state (include/rpgpu.h): index_state header after recovery
+INDEX_STATE = np.dtype([
+    ("base_offset", "<i8"), ("max_offset", "<i8"), ("base_timestamp", "<i8"),
+    ("max_timestamp", "<i8"), ("first_entry", "<u8"), ("n_entries", "<u8"),
+    ("assert_batch", "<i8"), ("tracked", "<u8"),
+])
+assert INDEX_STATE.itemsize == 64
+INDEX_DEFAULT_STEP = 32768  # segment_index::default_data_buffer_step (storage/segment_index.h:49)
+
 JOB_TOTALS = np.dtype([
     ("n_batches", "<u8"), ("n_records", "<u8"), ("decoded_bytes", "<u8"),
     ("batch_capacity_needed", "<u8"), ("record_capacity_needed", "<u8"),

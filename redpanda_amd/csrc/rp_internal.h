@@ -144,4 +144,9 @@ hipError_t scan_exclusive_u64(uint64_t* data, uint64_t n, void* temp, size_t tem
 hipError_t scan_exclusive_u64_devn(uint64_t* data, const uint64_t* d_n, uint64_t n_cap, void* temp, hipStream_t s);
 size_t scan_temp_bytes(uint64_t n);
 
+// rp_index.hip: segment index rebuild (rpgpu_segment_index), one wave per segment
+hipError_t launch_segment_index(const rpgpu_batch_result* batches, uint64_t cap, const rpgpu_segment_summary* sums,
+                                uint32_t n_segments, uint64_t step, rpgpu_index_state* states, uint32_t* rel_offset,
+                                uint32_t* rel_time, uint64_t* position, hipStream_t s);
+
 }  // namespace rp

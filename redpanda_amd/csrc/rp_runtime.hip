@@ -465,6 +465,24 @@ extern "C" {
 // one payload: staged to the device, decoded by one wave (rp_codec.hip).
 // The reference throws std::runtime_error on empty input, on `none` and on
 // any decode failure -> RPGPU_E_CODEC; gzip/zstd are not decoded here.
+// segment_index rebuild over a completed job's results (storage/log_replayer.cc:62-74,
+// storage/segment_index.cc:58-72, storage/index_state.cc:48-95); kernel in rp_index.hip
+int rpgpu_segment_index(rpgpu_ctx* c, const rpgpu_batch_result* d_batches, uint64_t batch_capacity,
+                        const rpgpu_segment_summary* d_summaries, uint32_t n_segments, uint64_t step,
+                        rpgpu_index_state* d_states, uint32_t* d_rel_offset, uint32_t* d_rel_time,
+                        uint64_t* d_position, void* stream) {
+    if (!c) return RPGPU_E_INVALID;
+    if (n_segments == 0) return RPGPU_OK;
+    if (!d_batches || !d_summaries || !d_states || !d_rel_offset || !d_rel_time || !d_position)
+        return fail(c, RPGPU_E_INVALID, "rpgpu_segment_index: missing argument");
+    if (step >= (1ull << 62)) return fail(c, RPGPU_E_INVALID, "rpgpu_segment_index: step out of range");
+    if (n_segments > 0x7FFFFFFFu) return fail(c, RPGPU_E_INVALID, "rpgpu_segment_index: too many segments");
+    hipSetDevice(c->device);
+    HIPCHK(c, launch_segment_index(d_batches, batch_capacity, d_summaries, n_segments, step, d_states, d_rel_offset,
+                                   d_rel_time, d_position, pick(c, stream)));
+    return RPGPU_OK;
+}
+
 int rpgpu_uncompress(rpgpu_ctx* c, int codec, const void* in, size_t n, void* out, size_t cap, size_t* out_len) {
     if (!c || (!in && n) || !out_len) return RPGPU_E_INVALID;
     *out_len = 0;

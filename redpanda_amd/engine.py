@@ -138,6 +138,48 @@ class Engine:
         check(self.L.rpgpu_submit(self.ctx, C.byref(job), C.c_void_p(s.cuda_stream)), self.ctx, "rpgpu_submit")
         return out
 
+    def segment_index(self, out: DeviceResult, base_offsets, step: int = abi.INDEX_DEFAULT_STEP, stream=None):
+        """Rebuild each segment's sparse index (segment_index::maybe_track over
+        the crc-good prefix, storage/log_replayer.cc:62-74) from a completed
+        disk-layout job `out`, on the device.  Returns device tensors
+        (states, relative_offset, relative_time, position); segment s's
+        entries are [first_entry, first_entry + n_entries) of each array."""
+        torch = _torch()
+        dev = out.batches.device
+        nseg = out.n_segments
+        cap = out.batches.numel() // abi.BATCH_RESULT.itemsize
+        st = np.zeros(max(nseg, 1), dtype=abi.INDEX_STATE)
+        st["base_offset"][:nseg] = np.asarray(base_offsets, dtype=np.int64)
+        states = torch.from_numpy(st.view(np.uint8).copy()).to(dev)
+        rel_off = torch.zeros(max(cap, 1), dtype=torch.int32, device=dev)
+        rel_time = torch.zeros(max(cap, 1), dtype=torch.int32, device=dev)
+        pos = torch.zeros(max(cap, 1), dtype=torch.int64, device=dev)
+        s = stream if stream is not None else torch.cuda.current_stream(dev)
+        if s.cuda_stream == 0:
+            # torch's legacy default stream: the library then launches on the
+            # context's non-blocking stream, which does not order after it
+            torch.cuda.synchronize(dev)
+        check(self.L.rpgpu_segment_index(self.ctx, C.c_void_p(out.batches.data_ptr()), cap,
+                                         C.c_void_p(out.summaries.data_ptr()), nseg, step,
+                                         C.c_void_p(states.data_ptr()), C.c_void_p(rel_off.data_ptr()),
+                                         C.c_void_p(rel_time.data_ptr()), C.c_void_p(pos.data_ptr()),
+                                         C.c_void_p(s.cuda_stream)), self.ctx, "rpgpu_segment_index")
+        return states, rel_off, rel_time, pos
+
+    @staticmethod
+    def index_to_host(states, rel_off, rel_time, pos, n_segments: int):
+        """Per segment: (index_state row, relative_offset, relative_time, position) numpy."""
+        _torch().cuda.synchronize(states.device)
+        st = np.frombuffer(states.cpu().numpy().tobytes(), dtype=abi.INDEX_STATE)[:n_segments]
+        ro = rel_off.cpu().numpy().view(np.uint32)
+        rt = rel_time.cpu().numpy().view(np.uint32)
+        ps = pos.cpu().numpy().view(np.uint64)
+        out = []
+        for s in st:
+            a, n = int(s["first_entry"]), int(s["n_entries"])
+            out.append((s, ro[a:a + n].copy(), rt[a:a + n].copy(), ps[a:a + n].copy()))
+        return out
+
     def uncompress(self, codec: int, payload: bytes, cap: int = None):
         """compression::compressor::uncompress for one payload on the device.
         Returns the decoded bytes; raises RpgpuError (RPGPU_E_CODEC) where the

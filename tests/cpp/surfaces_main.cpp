@@ -6,6 +6,8 @@
 //   surfaces_test cpu <segment>                 host walk: model:: crc helpers
 //   surfaces_test parse <segment> M R S E       continuous_batch_parser replay
 //   surfaces_test recover <segment>             log_replayer checkpoint
+//   surfaces_test index <segment> <base> <q>... log_replayer recovery + segment_index rebuild,
+//                                               find_nearest(offset) for each q
 //   surfaces_test uncompress <codec> <in> <out> compressor::uncompress
 //   surfaces_test wire <record_set>             kafka::batch_reader
 #include <cstdio>
@@ -172,6 +174,31 @@ int main(int argc, char** argv) {
             const storage::log_replayer::checkpoint c = storage::log_replayer::recover(seg.data(), seg.size());
             if (c.last_offset) std::printf("CKPT 1 %lld %zu\n", (long long)*c.last_offset, *c.truncate_file_pos);
             else std::printf("CKPT 0\n");
+            return 0;
+        }
+        if (mode == "index") {
+            const std::vector<uint8_t> seg = slurp(argv[2]);
+            storage::index_state st;
+            try {
+                const storage::log_replayer::checkpoint c =
+                  storage::log_replayer::recover(seg.data(), seg.size(), std::atoll(argv[3]), st);
+                if (c.last_offset) std::printf("CKPT 1 %lld %zu\n", (long long)*c.last_offset, *c.truncate_file_pos);
+                else std::printf("CKPT 0\n");
+            } catch (const std::runtime_error& e) {
+                std::printf("VASSERT\n");
+                return 0;
+            }
+            std::printf("STATE %lld %lld %lld %lld %zu\n", (long long)st.base_offset, (long long)st.max_offset,
+                        (long long)st.base_timestamp, (long long)st.max_timestamp, st.relative_offset_index.size());
+            for (size_t k = 0; k < st.relative_offset_index.size(); k++)
+                std::printf("E %u %u %llu\n", st.relative_offset_index[k], st.relative_time_index[k],
+                            (unsigned long long)st.position_index[k]);
+            const storage::segment_index idx(std::move(st));
+            for (int a = 4; a < argc; a++) {
+                const auto e = idx.find_nearest(std::atoll(argv[a]));
+                if (e) std::printf("NEAR %lld %zu\n", (long long)e->offset, e->filepos);
+                else std::printf("NEAR none\n");
+            }
             return 0;
         }
         if (mode == "wire") {

@@ -235,6 +235,33 @@ def test_log_replayer_checkpoint(driver, rplib, oracle, engine, tmp_path):
 
 
 @pytest.mark.gpu
+def test_log_replayer_segment_index(driver, rplib, oracle, engine, tmp_path):
+    """log_replayer::recover(.., index_state&) rebuilds the sparse index like
+    checksumming_consumer -> segment_index::maybe_track; checked against the
+    oracle's restatement over the oracle's own job results."""
+    for name, data in segment_cases(rplib):
+        arr = np.frombuffer(data, dtype=np.uint8)
+        job = oracle.run_job(arr, np.array([0, len(data)], np.uint64), abi.JOB_CRC)
+        base = int(job.batches["base_offset"][0]) if len(job.batches) else 0
+        (st, ro, rt, ps), = oracle.segment_index(job.batches, job.summaries, [base])
+        qs = [base - 1, base, base + 7, int(st["max_offset"]) + 5]
+        lines = run(driver, "index", write(tmp_path, name, data), base, *qs)
+        sm = job.summaries[0]
+        want = [f"CKPT 1 {int(sm['ckpt_last_offset'])} {int(sm['ckpt_truncate_pos'])}" if sm["has_checkpoint"]
+                else "CKPT 0"]
+        want.append(f"STATE {base} {int(st['max_offset'])} {int(st['base_timestamp'])} {int(st['max_timestamp'])} "
+                    f"{len(ro)}")
+        want += [f"E {int(a)} {int(b)} {int(c)}" for a, b, c in zip(ro, rt, ps)]
+        for q in qs:
+            if q < base or len(ro) == 0:
+                want.append("NEAR none")
+                continue
+            i = int(np.searchsorted(ro, np.uint32(q - base), side="right")) - 1
+            want.append("NEAR none" if i < 0 else f"NEAR {base + int(ro[i])} {int(ps[i])}")
+        assert lines == want, name
+
+
+@pytest.mark.gpu
 def test_compressor_uncompress(driver, oracle, engine, tmp_path):
     import json
     man = json.load(open(os.path.join(G, "manifest.json")))
