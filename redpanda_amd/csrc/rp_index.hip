@@ -12,9 +12,11 @@
 // wave per segment and walks the segment's batch results 64 at a time:
 //   * each lane holds one batch; an inclusive wave scan gives P (bytes of the
 //     tile up to and including the lane);
-//   * with `a` = bytes carried since the last entry and P_t = P at the last
-//     entry in this tile, the next entry is the first lane l > t with
-//     a + P_l - P_t >= step, i.e. one ballot + find-first-set per entry;
+//   * every lane finds its successor entry next(l) = the first lane j > l
+//     with P_j >= P_l + step by binary lifting over the lanes (sizes are
+//     non-negative on a parser chain, so P is monotone); the tile's first
+//     entry is the first lane where the carried bytes reach `step`, and the
+//     chain from it is one readlane per entry;
 //   * entry lanes write {relative offset, relative time, position} at their
 //     rank among the segment's entries.
 // The tile loads (the first 64 bytes of each 128-byte rpgpu_batch_result)
@@ -58,6 +60,12 @@ DEV int64_t shfl_xor_i64(int64_t v, int m) {
     return (int64_t)u64of(lo, hi);
 }
 
+DEV uint64_t shfl64(uint64_t v, int src) {
+    const uint32_t lo = __shfl((uint32_t)v, src, 64);
+    const uint32_t hi = __shfl((uint32_t)(v >> 32), src, 64);
+    return u64of(lo, hi);
+}
+
 DEV uint64_t rl64(uint64_t v, int l) { return u64of(rl((uint32_t)v, l), rl((uint32_t)(v >> 32), l)); }
 
 }  // namespace
@@ -67,9 +75,9 @@ struct IdxWalk {
     uint64_t a;          // segment_index::_acc (bytes since the last entry)
     uint64_t n_entries;
     uint64_t tracked;
-    int64_t base_ts, max_ts, max_off;
+    int64_t base_ts, max_off;
+    int64_t lane_max_ts;  // per-lane running max of max(first, last) timestamps, reduced once at the end
     int64_t assert_batch;
-    bool have_max;
 };
 
 // One tile of up to 64 tracked batches (lane l = batch tb + l).  Returns true
@@ -104,36 +112,57 @@ DEV bool walk_tile(const IdxTile& cur, uint64_t tb, uint64_t n, uint32_t l, uint
         const uint64_t o = shfl_up64(P, d);
         if (l >= (uint32_t)d) P += o;
     }
-    // the entry chain within the tile: next entry = first lane l > t with
-    // a + P_l - P_t >= step
-    uint64_t trig = 0, above = ~0ull, Pt = 0, a = w.a;
-    for (;;) {
-        const uint64_t thr = (step - a) + Pt;
-        const uint64_t m = __ballot(P >= thr) & valid & above;
-        if (!m) break;
-        const int t = __builtin_ctzll(m);
-        trig |= 1ull << t;
-        Pt = rl64(P, t);
-        a = 0;
-        above = t == 63 ? 0 : (~0ull << (t + 1));
-    }
     const int last = 63 - __builtin_clzll(valid);
+    uint64_t trig = 0, Pt = 0, a = w.a;
+    if (__ballot(mine && size_bytes < 0)) {
+        // negative sizes (never on a parser chain): P is not monotone, so
+        // find each entry with a ballot: the first lane l > t with
+        // a + P_l - P_t >= step
+        uint64_t above = ~0ull;
+        for (;;) {
+            const uint64_t thr = (step - a) + Pt;
+            const uint64_t m = __ballot(P >= thr) & valid & above;
+            if (!m) break;
+            const int t = __builtin_ctzll(m);
+            trig |= 1ull << t;
+            Pt = rl64(P, t);
+            a = 0;
+            above = t == 63 ? 0 : (~0ull << (t + 1));
+        }
+    } else {
+        // P is non-decreasing: every lane finds its successor entry in
+        // parallel, next(l) = first j > l with P_j >= P_l + step (binary
+        // lifting over lanes), then the chain is one readlane per entry
+        const uint64_t Pv = mine ? P : ~0ull;
+        const uint64_t target = P + step;
+        int pos = (int)l;
+#pragma unroll
+        for (int d = 32; d >= 1; d >>= 1) {
+            const int cand = pos + d;
+            const uint64_t pc = shfl64(Pv, cand & 63);
+            if (cand <= 63 && pc < target) pos = cand;
+        }
+        const uint32_t nxt = (pos + 1 > last) ? 64u : (uint32_t)(pos + 1);
+        // the first entry of the tile continues the carried acc (a <= step)
+        const uint64_t m0 = __ballot(P >= step - a) & valid;
+        if (m0) {
+            int t = __builtin_ctzll(m0);
+            for (;;) {
+                trig |= 1ull << t;
+                const uint32_t nx = uni32(rl(nxt, t));
+                if (nx >= 64u) break;
+                t = (int)nx;
+            }
+            Pt = rl64(P, t);
+            a = 0;
+        }
+    }
     w.a = a + (rl64(P, last) - Pt);
-    // max_timestamp = max(max_timestamp, max(first, last)) (index_state.cc:77-78)
+    // max_timestamp = max(max_timestamp, max(first, last)) (index_state.cc:77-78);
+    // the first batch's max_timestamp = first_timestamp is below its own max
     const int64_t lts = last_ts_raw > first_ts ? last_ts_raw : first_ts;
     if (w.n_entries == 0 && trig) w.base_ts = (int64_t)rl64((uint64_t)first_ts, __builtin_ctzll(trig));
-    int64_t m_ts = mine ? lts : INT64_MIN;
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        const int64_t v = shfl_xor_i64(m_ts, o);
-        m_ts = v > m_ts ? v : m_ts;
-    }
-    if (!w.have_max) {
-        // the first tracked batch sets max_timestamp = first_timestamp
-        w.max_ts = (int64_t)rl64((uint64_t)first_ts, 0);
-        w.have_max = true;
-    }
-    w.max_ts = m_ts > w.max_ts ? m_ts : w.max_ts;
+    if (mine && lts > w.lane_max_ts) w.lane_max_ts = lts;
     const int64_t lo = (int64_t)((uint64_t)b_off + (uint64_t)(int64_t)lod);
     w.max_off = (int64_t)rl64((uint64_t)lo, last);
     // add_entry (index_state.h:70-74)
@@ -173,8 +202,8 @@ __global__ __launch_bounds__(64) void k_segment_index(const rpgpu_batch_result* 
     // index makes the first tracked batch an entry (a = step)
     w.a = step;
     w.n_entries = w.tracked = 0;
-    w.base_ts = w.max_ts = w.max_off = 0;
-    w.have_max = false;
+    w.base_ts = w.max_off = 0;
+    w.lane_max_ts = INT64_MIN;
 
     if (n) {
         // four tiles in flight; unrolled by four so every tile keeps its own
@@ -196,12 +225,19 @@ __global__ __launch_bounds__(64) void k_segment_index(const rpgpu_batch_result* 
         }
 #undef RP_IDX_TILE
     }
+    int64_t max_ts = w.lane_max_ts;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        const int64_t v = shfl_xor_i64(max_ts, o);
+        max_ts = v > max_ts ? v : max_ts;
+    }
+    if (w.tracked == 0) max_ts = 0;
     if (l == 0) {
         rpgpu_index_state st;
         st.base_offset = idx_base;
         st.max_offset = w.max_off;
         st.base_timestamp = w.base_ts;
-        st.max_timestamp = w.max_ts;
+        st.max_timestamp = max_ts;
         st.first_entry = sm.first_batch;
         st.n_entries = w.n_entries;
         st.assert_batch = w.assert_batch;
