@@ -106,6 +106,46 @@ private:
     void* _p = nullptr;
 };
 
+// XXH64 (seed 0 in the reference's incremental_xxhash64, hashing/xx.h:36-71);
+// the checksum of the on-disk segment index (storage/index_state.cc:27-48).
+inline uint64_t xxh64(const uint8_t* p, size_t n, uint64_t seed = 0) {
+    constexpr uint64_t P1 = 0x9E3779B185EBCA87ull, P2 = 0xC2B2AE3D27D4EB4Full, P3 = 0x165667B19E3779F9ull,
+                       P4 = 0x85EBCA77C2B2AE63ull, P5 = 0x27D4EB2F165667C5ull;
+    auto rotl = [](uint64_t x, int r) { return (x << r) | (x >> (64 - r)); };
+    auto rd64 = [](const uint8_t* q) { uint64_t v; std::memcpy(&v, q, 8); return v; };
+    auto rd32 = [](const uint8_t* q) { uint32_t v; std::memcpy(&v, q, 4); return v; };
+    auto round = [&](uint64_t acc, uint64_t in) { return rotl(acc + in * P2, 31) * P1; };
+    auto merge = [&](uint64_t acc, uint64_t v) { return (acc ^ round(0, v)) * P1 + P4; };
+    const uint8_t* const end = p + n;
+    uint64_t h;
+    if (n >= 32) {
+        uint64_t v1 = seed + P1 + P2, v2 = seed + P2, v3 = seed, v4 = seed - P1;
+        for (; p + 32 <= end; p += 32) {
+            v1 = round(v1, rd64(p));
+            v2 = round(v2, rd64(p + 8));
+            v3 = round(v3, rd64(p + 16));
+            v4 = round(v4, rd64(p + 24));
+        }
+        h = rotl(v1, 1) + rotl(v2, 7) + rotl(v3, 12) + rotl(v4, 18);
+        h = merge(merge(merge(merge(h, v1), v2), v3), v4);
+    } else {
+        h = seed + P5;
+    }
+    h += (uint64_t)n;
+    for (; p + 8 <= end; p += 8) h = rotl(h ^ round(0, rd64(p)), 27) * P1 + P4;
+    if (p + 4 <= end) {
+        h = rotl(h ^ ((uint64_t)rd32(p) * P1), 23) * P2 + P3;
+        p += 4;
+    }
+    for (; p < end; p++) h = rotl(h ^ ((uint64_t)*p * P5), 11) * P1;
+    h ^= h >> 33;
+    h *= P2;
+    h ^= h >> 29;
+    h *= P3;
+    h ^= h >> 32;
+    return h;
+}
+
 }  // namespace rpgpu
 
 // ---------------------------------------------------------------------------
@@ -547,7 +587,84 @@ struct index_state {
     std::vector<uint32_t> relative_offset_index;
     std::vector<uint32_t> relative_time_index;
     std::vector<uint64_t> position_index;
+    uint32_t bitflags{0};
     bool empty() const { return relative_offset_index.empty(); }
+
+    static constexpr int8_t ondisk_version = 3;  // index_state.h:38
+
+    // index_state::checksum_state (storage/index_state.cc:27-48): xxhash64 of
+    // bitflags, base/max offset, base/max timestamp, the entry count and the
+    // three arrays, each as its native little-endian bytes
+    uint64_t checksum_state() const {
+        std::vector<uint8_t> b;
+        put_fields(b);
+        return rpgpu::xxh64(b.data(), b.size());
+    }
+
+    // index_state::checksum_and_serialize (storage/index_state.cc:189-236): the
+    // .base_index file body
+    std::vector<uint8_t> checksum_and_serialize() const {
+        std::vector<uint8_t> body;
+        put_fields(body);
+        const uint64_t checksum = rpgpu::xxh64(body.data(), body.size());
+        const uint32_t size = (uint32_t)(8 + body.size());  // checksum + the hashed fields
+        std::vector<uint8_t> out;
+        out.reserve(1 + 4 + size);
+        put(out, ondisk_version);
+        put(out, size);
+        put(out, checksum);
+        out.insert(out.end(), body.begin(), body.end());
+        return out;
+    }
+
+    // index_state::hydrate_from_buffer (storage/index_state.cc:95-186): nullopt
+    // on an unknown version, a size mismatch or a bad checksum (the reference
+    // then rebuilds the index from the log)
+    static std::optional<index_state> hydrate_from_buffer(const uint8_t* p, size_t n) {
+        size_t at = 0;
+        auto take = [&](auto& v) {
+            if (n - at < sizeof(v)) return false;
+            std::memcpy(&v, p + at, sizeof(v));
+            at += sizeof(v);
+            return true;
+        };
+        int8_t version;
+        uint32_t size, vsize;
+        uint64_t checksum;
+        index_state r;
+        if (!take(version) || version != ondisk_version) return std::nullopt;
+        if (!take(size) || n - at != size) return std::nullopt;
+        if (!take(checksum) || !take(r.bitflags) || !take(r.base_offset) || !take(r.max_offset) ||
+            !take(r.base_timestamp) || !take(r.max_timestamp) || !take(vsize))
+            return std::nullopt;
+        if ((n - at) / 16 < vsize) return std::nullopt;  // the reference's parser throws on a short read
+        r.relative_offset_index.resize(vsize);
+        r.relative_time_index.resize(vsize);
+        r.position_index.resize(vsize);
+        for (auto& v : r.relative_offset_index) take(v);
+        for (auto& v : r.relative_time_index) take(v);
+        for (auto& v : r.position_index) take(v);
+        if (r.checksum_state() != checksum) return std::nullopt;
+        return r;
+    }
+
+private:
+    template <class T>
+    static void put(std::vector<uint8_t>& b, T v) {
+        const auto* q = reinterpret_cast<const uint8_t*>(&v);
+        b.insert(b.end(), q, q + sizeof(T));
+    }
+    void put_fields(std::vector<uint8_t>& b) const {
+        put(b, bitflags);
+        put(b, base_offset);
+        put(b, max_offset);
+        put(b, base_timestamp);
+        put(b, max_timestamp);
+        put(b, (uint32_t)relative_offset_index.size());
+        for (uint32_t v : relative_offset_index) put(b, v);
+        for (uint32_t v : relative_time_index) put(b, v);
+        for (uint64_t v : position_index) put(b, v);
+    }
 };
 
 // storage/segment_index.h:30-100 (the lookups over a rebuilt index_state)

@@ -176,6 +176,11 @@ int main(int argc, char** argv) {
             else std::printf("CKPT 0\n");
             return 0;
         }
+        if (mode == "xxh64") {  // host only: the .base_index checksum primitive
+            const std::vector<uint8_t> b = slurp(argv[2]);
+            std::printf("%llu\n", (unsigned long long)rpgpu::xxh64(b.data(), b.size()));
+            return 0;
+        }
         if (mode == "index") {
             const std::vector<uint8_t> seg = slurp(argv[2]);
             storage::index_state st;
@@ -193,6 +198,21 @@ int main(int argc, char** argv) {
             for (size_t k = 0; k < st.relative_offset_index.size(); k++)
                 std::printf("E %u %u %llu\n", st.relative_offset_index[k], st.relative_time_index[k],
                             (unsigned long long)st.position_index[k]);
+            {
+                // .base_index round trip (index_state::checksum_and_serialize / hydrate_from_buffer)
+                std::vector<uint8_t> ser = st.checksum_and_serialize();
+                std::printf("SER ");
+                for (uint8_t c : ser) std::printf("%02x", c);
+                std::printf("\n");
+                const auto back = storage::index_state::hydrate_from_buffer(ser.data(), ser.size());
+                const bool same = back && back->relative_offset_index == st.relative_offset_index &&
+                                  back->relative_time_index == st.relative_time_index &&
+                                  back->position_index == st.position_index && back->max_offset == st.max_offset &&
+                                  back->max_timestamp == st.max_timestamp;
+                ser[ser.size() / 2] ^= 0x40;  // a flipped bit: checksum mismatch -> rebuild
+                const bool rejected = !storage::index_state::hydrate_from_buffer(ser.data(), ser.size());
+                std::printf("HYDRATE %d %d\n", same ? 1 : 0, rejected ? 1 : 0);
+            }
             const storage::segment_index idx(std::move(st));
             for (int a = 4; a < argc; a++) {
                 const auto e = idx.find_nearest(std::atoll(argv[a]));

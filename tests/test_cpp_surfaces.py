@@ -234,6 +234,30 @@ def test_log_replayer_checkpoint(driver, rplib, oracle, engine, tmp_path):
         assert line == want, name
 
 
+def test_xxh64_matches_xxhash(driver, tmp_path):
+    """rpgpu::xxh64 (the index checksum, hashing/xx.h incremental_xxhash64 with
+    seed 0) against the xxhash package over every tail-length path."""
+    import xxhash
+    rng = np.random.default_rng(7)
+    for n in list(range(0, 70)) + [1000, 4099]:
+        b = rng.integers(0, 256, n, dtype=np.uint8).tobytes()
+        (line,) = run(driver, "xxh64", write(tmp_path, f"x{n}", b))
+        assert int(line) == xxhash.xxh64_intdigest(b), n
+
+
+def serialize_index(st, ro, rt, ps) -> bytes:
+    """index_state::checksum_and_serialize (storage/index_state.cc:189-236) with
+    the checksum of checksum_state (:27-48): XXH64 (seed 0) of the LE fields."""
+    import struct
+    import xxhash
+    n = len(ro)
+    body = struct.pack("<Iqqqq", 0, int(st["base_offset"]), int(st["max_offset"]), int(st["base_timestamp"]),
+                       int(st["max_timestamp"]))
+    body += struct.pack("<I", n) + np.asarray(ro, "<u4").tobytes() + np.asarray(rt, "<u4").tobytes() \
+        + np.asarray(ps, "<u8").tobytes()
+    return struct.pack("<bIQ", 3, 8 + len(body), xxhash.xxh64_intdigest(body)) + body
+
+
 @pytest.mark.gpu
 def test_log_replayer_segment_index(driver, rplib, oracle, engine, tmp_path):
     """log_replayer::recover(.., index_state&) rebuilds the sparse index like
@@ -252,6 +276,8 @@ def test_log_replayer_segment_index(driver, rplib, oracle, engine, tmp_path):
         want.append(f"STATE {base} {int(st['max_offset'])} {int(st['base_timestamp'])} {int(st['max_timestamp'])} "
                     f"{len(ro)}")
         want += [f"E {int(a)} {int(b)} {int(c)}" for a, b, c in zip(ro, rt, ps)]
+        want.append("SER " + serialize_index(st, ro, rt, ps).hex())
+        want.append("HYDRATE 1 1")
         for q in qs:
             if q < base or len(ro) == 0:
                 want.append("NEAR none")
