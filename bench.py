@@ -237,9 +237,10 @@ def main():
         st.synchronize()
         ix = eng.index_to_host(*res, n_segments=len(parts))
         n_entries = int(sum(int(r[0]["n_entries"]) for r in ix))
-        index = {"kernel": "k_segment_index", "ms": round(e0.elapsed_time(e1) / reps, 4), "step": abi.INDEX_DEFAULT_STEP,
+        index = {"kernel": "k_idx_cut+k_idx_cand+k_idx_resolve+k_idx_emit", "ms": round(e0.elapsed_time(e1) / reps, 4), "step": abi.INDEX_DEFAULT_STEP,
                  "entries": n_entries, "tracked": int(sum(int(r[0]["tracked"]) for r in ix)),
-                 "note": "one wave per segment (serial entry chain), includes 3 output allocations"}
+                 "note": "piece-parallel (1024-batch pieces, candidate first entries, serial resolve), "
+                         "includes 3 output allocations"}
         del ix, res
 
     cpu = None

@@ -84,7 +84,8 @@ struct IdxWalk {
 // when tracking stops inside the tile (the reference's vassert).
 DEV bool walk_tile(const IdxTile& cur, uint64_t tb, uint64_t n, uint32_t l, uint64_t lt_mask, uint64_t step,
                    int64_t idx_base, uint64_t first_batch, IdxWalk& w, uint32_t* __restrict__ rel_offset,
-                   uint32_t* __restrict__ rel_time, uint64_t* __restrict__ position) {
+                   uint32_t* __restrict__ rel_time, uint64_t* __restrict__ position, uint64_t lo_b = 0,
+                   bool write = true) {
     const uint64_t i = tb + l;
     const uint64_t file_pos = u64of(cur.a.x, cur.a.y);
     const int64_t b_off = (int64_t)u64of(cur.a.z, cur.a.w);
@@ -92,7 +93,7 @@ DEV bool walk_tile(const IdxTile& cur, uint64_t tb, uint64_t n, uint32_t l, uint
     const int64_t last_ts_raw = (int64_t)u64of(cur.b.z, cur.b.w);
     const int64_t size_bytes = (int64_t)(int32_t)cur.c.z;
     const int32_t lod = (int32_t)cur.d.x;
-    uint64_t valid = __ballot(i < n);
+    uint64_t valid = __ballot(i < n && i >= lo_b);
     // vassert(batch_base_offset >= base_offset) (index_state.cc:57-63): the
     // reference aborts there, so tracking ends before that batch
     const uint64_t bad = __ballot(i < n && b_off < idx_base) & valid;
@@ -166,7 +167,7 @@ DEV bool walk_tile(const IdxTile& cur, uint64_t tb, uint64_t n, uint32_t l, uint
     const int64_t lo = (int64_t)((uint64_t)b_off + (uint64_t)(int64_t)lod);
     w.max_off = (int64_t)rl64((uint64_t)lo, last);
     // add_entry (index_state.h:70-74)
-    if ((trig >> l) & 1) {
+    if (write && ((trig >> l) & 1)) {
         const uint64_t k = first_batch + w.n_entries + __builtin_popcountll(trig & lt_mask);
         rel_offset[k] = (uint32_t)((uint64_t)b_off - (uint64_t)idx_base);
         rel_time[k] = (uint32_t)((uint64_t)lts - (uint64_t)w.base_ts);
@@ -244,6 +245,253 @@ __global__ __launch_bounds__(64) void k_segment_index(const rpgpu_batch_result* 
         st.tracked = w.tracked;
         states[s] = st;
     }
+}
+
+// ---------------------------------------------------------------------------
+// Piece-parallel rebuild.  A segment's tracked batches are cut into pieces of
+// kIdxPiece batches.  What a piece contributes depends only on the bytes
+// carried into it since the last entry (a_in), and only through which batch
+// becomes its first entry: a batch j of the piece can be that only if the
+// piece's bytes before j are < step, so the candidates are a prefix of the
+// piece (two batches for 16 KiB batches and a 32 KiB step).
+//   k_idx_cut      per segment: tracked count (the crc-good prefix, cut at the
+//                  vassert) and the state fields that need no walk
+//   k_idx_cand     per (piece, candidate): walk the piece with its first entry
+//                  forced at the candidate -> (entries, carried bytes out)
+//   k_idx_resolve  per segment, serial over pieces: a_in -> candidate -> a_out
+//                  (a piece whose first entry lies past the 64 precomputed
+//                  candidates is walked here instead)
+//   k_idx_emit     per piece: walk from the true a_in writing its entries at
+//                  their final ranks; timestamp max per segment
+// ---------------------------------------------------------------------------
+constexpr uint32_t kIdxPiece = 1024;  // batches per piece (16 tiles)
+constexpr uint32_t kIdxCand = 64;     // candidates precomputed per piece
+
+struct IdxCand {
+    uint64_t a_out;
+    uint32_t count;
+    uint32_t valid;
+};
+
+struct IdxWs {
+    uint64_t* cut;      // [nseg]
+    uint64_t* a_in;     // [nseg * max_pieces]
+    uint64_t* base;     // [nseg * max_pieces]
+    IdxCand* cand;      // [nseg * max_pieces * kIdxCand]
+    uint32_t max_pieces;
+};
+
+DEV uint64_t idx_tracked(const rpgpu_segment_summary& sm, uint64_t cap, int64_t& assert_batch) {
+    uint64_t n = sm.first_bad;
+    const uint64_t avail = sm.first_batch < cap ? cap - sm.first_batch : 0;
+    assert_batch = -1;
+    if (n > avail) {
+        n = avail;
+        assert_batch = -2;
+    }
+    return n;
+}
+
+// walk [from, end) of a segment starting with carried bytes a; no writes
+DEV void idx_walk_range(const rpgpu_batch_result* seg, uint64_t from, uint64_t end, uint64_t lo, uint64_t a,
+                        uint64_t step, int64_t idx_base, uint32_t l, uint64_t lt_mask, IdxWalk& w) {
+    w.a = a;
+    w.n_entries = w.tracked = 0;
+    w.base_ts = w.max_off = 0;
+    w.lane_max_ts = INT64_MIN;
+    w.assert_batch = -1;
+    for (uint64_t tb = from; tb < end; tb += 64) {
+        const IdxTile t = idx_load(seg, tb + l, end);
+        walk_tile(t, tb, end, l, lt_mask, step, idx_base, 0, w, nullptr, nullptr, nullptr, lo, false);
+    }
+}
+
+__global__ __launch_bounds__(256) void k_idx_cut(const rpgpu_batch_result* __restrict__ batches, uint64_t cap,
+                                                 const rpgpu_segment_summary* __restrict__ sums,
+                                                 rpgpu_index_state* __restrict__ states, IdxWs ws) {
+    const uint32_t s = blockIdx.x;
+    const rpgpu_segment_summary sm = sums[s];
+    const int64_t idx_base = states[s].base_offset;
+    int64_t assert_batch;
+    const uint64_t n = idx_tracked(sm, cap, assert_batch);
+    const rpgpu_batch_result* seg = batches + (sm.first_batch < cap ? sm.first_batch : 0);
+    __shared__ unsigned long long s_cut;
+    if (threadIdx.x == 0) s_cut = n;
+    __syncthreads();
+    uint64_t mine = n;
+    for (uint64_t i = threadIdx.x; i < n; i += 256)
+        if (seg[i].base_offset < idx_base) { mine = i; break; }
+    if (mine < n) atomicMin(&s_cut, (unsigned long long)mine);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const uint64_t cut = s_cut;
+        ws.cut[s] = cut;
+        rpgpu_index_state st;
+        st.base_offset = idx_base;
+        st.max_offset = cut ? (int64_t)((uint64_t)seg[cut - 1].base_offset + (uint64_t)(int64_t)seg[cut - 1].last_offset_delta) : 0;
+        st.base_timestamp = cut ? seg[0].first_timestamp : 0;
+        st.max_timestamp = cut ? INT64_MIN : 0;  // k_idx_emit folds in its maxima
+        st.first_entry = sm.first_batch;
+        st.n_entries = 0;
+        st.assert_batch = cut < n ? (int64_t)cut : assert_batch;
+        st.tracked = cut;
+        states[s] = st;
+    }
+}
+
+// grid (max_pieces, nseg), 4 waves per block: wave v takes candidates v, v+4, ...
+__global__ __launch_bounds__(256) void k_idx_cand(const rpgpu_batch_result* __restrict__ batches, uint64_t cap,
+                                                  const rpgpu_segment_summary* __restrict__ sums, uint64_t step,
+                                                  const rpgpu_index_state* __restrict__ states, IdxWs ws) {
+    const uint32_t p = blockIdx.x, s = blockIdx.y;
+    const uint32_t l = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const uint64_t cut = ws.cut[s];
+    const uint64_t from = (uint64_t)p * kIdxPiece;
+    if (from >= cut || p == 0) return;  // piece 0 starts with the forced first entry: no candidates needed
+    const uint64_t end = from + kIdxPiece < cut ? from + kIdxPiece : cut;
+    const rpgpu_segment_summary sm = sums[s];
+    const rpgpu_batch_result* seg = batches + sm.first_batch;
+    const int64_t idx_base = states[s].base_offset;
+    const uint64_t lt_mask = (1ull << l) - 1;
+    // candidates: lanes of the piece's first tile whose preceding piece bytes are < step
+    const uint64_t i0 = from + l;
+    const uint64_t sz = i0 < end ? (uint64_t)(int64_t)seg[i0].size_bytes : 0;
+    uint64_t P = sz;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint64_t o = shfl_up64(P, d);
+        if (l >= (uint32_t)d) P += o;
+    }
+    const uint64_t cmask = __ballot(i0 < end && (P - sz) < step);
+    IdxCand* out = ws.cand + ((uint64_t)s * ws.max_pieces + p) * kIdxCand;
+    for (uint32_t k = wv; k < kIdxCand; k += 4) {
+        if (!((cmask >> k) & 1)) {
+            if (l == 0) out[k].valid = 0;
+            continue;
+        }
+        IdxWalk w;
+        idx_walk_range(seg, from, end, from + k, step, step, idx_base, l, lt_mask, w);
+        if (l == 0) {
+            out[k].a_out = w.a;
+            out[k].count = (uint32_t)w.n_entries;
+            out[k].valid = 1;
+        }
+    }
+}
+
+// one wave per segment, serial over its pieces
+__global__ __launch_bounds__(64) void k_idx_resolve(const rpgpu_batch_result* __restrict__ batches,
+                                                    const rpgpu_segment_summary* __restrict__ sums, uint64_t step,
+                                                    rpgpu_index_state* __restrict__ states, IdxWs ws) {
+    const uint32_t s = blockIdx.x, l = threadIdx.x;
+    const uint64_t cut = ws.cut[s];
+    const rpgpu_segment_summary sm = sums[s];
+    const rpgpu_batch_result* seg = batches + sm.first_batch;
+    const int64_t idx_base = states[s].base_offset;
+    const uint64_t lt_mask = (1ull << l) - 1;
+    uint64_t a = step, entries = 0;
+    for (uint64_t p = 0; (uint64_t)p * kIdxPiece < cut; p++) {
+        const uint64_t from = p * kIdxPiece;
+        const uint64_t end = from + kIdxPiece < cut ? from + kIdxPiece : cut;
+        if (l == 0) {
+            ws.a_in[(uint64_t)s * ws.max_pieces + p] = a;
+            ws.base[(uint64_t)s * ws.max_pieces + p] = entries;
+        }
+        bool done = false;
+        if (p > 0) {
+            const uint64_t i0 = from + l;
+            uint64_t P = i0 < end ? (uint64_t)(int64_t)seg[i0].size_bytes : 0;
+#pragma unroll
+            for (int d = 1; d < 64; d <<= 1) {
+                const uint64_t o = shfl_up64(P, d);
+                if (l >= (uint32_t)d) P += o;
+            }
+            const uint64_t m = __ballot(i0 < end && P >= step - a);
+            if (m) {
+                const uint32_t k = __builtin_ctzll(m);
+                const IdxCand* c = ws.cand + ((uint64_t)s * ws.max_pieces + p) * kIdxCand + k;
+                if (c->valid) {
+                    a = c->a_out;
+                    entries += c->count;
+                    done = true;
+                }
+            }
+        }
+        if (!done) {
+            IdxWalk w;
+            idx_walk_range(seg, from, end, from, a, step, idx_base, l, lt_mask, w);
+            a = w.a;
+            entries += w.n_entries;
+        }
+    }
+    if (l == 0) states[s].n_entries = entries;
+}
+
+// grid (max_pieces, nseg): one wave per piece writes its entries
+__global__ __launch_bounds__(64) void k_idx_emit(const rpgpu_batch_result* __restrict__ batches,
+                                                 const rpgpu_segment_summary* __restrict__ sums, uint64_t step,
+                                                 rpgpu_index_state* __restrict__ states, IdxWs ws,
+                                                 uint32_t* __restrict__ rel_offset, uint32_t* __restrict__ rel_time,
+                                                 uint64_t* __restrict__ position) {
+    const uint32_t p = blockIdx.x, s = blockIdx.y, l = threadIdx.x;
+    const uint64_t cut = ws.cut[s];
+    const uint64_t from = (uint64_t)p * kIdxPiece;
+    if (from >= cut) return;
+    const uint64_t end = from + kIdxPiece < cut ? from + kIdxPiece : cut;
+    const rpgpu_segment_summary sm = sums[s];
+    const rpgpu_batch_result* seg = batches + sm.first_batch;
+    const int64_t idx_base = states[s].base_offset;
+    const uint64_t lt_mask = (1ull << l) - 1;
+    IdxWalk w;
+    w.a = ws.a_in[(uint64_t)s * ws.max_pieces + p];
+    w.n_entries = ws.base[(uint64_t)s * ws.max_pieces + p];
+    w.tracked = 0;
+    w.base_ts = seg[0].first_timestamp;
+    w.max_off = 0;
+    w.lane_max_ts = INT64_MIN;
+    w.assert_batch = -1;
+    for (uint64_t tb = from; tb < end; tb += 64) {
+        const IdxTile t = idx_load(seg, tb + l, end);
+        walk_tile(t, tb, end, l, lt_mask, step, idx_base, sm.first_batch, w, rel_offset, rel_time, position);
+    }
+    int64_t m = w.lane_max_ts;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        const int64_t v = shfl_xor_i64(m, o);
+        m = v > m ? v : m;
+    }
+    if (l == 0) atomicMax((long long*)&states[s].max_timestamp, (long long)m);
+}
+
+size_t segment_index_ws_bytes(uint32_t n_segments, uint64_t cap) {
+    const uint64_t mp = (cap + kIdxPiece - 1) / kIdxPiece + 1;
+    return 256 + (uint64_t)n_segments * 8 + 2 * (uint64_t)n_segments * mp * 8 +
+           (uint64_t)n_segments * mp * kIdxCand * sizeof(IdxCand) + 1024;
+}
+
+hipError_t launch_segment_index_pieces(const rpgpu_batch_result* batches, uint64_t cap,
+                                       const rpgpu_segment_summary* sums, uint32_t n_segments, uint64_t step,
+                                       rpgpu_index_state* states, uint32_t* rel_offset, uint32_t* rel_time,
+                                       uint64_t* position, void* wsp, hipStream_t s) {
+    const uint64_t mp = (cap + kIdxPiece - 1) / kIdxPiece + 1;
+    if (mp > 0xFFFFFFull) return hipErrorInvalidValue;
+    uint8_t* q = (uint8_t*)(((uintptr_t)wsp + 255) & ~(uintptr_t)255);
+    IdxWs ws;
+    ws.max_pieces = (uint32_t)mp;
+    ws.cut = (uint64_t*)q;
+    q += ((uint64_t)n_segments * 8 + 255) & ~255ull;
+    ws.a_in = (uint64_t*)q;
+    q += ((uint64_t)n_segments * mp * 8 + 255) & ~255ull;
+    ws.base = (uint64_t*)q;
+    q += ((uint64_t)n_segments * mp * 8 + 255) & ~255ull;
+    ws.cand = (IdxCand*)q;
+    hipLaunchKernelGGL(k_idx_cut, dim3(n_segments), dim3(256), 0, s, batches, cap, sums, states, ws);
+    hipLaunchKernelGGL(k_idx_cand, dim3((uint32_t)mp, n_segments), dim3(256), 0, s, batches, cap, sums, step,
+                       (const rpgpu_index_state*)states, ws);
+    hipLaunchKernelGGL(k_idx_resolve, dim3(n_segments), dim3(64), 0, s, batches, sums, step, states, ws);
+    hipLaunchKernelGGL(k_idx_emit, dim3((uint32_t)mp, n_segments), dim3(64), 0, s, batches, sums, step, states, ws,
+                       rel_offset, rel_time, position);
+    return hipGetLastError();
 }
 
 hipError_t launch_segment_index(const rpgpu_batch_result* batches, uint64_t cap, const rpgpu_segment_summary* sums,

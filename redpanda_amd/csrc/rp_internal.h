@@ -148,5 +148,10 @@ size_t scan_temp_bytes(uint64_t n);
 hipError_t launch_segment_index(const rpgpu_batch_result* batches, uint64_t cap, const rpgpu_segment_summary* sums,
                                 uint32_t n_segments, uint64_t step, rpgpu_index_state* states, uint32_t* rel_offset,
                                 uint32_t* rel_time, uint64_t* position, hipStream_t s);
+size_t segment_index_ws_bytes(uint32_t n_segments, uint64_t cap);
+hipError_t launch_segment_index_pieces(const rpgpu_batch_result* batches, uint64_t cap,
+                                       const rpgpu_segment_summary* sums, uint32_t n_segments, uint64_t step,
+                                       rpgpu_index_state* states, uint32_t* rel_offset, uint32_t* rel_time,
+                                       uint64_t* position, void* ws, hipStream_t s);
 
 }  // namespace rp

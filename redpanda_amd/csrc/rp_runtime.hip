@@ -104,6 +104,9 @@ struct rpgpu_ctx {
     size_t uws_bytes = 0;
     size_t ev_used = 0;
     uint32_t cu_count = 256;
+    // rpgpu_segment_index workspace (piece tables), grow-only
+    void* iws = nullptr;
+    size_t iws_bytes = 0;
     std::string err;
     // rpgpu_validate_host: a copy stream and two staging slots (segment
     // bytes in, per-batch results out), used alternately so the H2D copy of
@@ -188,6 +191,7 @@ int rpgpu_destroy(rpgpu_ctx* c) {
     if (c->stream) hipStreamSynchronize(c->stream);
     if (c->ws) hipFree(c->ws);
     if (c->uws) hipFree(c->uws);
+    if (c->iws) hipFree(c->iws);
     if (c->pin) hipHostFree(c->pin);
     if (c->d_tables) hipFree(c->d_tables);
     for (auto& set : c->ev_sets)
@@ -478,8 +482,27 @@ int rpgpu_segment_index(rpgpu_ctx* c, const rpgpu_batch_result* d_batches, uint6
     if (step >= (1ull << 62)) return fail(c, RPGPU_E_INVALID, "rpgpu_segment_index: step out of range");
     if (n_segments > 0x7FFFFFFFu) return fail(c, RPGPU_E_INVALID, "rpgpu_segment_index: too many segments");
     hipSetDevice(c->device);
-    HIPCHK(c, launch_segment_index(d_batches, batch_capacity, d_summaries, n_segments, step, d_states, d_rel_offset,
-                                   d_rel_time, d_position, pick(c, stream)));
+    hipStream_t s = pick(c, stream);
+    // RPGPU_INDEX_SERIAL=1: the one-wave-per-segment walk (A/B reference)
+    static const bool serial = [] { const char* e = getenv("RPGPU_INDEX_SERIAL"); return e && e[0] == '1'; }();
+    if (serial) {
+        HIPCHK(c, launch_segment_index(d_batches, batch_capacity, d_summaries, n_segments, step, d_states, d_rel_offset,
+                                       d_rel_time, d_position, s));
+        return RPGPU_OK;
+    }
+    const size_t need = segment_index_ws_bytes(n_segments, batch_capacity);
+    if (need > c->iws_bytes) {
+        if (c->iws) {
+            HIPCHK(c, hipDeviceSynchronize());  // the old tables may still be in use on any stream
+            HIPCHK(c, hipFree(c->iws));
+            c->iws = nullptr;
+            c->iws_bytes = 0;
+        }
+        HIPCHK(c, hipMalloc(&c->iws, need));
+        c->iws_bytes = need;
+    }
+    HIPCHK(c, launch_segment_index_pieces(d_batches, batch_capacity, d_summaries, n_segments, step, d_states,
+                                          d_rel_offset, d_rel_time, d_position, c->iws, s));
     return RPGPU_OK;
 }
 

@@ -184,6 +184,39 @@ def test_gpu_synthetic_results(engine, oracle, seed):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("kind", ["uniform16k", "tiny", "loguniform", "step0", "mixed_bad"])
+def test_gpu_many_pieces(engine, oracle, kind):
+    """Segments spanning many 1024-batch pieces: two candidates per piece
+    (16 KiB batches), first entries past the 64 precomputed candidates (tiny
+    batches: the serial fallback), log-uniform sizes, step 0, bad prefixes."""
+    rng = np.random.default_rng(hash(kind) & 0xFFFF)
+    counts = [20000, 1, 0, 4097, 9000]
+    n = sum(counts)
+    if kind in ("uniform16k", "step0"):
+        sizes = np.full(n, 16384)
+    elif kind == "tiny":
+        sizes = rng.integers(61, 600, n)
+    else:
+        sizes = np.exp(rng.uniform(np.log(61), np.log(1 << 20), n)).astype(np.int64)
+    offs = np.cumsum(rng.integers(1, 5, n))
+    ts = 1_600_000_000_000 + np.cumsum(rng.integers(-5, 1000, n))
+    segs, first = [], 0
+    for c in counts:
+        bad = int(rng.integers(0, c + 1)) if kind == "mixed_bad" else c
+        segs.append((first, c, bad))
+        first += c
+    b, sm = make_results(sizes, offs, first_ts=ts, max_ts=ts + 7, lod=rng.integers(0, 3, n), segs=segs)
+    step = 0 if kind == "step0" else STEP
+    bases = [int(offs[f]) if c else 0 for f, c, _ in segs]
+    if kind == "mixed_bad":
+        bases[3] = int(offs[segs[3][0] + 3000])  # vassert mid-segment
+    ref = oracle.segment_index(b, sm, bases, step=step)
+    out = _device_result(engine, b, sm)
+    got = engine.index_to_host(*engine.segment_index(out, bases, step=step), n_segments=len(counts))
+    assert_index_same(got, ref)
+
+
+@pytest.mark.gpu
 def test_gpu_reference_vectors(engine, oracle):
     """offset_index_utils_tests.cc:71-98 and :51-69 through the device kernel."""
     offs = [824, 849, 879, 901, 926, 948] + list(range(2000, 3024))
