@@ -379,20 +379,40 @@ __global__ __launch_bounds__(256) void k_idx_cand(const rpgpu_batch_result* __re
     }
 }
 
-// one wave per segment, serial over its pieces
+// one wave per segment, serial over its pieces.  The loads a piece needs (its
+// first 64 sizes and its 64-entry candidate row, one entry per lane) do not
+// depend on the carried state, so they are issued one piece ahead and the
+// serial chain itself is register work.
 __global__ __launch_bounds__(64) void k_idx_resolve(const rpgpu_batch_result* __restrict__ batches,
                                                     const rpgpu_segment_summary* __restrict__ sums, uint64_t step,
                                                     rpgpu_index_state* __restrict__ states, IdxWs ws) {
     const uint32_t s = blockIdx.x, l = threadIdx.x;
     const uint64_t cut = ws.cut[s];
+    if (cut == 0) {
+        if (l == 0) states[s].n_entries = 0;
+        return;
+    }
     const rpgpu_segment_summary sm = sums[s];
     const rpgpu_batch_result* seg = batches + sm.first_batch;
     const int64_t idx_base = states[s].base_offset;
     const uint64_t lt_mask = (1ull << l) - 1;
+    const uint64_t np = (cut + kIdxPiece - 1) / kIdxPiece;
+    const IdxCand* row0 = ws.cand + (uint64_t)s * ws.max_pieces * kIdxCand;
+    auto load_size = [&](uint64_t p) {
+        const uint64_t i = p * kIdxPiece + l;
+        return (int64_t)seg[i < cut ? i : cut - 1].size_bytes;
+    };
+    int64_t sz_next = load_size(0);
+    IdxCand c_next = row0[l];
     uint64_t a = step, entries = 0;
-    for (uint64_t p = 0; (uint64_t)p * kIdxPiece < cut; p++) {
+    for (uint64_t p = 0; p < np; p++) {
         const uint64_t from = p * kIdxPiece;
         const uint64_t end = from + kIdxPiece < cut ? from + kIdxPiece : cut;
+        const int64_t sz_cur = sz_next;
+        const IdxCand c_cur = c_next;
+        const uint64_t pn = p + 1 < np ? p + 1 : np - 1;
+        sz_next = load_size(pn);
+        c_next = row0[pn * kIdxCand + l];
         if (l == 0) {
             ws.a_in[(uint64_t)s * ws.max_pieces + p] = a;
             ws.base[(uint64_t)s * ws.max_pieces + p] = entries;
@@ -400,7 +420,7 @@ __global__ __launch_bounds__(64) void k_idx_resolve(const rpgpu_batch_result* __
         bool done = false;
         if (p > 0) {
             const uint64_t i0 = from + l;
-            uint64_t P = i0 < end ? (uint64_t)(int64_t)seg[i0].size_bytes : 0;
+            uint64_t P = i0 < end ? (uint64_t)sz_cur : 0;
 #pragma unroll
             for (int d = 1; d < 64; d <<= 1) {
                 const uint64_t o = shfl_up64(P, d);
@@ -408,11 +428,10 @@ __global__ __launch_bounds__(64) void k_idx_resolve(const rpgpu_batch_result* __
             }
             const uint64_t m = __ballot(i0 < end && P >= step - a);
             if (m) {
-                const uint32_t k = __builtin_ctzll(m);
-                const IdxCand* c = ws.cand + ((uint64_t)s * ws.max_pieces + p) * kIdxCand + k;
-                if (c->valid) {
-                    a = c->a_out;
-                    entries += c->count;
+                const int k = __builtin_ctzll(m);
+                if (rl(c_cur.valid, k)) {
+                    a = rl64(c_cur.a_out, k);
+                    entries += rl(c_cur.count, k);
                     done = true;
                 }
             }
