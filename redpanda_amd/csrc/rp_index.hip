@@ -254,11 +254,12 @@ __global__ __launch_bounds__(64) void k_segment_index(const rpgpu_batch_result* 
 // becomes its first entry: a batch j of the piece can be that only if the
 // piece's bytes before j are < step, so the candidates are a prefix of the
 // piece (two batches for 16 KiB batches and a 32 KiB step).
-//   k_idx_cut      per segment: tracked count (the crc-good prefix, cut at the
-//                  vassert) and the state fields that need no walk
+//   k_idx_cut      per piece: the first batch below the index base (the
+//                  vassert), atomicMin per segment -> tracked count
 //   k_idx_cand     per (piece, candidate): walk the piece with its first entry
 //                  forced at the candidate -> (entries, carried bytes out)
-//   k_idx_resolve  per segment, serial over pieces: a_in -> candidate -> a_out
+//   k_idx_resolve  per segment, serial over pieces: a_in -> candidate -> a_out;
+//                  writes the state fields that need no walk
 //                  (a piece whose first entry lies past the 64 precomputed
 //                  candidates is walked here instead)
 //   k_idx_emit     per piece: walk from the true a_in writing its entries at
@@ -306,37 +307,42 @@ DEV void idx_walk_range(const rpgpu_batch_result* seg, uint64_t from, uint64_t e
     }
 }
 
+// grid (max_pieces, nseg): the first batch below the index base offset (the
+// reference's vassert) per segment, by atomicMin over pieces; ws.cut starts
+// at ~0 and every reader takes min(ws.cut, tracked)
 __global__ __launch_bounds__(256) void k_idx_cut(const rpgpu_batch_result* __restrict__ batches, uint64_t cap,
                                                  const rpgpu_segment_summary* __restrict__ sums,
-                                                 rpgpu_index_state* __restrict__ states, IdxWs ws) {
-    const uint32_t s = blockIdx.x;
+                                                 const rpgpu_index_state* __restrict__ states, IdxWs ws) {
+    const uint32_t p = blockIdx.x, s = blockIdx.y;
     const rpgpu_segment_summary sm = sums[s];
-    const int64_t idx_base = states[s].base_offset;
     int64_t assert_batch;
     const uint64_t n = idx_tracked(sm, cap, assert_batch);
-    const rpgpu_batch_result* seg = batches + (sm.first_batch < cap ? sm.first_batch : 0);
-    __shared__ unsigned long long s_cut;
-    if (threadIdx.x == 0) s_cut = n;
-    __syncthreads();
-    uint64_t mine = n;
-    for (uint64_t i = threadIdx.x; i < n; i += 256)
+    const uint64_t from = (uint64_t)p * kIdxPiece;
+    if (from >= n) return;
+    const uint64_t end = from + kIdxPiece < n ? from + kIdxPiece : n;
+    const rpgpu_batch_result* seg = batches + sm.first_batch;
+    const int64_t idx_base = states[s].base_offset;
+    uint64_t mine = ~0ull;
+    for (uint64_t i = from + threadIdx.x; i < end; i += 256)
         if (seg[i].base_offset < idx_base) { mine = i; break; }
-    if (mine < n) atomicMin(&s_cut, (unsigned long long)mine);
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        const uint64_t cut = s_cut;
-        ws.cut[s] = cut;
-        rpgpu_index_state st;
-        st.base_offset = idx_base;
-        st.max_offset = cut ? (int64_t)((uint64_t)seg[cut - 1].base_offset + (uint64_t)(int64_t)seg[cut - 1].last_offset_delta) : 0;
-        st.base_timestamp = cut ? seg[0].first_timestamp : 0;
-        st.max_timestamp = cut ? INT64_MIN : 0;  // k_idx_emit folds in its maxima
-        st.first_entry = sm.first_batch;
-        st.n_entries = 0;
-        st.assert_batch = cut < n ? (int64_t)cut : assert_batch;
-        st.tracked = cut;
-        states[s] = st;
+    const uint64_t m = __ballot(mine != ~0ull);
+    if (m) {
+        // lowest lane with a hit has the wave's smallest index (lanes stride by 1)
+        uint64_t best = mine;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+            const uint64_t v = shfl64(best, (int)(threadIdx.x & 63) ^ o);
+            best = v < best ? v : best;
+        }
+        if ((threadIdx.x & 63) == 0) atomicMin((unsigned long long*)&ws.cut[s], (unsigned long long)best);
     }
+}
+
+DEV uint64_t idx_cut(const IdxWs& ws, uint32_t s, const rpgpu_segment_summary& sm, uint64_t cap) {
+    int64_t ab;
+    const uint64_t n = idx_tracked(sm, cap, ab);
+    const uint64_t c = ws.cut[s];
+    return c < n ? c : n;
 }
 
 // grid (max_pieces, nseg), 4 waves per block: wave v takes candidates v, v+4, ...
@@ -345,11 +351,11 @@ __global__ __launch_bounds__(256) void k_idx_cand(const rpgpu_batch_result* __re
                                                   const rpgpu_index_state* __restrict__ states, IdxWs ws) {
     const uint32_t p = blockIdx.x, s = blockIdx.y;
     const uint32_t l = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    const uint64_t cut = ws.cut[s];
+    const rpgpu_segment_summary sm = sums[s];
+    const uint64_t cut = idx_cut(ws, s, sm, cap);
     const uint64_t from = (uint64_t)p * kIdxPiece;
     if (from >= cut || p == 0) return;  // piece 0 starts with the forced first entry: no candidates needed
     const uint64_t end = from + kIdxPiece < cut ? from + kIdxPiece : cut;
-    const rpgpu_segment_summary sm = sums[s];
     const rpgpu_batch_result* seg = batches + sm.first_batch;
     const int64_t idx_base = states[s].base_offset;
     const uint64_t lt_mask = (1ull << l) - 1;
@@ -383,18 +389,30 @@ __global__ __launch_bounds__(256) void k_idx_cand(const rpgpu_batch_result* __re
 // first 64 sizes and its 64-entry candidate row, one entry per lane) do not
 // depend on the carried state, so they are issued one piece ahead and the
 // serial chain itself is register work.
-__global__ __launch_bounds__(64) void k_idx_resolve(const rpgpu_batch_result* __restrict__ batches,
+__global__ __launch_bounds__(64) void k_idx_resolve(const rpgpu_batch_result* __restrict__ batches, uint64_t cap,
                                                     const rpgpu_segment_summary* __restrict__ sums, uint64_t step,
                                                     rpgpu_index_state* __restrict__ states, IdxWs ws) {
     const uint32_t s = blockIdx.x, l = threadIdx.x;
-    const uint64_t cut = ws.cut[s];
-    if (cut == 0) {
-        if (l == 0) states[s].n_entries = 0;
-        return;
-    }
     const rpgpu_segment_summary sm = sums[s];
-    const rpgpu_batch_result* seg = batches + sm.first_batch;
+    int64_t assert_batch;
+    const uint64_t n = idx_tracked(sm, cap, assert_batch);
+    const uint64_t cut = idx_cut(ws, s, sm, cap);
+    const rpgpu_batch_result* seg = batches + (sm.first_batch < cap ? sm.first_batch : 0);
     const int64_t idx_base = states[s].base_offset;
+    if (l == 0) {
+        // the state fields that need no walk; k_idx_emit folds in the timestamp maxima
+        rpgpu_index_state st;
+        st.base_offset = idx_base;
+        st.max_offset = cut ? (int64_t)((uint64_t)seg[cut - 1].base_offset + (uint64_t)(int64_t)seg[cut - 1].last_offset_delta) : 0;
+        st.base_timestamp = cut ? seg[0].first_timestamp : 0;
+        st.max_timestamp = cut ? INT64_MIN : 0;
+        st.first_entry = sm.first_batch;
+        st.n_entries = 0;
+        st.assert_batch = cut < n ? (int64_t)cut : assert_batch;
+        st.tracked = cut;
+        states[s] = st;
+    }
+    if (cut == 0) return;
     const uint64_t lt_mask = (1ull << l) - 1;
     const uint64_t np = (cut + kIdxPiece - 1) / kIdxPiece;
     const IdxCand* row0 = ws.cand + (uint64_t)s * ws.max_pieces * kIdxCand;
@@ -447,17 +465,17 @@ __global__ __launch_bounds__(64) void k_idx_resolve(const rpgpu_batch_result* __
 }
 
 // grid (max_pieces, nseg): one wave per piece writes its entries
-__global__ __launch_bounds__(64) void k_idx_emit(const rpgpu_batch_result* __restrict__ batches,
+__global__ __launch_bounds__(64) void k_idx_emit(const rpgpu_batch_result* __restrict__ batches, uint64_t cap,
                                                  const rpgpu_segment_summary* __restrict__ sums, uint64_t step,
                                                  rpgpu_index_state* __restrict__ states, IdxWs ws,
                                                  uint32_t* __restrict__ rel_offset, uint32_t* __restrict__ rel_time,
                                                  uint64_t* __restrict__ position) {
     const uint32_t p = blockIdx.x, s = blockIdx.y, l = threadIdx.x;
-    const uint64_t cut = ws.cut[s];
+    const rpgpu_segment_summary sm = sums[s];
+    const uint64_t cut = idx_cut(ws, s, sm, cap);
     const uint64_t from = (uint64_t)p * kIdxPiece;
     if (from >= cut) return;
     const uint64_t end = from + kIdxPiece < cut ? from + kIdxPiece : cut;
-    const rpgpu_segment_summary sm = sums[s];
     const rpgpu_batch_result* seg = batches + sm.first_batch;
     const int64_t idx_base = states[s].base_offset;
     const uint64_t lt_mask = (1ull << l) - 1;
@@ -504,11 +522,14 @@ hipError_t launch_segment_index_pieces(const rpgpu_batch_result* batches, uint64
     ws.base = (uint64_t*)q;
     q += ((uint64_t)n_segments * mp * 8 + 255) & ~255ull;
     ws.cand = (IdxCand*)q;
-    hipLaunchKernelGGL(k_idx_cut, dim3(n_segments), dim3(256), 0, s, batches, cap, sums, states, ws);
+    hipError_t e = hipMemsetAsync(ws.cut, 0xFF, (size_t)n_segments * 8, s);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_idx_cut, dim3((uint32_t)mp, n_segments), dim3(256), 0, s, batches, cap, sums,
+                       (const rpgpu_index_state*)states, ws);
     hipLaunchKernelGGL(k_idx_cand, dim3((uint32_t)mp, n_segments), dim3(256), 0, s, batches, cap, sums, step,
                        (const rpgpu_index_state*)states, ws);
-    hipLaunchKernelGGL(k_idx_resolve, dim3(n_segments), dim3(64), 0, s, batches, sums, step, states, ws);
-    hipLaunchKernelGGL(k_idx_emit, dim3((uint32_t)mp, n_segments), dim3(64), 0, s, batches, sums, step, states, ws,
+    hipLaunchKernelGGL(k_idx_resolve, dim3(n_segments), dim3(64), 0, s, batches, cap, sums, step, states, ws);
+    hipLaunchKernelGGL(k_idx_emit, dim3((uint32_t)mp, n_segments), dim3(64), 0, s, batches, cap, sums, step, states, ws,
                        rel_offset, rel_time, position);
     return hipGetLastError();
 }
