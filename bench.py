@@ -237,8 +237,16 @@ def main():
         st.synchronize()
         ix = eng.index_to_host(*res, n_segments=len(parts))
         n_entries = int(sum(int(r[0]["n_entries"]) for r in ix))
+        gathered = None
+        if world > 1:
+            # the job's indexes at rank 0 (RCCL gather of the used entries only)
+            from redpanda_amd.shard import gather_segment_index
+            g = gather_segment_index(*res, parts, rank, world, dist)
+            if rank == 0:
+                gathered = {"partitions": len(g), "entries": int(sum(int(v[0]["n_entries"]) for v in g.values()))}
         index = {"kernel": "k_idx_cut+k_idx_cand+k_idx_resolve+k_idx_emit", "ms": round(e0.elapsed_time(e1) / reps, 4), "step": abi.INDEX_DEFAULT_STEP,
                  "entries": n_entries, "tracked": int(sum(int(r[0]["tracked"]) for r in ix)),
+                 "gathered_at_rank0": gathered,
                  "note": "piece-parallel (1024-batch pieces, candidate first entries, serial resolve), "
                          "includes 3 output allocations"}
         del ix, res

@@ -83,3 +83,40 @@ def gather_job_verdicts(summaries, bitmap, n_batches: int, parts: Sequence[int],
         b = np.unpackbits(got_b[r].cpu().numpy(), bitorder="little")[:nb]
         bits[tuple(rp)] = b
     return {"summaries": out, "bitmaps": bits}
+
+
+def gather_segment_index(states, rel_off, rel_time, pos, parts: Sequence[int], rank: int, world: int, dist):
+    """Gather each rank's rebuilt segment indexes (the outputs of
+    Engine.segment_index: rpgpu_index_state[len(parts)] as bytes plus the three
+    entry arrays) to rank 0.  Only the used entries travel: each rank packs
+    segment s's entries [first_entry, first_entry + n_entries) back to back.
+
+    Returns on rank 0 {partition: (index_state row, relative_offset,
+    relative_time, position)} for every partition of the job; None elsewhere."""
+    import torch
+    from . import abi
+    st = np.frombuffer(states.cpu().numpy().tobytes(), dtype=abi.INDEX_STATE)[: len(parts)]
+    sl = [(int(s["first_entry"]), int(s["n_entries"])) for s in st]
+    ro = torch.cat([rel_off[a:a + n] for a, n in sl]) if sl else rel_off[:0]
+    rt = torch.cat([rel_time[a:a + n] for a, n in sl]) if sl else rel_time[:0]
+    ps = torch.cat([pos[a:a + n] for a, n in sl]) if sl else pos[:0]
+    meta = torch.tensor(list(parts), dtype=torch.int64, device=states.device)
+    got = [gather_bytes(as_bytes(t), rank, world, dist) for t in (meta, states[: len(parts) * abi.INDEX_STATE.itemsize],
+                                                                   ro, rt, ps)]
+    if rank != 0:
+        return None
+    out = {}
+    for r in range(world):
+        rp = got[0][r].cpu().numpy().view(np.int64)
+        rs = got[1][r].cpu().numpy().view(abi.INDEX_STATE)
+        rro = got[2][r].cpu().numpy().view(np.uint32)
+        rrt = got[3][r].cpu().numpy().view(np.uint32)
+        rps = got[4][r].cpu().numpy().view(np.uint64)
+        if len(rs) != len(rp):
+            raise RuntimeError(f"rank {r}: {len(rs)} index states for {len(rp)} partitions")
+        k = 0
+        for p, s in zip(rp, rs):
+            n = int(s["n_entries"])
+            out[int(p)] = (s, rro[k:k + n], rrt[k:k + n], rps[k:k + n])
+            k += n
+    return out

@@ -95,3 +95,51 @@ def test_gloo_world2_gather_matches_single_process(rplib, oracle, tmp_path):
                                              bitorder="little")[: len(_oracle_job(_segments([p])).batches)]
                                for p in parts])
         assert got["bitmaps"][",".join(map(str, parts))] == want.tolist()
+
+
+def _index_worker(rank, world, port, out_path):
+    """Per rank: oracle job + oracle index rebuild over its partitions (in place
+    of the device engine), then the gather of the indexes to rank 0."""
+    import torch
+    import torch.distributed as dist
+    from oracle import oracle as O
+    from redpanda_amd.shard import gather_segment_index
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        parts = partitions_for_rank(N_PARTS, world, rank)
+        res = _oracle_job(_segments(parts))
+        ix = O.segment_index(res.batches, res.summaries, [0] * len(parts), step=4096)
+        cap = max(len(res.batches), 1)
+        st = np.zeros(len(parts), dtype=abi.INDEX_STATE)
+        ro, rt, ps = np.zeros(cap, np.uint32), np.zeros(cap, np.uint32), np.zeros(cap, np.uint64)
+        for k, (s, a, b, c) in enumerate(ix):
+            st[k] = s
+            f, n = int(s["first_entry"]), int(s["n_entries"])
+            ro[f:f + n], rt[f:f + n], ps[f:f + n] = a, b, c
+        got = gather_segment_index(torch.from_numpy(st.view(np.uint8).copy()), torch.from_numpy(ro.view(np.int32)),
+                                   torch.from_numpy(rt.view(np.int32)), torch.from_numpy(ps.view(np.int64)),
+                                   parts, rank, world, dist)
+        if rank == 0:
+            json.dump({str(p): {"n": int(v[0]["n_entries"]), "max_offset": int(v[0]["max_offset"]),
+                                "ro": v[1].tolist(), "ps": v[3].tolist()} for p, v in got.items()},
+                      open(out_path, "w"))
+        else:
+            assert got is None
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gloo_world2_index_gather_matches_single_process(rplib, oracle, tmp_path):
+    import torch.multiprocessing as mp
+    out = str(tmp_path / "rank0_index.json")
+    mp.spawn(_index_worker, args=(2, _free_port(), out), nprocs=2, join=True)
+    got = json.load(open(out))
+    assert sorted(int(p) for p in got) == list(range(N_PARTS))
+    for p in range(N_PARTS):
+        ref = _oracle_job(_segments([p]))
+        (s, ro, rt, ps), = oracle.segment_index(ref.batches, ref.summaries, [0], step=4096)
+        g = got[str(p)]
+        assert g["n"] == int(s["n_entries"]) > 0 and g["max_offset"] == int(s["max_offset"])
+        assert g["ro"] == ro.tolist() and g["ps"] == ps.tolist()
