@@ -387,8 +387,8 @@ __global__ __launch_bounds__(256) void k_idx_cand(const rpgpu_batch_result* __re
 
 // one wave per segment, serial over its pieces.  The loads a piece needs (its
 // first 64 sizes and its 64-entry candidate row, one entry per lane) do not
-// depend on the carried state, so they are issued one piece ahead and the
-// serial chain itself is register work.
+// depend on the carried state, so they are issued eight pieces at a time and
+// the serial chain itself is register work.
 __global__ __launch_bounds__(64) void k_idx_resolve(const rpgpu_batch_result* __restrict__ batches, uint64_t cap,
                                                     const rpgpu_segment_summary* __restrict__ sums, uint64_t step,
                                                     rpgpu_index_state* __restrict__ states, IdxWs ws) {
@@ -420,45 +420,53 @@ __global__ __launch_bounds__(64) void k_idx_resolve(const rpgpu_batch_result* __
         const uint64_t i = p * kIdxPiece + l;
         return (int64_t)seg[i < cut ? i : cut - 1].size_bytes;
     };
-    int64_t sz_next = load_size(0);
-    IdxCand c_next = row0[l];
     uint64_t a = step, entries = 0;
-    for (uint64_t p = 0; p < np; p++) {
-        const uint64_t from = p * kIdxPiece;
-        const uint64_t end = from + kIdxPiece < cut ? from + kIdxPiece : cut;
-        const int64_t sz_cur = sz_next;
-        const IdxCand c_cur = c_next;
-        const uint64_t pn = p + 1 < np ? p + 1 : np - 1;
-        sz_next = load_size(pn);
-        c_next = row0[pn * kIdxCand + l];
-        if (l == 0) {
-            ws.a_in[(uint64_t)s * ws.max_pieces + p] = a;
-            ws.base[(uint64_t)s * ws.max_pieces + p] = entries;
-        }
-        bool done = false;
-        if (p > 0) {
-            const uint64_t i0 = from + l;
-            uint64_t P = i0 < end ? (uint64_t)sz_cur : 0;
+    // eight pieces' loads issued together, then eight serial resolutions
+    constexpr int kAhead = 8;
+    for (uint64_t p0 = 0; p0 < np; p0 += kAhead) {
+        int64_t szv[kAhead];
+        IdxCand cv[kAhead];
 #pragma unroll
-            for (int d = 1; d < 64; d <<= 1) {
-                const uint64_t o = shfl_up64(P, d);
-                if (l >= (uint32_t)d) P += o;
+        for (int u = 0; u < kAhead; u++) {
+            const uint64_t pp = p0 + u < np ? p0 + u : np - 1;
+            szv[u] = load_size(pp);
+            cv[u] = row0[pp * kIdxCand + l];
+        }
+#pragma unroll
+        for (int u = 0; u < kAhead; u++) {
+            const uint64_t p = p0 + u;
+            if (p >= np) break;
+            const uint64_t from = p * kIdxPiece;
+            const uint64_t end = from + kIdxPiece < cut ? from + kIdxPiece : cut;
+            if (l == 0) {
+                ws.a_in[(uint64_t)s * ws.max_pieces + p] = a;
+                ws.base[(uint64_t)s * ws.max_pieces + p] = entries;
             }
-            const uint64_t m = __ballot(i0 < end && P >= step - a);
-            if (m) {
-                const int k = __builtin_ctzll(m);
-                if (rl(c_cur.valid, k)) {
-                    a = rl64(c_cur.a_out, k);
-                    entries += rl(c_cur.count, k);
-                    done = true;
+            bool done = false;
+            if (p > 0) {
+                const uint64_t i0 = from + l;
+                uint64_t P = i0 < end ? (uint64_t)szv[u] : 0;
+#pragma unroll
+                for (int d = 1; d < 64; d <<= 1) {
+                    const uint64_t o = shfl_up64(P, d);
+                    if (l >= (uint32_t)d) P += o;
+                }
+                const uint64_t m = __ballot(i0 < end && P >= step - a);
+                if (m) {
+                    const int k = __builtin_ctzll(m);
+                    if (rl(cv[u].valid, k)) {
+                        a = rl64(cv[u].a_out, k);
+                        entries += rl(cv[u].count, k);
+                        done = true;
+                    }
                 }
             }
-        }
-        if (!done) {
-            IdxWalk w;
-            idx_walk_range(seg, from, end, from, a, step, idx_base, l, lt_mask, w);
-            a = w.a;
-            entries += w.n_entries;
+            if (!done) {
+                IdxWalk w;
+                idx_walk_range(seg, from, end, from, a, step, idx_base, l, lt_mask, w);
+                a = w.a;
+                entries += w.n_entries;
+            }
         }
     }
     if (l == 0) states[s].n_entries = entries;
