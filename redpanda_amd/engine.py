@@ -138,23 +138,29 @@ class Engine:
         check(self.L.rpgpu_submit(self.ctx, C.byref(job), C.c_void_p(s.cuda_stream)), self.ctx, "rpgpu_submit")
         return out
 
-    def segment_index(self, out: DeviceResult, base_offsets, step: int = abi.INDEX_DEFAULT_STEP, stream=None):
+    def segment_index(self, out: DeviceResult, base_offsets, step: int = abi.INDEX_DEFAULT_STEP, stream=None,
+                      outputs=None):
         """Rebuild each segment's sparse index (segment_index::maybe_track over
         the crc-good prefix, storage/log_replayer.cc:62-74) from a completed
         disk-layout job `out`, on the device.  Returns device tensors
         (states, relative_offset, relative_time, position); segment s's
-        entries are [first_entry, first_entry + n_entries) of each array."""
+        entries are [first_entry, first_entry + n_entries) of each array.
+        `outputs` reuses a previous call's returned tensors (same job shape)."""
         torch = _torch()
         dev = out.batches.device
         nseg = out.n_segments
         cap = out.batches.numel() // abi.BATCH_RESULT.itemsize
-        st = np.zeros(max(nseg, 1), dtype=abi.INDEX_STATE)
-        st["base_offset"][:nseg] = np.asarray(base_offsets, dtype=np.int64)
-        states = torch.from_numpy(st.view(np.uint8).copy()).to(dev)
-        rel_off = torch.zeros(max(cap, 1), dtype=torch.int32, device=dev)
-        rel_time = torch.zeros(max(cap, 1), dtype=torch.int32, device=dev)
-        pos = torch.zeros(max(cap, 1), dtype=torch.int64, device=dev)
         s = stream if stream is not None else torch.cuda.current_stream(dev)
+        if outputs is None:
+            st = np.zeros(max(nseg, 1), dtype=abi.INDEX_STATE)
+            st["base_offset"][:nseg] = np.asarray(base_offsets, dtype=np.int64)
+            states = torch.from_numpy(st.view(np.uint8).copy()).to(dev)
+            rel_off = torch.zeros(max(cap, 1), dtype=torch.int32, device=dev)
+            rel_time = torch.zeros(max(cap, 1), dtype=torch.int32, device=dev)
+            pos = torch.zeros(max(cap, 1), dtype=torch.int64, device=dev)
+        else:
+            # base_offset is an input the kernels keep; every other field is rewritten
+            states, rel_off, rel_time, pos = outputs
         if s.cuda_stream == 0:
             # torch's legacy default stream: the library then launches on the
             # context's non-blocking stream, which does not order after it
