@@ -1,14 +1,21 @@
 #!/usr/bin/env python3
-"""Benchmark: validated batch GB/s on device-resident Redpanda segments.
+"""Benchmark: validated (+decoded) batch GB/s on device-resident Redpanda
+segments, with the roofline of the dominant kernel and the CPU baseline.
 
-Workload (BASELINE.json configs[1] / [3]): per GPU, 8 partitions x one 2 GiB
-on-disk segment of uncompressed 16 KiB record batches (seeded mt19937_64,
-reference recipe), i.e. 16 GiB = 1,048,576 batches per GPU.  One step = the
-whole pipeline over all 16 GiB: chain discovery, header_crc, batch CRC32C,
-record walk into the offset index, log_replayer checkpoint, validity bitmap.
-With --gpus N (torchrun, one rank per GPU) partitions are sharded p -> p % N
-and the only collective is the final RCCL gather of bitmaps + segment
-summaries to rank 0 (weak scaling).
+Headline workload (BASELINE.json configs[1] / [3], `value`): per GPU, 8
+partitions x one 2 GiB on-disk segment of uncompressed 16 KiB record batches
+(seeded mt19937_64, reference recipe), i.e. 16 GiB = 1,048,576 batches per
+GPU.  One step = the whole pipeline over all 16 GiB: chain discovery,
+header_crc, batch CRC32C, record walk into the offset index, log_replayer
+checkpoint, validity bitmap.  With --gpus N (torchrun, one rank per GPU)
+partitions are sharded p -> p % N and the only collective is the final RCCL
+gather of bitmaps + segment summaries to rank 0 (weak scaling).
+
+At N = 1 two more stanzas ride on the same JSON line (configs[2] and [4],
+SURVEY.md §8(d)): `c2` (LZ4 frames, 64 KiB..1 MiB decoded batches, decode +
+CRC + parse) and `c5` (skewed 200 B..1 MiB, none/lz4/snappy-java/raw snappy,
+corruptions), each with its own decode-kernel roofline and a liblz4 /
+libsnappy CPU baseline.
 
 Prints ONE JSON line on rank 0 (contract in the task statement).
 """
@@ -26,33 +33,45 @@ import numpy as np
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
+import synth  # noqa: E402  (test/bench data generator, not the product)
+
 SEG_BYTES = 2 << 30
 PARTITIONS_PER_GPU = 8
 BATCH_BYTES = 16384
-SEED = 0xC1
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+# C2: 8 partitions x 1.5 GiB of LZ4 segments (~16 GiB decoded per GPU);
+# C5: 128 partitions x 64 MiB (skewed batches, corruptions end chains early)
+C2_PARTS, C2_SEG = 8, 3 << 29
+C5_PARTS, C5_SEG = 128, 64 << 20
 
 
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def gen_partitions(partitions, seg_bytes, batch_bytes, torch, device, threads=8):
-    """Generate each partition's segment on the host (parallel, GIL released
-    inside librpgpu) and copy it into one device buffer."""
-    from redpanda_amd import _lib
+def host_threads() -> int:
+    """Host cores this process may use: the pool's CPU share where the box
+    sets one (OMP_NUM_THREADS = 16 per GPU there), else the affinity mask."""
+    env = os.environ.get("OMP_NUM_THREADS")
+    aff = len(os.sched_getaffinity(0))
+    return max(1, min(int(env), aff) if env and env.isdigit() else aff)
+
+
+def gen_partitions(partitions, seg_bytes, kw, torch, device, threads=None):
+    """Generate each partition's segment on the host (parallel, the GIL is
+    released inside librpgen) and copy it into one device buffer."""
     n = len(partitions)
-    data = torch.empty(n * seg_bytes, dtype=torch.uint8, device=device)
+    data = torch.empty(n * seg_bytes + 256, dtype=torch.uint8, device=device)
     counts = [0] * n
     host_first = None
     lock = threading.Lock()
-    sem = threading.Semaphore(threads)
+    sem = threading.Semaphore(threads or host_threads())
 
     def work(i, p):
         nonlocal host_first
         with sem:
             buf = np.empty(seg_bytes, dtype=np.uint8)
-            counts[i] = _lib.gen_segment(buf, p, seed=SEED, batch_bytes=batch_bytes)
+            counts[i] = synth.gen_segment(buf, p, **kw)
             with lock:
                 data[i * seg_bytes:(i + 1) * seg_bytes].copy_(torch.from_numpy(buf), non_blocking=False)
                 if i == 0:
@@ -66,17 +85,16 @@ def gen_partitions(partitions, seg_bytes, batch_bytes, torch, device, threads=8)
     return data, offs, counts, host_first
 
 
-def cpu_baseline(host_seg, seconds_budget=15.0):
+def cpu_baseline_c1(host_seg, seconds_budget=15.0):
     """The oracle's CPU restatement (SSE4.2 crc32c + record walk), timed on
     this box's host cores over a bounded sample of the same workload."""
     from oracle import oracle as O
-    cores = min(16, os.cpu_count() or 1)
+    cores = host_threads()
     sample = host_seg[: 1 << 30]  # 1 GiB sample = 65,536 batches
     # split the sample into `cores` slices on batch boundaries (16 KiB grid)
     per = (sample.size // BATCH_BYTES) // cores * BATCH_BYTES
     offs = np.arange(cores + 1, dtype=np.uint64) * np.uint64(per)
     sample = np.ascontiguousarray(sample[: int(offs[-1])])
-    # 1 core, single slice (sanity of the per-core rate)
     one = np.ascontiguousarray(sample[:per])
     nb1, s1, b1 = O.baseline_validate(one, [0, per], 1)
     reps, total_b, total_s = 0, 0, 0.0
@@ -85,16 +103,160 @@ def cpu_baseline(host_seg, seconds_budget=15.0):
         total_b += b
         total_s += s
         reps += 1
+    one_core = b1 / s1 / 1e9
     return {
         "value": round(total_b / total_s / 1e9, 3),
         "unit": "GB/s",
         "cores": cores,
         "kind": "port",
-        "sample": f"{sample.size >> 20} MiB of the C1 workload (65,536-batch slice of partition 0), "
-                  f"header_crc + batch CRC32C (SSE4.2) + record walk, {cores} threads x {reps} reps; "
-                  f"1 core: {b1 / s1 / 1e9:.2f} GB/s",
-        "one_core_GBs": round(b1 / s1 / 1e9, 3),
+        "sample": f"{sample.size >> 20} MiB of the C1 workload (partition 0), header_crc + batch CRC32C (SSE4.2) "
+                  f"+ record walk, {cores} pinned-per-core threads x {reps} reps",
+        "one_core_GBs": round(one_core, 3),
+        "host_logical_cpus": os.cpu_count(),
+        "all_host_cpus_linear_estimate_GBs": round(one_core * (os.cpu_count() or 1), 1),
     }
+
+
+def cpu_baseline_decode(host_seg, positions, seconds_budget=12.0):
+    """liblz4 1.9.3 / libsnappy 1.1.8 (the reference's codec libraries) over
+    the complete batches of one segment: stored crc + uncompress (the
+    reference's driver loops) + decoded crc, one thread per core."""
+    from oracle import oracle as O
+    cores = host_threads()
+    pos = np.asarray(positions, dtype=np.uint64)
+    reps, tb, td, ts = 0, 0, 0, 0.0
+    while ts < seconds_budget and reps < 200:
+        s, b, d = O.baseline_decode(host_seg, pos, cores)
+        tb, td, ts, reps = tb + b, td + d, ts + s, reps + 1
+    sub = pos[: max(1, len(pos) // 8)]
+    r1, b1, d1, s1 = 0, 0, 0, 0.0
+    while s1 < 3.0 and r1 < 50:
+        s, b, d = O.baseline_decode(host_seg, sub, 1)
+        b1, d1, s1, r1 = b1 + b, d1 + d, s1 + s, r1 + 1
+    return {
+        "value": round(tb / ts / 1e9, 3),
+        "unit": "GB/s (stored bytes)",
+        "decoded_GBs": round(td / ts / 1e9, 3),
+        "cores": cores,
+        "kind": "reference",
+        "sample": f"{len(pos)} batches ({tb // max(reps, 1) >> 20} MiB stored) of partition 0: stored crc + "
+                  f"liblz4 LZ4F_decompress / libsnappy RawUncompress (lz4_frame_compressor.cc:123-200 / "
+                  f"snappy_java_compressor.cc:76-129 loops) + decoded crc, {cores} threads x {reps} reps; "
+                  "record walk not included",
+        "one_core_GBs": round(b1 / s1 / 1e9, 3),
+        "one_core_decoded_GBs": round(d1 / s1 / 1e9, 3),
+        "host_logical_cpus": os.cpu_count(),
+    }
+
+
+def sized_outputs(eng, data, offs, flags, nseg, est_batches, torch, device):
+    """Outputs sized from the job's own totals (a probe run)."""
+    nb, nrec, ndec = est_batches, est_batches * 8, int(offs[-1]) * 2
+    for _ in range(4):
+        out = eng.alloc_outputs(nseg, nb + 16, nrec + 16, ndec + 4096)
+        eng.submit(data, offs, out, flags)
+        torch.cuda.synchronize(device)
+        t = out.totals_host()
+        if int(t["overflow"]) == 0:
+            return out
+        nb = max(nb, int(t["batch_capacity_needed"]))
+        nrec = max(nrec, int(t["record_capacity_needed"]))
+        ndec = max(ndec, int(t["decoded_capacity_needed"]))
+        del out
+    raise RuntimeError("output sizing did not converge")
+
+
+def run_compressed(name, kw, n_parts, seg_bytes, args, torch, device, eng, abi, desc):
+    """One compressed workload stanza (C2 / C5) on this GPU."""
+    t0 = time.time()
+    data, offs, counts, host_first = gen_partitions(list(range(n_parts)), seg_bytes, kw, torch, device)
+    log(f"[{name}] generated {n_parts} x {seg_bytes >> 20} MiB ({sum(counts)} batches) in {time.time() - t0:.1f}s")
+    flags = abi.JOB_CRC | abi.JOB_PARSE | abi.JOB_DECODE
+    d_offs = torch.from_numpy(offs.view(np.int64)).to(device)
+    out = sized_outputs(eng, data, offs, flags, n_parts, int(offs[-1]) // 4096 + 4096, torch, device)
+    for _ in range(args.warmup):
+        eng.submit(data, offs, out, flags, d_seg_offsets=d_offs)
+    torch.cuda.synchronize(device)
+    h = out.to_host()
+    b = h.batches
+    f = b["flags"]
+    comp = (f & abi.F_COMPRESSED) != 0
+    dec_ok = comp & ((f & abi.F_CODEC_OK) != 0)
+    stored = int(np.sum(b["size_bytes"].astype(np.int64)))
+    comp_in = int(np.sum(b["size_bytes"].astype(np.int64)[dec_ok] - abi.HEADER_SIZE))
+    decoded = int(np.sum(b["decoded_len"].astype(np.int64)[dec_ok]))
+    n_rec = int(h.totals["n_records"])
+    # size-independent parity properties of the measured job
+    crc_ok = (f & abi.F_CRC_OK) != 0
+    parity = {
+        "batches": int(len(b)),
+        "compressed": int(np.sum(comp)),
+        "codec_ok": int(np.sum(dec_ok)),
+        "crc_ok": int(np.sum(crc_ok)),
+        "parse_ok": int(np.sum((f & abi.F_PARSE_OK) != 0)),
+        "overflow": int(h.totals["overflow"]),
+        "records_eq_sum_parsed": bool(n_rec >= int(np.sum(b["records_parsed"].astype(np.int64)))),
+        "terminal_errc": {int(k): int(v) for k, v in zip(*np.unique(h.summaries["terminal_errc"], return_counts=True))},
+    }
+    if name == "c2":
+        parity["all_valid"] = bool(np.all(crc_ok) and np.all(dec_ok) and np.all(f & abi.F_PARSE_OK))
+    positions = b["file_pos"][(b["segment"] == 0) & ((f & abi.F_COMPLETE) != 0)]
+    del h
+    eng.set_timing(True)
+    torch.cuda.synchronize(device)
+    t1 = time.perf_counter()
+    for _ in range(args.steps):
+        eng.submit(data, offs, out, flags, d_seg_offsets=d_offs)
+    torch.cuda.synchronize(device)
+    el = (time.perf_counter() - t1) / args.steps
+    tm = eng.last_timings()
+    eng.set_timing(False)
+    dec_ms = tm["decode"]
+    dec_alg = comp_in + decoded
+    whole_alg = stored + comp_in + 2 * decoded + 64 * n_rec + 128 * len(b)
+    traffic = None
+    tfile = os.path.join(ROOT, "profiles", "decode_traffic.json")
+    if os.path.exists(tfile):
+        try:
+            tj = json.load(open(tfile)).get(name)
+            traffic = tj.get("bytes_per_step") if tj else None
+        except Exception:
+            traffic = None
+    cpu = None
+    if not args.no_cpu_baseline and len(positions):
+        cpu = cpu_baseline_decode(host_first, positions)
+    st = {
+        "workload": desc,
+        "partitions": n_parts,
+        "segment_bytes": seg_bytes,
+        "stored_bytes": stored,
+        "decoded_bytes": decoded,
+        "batches": int(len(b)),
+        "records": n_rec,
+        "ms_per_step": round(el * 1e3, 3),
+        "stored_GBps": round(stored / el / 1e9, 2),
+        "decoded_GBps": round(decoded / el / 1e9, 2),
+        "batches_per_s": round(len(b) / el, 1),
+        "hbm_fraction_whole_pipeline": round(whole_alg / el / 1e9 / HBM_PEAK_GBS, 4),
+        "whole_alg_bytes": whole_alg,
+        "stage_ms": {k: round(v, 4) for k, v in tm.items()},
+        "roofline": {
+            "bound": "hbm",
+            "kernel": "decode stage (k_decode*)",
+            "achieved": round(dec_alg / (dec_ms * 1e-3) / 1e9, 1) if dec_ms > 0 else None,
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": round(dec_alg / (dec_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4) if dec_ms > 0 else None,
+            "traffic": traffic,
+            "alg_bytes_per_launch": dec_alg,
+            "kernel_ms": round(dec_ms, 4),
+        },
+        "parity": parity,
+        "cpu_baseline": cpu,
+    }
+    del out, data, d_offs
+    torch.cuda.empty_cache()
+    return st
 
 
 def main():
@@ -111,13 +273,16 @@ def main():
     ap.add_argument("--no-index", action="store_true", help="skip the segment-index rebuild measurement")
     ap.add_argument("--batch-bytes", type=int, default=BATCH_BYTES,
                     help="size_bytes per batch (diagnostic; the headline workload is 16 KiB)")
+    ap.add_argument("--workloads", default="c1,c2,c5",
+                    help="c1 is the headline; c2/c5 stanzas run at N = 1 only")
     args = ap.parse_args()
+    workloads = set(args.workloads.split(","))
 
     import torch
     import torch.distributed as dist
     from redpanda_amd import abi
     from redpanda_amd.engine import Engine
-    from redpanda_amd.shard import as_bytes, gather_bytes, gather_job_verdicts, partitions_for_rank
+    from redpanda_amd.shard import as_bytes, gather_bytes, gather_job_verdicts, gather_sizes, partitions_for_rank
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -130,7 +295,8 @@ def main():
     seg_bytes = int(args.seg_gib * (1 << 30)) // BATCH_BYTES * BATCH_BYTES
     parts = partitions_for_rank(args.partitions * world, world, rank)
     t0 = time.time()
-    data, offs, counts, host_first = gen_partitions(parts, seg_bytes, args.batch_bytes, torch, device)
+    data, offs, counts, host_first = gen_partitions(parts, seg_bytes, dict(synth.C1, batch_bytes=args.batch_bytes),
+                                                    torch, device)
     n_batches = int(sum(counts))
     log(f"[rank {rank}] generated {len(parts)} x {seg_bytes >> 20} MiB, {n_batches} batches in {time.time() - t0:.1f}s")
 
@@ -140,16 +306,17 @@ def main():
     out = eng.alloc_outputs(len(parts), n_batches + 16, n_batches * rec_per_batch, 1)
     d_offs = torch.from_numpy(offs.view(np.int64)).to(device)
     chunk = args.chunk_kib << 10
+    payload = [out.bitmap, out.summaries] + ([out.batches] if args.gather == "index" else [])
+    # the gather's per-rank lengths are fixed for the run: negotiated once,
+    # outside the timed loop (no host sync per step)
+    sizes = [gather_sizes(as_bytes(t), world, dist) for t in payload] if world > 1 else None
 
     def step():
         eng.submit(data, offs, out, flags, chunk, d_seg_offsets=d_offs)
         if world > 1:
             # the one exchange: validity bitmaps + segment summaries to rank 0
-            payload = [out.bitmap, out.summaries]
-            if args.gather == "index":
-                payload.append(out.batches)
-            for t in payload:
-                gather_bytes(as_bytes(t), rank, world, dist)
+            for t, sz in zip(payload, sizes):
+                gather_bytes(as_bytes(t), rank, world, dist, sizes=sz)
 
     for _ in range(args.warmup):
         step()
@@ -207,6 +374,7 @@ def main():
     achieved = alg / (v_ms * 1e-3) / 1e9
     walk_alg = 64 * n_records + 128 * n_batches
     w_ms = tm.get("walk", 0.0)
+    whole_alg = seg_total + 64 * n_records + 64 * n_batches  # SURVEY §8(d) C1 bytes per unit
     traffic = None
     tfile = os.path.join(ROOT, "profiles", "validate_traffic.json")  # refreshed by scripts/parse_profile.py
     if os.path.exists(tfile):
@@ -244,16 +412,34 @@ def main():
             g = gather_segment_index(*res, parts, rank, world, dist)
             if rank == 0:
                 gathered = {"partitions": len(g), "entries": int(sum(int(v[0]["n_entries"]) for v in g.values()))}
-        index = {"kernel": "k_idx_cut+k_idx_cand+k_idx_resolve+k_idx_emit", "ms": round(e0.elapsed_time(e1) / reps, 4), "step": abi.INDEX_DEFAULT_STEP,
-                 "entries": n_entries, "tracked": int(sum(int(r[0]["tracked"]) for r in ix)),
-                 "gathered_at_rank0": gathered,
+        index = {"kernel": "k_idx_cut+k_idx_cand+k_idx_resolve+k_idx_emit", "ms": round(e0.elapsed_time(e1) / reps, 4),
+                 "step": abi.INDEX_DEFAULT_STEP, "entries": n_entries,
+                 "tracked": int(sum(int(r[0]["tracked"]) for r in ix)), "gathered_at_rank0": gathered,
                  "note": "piece-parallel (1024-batch pieces, candidate first entries, serial resolve); "
                          "outputs preallocated, timed region = the four kernels + workspace memset"}
         del ix, res
 
     cpu = None
     if rank == 0 and not args.no_cpu_baseline and host_first is not None:
-        cpu = cpu_baseline(host_first)
+        cpu = cpu_baseline_c1(host_first)
+    # release the C1 job before the compressed workloads
+    del out, data, d_offs, payload
+    torch.cuda.empty_cache()
+
+    extra = {}
+    if world == 1:
+        if "c2" in workloads:
+            extra["c2"] = run_compressed(
+                "c2", synth.C2, C2_PARTS, C2_SEG, args, torch, device, eng, abi,
+                "C2: 8 partitions x 1.5 GiB disk segments of LZ4 frames (64 KiB blocks, content size; 10% linked, "
+                "10% content checksum), decoded batches uniform 64 KiB..1 MiB, payload thirds random / alnum / "
+                "JSON-like (seed 0xC2): discover + header_crc + crc + LZ4F decode + decoded crc/header_crc + record walk")
+        if "c5" in workloads:
+            extra["c5"] = run_compressed(
+                "c5", synth.C5, C5_PARTS, C5_SEG, args, torch, device, eng, abi,
+                "C5: 128 partitions x 64 MiB, log-uniform 200 B..1 MiB batches, none 40 / lz4 30 / snappy-java 15 / "
+                "raw snappy 15, 1% payload + 0.2% header bit flips, 0.1% zeroed headers, truncated tails (seed 0xC5)")
+
     if rank == 0:
         line = {
             "metric": "validated+decoded batch GB/s per GPU and whole node; % of HBM peak",
@@ -281,7 +467,9 @@ def main():
                 "parity": {"all_batches_valid": all_ok, "bitmap_all_ones": bm_ok},
                 "stage_ms": {k: round(v, 4) for k, v in tm.items()},
                 "hbm_fraction_whole_pipeline": round(value / world / HBM_PEAK_GBS, 4),
+                "hbm_fraction_whole_pipeline_alg": round(whole_alg / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
                 "segment_index": index,
+                **extra,
             },
             "roofline": {
                 "bound": "hbm",

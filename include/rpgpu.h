@@ -347,31 +347,6 @@ typedef struct rpgpu_host_job {
 
 int rpgpu_validate_host(rpgpu_ctx* ctx, const rpgpu_host_job* job);
 
-/* ------------------------------------------------------------------------ */
-/* Synthetic workload (storage/tests/utils/random_batch.cc:50-154 recipe,    */
-/* seeded mt19937_64 so runs reproduce).  Host-side generator.               */
-/* ------------------------------------------------------------------------ */
-typedef struct rpgpu_gen_spec {
-    uint64_t seed;
-    uint64_t segment_bytes;          /* exact bytes per segment */
-    uint32_t batch_bytes;            /* target size_bytes per batch (0 = variable, see min/max) */
-    uint32_t min_batch_bytes;        /* variable mode: log-uniform in [min, max] */
-    uint32_t max_batch_bytes;
-    uint32_t value_bytes;            /* approximate record value size */
-    uint32_t key_bytes;
-    uint32_t headers_per_record;
-    uint32_t codec_mix;              /* 0 = none only; bitmask of codecs allowed (1<<codec) */
-    uint32_t corrupt_ppm_payload;    /* payload bit flips per million batches */
-    uint32_t corrupt_ppm_header;     /* header bit flips per million batches */
-    uint32_t corrupt_ppm_zero;       /* zeroed headers per million batches */
-    uint32_t threads;                /* 0 = all cores */
-    int64_t base_offset;
-} rpgpu_gen_spec;
-
-/* Fill `out` (segment_bytes) with one segment; returns number of batches or
- * <0.  The tail that cannot hold another batch is zero-filled (fallocated). */
-int64_t rpgpu_gen_segment(const rpgpu_gen_spec* spec, uint32_t segment_index, uint8_t* out);
-
 #ifdef __cplusplus
 } /* extern "C" */
 #endif

@@ -11,6 +11,7 @@
  *   ref_snappy_raw        <- snappy_standard_compressor.cc:43-65
  * Return 0 ok, -1 where the reference throws, -2 output capacity too small.
  */
+#define _POSIX_C_SOURCE 199309L
 #include <lz4.h>
 #include <lz4frame.h>
 #include <snappy-c.h>
@@ -152,3 +153,112 @@ size_t ref_snappy_compress(const uint8_t* src, size_t n, uint8_t* dst, size_t ca
 }
 
 size_t ref_snappy_bound(size_t n) { return snappy_max_compressed_length(n); }
+
+/* ------------------------------------------------------------------------ */
+/* CPU baseline of the decode path (bench.py cpu_baseline, C2 / C5): per     */
+/* batch of a disk segment, what the reference does on recovery + decode:   */
+/*   checksumming_consumer crc over BE40 ++ stored payload                   */
+/*     (storage/log_replayer.cc:48-79, model/record_utils.cc:68-91),          */
+/*   compressor::uncompress with the reference's codec libraries and driver  */
+/*     loops above (compression/compression.cc:34-55),                        */
+/*   reset_size_checksum_metadata's crc over BE40 ++ decoded bytes           */
+/*     (storage/parser_utils.cc:114-120).                                     */
+/* CRC32C with SSE4.2 crc32 instructions, as google crc32c's x86 path.       */
+/* One pthread per core, batches dealt round-robin; the clock covers the     */
+/* decode loop only (data preloaded).                                        */
+/* ------------------------------------------------------------------------ */
+#include <nmmintrin.h>
+#include <pthread.h>
+#include <time.h>
+
+__attribute__((target("sse4.2"))) static uint32_t hw_crc(uint32_t crc, const uint8_t* p, size_t n) {
+    uint64_t l = crc ^ 0xFFFFFFFFu;
+    while (n && ((uintptr_t)p & 7)) { l = _mm_crc32_u8((uint32_t)l, *p++); n--; }
+    while (n >= 8) {
+        uint64_t v;
+        memcpy(&v, p, 8);
+        l = _mm_crc32_u64(l, v);
+        p += 8;
+        n -= 8;
+    }
+    uint32_t s = (uint32_t)l;
+    while (n) { s = _mm_crc32_u8(s, *p++); n--; }
+    return s ^ 0xFFFFFFFFu;
+}
+
+static void be40(const uint8_t* h, uint8_t* be) {
+    static const int f[8][2] = {{21, 2}, {23, 4}, {27, 8}, {35, 8}, {43, 8}, {51, 2}, {53, 4}, {57, 4}};
+    int o = 0;
+    for (int k = 0; k < 8; k++)
+        for (int i = 0; i < f[k][1]; i++) be[o++] = h[f[k][0] + f[k][1] - 1 - i];
+}
+
+typedef struct {
+    const uint8_t* seg;
+    const uint64_t* pos;
+    uint64_t n, first, stride;
+    uint64_t stored, decoded, ok;
+} dec_task;
+
+static void* dec_worker(void* arg) {
+    dec_task* t = (dec_task*)arg;
+    size_t cap = 4u << 20;
+    uint8_t* buf = (uint8_t*)malloc(cap);
+    for (uint64_t i = t->first; i < t->n; i += t->stride) {
+        const uint8_t* h = t->seg + t->pos[i];
+        int32_t size;
+        memcpy(&size, h + 4, 4);
+        const size_t n = (size_t)size - 61;
+        uint8_t be[40];
+        be40(h, be);
+        uint32_t c = hw_crc(hw_crc(0, be, 40), h + 61, n);
+        uint32_t stored_crc;
+        memcpy(&stored_crc, h + 17, 4);
+        t->stored += (uint64_t)size;
+        const int codec = h[21] & 7;
+        size_t out = 0;
+        int rc = -1;
+        if (codec == 3) rc = ref_lz4f_uncompress(h + 61, n, buf, cap, &out);
+        else if (codec == 2) rc = ref_snappy_java(h + 61, n, buf, cap, &out);
+        else if (codec == 0) { rc = 0; out = 0; }
+        if (rc == 0 && codec) {
+            be[1] &= (uint8_t)~7u; /* codec bits cleared */
+            c ^= hw_crc(hw_crc(0, be, 40), buf, out);
+            t->decoded += out;
+        }
+        t->ok += (c != stored_crc) ? 1u : 0u; /* keeps both CRCs live */
+    }
+    free(buf);
+    return NULL;
+}
+
+/* pos[n]: file positions of the batches to process (all complete, in one
+ * segment buffer).  Returns seconds; stored/decoded byte totals out. */
+double ref_baseline_decode(const uint8_t* seg, const uint64_t* pos, uint64_t n, int threads, uint64_t* stored,
+                           uint64_t* decoded) {
+    if (threads < 1) threads = 1;
+    dec_task* t = (dec_task*)calloc((size_t)threads, sizeof(dec_task));
+    pthread_t* th = (pthread_t*)calloc((size_t)threads, sizeof(pthread_t));
+    struct timespec t0, t1;
+    clock_gettime(CLOCK_MONOTONIC, &t0);
+    for (int i = 0; i < threads; i++) {
+        t[i].seg = seg;
+        t[i].pos = pos;
+        t[i].n = n;
+        t[i].first = (uint64_t)i;
+        t[i].stride = (uint64_t)threads;
+        pthread_create(&th[i], NULL, dec_worker, &t[i]);
+    }
+    uint64_t s = 0, d = 0;
+    for (int i = 0; i < threads; i++) {
+        pthread_join(th[i], NULL);
+        s += t[i].stored;
+        d += t[i].decoded;
+    }
+    clock_gettime(CLOCK_MONOTONIC, &t1);
+    free(t);
+    free(th);
+    *stored = s;
+    *decoded = d;
+    return (double)(t1.tv_sec - t0.tv_sec) + 1e-9 * (double)(t1.tv_nsec - t0.tv_nsec);
+}

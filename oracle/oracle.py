@@ -109,6 +109,9 @@ def ref():
         R.ref_snappy_compress.argtypes = [C.c_void_p, C.c_size_t, C.c_void_p, C.c_size_t]
         R.ref_snappy_bound.restype = C.c_size_t
         R.ref_snappy_bound.argtypes = [C.c_size_t]
+        R.ref_baseline_decode.restype = C.c_double
+        R.ref_baseline_decode.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64, C.c_int, C.POINTER(C.c_uint64),
+                                          C.POINTER(C.c_uint64)]
         _ref = R
     return _ref
 
@@ -256,6 +259,20 @@ def baseline_validate(data: np.ndarray, seg_offsets, threads: int, hw: bool = Tr
                                      offs.size - 1, threads, 1 if hw else 0, C.byref(secs),
                                      C.byref(nbytes))
     return nb, secs.value, nbytes.value
+
+
+def baseline_decode(seg: np.ndarray, positions, threads: int):
+    """CPU baseline of the decode path over the batches at `positions` of
+    `seg` (stored crc + liblz4/libsnappy uncompress + decoded crc, one
+    pthread per core): (seconds, stored bytes, decoded bytes)."""
+    R = ref()
+    if R is None:
+        raise RuntimeError("codec harness (oracle/_ref/libcodecref.so) not built")
+    pos = np.ascontiguousarray(np.asarray(positions, dtype=np.uint64))
+    s, d = C.c_uint64(0), C.c_uint64(0)
+    secs = R.ref_baseline_decode(seg.ctypes.data_as(C.c_void_p), pos.ctypes.data_as(C.c_void_p), pos.size, threads,
+                                 C.byref(s), C.byref(d))
+    return secs, s.value, d.value
 
 
 def segment_index(batches: np.ndarray, summaries: np.ndarray, base_offsets, step: int = abi.INDEX_DEFAULT_STEP,

@@ -34,16 +34,6 @@ class JobC(C.Structure):
     ]
 
 
-class GenSpecC(C.Structure):
-    _fields_ = [
-        ("seed", C.c_uint64), ("segment_bytes", C.c_uint64), ("batch_bytes", C.c_uint32),
-        ("min_batch_bytes", C.c_uint32), ("max_batch_bytes", C.c_uint32), ("value_bytes", C.c_uint32),
-        ("key_bytes", C.c_uint32), ("headers_per_record", C.c_uint32), ("codec_mix", C.c_uint32),
-        ("corrupt_ppm_payload", C.c_uint32), ("corrupt_ppm_header", C.c_uint32),
-        ("corrupt_ppm_zero", C.c_uint32), ("threads", C.c_uint32), ("base_offset", C.c_int64),
-    ]
-
-
 def exported_symbols_from_header(path: str = HEADER):
     """Function names declared in include/rpgpu.h."""
     src = open(path).read()
@@ -95,7 +85,6 @@ def load():
         "rpgpu_uncompress": (i32, [vp, i32, vp, sz, vp, sz, C.POINTER(sz)]),
         "rpgpu_validate_host": (i32, [vp, vp]),
         "rpgpu_segment_index": (i32, [vp, vp, u64, vp, u32, u64, vp, vp, vp, vp, vp]),
-        "rpgpu_gen_segment": (C.c_int64, [C.POINTER(GenSpecC), u32, vp]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -124,21 +113,5 @@ def crc32c(data, crc: int = 0) -> int:
     return load().rpgpu_crc32c_extend(crc, a.ctypes.data_as(C.c_void_p), a.nbytes)
 
 
-def gen_segment(out, segment_index: int, *, seed: int, batch_bytes: int = 16384, min_batch: int = 0,
-                max_batch: int = 0, value_bytes: int = 1024, key_bytes: int = 16, headers: int = 2,
-                codec_mix: int = 1, corrupt_payload_ppm: int = 0, corrupt_header_ppm: int = 0,
-                corrupt_zero_ppm: int = 0, base_offset: int = 0) -> int:
-    """Fill the numpy uint8 array `out` with one synthetic segment."""
-    spec = GenSpecC(seed=seed, segment_bytes=out.nbytes, batch_bytes=batch_bytes, min_batch_bytes=min_batch,
-                    max_batch_bytes=max_batch, value_bytes=value_bytes, key_bytes=key_bytes,
-                    headers_per_record=headers, codec_mix=codec_mix, corrupt_ppm_payload=corrupt_payload_ppm,
-                    corrupt_ppm_header=corrupt_header_ppm, corrupt_ppm_zero=corrupt_zero_ppm, threads=0,
-                    base_offset=base_offset)
-    n = load().rpgpu_gen_segment(C.byref(spec), segment_index, out.ctypes.data_as(C.c_void_p))
-    if n < 0:
-        raise RpgpuError(f"rpgpu_gen_segment failed: {n}")
-    return n
-
-
-__all__ = ["load", "check", "crc32c", "gen_segment", "JobC", "GenSpecC", "RpgpuError", "abi",
+__all__ = ["load", "check", "crc32c", "JobC", "RpgpuError", "abi",
            "exported_symbols_from_header"]

@@ -1,5 +1,5 @@
 """Builds librpgpu.so in-tree: hand-written gfx950 kernels + the C-ABI host
-runtime (hipcc), the host generator (g++), linked into one shared library.
+runtime (hipcc), linked into one shared library.
 
 No JIT, no torch extension: the .so lives next to this file so it travels to
 the GPU box with the repo snapshot.
@@ -20,7 +20,7 @@ BUILD = os.path.join(HERE, "_build")
 ARCH = os.environ.get("RPGPU_ARCH", "gfx950")
 
 HIP_SOURCES = ["rp_kernels.hip", "rp_validate.hip", "rp_codec.hip", "rp_index.hip", "rp_runtime.hip"]
-CXX_SOURCES = ["rp_gen.cpp"]
+CXX_SOURCES = []
 
 
 def _hipcc():

@@ -82,6 +82,29 @@ class Engine:
         except Exception:
             pass
 
+    def _stream(self, dev, stream):
+        """The stream to launch on, and a finish() that orders torch's current
+        stream after the launch.  torch's legacy default stream (handle 0)
+        would make the library fall back to its private non-blocking stream,
+        which torch neither waits on nor tracks; such launches go to a torch
+        side stream that waits on the current one first."""
+        torch = _torch()
+        cur = torch.cuda.current_stream(dev)
+        s = stream if stream is not None else cur
+        if s.cuda_stream != 0:
+            return s, lambda *tensors: None
+        side = getattr(self, "_side", None)
+        if side is None or side.device != dev:
+            side = self._side = torch.cuda.Stream(dev)
+        side.wait_stream(s)
+
+        def finish(*tensors):
+            s.wait_stream(side)
+            for t in tensors:
+                if t is not None:
+                    t.record_stream(side)
+        return side, finish
+
     def set_timing(self, on: bool = True):
         check(self.L.rpgpu_set_timing(self.ctx, 1 if on else 0), self.ctx, "rpgpu_set_timing")
 
@@ -108,10 +131,13 @@ class Engine:
 
     def submit(self, data, seg_offsets, out: DeviceResult, flags: int = abi.JOB_CRC | abi.JOB_PARSE,
                chunk_bytes: int = 0, stream=None, d_seg_offsets=None, layout: int = abi.LAYOUT_DISK):
-        """Enqueue one job on `stream` (default: torch's current stream).
-        `data` is a torch uint8 CUDA tensor holding the concatenated segments
-        (abi.LAYOUT_DISK: Redpanda log segments; abi.LAYOUT_WIRE: Kafka v2
-        record sets as a produce request carries them)."""
+        """Enqueue one job ordered on `stream` (default: torch's current
+        stream; the launch itself goes to a side stream when that is the
+        legacy default stream, see _stream).  `data` is a torch uint8 CUDA
+        tensor holding the concatenated segments (abi.LAYOUT_DISK: Redpanda
+        log segments; abi.LAYOUT_WIRE: Kafka v2 record sets as a produce
+        request carries them).  Inputs and outputs are kept alive for the
+        allocator until the job is done."""
         torch = _torch()
         h_off = np.ascontiguousarray(np.asarray(seg_offsets, dtype=np.uint64))
         if d_seg_offsets is None:
@@ -134,8 +160,9 @@ class Engine:
         job.d_summaries = out.summaries.data_ptr()
         job.d_totals = out.totals.data_ptr()
         job.d_valid_bitmap = out.bitmap.data_ptr() if out.bitmap is not None else 0
-        s = stream if stream is not None else torch.cuda.current_stream(data.device)
+        s, finish = self._stream(data.device, stream)
         check(self.L.rpgpu_submit(self.ctx, C.byref(job), C.c_void_p(s.cuda_stream)), self.ctx, "rpgpu_submit")
+        finish(data, d_seg_offsets, out.batches, out.records, out.decoded, out.summaries, out.totals, out.bitmap)
         return out
 
     def segment_index(self, out: DeviceResult, base_offsets, step: int = abi.INDEX_DEFAULT_STEP, stream=None,
@@ -150,7 +177,6 @@ class Engine:
         dev = out.batches.device
         nseg = out.n_segments
         cap = out.batches.numel() // abi.BATCH_RESULT.itemsize
-        s = stream if stream is not None else torch.cuda.current_stream(dev)
         if outputs is None:
             st = np.zeros(max(nseg, 1), dtype=abi.INDEX_STATE)
             st["base_offset"][:nseg] = np.asarray(base_offsets, dtype=np.int64)
@@ -161,15 +187,20 @@ class Engine:
         else:
             # base_offset is an input the kernels keep; every other field is rewritten
             states, rel_off, rel_time, pos = outputs
-        if s.cuda_stream == 0:
-            # torch's legacy default stream: the library then launches on the
-            # context's non-blocking stream, which does not order after it
-            torch.cuda.synchronize(dev)
+            if states.numel() < nseg * abi.INDEX_STATE.itemsize or min(rel_off.numel(), rel_time.numel(),
+                                                                       pos.numel()) < cap:
+                raise RpgpuError("segment_index: `outputs` smaller than this job's segments / batch capacity")
+            have = np.frombuffer(states[: nseg * abi.INDEX_STATE.itemsize].cpu().numpy().tobytes(),
+                                 dtype=abi.INDEX_STATE)["base_offset"]
+            if not np.array_equal(have, np.asarray(base_offsets, dtype=np.int64)[:nseg]):
+                raise RpgpuError("segment_index: `outputs` were built for other base offsets")
+        s, finish = self._stream(dev, stream)
         check(self.L.rpgpu_segment_index(self.ctx, C.c_void_p(out.batches.data_ptr()), cap,
                                          C.c_void_p(out.summaries.data_ptr()), nseg, step,
                                          C.c_void_p(states.data_ptr()), C.c_void_p(rel_off.data_ptr()),
                                          C.c_void_p(rel_time.data_ptr()), C.c_void_p(pos.data_ptr()),
                                          C.c_void_p(s.cuda_stream)), self.ctx, "rpgpu_segment_index")
+        finish(out.batches, out.summaries, states, rel_off, rel_time, pos)
         return states, rel_off, rel_time, pos
 
     @staticmethod

@@ -24,15 +24,25 @@ def partitions_for_rank(n_partitions: int, world: int, rank: int) -> List[int]:
     return [p for p in range(n_partitions) if p % world == rank]
 
 
-def gather_bytes(t, rank: int, world: int, dist, dst: int = 0):
-    """Gather a 1-D uint8 tensor of any per-rank length to `dst`.  Returns the
-    list of per-rank tensors on dst, None elsewhere.  One small all_gather of
-    the lengths, then one gather of equal-size (padded) buffers."""
+def gather_sizes(t, world: int, dist) -> List[int]:
+    """Every rank's length of `t` (one small all_gather and a host sync):
+    negotiate once, then pass the result to gather_bytes for repeated gathers
+    of same-shaped payloads."""
     import torch
     n = torch.tensor([t.numel()], dtype=torch.int64, device=t.device)
     sizes = [torch.zeros_like(n) for _ in range(world)]
     dist.all_gather(sizes, n)
-    sizes = [int(s.item()) for s in sizes]
+    return [int(s.item()) for s in sizes]
+
+
+def gather_bytes(t, rank: int, world: int, dist, dst: int = 0, sizes: Sequence[int] = None):
+    """Gather a 1-D uint8 tensor of any per-rank length to `dst`.  Returns the
+    list of per-rank tensors on dst, None elsewhere.  The lengths come from
+    `sizes` (gather_sizes) or one small all_gather; then one gather of
+    equal-size (padded) buffers, with no host sync when `sizes` is given."""
+    import torch
+    if sizes is None:
+        sizes = gather_sizes(t, world, dist)
     m = max(sizes) if sizes else 0
     buf = t
     if t.numel() < m:
@@ -95,6 +105,9 @@ def gather_segment_index(states, rel_off, rel_time, pos, parts: Sequence[int], r
     relative_time, position)} for every partition of the job; None elsewhere."""
     import torch
     from . import abi
+    if states.is_cuda:
+        # the index kernels may still run on the stream that produced them
+        torch.cuda.synchronize(states.device)
     st = np.frombuffer(states.cpu().numpy().tobytes(), dtype=abi.INDEX_STATE)[: len(parts)]
     sl = [(int(s["first_entry"]), int(s["n_entries"])) for s in st]
     ro = torch.cat([rel_off[a:a + n] for a, n in sl]) if sl else rel_off[:0]

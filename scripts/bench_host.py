@@ -16,6 +16,7 @@ import torch  # noqa: E402
 
 from redpanda_amd import _lib, abi  # noqa: E402
 from redpanda_amd.engine import Engine  # noqa: E402
+import synth  # noqa: E402  (test/bench data generator, not the product)
 
 ap = argparse.ArgumentParser()
 ap.add_argument("--partitions", type=int, default=8)
@@ -27,7 +28,7 @@ seg = int(a.seg_gib * (1 << 30)) // 16384 * 16384
 segs = []
 for p in range(a.partitions):
     t = torch.empty(seg, dtype=torch.uint8, pin_memory=not a.pageable)
-    _lib.gen_segment(t.numpy(), p, seed=0xC1)
+    synth.gen_segment(t.numpy(), p, seed=0xC1)
     segs.append(t.numpy())
 eng = Engine(0)
 flags = abi.JOB_CRC | abi.JOB_PARSE

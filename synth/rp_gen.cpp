@@ -1,4 +1,5 @@
-// rp_gen.cpp — synthetic segment generator behind rpgpu_gen_segment.
+// rp_gen.cpp — synthetic segment generator (synth/rpgen.h; test and bench
+// data, never linked into the engine).
 //
 // Mirrors the reference's test batch recipe (storage/tests/utils/
 // random_batch.cc:50-154: records with ts/offset deltas = index, two headers
@@ -9,8 +10,11 @@
 // model/record_utils.cc:34-91 does.  Compressed batches go through the
 // reference's own codec libraries (liblz4 LZ4F with blockIndependent +
 // contentSize like lz4_frame_compressor.cc:69-113; snappy-java framing like
-// snappy_java_compressor.cc:57-74), loaded with dlopen.
+// snappy_java_compressor.cc:57-74; raw snappy like snappy_standard_compressor;
+// gzip like gzip_compressor.cc deflateInit2(15 + 16); zstd with the content
+// size like stream_zstd.cc), loaded with dlopen.
 #include <dlfcn.h>
+#include <nmmintrin.h>
 
 #include <algorithm>
 #include <cmath>
@@ -22,57 +26,67 @@
 #include <string>
 #include <vector>
 
-#include "rpgpu.h"
+#include <lz4frame.h>
+#include <snappy-c.h>
+#include <zlib.h>
+#include <zstd.h>
+
+#include "rpgen.h"
+
+constexpr uint32_t kHeaderSize = 61;  // model::packed_record_batch_header_size (model/record.h:473-487)
 
 namespace {
 
-// --- codec libraries ---------------------------------------------------------
-struct LZ4FPrefs {  // LZ4F_preferences_t (lz4 1.9.x ABI)
-    struct {
-        unsigned blockSizeID, blockMode, contentChecksumFlag, frameType;
-        unsigned long long contentSize;
-        unsigned dictID, blockChecksumFlag;
-    } frameInfo;
-    int compressionLevel;
-    unsigned autoFlush, favorDecSpeed, reserved[3];
-};
-typedef size_t (*lz4f_bound_t)(size_t, const LZ4FPrefs*);
-typedef size_t (*lz4f_compress_t)(void*, size_t, const void*, size_t, const LZ4FPrefs*);
-typedef unsigned (*lz4f_iserr_t)(size_t);
-typedef int (*snappy_compress_t)(const char*, size_t, char*, size_t*);
-typedef size_t (*snappy_bound_t)(size_t);
+// --- codec libraries (the reference's: liblz4, libsnappy, zlib, libzstd) ----
+bool lz4f_frame(const std::vector<uint8_t>& in, std::vector<uint8_t>& out, bool linked, bool cc, bool bc) {
+    LZ4F_preferences_t p;
+    std::memset(&p, 0, sizeof p);
+    p.compressionLevel = 1;
+    p.frameInfo.blockMode = linked ? LZ4F_blockLinked : LZ4F_blockIndependent;
+    p.frameInfo.contentSize = in.size();
+    p.frameInfo.blockSizeID = LZ4F_max64KB;  // 64 KiB blocks, as Kafka producers use
+    p.frameInfo.contentChecksumFlag = cc ? LZ4F_contentChecksumEnabled : LZ4F_noContentChecksum;
+    p.frameInfo.blockChecksumFlag = bc ? LZ4F_blockChecksumEnabled : LZ4F_noBlockChecksum;
+    const size_t bound = LZ4F_compressFrameBound(in.size(), &p);
+    out.resize(bound);
+    const size_t n = LZ4F_compressFrame(out.data(), bound, in.data(), in.size(), &p);
+    if (LZ4F_isError(n)) return false;
+    out.resize(n);
+    return true;
+}
 
-struct Codecs {
-    lz4f_bound_t lz4f_bound = nullptr;
-    lz4f_compress_t lz4f_compress = nullptr;
-    lz4f_iserr_t lz4f_iserr = nullptr;
-    snappy_compress_t snappy_compress = nullptr;
-    snappy_bound_t snappy_bound = nullptr;
-};
+bool snappy_block(const uint8_t* in, size_t n, std::vector<uint8_t>& out) {
+    size_t cl = snappy_max_compressed_length(n);
+    out.resize(cl);
+    if (snappy_compress((const char*)in, n, (char*)out.data(), &cl) != SNAPPY_OK) return false;
+    out.resize(cl);
+    return true;
+}
 
-const Codecs& codecs() {
-    static Codecs c;
-    static std::once_flag once;
-    std::call_once(once, [] {
-        const char* lz4_names[] = {"liblz4.so.1", "/opt/conda/lib/liblz4.so.1", "/lib/x86_64-linux-gnu/liblz4.so.1"};
-        for (const char* n : lz4_names) {
-            void* h = dlopen(n, RTLD_NOW | RTLD_LOCAL);
-            if (!h) continue;
-            c.lz4f_bound = (lz4f_bound_t)dlsym(h, "LZ4F_compressFrameBound");
-            c.lz4f_compress = (lz4f_compress_t)dlsym(h, "LZ4F_compressFrame");
-            c.lz4f_iserr = (lz4f_iserr_t)dlsym(h, "LZ4F_isError");
-            if (c.lz4f_bound && c.lz4f_compress && c.lz4f_iserr) break;
-        }
-        const char* sn_names[] = {"libsnappy.so.1", "/opt/conda/lib/libsnappy.so.1"};
-        for (const char* n : sn_names) {
-            void* h = dlopen(n, RTLD_NOW | RTLD_LOCAL);
-            if (!h) continue;
-            c.snappy_compress = (snappy_compress_t)dlsym(h, "snappy_compress");
-            c.snappy_bound = (snappy_bound_t)dlsym(h, "snappy_max_compressed_length");
-            if (c.snappy_compress && c.snappy_bound) break;
-        }
-    });
-    return c;
+// gzip_compressor::compress (compression/internal/gzip_compressor.cc): deflateInit2
+// (Z_DEFAULT_COMPRESSION, Z_DEFLATED, 15 + 16, 8, Z_DEFAULT_STRATEGY)
+bool gzip_member(const std::vector<uint8_t>& in, std::vector<uint8_t>& out) {
+    z_stream zs;
+    std::memset(&zs, 0, sizeof zs);
+    if (deflateInit2(&zs, Z_DEFAULT_COMPRESSION, Z_DEFLATED, 15 + 16, 8, Z_DEFAULT_STRATEGY) != Z_OK) return false;
+    out.resize(deflateBound(&zs, in.size()) + 64);
+    zs.next_in = const_cast<uint8_t*>(in.data());
+    zs.avail_in = (uInt)in.size();
+    zs.next_out = out.data();
+    zs.avail_out = (uInt)out.size();
+    const int r = deflate(&zs, Z_FINISH);
+    out.resize(zs.total_out);
+    deflateEnd(&zs);
+    return r == Z_STREAM_END;
+}
+
+// stream_zstd::do_compress (compression/stream_zstd.cc): content size always set
+bool zstd_frame(const std::vector<uint8_t>& in, std::vector<uint8_t>& out) {
+    out.resize(ZSTD_compressBound(in.size()));
+    const size_t n = ZSTD_compress(out.data(), out.size(), in.data(), in.size(), 3);
+    if (ZSTD_isError(n)) return false;
+    out.resize(n);
+    return true;
 }
 
 // --- encoding helpers ---------------------------------------------------------
@@ -155,7 +169,7 @@ void fill_kind(Rng& rng, uint8_t* p, size_t n, int kind, uint64_t& json_ctr) {
 
 // Encode records into `out` so that the encoded size is exactly `target`
 // (when target >= the minimal record size).  Returns the record count.
-int encode_records(Rng& rng, std::vector<uint8_t>& out, size_t target, const rpgpu_gen_spec* sp, int kind, uint64_t& jc) {
+int encode_records(Rng& rng, std::vector<uint8_t>& out, size_t target, const rpgen_spec* sp, int kind, uint64_t& jc) {
     const int nh = (int)sp->headers_per_record;
     const int32_t vbase = sp->value_bytes ? (int32_t)sp->value_bytes : 1024;
     const int32_t kbase = sp->key_bytes ? (int32_t)sp->key_bytes : 16;
@@ -234,52 +248,63 @@ int encode_records(Rng& rng, std::vector<uint8_t>& out, size_t target, const rpg
     return (int)specs.size();
 }
 
-bool compress_payload(int codec, const std::vector<uint8_t>& in, std::vector<uint8_t>& out) {
-    const Codecs& c = codecs();
-    if (codec == RPGPU_CODEC_LZ4) {
-        if (!c.lz4f_compress) return false;
-        LZ4FPrefs p;
-        std::memset(&p, 0, sizeof p);
-        p.compressionLevel = 1;
-        p.frameInfo.blockMode = 1;  // LZ4F_blockIndependent
-        p.frameInfo.contentSize = in.size();
-        p.frameInfo.blockSizeID = 4;  // 64 KiB blocks, as Kafka producers use
-        const size_t bound = c.lz4f_bound(in.size(), &p);
-        out.resize(bound);
-        const size_t n = c.lz4f_compress(out.data(), bound, in.data(), in.size(), &p);
-        if (c.lz4f_iserr(n)) return false;
-        out.resize(n);
-        return true;
-    }
-    if (codec == RPGPU_CODEC_SNAPPY) {
-        if (!c.snappy_compress) return false;
+// slot -> payload bytes under the batch's codec attribute
+bool compress_payload(int slot, const std::vector<uint8_t>& in, std::vector<uint8_t>& out, bool linked, bool cc,
+                      bool bc) {
+    switch (slot) {
+    case RPGEN_LZ4:
+        return lz4f_frame(in, out, linked, cc, bc);
+    case RPGEN_SNAPPY_JAVA: {
         static const uint8_t magic[8] = {0x82, 'S', 'N', 'A', 'P', 'P', 'Y', 0};
         out.assign(magic, magic + 8);
         uint8_t v[8];
-        wr_le(v, 1, 4);
+        wr_le(v, 1, 4);  // version, min_version: native little endian (snappy_java_compressor.cc:86-88)
         wr_le(v + 4, 1, 4);
         out.insert(out.end(), v, v + 8);
         const size_t chunk = 32 << 10;
-        std::vector<char> tmp(c.snappy_bound(chunk));
+        std::vector<uint8_t> tmp;
         for (size_t i = 0; i < in.size() || i == 0; i += chunk) {
             const size_t len = std::min(chunk, in.size() - i);
-            size_t cl = tmp.size();
-            if (c.snappy_compress((const char*)in.data() + i, len, tmp.data(), &cl) != 0) return false;
+            if (!snappy_block(in.data() + i, len, tmp)) return false;
             uint8_t be[4];
-            wr_be(be, (uint32_t)cl, 4);
+            wr_be(be, (uint32_t)tmp.size(), 4);
             out.insert(out.end(), be, be + 4);
-            out.insert(out.end(), tmp.data(), tmp.data() + cl);
+            out.insert(out.end(), tmp.begin(), tmp.end());
             if (in.empty()) break;
         }
         return true;
     }
+    case RPGEN_SNAPPY_RAW:
+        return snappy_block(in.data(), in.size(), out);
+    case RPGEN_GZIP:
+        return gzip_member(in, out);
+    case RPGEN_ZSTD:
+        return zstd_frame(in, out);
+    }
     return false;
 }
 
+int slot_codec(int slot) { return slot == RPGEN_SNAPPY_RAW ? RPGEN_SNAPPY_JAVA : slot; }
+
 }  // namespace
 
-extern "C" int64_t rpgpu_gen_segment(const rpgpu_gen_spec* sp, uint32_t segment_index, uint8_t* out) {
-    if (!sp || !out) return RPGPU_E_INVALID;
+extern "C" __attribute__((target("sse4.2"))) uint32_t rpgen_crc32c(uint32_t crc, const uint8_t* p, uint64_t n) {
+    uint64_t l = crc ^ 0xFFFFFFFFu;
+    while (n && ((uintptr_t)p & 7)) { l = _mm_crc32_u8((uint32_t)l, *p++); n--; }
+    while (n >= 8) {
+        uint64_t v;
+        std::memcpy(&v, p, 8);
+        l = _mm_crc32_u64(l, v);
+        p += 8;
+        n -= 8;
+    }
+    uint32_t s = (uint32_t)l;
+    while (n) { s = _mm_crc32_u8(s, *p++); n--; }
+    return s ^ 0xFFFFFFFFu;
+}
+
+extern "C" int64_t rpgen_segment(const rpgen_spec* sp, uint32_t segment_index, uint8_t* out) {
+    if (!sp || !out) return -1;
     Rng rng(sp->seed * 0x9E3779B97F4A7C15ull + (uint64_t)segment_index * 0xD1B54A32D192ED03ull + 1);
     const uint64_t len = sp->segment_bytes;
     std::memset(out, 0, len);
@@ -291,42 +316,54 @@ extern "C" int64_t rpgpu_gen_segment(const rpgpu_gen_spec* sp, uint32_t segment_
     std::vector<uint8_t> recs, comp;
     const uint32_t minb = sp->min_batch_bytes ? sp->min_batch_bytes : 200;
     const uint32_t maxb = sp->max_batch_bytes ? sp->max_batch_bytes : (1u << 20);
+    uint64_t wsum = 0;
+    for (int s = 0; s < RPGEN_SLOTS; s++) wsum += sp->codec_weights[s];
+    const bool mixed = wsum > sp->codec_weights[RPGEN_NONE];
     for (;;) {
         uint32_t target = sp->batch_bytes;
         if (!target) {
-            // log-uniform in [min, max]
+            // log-uniform (or uniform) in [min, max]
             const double u = (double)(rng.next() >> 11) / 9007199254740992.0;
-            target = (uint32_t)(minb * std::exp(u * std::log((double)maxb / (double)minb)));
+            target = sp->size_uniform ? (uint32_t)(minb + u * (double)(maxb - minb))
+                                      : (uint32_t)(minb * std::exp(u * std::log((double)maxb / (double)minb)));
             if (target < minb) target = minb;
         }
-        if (target < RPGPU_HEADER_SIZE + 16) target = RPGPU_HEADER_SIZE + 16;
-        // codec choice
-        int codec = 0;
-        if (sp->codec_mix & ~1u) {
-            uint32_t allowed[8];
-            int na = 0;
-            for (int c = 0; c < 5; c++)
-                if (sp->codec_mix & (1u << c)) allowed[na++] = (uint32_t)c;
-            codec = na ? (int)allowed[rng.below((uint32_t)na)] : 0;
-            if (codec == RPGPU_CODEC_GZIP || codec == RPGPU_CODEC_ZSTD) codec = 0;
+        if (target < kHeaderSize + 16) target = kHeaderSize + 16;
+        int slot = RPGEN_NONE;
+        if (mixed) {
+            uint64_t r = rng.next() % wsum;
+            for (slot = 0; slot < RPGEN_SLOTS - 1 && r >= sp->codec_weights[slot]; slot++) r -= sp->codec_weights[slot];
         }
-        const int kind = codec ? (int)rng.below(3) : K_ALNUM;
+        const int kind = slot ? (int)rng.below(3) : K_ALNUM;
+        bool linked = false, cc = false, bc = false;
+        if (slot == RPGEN_LZ4) {
+            linked = rng.below(1000000) < sp->lz4_linked_ppm;
+            cc = rng.below(1000000) < sp->lz4_content_checksum_ppm;
+            bc = rng.below(1000000) < sp->lz4_block_checksum_ppm;
+        }
         // uncompressed: size_bytes == target exactly; compressed: the
         // decoded payload is target - 61 bytes
         const uint64_t room = len - pos;
-        if (room < (uint64_t)RPGPU_HEADER_SIZE + 32) break;
-        size_t body = target - RPGPU_HEADER_SIZE;
-        if (!codec && body + RPGPU_HEADER_SIZE > room) break;
+        if (room < (uint64_t)kHeaderSize + 32) break;
+        const size_t body = target - kHeaderSize;
+        if (!slot && body + kHeaderSize > room && !sp->truncate_tail) break;
         const int nrec = encode_records(rng, recs, body, sp, kind, jc);
         if (nrec <= 0) break;
         const std::vector<uint8_t>* payload = &recs;
-        if (codec) {
-            if (!compress_payload(codec, recs, comp)) { codec = 0; }
+        if (slot) {
+            if (!compress_payload(slot, recs, comp, linked, cc, bc)) slot = RPGEN_NONE;
             else payload = &comp;
         }
-        const uint64_t size = RPGPU_HEADER_SIZE + payload->size();
-        if (size > room) break;
+        const int codec = slot_codec(slot);
+        const uint64_t size = kHeaderSize + payload->size();
+        if (size > room && !sp->truncate_tail) break;
+        // a batch that does not fit is built in scratch and cut at the end
+        std::vector<uint8_t> scratch;
         uint8_t* h = out + pos;
+        if (size > room) {
+            scratch.resize(size);
+            h = scratch.data();
+        }
         // header fields (header_crc and crc filled below)
         wr_le(h + 4, (uint32_t)size, 4);
         wr_le(h + 8, (uint64_t)offset, 8);
@@ -339,7 +376,7 @@ extern "C" int64_t rpgpu_gen_segment(const rpgpu_gen_spec* sp, uint32_t segment_
         wr_le(h + 51, (uint16_t)0xFFFF, 2);
         wr_le(h + 53, (uint32_t)0xFFFFFFFFu, 4);
         wr_le(h + 57, (uint32_t)nrec, 4);
-        std::memcpy(h + RPGPU_HEADER_SIZE, payload->data(), payload->size());
+        std::memcpy(h + kHeaderSize, payload->data(), payload->size());
         // crc: BE(attrs..record_count) ++ payload (model/record_utils.cc:68-91)
         uint8_t be[40];
         wr_be(be + 0, (uint16_t)codec, 2);
@@ -350,20 +387,24 @@ extern "C" int64_t rpgpu_gen_segment(const rpgpu_gen_spec* sp, uint32_t segment_
         wr_be(be + 30, (uint16_t)0xFFFF, 2);
         wr_be(be + 32, (uint32_t)0xFFFFFFFFu, 4);
         wr_be(be + 36, (uint32_t)nrec, 4);
-        uint32_t crc = rpgpu_crc32c_extend(0, be, 40);
-        crc = rpgpu_crc32c_extend(crc, h + RPGPU_HEADER_SIZE, payload->size());
+        uint32_t crc = rpgen_crc32c(0, be, 40);
+        crc = rpgen_crc32c(crc, h + kHeaderSize, payload->size());
         wr_le(h + 17, crc, 4);
-        wr_le(h + 0, rpgpu_crc32c_extend(0, h + 4, 57), 4);
+        wr_le(h + 0, rpgen_crc32c(0, h + 4, 57), 4);
+        if (size > room) {
+            std::memcpy(out + pos, h, room);  // truncated tail: header valid, payload cut
+            break;
+        }
         // fault injection (config 5 corruption injector)
         const uint32_t roll = (uint32_t)(rng.next() % 1000000u);
         if (roll < sp->corrupt_ppm_payload && payload->size() > 0) {
             const uint64_t bit = rng.next() % (payload->size() * 8);
-            h[RPGPU_HEADER_SIZE + bit / 8] ^= (uint8_t)(1u << (bit % 8));
+            h[kHeaderSize + bit / 8] ^= (uint8_t)(1u << (bit % 8));
         } else if (roll < sp->corrupt_ppm_payload + sp->corrupt_ppm_header) {
             const uint64_t bit = rng.next() % (61 * 8);
             h[bit / 8] ^= (uint8_t)(1u << (bit % 8));
         } else if (roll < sp->corrupt_ppm_payload + sp->corrupt_ppm_header + sp->corrupt_ppm_zero) {
-            std::memset(h, 0, RPGPU_HEADER_SIZE);
+            std::memset(h, 0, kHeaderSize);
         }
         pos += size;
         offset += nrec;

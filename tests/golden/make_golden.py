@@ -121,6 +121,27 @@ def segment_cases():
     C.append(("empty_batch", zero_rc, True, "record_count 0, empty payload"))
     neg_copy = bg.record(0, b"", b"", [], key_len=(1 << 31) + 5)
     C.append(("negative_int_copy", bg.batch(neg_copy, 1), False, "(int)len < 0 -> bad_alloc"))
+    # headers the discovery prefilter rejects although read_header_impl
+    # accepts them (storage/parser.cc:139-176 validates neither type nor
+    # size nor offsets): the chain must run through them
+    def chain(mid: bytes) -> bytes:
+        return (bg.batch(bg.simple_records(3, seed=40), 3, base_offset=0) + mid +
+                bg.batch(bg.simple_records(2, seed=41), 2, base_offset=100))
+    C.append(("type_zero_mid_chain", chain(bg.batch(bg.simple_records(2, seed=42), 2, base_offset=3, btype=0)),
+              True, "record_batch_type 0 chains"))
+    C.append(("type_99_mid_chain", chain(bg.batch(bg.simple_records(2, seed=43), 2, base_offset=3, btype=99)),
+              True, "record_batch_type 99 chains"))
+    C.append(("negative_base_offset_mid_chain",
+              chain(bg.batch(bg.simple_records(2, seed=44), 2, base_offset=-5)), True,
+              "negative base_offset chains"))
+    C.append(("codec_6_mid_chain", chain(bg.batch(bg.simple_records(2, seed=45), 2, base_offset=3, attrs=6)),
+              True, "codec bits 6: crc ok, compression() throws, chain continues"))
+    C.append(("negative_record_count_mid_chain",
+              chain(bg.batch(bg.simple_records(2, seed=46), -1, base_offset=3, lod=1)), False,
+              "record_count -1 chains; no record is walked"))
+    small = bg.batch(b"", 0, base_offset=3, size_bytes=40)
+    C.append(("size_40_valid_header_crc", bg.batch(bg.simple_records(3, seed=47), 3) + small + bytes(100), False,
+              "size_bytes 40 (< 61) with a valid header_crc: size-61 unsigned -> not enough bytes"))
     return C
 
 

@@ -6,6 +6,7 @@ import torch
 from redpanda_amd import _lib, abi
 from redpanda_amd.engine import Engine
 from oracle import oracle as O
+import synth  # noqa: E402  (test/bench data generator, not the product)
 
 def cmp(name, a, b, fields):
     ok = True
@@ -24,13 +25,13 @@ for case in range(4):
     for i, sb in enumerate(seg_bytes):
         a = np.zeros(sb, dtype=np.uint8)
         if case == 0:
-            _lib.gen_segment(a, i, seed=1)
+            synth.gen_segment(a, i, seed=1)
         elif case == 1:
-            _lib.gen_segment(a, i, seed=2, batch_bytes=0, min_batch=200, max_batch=200000)
+            synth.gen_segment(a, i, seed=2, batch_bytes=0, min_batch=200, max_batch=200000)
         elif case == 2:
-            _lib.gen_segment(a, i, seed=3, batch_bytes=0, min_batch=200, max_batch=100000, corrupt_payload_ppm=50000, value_bytes=100)
+            synth.gen_segment(a, i, seed=3, batch_bytes=0, min_batch=200, max_batch=100000, corrupt_payload_ppm=50000, value_bytes=100)
         else:
-            _lib.gen_segment(a, i, seed=4, batch_bytes=0, min_batch=200, max_batch=600000, corrupt_payload_ppm=10000, corrupt_header_ppm=5000)
+            synth.gen_segment(a, i, seed=4, batch_bytes=0, min_batch=200, max_batch=600000, corrupt_payload_ppm=10000, corrupt_header_ppm=5000)
         segs.append(a)
     offs = np.cumsum([0] + [s.size for s in segs]).astype(np.uint64)
     data = np.concatenate(segs)

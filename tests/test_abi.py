@@ -8,6 +8,7 @@ import subprocess
 import numpy as np
 
 from redpanda_amd import abi
+import synth  # noqa: E402  (test/bench data generator, not the product)
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
@@ -67,7 +68,7 @@ def test_no_device_entry_points_fail_loudly(rplib):
 
 def test_generator_segments_validate_in_oracle(rplib, oracle):
     a = np.zeros(2 << 20, dtype=np.uint8)
-    n = rplib.gen_segment(a, 0, seed=0xC1)
+    n = synth.gen_segment(a, 0, seed=0xC1)
     assert n == 128
     r = oracle.run_job(a, [0, a.size], abi.JOB_CRC | abi.JOB_PARSE)
     assert len(r.batches) == n
@@ -75,13 +76,13 @@ def test_generator_segments_validate_in_oracle(rplib, oracle):
     assert np.all(r.batches["flags"] == (abi.F_HEADER_OK | abi.F_COMPLETE | abi.F_CRC_OK | abi.F_PARSED |
                                          abi.F_PARSE_ASYNC_OK | abi.F_PARSE_OK | abi.F_INDEX_WRITTEN))
     b = np.zeros_like(a)
-    rplib.gen_segment(b, 0, seed=0xC1)
+    synth.gen_segment(b, 0, seed=0xC1)
     assert np.array_equal(a, b)  # seeded: reproducible
 
 
 def test_generator_codec_mix_decodes(rplib, oracle):
     a = np.zeros(4 << 20, dtype=np.uint8)
-    rplib.gen_segment(a, 2, seed=0xC2, batch_bytes=0, min_batch=64 << 10, max_batch=1 << 20,
+    synth.gen_segment(a, 2, seed=0xC2, batch_bytes=0, min_batch=64 << 10, max_batch=1 << 20,
                       codec_mix=(1 << abi.CODEC_LZ4) | (1 << abi.CODEC_SNAPPY))
     r = oracle.run_job(a, [0, a.size])
     f = r.batches["flags"]

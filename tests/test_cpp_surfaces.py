@@ -21,6 +21,7 @@ import pytest
 
 from redpanda_amd import abi
 from tests import batchgen as bg
+import synth  # noqa: E402  (test/bench data generator, not the product)
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 G = os.path.join(HERE, "golden")
@@ -41,7 +42,7 @@ def run(driver, *args):
 
 def gen(rplib, nbytes, idx, **kw):
     a = np.zeros(nbytes, dtype=np.uint8)
-    rplib.gen_segment(a, idx, **kw)
+    synth.gen_segment(a, idx, **kw)
     return a
 
 

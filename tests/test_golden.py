@@ -130,7 +130,8 @@ def test_negative_header_count(oracle):
 def test_ten_byte_varint(oracle):
     r = run(oracle, "ten_byte_varint")
     assert r.batches[0]["flags"] & abi.F_PARSE_OK
-    assert r.records[0]["ts_delta"] == -(1 << 63) + 0 or r.records[0]["ts_delta"] < 0
+    # 0xFF x 9, 0x01: LEB128 2^64 - 1, zigzag -> INT64_MIN (utils/vint.h:37-39, :82-98)
+    assert int(r.records[0]["ts_delta"]) == -(1 << 63)
 
 
 def test_key_overrun_last_record(oracle):
@@ -159,6 +160,41 @@ def test_negative_int_copy(oracle):
 def test_empty_batch(oracle):
     b = run(oracle, "empty_batch").batches[0]
     assert b["flags"] & abi.F_PARSE_OK and b["records_parsed"] == 0
+
+
+@pytest.mark.parametrize("name", ["type_zero_mid_chain", "type_99_mid_chain", "negative_base_offset_mid_chain",
+                                  "codec_6_mid_chain", "negative_record_count_mid_chain"])
+def test_prefilter_misses_still_chain(oracle, name):
+    """read_header_impl (storage/parser.cc:139-176) checks neither type, nor
+    offsets, nor codec bits, nor record_count: a header with a valid
+    header_crc chains whatever those fields hold."""
+    r = run(oracle, name)
+    assert len(r.batches) == 3
+    assert all(int(b["flags"]) & abi.F_HEADER_OK and int(b["flags"]) & abi.F_CRC_OK for b in r.batches)
+    s = r.summaries[0]
+    assert s["terminal_errc"] == abi.ERRC_END_OF_STREAM and s["first_bad"] == 3
+    mid = r.batches[1]
+    if name == "codec_6_mid_chain":
+        assert mid["flags"] & abi.F_CODEC_INVALID and not (mid["flags"] & abi.F_PARSED)
+    elif name == "negative_record_count_mid_chain":
+        assert mid["record_count"] == -1 and mid["records_parsed"] == 0
+        # record_count <= 0: for_each_record runs no record, so the payload is trailing bytes
+        assert mid["flags"] & abi.F_PARSE_ASYNC_OK and not (mid["flags"] & abi.F_PARSE_OK)
+    else:
+        assert mid["flags"] & abi.F_PARSE_OK and mid["records_parsed"] == 2
+
+
+def test_size_below_header_with_valid_header_crc(oracle):
+    """size_bytes 40: the header is accepted, size_bytes - 61 is computed
+    unsigned (storage/parser.cc:206-216) so the records can never be read:
+    the chain ends there with not-enough-bytes at eof."""
+    r = run(oracle, "size_40_valid_header_crc")
+    assert len(r.batches) == 2
+    b = r.batches[1]
+    assert b["flags"] & abi.F_HEADER_OK and not (b["flags"] & abi.F_COMPLETE) and b["size_bytes"] == 40
+    s = r.summaries[0]
+    assert s["terminal_errc"] == abi.ERRC_INPUT_STREAM_NOT_ENOUGH_BYTES and s["terminal_eof"] == 1
+    assert s["first_bad"] == 1 and s["ckpt_truncate_pos"] == r.batches[0]["size_bytes"]
 
 
 @pytest.mark.parametrize("ent", MAN["codecs"], ids=lambda e: e["name"])

@@ -13,6 +13,7 @@ import numpy as np
 import pytest
 
 from redpanda_amd import abi
+import synth  # noqa: E402  (test/bench data generator, not the product)
 
 STEP = abi.INDEX_DEFAULT_STEP
 
@@ -240,7 +241,7 @@ def test_gpu_after_recovery_job(engine, oracle, rplib):
     segs = []
     for i in range(4):
         a = np.zeros(3 << 20, dtype=np.uint8)
-        rplib.gen_segment(a, i, seed=11 + i, batch_bytes=0, min_batch=200, max_batch=200000,
+        synth.gen_segment(a, i, seed=11 + i, batch_bytes=0, min_batch=200, max_batch=200000,
                           corrupt_payload_ppm=(20000 if i % 2 else 0), base_offset=1000 * i)
         segs.append(a)
     offs = np.cumsum([0] + [s.size for s in segs]).astype(np.uint64)

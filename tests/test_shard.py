@@ -14,6 +14,7 @@ import pytest
 
 from redpanda_amd import abi
 from redpanda_amd.shard import partitions_for_rank
+import synth  # noqa: E402  (test/bench data generator, not the product)
 
 N_PARTS = 5
 SEG = 300_000
@@ -27,7 +28,7 @@ def _segments(parts):
     segs = []
     for p in parts:
         a = np.zeros(SEG + 997 * p, dtype=np.uint8)  # ragged per-partition sizes
-        _lib.gen_segment(a, p, **KW)
+        synth.gen_segment(a, p, **KW)
         segs.append(a)
     return segs
 

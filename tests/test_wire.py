@@ -18,6 +18,7 @@ import pytest
 
 from redpanda_amd import abi
 from tests import batchgen as bg
+import synth  # noqa: E402  (test/bench data generator, not the product)
 
 FLAGS = abi.JOB_CRC | abi.JOB_PARSE
 MAG_OFFSET = 8 + 4 + 4          # batch_reader_test.cc:76-78
@@ -27,7 +28,7 @@ LOD_OFFSET = CRC_OFFSET + 4 + 2  # :81-83
 
 def gen(rplib, nbytes, idx, **kw):
     a = np.zeros(nbytes, dtype=np.uint8)
-    rplib.gen_segment(a, idx, **kw)
+    synth.gen_segment(a, idx, **kw)
     return a
 
 
