@@ -834,7 +834,16 @@ int rpo_uncompress(int codec, const uint8_t* s, size_t n, uint8_t* dst, size_t c
     }
 }
 
+static uint64_t decode_capacity_raw(int codec, const uint8_t* s, size_t n);
+
+/* Engine plan rule (not reference semantics): bytes reserved in the decoded
+ * arena for one compressed payload, from its frame structure alone, rounded
+ * up to 16 so every slot starts 16-byte aligned. */
 uint64_t rpo_decode_capacity(int codec, const uint8_t* s, size_t n) {
+    return (decode_capacity_raw(codec, s, n) + 15) & ~(uint64_t)15;
+}
+
+static uint64_t decode_capacity_raw(int codec, const uint8_t* s, size_t n) {
     if (n == 0) return 0;
     if (codec == RPGPU_CODEC_LZ4) {
         lz4f_info fi;

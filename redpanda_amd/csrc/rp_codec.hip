@@ -7,259 +7,505 @@
 //     (compression/internal/snappy_java_compressor.cc:76-129), falling back to
 //     snappy_standard_compressor (compression/snappy_standard_compressor.cc:
 //     43-78) over snappy 1.1.8 RawUncompress.
-// The control flow is the oracle's (oracle/rp_oracle.c), which restates those
-// libraries; every accept/reject decision is kept.
+// The control flow (every accept/reject decision) is the oracle's
+// (oracle/rp_oracle.c), which restates those libraries.
 //
-// One wave per payload.  Control state (positions, tokens, lengths) is
-// uniform; input bytes are read through a 256-byte window held one dword per
-// lane (v_readlane), literal and match copies are spread over the 64 lanes.
-// A match reads output this wave stored earlier: a workgroup-scope
-// release/acquire fence makes those stores visible first, issued only when
-// the match source overlaps output written since the last fence.
+// Execution model: one wave decodes one piece (an LZ4 block of a
+// block-independent frame, a snappy-java chunk, or a whole sequential frame).
+//   * Parsing is wave-uniform: token / tag bytes come out of a 512-byte input
+//     window held one dword per lane (two VGPRs), read with v_readlane.
+//   * Output goes through a per-wave LDS ring (kRing bytes, indexed by the
+//     absolute arena address) and leaves for HBM in coalesced 16-byte-per-lane
+//     stores of whole 1 KiB chunks.
+//   * Literals up to 64 bytes are copied at once, one byte per lane, from the
+//     input window (ds_bpermute); longer ones stream from global memory.
+//   * Matches are queued, one per lane, into a group covering at most kSpan
+//     output bytes.  When the group closes, every match whose source ends
+//     before the group's first match is final and is copied lane-parallel:
+//     from the ring when the source is still in it, else from HBM (the
+//     wave's own earlier stores, read back with sc1 loads).  The rest
+//     (sources inside the group) are copied in order, one match per step,
+//     64 bytes per lane-parallel LDS round trip.
+//   * Long matches (> 64 bytes), zero offsets and long literals run on the
+//     spot, flushing the ring as they go.
+// Integer/byte work only: no MFMA.
 #include "rp_device.h"
-#ifdef RPGPU_CHECKED
+#if defined(RPGPU_CHECKED) || defined(RPGPU_TRACE)
 #include <cstdio>
+#endif
+// RPGPU_TRACE: diagnostic build (scripts/build_exp.py trace -DRPGPU_TRACE
+// --unit rp_codec.hip) printing the decode engine's steps; never measured
+#ifdef RPGPU_TRACE
+#define TRACE(...) do { if (lane() == 0) printf(__VA_ARGS__); } while (0)
+#else
+#define TRACE(...) do { } while (0)
+#endif
+#if defined(RPGPU_TRACE_ITEMS)
+#include <cstdio>
+#define TRACE_ITEM(...) do { if (lane() == 0) printf(__VA_ARGS__); } while (0)
+#else
+#define TRACE_ITEM(...) do { } while (0)
 #endif
 
 namespace rp {
 
+typedef __attribute__((address_space(3))) uint8_t lds_u8;
+typedef uint32_t v4u32 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) v4u32 lds_v4;
+
+#ifndef RPGPU_RING_KIB
+#define RPGPU_RING_KIB 16
+#endif
+constexpr uint32_t kRing = RPGPU_RING_KIB * 1024u;  // per-wave output ring
+constexpr uint32_t kRM = kRing - 1u;
+static_assert((kRing & kRM) == 0 && kRing >= 8192, "ring must be a power of two >= 8 KiB");
+constexpr uint32_t kDecWaves = 4;      // waves per workgroup of the decode kernels
+constexpr int64_t kSpan = 2048;        // output bytes one match group may cover
+constexpr uint32_t kFarMax = 48;       // far matches up to this length are copied lane-parallel
+constexpr uint32_t kBufFlags = 0x00020000u;  // buffer resource word 3 (raw, 32-bit data format)
+constexpr int kSc1 = 16;               // cache policy: sc1 (L2-coherent, bypasses the vector L1)
+
 // ---------------------------------------------------------------------------
-// input window
+// input window: 512 bytes, lane l holds dwords base + 4 l (w0) and base + 256
+// + 4 l (w1); base is 4-aligned in absolute address
 // ---------------------------------------------------------------------------
 struct In {
     const uint8_t* src;  // stream start
     int64_t n;           // stream bytes
     int64_t base;        // stream offset of the window start
-    uint32_t w;          // this lane's window dword
+    uint32_t w0, w1;
 };
+
+DEV uint32_t ld_dw(const uint8_t* src, int64_t n, uintptr_t a) {
+    return a < (uintptr_t)(src + n) ? *(const uint32_t*)a : 0u;  // a is 4-aligned: never crosses a page
+}
 
 DEV void in_init(In& in, const uint8_t* src, int64_t n) {
     in.src = src;
     in.n = n;
     in.base = -(1ll << 60);
-    in.w = 0;
+    in.w0 = in.w1 = 0;
 }
 
 DEV void in_load(In& in, int64_t ip) {
     const uintptr_t a = ((uintptr_t)(in.src + ip)) & ~(uintptr_t)3;
     in.base = (int64_t)(a - (uintptr_t)in.src);
     const uintptr_t mine = a + 4u * lane();
-    const uintptr_t end = (uintptr_t)(in.src + in.n);
-    in.w = mine < end ? *(const uint32_t*)mine : 0u;
+    in.w0 = ld_dw(in.src, in.n, mine);
+    in.w1 = ld_dw(in.src, in.n, mine + 256u);
 }
 
-// byte ip of the stream (uniform ip >= 0; bytes past the stream read as the
-// memory that follows it or zero, never faulting)
+// byte ip of the stream (uniform; bytes past the stream read as zero)
 DEV uint32_t in_byte(In& in, int64_t ip) {
     int64_t o = ip - in.base;
-    if (o < 0 || o >= 256) {
+    if (o < 0 || o >= 512) {
         in_load(in, ip);
         o = ip - in.base;
     }
-    return (rl(in.w, (int)(o >> 2)) >> (8 * (uint32_t)(o & 3))) & 0xFFu;
+    const int li = (int)((o >> 2) & 63);
+    const uint32_t w = o < 256 ? rl(in.w0, li) : rl(in.w1, li);
+    return (w >> (8 * (uint32_t)(o & 3))) & 0xFFu;
 }
 DEV uint32_t in_le16(In& in, int64_t ip) { return in_byte(in, ip) | (in_byte(in, ip + 1) << 8); }
 DEV uint32_t in_le32(In& in, int64_t ip) { return in_le16(in, ip) | (in_le16(in, ip + 2) << 16); }
 
 // ---------------------------------------------------------------------------
-// wave-cooperative copies
+// output state.  Positions are absolute arena offsets (uniform, 64-bit).
 // ---------------------------------------------------------------------------
-DEV void vis_fence() {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-}
-
-// Loads of output this wave wrote: agent-scope relaxed loads (sc1) skip the
-// vector L1, which may hold a copy of the line taken by another wave of the
-// CU before these bytes were stored (arena slots and blocks are adjacent;
-// the workgroup-scope acquire does not invalidate L1).  The release in
-// vis_fence has put the stores in L2 first.
-DEV uint32_t ld_out8(const uint8_t* p) {
-    return __hip_atomic_load(const_cast<uint8_t*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-DEV uint32_t ld_out32(const uint8_t* p) {  // 4 bytes at any address
-    const uintptr_t a = (uintptr_t)p;
-    uint32_t* q = (uint32_t*)(a & ~(uintptr_t)3);
-    const uint32_t sh = (uint32_t)(a & 3);
-    const uint32_t lo = __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const uint32_t hi = sh ? __hip_atomic_load(q + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
-    return __builtin_amdgcn_alignbyte(hi, lo, sh);
-}
-
-// Output of one decode: the arena, plus an optional per-wave LDS ring of the
-// last kRing output bytes.  Near matches (offset + length <= kRing) read the
-// ring: LDS is in order within a wave, so no fence and no round trip through
-// L2.  Far matches read the arena behind a fence with L1-bypassing loads.
-typedef __attribute__((address_space(3))) uint8_t lds_u8;
-#ifndef RPGPU_RING_BYTES
-#define RPGPU_RING_BYTES 4096
-#endif
-constexpr int64_t kRing = RPGPU_RING_BYTES > 0 ? RPGPU_RING_BYTES : 1;  // 0: no ring
-constexpr uint32_t kRingWaves = 4;  // waves per workgroup of the decode kernels
-
-struct Out {
-    uint8_t* dst;
-    lds_u8* ring;    // nullptr: no ring
-    int64_t fenced;  // arena bytes below this are visible to loads
+struct Dec {
+    uint8_t* arena;           // decoded arena (global)
+    lds_u8* ring;             // this wave's kRing bytes
+    __amdgpu_buffer_rsrc_t rs;  // arena window for sc1 read-backs, based at `lo`
+    uint64_t lo;              // lowest position this decode may read (frame start)
+    uint64_t base;            // position of relative output 0
+    uint64_t op;              // next output position
+    uint64_t flushed;         // bytes below are stored to the arena
+    uint64_t confirmed;       // bytes below are visible to sc1 loads (vmcnt drained)
+    uint64_t ring_lo;         // the ring holds [max(ring_lo, op - kRing), op)
 };
 
-DEV void out_init(Out& o, uint8_t* dst, lds_u8* ring) {
-    o.dst = dst;
-    o.ring = ring;
-    o.fenced = 0;
+// matches waiting in the open group, lane j = j-th match
+struct Group {
+    uint32_t rop, off, ml;    // per lane: output position - m0, offset, length
+    uint32_t n;               // queued matches
+    uint64_t m0;              // output position of the first queued match
+};
+
+DEV void dec_init(Dec& d, uint8_t* arena, uint64_t arena_cap, lds_u8* ring, uint64_t at) {
+    d.arena = arena;
+    d.ring = ring;
+    d.lo = at;
+    d.base = at;
+    d.op = at;
+    d.flushed = at;
+    d.confirmed = at;
+    d.ring_lo = at;
+    // read-backs past the arena's end return zeros instead of faulting
+    const uint64_t room = arena_cap > at ? arena_cap - at : 0;
+    d.rs = __builtin_amdgcn_make_buffer_rsrc(arena + at, 0, (int)(room < 0x7FFFFFFFull ? room : 0x7FFFFFFFull), kBufFlags);
 }
 
-DEV void put(Out& o, int64_t at, uint32_t v, bool valid) {
-    if (valid) {
-        o.dst[at] = (uint8_t)v;
-        if (o.ring) o.ring[at & (kRing - 1)] = (uint8_t)v;
+DEV void wait_vm() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
+// make every stored byte below `upto` visible to the sc1 read-backs
+DEV void confirm(Dec& d, uint64_t upto) {
+    if (upto > d.confirmed) {
+        wait_vm();
+        d.confirmed = d.flushed;
     }
 }
 
-// Bulk copy of bytes this decode does not write (its input) to the output at
-// op: bytes up to the destination's 16-byte alignment, then 16 bytes per lane
-// (1 KiB per wave store, four stores' loads issued together) assembled from
-// aligned dword loads of the source, then the < 16-byte tail.  The ring
-// receives the copy's last kRing bytes.  (Byte-per-lane copies moved 64 bytes
-// per load round trip: 0.03 B/cycle per wave on stored LZ4 blocks.)
-DEV uint4 ld16_any(const uint8_t* s) {
-    const uint32_t* q = (const uint32_t*)((uintptr_t)s & ~(uintptr_t)3);
-    const uint32_t sh = (uint32_t)((uintptr_t)s & 3);
-    const uint32_t w0 = q[0], w1 = q[1], w2 = q[2], w3 = q[3];
-    const uint32_t w4 = sh ? q[4] : 0u;  // holds byte 15 only when the source is unaligned
-    return make_uint4(__builtin_amdgcn_alignbyte(w1, w0, sh), __builtin_amdgcn_alignbyte(w2, w1, sh),
-                      __builtin_amdgcn_alignbyte(w3, w2, sh), __builtin_amdgcn_alignbyte(w4, w3, sh));
+DEV uint32_t rd_back8(const Dec& d, uint64_t at) {
+    return __builtin_amdgcn_raw_buffer_load_b8(d.rs, (uint32_t)(at - d.lo), 0, kSc1);
 }
 
-DEV void copy_bulk(Out& o, int64_t op, const uint8_t* src, int64_t len) {
-    if (len <= 0) return;
-    const int64_t l = (int64_t)lane();
-    int64_t head = (int64_t)((16u - ((uintptr_t)(o.dst + op) & 15u)) & 15u);
-    if (head > len) head = len;
-    if (l < head) put(o, op + l, src[l], true);
-    const int64_t mid_end = head + ((len - head) & ~15ll);
-    const int64_t ring_from = len - kRing;  // bytes before this never reach the ring
-    for (int64_t c = head; c < mid_end; c += 4096) {
-        uint4 v[4];
+// store ring bytes [d.flushed, upto) to the arena: whole 16-byte pieces as
+// one ds_read_b128 + global_store_dwordx4 per lane (1 KiB per wave
+// instruction), ragged edge pieces byte by byte.  The trip count is made
+// uniform up front: a loop whose exit the compiler treats per lane left
+// chunks unstored (lanes dropped from EXEC) when it was written as
+// while (flushed < upto).
+DEV void flush(Dec& d, uint64_t upto) {
+    const uint64_t f = uni64(d.flushed);
+    upto = uni64(upto);
+    if (f >= upto) return;
+    TRACE("flush %llu..%llu\n", (unsigned long long)f, (unsigned long long)upto);
+    const uint32_t l = lane();
+    const uint64_t c_first = f & ~1023ull;
+    const uint32_t nchunks = uni32((uint32_t)((((upto + 1023) & ~1023ull) - c_first) >> 10));
+    for (uint32_t i = 0; i < nchunks; i++) {
+        const uint64_t a = c_first + ((uint64_t)i << 10) + 16u * l;
+        const uint32_t r = (uint32_t)a & kRM;
+        if (a >= f && a + 16 <= upto) {
+            *(v4u32*)(d.arena + a) = *(const lds_v4*)(d.ring + r);
+        } else if (a + 16 > f && a < upto) {
 #pragma unroll
-        for (int u = 0; u < 4; u++) {
-            const int64_t k = c + 1024 * u + 16 * l;
-            if (k < mid_end) v[u] = ld16_any(src + k);
+            for (uint32_t b = 0; b < 16; b++)
+                if (a + b >= f && a + b < upto) d.arena[a + b] = d.ring[r + b];
         }
+    }
+    d.flushed = upto;
+}
+
+// flush whole chunks only (the ragged tail stays in the ring until the end)
+DEV void flush_chunks(Dec& d) { flush(d, d.op & ~1023ull); }
+
+// ---------------------------------------------------------------------------
+// match groups
+// ---------------------------------------------------------------------------
+DEV void group_init(Group& g) {
+    g.rop = g.off = g.ml = 0;
+    g.n = 0;
+    g.m0 = 0;
+}
+
+DEV uint32_t wave_max(uint32_t v) {
 #pragma unroll
-        for (int u = 0; u < 4; u++) {
-            const int64_t k = c + 1024 * u + 16 * l;
-            if (k < mid_end) {
-                *(uint4*)(o.dst + op + k) = v[u];
-                if (o.ring && k + 16 > ring_from) {
-                    const int64_t at = op + k;
-                    if (((uintptr_t)o.dst & 15u) == 0) {  // ring slot 16-byte aligned as well
-                        typedef __attribute__((address_space(3))) uint32_t lds_u32;
-                        lds_u32* r = (lds_u32*)(o.ring + (at & (kRing - 1)));
-                        r[0] = v[u].x;
-                        r[1] = v[u].y;
-                        r[2] = v[u].z;
-                        r[3] = v[u].w;
-                    } else {
-                        const uint32_t wv[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+    for (int o = 32; o > 0; o >>= 1) {
+        const uint32_t w = (uint32_t)__shfl_xor((int)v, o, 64);
+        v = w > v ? w : v;
+    }
+    return v;
+}
+
+// one match, uniform, sources final (written or in the arena): each source
+// byte from the ring when the ring still holds it, else read back from the
+// arena.  `top` = the highest position written so far.  Handles overlap
+// (off < ml) and off == 0 (zeros, as liblz4's write32(op, 0) /
+// LZ4_memcpy_using_offset_base produce).  Long copies flush as they go so
+// the ring never overwrites unstored bytes.
+DEV uint64_t ring_bound(const Dec& d, uint64_t top) {
+    const uint64_t r = top > kRing ? top - kRing : 0;
+    return r > d.ring_lo ? r : d.ring_lo;
+}
+
+DEV void match_serial(Dec& d, uint64_t op, uint32_t off, uint32_t ml, uint64_t top) {
+    const uint32_t l = lane();
+    TRACE("serial op=%llu off=%u ml=%u top=%llu\n", (unsigned long long)op, off, ml, (unsigned long long)top);
+    const uint32_t o32 = (uint32_t)op;
+    if (off == 0) {
+        for (uint32_t c = 0; c < ml; c += 64) {
+            if (c + l < ml) d.ring[(o32 + c + l) & kRM] = 0;
+            d.op = op + (c + 64 < ml ? c + 64 : ml);
+            if ((d.op & ~1023ull) > d.flushed + 2048) flush_chunks(d);
+        }
+        return;
+    }
+    const uint64_t s = op - off;
+    const uint32_t s32 = (uint32_t)s;
+    if (off < 64 && off < ml) {
+        // period off: lanes k < L = off * floor(64 / off) hold the pattern
+        // once; every chunk of L output bytes repeats it
+        const uint32_t L = off * (64u / off);
+        const uint32_t k = l < L ? l : 0u;
+        // k mod off: with inv = floor(2^16 / off) + 1 the quotient
+        // (k * inv) >> 16 is exact for k < 64, off < 64
+        const uint32_t inv = 65536u / off + 1u;
+        const uint32_t kmod = k - off * ((k * inv) >> 16);
+        const uint64_t bnd = ring_bound(d, top > op + 64 ? top : op + 64);
+        if (s < bnd) confirm(d, bnd);
+        const uint32_t v = s + kmod >= bnd ? (uint32_t)d.ring[(s32 + kmod) & kRM] : rd_back8(d, s + kmod);
+        for (uint32_t c = 0; c < ml; c += L) {
+            if (l < L && c + l < ml) d.ring[(o32 + c + l) & kRM] = (uint8_t)v;
+            d.op = op + (c + L < ml ? c + L : ml);
+            if ((d.op & ~1023ull) > d.flushed + 2048) flush_chunks(d);
+        }
+        return;
+    }
+    // 64-byte steps; with off >= 64 every source byte is final before it is read
+    for (uint32_t c = 0; c < ml; c += 64) {
+        const uint64_t wt = op + c + 64;
+        const uint64_t bnd = ring_bound(d, top > wt ? top : wt);
+        if (s + c < bnd) confirm(d, bnd);
+        const bool act = c + l < ml;
+        const uint32_t cut = s + c >= bnd ? 0u : (uint32_t)(bnd - (s + c) < 64 ? bnd - (s + c) : 64);
+        uint32_t v = d.ring[(s32 + c + l) & kRM];
+        if (act && l < cut) v = rd_back8(d, s + c + l);
+        if (act) d.ring[(o32 + c + l) & kRM] = (uint8_t)v;
+        d.op = op + (c + 64 < ml ? c + 64 : ml);
+        if ((d.op & ~1023ull) > d.flushed + 2048) flush_chunks(d);
+    }
+}
+
+// run the open group (see the header).  Every byte below d.op other than
+// the queued matches' outputs is already in the ring.  Per-lane arithmetic
+// is 32-bit: ring slots only need the low bits of a position, and every
+// source lies within 4 GiB above d.lo.
+DEV void group_exec(Dec& d, Group& g) {
+    if (g.n == 0) return;
+    const uint32_t l = lane();
+    const bool mine = l < g.n;
+    const uint64_t end = d.op;
+    const uint64_t near_lo = ring_bound(d, end);
+    // relative to d.lo (all sources are at or above it)
+    const uint32_t m0r = (uint32_t)(g.m0 - d.lo);
+    const uint32_t opr = m0r + g.rop;
+    const uint32_t sr = opr - g.off;
+    const uint32_t nlr = (uint32_t)(near_lo - d.lo);
+    const uint32_t lo32 = (uint32_t)d.lo;  // ring slot of relative position p: (lo32 + p) & kRM
+    const bool indep = mine && sr + g.ml <= m0r;
+    const bool near = sr >= nlr;
+    const bool ring_par = indep && near;
+    const bool far_par = indep && !near && g.ml <= kFarMax;
+    TRACE("group n=%u m0=%llu end=%llu ring=%llx far=%llx\n", g.n, (unsigned long long)g.m0, (unsigned long long)end,
+          (unsigned long long)__ballot(ring_par), (unsigned long long)__ballot(far_par));
+    // lane-parallel, sources in the ring
+    if (__ballot(ring_par)) {
+        const uint32_t kmax = wave_max(ring_par ? g.ml : 0u);
+        const uint32_t rs = lo32 + sr, ro = lo32 + opr;
+        for (uint32_t k = 0; k < kmax; k += 8) {
+            uint32_t v[8];
 #pragma unroll
-                        for (int b = 0; b < 16; b++) o.ring[(at + b) & (kRing - 1)] = (uint8_t)(wv[b >> 2] >> (8 * (b & 3)));
-                    }
+            for (int i = 0; i < 8; i++) v[i] = d.ring[(rs + k + i) & kRM];
+#pragma unroll
+            for (int i = 0; i < 8; i++)
+                if (ring_par && k + i < g.ml) d.ring[(ro + k + i) & kRM] = (uint8_t)v[i];
+        }
+    }
+    // lane-parallel, sources read back from the arena: 64 bytes from the
+    // 16-aligned address at or below the source, each byte placed by its
+    // window offset; bytes at or above near_lo (a source straddling a direct
+    // copy's end) come from the ring, where they may not be stored yet
+    if (__ballot(far_par)) {
+        confirm(d, d.lo + wave_max(far_par ? sr + g.ml : 0u));
+        const uint32_t sa = sr & 15u;
+        // unconditional: lanes outside far_par read harmless bytes (the
+        // resource returns zeros past its range)
+        uint32_t qa[16];
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            auto t = __builtin_amdgcn_raw_buffer_load_b128(d.rs, far_par ? (sr & ~15u) + 16 * i : 0u, 0, kSc1);
+            qa[4 * i] = t[0];
+            qa[4 * i + 1] = t[1];
+            qa[4 * i + 2] = t[2];
+            qa[4 * i + 3] = t[3];
+        }
+        const uint32_t cut = (far_par && sr + g.ml > nlr) ? nlr - sr : 0xFFFFFFFFu;
+        const uint32_t ws = lo32 + sr - sa, wo = lo32 + opr - sa;  // ring slots of window byte 0
+        const uint32_t kend = far_par ? sa + g.ml : 0u;            // window bytes [sa, kend) are the source
+        const uint32_t tmax = (wave_max(kend) + 3) >> 2;
+#pragma unroll 1
+        for (uint32_t t = 0; t < tmax; t++) {
+            const uint32_t dw = qa[t];  // uniform index: v_movrels
+#pragma unroll
+            for (uint32_t b = 0; b < 4; b++) {
+                const uint32_t w = 4 * t + b;
+                if (w >= sa && w < kend) {
+                    uint32_t byte = (dw >> (8 * b)) & 0xFFu;
+                    if (w - sa >= cut) byte = d.ring[(ws + w) & kRM];
+                    d.ring[(wo + w) & kRM] = (uint8_t)byte;
                 }
             }
         }
     }
-    if (l < len - mid_end) put(o, op + mid_end + l, src[mid_end + l], true);
-}
-
-// literals: src[ip, ip + len) -> out[op, ...).  Bytes inside the 256-byte
-// input window come from its registers (ds_bpermute), the rest from memory;
-// long runs take the bulk copy.
-DEV void copy_lit(Out& o, int64_t op, In& in, const uint8_t* src, int64_t ip, int64_t len) {
-    if (len <= 0) return;
-    if (len >= 256) {
-        copy_bulk(o, op, src + ip, len);
-        return;
-    }
-    if (ip < in.base || ip >= in.base + 192) in_load(in, ip);
-    for (int64_t c = 0; c < len; c += 64) {
-        const int64_t k = c + (int64_t)lane();
-        const bool valid = k < len;
-        const int64_t w = ip + k - in.base;
-        const bool inwin = w >= 0 && w < 256;
-        const uint32_t word = (uint32_t)__shfl((int)in.w, (int)((w >> 2) & 63), 64);
-        uint32_t v = (word >> (8 * (uint32_t)(w & 3))) & 0xFFu;
-        if (valid && !inwin) v = src[ip + k];
-        put(o, op + k, v, valid);
-    }
-}
-
-// raw bytes straight from memory (stored LZ4 blocks)
-DEV void copy_raw(Out& o, int64_t op, const uint8_t* src, int64_t ip, int64_t len) { copy_bulk(o, op, src + ip, len); }
-
-// forward copy out[op + k] = out[op + k - off] (k < len): with off < len the
-// source repeats with period off; off == 0 writes zeros (as liblz4's
-// write32(op, 0) / LZ4_memcpy_using_offset_base produce)
-DEV void copy_match(Out& o, int64_t op, int64_t off, int64_t len) {
-    if (len <= 0) return;
-    if (off == 0) {
-        for (int64_t c = 0; c < len; c += 64) put(o, op + c + lane(), 0u, c + (int64_t)lane() < len);
-        return;
-    }
-    const int64_t s0 = op - off;
-    if (o.ring && off + len <= kRing) {
-        // every source byte is below op and within the ring
-        for (int64_t c = 0; c < len; c += 64) {
-            const int64_t k = c + (int64_t)lane();
-            const bool valid = k < len;
-            const int64_t sk = off >= len ? k : (int64_t)((uint32_t)k % (uint32_t)off);
-            const uint32_t v = valid ? (uint32_t)o.ring[(s0 + sk) & (kRing - 1)] : 0u;
-            put(o, op + k, v, valid);
+    // in order: matches whose sources lie inside the group (or that are too
+    // long for the lane-parallel read-back)
+    const uint64_t serial = __ballot(mine && !ring_par && !far_par);
+    if (serial) {
+        const uint64_t keep = d.op;
+        uint64_t m = serial;
+        while (m) {
+            const int j = __builtin_ctzll(m);
+            m &= m - 1;
+            const uint64_t o = g.m0 + rl(g.rop, j);
+            match_serial(d, o, rl(g.off, j), rl(g.ml, j), keep);
         }
-        return;
+        d.op = keep;
     }
-    const int64_t span = off < len ? off : len;
-    if (s0 + span > o.fenced) {
-        vis_fence();
-        o.fenced = op;
-    }
-    for (int64_t c = 0; c < len; c += 64) {
-        const int64_t k = c + (int64_t)lane();
-        const bool valid = k < len;
-        const int64_t sk = off >= len ? k : (int64_t)((uint32_t)k % (uint32_t)off);
-        const uint32_t v = valid ? ld_out8(o.dst + s0 + sk) : 0u;
-        put(o, op + k, v, valid);
-    }
+    g.n = 0;
+    flush_chunks(d);
 }
 
-// XXH32 (lz4 1.9.3 xxhash.c), uniform over global memory
-DEV uint32_t rotl32(uint32_t x, int r) { return (x << r) | (x >> (32 - r)); }
-template <bool OUT>
-DEV uint32_t xxh32_t(const uint8_t* p, int64_t n, uint32_t seed);
-DEV uint32_t xxh32_dev(const uint8_t* p, int64_t n, uint32_t seed) { return xxh32_t<false>(p, n, seed); }
-DEV uint32_t xxh32_out(const uint8_t* p, int64_t n, uint32_t seed) { return xxh32_t<true>(p, n, seed); }
+// One sequence at d.op: the literal bytes [lip, lip + llen) of the stream,
+// then (has_match) a match (off, ml).  The open group closes first when it
+// cannot take the sequence (one group_exec call site per parser).  Literals
+// up to 64 bytes are one byte per lane from the input window (ds_bpermute);
+// longer ones stream 16 bytes per lane from global memory.  Matches join
+// the group unless they are long or have offset 0.
+DEV void emit_seq(Dec& d, Group& g, In& in, int64_t lip, int64_t llen, uint32_t off, uint32_t ml, bool has_match) {
+    const uint32_t l = lane();
+    const bool big_lit = llen > 64;
+    const bool big_match = has_match && (off == 0 || ml > 64);
+    const uint64_t mend = d.op + (uint64_t)llen + (has_match ? ml : 0u);
+    if (g.n && (big_lit || big_match || g.n == 64 || mend - g.m0 > (uint64_t)kSpan)) group_exec(d, g);
+    const uint64_t op = d.op;
+    if (llen > 0 && !big_lit) {
+        if (lip < in.base || lip + llen > in.base + 512) in_load(in, lip);
+        const int64_t o = lip + (int64_t)l - in.base;  // lanes < llen: inside the window
+        const int li = (int)((o >> 2) & 63);
+        const uint32_t v0 = (uint32_t)__shfl((int)in.w0, li, 64);
+        const uint32_t v1 = (uint32_t)__shfl((int)in.w1, li, 64);
+        const uint32_t w = o < 256 ? v0 : v1;
+        if ((int64_t)l < llen) d.ring[((uint32_t)op + l) & kRM] = (uint8_t)(w >> (8 * (uint32_t)(o & 3)));
+        d.op = op + (uint64_t)llen;
+    } else if (big_lit) {
+        const uint8_t* src = in.src + lip;
+        const uint32_t o32 = (uint32_t)op;
+        for (int64_t c = 0; c < llen; c += 1024) {
+            const int64_t k = c + 16 * (int64_t)l;
+            const uint32_t r = o32 + (uint32_t)k;
+            if (k + 16 <= llen) {
+                const uint4 v = ld16u(src + k);
+                const uint32_t wv[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+                for (int bb = 0; bb < 16; bb++) d.ring[(r + bb) & kRM] = (uint8_t)(wv[bb >> 2] >> (8 * (bb & 3)));
+            } else {
+                for (int64_t bb = k; bb < llen && bb < k + 16; bb++) d.ring[(o32 + (uint32_t)bb) & kRM] = src[bb];
+            }
+            d.op = op + (uint64_t)(c + 1024 < llen ? c + 1024 : llen);
+            flush_chunks(d);
+        }
+    }
+    if (!has_match) return;
+    const uint64_t mo = d.op;
+    if (big_match) {
+        match_serial(d, mo, off, ml, mo);
+        d.op = mo + ml;
+        flush_chunks(d);
+        return;
+    }
+    if (g.n == 0) g.m0 = mo;
+    const uint32_t j = g.n;
+    const bool me = l == j;
+    g.rop = me ? (uint32_t)(mo - g.m0) : g.rop;
+    g.off = me ? off : g.off;
+    g.ml = me ? ml : g.ml;
+    g.n = j + 1;
+    d.op = mo + ml;
+}
 
-// OUT: p is output this wave (or this kernel) wrote: L1-bypassing loads
-template <bool OUT>
-DEV uint32_t xxh32_t(const uint8_t* p, int64_t n, uint32_t seed) {
+// end of a decode: everything queued is run and stored
+DEV void dec_finish(Dec& d, Group& g) {
+    group_exec(d, g);
+    flush(d, d.op);
+}
+
+// a run of raw bytes straight to the arena (stored LZ4 blocks): 16 bytes per
+// lane, 4 KiB per step, then the ring no longer covers what lies below
+DEV void copy_direct(Dec& d, Group& g, const uint8_t* src, int64_t len) {
+    if (len <= 0) return;
+    TRACE_ITEM("  cd enter op %llu len %lld\n", (unsigned long long)d.op, (long long)len);
+    dec_finish(d, g);
+    TRACE_ITEM("  cd finished\n");
+    const int64_t l = lane();
+    uint8_t* dst = d.arena + d.op;
+    int64_t head = (int64_t)((16u - ((uintptr_t)dst & 15u)) & 15u);
+    if (head > len) head = len;
+    if (l < head) dst[l] = src[l];
+    const int64_t mid = head + ((len - head) & ~15ll);
+    for (int64_t c = head; c < mid; c += 4096) {
+        uint4 v[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const int64_t k = c + 1024 * u + 16 * l;
+            if (k < mid) v[u] = ld16u(src + k);
+        }
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const int64_t k = c + 1024 * u + 16 * l;
+            if (k < mid) *(uint4*)(dst + k) = v[u];
+        }
+    }
+    if (l < len - mid) dst[mid + l] = src[mid + l];
+    TRACE_ITEM("  cd copied\n");
+    d.op += (uint64_t)len;
+    d.flushed = d.op;
+    d.ring_lo = d.op;
+}
+
+// ---------------------------------------------------------------------------
+// XXH32 (lz4 1.9.3 xxhash.c): stripes streamed 1 KiB per row (lane l holds
+// stripe 64 r + l, pre-multiplied by PRIME2), the four accumulators advance
+// on the scalar unit, one readlane per word.  Read with sc1 loads so bytes
+// this kernel stored are seen.
+// ---------------------------------------------------------------------------
+DEV uint32_t rotl32(uint32_t x, int r) { return (x << r) | (x >> (32 - r)); }
+
+__device__ __attribute__((noinline)) uint32_t xxh32_wave(const uint8_t* p, uint64_t n, uint32_t seed) {
     const uint32_t P1 = 0x9E3779B1u, P2 = 0x85EBCA77u, P3 = 0xC2B2AE3Du, P4 = 0x27D4EB2Fu, P5 = 0x165667B1u;
-    int64_t i = 0;
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(p), 0, 0x7FFFFFFF, kBufFlags);
+    const uint32_t l = lane();
+    uint64_t i = 0;
     uint32_t h;
     if (n >= 16) {
         uint32_t v1 = seed + P1 + P2, v2 = seed + P2, v3 = seed, v4 = seed - P1;
-        for (; i + 16 <= n; i += 16) {
-            v1 = rotl32(v1 + (OUT ? ld_out32(p + i) : ldu32(p + i)) * P2, 13) * P1;
-            v2 = rotl32(v2 + (OUT ? ld_out32(p + i + 4) : ldu32(p + i + 4)) * P2, 13) * P1;
-            v3 = rotl32(v3 + (OUT ? ld_out32(p + i + 8) : ldu32(p + i + 8)) * P2, 13) * P1;
-            v4 = rotl32(v4 + (OUT ? ld_out32(p + i + 12) : ldu32(p + i + 12)) * P2, 13) * P1;
+        const uint64_t nst = n / 16;
+        auto row = [&](uint64_t r) __attribute__((always_inline)) {
+            uint4 q = make_uint4(0, 0, 0, 0);
+            if (r * 64 + l < nst) {
+                auto t = __builtin_amdgcn_raw_buffer_load_b128(rs, (uint32_t)(16 * (r * 64 + l)), 0, kSc1);
+                q = make_uint4(t[0], t[1], t[2], t[3]);
+            }
+            return q;
+        };
+        uint4 cur = row(0);
+        for (uint64_t r = 0; r * 64 < nst; r++) {
+            const uint4 nxt = row(r + 1);
+            const uint32_t x = cur.x * P2, y = cur.y * P2, z = cur.z * P2, w = cur.w * P2;
+            const uint32_t cnt = (uint32_t)(nst - r * 64 < 64 ? nst - r * 64 : 64);
+            for (uint32_t k = 0; k < cnt; k++) {
+                v1 = rotl32(v1 + rl(x, (int)k), 13) * P1;
+                v2 = rotl32(v2 + rl(y, (int)k), 13) * P1;
+                v3 = rotl32(v3 + rl(z, (int)k), 13) * P1;
+                v4 = rotl32(v4 + rl(w, (int)k), 13) * P1;
+            }
+            cur = nxt;
         }
+        i = nst * 16;
         h = rotl32(v1, 1) + rotl32(v2, 7) + rotl32(v3, 12) + rotl32(v4, 18);
     } else {
         h = seed + P5;
     }
     h += (uint32_t)n;
-    for (; i + 4 <= n; i += 4) h = rotl32(h + (OUT ? ld_out32(p + i) : ldu32(p + i)) * P3, 17) * P4;
-    for (; i < n; i++) h = rotl32(h + (OUT ? ld_out8(p + i) : (uint32_t)p[i]) * P5, 11) * P1;
+    // the last < 16 bytes: lane k < 16 holds byte i + k
+    const uint32_t rem = (uint32_t)(n - i);
+    const uint32_t b = l < rem ? __builtin_amdgcn_raw_buffer_load_b8(rs, (uint32_t)(i + l), 0, kSc1) : 0u;
+    uint32_t k = 0;
+    for (; k + 4 <= rem; k += 4) {
+        const uint32_t wd = rl(b, (int)k) | (rl(b, (int)k + 1) << 8) | (rl(b, (int)k + 2) << 16) | (rl(b, (int)k + 3) << 24);
+        h = rotl32(h + wd * P3, 17) * P4;
+    }
+    for (; k < rem; k++) h = rotl32(h + rl(b, (int)k) * P5, 11) * P1;
     h ^= h >> 15;
     h *= P2;
     h ^= h >> 13;
@@ -271,7 +517,8 @@ DEV uint32_t xxh32_t(const uint8_t* p, int64_t n, uint32_t seed) {
 // ---------------------------------------------------------------------------
 // LZ4 block: rpo_lz4_block_decode (oracle) = lz4 1.9.3 LZ4_decompress_generic
 // for LZ4_decompress_safe_usingDict (fast loop + safe loop, every check).
-// Returns the decoded length or -1.  H = history bytes before dst.
+// Output starts at d.op; H = history bytes before it.  Returns the decoded
+// length or -1.
 // ---------------------------------------------------------------------------
 constexpr int64_t kMinMatch = 4, kLastLiterals = 5, kMfLimit = 12, kFastSafeDistance = 64;
 
@@ -294,74 +541,67 @@ DEV uint32_t lz_read_var(In& in, int64_t& ip, int64_t lencheck, bool loop_check,
     return length;
 }
 
-DEV int64_t lz4_block(In& in, const uint8_t* src, int64_t n, Out& o, int64_t obase, int64_t oend, int64_t H) {
+DEV int64_t lz4_block(In& in, int64_t n, Dec& d, Group& g, int64_t oend, int64_t H) {
     const int64_t iend = n;
     int64_t ip = 0, op = 0;
     const int64_t shortiend = iend - 14 - 2, shortoend = oend - 14 - 18;
     uint32_t token;
-    int64_t length, offset, cpy;
+    int64_t length, offset = 0, cpy = 0, lip = 0, llen = 0, ml = 0;
     int err;
+    bool last = false;
 
     if (oend == 0) return (n == 1 && in_byte(in, 0) == 0) ? 0 : -1;
     if (n == 0) return -1;
 
-    if (oend - op < kFastSafeDistance) goto safe_decode;
+    // The two loops of LZ4_decompress_generic as one: `safe` is the safe
+    // loop (entered for good at the first fast-loop exit); every path ends at
+    // `emit` with the sequence's literal (lip, llen) and match (offset, ml).
+    bool safe = oend - op < kFastSafeDistance;
     for (;;) {
         token = in_byte(in, ip++);
         length = token >> 4;
-        if (length == 15) {
-            length += lz_read_var(in, ip, iend - 15, true, true, err);
-            if (err == 1) return -1;
-            cpy = op + length;
-            if (cpy > oend - 32 || ip + length > iend - 32) goto safe_literal_copy;
-            copy_lit(o, obase + op, in, src, ip, length);
-            ip += length;
-            op = cpy;
-        } else {
-            cpy = op + length;
-            if (ip > iend - (16 + 1)) goto safe_literal_copy;
-            copy_lit(o, obase + op, in, src, ip, length);
-            ip += length;
-            op = cpy;
-        }
-        offset = in_le16(in, ip);
-        ip += 2;
-        length = token & 15;
-        if (length == 15) {
-            if (offset > op + H) return -1;
-            length += lz_read_var(in, ip, iend - kLastLiterals + 1, true, false, err);
-            if (err) return -1;
-            length += kMinMatch;
-            if (op + length >= oend - kFastSafeDistance) goto safe_match_copy;
-        } else {
-            length += kMinMatch;
-            if (op + length >= oend - kFastSafeDistance) goto safe_match_copy;
-            if (offset <= op + H && offset >= 8) {
-                copy_match(o, obase + op, offset, length);
-                op += length;
-                continue;
+        if (!safe) {
+            if (length == 15) {
+                length += lz_read_var(in, ip, iend - 15, true, true, err);
+                if (err == 1) return -1;
+                cpy = op + length;
+                if (cpy > oend - 32 || ip + length > iend - 32) { safe = true; goto safe_literal_copy; }
+            } else {
+                cpy = op + length;
+                if (ip > iend - (16 + 1)) { safe = true; goto safe_literal_copy; }
             }
+            lip = ip;
+            llen = length;
+            ip += length;
+            op = cpy;
+            offset = in_le16(in, ip);
+            ip += 2;
+            length = token & 15;
+            if (length == 15) {
+                if (offset > op + H) return -1;
+                length += lz_read_var(in, ip, iend - kLastLiterals + 1, true, false, err);
+                if (err) return -1;
+                length += kMinMatch;
+                if (op + length >= oend - kFastSafeDistance) { safe = true; goto safe_match_copy; }
+            } else {
+                length += kMinMatch;
+                if (op + length >= oend - kFastSafeDistance) { safe = true; goto safe_match_copy; }
+            }
+            if (offset > op + H) return -1;
+            ml = length;
+            goto emit;
         }
-        if (offset > op + H) return -1;
-        copy_match(o, obase + op, offset, length);
-        op += length;
-    }
-
-safe_decode:
-    for (;;) {
-        token = in_byte(in, ip++);
-        length = token >> 4;
         if (length != 15 && ip < shortiend && op <= shortoend) {
-            copy_lit(o, obase + op, in, src, ip, length);
+            lip = ip;
+            llen = length;
             op += length;
             ip += length;
             length = token & 15;
             offset = in_le16(in, ip);
             ip += 2;
             if (length != 15 && offset >= 8 && offset <= op + H) {
-                copy_match(o, obase + op, offset, length + kMinMatch);
-                op += length + kMinMatch;
-                continue;
+                ml = length + kMinMatch;
+                goto emit;
             }
             goto lbl_copy_match;
         }
@@ -371,14 +611,15 @@ safe_decode:
         }
         cpy = op + length;
     safe_literal_copy:
+        lip = ip;
+        llen = length;
         if (cpy > oend - kMfLimit || ip + length > iend - (2 + 1 + kLastLiterals)) {
             if (ip + length != iend || cpy > oend) return -1;
-            copy_lit(o, obase + op, in, src, ip, length);
             ip += length;
             op += length;
-            break;
+            last = true;
+            goto emit;
         }
-        copy_lit(o, obase + op, in, src, ip, length);
         ip += length;
         op = cpy;
         offset = in_le16(in, ip);
@@ -392,19 +633,14 @@ safe_decode:
         length += kMinMatch;
     safe_match_copy:
         if (offset > op + H) return -1;
-        if (offset > op) {
-            // match starts in the history (prefix / external dictionary)
-            if (op + length > oend - kLastLiterals) return -1;
-            copy_match(o, obase + op, offset, length);
-            op += length;
-            continue;
-        }
-        cpy = op + length;
-        if (cpy > oend - kMfLimit) {
-            if (cpy > oend - kLastLiterals) return -1;
-        }
-        copy_match(o, obase + op, offset, length);
-        op = cpy;
+        // a match starting in the history (offset > op) ends by oend - 5;
+        // so does one inside the block (cpy > oend - 12 -> cpy <= oend - 5)
+        if (op + length > oend - kLastLiterals) return -1;
+        ml = length;
+    emit:
+        emit_seq(d, g, in, lip, llen, (uint32_t)offset, (uint32_t)ml, !last);
+        if (last) break;
+        op += ml;
     }
     return op;
 }
@@ -414,52 +650,77 @@ safe_decode:
 // LZ4F_decompress loop of do_uncompressed, including its output-buffer
 // estimate (contentSize, or 4x the input; grown 1.5x + 1 KiB whenever a call
 // returns with it full), which decides how much of a truncated frame is
-// returned.  dst has room for the planned capacity (decode_capacity_dev).
-// Returns 0 (out_len set) or -1 where the reference throws.
+// returned.  Output at d.op, which has room for the planned capacity
+// (decode_capacity_dev).  Returns 0 (out_len set) or -1 where the reference
+// throws.
+//
+// single != 0: the stream is one planned block of a block-independent frame
+// (its data, then its checksum when kBlkChecksum): the header is not read,
+// the block is decoded with oend = bcap and the unit ends after it.
 // ---------------------------------------------------------------------------
-DEV int lz4f_decode(In& in, const uint8_t* s, int64_t n, Out& o, int64_t& out_len) {
+DEV int lz4_unit(In& in, const uint8_t* s, int64_t n, Dec& d, Group& g, uint32_t single, uint32_t bcap,
+                 int64_t& out_len) {
     out_len = 0;
-    if (n < 7) return -1;                                        // frameHeader_incomplete
-    const uint32_t magic = in_le32(in, 0);
-    int64_t pos;
-    if ((magic & 0xFFFFFFF0u) == 0x184D2A50u) {                  // skippable frame
-        if (n < 8) return -1;
-        pos = 4;
-        if (n - pos < 4) return 0;
-        const uint32_t sz = in_le32(in, pos);
-        pos += 4;
-        if (n - pos < (int64_t)sz) return 0;
-        pos += sz;
-        return pos < n ? -1 : 0;
+    int64_t pos, bmax;
+    bool linked, bcs, ccs;
+    uint64_t content_size, est;
+    if (single) {
+        pos = 0;
+        bmax = bcap;
+        linked = false;
+        bcs = (single & kBlkChecksum) != 0;
+        ccs = false;
+        content_size = 0;
+        est = ~0ull >> 2;
+    } else {
+        if (n < 7) return -1;                                    // frameHeader_incomplete
+        const uint32_t magic = in_le32(in, 0);
+        if ((magic & 0xFFFFFFF0u) == 0x184D2A50u) {              // skippable frame
+            if (n < 8) return -1;
+            pos = 4;
+            if (n - pos < 4) return 0;
+            const uint32_t sz = in_le32(in, pos);
+            pos += 4;
+            if (n - pos < (int64_t)sz) return 0;
+            pos += sz;
+            return pos < n ? -1 : 0;
+        }
+        if (magic != 0x184D2204u) return -1;                     // frameType_unknown
+        const uint32_t flg = in_byte(in, 4);
+        const int64_t hsize = 7 + (((flg >> 3) & 1) ? 8 : 0) + ((flg & 1) ? 4 : 0);
+        if (n < hsize) return -1;
+        if ((flg >> 1) & 1) return -1;                           // reservedFlag_set
+        if (((flg >> 6) & 3) != 1) return -1;                    // headerVersion_wrong
+        const uint32_t bd = in_byte(in, 5);
+        if ((bd >> 7) & 1) return -1;
+        const uint32_t bsid = (bd >> 4) & 7;
+        if (bsid < 4) return -1;                                 // maxBlockSize_invalid
+        if (bd & 15) return -1;
+        if (((xxh32_wave(s + 4, (uint64_t)(hsize - 5), 0) >> 8) & 0xFFu) != in_byte(in, hsize - 1)) return -1;
+        linked = !((flg >> 5) & 1);
+        bcs = (flg >> 4) & 1;
+        ccs = (flg >> 2) & 1;
+        const bool csf = (flg >> 3) & 1;
+        content_size = csf ? ((uint64_t)in_le32(in, 6) | ((uint64_t)in_le32(in, 10) << 32)) : 0;
+        bmax = bsid == 4 ? (64 << 10) : bsid == 5 ? (256 << 10) : bsid == 6 ? (1 << 20) : (4 << 20);
+        pos = hsize;
+        // compute_frame_uncompressed_size (lz4_frame_compressor.cc:115-121)
+        est = (content_size == 0 || content_size > (uint64_t)n * 255) ? (uint64_t)n * 4 : content_size;
     }
-    if (magic != 0x184D2204u) return -1;                         // frameType_unknown
-    const uint32_t flg = in_byte(in, 4);
-    const int64_t hsize = 7 + (((flg >> 3) & 1) ? 8 : 0) + ((flg & 1) ? 4 : 0);
-    if (n < hsize) return -1;
-    if ((flg >> 1) & 1) return -1;                               // reservedFlag_set
-    if (((flg >> 6) & 3) != 1) return -1;                        // headerVersion_wrong
-    const uint32_t bd = in_byte(in, 5);
-    if ((bd >> 7) & 1) return -1;
-    const uint32_t bsid = (bd >> 4) & 7;
-    if (bsid < 4) return -1;                                     // maxBlockSize_invalid
-    if (bd & 15) return -1;
-    if (((xxh32_dev(s + 4, hsize - 5, 0) >> 8) & 0xFFu) != in_byte(in, hsize - 1)) return -1;  // headerChecksum_invalid
-    const bool linked = !((flg >> 5) & 1);
-    const bool bcs = (flg >> 4) & 1;
-    const bool ccs = (flg >> 2) & 1;
-    const bool csf = (flg >> 3) & 1;
-    const uint64_t content_size = csf ? ((uint64_t)in_le32(in, 6) | ((uint64_t)in_le32(in, 10) << 32)) : 0;
-    const int64_t bmax = bsid == 4 ? (64 << 10) : bsid == 5 ? (256 << 10) : bsid == 6 ? (1 << 20) : (4 << 20);
-    pos = hsize;
-    // compute_frame_uncompressed_size (lz4_frame_compressor.cc:115-121)
-    uint64_t est = (content_size == 0 || content_size > (uint64_t)n * 255) ? (uint64_t)n * 4 : content_size;
     uint64_t remaining = content_size;
     int64_t out = 0;
-    for (;;) {
-        if (n - pos < 4) { out_len = out; return 0; }            // waiting for a block header
-        const uint32_t bh = in_le32(in, pos);
-        pos += 4;
-        if (bh == 0) break;                                      // end mark
+    const uint64_t start = d.op;
+    for (uint32_t blk_no = 0;; blk_no++) {
+        uint32_t bh;
+        if (single) {
+            if (blk_no) break;
+            bh = (uint32_t)(n - (bcs ? 4 : 0)) | ((single & kBlkRaw) ? 0x80000000u : 0u);
+        } else {
+            if (n - pos < 4) { out_len = out; return 0; }        // waiting for a block header
+            bh = in_le32(in, pos);
+            pos += 4;
+            if (bh == 0) break;                                  // end mark
+        }
         const int64_t bsz = bh & 0x7FFFFFFFu;
         if (bsz > bmax) return -1;                               // maxBlockSize_invalid
         if (bh & 0x80000000u) {
@@ -470,7 +731,7 @@ DEV int lz4f_decode(In& in, const uint8_t* s, int64_t n, Out& o, int64_t& out_le
                 const int64_t space = (int64_t)(est - (uint64_t)out), avail = n - pos;
                 int64_t k = left < avail ? left : avail;
                 if (k > space) k = space;
-                copy_raw(o, out, s, pos, k);
+                copy_direct(d, g, s + pos, k);
                 out += k;
                 pos += k;
                 left -= k;
@@ -481,7 +742,7 @@ DEV int lz4f_decode(In& in, const uint8_t* s, int64_t n, Out& o, int64_t& out_le
             }
             if (bcs) {
                 if (n - pos < 4) { out_len = out; return 0; }
-                if (in_le32(in, pos) != xxh32_dev(s + blk, bsz, 0)) return -1;
+                if (in_le32(in, pos) != xxh32_wave(s + blk, (uint64_t)bsz, 0)) return -1;
                 pos += 4;
             }
             continue;
@@ -490,18 +751,19 @@ DEV int lz4f_decode(In& in, const uint8_t* s, int64_t n, Out& o, int64_t& out_le
         if (pos == n) { out_len = out; return 0; }
         const int64_t need = bsz + (bcs ? 4 : 0);
         if (n - pos < need) { out_len = out; return 0; }         // dstage_storeCBlock: wait
-        if (bcs && in_le32(in, pos + bsz) != xxh32_dev(s + pos, bsz, 0)) return -1;
+        if (bcs && in_le32(in, pos + bsz) != xxh32_wave(s + pos, (uint64_t)bsz, 0)) return -1;
         In bin;
         in_init(bin, s + pos, bsz);
-        const int64_t d = lz4_block(bin, s + pos, bsz, o, out, bmax, linked ? out : 0);
-        if (d < 0) return -1;                                    // decompressionFailed
+        d.op = start + (uint64_t)out;
+        const int64_t dd = lz4_block(bin, bsz, d, g, bmax, linked ? out : 0);
+        if (dd < 0) return -1;                                   // decompressionFailed
         pos += need;
-        if (content_size) remaining -= (uint64_t)d;
+        if (content_size) remaining -= (uint64_t)dd;
         const int64_t space = (int64_t)(est - (uint64_t)out);
-        if (space >= bmax || d <= space) { out += d; continue; }
+        if (space >= bmax || dd <= space) { out += dd; continue; }
         // decoded into tmpOut: `space` bytes flushed now, the rest on later
         // calls — which only happen while input remains
-        int64_t pending = d - space;
+        int64_t pending = dd - space;
         out += space;
         while (pending) {
             if ((uint64_t)out == est) est = 1024 + ((est * 3) + 1) / 2;
@@ -511,11 +773,13 @@ DEV int lz4f_decode(In& in, const uint8_t* s, int64_t n, Out& o, int64_t& out_le
             pending -= f;
         }
     }
+    if (single) { out_len = out; return 0; }
     if (remaining) return -1;                                    // frameSize_wrong
     if (ccs) {
         if (n - pos < 4) { out_len = out; return 0; }
-        vis_fence();
-        if (in_le32(in, pos) != xxh32_out(o.dst, out, 0)) return -1;
+        dec_finish(d, g);
+        wait_vm();
+        if (in_le32(in, pos) != xxh32_wave(d.arena + start, (uint64_t)out, 0)) return -1;
         pos += 4;
     }
     out_len = out;
@@ -543,9 +807,16 @@ DEV int snappy_varint_in(In& in, int64_t pos, int64_t n, uint32_t& v, int64_t& u
     return -1;
 }
 
-// DecompressAllTags over [ip, n): succeeds iff the tags end exactly at n and
-// exactly ulen bytes come out
-DEV int snappy_tags(In& in, const uint8_t* s, int64_t n, int64_t ip, Out& o, int64_t obase, int64_t ulen) {
+// snappy_raw_checked: varint length, then DecompressAllTags over the rest:
+// succeeds iff the tags end exactly at n and exactly ulen bytes come out
+// (output from d.op)
+DEV int snappy_raw_checked(In& in, int64_t n, Dec& d, Group& g, int64_t& out_len) {
+    uint32_t ulen32;
+    int64_t ip;
+    if (snappy_varint_in(in, 0, n, ulen32, ip)) return -1;
+    // no tag sequence expands more than 64/3 per input byte
+    if ((uint64_t)ulen32 > 22ull * (uint64_t)n + 64) return -1;
+    const int64_t ulen = ulen32;
     int64_t op = 0;
     while (ip < n) {
         const uint32_t c = in_byte(in, ip);
@@ -556,8 +827,9 @@ DEV int snappy_tags(In& in, const uint8_t* s, int64_t n, int64_t ip, Out& o, int
         else extra = 4;
         if (n - ip < 1 + extra) return -1;
         ip++;
+        int64_t lip = 0, lit = 0, len = 0, off = 0;
         if ((c & 3) == 0) {
-            int64_t lit = (int64_t)(c >> 2) + 1;
+            lit = (int64_t)(c >> 2) + 1;
             if (lit >= 61) {
                 const int64_t ll = lit - 60;
                 uint32_t v = 0;
@@ -567,11 +839,9 @@ DEV int snappy_tags(In& in, const uint8_t* s, int64_t n, int64_t ip, Out& o, int
             }
             if (n - ip < lit) return -1;       // premature end of input
             if (ulen - op < lit) return -1;    // SnappyArrayWriter::Append overflow
-            copy_lit(o, obase + op, in, s, ip, lit);
-            op += lit;
+            lip = ip;
             ip += lit;
         } else {
-            int64_t len, off;
             if ((c & 3) == 1) {
                 len = 4 + ((c >> 2) & 7);
                 off = ((int64_t)(c >> 5) << 8) | in_byte(in, ip);
@@ -585,88 +855,106 @@ DEV int snappy_tags(In& in, const uint8_t* s, int64_t n, int64_t ip, Out& o, int
             ip += extra;
             // AppendFromSelf: Produced() <= offset - 1u || op_end > op_limit_
             if (off == 0 || op < off || ulen - op < len) return -1;
-            copy_match(o, obase + op, off, len);
-            op += len;
         }
+        emit_seq(d, g, in, lip, lit, (uint32_t)off, (uint32_t)len, (c & 3) != 0);
+        op += lit + len;
     }
-    return op == ulen ? 0 : -1;
-}
-
-DEV int snappy_raw_checked(In& in, const uint8_t* s, int64_t n, Out& o, int64_t obase, int64_t& out_len) {
-    uint32_t ulen;
-    int64_t used;
-    if (snappy_varint_in(in, 0, n, ulen, used)) return -1;
-    // no tag sequence expands more than 64/3 per input byte
-    if ((uint64_t)ulen > 22ull * (uint64_t)n + 64) return -1;
-    if (snappy_tags(in, s, n, used, o, obase, ulen)) return -1;
+    if (op != ulen) return -1;
     out_len = ulen;
     return 0;
 }
 
-DEV int snappy_raw(In& in, const uint8_t* s, int64_t n, Out& o, int64_t& out_len) {
-    uint32_t ulen;
-    int64_t used;
-    out_len = 0;
-    if (snappy_varint_in(in, 0, n, ulen, used)) return -1;
-    if (ulen == 0) return 0;  // "empty frame": RawUncompress is not called
-    return snappy_raw_checked(in, s, n, o, 0, out_len);
-}
-
-DEV int snappy_java(In& in, const uint8_t* s, int64_t n, Out& o, int64_t& out_len) {
+// snappy_java_compressor::uncompress: the xerial stream's chunks one after
+// the other, or the raw fallback (snappy_standard_compressor: length 0 is
+// an empty result, RawUncompress not called).  single: the stream is one
+// planned raw chunk.
+DEV int snappy_unit(In& in, const uint8_t* s, int64_t n, Dec& d, Group& g, uint32_t single, int64_t& out_len) {
     out_len = 0;
     const uint8_t magic[8] = {0x82, 'S', 'N', 'A', 'P', 'P', 'Y', 0};
-    bool java = n >= 16;
+    bool java = !single && n >= 16;
     for (int i = 0; i < 8 && java; i++) java = in_byte(in, i) == magic[i];
-    if (!java) return snappy_raw(in, s, n, o, out_len);
-    const int32_t min_version = (int32_t)in_le32(in, 12);  // native little endian
-    if (min_version < 1) return -1;
-    int64_t pos = 16, out = 0;
-    while (pos != n) {
-        if (n - pos < 4) return -1;                         // consume_be_type out_of_range
-        const int32_t clen = (int32_t)((in_byte(in, pos) << 24) | (in_byte(in, pos + 1) << 16) |
-                                       (in_byte(in, pos + 2) << 8) | in_byte(in, pos + 3));
-        pos += 4;
-        if (clen < 0) return -1;
-        if (n - pos < (int64_t)clen) return -1;             // consume_to out_of_range
+    int64_t pos = 0, out = 0;
+    if (java) {
+        const int32_t min_version = (int32_t)in_le32(in, 12);  // native little endian
+        if (min_version < 1) return -1;
+        pos = 16;
+    } else if (!single) {
+        uint32_t ulen;
+        int64_t used;
+        if (snappy_varint_in(in, 0, n, ulen, used)) return -1;
+        if (ulen == 0) return 0;  // "empty frame"
+    }
+    const uint64_t start = d.op;
+    for (;;) {
+        const uint8_t* cs = s;
+        int64_t clen = n;
+        if (java) {
+            if (pos == n) break;
+            if (n - pos < 4) return -1;                     // consume_be_type out_of_range
+            const int32_t cl = (int32_t)((in_byte(in, pos) << 24) | (in_byte(in, pos + 1) << 16) |
+                                         (in_byte(in, pos + 2) << 8) | in_byte(in, pos + 3));
+            pos += 4;
+            if (cl < 0) return -1;
+            if (n - pos < (int64_t)cl) return -1;           // consume_to out_of_range
+            cs = s + pos;
+            clen = cl;
+            pos += cl;
+        }
         In cin;
-        in_init(cin, s + pos, clen);
+        in_init(cin, cs, clen);
         int64_t got = 0;
-        if (snappy_raw_checked(cin, s + pos, clen, o, out, got)) return -1;
+        d.op = start + (uint64_t)out;
+        if (snappy_raw_checked(cin, clen, d, g, got)) return -1;
         out += got;
-        pos += clen;
+        if (!java) break;
     }
     out_len = out;
     return 0;
 }
 
 // compression::compressor::uncompress dispatch (compression/compression.cc:34-55)
-DEV int decode_payload(int codec, const uint8_t* s, int64_t n, uint8_t* dst, lds_u8* ring, int64_t& out_len) {
+// for one unit of work; output at d.op, complete and stored when it returns 0
+DEV int decode_unit(int codec, const uint8_t* s, int64_t n, Dec& d, uint32_t single, uint32_t bcap,
+                    int64_t& out_len) {
     out_len = 0;
     if (n == 0) return -1;
     In in;
     in_init(in, s, n);
-    Out o;
-    out_init(o, dst, ring);
-    if (codec == RPGPU_CODEC_SNAPPY) return snappy_java(in, s, n, o, out_len);
-    if (codec == RPGPU_CODEC_LZ4) return lz4f_decode(in, s, n, o, out_len);
-    return -1;
+    Group g;
+    group_init(g);
+    int rc = -1;
+    TRACE_ITEM("  unit codec %d\n", codec);
+    if (codec == RPGPU_CODEC_SNAPPY) rc = snappy_unit(in, s, n, d, g, single, out_len);
+    else if (codec == RPGPU_CODEC_LZ4) rc = lz4_unit(in, s, n, d, g, single, bcap, out_len);
+    TRACE_ITEM("  unit rc %d\n", rc);
+    if (rc == 0) dec_finish(d, g);  // a truncated frame may have decoded past out_len: harmless
+    TRACE_ITEM("  unit finished\n");
+    return rc;
 }
 
 // ---------------------------------------------------------------------------
-// Block-parallel decode.  A payload whose pieces are independent and whose
-// frame is structurally complete decodes to the concatenation of its pieces
-// (or fails when any piece fails): that is the sequential decoder's result
-// for such frames, since every flush of do_uncompressed happens while input
-// remains.  Those frames are split into BlockItems at the plan rule's
-// positions (decode_capacity_dev); everything else (linked LZ4 blocks,
-// truncated or malformed frames, raw snappy) takes the sequential path.
+// Planning: frames whose pieces are independent and that are structurally
+// complete decode to the concatenation of their pieces (or fail when any
+// piece fails): that is the sequential decoder's result for such frames,
+// since every flush of do_uncompressed happens while input remains.  Those
+// frames are split into BlockItems at the plan rule's positions
+// (decode_capacity_dev); everything else (linked LZ4 blocks, truncated or
+// malformed frames, raw snappy) is decoded whole by one wave.
 // ---------------------------------------------------------------------------
+
+// Wave-uniform atomic fetch-add of `v` (lane 0's contribution; the other
+// lanes add 0).  Every lane executes the atomic: written as
+// `if (lane() == 0) x = atomicAdd(..)` followed by readfirstlane, the
+// compiler's divergence analysis took the claimed value for a per-lane one
+// and built the claim loop of k_decode_blocks with a per-lane exit whose
+// lanes never all left (the decode kernel did not terminate).
+DEV uint32_t wave_fetch_add(uint32_t* p, uint32_t v) {
+    return uni32(atomicAdd(p, lane() == 0 ? v : 0u));
+}
 
 // reserve `nb` items (wave-uniform); UINT32_MAX when the list is full
 DEV uint32_t reserve_blocks(const DeviceJob& j, uint32_t nb) {
-    uint32_t first = 0;
-    if (lane() == 0) first = atomicAdd(&j.counters[4], nb);
-    first = rl(first, 0);
+    const uint32_t first = wave_fetch_add(&j.counters[4], nb);
     return ((uint64_t)first + nb <= j.block_capacity) ? first : 0xFFFFFFFFu;
 }
 
@@ -682,7 +970,7 @@ DEV bool plan_lz4f(const DeviceJob& j, In& in, int64_t n, uint64_t src_abs, uint
     const uint32_t bd = in_byte(in, 5);
     const uint32_t bsid = (bd >> 4) & 7;
     if (((bd >> 7) & 1) || bsid < 4 || (bd & 15)) return false;
-    if (((xxh32_dev(in.src + 4, hsize - 5, 0) >> 8) & 0xFFu) != in_byte(in, hsize - 1)) return false;
+    if (((xxh32_wave(in.src + 4, (uint64_t)(hsize - 5), 0) >> 8) & 0xFFu) != in_byte(in, hsize - 1)) return false;
     const bool bcs = (flg >> 4) & 1, ccs = (flg >> 2) & 1, csf = (flg >> 3) & 1;
     const int64_t bmax = bsid == 4 ? (64 << 10) : bsid == 5 ? (256 << 10) : bsid == 6 ? (1 << 20) : (4 << 20);
     // structure: every block present, the end mark, the content checksum,
@@ -800,39 +1088,27 @@ DEV bool plan_snappy_java(const DeviceJob& j, In& in, int64_t n, uint64_t src_ab
 
 // ---------------------------------------------------------------------------
 // k_decode: one wave per compressed batch of the job (work list built by
-// k_emit), claimed dynamically.  Block-parallel frames are only planned here;
-// the rest are decoded on the spot.  Each item writes only its own batch
-// result, its own plan and its own planned arena slot.
+// k_emit), wave-strided: the frame is planned into BlockItems, or queued
+// whole on the sequential list.  Each item writes only its own plan.
 // ---------------------------------------------------------------------------
-#if RPGPU_RING_BYTES > 0
-#define RP_WAVE_RING(name)                              \
-    __shared__ uint8_t name##_lds[kRingWaves * kRing]; \
-    lds_u8* name = (lds_u8*)(name##_lds + (threadIdx.x >> 6) * kRing)
-#else
-#define RP_WAVE_RING(name) lds_u8* name = nullptr
-#endif
-
 __global__ __launch_bounds__(256) void k_decode(DeviceJob j) {
-    RP_WAVE_RING(ring);
     const uint32_t count = j.counters[2];
-    for (;;) {
-        uint32_t item = 0;
-        if (lane() == 0) item = atomicAdd(&j.counters[3], 1u);
-        item = rl(item, 0);
-        if (item >= count) break;
-        const uint64_t b = j.decode_list[item];
-        rpgpu_batch_result* R = &j.batches[b];
+    const uint32_t nw = gridDim.x * (blockDim.x >> 6);
+    for (uint32_t item = blockIdx.x * (blockDim.x >> 6) + uni32(threadIdx.x >> 6); item < count; item += nw) {
+        const uint32_t b = j.decode_list[item];
+        const rpgpu_batch_result* R = &j.batches[b];
         const uint32_t seg = uni32(R->segment);
         const uint64_t S = uni64(j.seg_off[seg]) + uni64(R->file_pos) + RPGPU_HEADER_SIZE;
         const int64_t n = (int64_t)uni32((uint32_t)(R->size_bytes - (int32_t)RPGPU_HEADER_SIZE));
         const int codec = (int)(uni32((uint32_t)(uint16_t)R->attrs) & 7u);
         const uint64_t doff = uni64(j.dcap[b]);
         const uint64_t cap = uni64(j.dcap[b + 1]) - doff;
-        uint32_t addf = 0, dl = 0;
         FramePlan fp;
         fp.mode = 0;
+        fp.first = fp.nb = fp.ccs = fp.ccs_val = fp.csf = 0;
+        fp.content_size = 0;
         if (doff + cap > j.decoded_capacity) {
-            addf = RPGPU_F_DECODE_OVERFLOW;
+            fp.mode = 3;  // no room: DECODE_OVERFLOW
         } else {
             In in;
             in_init(in, j.data + S, n);
@@ -843,78 +1119,73 @@ __global__ __launch_bounds__(256) void k_decode(DeviceJob j) {
             }
             if (!planned) {
                 fp.mode = 0;
-                int64_t got = 0;
-                if (decode_payload(codec, j.data + S, n, j.decoded + doff, ring, got) == 0) {
-                    addf = RPGPU_F_CODEC_OK;
-                    dl = (uint32_t)got;
-                }
+                const uint32_t at = wave_fetch_add(&j.counters[6], 1u);
+                if (lane() == 0) j.seq_list[at] = item;
             }
         }
-        if (lane() == 0) {
-            if (j.block_capacity) j.plans[item] = fp;
-            if (addf) {
-                R->flags = R->flags | addf;
-                if (addf & RPGPU_F_CODEC_OK) R->decoded_len = dl;
-            }
-        }
+        if (lane() == 0) j.plans[item] = fp;
     }
 }
 
-// one wave per BlockItem, wave-strided (a dynamic lane-0 atomic claim here
-// compiled to a loop that never terminated on gfx950)
+// ---------------------------------------------------------------------------
+// k_decode_blocks: persistent waves take work by one agent-scope counter:
+// first the sequential frames (the longest items), then the BlockItems.
+// The claim is one lane-0 atomicAdd whose result is made uniform by
+// readfirstlane; `total` is read once, before the loop, so every wave
+// leaves the loop when its claim passes it.
+// ---------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void k_decode_blocks(DeviceJob j) {
-    RP_WAVE_RING(ring);
+    extern __shared__ __attribute__((aligned(16))) uint8_t dlds[];
+    // the wave's ring; readfirstlane makes its base provably wave-uniform
+    lds_u8* ring = (lds_u8*)(dlds + uni32(threadIdx.x >> 6) * kRing);
+    const uint32_t nseq = j.counters[6];
     const uint32_t reserved = j.counters[4];
-    const uint32_t count = reserved < j.block_capacity ? reserved : j.block_capacity;
-#ifdef RPGPU_CHECKED
-    const uint64_t t_start = __builtin_amdgcn_s_memtime();
-    if (blockIdx.x == 0 && threadIdx.x == 0) printf("RPGPU_CHECK blocks reserved=%u cap=%u\n", reserved, j.block_capacity);
-#endif
-    const uint32_t nw = gridDim.x * (blockDim.x >> 6);
-    for (uint32_t item = blockIdx.x * (blockDim.x >> 6) + uni32(threadIdx.x >> 6); item < count; item += nw) {
-#ifdef RPGPU_CHECKED
-        if (__builtin_amdgcn_s_memtime() - t_start > 20000000000ull) {
-            if (lane() == 0) printf("RPGPU_CHECK blocks timeout at item %u\n", item);
-            break;
-        }
-#endif
-        const BlockItem it = j.blocks[item];
-        const uint64_t srcp = uni64(it.src), dstp = uni64(it.dst);
-        const uint32_t csize = uni32(it.csize), kind = uni32(it.kind), bcap = uni32(it.cap);
-#ifdef RPGPU_CHECKED
-        if (lane() == 0)
-            printf("RPGPU_CHECK block %u src=%llu dst=%llu csize=%u kind=%u cap=%u dlen=%llu dcap=%llu\n", item,
-                   (unsigned long long)srcp, (unsigned long long)dstp, csize, kind, bcap,
-                   (unsigned long long)j.data_len, (unsigned long long)j.decoded_capacity);
-#endif
-        const uint8_t* src = j.data + srcp;
-        uint8_t* dst = j.decoded + dstp;
-        int64_t out = -1;
-        In in;
-        in_init(in, src, csize);
-        Out o;
-        out_init(o, dst, ring);
-        if (kind & kBlkSnappy) {
-            int64_t got = 0;
-            if (snappy_raw_checked(in, src, csize, o, 0, got) == 0) out = got;
+    const uint32_t nblk = reserved < j.block_capacity ? reserved : j.block_capacity;
+    const uint32_t total = nseq + nblk;
+    for (;;) {
+        const uint32_t item = wave_fetch_add(&j.counters[5], 1u);
+        if (item >= total) break;
+        // the unit: a whole frame (sequential list) or one planned piece
+        uint32_t b = 0, single = 0, bcap = 0, blk = 0;
+        int codec;
+        uint64_t src, dst;
+        int64_t n;
+        if (item < nseq) {
+            b = uni32(j.decode_list[uni32(j.seq_list[item])]);
+            const rpgpu_batch_result* R = &j.batches[b];
+            src = uni64(j.seg_off[uni32(R->segment)]) + uni64(R->file_pos) + RPGPU_HEADER_SIZE;
+            n = (int64_t)uni32((uint32_t)(R->size_bytes - (int32_t)RPGPU_HEADER_SIZE));
+            codec = (int)(uni32((uint32_t)(uint16_t)R->attrs) & 7u);
+            dst = uni64(j.dcap[b]);
         } else {
-            // dstage_getBlockChecksum before the block is used
-            bool ok = true;
-            if (kind & kBlkChecksum) {
-                In cin;
-                in_init(cin, src + csize, 4);
-                ok = in_le32(cin, 0) == xxh32_dev(src, csize, 0);
-            }
-            if (ok) {
-                if (kind & kBlkRaw) {
-                    copy_raw(o, 0, src, 0, csize);
-                    out = csize;
-                } else {
-                    out = lz4_block(in, src, csize, o, 0, bcap, 0);
+            blk = item - nseq;
+            const BlockItem it = j.blocks[blk];
+            const uint32_t kind = uni32(it.kind);
+            src = uni64(it.src);
+            dst = uni64(it.dst);
+            bcap = uni32(it.cap);
+            codec = (kind & kBlkSnappy) ? RPGPU_CODEC_SNAPPY : RPGPU_CODEC_LZ4;
+            single = kind | 0x100u;
+            n = (int64_t)uni32(it.csize) + ((kind & kBlkChecksum) ? 4 : 0);
+        }
+        Dec d;
+        dec_init(d, j.decoded, j.decoded_capacity, ring, dst);
+        int64_t got = 0;
+        TRACE_ITEM("item %u/%u wg %u w %u codec %d single %x n %lld src %llu dst %llu cap %u\n", item, total, blockIdx.x,
+                   threadIdx.x >> 6, codec, single, (long long)n, (unsigned long long)src, (unsigned long long)dst, bcap);
+        const int rc = decode_unit(codec, j.data + src, n, d, single, bcap, got);
+        TRACE_ITEM("done %u rc %d got %lld\n", item, rc, (long long)got);
+        if (lane() == 0) {
+            if (item < nseq) {
+                if (rc == 0) {
+                    rpgpu_batch_result* R = &j.batches[b];
+                    R->flags = R->flags | RPGPU_F_CODEC_OK;
+                    R->decoded_len = (uint32_t)got;
                 }
+            } else {
+                j.blocks[blk].out = (int32_t)(rc == 0 ? got : -1);
             }
         }
-        if (lane() == 0) j.blocks[item].out = (int32_t)(out < 0 ? -1 : out);
     }
 }
 
@@ -925,10 +1196,15 @@ __global__ __launch_bounds__(256) void k_decode_finish(DeviceJob j) {
     const uint32_t nw = gridDim.x * (blockDim.x >> 6);
     for (uint32_t item = blockIdx.x * (blockDim.x >> 6) + uni32(threadIdx.x >> 6); item < count; item += nw) {
         const FramePlan fp = j.plans[item];
-        if (uni32(fp.mode) == 0) continue;
-        const uint32_t first = uni32(fp.first), nb = uni32(fp.nb);
-        const uint64_t b = j.decode_list[item];
+        const uint32_t mode = uni32(fp.mode);
+        const uint32_t b = uni32(j.decode_list[item]);
         rpgpu_batch_result* R = &j.batches[b];
+        if (mode == 3) {
+            if (lane() == 0) R->flags = R->flags | RPGPU_F_DECODE_OVERFLOW;
+            continue;
+        }
+        if (mode == 0) continue;
+        const uint32_t first = uni32(fp.first), nb = uni32(fp.nb);
         const uint64_t d0 = uni64(j.dcap[b]);
         bool ok = true;
         uint64_t run = d0;  // where the next piece belongs
@@ -937,26 +1213,30 @@ __global__ __launch_bounds__(256) void k_decode_finish(DeviceJob j) {
             const int32_t out = (int32_t)uni32((uint32_t)it.out);
             if (out < 0) { ok = false; break; }
             const uint64_t at = uni64(it.dst);
+            if (at < run) { ok = false; break; }  // a piece longer than planned (cannot happen: out <= cap)
             if (at != run) {
-                // forward move to a lower address, 64 bytes per step: each
-                // step loads before it stores
-                uint8_t* d = j.decoded;
-                for (int64_t o = 0; o < out; o += 64) {
+                // forward move to a lower address in 1 KiB steps (each step
+                // loads before it stores; the gap is at least the shortfall)
+                uint8_t* dd = j.decoded;
+                const int64_t gap = (int64_t)(at - run);
+                const int64_t step = gap < 64 ? gap : 64;
+                for (int64_t o = 0; o < out; o += step) {
                     const int64_t k2 = o + lane();
                     uint8_t v = 0;
-                    if (k2 < out) v = (uint8_t)ld_out8(d + at + k2);
-                    __builtin_amdgcn_s_waitcnt(0);
-                    if (k2 < out) d[run + k2] = v;
+                    if (lane() < step && k2 < out) v = dd[at + k2];
+                    wait_vm();
+                    if (lane() < step && k2 < out) dd[run + k2] = v;
+                    wait_vm();
                 }
             }
             run += (uint64_t)out;
         }
         const uint64_t total = run - d0;
-        if (ok && uni32(fp.mode) == 1) {
+        if (ok && mode == 1) {
             if (uni32(fp.csf) && total != uni64(fp.content_size)) ok = false;  // frameSize_wrong
             if (ok && uni32(fp.ccs)) {
-                vis_fence();
-                if (xxh32_out(j.decoded + d0, (int64_t)total, 0) != uni32(fp.ccs_val)) ok = false;
+                wait_vm();
+                if (xxh32_wave(j.decoded + d0, total, 0) != uni32(fp.ccs_val)) ok = false;
             }
         }
         if (lane() == 0 && ok) {
@@ -967,14 +1247,25 @@ __global__ __launch_bounds__(256) void k_decode_finish(DeviceJob j) {
 }
 
 __global__ __launch_bounds__(64) void k_uncompress_one(int codec, const uint8_t* src, uint64_t n, uint8_t* dst,
-                                                       int64_t* res) {
-    RP_WAVE_RING(ring);
+                                                       uint64_t cap, int64_t* res) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t dlds[];
+    Dec d;
+    dec_init(d, dst, cap, (lds_u8*)dlds, 0);
     int64_t got = 0;
-    const int rc = decode_payload(codec, src, (int64_t)n, dst, ring, got);
+    const int rc = decode_unit(codec, src, (int64_t)n, d, 0, 0, got);
     if (lane() == 0) {
         res[0] = rc;
         res[1] = got;
     }
+}
+
+static void set_lds_attrs() {
+    static bool done = false;
+    if (done) return;
+    (void)hipFuncSetAttribute((const void*)k_decode_blocks, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)(kDecWaves * kRing));
+    (void)hipFuncSetAttribute((const void*)k_uncompress_one, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kRing);
+    done = true;
 }
 
 hipError_t launch_decode(const DeviceJob& j, hipStream_t s, uint32_t grid) {
@@ -983,19 +1274,20 @@ hipError_t launch_decode(const DeviceJob& j, hipStream_t s, uint32_t grid) {
 }
 
 hipError_t launch_decode_blocks(const DeviceJob& j, hipStream_t s, uint32_t grid) {
-    if (j.block_capacity) hipLaunchKernelGGL(k_decode_blocks, dim3(grid), dim3(256), 0, s, j);
+    set_lds_attrs();
+    hipLaunchKernelGGL(k_decode_blocks, dim3(grid), dim3(64 * kDecWaves), kDecWaves * kRing, s, j);
     return hipGetLastError();
 }
 
 hipError_t launch_decode_finish(const DeviceJob& j, hipStream_t s, uint32_t grid) {
-    if (j.block_capacity) hipLaunchKernelGGL(k_decode_finish, dim3(grid), dim3(256), 0, s, j);
+    hipLaunchKernelGGL(k_decode_finish, dim3(grid), dim3(256), 0, s, j);
     return hipGetLastError();
 }
 
 hipError_t launch_uncompress_one(int codec, const uint8_t* src, uint64_t n, uint8_t* dst, uint64_t cap, int64_t* res,
                                  hipStream_t s) {
-    (void)cap;
-    hipLaunchKernelGGL(k_uncompress_one, dim3(1), dim3(64), 0, s, codec, src, n, dst, res);
+    set_lds_attrs();
+    hipLaunchKernelGGL(k_uncompress_one, dim3(1), dim3(64), kRing, s, codec, src, n, dst, cap, res);
     return hipGetLastError();
 }
 

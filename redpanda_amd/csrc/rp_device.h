@@ -322,8 +322,14 @@ HD int snappy_varint32_dev(const uint8_t* s, uint64_t n, uint32_t* v) {
     return -1;
 }
 
-// Same rule as the oracle's rpo_decode_capacity (engine plan rule).
+// Same rule as the oracle's rpo_decode_capacity (engine plan rule): the
+// frame's planned bytes rounded up to 16, so every slot of the decoded
+// arena starts 16-byte aligned (whole-chunk stores)
+HD uint64_t decode_capacity_raw(int codec, const uint8_t* s, uint64_t n);
 HD uint64_t decode_capacity_dev(int codec, const uint8_t* s, uint64_t n) {
+    return (decode_capacity_raw(codec, s, n) + 15) & ~15ull;
+}
+HD uint64_t decode_capacity_raw(int codec, const uint8_t* s, uint64_t n) {
     if (n == 0) return 0;
     if (codec == RPGPU_CODEC_LZ4) {
         if (n < 7) return 0;

@@ -81,7 +81,7 @@ constexpr uint32_t kBlkRaw = 1, kBlkChecksum = 2, kBlkSnappy = 4;
 
 // Per decode item: how its payload is being decoded
 struct FramePlan {
-    uint32_t mode;   // 0 decoded sequentially by k_decode, 1 LZ4F blocks, 2 snappy-java chunks
+    uint32_t mode;   // 0 decoded whole by one wave, 1 LZ4F blocks, 2 snappy-java chunks, 3 no arena room
     uint32_t first;  // first BlockItem
     uint32_t nb;     // number of BlockItems
     uint32_t ccs;    // LZ4F: content checksum present
@@ -116,9 +116,10 @@ struct DeviceJob {
     rpgpu_job_totals* totals;
     uint64_t* bitmap;
     const Tables* tables;
-    uint32_t* counters;           // [0] rewalks, [1] overflow bits, [2] decode items, [3] decode cursor,
-                                  // [4] block items reserved
+    uint32_t* counters;           // [0] rewalks, [1] overflow bits, [2] decode items, [3] unused,
+                                  // [4] block items reserved, [5] decode claim cursor, [6] sequential frames
     uint32_t* decode_list;        // batch_capacity: ordinals of batches to uncompress
+    uint32_t* seq_list;           // batch_capacity: decode items decoded whole by one wave
     BlockItem* blocks;            // block work list ([4] items reserved, [5] claim cursor)
     uint32_t block_capacity;
     FramePlan* plans;             // one per decode item

@@ -336,6 +336,7 @@ int rpgpu_submit(rpgpu_ctx* c, const rpgpu_job* job, void* stream) {
     const size_t o_dcap = take((bcap + 1) * 8);
     const size_t o_counters = take(32);
     const size_t o_dlist = take((bcap + 1) * 4);
+    const size_t o_slist = take((bcap + 1) * 4);
     const size_t o_fbad = take((size_t)nseg * 4);
     // block-parallel decode: one item per LZ4F block / snappy-java chunk
     const bool dec = (job->flags & RPGPU_JOB_DECODE) && job->d_decoded;
@@ -380,6 +381,7 @@ int rpgpu_submit(rpgpu_ctx* c, const rpgpu_job* job, void* stream) {
     j.tables = c->d_tables;
     j.counters = (uint32_t*)(ws + o_counters);
     j.decode_list = (uint32_t*)(ws + o_dlist);
+    j.seq_list = (uint32_t*)(ws + o_slist);
     j.seg_first_bad = (uint32_t*)(ws + o_fbad);
     j.blocks = (BlockItem*)(ws + o_blocks);
     j.block_capacity = (uint32_t)bl_cap64;
@@ -530,7 +532,7 @@ int rpgpu_uncompress(rpgpu_ctx* c, int codec, const void* in, size_t n, void* ou
     int64_t* d_res = (int64_t*)(d_out + out_sz);
     HIPCHK(c, hipMemsetAsync(d_in + n, 0, in_sz - n, c->stream));
     HIPCHK(c, hipMemcpyAsync(d_in, in, n, hipMemcpyHostToDevice, c->stream));
-    HIPCHK(c, launch_uncompress_one(codec, d_in, n, d_out, dcap, d_res, c->stream));
+    HIPCHK(c, launch_uncompress_one(codec, d_in, n, d_out, out_sz, d_res, c->stream));
     int64_t res[2] = {0, 0};
     HIPCHK(c, hipMemcpyAsync(res, d_res, sizeof res, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));

@@ -8,7 +8,7 @@
 //   surfaces_test recover <segment>             log_replayer checkpoint
 //   surfaces_test index <segment> <base> <q>... log_replayer recovery + segment_index rebuild,
 //                                               find_nearest(offset) for each q
-//   surfaces_test uncompress <codec> <in> <out> compressor::uncompress
+//   surfaces_test uncompress (<codec> <in> <out>)+  compressor::uncompress
 //   surfaces_test wire <record_set>             kafka::batch_reader
 #include <cstdio>
 #include <cstdlib>
@@ -259,18 +259,21 @@ int main(int argc, char** argv) {
             }
             return 0;
         }
-        if (mode == "uncompress" && argc == 5) {
-            const std::vector<uint8_t> in = slurp(argv[3]);
-            try {
-                const rpgpu::iobuf out = compression::compressor::uncompress(
-                  rpgpu::iobuf(in.data(), in.size()), (compression::type)std::atoi(argv[2]));
-                std::ofstream f(argv[4], std::ios::binary);
-                f.write((const char*)out.data(), (std::streamsize)out.size_bytes());
-                std::printf("U ok %zu\n", out.size_bytes());
-            } catch (const std::logic_error& e) {
-                std::printf("U logic_error\n");
-            } catch (const std::runtime_error& e) {
-                std::printf("U runtime_error\n");
+        if (mode == "uncompress" && argc >= 5 && (argc - 2) % 3 == 0) {
+            // one or more (codec, in, out) triples: one line each
+            for (int a = 2; a + 2 < argc; a += 3) {
+                const std::vector<uint8_t> in = slurp(argv[a + 1]);
+                try {
+                    const rpgpu::iobuf out = compression::compressor::uncompress(
+                      rpgpu::iobuf(in.data(), in.size()), (compression::type)std::atoi(argv[a]));
+                    std::ofstream f(argv[a + 2], std::ios::binary);
+                    f.write((const char*)out.data(), (std::streamsize)out.size_bytes());
+                    std::printf("U ok %zu\n", out.size_bytes());
+                } catch (const std::logic_error& e) {
+                    std::printf("U logic_error\n");
+                } catch (const std::runtime_error& e) {
+                    std::printf("U runtime_error\n");
+                }
             }
             return 0;
         }

@@ -271,6 +271,11 @@ def test_log_replayer_segment_index(driver, rplib, oracle, engine, tmp_path):
         (st, ro, rt, ps), = oracle.segment_index(job.batches, job.summaries, [base])
         qs = [base - 1, base, base + 7, int(st["max_offset"]) + 5]
         lines = run(driver, "index", write(tmp_path, name, data), base, *qs)
+        if int(st["assert_batch"]) >= 0:
+            # a tracked batch below the index base: the reference vasserts
+            # (storage/index_state.cc:55-58); the C++ surface throws there
+            assert lines == ["VASSERT"], name
+            continue
         sm = job.summaries[0]
         want = [f"CKPT 1 {int(sm['ckpt_last_offset'])} {int(sm['ckpt_truncate_pos'])}" if sm["has_checkpoint"]
                 else "CKPT 0"]
@@ -292,10 +297,14 @@ def test_log_replayer_segment_index(driver, rplib, oracle, engine, tmp_path):
 def test_compressor_uncompress(driver, oracle, engine, tmp_path):
     import json
     man = json.load(open(os.path.join(G, "manifest.json")))
+    args = []
     for ent in man["codecs"]:
+        args += [ent["codec"], os.path.join(G, "codecs", ent["name"] + ".bin"), str(tmp_path / (ent["name"] + ".out"))]
+    lines = run(driver, "uncompress", *args)  # one process (one HIP context) for every fixture
+    assert len(lines) == len(man["codecs"])
+    for ent, line in zip(man["codecs"], lines):
         src = os.path.join(G, "codecs", ent["name"] + ".bin")
         out = str(tmp_path / (ent["name"] + ".out"))
-        (line,) = run(driver, "uncompress", ent["codec"], src, out)
         data = open(src, "rb").read()
         rc, want = oracle.uncompress(ent["codec"], data, max(len(data) * 300, 1 << 20))
         if rc == 0:
