@@ -40,6 +40,18 @@
 #else
 #define TRACE(...) do { } while (0)
 #endif
+// RPGPU_DSTAMPS: diagnostic build of the decode kernel (scripts/build_exp.py
+// dstamps -DRPGPU_DSTAMPS --unit rp_codec.hip): s_memtime cycle totals per
+// item kind and per engine phase, printed by k_print_dstamps; never measured
+#ifdef RPGPU_DSTAMPS
+#include <cstdio>
+__device__ unsigned long long g_dst[32];
+#define DST(d, i, x) ((d).st[i] += (uint64_t)(x))
+#define DCLK() __builtin_amdgcn_s_memtime()
+#else
+#define DST(d, i, x) do { } while (0)
+#define DCLK() 0ull
+#endif
 #if defined(RPGPU_TRACE_ITEMS)
 #include <cstdio>
 #define TRACE_ITEM(...) do { if (lane() == 0) printf(__VA_ARGS__); } while (0)
@@ -74,6 +86,9 @@ struct In {
     int64_t n;           // stream bytes
     int64_t base;        // stream offset of the window start
     uint32_t w0, w1;
+#ifdef RPGPU_DSTAMPS
+    uint64_t loads;      // window (re)loads
+#endif
 };
 
 DEV uint32_t ld_dw(const uint8_t* src, int64_t n, uintptr_t a) {
@@ -85,9 +100,15 @@ DEV void in_init(In& in, const uint8_t* src, int64_t n) {
     in.n = n;
     in.base = -(1ll << 60);
     in.w0 = in.w1 = 0;
+#ifdef RPGPU_DSTAMPS
+    in.loads = 0;
+#endif
 }
 
 DEV void in_load(In& in, int64_t ip) {
+#ifdef RPGPU_DSTAMPS
+    in.loads++;
+#endif
     const uintptr_t a = ((uintptr_t)(in.src + ip)) & ~(uintptr_t)3;
     in.base = (int64_t)(a - (uintptr_t)in.src);
     const uintptr_t mine = a + 4u * lane();
@@ -122,6 +143,10 @@ struct Dec {
     uint64_t flushed;         // bytes below are stored to the arena
     uint64_t confirmed;       // bytes below are visible to sc1 loads (vmcnt drained)
     uint64_t ring_lo;         // the ring holds [max(ring_lo, op - kRing), op)
+#ifdef RPGPU_DSTAMPS
+    uint64_t st[8];           // 0 sequences, 1 groups, 2 group cycles, 3 serial matches, 4 far groups,
+                              // 5 flush cycles, 6 ring-parallel lanes, 7 far-parallel lanes
+#endif
 };
 
 // matches waiting in the open group, lane j = j-th match
@@ -143,6 +168,9 @@ DEV void dec_init(Dec& d, uint8_t* arena, uint64_t arena_cap, lds_u8* ring, uint
     // read-backs past the arena's end return zeros instead of faulting
     const uint64_t room = arena_cap > at ? arena_cap - at : 0;
     d.rs = __builtin_amdgcn_make_buffer_rsrc(arena + at, 0, (int)(room < 0x7FFFFFFFull ? room : 0x7FFFFFFFull), kBufFlags);
+#ifdef RPGPU_DSTAMPS
+    for (int i = 0; i < 8; i++) d.st[i] = 0;
+#endif
 }
 
 DEV void wait_vm() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
@@ -169,6 +197,7 @@ DEV void flush(Dec& d, uint64_t upto) {
     const uint64_t f = uni64(d.flushed);
     upto = uni64(upto);
     if (f >= upto) return;
+    const uint64_t t0 = DCLK();
     TRACE("flush %llu..%llu\n", (unsigned long long)f, (unsigned long long)upto);
     const uint32_t l = lane();
     const uint64_t c_first = f & ~1023ull;
@@ -185,6 +214,7 @@ DEV void flush(Dec& d, uint64_t upto) {
         }
     }
     d.flushed = upto;
+    (void)t0;
 }
 
 // flush whole chunks only (the ragged tail stays in the ring until the end)
@@ -273,6 +303,8 @@ DEV void match_serial(Dec& d, uint64_t op, uint32_t off, uint32_t ml, uint64_t t
 // source lies within 4 GiB above d.lo.
 DEV void group_exec(Dec& d, Group& g) {
     if (g.n == 0) return;
+    const uint64_t t0 = DCLK();
+    DST(d, 1, 1);
     const uint32_t l = lane();
     const bool mine = l < g.n;
     const uint64_t end = d.op;
@@ -287,6 +319,9 @@ DEV void group_exec(Dec& d, Group& g) {
     const bool near = sr >= nlr;
     const bool ring_par = indep && near;
     const bool far_par = indep && !near && g.ml <= kFarMax;
+    DST(d, 6, __builtin_popcountll(__ballot(ring_par)));
+
+    DST(d, 4, __ballot(far_par) ? 1 : 0);
     TRACE("group n=%u m0=%llu end=%llu ring=%llx far=%llx\n", g.n, (unsigned long long)g.m0, (unsigned long long)end,
           (unsigned long long)__ballot(ring_par), (unsigned long long)__ballot(far_par));
     // lane-parallel, sources in the ring
@@ -341,6 +376,7 @@ DEV void group_exec(Dec& d, Group& g) {
     // in order: matches whose sources lie inside the group (or that are too
     // long for the lane-parallel read-back)
     const uint64_t serial = __ballot(mine && !ring_par && !far_par);
+    DST(d, 3, __builtin_popcountll(serial));
     if (serial) {
         const uint64_t keep = d.op;
         uint64_t m = serial;
@@ -354,6 +390,7 @@ DEV void group_exec(Dec& d, Group& g) {
     }
     g.n = 0;
     flush_chunks(d);
+    DST(d, 2, DCLK() - t0);
 }
 
 // One sequence at d.op: the literal bytes [lip, lip + llen) of the stream,
@@ -364,6 +401,7 @@ DEV void group_exec(Dec& d, Group& g) {
 // the group unless they are long or have offset 0.
 DEV void emit_seq(Dec& d, Group& g, In& in, int64_t lip, int64_t llen, uint32_t off, uint32_t ml, bool has_match) {
     const uint32_t l = lane();
+    DST(d, 0, 1);
     const bool big_lit = llen > 64;
     const bool big_match = has_match && (off == 0 || ml > 64);
     const uint64_t mend = d.op + (uint64_t)llen + (has_match ? ml : 0u);
@@ -755,7 +793,13 @@ DEV int lz4_unit(In& in, const uint8_t* s, int64_t n, Dec& d, Group& g, uint32_t
         In bin;
         in_init(bin, s + pos, bsz);
         d.op = start + (uint64_t)out;
+        const uint64_t tb0 = DCLK();
         const int64_t dd = lz4_block(bin, bsz, d, g, bmax, linked ? out : 0);
+        DST(d, 1, 0);
+#ifdef RPGPU_DSTAMPS
+        d.st[5] += bin.loads;  // (reuses the flush slot: window loads)
+        d.st[7] += DCLK() - tb0;  // (reuses the far-lanes slot: block cycles)
+#endif
         if (dd < 0) return -1;                                   // decompressionFailed
         pos += need;
         if (content_size) remaining -= (uint64_t)dd;
@@ -1173,8 +1217,23 @@ __global__ __launch_bounds__(256) void k_decode_blocks(DeviceJob j) {
         int64_t got = 0;
         TRACE_ITEM("item %u/%u wg %u w %u codec %d single %x n %lld src %llu dst %llu cap %u\n", item, total, blockIdx.x,
                    threadIdx.x >> 6, codec, single, (long long)n, (unsigned long long)src, (unsigned long long)dst, bcap);
+        const uint64_t it0 = DCLK();
         const int rc = decode_unit(codec, j.data + src, n, d, single, bcap, got);
         TRACE_ITEM("done %u rc %d got %lld\n", item, rc, (long long)got);
+#ifdef RPGPU_DSTAMPS
+        {
+            const uint64_t dt = DCLK() - it0;
+            // kinds: 0 whole frames, 1 LZ4 blocks, 2 raw blocks, 3 snappy chunks
+            const int kind = item < nseq ? 0 : (codec == RPGPU_CODEC_SNAPPY ? 3 : ((single & kBlkRaw) ? 2 : 1));
+            if (lane() == 0) {
+                atomicAdd(&g_dst[2 * kind], (unsigned long long)dt);
+                atomicAdd(&g_dst[2 * kind + 1], 1ull);
+                atomicMax(&g_dst[8 + kind], (unsigned long long)dt);
+                for (int i = 0; i < 8; i++) atomicAdd(&g_dst[16 + i], (unsigned long long)d.st[i]);
+                atomicAdd(&g_dst[24 + kind], (unsigned long long)got);
+            }
+        }
+#endif
         if (lane() == 0) {
             if (item < nseq) {
                 if (rc == 0) {
@@ -1188,6 +1247,19 @@ __global__ __launch_bounds__(256) void k_decode_blocks(DeviceJob j) {
         }
     }
 }
+
+#ifdef RPGPU_DSTAMPS
+__global__ void k_print_dstamps() {
+    const char* kn[4] = {"frames", "lz4 blocks", "raw blocks", "snappy chunks"};
+    for (int k = 0; k < 4; k++)
+        printf("RPGPU_DSTAMPS %s: n=%llu cycles=%llu avg=%.0f max=%llu bytes=%llu\n", kn[k], g_dst[2 * k + 1], g_dst[2 * k],
+               g_dst[2 * k + 1] ? (double)g_dst[2 * k] / (double)g_dst[2 * k + 1] : 0.0, g_dst[8 + k], g_dst[24 + k]);
+    printf("RPGPU_DSTAMPS seqs=%llu groups=%llu group_cycles=%llu serial=%llu far_groups=%llu window_loads=%llu "
+           "ring_lanes=%llu lz4_block_cycles=%llu\n", g_dst[16], g_dst[17], g_dst[18], g_dst[19], g_dst[20], g_dst[21], g_dst[22],
+           g_dst[23]);
+    for (int i = 0; i < 32; i++) g_dst[i] = 0;
+}
+#endif
 
 // one wave per block-parallel frame: all pieces decoded, moved together
 // when an earlier one came out short, content size / checksum checked
@@ -1276,6 +1348,9 @@ hipError_t launch_decode(const DeviceJob& j, hipStream_t s, uint32_t grid) {
 hipError_t launch_decode_blocks(const DeviceJob& j, hipStream_t s, uint32_t grid) {
     set_lds_attrs();
     hipLaunchKernelGGL(k_decode_blocks, dim3(grid), dim3(64 * kDecWaves), kDecWaves * kRing, s, j);
+#ifdef RPGPU_DSTAMPS
+    hipLaunchKernelGGL(k_print_dstamps, dim3(1), dim3(1), 0, s);
+#endif
     return hipGetLastError();
 }
 
