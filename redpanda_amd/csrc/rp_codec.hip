@@ -31,6 +31,13 @@
 //     the offset.
 // Integer/byte work only: no MFMA.
 #include "rp_device.h"
+// RPGPU_DSTAMPS: diagnostic build of the decode kernel (scripts/build_exp.py
+// dstamps -DRPGPU_DSTAMPS --unit rp_codec.hip): per unit kind, wall-clock
+// totals / maxima / finish times, printed by k_print_dstamps; never measured
+#ifdef RPGPU_DSTAMPS
+#include <cstdio>
+__device__ unsigned long long g_dst[64];
+#endif
 
 namespace rp {
 
@@ -91,6 +98,9 @@ DEV uint4 shr1(const uint4& w) {
 
 // 16 bytes (the first len of them significant, 1..16) at output o
 DEV void put(const Dst& d, int64_t o, const uint4& v, uint32_t len) {
+#ifdef RPGPU_EXP_NOCOPY
+    return;
+#endif
     if (o + 16 <= d.lim) {
         gst16(d.p + o, v);
         return;
@@ -102,6 +112,9 @@ DEV void put(const Dst& d, int64_t o, const uint4& v, uint32_t len) {
 
 // len stream bytes from ip to output o (64 bytes in flight per step)
 DEV void copy_in(const Src& s, int64_t ip, const Dst& d, int64_t o, int64_t len) {
+#ifdef RPGPU_EXP_NOCOPY
+    return;
+#endif
     int64_t c = 0;
     for (; c + 64 <= len && ip + c + 64 <= s.rl && o + c + 64 <= d.lim; c += 64) {
         const uint4 a = gld16(s.p + ip + c), b = gld16(s.p + ip + c + 16), e = gld16(s.p + ip + c + 32),
@@ -143,6 +156,13 @@ constexpr PatTab make_pat() {
 __constant__ PatTab kPat = make_pat();
 
 DEV void copy_match(const Dst& d, int64_t o, uint32_t off, int64_t ml) {
+#ifdef RPGPU_EXP_NOCOPY
+    return;
+#endif
+#ifdef RPGPU_EXP_NOMATCHLOAD
+    for (int64_t c = 0; c < ml; c += 16) put(d, o + c, make_uint4(off, 0, 0, 0), (uint32_t)(ml - c < 16 ? ml - c : 16));
+    return;
+#endif
     if (off >= 16) {
         const uint8_t* s = d.p + o - off;
         int64_t c = 0;
@@ -239,11 +259,26 @@ __device__ __attribute__((noinline)) uint32_t xxh32_lane(const uint8_t* p, uint6
 // ---------------------------------------------------------------------------
 // LZ4 block: rpo_lz4_block_decode (oracle) = lz4 1.9.3 LZ4_decompress_generic
 // for LZ4_decompress_safe_usingDict (fast loop + safe loop, every check).
-// Output at d.p (block capacity oend); H = history bytes before it.
-// Returns the decoded length or -1.  Positions are 32-bit: a block is at
-// most 4 MiB in and out, and a length read from it at most 255x that.
+// One sequence walk, two sinks: DirectSink copies on the spot (the lane
+// engine), RecSink writes SeqRecs for the wave engine and may suspend the
+// walk when its buffer is full (PState holds the resume point).  Every
+// accept/reject decision depends on positions and lengths only, never on
+// byte values, so the walk alone decides the block's verdict and length.
+// H = history bytes before the block; `need` records the most history any
+// match reached for (a walk run with H = 65536 then fails iff need > the
+// real H: every history check of the reference fails the block).
+// Positions are 32-bit: a block is at most 4 MiB in and out, and a length
+// read from it at most 255x that.
 // ---------------------------------------------------------------------------
 constexpr int32_t kMinMatch = 4, kLastLiterals = 5, kMfLimit = 12, kFastSafeDistance = 64;
+
+struct PState {
+    int32_t ip, op;    // resume point (stream / output position)
+    int32_t need;      // max over matches of offset - match position
+    int32_t st;        // 0 walking, 1 done (op = decoded length), -1 rejected
+    uint32_t ulen;     // snappy: the stream's uncompressed length
+    uint32_t safe;     // lz4: in the safe loop
+};
 
 DEV int32_t lz_read_var(const Src& s, int32_t& ip, int32_t lencheck, bool loop_check, bool initial_check, int& err) {
     int32_t length = 0;
@@ -265,20 +300,53 @@ DEV int32_t lz_read_var(const Src& s, int32_t& ip, int32_t lencheck, bool loop_c
     return length;
 }
 
-DEV int32_t lz4_block(const Src& s, const Dst& d, int32_t oend, int64_t H64) {
+DEV void lz4_begin(PState& ps, const Src& s, int32_t oend) {
+    ps.ip = ps.op = ps.need = 0;
+    ps.ulen = 0;
+    ps.safe = oend < kFastSafeDistance;
+    ps.st = 0;
+    if (oend == 0) ps.st = (s.n == 1 && b8(s, 0) == 0) ? 1 : -1;
+    else if (s.n == 0) ps.st = -1;
+}
+
+// sinks: seq(w, tip, lip, llen, lo, off, ml) with the 16 stream bytes at
+// the token (w, from tip), the literal [lip, lip + llen) to output lo and
+// the match (off, ml; ml = 0: none) at lo + llen; false = suspend after it
+struct DirectSink {
+    const Src& s;
+    const Dst& d;
+    DEV bool seq(const uint4& w, int32_t tip, int32_t lip, int32_t llen, int32_t lo, uint32_t off, int32_t ml) {
+        if (llen > 0) {
+            // short literals right behind the token are already in w
+            if (lip == tip + 1 && llen <= 15) put(d, lo, shr1(w), (uint32_t)llen);
+            else copy_in(s, lip, d, lo, llen);
+        }
+        if (ml > 0) copy_match(d, (int64_t)lo + llen, off, ml);
+        return true;
+    }
+};
+struct RecSink {
+    SeqRec* out;
+    uint32_t n, cap;
+    DEV bool seq(const uint4&, int32_t, int32_t lip, int32_t llen, int32_t, uint32_t off, int32_t ml) {
+        out[n] = SeqRec{(uint32_t)lip, (uint32_t)llen, (uint32_t)ml, off};
+        return ++n < cap;
+    }
+};
+
+template <class Sink>
+DEV void lz4_run(const Src& s, int32_t oend, int32_t H, PState& ps, Sink& sink) {
+    if (ps.st) return;
     const int32_t iend = (int32_t)s.n;
-    const int32_t H = H64 > 65536 ? 65536 : (int32_t)H64;  // offsets are < 65536
-    if (oend == 0) return (iend == 1 && b8(s, 0) == 0) ? 0 : -1;
-    if (iend == 0) return -1;
     const int32_t shortiend = iend - 14 - 2, shortoend = oend - 14 - 18;
-    int32_t ip = 0, op = 0, length, offset = 0, cpy = 0, lip = 0, llen = 0, ml = 0;
+    int32_t ip = ps.ip, op = ps.op, need = ps.need, length, offset = 0, cpy = 0, lip = 0, llen = 0, ml = 0;
     int err;
-    bool last = false;
+    bool last = false, safe = ps.safe != 0;
+#define LZ_FAIL() do { ps.st = -1; return; } while (0)
     // The two loops of LZ4_decompress_generic as one: `safe` is the safe
     // loop (entered for good at the first fast-loop exit); every path ends at
     // `emit` with the sequence's literal (lip, llen; op already past it) and
     // match (offset, ml).
-    bool safe = oend - op < kFastSafeDistance;
     for (;;) {
         const int32_t tip = ip;
         const uint4 w = ld16(s, tip);  // the token and the 15 bytes after it
@@ -289,7 +357,7 @@ DEV int32_t lz4_block(const Src& s, const Dst& d, int32_t oend, int64_t H64) {
         if (!safe) {
             if (length == 15) {
                 length += lz_read_var(s, ip, iend - 15, true, true, err);
-                if (err == 1) return -1;
+                if (err == 1) LZ_FAIL();
                 cpy = op + length;
                 if (cpy > oend - 32 || ip + length > iend - 32) { safe = true; goto safe_literal_copy; }
             } else {
@@ -304,16 +372,16 @@ DEV int32_t lz4_block(const Src& s, const Dst& d, int32_t oend, int64_t H64) {
             ip += 2;
             length = (int32_t)(token & 15);
             if (length == 15) {
-                if (offset > op + H) return -1;
+                if (offset > op + H) LZ_FAIL();
                 length += lz_read_var(s, ip, iend - kLastLiterals + 1, true, false, err);
-                if (err) return -1;
+                if (err) LZ_FAIL();
                 length += kMinMatch;
                 if (op + length >= oend - kFastSafeDistance) { safe = true; goto safe_match_copy; }
             } else {
                 length += kMinMatch;
                 if (op + length >= oend - kFastSafeDistance) { safe = true; goto safe_match_copy; }
             }
-            if (offset > op + H) return -1;
+            if (offset > op + H) LZ_FAIL();
             ml = length;
             goto emit;
         }
@@ -333,14 +401,14 @@ DEV int32_t lz4_block(const Src& s, const Dst& d, int32_t oend, int64_t H64) {
         }
         if (length == 15) {
             length += lz_read_var(s, ip, iend - 15, true, true, err);
-            if (err == 1) return -1;
+            if (err == 1) LZ_FAIL();
         }
         cpy = op + length;
     safe_literal_copy:
         lip = ip;
         llen = length;
         if (cpy > oend - kMfLimit || ip + length > iend - (2 + 1 + kLastLiterals)) {
-            if (ip + length != iend || cpy > oend) return -1;
+            if (ip + length != iend || cpy > oend) LZ_FAIL();
             ip += length;
             op += length;
             last = true;
@@ -354,29 +422,46 @@ DEV int32_t lz4_block(const Src& s, const Dst& d, int32_t oend, int64_t H64) {
     lbl_copy_match:
         if (length == 15) {
             length += lz_read_var(s, ip, iend - kLastLiterals + 1, true, false, err);
-            if (err) return -1;
+            if (err) LZ_FAIL();
         }
         length += kMinMatch;
     safe_match_copy:
-        if (offset > op + H) return -1;
+        if (offset > op + H) LZ_FAIL();
         // a match starting in the history (offset > op) ends by oend - 5;
         // so does one inside the block (cpy > oend - 12 -> cpy <= oend - 5)
-        if (op + length > oend - kLastLiterals) return -1;
+        if (op + length > oend - kLastLiterals) LZ_FAIL();
         ml = length;
     emit:
 #undef RD_OFFSET
-        if (llen > 0) {
-            // short literals right behind the token are already in w
-            if (lip == tip + 1 && llen <= 15) put(d, op - llen, shr1(w), (uint32_t)llen);
-            else copy_in(s, lip, d, op - llen, llen);
+        if (last) {
+            sink.seq(w, tip, lip, llen, op - llen, 0u, 0);
+            ps.st = 1;
+            ps.op = op;
+            ps.need = need;
+            return;
         }
-        if (last) break;
-        copy_match(d, op, (uint32_t)offset, ml);
+        if (offset - op > need) need = offset - op;
+        const bool go = sink.seq(w, tip, lip, llen, op - llen, (uint32_t)offset, ml);
         op += ml;
+        if (!go) {
+            ps.ip = ip;
+            ps.op = op;
+            ps.need = need;
+            ps.safe = safe;
+            return;
+        }
     }
-    return op;
+#undef LZ_FAIL
 }
 
+// the lane engine's block decode: decoded length or -1
+DEV int32_t lz4_block(const Src& s, const Dst& d, int32_t oend, int64_t H64) {
+    PState ps;
+    lz4_begin(ps, s, oend);
+    DirectSink sink{s, d};
+    lz4_run(s, oend, H64 > 65536 ? 65536 : (int32_t)H64, ps, sink);  // offsets are < 65536
+    return ps.st == 1 ? ps.op : -1;
+}
 // ---------------------------------------------------------------------------
 // LZ4 frame: rpo_lz4f_uncompress (oracle) — LZ4F_getFrameInfo + the
 // LZ4F_decompress loop of do_uncompressed, including its output-buffer
@@ -535,31 +620,44 @@ DEV int snappy_varint(const Src& s, int64_t pos, int64_t n, uint32_t& v, int64_t
 }
 
 // snappy_raw_checked: varint length, then DecompressAllTags over the rest:
-// succeeds iff the tags end exactly at n and exactly ulen bytes come out
-DEV int snappy_raw_checked(const Src& s, const Dst& d, int64_t& out_len) {
-    const int64_t n = s.n;
-    uint32_t ulen32;
-    int64_t ip;
-    if (snappy_varint(s, 0, n, ulen32, ip)) return -1;
+// succeeds iff the tags end exactly at n and exactly ulen bytes come out.
+// whole: snappy_standard_compressor semantics for a raw payload (length 0
+// is an empty result, the tags are not looked at).  Positions are 32-bit:
+// streams are batch payloads (< 2 GiB).
+DEV void snappy_begin(PState& ps, const Src& s, bool whole) {
+    ps.ip = ps.op = ps.need = 0;
+    ps.safe = 0;
+    ps.st = 0;
+    uint32_t ulen;
+    int64_t used;
+    if (snappy_varint(s, 0, s.n, ulen, used)) { ps.st = -1; return; }
+    ps.ulen = ulen;
+    ps.ip = (int32_t)used;
+    if (whole && ulen == 0) { ps.st = 1; return; }  // "empty frame"
     // no tag sequence expands more than 64/3 per input byte
-    if ((uint64_t)ulen32 > 22ull * (uint64_t)n + 64) return -1;
-    const int64_t ulen = ulen32;
-    int64_t op = 0;
+    if ((uint64_t)ulen > 22ull * (uint64_t)s.n + 64) ps.st = -1;
+}
+
+template <class Sink>
+DEV void snappy_run(const Src& s, PState& ps, Sink& sink) {
+    if (ps.st) return;
+    const int64_t n = s.n, ulen = ps.ulen;
+    int64_t ip = ps.ip, op = ps.op;
     while (ip < n) {
         const uint4 w = ld16(s, ip);  // the tag and the 15 bytes after it
         const uint32_t c = w.x & 0xFFu;
         const uint32_t t = c & 3;
         const int64_t extra = t == 0 ? (((c >> 2) >= 60) ? (int64_t)((c >> 2) - 59) : 0) : t == 1 ? 1 : t == 2 ? 2 : 4;
-        if (n - ip < 1 + extra) return -1;
+        if (n - ip < 1 + extra) { ps.st = -1; return; }
         const uint32_t x = at32(w, 1);  // the tag's extra bytes (at most 4)
+        bool go;
         if (t == 0) {
             int64_t lit = (int64_t)(c >> 2) + 1;
             if (lit >= 61) lit = (int64_t)(extra == 4 ? x : x & ((1u << (8 * extra)) - 1u)) + 1;
             const int64_t lip = ip + 1 + extra;
-            if (n - lip < lit) return -1;      // premature end of input
-            if (ulen - op < lit) return -1;    // SnappyArrayWriter::Append overflow
-            if (extra == 0 && lit <= 15) put(d, op, shr1(w), (uint32_t)lit);
-            else copy_in(s, lip, d, op, lit);
+            if (n - lip < lit) { ps.st = -1; return; }      // premature end of input
+            if (ulen - op < lit) { ps.st = -1; return; }    // SnappyArrayWriter::Append overflow
+            go = sink.seq(w, (int32_t)ip, (int32_t)lip, (int32_t)lit, (int32_t)op, 0u, 0);
             op += lit;
             ip = lip + lit;
         } else {
@@ -567,16 +665,29 @@ DEV int snappy_raw_checked(const Src& s, const Dst& d, int64_t& out_len) {
             const int64_t off = t == 1 ? (int64_t)(((c >> 5) << 8) | (x & 0xFFu)) : t == 2 ? (int64_t)(x & 0xFFFFu) : (int64_t)x;
             ip += 1 + extra;
             // AppendFromSelf: Produced() <= offset - 1u || op_end > op_limit_
-            if (off == 0 || op < off || ulen - op < len) return -1;
-            copy_match(d, op, (uint32_t)off, len);
+            if (off == 0 || op < off || ulen - op < len) { ps.st = -1; return; }
+            go = sink.seq(w, (int32_t)ip, 0, 0, (int32_t)op, (uint32_t)off, (int32_t)len);
             op += len;
         }
+        if (!go && ip < n) {
+            ps.ip = (int32_t)ip;
+            ps.op = (int32_t)op;
+            return;
+        }
     }
-    if (op != ulen) return -1;
-    out_len = ulen;
-    return 0;
+    ps.op = (int32_t)op;
+    ps.st = op == ulen ? 1 : -1;
 }
 
+DEV int snappy_raw_checked(const Src& s, const Dst& d, int64_t& out_len) {
+    PState ps;
+    snappy_begin(ps, s, false);
+    DirectSink sink{s, d};
+    snappy_run(s, ps, sink);
+    if (ps.st != 1) return -1;
+    out_len = ps.ulen;
+    return 0;
+}
 // snappy_java_compressor::uncompress: the xerial stream's chunks one after
 // the other, or the raw fallback (snappy_standard_compressor: length 0 is
 // an empty result, RawUncompress not called).  single: the stream is one
@@ -707,15 +818,18 @@ DEV uint32_t reserve_blocks(const DeviceJob& j, uint32_t nb) {
     return ((uint64_t)first + nb <= j.block_capacity) ? first : 0xFFFFFFFFu;
 }
 
-// LZ4F frame of independent blocks (lz4_frame_compressor.cc:115-200 over
-// lz4 1.9.3): returns true and fills the plan when eligible
-DEV bool plan_lz4f(const DeviceJob& j, In& in, int64_t n, uint64_t src_abs, uint64_t dst_abs, FramePlan& fp) {
+// LZ4F frame (lz4_frame_compressor.cc:115-200 over lz4 1.9.3), complete in
+// structure: returns true and fills the plan when eligible.  Independent
+// blocks go to the block list; a linked frame's blocks (at most 64) are
+// decoded in order by one wave of k_lz_exec (link_list)
+DEV bool plan_lz4f(const DeviceJob& j, In& in, int64_t n, uint64_t src_abs, uint64_t dst_abs, uint32_t item,
+                   FramePlan& fp) {
     if (n < 7) return false;
     if (in_le32(in, 0) != 0x184D2204u) return false;
     const uint32_t flg = in_byte(in, 4);
     const int64_t hsize = 7 + (((flg >> 3) & 1) ? 8 : 0) + ((flg & 1) ? 4 : 0);
     if (n < hsize || ((flg >> 1) & 1) || ((flg >> 6) & 3) != 1) return false;
-    if (!((flg >> 5) & 1)) return false;  // linked blocks: sequential
+    const bool linked = !((flg >> 5) & 1);
     const uint32_t bd = in_byte(in, 5);
     const uint32_t bsid = (bd >> 4) & 7;
     if (((bd >> 7) & 1) || bsid < 4 || (bd & 15)) return false;
@@ -745,7 +859,7 @@ DEV bool plan_lz4f(const DeviceJob& j, In& in, int64_t n, uint64_t src_abs, uint
         ccs_val = in_le32(in, pos);
         pos += 4;
     }
-    if (pos != n || nb == 0) return false;
+    if (pos != n || nb == 0 || (linked && nb > 64)) return false;
     const uint32_t first = reserve_blocks(j, nb);
     if (first == 0xFFFFFFFFu) return false;
     pos = hsize;
@@ -759,13 +873,17 @@ DEV bool plan_lz4f(const DeviceJob& j, In& in, int64_t n, uint64_t src_abs, uint
             it.src = src_abs + (uint64_t)pos + 4;
             it.dst = dst_abs + plan;
             it.csize = (uint32_t)bsz;
-            it.kind = (raw ? kBlkRaw : 0u) | (bcs ? kBlkChecksum : 0u);
+            it.kind = (raw ? kBlkRaw : 0u) | (bcs ? kBlkChecksum : 0u) | (linked ? kBlkLinked : 0u);
             it.out = -1;
             it.cap = raw ? (uint32_t)bsz : (uint32_t)bmax;
             j.blocks[first + k] = it;
         }
         plan += raw ? (uint64_t)bsz : (uint64_t)bmax;
         pos += 4 + bsz + (bcs ? 4 : 0);
+    }
+    if (linked) {
+        const uint32_t at = wave_fetch_add(&j.counters[7], 1u);
+        if (lane() == 0) j.link_list[at] = item;
     }
     fp.mode = 1;
     fp.first = first;
@@ -833,6 +951,32 @@ DEV bool plan_snappy_java(const DeviceJob& j, In& in, int64_t n, uint64_t src_ab
     return true;
 }
 
+// a raw (non-xerial) snappy payload: one item, decoded whole by one lane's
+// walk and executed by the wave engine
+DEV bool plan_snappy_whole(const DeviceJob& j, int64_t n, uint64_t src_abs, uint64_t dst_abs, uint64_t cap, FramePlan& fp) {
+    if (cap > 0xFFFFFFFFull) return false;
+    const uint32_t first = reserve_blocks(j, 1);
+    if (first == 0xFFFFFFFFu) return false;
+    if (lane() == 0) {
+        BlockItem it;
+        it.src = src_abs;
+        it.dst = dst_abs;
+        it.csize = (uint32_t)n;
+        it.kind = kBlkSnappy | kBlkWhole;
+        it.out = -1;
+        it.cap = (uint32_t)cap;
+        j.blocks[first] = it;
+    }
+    fp.mode = 2;
+    fp.first = first;
+    fp.nb = 1;
+    fp.ccs = 0;
+    fp.ccs_val = 0;
+    fp.csf = 0;
+    fp.content_size = 0;
+    return true;
+}
+
 // ---------------------------------------------------------------------------
 // k_decode: one wave per compressed batch of the job (work list built by
 // k_emit), wave-strided: the frame is planned into BlockItems, or queued
@@ -861,8 +1005,14 @@ __global__ __launch_bounds__(256) void k_decode(DeviceJob j) {
             in_init(in, j.data + S, n);
             bool planned = false;
             if (n > 0 && j.block_capacity) {
-                if (codec == RPGPU_CODEC_LZ4) planned = plan_lz4f(j, in, n, S, doff, fp);
-                else if (codec == RPGPU_CODEC_SNAPPY) planned = plan_snappy_java(j, in, n, S, doff, fp);
+                if (codec == RPGPU_CODEC_LZ4) {
+                    planned = plan_lz4f(j, in, n, S, doff, item, fp);
+                } else if (codec == RPGPU_CODEC_SNAPPY) {
+                    const uint8_t magic[8] = {0x82, 'S', 'N', 'A', 'P', 'P', 'Y', 0};
+                    bool java = n >= 16;
+                    for (int i = 0; i < 8 && java; i++) java = in_byte(in, i) == magic[i];
+                    planned = java ? plan_snappy_java(j, in, n, S, doff, fp) : plan_snappy_whole(j, n, S, doff, cap, fp);
+                }
             }
             if (!planned) {
                 fp.mode = 0;
@@ -875,53 +1025,450 @@ __global__ __launch_bounds__(256) void k_decode(DeviceJob j) {
 }
 
 // ---------------------------------------------------------------------------
-// k_decode_blocks: every lane takes units off one agent-scope counter
-// (counters[5]) until the list is exhausted: first the sequential frames
-// (the longest units), then the BlockItems.
+// Wave engine (k_lz_exec).  Lanes first walk up to 64 pieces in parallel
+// (lz4_run / snappy_run into RecSink: kRecsPerLane SeqRecs each); then the
+// wave executes the pieces in order against a 64 KiB LDS ring holding the
+// last 64 KiB of output (every LZ4 offset, and every snappy offset of a
+// piece up to 64 KiB, lands in it), storing whole 1 KiB chunks to the arena
+// with coalesced 16-byte-per-lane stores.
+//   * Records run 64 at a time, one per lane: a prefix sum places them, the
+//     literals are copied lane-parallel, then the matches in rounds: in each
+//     round every match whose source ends before the first unexecuted
+//     match's output (all bytes there are final), plus that first match
+//     itself (whose source may overlap its own output), copies at once.
+//   * Records longer than kBig run alone, wave-cooperatively.
+//   * Linked frames keep the ring across blocks (positions count from the
+//     frame start); a batch's writes may then overwrite ring slots 64 KiB
+//     back, so a match whose source lies before (batch end - 64 KiB) reads
+//     it back from the arena (sc1 loads of bytes stored long before).
+//   * Raw blocks are plain 16-byte-per-lane copies (through the ring in a
+//     linked frame, whose later blocks may copy from them).
+// ---------------------------------------------------------------------------
+typedef __attribute__((address_space(3))) uint8_t lds_u8;
+constexpr uint32_t kXRing = 65536, kXM = kXRing - 1;
+constexpr uint32_t kBig = 256;                 // longer literals / matches run wave-cooperatively
+constexpr uint32_t kBufFlags = 0x00020000u;    // buffer resource word 3 (raw, 32-bit data format)
+constexpr int kSc1 = 16;                       // cache policy: sc1 (L2-coherent, bypasses the vector L1)
+
+struct XRing {
+    lds_u8* r;
+    uint8_t* dst;           // arena address of position 0
+    uint32_t op;            // next output position (uniform)
+    uint32_t flushed;       // positions below are stored to dst
+    bool linked;            // positions run across blocks (the ring wraps)
+    __amdgpu_buffer_rsrc_t rs;  // dst window for far read-backs (linked)
+};
+
+DEV void wait_vm() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
+// 16 ring bytes at position p (wrapping)
+DEV uint4 xld16(const lds_u8* r, uint32_t p) {
+    const uint32_t sl = p & kXM;
+    if (sl <= kXRing - 16) {
+        uint4 v;
+        __builtin_memcpy(&v, r + sl, 16);
+        return v;
+    }
+    uint32_t w[4] = {0, 0, 0, 0};
+#pragma unroll
+    for (uint32_t k = 0; k < 16; k++) w[k >> 2] |= (uint32_t)r[(p + k) & kXM] << (8 * (k & 3));
+    return make_uint4(w[0], w[1], w[2], w[3]);
+}
+// the first len (1..16) bytes of v to ring position p (wrapping), exactly
+DEV void xst(lds_u8* r, uint32_t p, const uint4& v, uint32_t len) {
+    const uint32_t sl = p & kXM;
+    if (sl <= kXRing - 16) {
+        lds_u8* q = r + sl;
+        if (len == 16) {
+            __builtin_memcpy(q, &v, 16);
+            return;
+        }
+        uint64_t lo = (uint64_t)v.x | ((uint64_t)v.y << 32), hi = (uint64_t)v.z | ((uint64_t)v.w << 32);
+        if (len & 8) { __builtin_memcpy(q, &lo, 8); q += 8; lo = hi; }
+        if (len & 4) { const uint32_t t = (uint32_t)lo; __builtin_memcpy(q, &t, 4); q += 4; lo >>= 32; }
+        if (len & 2) { const uint16_t t = (uint16_t)lo; __builtin_memcpy(q, &t, 2); q += 2; lo >>= 16; }
+        if (len & 1) *q = (uint8_t)lo;
+        return;
+    }
+#pragma unroll
+    for (uint32_t k = 0; k < 16; k++)
+        if (k < len) r[(p + k) & kXM] = (uint8_t)(dw(v, k >> 2) >> (8 * (k & 3)));
+}
+
+// store ring positions [x.flushed, upto) to the arena: whole 16-byte pieces
+// as one ds_read_b128 + global_store_dwordx4 per lane, edge pieces byte by
+// byte.  Uniform trip count.
+DEV void xflush(XRing& x, uint32_t upto) {
+    const uint32_t f = x.flushed;
+    if (f >= upto) return;
+    const uint32_t l = lane();
+    const uint32_t c0 = f & ~1023u;
+    const uint32_t nch = (((upto + 1023u) & ~1023u) - c0) >> 10;
+    for (uint32_t i = 0; i < nch; i++) {
+        const uint32_t a = c0 + (i << 10) + 16u * l;
+        if (a >= f && a + 16 <= upto) {
+            gst16(x.dst + a, xld16(x.r, a));
+        } else if (a + 16 > f && a < upto) {
+#pragma unroll
+            for (uint32_t b = 0; b < 16; b++)
+                if (a + b >= f && a + b < upto) x.dst[a + b] = x.r[(a + b) & kXM];
+        }
+    }
+    x.flushed = upto;
+}
+DEV void xflush_chunks(XRing& x) { xflush(x, x.op & ~1023u); }
+
+// inclusive prefix sum over the wave
+DEV uint32_t wave_scan(uint32_t v) {
+    const uint32_t l = lane();
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t t = (uint32_t)__shfl_up((int)v, o, 64);
+        if (l >= (uint32_t)o) v += t;
+    }
+    return v;
+}
+
+// one lane's match: ml bytes at d from d - off (every source byte final or
+// this match's own earlier output)
+DEV void xmatch(XRing& x, uint32_t d, uint32_t off, uint32_t ml, bool far) {
+    const uint32_t s = d - off;
+    if (far) {
+        for (uint32_t c = 0; c < ml; c += 16) {
+            const auto t = __builtin_amdgcn_raw_buffer_load_b128(x.rs, s + c, 0, kSc1);
+            xst(x.r, d + c, make_uint4(t[0], t[1], t[2], t[3]), ml - c < 16 ? ml - c : 16);
+        }
+        return;
+    }
+    if (off >= 16) {
+        for (uint32_t c = 0; c < ml; c += 16) xst(x.r, d + c, xld16(x.r, s + c), ml - c < 16 ? ml - c : 16);
+        return;
+    }
+    uint4 p = make_uint4(0, 0, 0, 0);
+    uint32_t step = 16;
+    if (off) {
+        const uint4 v = xld16(x.r, s);  // bytes [s, s + off) are the pattern
+        const uint4 sa = *(const uint4*)&kPat.a[off][0], sb = *(const uint4*)&kPat.b[off][0];
+        p.x = __builtin_amdgcn_perm(v.y, v.x, sa.x) | __builtin_amdgcn_perm(v.w, v.z, sb.x);
+        p.y = __builtin_amdgcn_perm(v.y, v.x, sa.y) | __builtin_amdgcn_perm(v.w, v.z, sb.y);
+        p.z = __builtin_amdgcn_perm(v.y, v.x, sa.z) | __builtin_amdgcn_perm(v.w, v.z, sb.z);
+        p.w = __builtin_amdgcn_perm(v.y, v.x, sa.w) | __builtin_amdgcn_perm(v.w, v.z, sb.w);
+        step = off * (((0x00000001112347F0ull >> (4 * off)) & 15u) + 1u);
+    }
+    for (uint32_t c = 0; c < ml; c += step) xst(x.r, d + c, p, ml - c < 16 ? ml - c : 16);
+}
+
+// up to 64 records (lane k < m holds record k), none longer than kBig
+DEV void xbatch(XRing& x, const Src& s, const SeqRec& r, uint32_t m) {
+    const uint32_t l = lane();
+    const bool v = l < m;
+    const uint32_t len = v ? r.ll + r.ml : 0u;
+    const uint32_t incl = wave_scan(len);
+    const uint32_t o = x.op + incl - len;
+    const uint32_t hi = x.op + rl(incl, (int)m - 1);
+    if (v && r.ll) {
+        for (uint32_t c = 0; c < r.ll; c += 16)
+            xst(x.r, o + c, ld16(s, (int64_t)r.lip + c), r.ll - c < 16 ? r.ll - c : 16);
+    }
+    const uint32_t d = o + r.ll, src = d - r.off;
+    bool pend = v && r.ml > 0;
+    // sources before (batch end - 64 KiB): their ring slots may be rewritten by this batch
+    const bool far = x.linked && pend && hi > kXRing && src < hi - kXRing;
+    if (__ballot(far)) wait_vm();
+    for (;;) {
+        const uint64_t pm = __ballot(pend);
+        if (!pm) break;
+        const int first = __builtin_ctzll(pm);
+        const uint32_t f = rl(d, first);
+        const bool ready = pend && (src + r.ml <= f || l == (uint32_t)first);
+        if (ready) xmatch(x, d, r.off, r.ml, far);
+        pend = pend && !ready;
+    }
+    x.op = hi;
+    if ((x.op & ~1023u) > x.flushed) xflush_chunks(x);
+}
+
+// one long record, wave-cooperatively
+DEV void xbig(XRing& x, const Src& s, uint32_t lip, uint32_t ll, uint32_t ml, uint32_t off) {
+    const uint32_t l = lane();
+    for (uint32_t c = 0; c < ll; c += 1024) {
+        const uint32_t k = c + 16 * l;
+        if (k < ll) xst(x.r, x.op + k, ld16(s, (int64_t)lip + k), ll - k < 16 ? ll - k : 16);
+        const uint32_t e = x.op + (c + 1024 < ll ? c + 1024 : ll);
+        if ((e & ~1023u) > x.flushed) xflush(x, e & ~1023u);
+    }
+    x.op += ll;
+    if (ml == 0) return;
+    const uint32_t d = x.op, sp = d - off;
+    if (off == 0 || off >= 64) {
+        // 64 bytes per step, one per lane; a step never reads what it
+        // writes (off >= 64).  Sources more than 63 KiB back are read from
+        // the arena (stored: the flush lags at most 3 KiB), as the ring may
+        // no longer hold them
+        const bool far = off > kXRing - 1024;
+        for (uint32_t c = 0; c < 64 * ((ml + 63) / 64); c += 64) {
+            if (far) wait_vm();
+            uint32_t v = 0;
+            if (off && c + l < ml)
+                v = far ? __builtin_amdgcn_raw_buffer_load_b8(x.rs, sp + c + l, 0, kSc1) : (uint32_t)x.r[(sp + c + l) & kXM];
+            if (c + l < ml) x.r[(d + c + l) & kXM] = (uint8_t)v;
+            const uint32_t step = 64;
+            const uint32_t e = d + (c + step < ml ? c + step : ml);
+            if ((e & ~1023u) > x.flushed + 2048) xflush(x, e & ~1023u);
+        }
+    } else {
+        // period off: lanes k < L = off * floor(64 / off) hold the pattern
+        // once; every L output bytes repeat it
+        const uint32_t L = off * (64u / off);
+        const uint32_t k = l < L ? l : 0u;
+        const uint32_t inv = 65536u / off + 1u;  // (k * inv) >> 16 = k / off for k < 64, off < 64
+        const uint32_t v = x.r[(sp + (k - off * ((k * inv) >> 16))) & kXM];
+        for (uint32_t c = 0; c < ml; c += L) {
+            if (l < L && c + l < ml) x.r[(d + c + l) & kXM] = (uint8_t)v;
+            const uint32_t e = d + (c + L < ml ? c + L : ml);
+            if ((e & ~1023u) > x.flushed + 2048) xflush(x, e & ~1023u);
+        }
+    }
+    x.op += ml;
+    if ((x.op & ~1023u) > x.flushed) xflush_chunks(x);
+}
+
+DEV void xrecords(XRing& x, const Src& s, const SeqRec* recs, uint32_t cnt) {
+    const uint32_t l = lane();
+    for (uint32_t b = 0; b < cnt;) {
+        const uint32_t k = b + l;
+        SeqRec r{0, 0, 0, 0};
+        if (k < cnt) r = recs[k];
+        const bool big = k < cnt && (r.ll > kBig || r.ml > kBig);
+        const uint64_t bb = __ballot(big);
+        uint32_t m = cnt - b < 64 ? cnt - b : 64;
+        if (bb) {
+            const uint32_t fb = (uint32_t)__builtin_ctzll(bb);
+            if (fb < m) m = fb;
+        }
+        if (m == 0) {
+            xbig(x, s, uni32(r.lip), uni32(r.ll), uni32(r.ml), uni32(r.off));
+            b += 1;
+        } else {
+            xbatch(x, s, r, m);
+            b += m;
+        }
+    }
+}
+
+// raw bytes straight from the stream to the arena (an independent raw
+// block): 16 bytes per lane, 4 KiB per step
+DEV void xcopy_raw(uint8_t* dst, const Src& s, uint32_t len) {
+    const uint32_t l = lane();
+    uint32_t c = 0;
+    for (; c + 4096 <= len; c += 4096) {
+        uint4 v[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++) v[u] = ld16(s, (int64_t)c + 1024 * u + 16 * l);
+#pragma unroll
+        for (int u = 0; u < 4; u++) gst16(dst + c + 1024 * u + 16 * l, v[u]);
+    }
+    for (; c < len; c += 1024) {
+        const uint32_t k = c + 16 * l;
+        if (k + 16 <= len) gst16(dst + k, ld16(s, k));
+        else if (k < len)
+            for (uint32_t b = k; b < len; b++) dst[b] = s.p[b];
+    }
+}
+
+// A lane's piece: its stream, walk state and records
+struct Piece {
+    Src s;
+    PState ps;
+    uint32_t nrec;
+    uint32_t kind, cap;
+    uint64_t dst;
+};
+
+// walk (or continue walking) this lane's piece into its record buffer
+DEV void piece_walk(Piece& pc, SeqRec* buf) {
+    RecSink sink{buf, 0, kRecsPerLane};
+    if (pc.kind & kBlkSnappy) snappy_run(pc.s, pc.ps, sink);
+    else lz4_run(pc.s, (int32_t)pc.cap, 65536, pc.ps, sink);
+    pc.nrec = sink.n;
+}
+
+DEV void piece_begin(Piece& pc, const DeviceJob& j, const BlockItem& it) {
+    const uint64_t n = it.csize;
+    pc.s = Src{j.data + it.src, (int64_t)n, (int64_t)(j.data_len - it.src)};
+    pc.kind = it.kind;
+    pc.cap = it.cap;
+    pc.dst = it.dst;
+    pc.nrec = 0;
+    pc.ps.ip = pc.ps.op = pc.ps.need = 0;
+    pc.ps.ulen = 0;
+    pc.ps.safe = 0;
+    pc.ps.st = 0;
+    if ((it.kind & kBlkChecksum) && le32(Src{pc.s.p, (int64_t)n + 4, pc.s.rl}, (int64_t)n) != xxh32_lane(pc.s.p, n, 0)) {
+        pc.ps.st = -1;  // block checksum mismatch (LZ4F_decompress, checked before the block decodes)
+        return;
+    }
+    if (it.kind & kBlkRaw) {
+        pc.ps.st = 1;
+        pc.ps.op = (int32_t)n;
+        return;
+    }
+    if (it.kind & kBlkSnappy) snappy_begin(pc.ps, pc.s, (it.kind & kBlkWhole) != 0);
+    else lz4_begin(pc.ps, pc.s, (int32_t)it.cap);
+}
+
+DEV uint64_t rl64(uint64_t v, uint32_t l) { return (uint64_t)rl((uint32_t)v, (int)l) | ((uint64_t)rl((uint32_t)(v >> 32), (int)l) << 32); }
+
+// execute lane jl's piece (walked by piece_walk) at x.op; returns its decoded
+// length or -1.  Resumes the walk (lane jl alone) while records remain.
+DEV int32_t piece_exec(XRing& x, Piece& pc, SeqRec* region, uint32_t jl, uint32_t hist) {
+    const uint32_t l = lane();
+    int32_t st = (int32_t)rl((uint32_t)pc.ps.st, (int)jl);
+    if (st < 0) return -1;
+    const uint32_t kind = rl(pc.kind, (int)jl);
+    const Src s{(const uint8_t*)(uintptr_t)rl64((uint64_t)(uintptr_t)pc.s.p, jl), (int64_t)rl64((uint64_t)pc.s.n, jl),
+                (int64_t)rl64((uint64_t)pc.s.rl, jl)};
+    if (kind & kBlkRaw) {
+        const uint32_t n = (uint32_t)s.n;
+        if (x.linked) xbig(x, s, 0, n, 0, 0);
+        else xcopy_raw(x.dst + x.op, s, n);
+        return (int32_t)n;
+    }
+    const uint32_t start = x.op;
+    const SeqRec* buf = region + (size_t)jl * kRecsPerLane;
+    for (;;) {
+        const uint32_t nrec = rl(pc.nrec, (int)jl);
+        xrecords(x, s, buf, nrec);
+        if (st != 0) break;
+        if (l == jl) piece_walk(pc, region + (size_t)jl * kRecsPerLane);
+        st = (int32_t)rl((uint32_t)pc.ps.st, (int)jl);
+        if (st < 0) return -1;
+    }
+    // history check of the walk (run with H = 64 KiB)
+    const int32_t need = (int32_t)rl((uint32_t)pc.ps.need, (int)jl);
+    if (need > (int32_t)hist) return -1;
+    return (int32_t)(x.op - start);
+}
+
+// the pieces of one linked LZ4F frame (blocks first .. first + nb - 1, nb <= 64)
+DEV void exec_linked(const DeviceJob& j, lds_u8* ring, SeqRec* region, uint32_t item) {
+    const uint32_t l = lane();
+    const uint32_t first = uni32(j.plans[item].first), nb = uni32(j.plans[item].nb);
+    Piece pc;
+    pc.ps.st = -1;
+    pc.nrec = 0;
+    pc.kind = 0;
+    pc.s = Src{nullptr, 0, 0};
+    if (l < nb) {
+        const BlockItem it = j.blocks[first + l];
+        piece_begin(pc, j, it);
+        piece_walk(pc, region + (size_t)l * kRecsPerLane);
+    }
+    const uint64_t fdst = uni64(j.dcap[j.decode_list[item]]);
+    XRing x;
+    x.r = ring;
+    x.dst = j.decoded + fdst;
+    x.op = 0;
+    x.flushed = 0;
+    x.linked = true;
+    const uint64_t room = j.decoded_capacity - fdst;
+    x.rs = __builtin_amdgcn_make_buffer_rsrc(x.dst, 0, (int)(room < 0x7FFFFFFFull ? room : 0x7FFFFFFFull), kBufFlags);
+    bool ok = true;
+    for (uint32_t k = 0; k < nb; k++) {
+        const uint32_t at = x.op;
+        const int32_t dd = ok ? piece_exec(x, pc, region, k, at) : -1;
+        if (dd < 0) ok = false;
+        if (l == 0) {
+            j.blocks[first + k].dst = fdst + at;
+            j.blocks[first + k].out = dd;
+        }
+    }
+    xflush(x, x.op);
+}
+
+// 64 consecutive block items (independent pieces; linked blocks are skipped)
+DEV void exec_chunk(const DeviceJob& j, lds_u8* ring, SeqRec* region, uint32_t base, uint32_t nblk) {
+    const uint32_t l = lane();
+    const uint32_t it_i = base + l;
+    Piece pc;
+    pc.ps.st = -1;
+    pc.nrec = 0;
+    pc.kind = 0;
+    pc.s = Src{nullptr, 0, 0};
+    bool act = false;
+    if (it_i < nblk) {
+        const BlockItem it = j.blocks[it_i];
+        act = !(it.kind & kBlkLinked);
+        if (act) {
+            piece_begin(pc, j, it);
+            piece_walk(pc, region + (size_t)l * kRecsPerLane);
+        }
+    }
+    uint64_t todo = __ballot(act);
+    while (todo) {
+        const uint32_t jl = (uint32_t)__builtin_ctzll(todo);
+        todo &= todo - 1;
+        const uint64_t dst = rl64(pc.dst, jl);
+        XRing x;
+        x.r = ring;
+        x.dst = j.decoded + dst;
+        x.op = 0;
+        x.flushed = 0;
+        // a piece longer than the ring wraps it: wrap-aware like a linked frame
+        x.linked = rl(pc.cap, (int)jl) > kXRing;
+        const uint64_t room = j.decoded_capacity - dst;
+        x.rs = __builtin_amdgcn_make_buffer_rsrc(x.dst, 0, (int)(room < 0x7FFFFFFFull ? room : 0x7FFFFFFFull), kBufFlags);
+        const int32_t dd = piece_exec(x, pc, region, jl, 0);
+        if (dd >= 0) xflush(x, x.op);
+        if (l == 0) j.blocks[base + jl].out = dd;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// k_lz_exec: persistent, one wave per workgroup (64 KiB LDS ring each),
+// j.exec_waves of them; units by one agent-scope counter (counters[8]):
+// first the linked frames, then the block list in chunks of 64.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(64) void k_lz_exec(DeviceJob j) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t xlds[];
+    lds_u8* ring = (lds_u8*)xlds;
+    SeqRec* region = j.seqs + (size_t)blockIdx.x * 64 * kRecsPerLane;
+    const uint32_t nlink = j.counters[7];
+    const uint32_t reserved = j.counters[4];
+    const uint32_t nblk = reserved < j.block_capacity ? reserved : j.block_capacity;
+    const uint32_t total = nlink + (nblk + 63) / 64;
+    for (;;) {
+        const uint32_t u = wave_fetch_add(&j.counters[8], 1u);
+        if (u >= total) break;
+        if (u < nlink) exec_linked(j, ring, region, uni32(j.link_list[u]));
+        else exec_chunk(j, ring, region, (u - nlink) * 64, nblk);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// k_decode_blocks: the sequential frames (what the planner did not split:
+// truncated or malformed frames, linked frames of more than 64 blocks,
+// unplannable snappy-java streams), one per lane through the lane engine,
+// taken off counters[5].
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void k_decode_blocks(DeviceJob j) {
     const uint32_t nseq = j.counters[6];
-    const uint32_t reserved = j.counters[4];
-    const uint32_t nblk = reserved < j.block_capacity ? reserved : j.block_capacity;
-    const uint32_t total = nseq + nblk;
     const int64_t data_len = (int64_t)j.data_len;
     for (;;) {
         const uint32_t item = atomicAdd(&j.counters[5], 1u);
-        if (item >= total) break;
-        uint32_t b = 0, single = 0, bcap = 0, blk = 0;
-        int codec;
-        uint64_t src, dst, cap;
-        int64_t n;
-        if (item < nseq) {
-            b = j.decode_list[j.seq_list[item]];
-            const rpgpu_batch_result* R = &j.batches[b];
-            src = j.seg_off[R->segment] + R->file_pos + RPGPU_HEADER_SIZE;
-            n = (int64_t)(uint32_t)(R->size_bytes - (int32_t)RPGPU_HEADER_SIZE);
-            codec = (int)((uint32_t)(uint16_t)R->attrs & 7u);
-            dst = j.dcap[b];
-            cap = j.dcap[b + 1] - dst;
-        } else {
-            blk = item - nseq;
-            const BlockItem it = j.blocks[blk];
-            src = it.src;
-            dst = it.dst;
-            bcap = it.cap;
-            cap = it.cap;
-            codec = (it.kind & kBlkSnappy) ? RPGPU_CODEC_SNAPPY : RPGPU_CODEC_LZ4;
-            single = it.kind | 0x100u;
-            n = (int64_t)it.csize + ((it.kind & kBlkChecksum) ? 4 : 0);
-        }
+        if (item >= nseq) break;
+        const uint32_t b = j.decode_list[j.seq_list[item]];
+        rpgpu_batch_result* R = &j.batches[b];
+        const uint64_t src = j.seg_off[R->segment] + R->file_pos + RPGPU_HEADER_SIZE;
+        const int64_t n = (int64_t)(uint32_t)(R->size_bytes - (int32_t)RPGPU_HEADER_SIZE);
+        const int codec = (int)((uint32_t)(uint16_t)R->attrs & 7u);
+        const uint64_t dst = j.dcap[b], cap = j.dcap[b + 1] - dst;
         int64_t got = 0;
         const int rc = decode_unit(codec, Src{j.data + src, n, data_len - (int64_t)src}, Dst{j.decoded + dst, (int64_t)cap},
-                                   single, bcap, got);
-        if (item < nseq) {
-            if (rc == 0) {
-                rpgpu_batch_result* R = &j.batches[b];
-                R->flags = R->flags | RPGPU_F_CODEC_OK;
-                R->decoded_len = (uint32_t)got;
-            }
-        } else {
-            j.blocks[blk].out = (int32_t)(rc == 0 ? got : -1);
+                                   0, 0, got);
+        if (rc == 0) {
+            R->flags = R->flags | RPGPU_F_CODEC_OK;
+            R->decoded_len = (uint32_t)got;
         }
     }
 }
@@ -981,13 +1528,47 @@ __global__ __launch_bounds__(64) void k_uncompress_one(int codec, const uint8_t*
     res[1] = got;
 }
 
+#ifdef RPGPU_DSTAMPS
+__global__ void k_print_dstamps() {
+    const char* kn[5] = {"lz4 frames", "snappy streams", "lz4 blocks", "raw blocks", "snappy chunks"};
+    const unsigned long long t0 = g_dst[63];
+    for (int k = 0; k < 5; k++) {
+        const unsigned long long* g = &g_dst[8 * k];
+        if (!g[0]) continue;
+        printf("RPGPU_DSTAMPS %s: n=%llu avg_us=%.1f max_us=%.1f first_start_us=%.1f last_end_us=%.1f in=%llu out=%llu max_in=%llu\n",
+               kn[k], g[0], g[1] / 100.0 / g[0], g[2] / 100.0, (g[7] - t0) / 100.0, (g[3] - t0) / 100.0, g[4], g[5], g[6]);
+    }
+    for (int i = 0; i < 64; i++) g_dst[i] = (i % 8 == 7 || i == 63) ? ~0ull : 0ull;
+}
+__global__ void k_init_dstamps() {
+    for (int i = 0; i < 64; i++) g_dst[i] = (i % 8 == 7 || i == 63) ? ~0ull : 0ull;
+}
+#endif
+
 hipError_t launch_decode(const DeviceJob& j, hipStream_t s, uint32_t grid) {
     hipLaunchKernelGGL(k_decode, dim3(grid), dim3(256), 0, s, j);
     return hipGetLastError();
 }
 
 hipError_t launch_decode_blocks(const DeviceJob& j, hipStream_t s, uint32_t grid) {
+#ifdef RPGPU_DSTAMPS
+    hipLaunchKernelGGL(k_init_dstamps, dim3(1), dim3(1), 0, s);
+#endif
     hipLaunchKernelGGL(k_decode_blocks, dim3(grid), dim3(256), 0, s, j);
+#ifdef RPGPU_DSTAMPS
+    hipLaunchKernelGGL(k_print_dstamps, dim3(1), dim3(1), 0, s);
+#endif
+    return hipGetLastError();
+}
+
+hipError_t launch_lz_exec(const DeviceJob& j, hipStream_t s) {
+    static bool attr = false;
+    if (!attr) {
+        (void)hipFuncSetAttribute((const void*)k_lz_exec, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kXRing);
+        attr = true;
+    }
+    if (!j.exec_waves) return hipSuccess;
+    hipLaunchKernelGGL(k_lz_exec, dim3(j.exec_waves), dim3(64), kXRing, s, j);
     return hipGetLastError();
 }
 

@@ -66,18 +66,31 @@ struct SegTerm {
     int32_t eof;
 };
 
-// One independently decodable piece of a compressed payload (an LZ4F block
-// of a block-independent frame, or a snappy-java chunk), decoded by its own
-// wave into its planned arena position.
+// One piece of a planned compressed payload: an LZ4F block, a snappy-java
+// chunk, or a whole raw snappy stream.  Independent pieces decode into their
+// planned arena position; the blocks of a linked LZ4F frame are decoded in
+// order by one wave, which rewrites `dst` with the position each landed at.
 struct BlockItem {
     uint64_t src;    // absolute offset of the block data in the job's data
-    uint64_t dst;    // absolute offset in the decoded arena (planned)
+    uint64_t dst;    // absolute offset in the decoded arena (planned; actual for linked blocks)
     uint32_t csize;  // block data bytes
     uint32_t kind;   // kBlk* bits
-    int32_t out;     // decoded bytes, -1 on failure (written by k_decode_blocks)
-    uint32_t cap;    // bytes reserved at dst
+    int32_t out;     // decoded bytes, -1 on failure (written by k_lz_exec)
+    uint32_t cap;    // bytes reserved at dst (LZ4: the block maximum = the decoder's output bound)
 };
-constexpr uint32_t kBlkRaw = 1, kBlkChecksum = 2, kBlkSnappy = 4;
+// kBlkWhole: a raw (non-xerial) snappy payload, snappy_standard_compressor
+// semantics (length 0 is an empty result whatever follows)
+constexpr uint32_t kBlkRaw = 1, kBlkChecksum = 2, kBlkSnappy = 4, kBlkLinked = 8, kBlkWhole = 16;
+
+// One parsed sequence of an LZ4 block / snappy tag: literal bytes
+// [lip, lip + ll) of the piece's stream, then ml bytes copied from `off`
+// back (ml = 0: literal only).  Written by the parse phase of k_lz_exec,
+// executed by its wave phase.
+struct SeqRec {
+    uint32_t lip, ll, ml, off;
+};
+constexpr uint32_t kRecsPerLane = 4096;   // parse-phase records per lane before the wave executes them
+constexpr uint32_t kExecWgsPerCu = 2;     // k_lz_exec: one wave per workgroup, 64 KiB LDS ring each
 
 // Per decode item: how its payload is being decoded
 struct FramePlan {
@@ -117,9 +130,13 @@ struct DeviceJob {
     uint64_t* bitmap;
     const Tables* tables;
     uint32_t* counters;           // [0] rewalks, [1] overflow bits, [2] decode items, [3] unused,
-                                  // [4] block items reserved, [5] decode claim cursor, [6] sequential frames
+                                  // [4] block items reserved, [5] sequential-frame claim cursor,
+                                  // [6] sequential frames, [7] linked frames, [8] k_lz_exec claim cursor
     uint32_t* decode_list;        // batch_capacity: ordinals of batches to uncompress
-    uint32_t* seq_list;           // batch_capacity: decode items decoded whole by one wave
+    uint32_t* seq_list;           // batch_capacity: decode items decoded whole by one lane
+    uint32_t* link_list;          // batch_capacity: decode items whose linked LZ4F blocks one wave decodes in order
+    SeqRec* seqs;                 // k_lz_exec parse records: kRecsPerLane per lane of each resident wave
+    uint32_t exec_waves;          // k_lz_exec grid (one wave per workgroup; sizes `seqs`)
     BlockItem* blocks;            // block work list ([4] items reserved, [5] claim cursor)
     uint32_t block_capacity;
     FramePlan* plans;             // one per decode item
@@ -135,6 +152,7 @@ hipError_t launch_validate(const DeviceJob& j, hipStream_t s, uint32_t grid);  /
 hipError_t launch_walk(const DeviceJob& j, hipStream_t s, uint32_t grid);
 hipError_t launch_decode(const DeviceJob& j, hipStream_t s, uint32_t grid);    // rp_codec.hip
 hipError_t launch_decode_blocks(const DeviceJob& j, hipStream_t s, uint32_t grid);
+hipError_t launch_lz_exec(const DeviceJob& j, hipStream_t s);
 hipError_t launch_decode_finish(const DeviceJob& j, hipStream_t s, uint32_t grid);
 // one payload, one wave (rpgpu_uncompress); res[0] = rc (0 / -1 / -2), res[1] = out_len
 hipError_t launch_uncompress_one(int codec, const uint8_t* src, uint64_t n, uint8_t* dst, uint64_t cap,

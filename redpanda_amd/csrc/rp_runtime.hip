@@ -107,6 +107,10 @@ struct rpgpu_ctx {
     // rpgpu_segment_index workspace (piece tables), grow-only
     void* iws = nullptr;
     size_t iws_bytes = 0;
+    // k_lz_exec parse records (kRecsPerLane per lane of each resident wave),
+    // allocated on the first decode job
+    SeqRec* seqs = nullptr;
+    uint32_t exec_waves = 0;
     std::string err;
     // rpgpu_validate_host: a copy stream and two staging slots (segment
     // bytes in, per-batch results out), used alternately so the H2D copy of
@@ -192,6 +196,7 @@ int rpgpu_destroy(rpgpu_ctx* c) {
     if (c->ws) hipFree(c->ws);
     if (c->uws) hipFree(c->uws);
     if (c->iws) hipFree(c->iws);
+    if (c->seqs) hipFree(c->seqs);
     if (c->pin) hipHostFree(c->pin);
     if (c->d_tables) hipFree(c->d_tables);
     for (auto& set : c->ev_sets)
@@ -334,9 +339,10 @@ int rpgpu_submit(rpgpu_ctx* c, const rpgpu_job* job, void* stream) {
     const size_t o_segterm = take(nseg * sizeof(SegTerm));
     const size_t o_slots = take((bcap + 1) * 8);
     const size_t o_dcap = take((bcap + 1) * 8);
-    const size_t o_counters = take(32);
+    const size_t o_counters = take(64);
     const size_t o_dlist = take((bcap + 1) * 4);
     const size_t o_slist = take((bcap + 1) * 4);
+    const size_t o_llist = take((bcap + 1) * 4);
     const size_t o_fbad = take((size_t)nseg * 4);
     // block-parallel decode: one item per LZ4F block / snappy-java chunk
     const bool dec = (job->flags & RPGPU_JOB_DECODE) && job->d_decoded;
@@ -346,6 +352,14 @@ int rpgpu_submit(rpgpu_ctx* c, const rpgpu_job* job, void* stream) {
     const size_t o_plans = take(dec ? (bcap + 1) * sizeof(FramePlan) : 0);
     const size_t o_scan = take(scan_temp_bytes(std::max<uint64_t>(tc, bcap)) + 64);
     const size_t need = off;
+    if (dec && !c->seqs) {
+        const uint32_t waves = c->cu_count * kExecWgsPerCu;
+        if (hipMalloc(&c->seqs, (size_t)waves * 64 * kRecsPerLane * sizeof(SeqRec)) != hipSuccess) {
+            c->seqs = nullptr;
+            return fail(c, RPGPU_E_NOMEM, "decode sequence workspace");
+        }
+        c->exec_waves = waves;
+    }
     if (need > c->ws_bytes) {
         if (c->ws) { hipStreamSynchronize(s); hipFree(c->ws); c->ws = nullptr; }
         if (hipMalloc(&c->ws, need) != hipSuccess) { c->ws_bytes = 0; return fail(c, RPGPU_E_NOMEM, "workspace"); }
@@ -382,6 +396,9 @@ int rpgpu_submit(rpgpu_ctx* c, const rpgpu_job* job, void* stream) {
     j.counters = (uint32_t*)(ws + o_counters);
     j.decode_list = (uint32_t*)(ws + o_dlist);
     j.seq_list = (uint32_t*)(ws + o_slist);
+    j.link_list = (uint32_t*)(ws + o_llist);
+    j.seqs = c->seqs;
+    j.exec_waves = c->exec_waves;
     j.seg_first_bad = (uint32_t*)(ws + o_fbad);
     j.blocks = (BlockItem*)(ws + o_blocks);
     j.block_capacity = (uint32_t)bl_cap64;
@@ -414,7 +431,7 @@ int rpgpu_submit(rpgpu_ctx* c, const rpgpu_job* job, void* stream) {
         HIPCHK(c, hipEventRecord(ev[0], s));
     }
     STAGE("chunk_base", launch_chunk_base(j, s));
-    HIPCHK(c, hipMemsetAsync(j.counters, 0, 32, s));
+    HIPCHK(c, hipMemsetAsync(j.counters, 0, 64, s));
     HIPCHK(c, hipMemsetAsync(j.seg_first_bad, 0xFF, (size_t)nseg * 4, s));
     STAGE("discover", launch_discover(j, s));
     if (tm) HIPCHK(c, hipEventRecord(ev[1], s));
@@ -429,6 +446,7 @@ int rpgpu_submit(rpgpu_ctx* c, const rpgpu_job* job, void* stream) {
     if ((job->flags & RPGPU_JOB_DECODE) && j.decoded) {
         STAGE("decode", launch_decode(j, s, c->cu_count * 8));
         STAGE("decode_blocks", launch_decode_blocks(j, s, c->cu_count * 8));
+        STAGE("lz_exec", launch_lz_exec(j, s));
         STAGE("decode_finish", launch_decode_finish(j, s, c->cu_count * 8));
     }
     if (tm) HIPCHK(c, hipEventRecord(ev[3], s));

@@ -9,3 +9,7 @@ timeout -s KILL 200 rocprofv3 --pmc SQ_INSTS_LDS SQ_INSTS_SMEM SQ_INSTS_VMEM_RD 
 echo "pass b ok"
 timeout -s KILL 200 rocprofv3 --pmc SQ_INSTS_BRANCH SQ_ACTIVE_INST_MISC SQ_INST_CYCLES_SALU SQ_INSTS_FLAT SQ_INSTS_FLAT_LDS_ONLY GRBM_GUI_ACTIVE GRBM_COUNT -d gpurun_out/${TAG}_c -o c --output-format csv -- python3 scripts/dbg_job.py c2 4 32 > gpurun_out/${TAG}_c.log 2>&1
 echo "pass c ok"
+if [ "${2:-}" = "tcp" ]; then
+timeout -s KILL 200 rocprofv3 --pmc TCP_UTCL1_TRANSLATION_MISS_sum TCP_UTCL1_TRANSLATION_HIT_sum TCP_TCC_READ_REQ_sum TCP_TCC_WRITE_REQ_sum -d gpurun_out/${TAG}_d -o d --output-format csv -- python3 scripts/dbg_job.py c2 4 32 > gpurun_out/${TAG}_d.log 2>&1
+echo "pass d ok"
+fi
