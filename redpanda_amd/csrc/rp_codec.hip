@@ -280,7 +280,30 @@ struct PState {
     uint32_t safe;     // lz4: in the safe loop
 };
 
-DEV int32_t lz_read_var(const Src& s, int32_t& ip, int32_t lencheck, bool loop_check, bool initial_check, int& err) {
+// the input window: 16 stream bytes from wb, reloaded (one unaligned
+// 16-byte load) only when a read falls outside it; an LZ4 sequence of
+// short lengths spans 3-4 bytes, so one load serves several
+struct Win {
+    uint4 w;
+    int32_t wb;
+};
+DEV void win_need(Win& W, const Src& s, int32_t p, int32_t nbytes) {
+    if (p < W.wb || p + nbytes > W.wb + 16) {
+        W.w = ld16(s, p);
+        W.wb = p;
+    }
+}
+DEV uint32_t win_byte(Win& W, const Src& s, int32_t p) {
+    win_need(W, s, p, 1);
+    const uint32_t k = (uint32_t)(p - W.wb);
+    return (dw(W.w, k >> 2) >> (8 * (k & 3))) & 0xFFu;
+}
+DEV uint32_t win_le16(Win& W, const Src& s, int32_t p) {
+    win_need(W, s, p, 2);
+    return at32(W.w, (uint32_t)(p - W.wb)) & 0xFFFFu;
+}
+
+DEV int32_t lz_read_var(Win& W, const Src& s, int32_t& ip, int32_t lencheck, bool loop_check, bool initial_check, int& err) {
     int32_t length = 0;
     uint32_t b;
     err = 0;
@@ -289,7 +312,7 @@ DEV int32_t lz_read_var(const Src& s, int32_t& ip, int32_t lencheck, bool loop_c
         return length;
     }
     do {
-        b = b8(s, ip);
+        b = win_byte(W, s, ip);
         ip++;
         length += (int32_t)b;
         if (loop_check && ip >= lencheck) {
@@ -309,16 +332,16 @@ DEV void lz4_begin(PState& ps, const Src& s, int32_t oend) {
     else if (s.n == 0) ps.st = -1;
 }
 
-// sinks: seq(w, tip, lip, llen, lo, off, ml) with the 16 stream bytes at
-// the token (w, from tip), the literal [lip, lip + llen) to output lo and
-// the match (off, ml; ml = 0: none) at lo + llen; false = suspend after it
+// sinks: seq(w, wb, lip, llen, lo, off, ml) with the input window (16 stream
+// bytes from wb), the literal [lip, lip + llen) to output lo and the match
+// (off, ml; ml = 0: none) at lo + llen; false = suspend after it
 struct DirectSink {
     const Src& s;
     const Dst& d;
-    DEV bool seq(const uint4& w, int32_t tip, int32_t lip, int32_t llen, int32_t lo, uint32_t off, int32_t ml) {
+    DEV bool seq(const uint4& w, int32_t wb, int32_t lip, int32_t llen, int32_t lo, uint32_t off, int32_t ml) {
         if (llen > 0) {
-            // short literals right behind the token are already in w
-            if (lip == tip + 1 && llen <= 15) put(d, lo, shr1(w), (uint32_t)llen);
+            // short literals right behind a window-leading token are already in w
+            if (lip == wb + 1 && llen <= 15) put(d, lo, shr1(w), (uint32_t)llen);
             else copy_in(s, lip, d, lo, llen);
         }
         if (ml > 0) copy_match(d, (int64_t)lo + llen, off, ml);
@@ -342,21 +365,22 @@ DEV void lz4_run(const Src& s, int32_t oend, int32_t H, PState& ps, Sink& sink) 
     int32_t ip = ps.ip, op = ps.op, need = ps.need, length, offset = 0, cpy = 0, lip = 0, llen = 0, ml = 0;
     int err;
     bool last = false, safe = ps.safe != 0;
+    Win W;
+    W.w = ld16(s, ip);
+    W.wb = ip;
 #define LZ_FAIL() do { ps.st = -1; return; } while (0)
     // The two loops of LZ4_decompress_generic as one: `safe` is the safe
     // loop (entered for good at the first fast-loop exit); every path ends at
     // `emit` with the sequence's literal (lip, llen; op already past it) and
     // match (offset, ml).
     for (;;) {
-        const int32_t tip = ip;
-        const uint4 w = ld16(s, tip);  // the token and the 15 bytes after it
-        const uint32_t token = w.x & 0xFFu;
+        const uint32_t token = win_byte(W, s, ip);
         ip++;
         length = (int32_t)(token >> 4);
-#define RD_OFFSET() (ip - tip <= 14 ? (int32_t)(at32(w, (uint32_t)(ip - tip)) & 0xFFFFu) : (int32_t)le16(s, ip))
+#define RD_OFFSET() ((int32_t)win_le16(W, s, ip))
         if (!safe) {
             if (length == 15) {
-                length += lz_read_var(s, ip, iend - 15, true, true, err);
+                length += lz_read_var(W, s, ip, iend - 15, true, true, err);
                 if (err == 1) LZ_FAIL();
                 cpy = op + length;
                 if (cpy > oend - 32 || ip + length > iend - 32) { safe = true; goto safe_literal_copy; }
@@ -373,7 +397,7 @@ DEV void lz4_run(const Src& s, int32_t oend, int32_t H, PState& ps, Sink& sink) 
             length = (int32_t)(token & 15);
             if (length == 15) {
                 if (offset > op + H) LZ_FAIL();
-                length += lz_read_var(s, ip, iend - kLastLiterals + 1, true, false, err);
+                length += lz_read_var(W, s, ip, iend - kLastLiterals + 1, true, false, err);
                 if (err) LZ_FAIL();
                 length += kMinMatch;
                 if (op + length >= oend - kFastSafeDistance) { safe = true; goto safe_match_copy; }
@@ -400,7 +424,7 @@ DEV void lz4_run(const Src& s, int32_t oend, int32_t H, PState& ps, Sink& sink) 
             goto lbl_copy_match;
         }
         if (length == 15) {
-            length += lz_read_var(s, ip, iend - 15, true, true, err);
+            length += lz_read_var(W, s, ip, iend - 15, true, true, err);
             if (err == 1) LZ_FAIL();
         }
         cpy = op + length;
@@ -421,7 +445,7 @@ DEV void lz4_run(const Src& s, int32_t oend, int32_t H, PState& ps, Sink& sink) 
         length = (int32_t)(token & 15);
     lbl_copy_match:
         if (length == 15) {
-            length += lz_read_var(s, ip, iend - kLastLiterals + 1, true, false, err);
+            length += lz_read_var(W, s, ip, iend - kLastLiterals + 1, true, false, err);
             if (err) LZ_FAIL();
         }
         length += kMinMatch;
@@ -434,14 +458,14 @@ DEV void lz4_run(const Src& s, int32_t oend, int32_t H, PState& ps, Sink& sink) 
     emit:
 #undef RD_OFFSET
         if (last) {
-            sink.seq(w, tip, lip, llen, op - llen, 0u, 0);
+            sink.seq(W.w, W.wb, lip, llen, op - llen, 0u, 0);
             ps.st = 1;
             ps.op = op;
             ps.need = need;
             return;
         }
         if (offset - op > need) need = offset - op;
-        const bool go = sink.seq(w, tip, lip, llen, op - llen, (uint32_t)offset, ml);
+        const bool go = sink.seq(W.w, W.wb, lip, llen, op - llen, (uint32_t)offset, ml);
         op += ml;
         if (!go) {
             ps.ip = ip;
@@ -643,13 +667,19 @@ DEV void snappy_run(const Src& s, PState& ps, Sink& sink) {
     if (ps.st) return;
     const int64_t n = s.n, ulen = ps.ulen;
     int64_t ip = ps.ip, op = ps.op;
+    Win W;
+    W.w = ld16(s, ip);
+    W.wb = (int32_t)ip;
     while (ip < n) {
-        const uint4 w = ld16(s, ip);  // the tag and the 15 bytes after it
-        const uint32_t c = w.x & 0xFFu;
+        const uint32_t c = win_byte(W, s, (int32_t)ip);
         const uint32_t t = c & 3;
         const int64_t extra = t == 0 ? (((c >> 2) >= 60) ? (int64_t)((c >> 2) - 59) : 0) : t == 1 ? 1 : t == 2 ? 2 : 4;
         if (n - ip < 1 + extra) { ps.st = -1; return; }
-        const uint32_t x = at32(w, 1);  // the tag's extra bytes (at most 4)
+        uint32_t x = 0;  // the tag's extra bytes (at most 4)
+        if (extra) {
+            win_need(W, s, (int32_t)ip + 1, (int32_t)extra);
+            x = at32(W.w, (uint32_t)(ip + 1 - W.wb));
+        }
         bool go;
         if (t == 0) {
             int64_t lit = (int64_t)(c >> 2) + 1;
@@ -657,7 +687,7 @@ DEV void snappy_run(const Src& s, PState& ps, Sink& sink) {
             const int64_t lip = ip + 1 + extra;
             if (n - lip < lit) { ps.st = -1; return; }      // premature end of input
             if (ulen - op < lit) { ps.st = -1; return; }    // SnappyArrayWriter::Append overflow
-            go = sink.seq(w, (int32_t)ip, (int32_t)lip, (int32_t)lit, (int32_t)op, 0u, 0);
+            go = sink.seq(W.w, W.wb, (int32_t)lip, (int32_t)lit, (int32_t)op, 0u, 0);
             op += lit;
             ip = lip + lit;
         } else {
@@ -666,7 +696,7 @@ DEV void snappy_run(const Src& s, PState& ps, Sink& sink) {
             ip += 1 + extra;
             // AppendFromSelf: Produced() <= offset - 1u || op_end > op_limit_
             if (off == 0 || op < off || ulen - op < len) { ps.st = -1; return; }
-            go = sink.seq(w, (int32_t)ip, 0, 0, (int32_t)op, (uint32_t)off, (int32_t)len);
+            go = sink.seq(W.w, W.wb, 0, 0, (int32_t)op, (uint32_t)off, (int32_t)len);
             op += len;
         }
         if (!go && ip < n) {
@@ -1045,8 +1075,13 @@ __global__ __launch_bounds__(256) void k_decode(DeviceJob j) {
 //     linked frame, whose later blocks may copy from them).
 // ---------------------------------------------------------------------------
 typedef __attribute__((address_space(3))) uint8_t lds_u8;
-constexpr uint32_t kXRing = 65536, kXM = kXRing - 1;
-constexpr uint32_t kBig = 256;                 // longer literals / matches run wave-cooperatively
+constexpr uint32_t kXRing = kXRingKiB * 1024u, kXM = kXRing - 1;
+static_assert((kXRing & kXM) == 0 && kXRing >= 8192, "ring: a power of two >= 8 KiB");
+constexpr uint32_t kBig = 128;                 // longer literals / matches run wave-cooperatively
+// ring stores are deferred: unflushed output stays below kFlushLag (+ one
+// batch, <= 64 x 2 kBig = 16 KiB), so a batch issues no global store and the
+// loads it waits on are counted exactly (gfx9's vmcnt also counts stores)
+constexpr uint32_t kFlushLag = 24u << 10;
 constexpr uint32_t kBufFlags = 0x00020000u;    // buffer resource word 3 (raw, 32-bit data format)
 constexpr int kSc1 = 16;                       // cache policy: sc1 (L2-coherent, bypasses the vector L1)
 
@@ -1055,7 +1090,8 @@ struct XRing {
     uint8_t* dst;           // arena address of position 0
     uint32_t op;            // next output position (uniform)
     uint32_t flushed;       // positions below are stored to dst
-    bool linked;            // positions run across blocks (the ring wraps)
+    bool linked;            // positions may pass the ring size (the ring wraps)
+    bool hist;              // later pieces copy from this output (a linked frame): raw pieces go through the ring
     __amdgpu_buffer_rsrc_t rs;  // dst window for far read-backs (linked)
 };
 
@@ -1118,14 +1154,16 @@ DEV void xflush(XRing& x, uint32_t upto) {
 }
 DEV void xflush_chunks(XRing& x) { xflush(x, x.op & ~1023u); }
 
-// inclusive prefix sum over the wave
+// inclusive prefix sum over the wave on the DPP network (no LDS round
+// trips): row_shr 1/2/4/8 within each 16-lane row, then row_bcast:15 and
+// row_bcast:31 carry the row totals upward
 DEV uint32_t wave_scan(uint32_t v) {
-    const uint32_t l = lane();
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t t = (uint32_t)__shfl_up((int)v, o, 64);
-        if (l >= (uint32_t)o) v += t;
-    }
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xF, 0xF, true);  // row_shr:1
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xF, 0xF, true);  // row_shr:2
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xF, 0xF, true);  // row_shr:4
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xF, 0xF, true);  // row_shr:8
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xA, 0xF, false); // row_bcast:15
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xC, 0xF, false); // row_bcast:31
     return v;
 }
 
@@ -1158,34 +1196,63 @@ DEV void xmatch(XRing& x, uint32_t d, uint32_t off, uint32_t ml, bool far) {
     for (uint32_t c = 0; c < ml; c += step) xst(x.r, d + c, p, ml - c < 16 ? ml - c : 16);
 }
 
-// up to 64 records (lane k < m holds record k), none longer than kBig
-DEV void xbatch(XRing& x, const Src& s, const SeqRec& r, uint32_t m) {
+// the records of lanes [lo, hi) (none longer than kBig); lit0 = the first
+// 16 bytes of each lane's literal (loaded a window ahead)
+DEV void xbatch(XRing& x, const Src& s, const SeqRec& r, uint32_t lo, uint32_t hi_lane, const uint4& lit0) {
     const uint32_t l = lane();
-    const bool v = l < m;
+#ifdef RPGPU_DSTAMPS
+    const uint64_t c0 = __builtin_amdgcn_s_memtime();
+#endif
+    const bool v = l >= lo && l < hi_lane;
     const uint32_t len = v ? r.ll + r.ml : 0u;
     const uint32_t incl = wave_scan(len);
+#ifdef RPGPU_DSTAMPS
+    const uint64_t c1 = __builtin_amdgcn_s_memtime();
+#endif
     const uint32_t o = x.op + incl - len;
-    const uint32_t hi = x.op + rl(incl, (int)m - 1);
+    const uint32_t hi = x.op + rl(incl, (int)hi_lane - 1);
     if (v && r.ll) {
-        for (uint32_t c = 0; c < r.ll; c += 16)
+        xst(x.r, o, lit0, r.ll < 16 ? r.ll : 16);
+        for (uint32_t c = 16; c < r.ll; c += 16)
             xst(x.r, o + c, ld16(s, (int64_t)r.lip + c), r.ll - c < 16 ? r.ll - c : 16);
     }
     const uint32_t d = o + r.ll, src = d - r.off;
     bool pend = v && r.ml > 0;
+#ifdef RPGPU_DSTAMPS
+    const uint64_t c2 = __builtin_amdgcn_s_memtime();
+    uint32_t rounds = 0;
+#endif
     // sources before (batch end - 64 KiB): their ring slots may be rewritten by this batch
     const bool far = x.linked && pend && hi > kXRing && src < hi - kXRing;
     if (__ballot(far)) wait_vm();
     for (;;) {
         const uint64_t pm = __ballot(pend);
         if (!pm) break;
+#ifdef RPGPU_DSTAMPS
+        rounds++;
+#endif
         const int first = __builtin_ctzll(pm);
         const uint32_t f = rl(d, first);
         const bool ready = pend && (src + r.ml <= f || l == (uint32_t)first);
         if (ready) xmatch(x, d, r.off, r.ml, far);
         pend = pend && !ready;
     }
+#ifdef RPGPU_DSTAMPS
+    const uint64_t c3 = __builtin_amdgcn_s_memtime();
+#endif
     x.op = hi;
-    if ((x.op & ~1023u) > x.flushed) xflush_chunks(x);
+    if (x.op - x.flushed > kFlushLag) xflush_chunks(x);
+#ifdef RPGPU_DSTAMPS
+    const uint64_t c4 = __builtin_amdgcn_s_memtime();
+    if (l == 0) {
+        atomicAdd(&g_dst[16], c1 - c0);   // scan
+        atomicAdd(&g_dst[17], c2 - c1);   // literals
+        atomicAdd(&g_dst[18], c3 - c2);   // rounds
+        atomicAdd(&g_dst[19], c4 - c3);   // flush
+        atomicAdd(&g_dst[20], 1ull);      // batches
+        atomicAdd(&g_dst[21], (unsigned long long)rounds);
+    }
+#endif
 }
 
 // one long record, wave-cooperatively
@@ -1195,26 +1262,25 @@ DEV void xbig(XRing& x, const Src& s, uint32_t lip, uint32_t ll, uint32_t ml, ui
         const uint32_t k = c + 16 * l;
         if (k < ll) xst(x.r, x.op + k, ld16(s, (int64_t)lip + k), ll - k < 16 ? ll - k : 16);
         const uint32_t e = x.op + (c + 1024 < ll ? c + 1024 : ll);
-        if ((e & ~1023u) > x.flushed) xflush(x, e & ~1023u);
+        if (e - x.flushed > kFlushLag) xflush(x, e & ~1023u);
     }
     x.op += ll;
     if (ml == 0) return;
     const uint32_t d = x.op, sp = d - off;
     if (off == 0 || off >= 64) {
         // 64 bytes per step, one per lane; a step never reads what it
-        // writes (off >= 64).  Sources more than 63 KiB back are read from
-        // the arena (stored: the flush lags at most 3 KiB), as the ring may
-        // no longer hold them
-        const bool far = off > kXRing - 1024;
+        // writes (off >= 64).  Sources more than ring - 1 KiB back are read
+        // from the arena (stored: the flush lags at most kFlushLag + 1 KiB),
+        // as the ring may no longer hold them
+        const bool far = x.linked && off > kXRing - 1024;
         for (uint32_t c = 0; c < 64 * ((ml + 63) / 64); c += 64) {
             if (far) wait_vm();
             uint32_t v = 0;
             if (off && c + l < ml)
                 v = far ? __builtin_amdgcn_raw_buffer_load_b8(x.rs, sp + c + l, 0, kSc1) : (uint32_t)x.r[(sp + c + l) & kXM];
             if (c + l < ml) x.r[(d + c + l) & kXM] = (uint8_t)v;
-            const uint32_t step = 64;
-            const uint32_t e = d + (c + step < ml ? c + step : ml);
-            if ((e & ~1023u) > x.flushed + 2048) xflush(x, e & ~1023u);
+            const uint32_t e = d + (c + 64 < ml ? c + 64 : ml);
+            if (e - x.flushed > kFlushLag) xflush(x, e & ~1023u);
         }
     } else {
         // period off: lanes k < L = off * floor(64 / off) hold the pattern
@@ -1226,33 +1292,48 @@ DEV void xbig(XRing& x, const Src& s, uint32_t lip, uint32_t ll, uint32_t ml, ui
         for (uint32_t c = 0; c < ml; c += L) {
             if (l < L && c + l < ml) x.r[(d + c + l) & kXM] = (uint8_t)v;
             const uint32_t e = d + (c + L < ml ? c + L : ml);
-            if ((e & ~1023u) > x.flushed + 2048) xflush(x, e & ~1023u);
+            if (e - x.flushed > kFlushLag) xflush(x, e & ~1023u);
         }
     }
     x.op += ml;
-    if ((x.op & ~1023u) > x.flushed) xflush_chunks(x);
+    if (x.op - x.flushed > kFlushLag) xflush_chunks(x);
 }
 
+DEV SeqRec rec_at(const SeqRec* recs, uint32_t k, uint32_t cnt) {
+    SeqRec r{0, 0, 0, 0};
+    if (k < cnt) r = recs[k];
+    return r;
+}
+DEV uint4 lit_head(const Src& s, const SeqRec& r) {
+    return (r.ll && r.ll <= kBig) ? ld16(s, (int64_t)r.lip) : make_uint4(0, 0, 0, 0);
+}
+
+// records [0, cnt) in windows of 64 (lane k = record 64 w + k): records are
+// loaded two windows ahead and literal heads one window ahead, so the
+// global-load latency hides behind the previous window's LDS work; a record
+// longer than kBig splits its window and runs alone
 DEV void xrecords(XRing& x, const Src& s, const SeqRec* recs, uint32_t cnt) {
     const uint32_t l = lane();
-    for (uint32_t b = 0; b < cnt;) {
-        const uint32_t k = b + l;
-        SeqRec r{0, 0, 0, 0};
-        if (k < cnt) r = recs[k];
-        const bool big = k < cnt && (r.ll > kBig || r.ml > kBig);
-        const uint64_t bb = __ballot(big);
-        uint32_t m = cnt - b < 64 ? cnt - b : 64;
-        if (bb) {
-            const uint32_t fb = (uint32_t)__builtin_ctzll(bb);
-            if (fb < m) m = fb;
+    SeqRec r0 = rec_at(recs, l, cnt), r1 = rec_at(recs, 64 + l, cnt);
+    uint4 lit0 = lit_head(s, r0);
+    for (uint32_t b = 0; b < cnt; b += 64) {
+        const SeqRec r2 = rec_at(recs, b + 128 + l, cnt);
+        const uint4 lit1 = lit_head(s, r1);
+        const uint32_t n = cnt - b < 64 ? cnt - b : 64;
+        const uint64_t bigm = __ballot(l < n && (r0.ll > kBig || r0.ml > kBig));
+        uint32_t lo = 0;
+        for (;;) {
+            const uint64_t bm = bigm & (~0ull << lo);
+            const uint32_t e = bm ? (uint32_t)__builtin_ctzll(bm) : n;
+            if (e > lo) xbatch(x, s, r0, lo, e, lit0);
+            if (!bm) break;
+            xbig(x, s, rl(r0.lip, (int)e), rl(r0.ll, (int)e), rl(r0.ml, (int)e), rl(r0.off, (int)e));
+            lo = e + 1;
+            if (lo >= n) break;
         }
-        if (m == 0) {
-            xbig(x, s, uni32(r.lip), uni32(r.ll), uni32(r.ml), uni32(r.off));
-            b += 1;
-        } else {
-            xbatch(x, s, r, m);
-            b += m;
-        }
+        r0 = r1;
+        r1 = r2;
+        lit0 = lit1;
     }
 }
 
@@ -1276,30 +1357,19 @@ DEV void xcopy_raw(uint8_t* dst, const Src& s, uint32_t len) {
     }
 }
 
-// A lane's piece: its stream, walk state and records
+// A piece's stream and walk state (one lane)
 struct Piece {
     Src s;
     PState ps;
-    uint32_t nrec;
     uint32_t kind, cap;
-    uint64_t dst;
 };
 
-// walk (or continue walking) this lane's piece into its record buffer
-DEV void piece_walk(Piece& pc, SeqRec* buf) {
-    RecSink sink{buf, 0, kRecsPerLane};
-    if (pc.kind & kBlkSnappy) snappy_run(pc.s, pc.ps, sink);
-    else lz4_run(pc.s, (int32_t)pc.cap, 65536, pc.ps, sink);
-    pc.nrec = sink.n;
-}
-
+// a piece's stream, block checksum and walk start (per lane)
 DEV void piece_begin(Piece& pc, const DeviceJob& j, const BlockItem& it) {
     const uint64_t n = it.csize;
     pc.s = Src{j.data + it.src, (int64_t)n, (int64_t)(j.data_len - it.src)};
     pc.kind = it.kind;
     pc.cap = it.cap;
-    pc.dst = it.dst;
-    pc.nrec = 0;
     pc.ps.ip = pc.ps.op = pc.ps.need = 0;
     pc.ps.ulen = 0;
     pc.ps.safe = 0;
@@ -1317,110 +1387,189 @@ DEV void piece_begin(Piece& pc, const DeviceJob& j, const BlockItem& it) {
     else lz4_begin(pc.ps, pc.s, (int32_t)it.cap);
 }
 
-DEV uint64_t rl64(uint64_t v, uint32_t l) { return (uint64_t)rl((uint32_t)v, (int)l) | ((uint64_t)rl((uint32_t)(v >> 32), (int)l) << 32); }
+template <class Sink>
+DEV void piece_run(const Src& s, uint32_t kind, uint32_t cap, PState& ps, Sink& sink) {
+    if (kind & kBlkSnappy) snappy_run(s, ps, sink);
+    else lz4_run(s, (int32_t)cap, 65536, ps, sink);  // H = 64 KiB: the history check is `need` (see lz4_run)
+}
 
-// execute lane jl's piece (walked by piece_walk) at x.op; returns its decoded
-// length or -1.  Resumes the walk (lane jl alone) while records remain.
-DEV int32_t piece_exec(XRing& x, Piece& pc, SeqRec* region, uint32_t jl, uint32_t hist) {
+// records into slabs of the pool; false (suspend) once the pool is exhausted
+struct SlabSink {
+    SeqRec* pool;
+    uint32_t* slab_next;
+    uint32_t* cursor;
+    uint32_t pool_slabs;
+    uint32_t slab, pos, n;
+    DEV bool seq(const uint4&, int32_t, int32_t lip, int32_t llen, int32_t, uint32_t off, int32_t ml) {
+        pool[(size_t)slab * kSlabRecs + pos] = SeqRec{(uint32_t)lip, (uint32_t)llen, (uint32_t)ml, off};
+        n++;
+        if (++pos < kSlabRecs) return true;
+        const uint32_t ns = atomicAdd(cursor, 1u);
+        if (ns >= pool_slabs) return false;
+        slab_next[slab] = ns;
+        slab = ns;
+        pos = 0;
+        return true;
+    }
+};
+
+// ---------------------------------------------------------------------------
+// k_lz_walk: one lane per piece (every planned BlockItem, linked or not),
+// taken off counters[10]: block checksum, then the walk into slab records.
+// High occupancy: the walk is a chain of dependent loads per lane.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_lz_walk(DeviceJob j) {
+    const uint32_t reserved = j.counters[4];
+    const uint32_t nblk = reserved < j.block_capacity ? reserved : j.block_capacity;
+    for (;;) {
+        const uint32_t p = atomicAdd(&j.counters[10], 1u);
+        if (p >= nblk) break;
+        Piece pc;
+        piece_begin(pc, j, j.blocks[p]);
+        PieceState out;
+        out.nrec = 0;
+        out.first_slab = 0xFFFFFFFFu;
+        if (pc.ps.st == 0) {
+            const uint32_t fs = atomicAdd(&j.counters[9], 1u);
+            if (fs < j.pool_slabs) {
+                out.first_slab = fs;
+                SlabSink sink{j.pool, j.slab_next, &j.counters[9], j.pool_slabs, fs, 0, 0};
+                piece_run(pc.s, pc.kind, pc.cap, pc.ps, sink);
+                out.nrec = sink.n;
+            }
+        }
+        out.ip = pc.ps.ip;
+        out.op = pc.ps.op;
+        out.need = pc.ps.need;
+        out.st = pc.ps.st;
+        out.ulen = pc.ps.ulen;
+        out.safe = pc.ps.safe;
+        j.pstate[p] = out;
+    }
+}
+
+// execute piece p at x.op (its walk stored by k_lz_walk); returns its decoded
+// length or -1.  `hist` = output bytes before it that its matches may reach.
+// A walk the pool cut short continues here, on lane 0, kRecsPerLane records
+// at a time through the wave's own buffer.
+DEV int32_t exec_piece(XRing& x, const DeviceJob& j, uint32_t p, uint32_t hist, SeqRec* buf) {
     const uint32_t l = lane();
-    int32_t st = (int32_t)rl((uint32_t)pc.ps.st, (int)jl);
+    const BlockItem& itr = j.blocks[p];
+    const uint64_t src = uni64(itr.src);
+    const uint32_t csize = uni32(itr.csize), kind = uni32(itr.kind), cap = uni32(itr.cap);
+    const PieceState& psr = j.pstate[p];
+    int32_t st = (int32_t)uni32((uint32_t)psr.st);
     if (st < 0) return -1;
-    const uint32_t kind = rl(pc.kind, (int)jl);
-    const Src s{(const uint8_t*)(uintptr_t)rl64((uint64_t)(uintptr_t)pc.s.p, jl), (int64_t)rl64((uint64_t)pc.s.n, jl),
-                (int64_t)rl64((uint64_t)pc.s.rl, jl)};
+    const Src s{j.data + src, (int64_t)csize, (int64_t)(j.data_len - src)};
     if (kind & kBlkRaw) {
-        const uint32_t n = (uint32_t)s.n;
-        if (x.linked) xbig(x, s, 0, n, 0, 0);
-        else xcopy_raw(x.dst + x.op, s, n);
-        return (int32_t)n;
+        if (x.hist) xbig(x, s, 0, csize, 0, 0);
+        else {
+            xcopy_raw(x.dst + x.op, s, csize);
+            x.op += csize;
+            x.flushed = x.op;
+        }
+        return (int32_t)csize;
     }
     const uint32_t start = x.op;
-    const SeqRec* buf = region + (size_t)jl * kRecsPerLane;
-    for (;;) {
-        const uint32_t nrec = rl(pc.nrec, (int)jl);
-        xrecords(x, s, buf, nrec);
-        if (st != 0) break;
-        if (l == jl) piece_walk(pc, region + (size_t)jl * kRecsPerLane);
-        st = (int32_t)rl((uint32_t)pc.ps.st, (int)jl);
+    uint32_t nrec = uni32(psr.nrec), slab = uni32(psr.first_slab);
+    int32_t need = (int32_t)uni32((uint32_t)psr.need);
+    while (nrec) {
+        const uint32_t c = nrec < kSlabRecs ? nrec : kSlabRecs;
+        const uint32_t next = c == kSlabRecs ? uni32(j.slab_next[slab]) : 0u;
+        xrecords(x, s, j.pool + (size_t)slab * kSlabRecs, c);
+        nrec -= c;
+        slab = next;
+    }
+    if (st == 0) {
+        PState ps;
+        ps.ip = (int32_t)uni32((uint32_t)psr.ip);
+        ps.op = (int32_t)uni32((uint32_t)psr.op);
+        ps.need = need;
+        ps.st = 0;
+        ps.ulen = uni32(psr.ulen);
+        ps.safe = uni32(psr.safe);
+        for (;;) {
+            uint32_t n = 0;
+            if (l == 0) {
+                RecSink sink{buf, 0, kRecsPerLane};
+                piece_run(s, kind, cap, ps, sink);
+                n = sink.n;
+            }
+            wait_vm();  // lane 0's records, stored through this CU's L1, are then seen by every lane
+            n = rl(n, 0);
+            st = (int32_t)rl((uint32_t)ps.st, 0);
+            xrecords(x, s, buf, n);
+            if (st != 0) break;
+        }
         if (st < 0) return -1;
+        need = (int32_t)rl((uint32_t)ps.need, 0);
     }
     // history check of the walk (run with H = 64 KiB)
-    const int32_t need = (int32_t)rl((uint32_t)pc.ps.need, (int)jl);
     if (need > (int32_t)hist) return -1;
     return (int32_t)(x.op - start);
 }
 
-// the pieces of one linked LZ4F frame (blocks first .. first + nb - 1, nb <= 64)
-DEV void exec_linked(const DeviceJob& j, lds_u8* ring, SeqRec* region, uint32_t item) {
-    const uint32_t l = lane();
-    const uint32_t first = uni32(j.plans[item].first), nb = uni32(j.plans[item].nb);
-    Piece pc;
-    pc.ps.st = -1;
-    pc.nrec = 0;
-    pc.kind = 0;
-    pc.s = Src{nullptr, 0, 0};
-    if (l < nb) {
-        const BlockItem it = j.blocks[first + l];
-        piece_begin(pc, j, it);
-        piece_walk(pc, region + (size_t)l * kRecsPerLane);
-    }
-    const uint64_t fdst = uni64(j.dcap[j.decode_list[item]]);
-    XRing x;
+DEV void xring_init(XRing& x, const DeviceJob& j, lds_u8* ring, uint64_t dst, bool linked, bool hist) {
     x.r = ring;
-    x.dst = j.decoded + fdst;
+    x.dst = j.decoded + dst;
     x.op = 0;
     x.flushed = 0;
-    x.linked = true;
-    const uint64_t room = j.decoded_capacity - fdst;
+    x.linked = linked;
+    x.hist = hist;
+    const uint64_t room = j.decoded_capacity - dst;
     x.rs = __builtin_amdgcn_make_buffer_rsrc(x.dst, 0, (int)(room < 0x7FFFFFFFull ? room : 0x7FFFFFFFull), kBufFlags);
+}
+
+// the blocks of one linked LZ4F frame, in order, one position space
+DEV void exec_linked(const DeviceJob& j, lds_u8* ring, SeqRec* buf, uint32_t item) {
+    const uint32_t first = uni32(j.plans[item].first), nb = uni32(j.plans[item].nb);
+    const uint64_t fdst = uni64(j.dcap[uni32(j.decode_list[item])]);
+    XRing x;
+    xring_init(x, j, ring, fdst, true, true);
+#ifdef RPGPU_DSTAMPS
+    const uint64_t t1 = wall_clock64();
+#endif
     bool ok = true;
     for (uint32_t k = 0; k < nb; k++) {
         const uint32_t at = x.op;
-        const int32_t dd = ok ? piece_exec(x, pc, region, k, at) : -1;
+        const int32_t dd = ok ? exec_piece(x, j, first + k, at, buf) : -1;
         if (dd < 0) ok = false;
-        if (l == 0) {
+        if (lane() == 0) {
             j.blocks[first + k].dst = fdst + at;
             j.blocks[first + k].out = dd;
         }
     }
     xflush(x, x.op);
+#ifdef RPGPU_DSTAMPS
+    if (lane() == 0) { atomicAdd(&g_dst[10], wall_clock64() - t1); atomicAdd(&g_dst[9], 1ull); }
+#endif
 }
 
-// 64 consecutive block items (independent pieces; linked blocks are skipped)
-DEV void exec_chunk(const DeviceJob& j, lds_u8* ring, SeqRec* region, uint32_t base, uint32_t nblk) {
-    const uint32_t l = lane();
-    const uint32_t it_i = base + l;
-    Piece pc;
-    pc.ps.st = -1;
-    pc.nrec = 0;
-    pc.kind = 0;
-    pc.s = Src{nullptr, 0, 0};
-    bool act = false;
-    if (it_i < nblk) {
-        const BlockItem it = j.blocks[it_i];
-        act = !(it.kind & kBlkLinked);
-        if (act) {
-            piece_begin(pc, j, it);
-            piece_walk(pc, region + (size_t)l * kRecsPerLane);
-        }
-    }
-    uint64_t todo = __ballot(act);
-    while (todo) {
-        const uint32_t jl = (uint32_t)__builtin_ctzll(todo);
-        todo &= todo - 1;
-        const uint64_t dst = rl64(pc.dst, jl);
+// up to 64 consecutive block items (independent pieces; linked ones skipped)
+DEV void exec_chunk(const DeviceJob& j, lds_u8* ring, SeqRec* buf, uint32_t base, uint32_t nblk) {
+    const uint32_t end = base + 64 < nblk ? base + 64 : nblk;
+    for (uint32_t p = base; p < end; p++) {
+        const uint32_t kind = uni32(j.blocks[p].kind);
+        if (kind & kBlkLinked) continue;
+        const uint64_t dst = uni64(j.blocks[p].dst);
         XRing x;
-        x.r = ring;
-        x.dst = j.decoded + dst;
-        x.op = 0;
-        x.flushed = 0;
         // a piece longer than the ring wraps it: wrap-aware like a linked frame
-        x.linked = rl(pc.cap, (int)jl) > kXRing;
-        const uint64_t room = j.decoded_capacity - dst;
-        x.rs = __builtin_amdgcn_make_buffer_rsrc(x.dst, 0, (int)(room < 0x7FFFFFFFull ? room : 0x7FFFFFFFull), kBufFlags);
-        const int32_t dd = piece_exec(x, pc, region, jl, 0);
+        xring_init(x, j, ring, dst, uni32(j.blocks[p].cap) > kXRing, false);
+#ifdef RPGPU_DSTAMPS
+        const uint64_t e0 = wall_clock64();
+#endif
+        const int32_t dd = exec_piece(x, j, p, 0, buf);
         if (dd >= 0) xflush(x, x.op);
-        if (l == 0) j.blocks[base + jl].out = dd;
+        if (lane() == 0) j.blocks[p].out = dd;
+#ifdef RPGPU_DSTAMPS
+        if (lane() == 0) {
+            const int k = (kind & kBlkRaw) ? 4 : (kind & kBlkSnappy) ? 6 : 2;
+            atomicAdd(&g_dst[k], wall_clock64() - e0);
+            atomicAdd(&g_dst[k + 1], 1ull);
+            atomicAdd(&g_dst[11], (unsigned long long)j.pstate[p].nrec);
+            if (j.pstate[p].st == 0) atomicAdd(&g_dst[12], 1ull);
+        }
+#endif
     }
 }
 
@@ -1432,7 +1581,7 @@ DEV void exec_chunk(const DeviceJob& j, lds_u8* ring, SeqRec* region, uint32_t b
 __global__ __launch_bounds__(64) void k_lz_exec(DeviceJob j) {
     extern __shared__ __attribute__((aligned(16))) uint8_t xlds[];
     lds_u8* ring = (lds_u8*)xlds;
-    SeqRec* region = j.seqs + (size_t)blockIdx.x * 64 * kRecsPerLane;
+    SeqRec* buf = j.seqs + (size_t)blockIdx.x * 64 * kRecsPerLane;
     const uint32_t nlink = j.counters[7];
     const uint32_t reserved = j.counters[4];
     const uint32_t nblk = reserved < j.block_capacity ? reserved : j.block_capacity;
@@ -1440,8 +1589,8 @@ __global__ __launch_bounds__(64) void k_lz_exec(DeviceJob j) {
     for (;;) {
         const uint32_t u = wave_fetch_add(&j.counters[8], 1u);
         if (u >= total) break;
-        if (u < nlink) exec_linked(j, ring, region, uni32(j.link_list[u]));
-        else exec_chunk(j, ring, region, (u - nlink) * 64, nblk);
+        if (u < nlink) exec_linked(j, ring, buf, uni32(j.link_list[u]));
+        else exec_chunk(j, ring, buf, (u - nlink) * 64, nblk);
     }
 }
 
@@ -1530,18 +1679,16 @@ __global__ __launch_bounds__(64) void k_uncompress_one(int codec, const uint8_t*
 
 #ifdef RPGPU_DSTAMPS
 __global__ void k_print_dstamps() {
-    const char* kn[5] = {"lz4 frames", "snappy streams", "lz4 blocks", "raw blocks", "snappy chunks"};
-    const unsigned long long t0 = g_dst[63];
-    for (int k = 0; k < 5; k++) {
-        const unsigned long long* g = &g_dst[8 * k];
-        if (!g[0]) continue;
-        printf("RPGPU_DSTAMPS %s: n=%llu avg_us=%.1f max_us=%.1f first_start_us=%.1f last_end_us=%.1f in=%llu out=%llu max_in=%llu\n",
-               kn[k], g[0], g[1] / 100.0 / g[0], g[2] / 100.0, (g[7] - t0) / 100.0, (g[3] - t0) / 100.0, g[4], g[5], g[6]);
-    }
-    for (int i = 0; i < 64; i++) g_dst[i] = (i % 8 == 7 || i == 63) ? ~0ull : 0ull;
+    const unsigned long long* g = g_dst;
+    printf("RPGPU_DSTAMPS lz4 pieces=%llu exec_ms=%.1f | raw=%llu exec_ms=%.1f | snappy=%llu exec_ms=%.1f | "
+           "linked=%llu exec_ms=%.1f | records=%llu pool-cut=%llu (wave-summed ms)\n",
+           g[3], g[2] / 1e5, g[5], g[4] / 1e5, g[7], g[6] / 1e5, g[9], g[10] / 1e5, g[11], g[12]);
+    printf("RPGPU_DSTAMPS batches=%llu rounds=%llu | per batch clk: scan=%.0f lit=%.0f rounds=%.0f flush=%.0f\n", g[20], g[21],
+           (double)g[16] / g[20], (double)g[17] / g[20], (double)g[18] / g[20], (double)g[19] / g[20]);
+    for (int i = 0; i < 64; i++) g_dst[i] = 0;
 }
 __global__ void k_init_dstamps() {
-    for (int i = 0; i < 64; i++) g_dst[i] = (i % 8 == 7 || i == 63) ? ~0ull : 0ull;
+    for (int i = 0; i < 64; i++) g_dst[i] = 0;
 }
 #endif
 
@@ -1551,13 +1698,12 @@ hipError_t launch_decode(const DeviceJob& j, hipStream_t s, uint32_t grid) {
 }
 
 hipError_t launch_decode_blocks(const DeviceJob& j, hipStream_t s, uint32_t grid) {
-#ifdef RPGPU_DSTAMPS
-    hipLaunchKernelGGL(k_init_dstamps, dim3(1), dim3(1), 0, s);
-#endif
     hipLaunchKernelGGL(k_decode_blocks, dim3(grid), dim3(256), 0, s, j);
-#ifdef RPGPU_DSTAMPS
-    hipLaunchKernelGGL(k_print_dstamps, dim3(1), dim3(1), 0, s);
-#endif
+    return hipGetLastError();
+}
+
+hipError_t launch_lz_walk(const DeviceJob& j, hipStream_t s, uint32_t grid) {
+    hipLaunchKernelGGL(k_lz_walk, dim3(grid), dim3(256), 0, s, j);
     return hipGetLastError();
 }
 
@@ -1568,7 +1714,13 @@ hipError_t launch_lz_exec(const DeviceJob& j, hipStream_t s) {
         attr = true;
     }
     if (!j.exec_waves) return hipSuccess;
+#ifdef RPGPU_DSTAMPS
+    hipLaunchKernelGGL(k_init_dstamps, dim3(1), dim3(1), 0, s);
+#endif
     hipLaunchKernelGGL(k_lz_exec, dim3(j.exec_waves), dim3(64), kXRing, s, j);
+#ifdef RPGPU_DSTAMPS
+    hipLaunchKernelGGL(k_print_dstamps, dim3(1), dim3(1), 0, s);
+#endif
     return hipGetLastError();
 }
 

@@ -89,8 +89,23 @@ constexpr uint32_t kBlkRaw = 1, kBlkChecksum = 2, kBlkSnappy = 4, kBlkLinked = 8
 struct SeqRec {
     uint32_t lip, ll, ml, off;
 };
-constexpr uint32_t kRecsPerLane = 4096;   // parse-phase records per lane before the wave executes them
-constexpr uint32_t kExecWgsPerCu = 2;     // k_lz_exec: one wave per workgroup, 64 KiB LDS ring each
+// k_lz_walk stores each piece's records in slabs of kSlabRecs taken from
+// one pool (bump counter); slab_next chains a piece's slabs
+constexpr uint32_t kSlabRecs = 512;
+#ifndef RPGPU_XRING_KIB
+#define RPGPU_XRING_KIB 64
+#endif
+constexpr uint32_t kXRingKiB = RPGPU_XRING_KIB;       // k_lz_exec LDS ring per wave
+constexpr uint32_t kExecWgsPerCu = 160 / kXRingKiB;   // one wave per workgroup
+constexpr uint32_t kRecsPerLane = 256;                // k_lz_exec's own walk (pool exhausted): records per pass
+
+// A piece's walk result (k_lz_walk -> k_lz_exec)
+struct PieceState {
+    int32_t ip, op, need, st;   // the walk's PState (st: 1 done, -1 rejected, 0 suspended: pool exhausted)
+    uint32_t ulen, safe;
+    uint32_t nrec;              // records stored
+    uint32_t first_slab;        // 0xFFFFFFFF: none
+};
 
 // Per decode item: how its payload is being decoded
 struct FramePlan {
@@ -131,12 +146,17 @@ struct DeviceJob {
     const Tables* tables;
     uint32_t* counters;           // [0] rewalks, [1] overflow bits, [2] decode items, [3] unused,
                                   // [4] block items reserved, [5] sequential-frame claim cursor,
-                                  // [6] sequential frames, [7] linked frames, [8] k_lz_exec claim cursor
+                                  // [6] sequential frames, [7] linked frames, [8] k_lz_exec claim cursor,
+                                  // [9] slab pool cursor, [10] k_lz_walk claim cursor
     uint32_t* decode_list;        // batch_capacity: ordinals of batches to uncompress
     uint32_t* seq_list;           // batch_capacity: decode items decoded whole by one lane
     uint32_t* link_list;          // batch_capacity: decode items whose linked LZ4F blocks one wave decodes in order
-    SeqRec* seqs;                 // k_lz_exec parse records: kRecsPerLane per lane of each resident wave
+    SeqRec* seqs;                 // k_lz_exec's own walks: kRecsPerLane per lane of each resident wave
     uint32_t exec_waves;          // k_lz_exec grid (one wave per workgroup; sizes `seqs`)
+    PieceState* pstate;           // block_capacity: walk results
+    SeqRec* pool;                 // record slabs
+    uint32_t* slab_next;          // pool_slabs: next slab of the same piece
+    uint32_t pool_slabs;
     BlockItem* blocks;            // block work list ([4] items reserved, [5] claim cursor)
     uint32_t block_capacity;
     FramePlan* plans;             // one per decode item
@@ -152,6 +172,7 @@ hipError_t launch_validate(const DeviceJob& j, hipStream_t s, uint32_t grid);  /
 hipError_t launch_walk(const DeviceJob& j, hipStream_t s, uint32_t grid);
 hipError_t launch_decode(const DeviceJob& j, hipStream_t s, uint32_t grid);    // rp_codec.hip
 hipError_t launch_decode_blocks(const DeviceJob& j, hipStream_t s, uint32_t grid);
+hipError_t launch_lz_walk(const DeviceJob& j, hipStream_t s, uint32_t grid);
 hipError_t launch_lz_exec(const DeviceJob& j, hipStream_t s);
 hipError_t launch_decode_finish(const DeviceJob& j, hipStream_t s, uint32_t grid);
 // one payload, one wave (rpgpu_uncompress); res[0] = rc (0 / -1 / -2), res[1] = out_len

@@ -111,6 +111,9 @@ struct rpgpu_ctx {
     // allocated on the first decode job
     SeqRec* seqs = nullptr;
     uint32_t exec_waves = 0;
+    // k_lz_walk record pool (slabs) and its chain links, grow-only
+    void* pool = nullptr;
+    size_t pool_bytes = 0;
     std::string err;
     // rpgpu_validate_host: a copy stream and two staging slots (segment
     // bytes in, per-batch results out), used alternately so the H2D copy of
@@ -197,6 +200,7 @@ int rpgpu_destroy(rpgpu_ctx* c) {
     if (c->uws) hipFree(c->uws);
     if (c->iws) hipFree(c->iws);
     if (c->seqs) hipFree(c->seqs);
+    if (c->pool) hipFree(c->pool);
     if (c->pin) hipHostFree(c->pin);
     if (c->d_tables) hipFree(c->d_tables);
     for (auto& set : c->ev_sets)
@@ -350,6 +354,7 @@ int rpgpu_submit(rpgpu_ctx* c, const rpgpu_job* job, void* stream) {
     const uint64_t bl_cap64 = dec ? std::min<uint64_t>(data_len / 16384 + 2 * bcap + 64, 0x7FFFFFFFull) : 0;
     const size_t o_blocks = take(bl_cap64 * sizeof(BlockItem));
     const size_t o_plans = take(dec ? (bcap + 1) * sizeof(FramePlan) : 0);
+    const size_t o_pstate = take(bl_cap64 * sizeof(PieceState));
     const size_t o_scan = take(scan_temp_bytes(std::max<uint64_t>(tc, bcap)) + 64);
     const size_t need = off;
     if (dec && !c->seqs) {
@@ -359,6 +364,17 @@ int rpgpu_submit(rpgpu_ctx* c, const rpgpu_job* job, void* stream) {
             return fail(c, RPGPU_E_NOMEM, "decode sequence workspace");
         }
         c->exec_waves = waves;
+    }
+    // record pool: a compressed LZ4 byte yields at most 1/3 record (16 B),
+    // typical data far fewer (C2: 0.33 B of records per stored byte); sized
+    // from the job's bytes, clamped; pieces that do not fit are walked by
+    // k_lz_exec itself
+    const size_t slab_bytes = kSlabRecs * sizeof(SeqRec) + 4;
+    const size_t pool_want = dec ? std::min<size_t>(std::max<size_t>(data_len / 2, 256ull << 20), 8ull << 30) : 0;
+    if (pool_want > c->pool_bytes) {
+        if (c->pool) { hipStreamSynchronize(s); hipFree(c->pool); c->pool = nullptr; c->pool_bytes = 0; }
+        if (hipMalloc(&c->pool, pool_want) != hipSuccess) { c->pool = nullptr; return fail(c, RPGPU_E_NOMEM, "decode record pool"); }
+        c->pool_bytes = pool_want;
     }
     if (need > c->ws_bytes) {
         if (c->ws) { hipStreamSynchronize(s); hipFree(c->ws); c->ws = nullptr; }
@@ -399,6 +415,13 @@ int rpgpu_submit(rpgpu_ctx* c, const rpgpu_job* job, void* stream) {
     j.link_list = (uint32_t*)(ws + o_llist);
     j.seqs = c->seqs;
     j.exec_waves = c->exec_waves;
+    j.pstate = (PieceState*)(ws + o_pstate);
+    j.pool_slabs = (uint32_t)std::min<size_t>(c->pool_bytes / slab_bytes, 0xFFFFFFF0ull);
+    // RPGPU_POOL_SLABS: test override shrinking the record pool (exercises
+    // k_lz_exec's own walk of the pieces the pool cuts short)
+    if (const char* e = getenv("RPGPU_POOL_SLABS")) j.pool_slabs = std::min<uint32_t>(j.pool_slabs, (uint32_t)atoi(e));
+    j.pool = (SeqRec*)c->pool;
+    j.slab_next = (uint32_t*)((uint8_t*)c->pool + (size_t)j.pool_slabs * kSlabRecs * sizeof(SeqRec));
     j.seg_first_bad = (uint32_t*)(ws + o_fbad);
     j.blocks = (BlockItem*)(ws + o_blocks);
     j.block_capacity = (uint32_t)bl_cap64;
@@ -446,6 +469,7 @@ int rpgpu_submit(rpgpu_ctx* c, const rpgpu_job* job, void* stream) {
     if ((job->flags & RPGPU_JOB_DECODE) && j.decoded) {
         STAGE("decode", launch_decode(j, s, c->cu_count * 8));
         STAGE("decode_blocks", launch_decode_blocks(j, s, c->cu_count * 8));
+        STAGE("lz_walk", launch_lz_walk(j, s, c->cu_count * 16));
         STAGE("lz_exec", launch_lz_exec(j, s));
         STAGE("decode_finish", launch_decode_finish(j, s, c->cu_count * 8));
     }
