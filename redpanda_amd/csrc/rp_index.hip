@@ -274,12 +274,18 @@ struct IdxCand {
     uint32_t valid;
 };
 
+// Pieces are laid out densely: segment s owns global pieces
+// [pbase[s], pbase[s + 1]), ceil(tracked / 1024) of them, so the workspace and
+// the grids grow with the batch capacity plus the segment count (at most
+// cap / 1024 + nseg pieces), not with their product.
 struct IdxWs {
     uint64_t* cut;      // [nseg]
-    uint64_t* a_in;     // [nseg * max_pieces]
-    uint64_t* base;     // [nseg * max_pieces]
-    IdxCand* cand;      // [nseg * max_pieces * kIdxCand]
-    uint32_t max_pieces;
+    uint64_t* pbase;    // [nseg + 1]: exclusive scan of the pieces per segment
+    uint64_t* a_in;     // [max_pieces]
+    uint64_t* base;     // [max_pieces]
+    IdxCand* cand;      // [max_pieces * kIdxCand]
+    uint32_t n_segments;
+    uint32_t max_pieces;  // bound on the total (grid size)
 };
 
 DEV uint64_t idx_tracked(const rpgpu_segment_summary& sm, uint64_t cap, int64_t& assert_batch) {
@@ -307,17 +313,69 @@ DEV void idx_walk_range(const rpgpu_batch_result* seg, uint64_t from, uint64_t e
     }
 }
 
-// grid (max_pieces, nseg): the first batch below the index base offset (the
+// one workgroup: pieces per segment (from the tracked count, which bounds
+// every later cut) and their exclusive scan, clamped to the workspace bound
+__global__ __launch_bounds__(1024) void k_idx_layout(const rpgpu_segment_summary* __restrict__ sums, uint64_t cap,
+                                                     IdxWs ws) {
+    __shared__ uint64_t part[1024 / 64];
+    __shared__ uint64_t carry;
+    const uint32_t t = threadIdx.x, l = t & 63, wv = t >> 6;
+    if (t == 0) carry = 0;
+    __syncthreads();
+    for (uint32_t b = 0; b < ws.n_segments; b += 1024) {
+        const uint32_t s = b + t;
+        uint64_t np = 0;
+        if (s < ws.n_segments) {
+            int64_t ab;
+            np = (idx_tracked(sums[s], cap, ab) + kIdxPiece - 1) / kIdxPiece;
+        }
+        uint64_t P = np;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint64_t o = shfl_up64(P, d);
+            if (l >= (uint32_t)d) P += o;
+        }
+        if (l == 63) part[wv] = P;
+        __syncthreads();
+        uint64_t before = carry;
+        for (uint32_t k = 0; k < wv; k++) before += part[k];
+        const uint64_t lim = ws.max_pieces;
+        const uint64_t e0 = before + P - np, e1 = before + P;
+        if (s < ws.n_segments) ws.pbase[s] = e0 < lim ? e0 : lim;
+        if (s + 1 == ws.n_segments) ws.pbase[s + 1] = e1 < lim ? e1 : lim;
+        __syncthreads();
+        if (t == 1023) carry = before + P;
+        __syncthreads();
+    }
+}
+
+// global piece g -> (segment, piece within it); false past the last piece
+DEV bool idx_piece(const IdxWs& ws, uint64_t g, uint32_t& s, uint64_t& p) {
+    if (g >= ws.pbase[ws.n_segments]) return false;
+    uint32_t lo = 0, hi = ws.n_segments;  // last s with pbase[s] <= g
+    while (hi - lo > 1) {
+        const uint32_t m = (lo + hi) >> 1;
+        if (ws.pbase[m] <= g) lo = m;
+        else hi = m;
+    }
+    s = lo;
+    p = g - ws.pbase[lo];
+    return true;
+}
+
+// grid (max_pieces): the first batch below the index base offset (the
 // reference's vassert) per segment, by atomicMin over pieces; ws.cut starts
 // at ~0 and every reader takes min(ws.cut, tracked)
 __global__ __launch_bounds__(256) void k_idx_cut(const rpgpu_batch_result* __restrict__ batches, uint64_t cap,
                                                  const rpgpu_segment_summary* __restrict__ sums,
                                                  const rpgpu_index_state* __restrict__ states, IdxWs ws) {
-    const uint32_t p = blockIdx.x, s = blockIdx.y;
+    uint32_t s;
+    uint64_t p;
+    if (!idx_piece(ws, blockIdx.x, s, p)) return;
     const rpgpu_segment_summary sm = sums[s];
     int64_t assert_batch;
     const uint64_t n = idx_tracked(sm, cap, assert_batch);
-    const uint64_t from = (uint64_t)p * kIdxPiece;
+    const uint64_t from = p * kIdxPiece;
     if (from >= n) return;
     const uint64_t end = from + kIdxPiece < n ? from + kIdxPiece : n;
     const rpgpu_batch_result* seg = batches + sm.first_batch;
@@ -345,15 +403,17 @@ DEV uint64_t idx_cut(const IdxWs& ws, uint32_t s, const rpgpu_segment_summary& s
     return c < n ? c : n;
 }
 
-// grid (max_pieces, nseg), 4 waves per block: wave v takes candidates v, v+4, ...
+// grid (max_pieces), 4 waves per block: wave v takes candidates v, v+4, ...
 __global__ __launch_bounds__(256) void k_idx_cand(const rpgpu_batch_result* __restrict__ batches, uint64_t cap,
                                                   const rpgpu_segment_summary* __restrict__ sums, uint64_t step,
                                                   const rpgpu_index_state* __restrict__ states, IdxWs ws) {
-    const uint32_t p = blockIdx.x, s = blockIdx.y;
+    uint32_t s;
+    uint64_t p;
+    if (!idx_piece(ws, blockIdx.x, s, p)) return;
     const uint32_t l = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const rpgpu_segment_summary sm = sums[s];
     const uint64_t cut = idx_cut(ws, s, sm, cap);
-    const uint64_t from = (uint64_t)p * kIdxPiece;
+    const uint64_t from = p * kIdxPiece;
     if (from >= cut || p == 0) return;  // piece 0 starts with the forced first entry: no candidates needed
     const uint64_t end = from + kIdxPiece < cut ? from + kIdxPiece : cut;
     const rpgpu_batch_result* seg = batches + sm.first_batch;
@@ -369,7 +429,7 @@ __global__ __launch_bounds__(256) void k_idx_cand(const rpgpu_batch_result* __re
         if (l >= (uint32_t)d) P += o;
     }
     const uint64_t cmask = __ballot(i0 < end && (P - sz) < step);
-    IdxCand* out = ws.cand + ((uint64_t)s * ws.max_pieces + p) * kIdxCand;
+    IdxCand* out = ws.cand + (ws.pbase[s] + p) * kIdxCand;
     for (uint32_t k = wv; k < kIdxCand; k += 4) {
         if (!((cmask >> k) & 1)) {
             if (l == 0) out[k].valid = 0;
@@ -414,8 +474,10 @@ __global__ __launch_bounds__(64) void k_idx_resolve(const rpgpu_batch_result* __
     }
     if (cut == 0) return;
     const uint64_t lt_mask = (1ull << l) - 1;
-    const uint64_t np = (cut + kIdxPiece - 1) / kIdxPiece;
-    const IdxCand* row0 = ws.cand + (uint64_t)s * ws.max_pieces * kIdxCand;
+    const uint64_t pb = ws.pbase[s];
+    uint64_t np = (cut + kIdxPiece - 1) / kIdxPiece;
+    if (np > ws.pbase[s + 1] - pb) np = ws.pbase[s + 1] - pb;  // the layout's clamp (never taken for real jobs)
+    const IdxCand* row0 = ws.cand + pb * kIdxCand;
     auto load_size = [&](uint64_t p) {
         const uint64_t i = p * kIdxPiece + l;
         return (int64_t)seg[i < cut ? i : cut - 1].size_bytes;
@@ -439,8 +501,8 @@ __global__ __launch_bounds__(64) void k_idx_resolve(const rpgpu_batch_result* __
             const uint64_t from = p * kIdxPiece;
             const uint64_t end = from + kIdxPiece < cut ? from + kIdxPiece : cut;
             if (l == 0) {
-                ws.a_in[(uint64_t)s * ws.max_pieces + p] = a;
-                ws.base[(uint64_t)s * ws.max_pieces + p] = entries;
+                ws.a_in[pb + p] = a;
+                ws.base[pb + p] = entries;
             }
             bool done = false;
             if (p > 0) {
@@ -472,24 +534,27 @@ __global__ __launch_bounds__(64) void k_idx_resolve(const rpgpu_batch_result* __
     if (l == 0) states[s].n_entries = entries;
 }
 
-// grid (max_pieces, nseg): one wave per piece writes its entries
+// grid (max_pieces): one wave per piece writes its entries
 __global__ __launch_bounds__(64) void k_idx_emit(const rpgpu_batch_result* __restrict__ batches, uint64_t cap,
                                                  const rpgpu_segment_summary* __restrict__ sums, uint64_t step,
                                                  rpgpu_index_state* __restrict__ states, IdxWs ws,
                                                  uint32_t* __restrict__ rel_offset, uint32_t* __restrict__ rel_time,
                                                  uint64_t* __restrict__ position) {
-    const uint32_t p = blockIdx.x, s = blockIdx.y, l = threadIdx.x;
+    uint32_t s;
+    uint64_t p;
+    if (!idx_piece(ws, blockIdx.x, s, p)) return;
+    const uint32_t l = threadIdx.x;
     const rpgpu_segment_summary sm = sums[s];
     const uint64_t cut = idx_cut(ws, s, sm, cap);
-    const uint64_t from = (uint64_t)p * kIdxPiece;
+    const uint64_t from = p * kIdxPiece;
     if (from >= cut) return;
     const uint64_t end = from + kIdxPiece < cut ? from + kIdxPiece : cut;
     const rpgpu_batch_result* seg = batches + sm.first_batch;
     const int64_t idx_base = states[s].base_offset;
     const uint64_t lt_mask = (1ull << l) - 1;
     IdxWalk w;
-    w.a = ws.a_in[(uint64_t)s * ws.max_pieces + p];
-    w.n_entries = ws.base[(uint64_t)s * ws.max_pieces + p];
+    w.a = ws.a_in[ws.pbase[s] + p];
+    w.n_entries = ws.base[ws.pbase[s] + p];
     w.tracked = 0;
     w.base_ts = seg[0].first_timestamp;
     w.max_off = 0;
@@ -508,36 +573,44 @@ __global__ __launch_bounds__(64) void k_idx_emit(const rpgpu_batch_result* __res
     if (l == 0) atomicMax((long long*)&states[s].max_timestamp, (long long)m);
 }
 
+// pieces: sum over segments of ceil(tracked / 1024) <= cap / 1024 + nseg
+// (the segments' tracked batches are disjoint ranges of the batch results)
+static uint64_t idx_max_pieces(uint32_t n_segments, uint64_t cap) { return cap / kIdxPiece + n_segments + 1; }
+
 size_t segment_index_ws_bytes(uint32_t n_segments, uint64_t cap) {
-    const uint64_t mp = (cap + kIdxPiece - 1) / kIdxPiece + 1;
-    return 256 + (uint64_t)n_segments * 8 + 2 * (uint64_t)n_segments * mp * 8 +
-           (uint64_t)n_segments * mp * kIdxCand * sizeof(IdxCand) + 1024;
+    const uint64_t mp = idx_max_pieces(n_segments, cap);
+    return 256 + ((uint64_t)n_segments * 8 + 256) + ((uint64_t)n_segments * 8 + 8 + 256) + 2 * (mp * 8 + 256) +
+           mp * kIdxCand * sizeof(IdxCand) + 1024;
 }
 
 hipError_t launch_segment_index_pieces(const rpgpu_batch_result* batches, uint64_t cap,
                                        const rpgpu_segment_summary* sums, uint32_t n_segments, uint64_t step,
                                        rpgpu_index_state* states, uint32_t* rel_offset, uint32_t* rel_time,
                                        uint64_t* position, void* wsp, hipStream_t s) {
-    const uint64_t mp = (cap + kIdxPiece - 1) / kIdxPiece + 1;
-    if (mp > 0xFFFFFFull) return hipErrorInvalidValue;
+    const uint64_t mp = idx_max_pieces(n_segments, cap);
+    if (mp > 0x7FFFFFFFull) return hipErrorInvalidValue;
     uint8_t* q = (uint8_t*)(((uintptr_t)wsp + 255) & ~(uintptr_t)255);
     IdxWs ws;
+    ws.n_segments = n_segments;
     ws.max_pieces = (uint32_t)mp;
     ws.cut = (uint64_t*)q;
     q += ((uint64_t)n_segments * 8 + 255) & ~255ull;
+    ws.pbase = (uint64_t*)q;
+    q += ((uint64_t)n_segments * 8 + 8 + 255) & ~255ull;
     ws.a_in = (uint64_t*)q;
-    q += ((uint64_t)n_segments * mp * 8 + 255) & ~255ull;
+    q += (mp * 8 + 255) & ~255ull;
     ws.base = (uint64_t*)q;
-    q += ((uint64_t)n_segments * mp * 8 + 255) & ~255ull;
+    q += (mp * 8 + 255) & ~255ull;
     ws.cand = (IdxCand*)q;
     hipError_t e = hipMemsetAsync(ws.cut, 0xFF, (size_t)n_segments * 8, s);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_idx_cut, dim3((uint32_t)mp, n_segments), dim3(256), 0, s, batches, cap, sums,
+    hipLaunchKernelGGL(k_idx_layout, dim3(1), dim3(1024), 0, s, sums, cap, ws);
+    hipLaunchKernelGGL(k_idx_cut, dim3((uint32_t)mp), dim3(256), 0, s, batches, cap, sums,
                        (const rpgpu_index_state*)states, ws);
-    hipLaunchKernelGGL(k_idx_cand, dim3((uint32_t)mp, n_segments), dim3(256), 0, s, batches, cap, sums, step,
+    hipLaunchKernelGGL(k_idx_cand, dim3((uint32_t)mp), dim3(256), 0, s, batches, cap, sums, step,
                        (const rpgpu_index_state*)states, ws);
     hipLaunchKernelGGL(k_idx_resolve, dim3(n_segments), dim3(64), 0, s, batches, cap, sums, step, states, ws);
-    hipLaunchKernelGGL(k_idx_emit, dim3((uint32_t)mp, n_segments), dim3(64), 0, s, batches, cap, sums, step, states, ws,
+    hipLaunchKernelGGL(k_idx_emit, dim3((uint32_t)mp), dim3(64), 0, s, batches, cap, sums, step, states, ws,
                        rel_offset, rel_time, position);
     return hipGetLastError();
 }

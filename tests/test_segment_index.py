@@ -218,6 +218,32 @@ def test_gpu_many_pieces(engine, oracle, kind):
 
 
 @pytest.mark.gpu
+def test_gpu_many_segments(engine, oracle):
+    """Thousands of small segments (recovery of a long log): pieces are laid
+    out densely (workspace ~ capacity / 1024 + segments, not their product),
+    and the layout's scan crosses several 1024-segment rounds."""
+    rng = np.random.default_rng(77)
+    nseg = 3000
+    counts = rng.integers(0, 40, nseg)
+    counts[5] = 2500  # one segment of three pieces among them
+    n = int(counts.sum())
+    sizes = np.exp(rng.uniform(np.log(61), np.log(1 << 17), n)).astype(np.int64)
+    offs = np.cumsum(rng.integers(1, 5, n))
+    ts = 1_600_000_000_000 + np.cumsum(rng.integers(-5, 1000, n))
+    segs, first = [], 0
+    for c in counts:
+        c = int(c)
+        segs.append((first, c, int(rng.integers(0, c + 1)) if c and rng.random() < 0.3 else c))
+        first += c
+    b, sm = make_results(sizes, offs, first_ts=ts, max_ts=ts + 3, lod=rng.integers(0, 3, n), segs=segs)
+    bases = [int(offs[f]) if c else 0 for f, c, _ in segs]
+    ref = oracle.segment_index(b, sm, bases)
+    out = _device_result(engine, b, sm)
+    got = engine.index_to_host(*engine.segment_index(out, bases), n_segments=nseg)
+    assert_index_same(got, ref)
+
+
+@pytest.mark.gpu
 def test_gpu_reference_vectors(engine, oracle):
     """offset_index_utils_tests.cc:71-98 and :51-69 through the device kernel."""
     offs = [824, 849, 879, 901, 926, 948] + list(range(2000, 3024))
