@@ -65,6 +65,8 @@ enum rpgpu_status {
     RPGPU_E_UNSUPPORTED = -6,  /* codec not decoded by this engine (gzip/zstd) */
     RPGPU_E_HIP = -7,          /* kernel launch / runtime error */
 };
+/* rpgpu_poll: the job is still running (a positive, non-error status). */
+#define RPGPU_PENDING 1
 
 /* ------------------------------------------------------------------------ */
 /* Per-batch verdict flags (rpgpu_batch_result.flags).  Each bit is pinned    */
@@ -269,6 +271,32 @@ typedef struct rpgpu_job {
  * bounds. */
 int rpgpu_submit(rpgpu_ctx* ctx, const rpgpu_job* job, void* stream);
 
+/* Asynchronous completion for a reactor that must not block (SURVEY.md
+ * §8(b) segment-engine row; storage::continuous_batch_parser::consume
+ * returns a future, storage/parser.h:94-136): the same pipeline as
+ * rpgpu_submit, plus a completion event on the launch stream.
+ * rpgpu_poll is non-blocking: RPGPU_OK once every output is written,
+ * RPGPU_PENDING while the job runs, < 0 on a device error.  rpgpu_wait
+ * blocks until then.  rpgpu_release frees the handle (after completion or
+ * not: the job itself is not cancelled). */
+typedef struct rpgpu_pending rpgpu_pending;
+int rpgpu_submit_async(rpgpu_ctx* ctx, const rpgpu_job* job, void* stream, rpgpu_pending** out);
+int rpgpu_poll(rpgpu_pending* p);
+int rpgpu_wait(rpgpu_pending* p);
+int rpgpu_release(rpgpu_pending* p);
+
+/* Output sizes a job needs, before it runs (the segment-engine row's "sized
+ * by a query call").  Reads only d_data, d_seg_offsets, h_seg_offsets,
+ * n_segments, layout, flags and chunk_bytes of `job`; the chain is
+ * discovered and planned into context scratch.  Synchronous on `stream`. */
+typedef struct rpgpu_capacity {
+    uint64_t n_batches;          /* batch_capacity needed */
+    uint64_t record_capacity;    /* record index slots needed (RPGPU_JOB_PARSE) */
+    uint64_t decoded_capacity;   /* decoded arena bytes needed (RPGPU_JOB_DECODE; 0 otherwise) */
+    uint64_t reserved;
+} rpgpu_capacity;
+int rpgpu_query_capacity(rpgpu_ctx* ctx, const rpgpu_job* job, void* stream, rpgpu_capacity* out);
+
 /* Device time of the pipeline stages, measured with HIP events recorded on
  * the launch stream, averaged over every timed rpgpu_submit since the
  * previous call (milliseconds; the call resets the average).  Indices:
@@ -320,12 +348,24 @@ int rpgpu_segment_index(rpgpu_ctx* ctx, const rpgpu_batch_result* d_batches, uin
 /* compression::compressor::uncompress (compression/compression.h:21-24)     */
 /* ------------------------------------------------------------------------ */
 
-/* Decode one payload (host pointers) on the device.  *out_len receives the
- * decoded size; returns RPGPU_E_CODEC where the reference throws
- * std::runtime_error, RPGPU_E_OVERFLOW if cap is too small (out_len then
- * holds the size needed when known). */
+/* Decode one payload (host pointers).  LZ4 and snappy run on the device;
+ * gzip and zstd run on the host, the reference's own loops over zlib /
+ * libzstd (gzip_compressor.cc:161-230, stream_zstd.cc:152-178: the CPU
+ * fallback of SURVEY.md §8(b)).  *out_len receives the decoded size;
+ * returns RPGPU_E_CODEC where the reference throws std::runtime_error,
+ * RPGPU_E_OVERFLOW if cap is too small (out_len then holds the size needed),
+ * RPGPU_E_UNSUPPORTED when zlib / libzstd cannot be loaded.  ctx may be
+ * NULL for gzip / zstd (no device work). */
 int rpgpu_uncompress(rpgpu_ctx* ctx, int codec, const void* in, size_t n,
                      void* out, size_t cap, size_t* out_len);
+
+/* n payloads in one device round trip (the per-batch call sites
+ * storage/parser_utils.cc:51 and kafka/protocol/kafka_batch_adapter.cc:259,
+ * batched).  Arrays of n entries; status[i] is what rpgpu_uncompress would
+ * return for payload i.  Returns RPGPU_OK when every payload has a status. */
+int rpgpu_uncompress_batch(rpgpu_ctx* ctx, uint32_t n, const int* codecs, const void* const* in,
+                           const size_t* in_len, void* const* out, const size_t* cap, size_t* out_len,
+                           int* status);
 
 /* ------------------------------------------------------------------------ */
 /* Host segment path: pinned, double-buffered H2D of host-resident segments  */

@@ -309,8 +309,9 @@ inline int32_t crc_record_batch(const record_batch_header& h, const rpgpu::iobuf
 
 // ---------------------------------------------------------------------------
 // compression::compressor::uncompress — compression/compression.h:21-24
-// (lz4 and snappy decoded on the GPU; throws std::runtime_error where the
-// reference throws; gzip/zstd are not decoded by this engine)
+// (lz4 and snappy decoded on the GPU, gzip and zstd by the reference's loops
+// over zlib / libzstd on the host; throws std::runtime_error where the
+// reference throws, std::logic_error only when zlib / libzstd is absent)
 // ---------------------------------------------------------------------------
 namespace compression {
 using type = model::compression;

@@ -34,6 +34,12 @@ class JobC(C.Structure):
     ]
 
 
+class CapacityC(C.Structure):
+    """rpgpu_capacity (include/rpgpu.h)."""
+    _fields_ = [("n_batches", C.c_uint64), ("record_capacity", C.c_uint64), ("decoded_capacity", C.c_uint64),
+                ("reserved", C.c_uint64)]
+
+
 def exported_symbols_from_header(path: str = HEADER):
     """Function names declared in include/rpgpu.h."""
     src = open(path).read()
@@ -83,6 +89,12 @@ def load():
         "rpgpu_last_timings": (i32, [vp, C.POINTER(C.c_float), i32]),
         "rpgpu_set_timing": (i32, [vp, i32]),
         "rpgpu_uncompress": (i32, [vp, i32, vp, sz, vp, sz, C.POINTER(sz)]),
+        "rpgpu_uncompress_batch": (i32, [vp, u32, vp, vp, vp, vp, vp, vp, vp]),
+        "rpgpu_submit_async": (i32, [vp, C.POINTER(JobC), vp, C.POINTER(vp)]),
+        "rpgpu_poll": (i32, [vp]),
+        "rpgpu_wait": (i32, [vp]),
+        "rpgpu_release": (i32, [vp]),
+        "rpgpu_query_capacity": (i32, [vp, C.POINTER(JobC), vp, C.POINTER(CapacityC)]),
         "rpgpu_validate_host": (i32, [vp, vp]),
         "rpgpu_segment_index": (i32, [vp, vp, u64, vp, u32, u64, vp, vp, vp, vp, vp]),
     }
@@ -113,5 +125,5 @@ def crc32c(data, crc: int = 0) -> int:
     return load().rpgpu_crc32c_extend(crc, a.ctypes.data_as(C.c_void_p), a.nbytes)
 
 
-__all__ = ["load", "check", "crc32c", "JobC", "RpgpuError", "abi",
+__all__ = ["load", "check", "crc32c", "JobC", "CapacityC", "RpgpuError", "abi",
            "exported_symbols_from_header"]

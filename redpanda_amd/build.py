@@ -20,7 +20,7 @@ BUILD = os.path.join(HERE, "_build")
 ARCH = os.environ.get("RPGPU_ARCH", "gfx950")
 
 HIP_SOURCES = ["rp_kernels.hip", "rp_validate.hip", "rp_codec.hip", "rp_index.hip", "rp_runtime.hip"]
-CXX_SOURCES = []
+CXX_SOURCES = ["rp_hostcodec.cpp"]
 
 
 def _hipcc():

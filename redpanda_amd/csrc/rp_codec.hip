@@ -1075,13 +1075,28 @@ __global__ __launch_bounds__(256) void k_decode(DeviceJob j) {
 //     linked frame, whose later blocks may copy from them).
 // ---------------------------------------------------------------------------
 typedef __attribute__((address_space(3))) uint8_t lds_u8;
-constexpr uint32_t kXRing = kXRingKiB * 1024u, kXM = kXRing - 1;
-static_assert((kXRing & kXM) == 0 && kXRing >= 8192, "ring: a power of two >= 8 KiB");
-constexpr uint32_t kBig = 128;                 // longer literals / matches run wave-cooperatively
-// ring stores are deferred: unflushed output stays below kFlushLag (+ one
-// batch, <= 64 x 2 kBig = 16 KiB), so a batch issues no global store and the
-// loads it waits on are counted exactly (gfx9's vmcnt also counts stores)
-constexpr uint32_t kFlushLag = 24u << 10;
+// The ring is small so that many waves share a CU: the execution is a chain
+// of LDS and load latencies per wave, and throughput scales with the waves
+// resident (16 KiB: 10 per CU; the 64 KiB ring of the first wave engine
+// allowed 2).  Matches reaching further back than the ring read the arena.
+#ifndef RPGPU_XRING_KIB
+#define RPGPU_XRING_KIB 16
+#endif
+constexpr uint32_t kXRing = RPGPU_XRING_KIB * 1024u, kXM = kXRing - 1;
+static_assert((kXRing & kXM) == 0 && kXRing >= 16384, "ring: a power of two >= 16 KiB");
+// longer literals / matches run wave-cooperatively (a 64-record batch then
+// writes at most 128 kBig bytes)
+constexpr uint32_t kBig = kXRing >= 32768 ? 128 : 64;
+// ring stores are deferred: unflushed output stays below kFlushLag (+ the
+// 1 KiB flush granule + one batch), so most batches issue no global store
+// and the loads they wait on are counted exactly (gfx9's vmcnt also counts
+// stores)
+constexpr uint32_t kFlushLag = kXRing >= 65536 ? (24u << 10) : kXRing / 4;
+// a batch overwrites ring slots up to 128 kBig bytes behind the front, and
+// its far matches read up to kBig bytes past (front - ring): both must lie
+// below the flushed position; xbig's far reads need ring >= lag + 2 KiB + 64
+static_assert(kFlushLag + 1024 + 128 * kBig + kBig <= kXRing, "ring too small for the flush lag and a batch");
+static_assert(kXRing >= kFlushLag + 2048 + 128, "ring too small for xbig's far reads");
 constexpr uint32_t kBufFlags = 0x00020000u;    // buffer resource word 3 (raw, 32-bit data format)
 constexpr int kSc1 = 16;                       // cache policy: sc1 (L2-coherent, bypasses the vector L1)
 
@@ -1581,7 +1596,7 @@ DEV void exec_chunk(const DeviceJob& j, lds_u8* ring, SeqRec* buf, uint32_t base
 __global__ __launch_bounds__(64) void k_lz_exec(DeviceJob j) {
     extern __shared__ __attribute__((aligned(16))) uint8_t xlds[];
     lds_u8* ring = (lds_u8*)xlds;
-    SeqRec* buf = j.seqs + (size_t)blockIdx.x * 64 * kRecsPerLane;
+    SeqRec* buf = j.seqs + (size_t)blockIdx.x * kRecsPerLane;
     const uint32_t nlink = j.counters[7];
     const uint32_t reserved = j.counters[4];
     const uint32_t nblk = reserved < j.block_capacity ? reserved : j.block_capacity;
@@ -1622,45 +1637,104 @@ __global__ __launch_bounds__(256) void k_decode_blocks(DeviceJob j) {
     }
 }
 
-// one lane per block-parallel frame: all pieces decoded, moved together
-// when an earlier one came out short, content size / checksum checked
+// XXH32 of n bytes at p by one wave: lane l loads stripe l of each 1 KiB row
+// (the next row in flight while this one is folded) and the four
+// accumulators run on the scalar unit, one readlane per stripe dword, so a
+// 1 MiB content checksum is ~2M scalar cycles instead of a one-lane walk of
+// dependent vector loads (lz4 1.9.3 xxhash.c XXH32, as xxh32_lane)
+DEV uint32_t xxh32_wave(const uint8_t* p, uint64_t n, uint32_t seed) {
+    const uint32_t P1 = 0x9E3779B1u, P2 = 0x85EBCA77u, P3 = 0xC2B2AE3Du, P4 = 0x27D4EB2Fu, P5 = 0x165667B1u;
+    const uint32_t l = lane();
+    const uint64_t ns = n >> 4;  // whole stripes
+    uint32_t h;
+    if (ns) {
+        uint32_t v1 = seed + P1 + P2, v2 = seed + P2, v3 = seed, v4 = seed - P1;
+        uint4 q = l < ns ? gld16(p + 16 * (uint64_t)l) : make_uint4(0, 0, 0, 0);
+        for (uint64_t r = 0; r < ns; r += 64) {
+            const uint64_t k = r + 64 + l;
+            const uint4 nq = k < ns ? gld16(p + 16 * k) : make_uint4(0, 0, 0, 0);
+            const uint32_t cnt = ns - r < 64 ? (uint32_t)(ns - r) : 64u;
+            for (uint32_t i = 0; i < cnt; i++) {
+                v1 = rotl32(v1 + rl(q.x, (int)i) * P2, 13) * P1;
+                v2 = rotl32(v2 + rl(q.y, (int)i) * P2, 13) * P1;
+                v3 = rotl32(v3 + rl(q.z, (int)i) * P2, 13) * P1;
+                v4 = rotl32(v4 + rl(q.w, (int)i) * P2, 13) * P1;
+            }
+            q = nq;
+        }
+        h = rotl32(v1, 1) + rotl32(v2, 7) + rotl32(v3, 12) + rotl32(v4, 18);
+    } else {
+        h = seed + P5;
+    }
+    h += (uint32_t)n;
+    // the last < 16 bytes: lane k holds byte k
+    uint64_t i = ns << 4;
+    const uint32_t t = (uint32_t)(n - i);
+    const uint32_t b = l < t ? (uint32_t)p[i + l] : 0u;
+    uint32_t k = 0;
+    for (; k + 4 <= t; k += 4) {
+        const uint32_t wd = rl(b, (int)k) | (rl(b, (int)k + 1) << 8) | (rl(b, (int)k + 2) << 16) | (rl(b, (int)k + 3) << 24);
+        h = rotl32(h + wd * P3, 17) * P4;
+    }
+    for (; k < t; k++) h = rotl32(h + rl(b, (int)k) * P5, 11) * P1;
+    h ^= h >> 15;
+    h *= P2;
+    h ^= h >> 13;
+    h *= P3;
+    h ^= h >> 16;
+    return h;
+}
+
+// one wave per block-parallel frame: all pieces decoded, moved together
+// when an earlier one came out short (ascending 1 KiB steps, each loaded
+// whole before it is stored: safe for any gap), content size / checksum
+// checked
 __global__ __launch_bounds__(256) void k_decode_finish(DeviceJob j) {
     const uint32_t count = j.counters[2];
-    const uint32_t nt = gridDim.x * blockDim.x;
-    for (uint32_t item = blockIdx.x * blockDim.x + threadIdx.x; item < count; item += nt) {
-        const FramePlan fp = j.plans[item];
-        const uint32_t b = j.decode_list[item];
+    const uint32_t nw = gridDim.x * (blockDim.x >> 6);
+    const uint32_t l = lane();
+    for (uint32_t item = blockIdx.x * (blockDim.x >> 6) + uni32(threadIdx.x >> 6); item < count; item += nw) {
+        const uint32_t mode = uni32(j.plans[item].mode);
+        const uint32_t b = uni32(j.decode_list[item]);
         rpgpu_batch_result* R = &j.batches[b];
-        if (fp.mode == 3) {
-            R->flags = R->flags | RPGPU_F_DECODE_OVERFLOW;
+        if (mode == 3) {
+            if (l == 0) R->flags = R->flags | RPGPU_F_DECODE_OVERFLOW;
             continue;
         }
-        if (fp.mode == 0) continue;
-        const uint64_t d0 = j.dcap[b];
+        if (mode == 0) continue;
+        const uint32_t first = uni32(j.plans[item].first), nb = uni32(j.plans[item].nb);
+        const uint64_t d0 = uni64(j.dcap[b]);
         bool ok = true;
         uint64_t run = d0;  // where the next piece belongs
-        for (uint32_t k = 0; k < fp.nb; k++) {
-            const BlockItem& it = j.blocks[fp.first + k];
-            const int32_t out = it.out;
+        for (uint32_t k = 0; k < nb; k++) {
+            const int32_t out = (int32_t)uni32((uint32_t)j.blocks[first + k].out);
             if (out < 0) { ok = false; break; }
-            const uint64_t at = it.dst;
+            const uint64_t at = uni64(j.blocks[first + k].dst);
             if (at < run) { ok = false; break; }  // a piece longer than planned (cannot happen: out <= cap)
             if (at != run) {
-                // move down in ascending 16-byte pieces, each loaded before
-                // it is stored (safe for any gap)
                 uint8_t* dd = j.decoded;
-                int64_t o = 0;
-                for (; o + 16 <= out; o += 16) gst16(dd + run + o, gld16(dd + at + o));
-                for (; o < out; o++) dd[run + o] = dd[at + o];
+                for (uint32_t o = 0; o < (uint32_t)out; o += 1024) {
+                    const uint32_t c = o + 16 * l;
+                    if (c + 16 <= (uint32_t)out) {
+                        const uint4 v = gld16(dd + at + c);
+                        gst16(dd + run + c, v);
+                    }
+                }
+                wait_vm();
+                // the last < 16 bytes, forward byte by byte (dst below src)
+                if (l == 0)
+                    for (uint32_t e = (uint32_t)out & ~15u; e < (uint32_t)out; e++) dd[run + e] = dd[at + e];
+                wait_vm();
             }
             run += (uint64_t)out;
         }
         const uint64_t total = run - d0;
-        if (ok && fp.mode == 1) {
-            if (fp.csf && total != fp.content_size) ok = false;  // frameSize_wrong
-            if (ok && fp.ccs && xxh32_lane(j.decoded + d0, total, 0) != fp.ccs_val) ok = false;
+        if (ok && mode == 1) {
+            if (uni32(j.plans[item].csf) && total != uni64(j.plans[item].content_size)) ok = false;  // frameSize_wrong
+            if (ok && uni32(j.plans[item].ccs) && xxh32_wave(j.decoded + d0, total, 0) != uni32(j.plans[item].ccs_val))
+                ok = false;
         }
-        if (ok) {
+        if (ok && l == 0) {
             R->flags = R->flags | RPGPU_F_CODEC_OK;
             R->decoded_len = (uint32_t)total;
         }
@@ -1677,6 +1751,21 @@ __global__ __launch_bounds__(64) void k_uncompress_one(int codec, const uint8_t*
     res[1] = got;
 }
 
+// rpgpu_uncompress_batch: one lane per payload (staged inputs, planned
+// output slots), res[2 i] = rc, res[2 i + 1] = decoded length
+__global__ __launch_bounds__(256) void k_uncompress_many(const UncItem* __restrict__ items, uint32_t count,
+                                                         const uint8_t* in, uint64_t in_total, uint8_t* out,
+                                                         int64_t* res) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= count) return;
+    const UncItem it = items[i];
+    int64_t got = 0;
+    const int rc = decode_unit(it.codec, Src{in + it.src, (int64_t)it.n, (int64_t)(in_total - it.src)},
+                               Dst{out + it.dst, (int64_t)it.cap}, 0, 0, got);
+    res[2 * i] = rc;
+    res[2 * i + 1] = got;
+}
+
 #ifdef RPGPU_DSTAMPS
 __global__ void k_print_dstamps() {
     const unsigned long long* g = g_dst;
@@ -1691,6 +1780,8 @@ __global__ void k_init_dstamps() {
     for (int i = 0; i < 64; i++) g_dst[i] = 0;
 }
 #endif
+
+uint32_t lz_exec_wgs_per_cu() { return (160u * 1024u) / kXRing; }
 
 hipError_t launch_decode(const DeviceJob& j, hipStream_t s, uint32_t grid) {
     hipLaunchKernelGGL(k_decode, dim3(grid), dim3(256), 0, s, j);
@@ -1726,6 +1817,13 @@ hipError_t launch_lz_exec(const DeviceJob& j, hipStream_t s) {
 
 hipError_t launch_decode_finish(const DeviceJob& j, hipStream_t s, uint32_t grid) {
     hipLaunchKernelGGL(k_decode_finish, dim3(grid), dim3(256), 0, s, j);
+    return hipGetLastError();
+}
+
+hipError_t launch_uncompress_many(const UncItem* items, uint32_t count, const uint8_t* in, uint64_t in_total,
+                                  uint8_t* out, int64_t* res, hipStream_t s) {
+    if (!count) return hipSuccess;
+    hipLaunchKernelGGL(k_uncompress_many, dim3((count + 255) / 256), dim3(256), 0, s, items, count, in, in_total, out, res);
     return hipGetLastError();
 }
 

@@ -92,12 +92,10 @@ struct SeqRec {
 // k_lz_walk stores each piece's records in slabs of kSlabRecs taken from
 // one pool (bump counter); slab_next chains a piece's slabs
 constexpr uint32_t kSlabRecs = 512;
-#ifndef RPGPU_XRING_KIB
-#define RPGPU_XRING_KIB 64
-#endif
-constexpr uint32_t kXRingKiB = RPGPU_XRING_KIB;       // k_lz_exec LDS ring per wave
-constexpr uint32_t kExecWgsPerCu = 160 / kXRingKiB;   // one wave per workgroup
 constexpr uint32_t kRecsPerLane = 256;                // k_lz_exec's own walk (pool exhausted): records per pass
+// k_lz_exec workgroups (one wave, one LDS ring each) resident per CU, as
+// compiled into rp_codec.hip (its ring size decides it)
+uint32_t lz_exec_wgs_per_cu();
 
 // A piece's walk result (k_lz_walk -> k_lz_exec)
 struct PieceState {
@@ -151,7 +149,7 @@ struct DeviceJob {
     uint32_t* decode_list;        // batch_capacity: ordinals of batches to uncompress
     uint32_t* seq_list;           // batch_capacity: decode items decoded whole by one lane
     uint32_t* link_list;          // batch_capacity: decode items whose linked LZ4F blocks one wave decodes in order
-    SeqRec* seqs;                 // k_lz_exec's own walks: kRecsPerLane per lane of each resident wave
+    SeqRec* seqs;                 // k_lz_exec's own walks: kRecsPerLane per resident wave
     uint32_t exec_waves;          // k_lz_exec grid (one wave per workgroup; sizes `seqs`)
     PieceState* pstate;           // block_capacity: walk results
     SeqRec* pool;                 // record slabs
@@ -178,6 +176,14 @@ hipError_t launch_decode_finish(const DeviceJob& j, hipStream_t s, uint32_t grid
 // one payload, one wave (rpgpu_uncompress); res[0] = rc (0 / -1 / -2), res[1] = out_len
 hipError_t launch_uncompress_one(int codec, const uint8_t* src, uint64_t n, uint8_t* dst, uint64_t cap,
                                  int64_t* res, hipStream_t s);
+// rpgpu_uncompress_batch: one payload per lane
+struct UncItem {
+    uint64_t src, n;    // input bytes [src, src + n) of the staged inputs
+    uint64_t dst, cap;  // output slot [dst, dst + cap) (cap includes 16 bytes of wild-copy room)
+    int32_t codec, pad;
+};
+hipError_t launch_uncompress_many(const UncItem* items, uint32_t count, const uint8_t* in, uint64_t in_total,
+                                  uint8_t* out, int64_t* res, hipStream_t s);
 hipError_t launch_finalize(const DeviceJob& j, hipStream_t s);
 hipError_t scan_exclusive_u64(uint64_t* data, uint64_t n, void* temp, size_t temp_bytes, hipStream_t s);
 // n = min(*d_n, n_cap), read on the device

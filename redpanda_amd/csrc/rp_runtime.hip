@@ -17,6 +17,7 @@
 #include <vector>
 
 #include "rp_device.h"
+#include "rp_hostcodec.h"
 
 namespace rp {
 
@@ -104,6 +105,14 @@ struct rpgpu_ctx {
     size_t uws_bytes = 0;
     size_t ev_used = 0;
     uint32_t cu_count = 256;
+    // rpgpu_query_capacity scratch (summaries, totals, batch results), grow-only
+    void* qws = nullptr;
+    size_t qws_bytes = 0;
+    // rpgpu_uncompress_batch staging: pinned host and device, grow-only
+    void* bh = nullptr;
+    size_t bh_bytes = 0;
+    void* bd = nullptr;
+    size_t bd_bytes = 0;
     // rpgpu_segment_index workspace (piece tables), grow-only
     void* iws = nullptr;
     size_t iws_bytes = 0;
@@ -160,6 +169,16 @@ int fail(rpgpu_ctx* c, int code, const char* what, hipError_t e = hipSuccess) {
 
 size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 
+// gzip / zstd: the CPU fallback behind compressor::uncompress (rp_hostcodec.cpp)
+int host_codec(rpgpu_ctx* c, int codec, const void* in, size_t n, void* out, size_t cap, size_t* out_len) {
+    const int rc = host_uncompress(codec, (const uint8_t*)in, n, (uint8_t*)out, cap, out_len);
+    if (rc == 0) return RPGPU_OK;
+    if (rc == kHostCodecOverflow) return fail(c, RPGPU_E_OVERFLOW, "rpgpu_uncompress: output capacity too small");
+    if (rc == kHostCodecMissing) return fail(c, RPGPU_E_UNSUPPORTED, "rpgpu_uncompress: zlib / libzstd not loadable");
+    *out_len = 0;
+    return fail(c, RPGPU_E_CODEC, codec == RPGPU_CODEC_GZIP ? "gzip uncompress error" : "ZSTD error");
+}
+
 }  // namespace
 
 extern "C" {
@@ -199,6 +218,9 @@ int rpgpu_destroy(rpgpu_ctx* c) {
     if (c->ws) hipFree(c->ws);
     if (c->uws) hipFree(c->uws);
     if (c->iws) hipFree(c->iws);
+    if (c->qws) hipFree(c->qws);
+    if (c->bd) hipFree(c->bd);
+    if (c->bh) hipHostFree(c->bh);
     if (c->seqs) hipFree(c->seqs);
     if (c->pool) hipFree(c->pool);
     if (c->pin) hipHostFree(c->pin);
@@ -311,7 +333,27 @@ int rpgpu_last_timings(rpgpu_ctx* c, float* ms, int n) {
 // ---------------------------------------------------------------------------
 // submit
 // ---------------------------------------------------------------------------
-int rpgpu_submit(rpgpu_ctx* c, const rpgpu_job* job, void* stream) {
+}  // extern "C"
+
+namespace {
+// device addresses of the plan a stopped submit leaves in the workspace
+struct PlanPtrs {
+    const uint64_t* n_batches;  // chunk_count[total_chunks]
+    const uint64_t* slots;      // exclusive scan of index slots (batch_capacity + 1)
+    const uint64_t* dcap;       // exclusive scan of decode bytes (batch_capacity + 1)
+};
+enum SubmitStop { kRunAll = 0, kStopAfterCount = 1, kStopAfterPlan = 2 };
+int submit_impl(rpgpu_ctx* c, const rpgpu_job* job, void* stream, int stop, PlanPtrs* plan);
+}  // namespace
+
+extern "C" {
+
+int rpgpu_submit(rpgpu_ctx* c, const rpgpu_job* job, void* stream) { return submit_impl(c, job, stream, kRunAll, nullptr); }
+
+}  // extern "C"
+
+namespace {
+int submit_impl(rpgpu_ctx* c, const rpgpu_job* job, void* stream, int stop, PlanPtrs* plan) {
     if (!c || !job || !job->d_data || !job->d_seg_offsets || !job->h_seg_offsets || job->n_segments == 0 ||
         !job->d_batches || !job->d_summaries || !job->d_totals)
         return fail(c, RPGPU_E_INVALID, "rpgpu_submit: missing argument");
@@ -358,8 +400,8 @@ int rpgpu_submit(rpgpu_ctx* c, const rpgpu_job* job, void* stream) {
     const size_t o_scan = take(scan_temp_bytes(std::max<uint64_t>(tc, bcap)) + 64);
     const size_t need = off;
     if (dec && !c->seqs) {
-        const uint32_t waves = c->cu_count * kExecWgsPerCu;
-        if (hipMalloc(&c->seqs, (size_t)waves * 64 * kRecsPerLane * sizeof(SeqRec)) != hipSuccess) {
+        const uint32_t waves = c->cu_count * lz_exec_wgs_per_cu();
+        if (hipMalloc(&c->seqs, (size_t)waves * kRecsPerLane * sizeof(SeqRec)) != hipSuccess) {
             c->seqs = nullptr;
             return fail(c, RPGPU_E_NOMEM, "decode sequence workspace");
         }
@@ -460,10 +502,17 @@ int rpgpu_submit(rpgpu_ctx* c, const rpgpu_job* job, void* stream) {
     if (tm) HIPCHK(c, hipEventRecord(ev[1], s));
     STAGE("resolve", launch_resolve(j, s));
     STAGE("scan_chunks", scan_exclusive_u64(j.chunk_count, tc, scan_tmp, 0, s));
+    if (plan) {
+        plan->n_batches = j.chunk_count + tc;
+        plan->slots = j.slots;
+        plan->dcap = j.dcap;
+    }
+    if (stop == kStopAfterCount) return RPGPU_OK;
     STAGE("emit", launch_emit(j, s));
     const uint64_t* d_nb = j.chunk_count + tc;
     STAGE("scan_slots", scan_exclusive_u64_devn(j.slots, d_nb, bcap, scan_tmp, s));
     STAGE("scan_dcap", scan_exclusive_u64_devn(j.dcap, d_nb, bcap, scan_tmp, s));
+    if (stop == kStopAfterPlan) return RPGPU_OK;
     if (tm) HIPCHK(c, hipEventRecord(ev[2], s));
     // decode first: k_validate checksums and walks the decoded payloads
     if ((job->flags & RPGPU_JOB_DECODE) && j.decoded) {
@@ -483,6 +532,115 @@ int rpgpu_submit(rpgpu_ctx* c, const rpgpu_job* job, void* stream) {
     STAGE("finalize", launch_finalize(j, s));
     if (tm) HIPCHK(c, hipEventRecord(ev[6], s));
 #undef STAGE
+    return RPGPU_OK;
+}
+}  // namespace
+
+extern "C" {
+
+// ---------------------------------------------------------------------------
+// output sizing before the run (SURVEY §8(b) segment-engine row: "result
+// arrays ... sized by a query call"): the chain is discovered and planned
+// (discover -> resolve -> emit -> scans) into context scratch, twice: once to
+// count the batches, once with that many result slots to plan the record
+// index and the decode arena.  Synchronous.
+// ---------------------------------------------------------------------------
+int rpgpu_query_capacity(rpgpu_ctx* c, const rpgpu_job* job, void* stream, rpgpu_capacity* out) {
+    if (!c || !job || !out) return RPGPU_E_INVALID;
+    if (!job->d_data || !job->d_seg_offsets || !job->h_seg_offsets || job->n_segments == 0)
+        return fail(c, RPGPU_E_INVALID, "rpgpu_query_capacity: missing argument");
+    hipSetDevice(c->device);
+    hipStream_t s = pick(c, stream);
+    const uint32_t nseg = job->n_segments;
+    auto grow = [&](void** p, size_t* have, size_t want) -> int {
+        if (want <= *have) return RPGPU_OK;
+        if (*p) { HIPCHK(c, hipStreamSynchronize(s)); HIPCHK(c, hipFree(*p)); *p = nullptr; *have = 0; }
+        if (hipMalloc(p, want) != hipSuccess) { *p = nullptr; return fail(c, RPGPU_E_NOMEM, "rpgpu_query_capacity: scratch"); }
+        *have = want;
+        return RPGPU_OK;
+    };
+    const size_t fixed = align_up((size_t)nseg * sizeof(rpgpu_segment_summary), 256) + align_up(sizeof(rpgpu_job_totals), 256);
+    int rc = grow(&c->qws, &c->qws_bytes, fixed + 256);
+    if (rc) return rc;
+    rpgpu_job q = *job;
+    q.d_summaries = (rpgpu_segment_summary*)c->qws;
+    q.d_totals = (rpgpu_job_totals*)((uint8_t*)c->qws + align_up((size_t)nseg * sizeof(rpgpu_segment_summary), 256));
+    q.d_batches = (rpgpu_batch_result*)((uint8_t*)c->qws + fixed);
+    q.batch_capacity = 0;
+    q.d_records = nullptr;
+    q.record_capacity = 0;
+    q.d_decoded = nullptr;
+    q.decoded_capacity = 0;
+    q.d_valid_bitmap = nullptr;
+    PlanPtrs pp;
+    rc = submit_impl(c, &q, stream, kStopAfterCount, &pp);
+    if (rc) return rc;
+    uint64_t nb = 0;
+    HIPCHK(c, hipMemcpyAsync(&nb, pp.n_batches, 8, hipMemcpyDeviceToHost, s));
+    HIPCHK(c, hipStreamSynchronize(s));
+    rc = grow(&c->qws, &c->qws_bytes, fixed + (size_t)(nb + 1) * sizeof(rpgpu_batch_result));
+    if (rc) return rc;
+    q.d_summaries = (rpgpu_segment_summary*)c->qws;
+    q.d_totals = (rpgpu_job_totals*)((uint8_t*)c->qws + align_up((size_t)nseg * sizeof(rpgpu_segment_summary), 256));
+    q.d_batches = (rpgpu_batch_result*)((uint8_t*)c->qws + fixed);
+    q.batch_capacity = nb;
+    rc = submit_impl(c, &q, stream, kStopAfterPlan, &pp);
+    if (rc) return rc;
+    uint64_t v[2] = {0, 0};
+    HIPCHK(c, hipMemcpyAsync(&v[0], pp.slots + nb, 8, hipMemcpyDeviceToHost, s));
+    HIPCHK(c, hipMemcpyAsync(&v[1], pp.dcap + nb, 8, hipMemcpyDeviceToHost, s));
+    HIPCHK(c, hipStreamSynchronize(s));
+    out->n_batches = nb;
+    out->record_capacity = v[0];
+    out->decoded_capacity = (job->flags & RPGPU_JOB_DECODE) ? v[1] : 0;
+    out->reserved = 0;
+    return RPGPU_OK;
+}
+
+// ---------------------------------------------------------------------------
+// non-blocking completion (rpgpu_poll / rpgpu_wait on a job):
+// rpgpu_submit followed by an event on the launch stream
+// ---------------------------------------------------------------------------
+struct rpgpu_pending {
+    rpgpu_ctx* c;
+    hipEvent_t ev;
+};
+
+int rpgpu_submit_async(rpgpu_ctx* c, const rpgpu_job* job, void* stream, rpgpu_pending** out) {
+    if (!c || !out) return RPGPU_E_INVALID;
+    *out = nullptr;
+    const int rc = submit_impl(c, job, stream, kRunAll, nullptr);
+    if (rc) return rc;
+    rpgpu_pending* p = new rpgpu_pending{c, nullptr};
+    hipError_t e = hipEventCreateWithFlags(&p->ev, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventRecord(p->ev, pick(c, stream));
+    if (e != hipSuccess) {
+        if (p->ev) (void)hipEventDestroy(p->ev);
+        delete p;
+        return fail(c, RPGPU_E_HIP, "rpgpu_submit_async: event", e);
+    }
+    *out = p;
+    return RPGPU_OK;
+}
+
+int rpgpu_poll(rpgpu_pending* p) {
+    if (!p) return RPGPU_E_INVALID;
+    const hipError_t e = hipEventQuery(p->ev);
+    if (e == hipSuccess) return RPGPU_OK;
+    if (e == hipErrorNotReady) return RPGPU_PENDING;
+    return fail(p->c, RPGPU_E_HIP, "rpgpu_poll", e);
+}
+
+int rpgpu_wait(rpgpu_pending* p) {
+    if (!p) return RPGPU_E_INVALID;
+    HIPCHK(p->c, hipEventSynchronize(p->ev));
+    return RPGPU_OK;
+}
+
+int rpgpu_release(rpgpu_pending* p) {
+    if (!p) return RPGPU_E_INVALID;
+    (void)hipEventDestroy(p->ev);
+    delete p;
     return RPGPU_OK;
 }
 
@@ -551,15 +709,16 @@ int rpgpu_segment_index(rpgpu_ctx* c, const rpgpu_batch_result* d_batches, uint6
 }
 
 int rpgpu_uncompress(rpgpu_ctx* c, int codec, const void* in, size_t n, void* out, size_t cap, size_t* out_len) {
-    if (!c || (!in && n) || !out_len) return RPGPU_E_INVALID;
+    if ((!in && n) || !out_len || (!out && cap)) return RPGPU_E_INVALID;
+    // gzip / zstd run on the host: no context needed (ctx may be NULL)
+    if (!c && codec != RPGPU_CODEC_GZIP && codec != RPGPU_CODEC_ZSTD) return RPGPU_E_INVALID;
     *out_len = 0;
     if (codec < 0 || codec > RPGPU_CODEC_ZSTD) return fail(c, RPGPU_E_INVALID, "rpgpu_uncompress: unknown codec");
     // compressor::uncompress (compression/compression.cc:34-53): an empty
     // buffer throws before the codec dispatch
     if (n == 0) return fail(c, RPGPU_E_CODEC, "rpgpu_uncompress: asked to decompress an empty buffer");
     if (codec == RPGPU_CODEC_NONE) return fail(c, RPGPU_E_CODEC, "compressor: nothing to uncompress for 'none'");
-    if (codec == RPGPU_CODEC_GZIP || codec == RPGPU_CODEC_ZSTD)
-        return fail(c, RPGPU_E_UNSUPPORTED, "rpgpu_uncompress: gzip/zstd are not decoded by the engine");
+    if (codec == RPGPU_CODEC_GZIP || codec == RPGPU_CODEC_ZSTD) return host_codec(c, codec, in, n, out, cap, out_len);
     hipSetDevice(c->device);
     const uint64_t dcap = decode_capacity_dev(codec, (const uint8_t*)in, n);
     const size_t in_sz = align_up(n + 16, 256), out_sz = align_up(dcap + 16, 256);
@@ -582,6 +741,79 @@ int rpgpu_uncompress(rpgpu_ctx* c, int codec, const void* in, size_t n, void* ou
     *out_len = (size_t)res[1];
     if ((size_t)res[1] > cap) return fail(c, RPGPU_E_OVERFLOW, "rpgpu_uncompress: output capacity too small");
     if (res[1]) HIPCHK(c, hipMemcpy(out, d_out, (size_t)res[1], hipMemcpyDeviceToHost));
+    return RPGPU_OK;
+}
+
+// Many payloads per GPU round trip (the per-batch call sites of
+// compressor::uncompress, storage/parser_utils.cc:51 and
+// kafka/protocol/kafka_batch_adapter.cc:259, batched): lz4/snappy payloads
+// are staged into one pinned buffer, copied once, decoded one per lane, and
+// their outputs copied back once; gzip/zstd go to the host fallback; every
+// payload gets its own status (the rpgpu_uncompress codes).
+int rpgpu_uncompress_batch(rpgpu_ctx* c, uint32_t n, const int* codecs, const void* const* in, const size_t* in_len,
+                           void* const* out, const size_t* cap, size_t* out_len, int* status) {
+    if (!c || (n && (!codecs || !in || !in_len || !out || !cap || !out_len || !status))) return RPGPU_E_INVALID;
+    std::vector<uint32_t> dev;  // payloads decoded on the device
+    std::vector<UncItem> items;
+    uint64_t in_total = 0, out_total = 0;
+    for (uint32_t i = 0; i < n; i++) {
+        out_len[i] = 0;
+        const int codec = codecs[i];
+        if (codec < 0 || codec > RPGPU_CODEC_ZSTD || (!in[i] && in_len[i])) { status[i] = RPGPU_E_INVALID; continue; }
+        if (in_len[i] == 0 || codec == RPGPU_CODEC_NONE) { status[i] = RPGPU_E_CODEC; continue; }
+        if (codec == RPGPU_CODEC_GZIP || codec == RPGPU_CODEC_ZSTD) {
+            status[i] = host_codec(c, codec, in[i], in_len[i], out[i], cap[i], &out_len[i]);
+            continue;
+        }
+        UncItem it;
+        it.src = in_total;
+        it.n = in_len[i];
+        it.dst = out_total;
+        it.cap = align_up(decode_capacity_dev(codec, (const uint8_t*)in[i], in_len[i]) + 16, 16);
+        it.codec = codec;
+        it.pad = 0;
+        in_total += align_up(in_len[i], 16);
+        out_total += it.cap;
+        items.push_back(it);
+        dev.push_back(i);
+        status[i] = RPGPU_E_CODEC;
+    }
+    if (items.empty()) return RPGPU_OK;
+    hipSetDevice(c->device);
+    hipStream_t s = c->stream;
+    const uint32_t m = (uint32_t)items.size();
+    // device: [inputs + 16][items][results][outputs]; host (pinned): the same
+    // first three parts, then the outputs coming back
+    const size_t o_items = align_up(in_total + 16, 256), o_res = align_up(o_items + m * sizeof(UncItem), 256);
+    const size_t o_out = align_up(o_res + (size_t)m * 16, 256), total = o_out + out_total;
+    if (total > c->bd_bytes) {
+        if (c->bd) { HIPCHK(c, hipStreamSynchronize(s)); HIPCHK(c, hipFree(c->bd)); c->bd = nullptr; c->bd_bytes = 0; }
+        if (hipMalloc(&c->bd, total) != hipSuccess) { c->bd = nullptr; return fail(c, RPGPU_E_NOMEM, "uncompress batch staging"); }
+        c->bd_bytes = total;
+    }
+    if (total > c->bh_bytes) {
+        if (c->bh) { HIPCHK(c, hipStreamSynchronize(s)); HIPCHK(c, hipHostFree(c->bh)); c->bh = nullptr; c->bh_bytes = 0; }
+        if (hipHostMalloc(&c->bh, total, hipHostMallocDefault) != hipSuccess) { c->bh = nullptr; return fail(c, RPGPU_E_NOMEM, "uncompress batch pinned staging"); }
+        c->bh_bytes = total;
+    }
+    uint8_t* h = (uint8_t*)c->bh;
+    uint8_t* d = (uint8_t*)c->bd;
+    std::memset(h + in_total, 0, o_items - in_total);
+    for (uint32_t k = 0; k < m; k++) std::memcpy(h + items[k].src, in[dev[k]], items[k].n);
+    std::memcpy(h + o_items, items.data(), m * sizeof(UncItem));
+    HIPCHK(c, hipMemcpyAsync(d, h, o_res, hipMemcpyHostToDevice, s));
+    HIPCHK(c, launch_uncompress_many((const UncItem*)(d + o_items), m, d, in_total + 16, d + o_out, (int64_t*)(d + o_res), s));
+    HIPCHK(c, hipMemcpyAsync(h + o_res, d + o_res, total - o_res, hipMemcpyDeviceToHost, s));
+    HIPCHK(c, hipStreamSynchronize(s));
+    const int64_t* res = (const int64_t*)(h + o_res);
+    for (uint32_t k = 0; k < m; k++) {
+        const uint32_t i = dev[k];
+        if (res[2 * k] != 0) { status[i] = RPGPU_E_CODEC; continue; }
+        out_len[i] = (size_t)res[2 * k + 1];
+        if (out_len[i] > cap[i]) { status[i] = RPGPU_E_OVERFLOW; continue; }
+        if (out_len[i]) std::memcpy(out[i], h + o_out + items[k].dst, out_len[i]);
+        status[i] = RPGPU_OK;
+    }
     return RPGPU_OK;
 }
 

@@ -13,7 +13,7 @@ from dataclasses import dataclass
 import numpy as np
 
 from . import abi
-from ._lib import JobC, RpgpuError, check, load
+from ._lib import CapacityC, JobC, RpgpuError, check, load
 
 
 def _torch():
@@ -128,6 +128,72 @@ class Engine:
             bitmap=torch.zeros(((max(batch_capacity, 1) + 63) // 64) * 8, dtype=u8, device=dev) if bitmap else None,
             n_segments=n_segments,
         )
+
+    def _job(self, data, seg_offsets, out, flags, chunk_bytes, d_seg_offsets, layout):
+        torch = _torch()
+        h_off = np.ascontiguousarray(np.asarray(seg_offsets, dtype=np.uint64))
+        if d_seg_offsets is None:
+            d_seg_offsets = torch.from_numpy(h_off.view(np.int64)).to(data.device)
+        job = JobC()
+        job.d_data = data.data_ptr()
+        job.d_seg_offsets = d_seg_offsets.data_ptr()
+        job.h_seg_offsets = h_off.ctypes.data
+        job.n_segments = h_off.size - 1
+        job.layout = layout
+        job.flags = flags
+        job.chunk_bytes = chunk_bytes
+        if out is not None:
+            job.d_batches = out.batches.data_ptr()
+            job.batch_capacity = out.batches.numel() // abi.BATCH_RESULT.itemsize
+            job.d_records = out.records.data_ptr()
+            job.record_capacity = out.records.numel() // abi.RECORD_INDEX.itemsize
+            job.d_decoded = out.decoded.data_ptr()
+            job.decoded_capacity = out.decoded.numel()
+            job.d_summaries = out.summaries.data_ptr()
+            job.d_totals = out.totals.data_ptr()
+            job.d_valid_bitmap = out.bitmap.data_ptr() if out.bitmap is not None else 0
+        return job, (h_off, d_seg_offsets)
+
+    def query_capacity(self, data, seg_offsets, flags: int = abi.JOB_CRC | abi.JOB_PARSE, chunk_bytes: int = 0,
+                       layout: int = abi.LAYOUT_DISK, stream=None):
+        """rpgpu_query_capacity: (n_batches, record_capacity, decoded_capacity)
+        the job needs, before it runs (synchronous)."""
+        job, keep = self._job(data, seg_offsets, None, flags, chunk_bytes, None, layout)
+        s, finish = self._stream(data.device, stream)
+        cap = CapacityC()
+        check(self.L.rpgpu_query_capacity(self.ctx, C.byref(job), C.c_void_p(s.cuda_stream), C.byref(cap)), self.ctx,
+              "rpgpu_query_capacity")
+        finish(data, keep[1])
+        return int(cap.n_batches), int(cap.record_capacity), int(cap.decoded_capacity)
+
+    def submit_async(self, data, seg_offsets, out: DeviceResult, flags: int = abi.JOB_CRC | abi.JOB_PARSE,
+                     chunk_bytes: int = 0, layout: int = abi.LAYOUT_DISK):
+        """rpgpu_submit_async on the context's own stream: returns a Pending
+        whose poll() never blocks.  Inputs and outputs stay referenced by it
+        until it completes."""
+        job, keep = self._job(data, seg_offsets, out, flags, chunk_bytes, None, layout)
+        torch = _torch()
+        torch.cuda.current_stream(data.device).synchronize()  # inputs written by torch are complete
+        p = C.c_void_p()
+        check(self.L.rpgpu_submit_async(self.ctx, C.byref(job), None, C.byref(p)), self.ctx, "rpgpu_submit_async")
+        return Pending(self, p, (data, out, keep))
+
+    def uncompress_batch(self, codecs, payloads, caps=None):
+        """rpgpu_uncompress_batch: [(status, bytes)] per payload, one device
+        round trip for the lz4/snappy ones."""
+        n = len(payloads)
+        srcs = [np.frombuffer(bytes(p), dtype=np.uint8) for p in payloads]
+        caps = caps or [max(len(p) * 300, 1 << 20) for p in payloads]
+        outs = [np.zeros(max(c, 1), dtype=np.uint8) for c in caps]
+        ci = (C.c_int * max(n, 1))(*codecs)
+        ip = (C.c_void_p * max(n, 1))(*[s.ctypes.data for s in srcs])
+        il = (C.c_size_t * max(n, 1))(*[s.nbytes for s in srcs])
+        op = (C.c_void_p * max(n, 1))(*[o.ctypes.data for o in outs])
+        oc = (C.c_size_t * max(n, 1))(*caps)
+        ol = (C.c_size_t * max(n, 1))()
+        st = (C.c_int * max(n, 1))()
+        check(self.L.rpgpu_uncompress_batch(self.ctx, n, ci, ip, il, op, oc, ol, st), self.ctx, "rpgpu_uncompress_batch")
+        return [(int(st[i]), outs[i][: ol[i]].tobytes() if st[i] == 0 else int(ol[i])) for i in range(n)]
 
     def submit(self, data, seg_offsets, out: DeviceResult, flags: int = abi.JOB_CRC | abi.JOB_PARSE,
                chunk_bytes: int = 0, stream=None, d_seg_offsets=None, layout: int = abi.LAYOUT_DISK):
@@ -271,6 +337,37 @@ class Engine:
         check(rc, self.ctx, "rpgpu_validate_host")
         nb = int(min(tot[0]["n_batches"], batch_capacity))
         return batches[:nb], sums[:n], tot[0]
+
+
+class Pending:
+    """An in-flight job (rpgpu_pending)."""
+
+    def __init__(self, eng, handle, keep):
+        self.eng, self.h, self._keep = eng, handle, keep
+
+    def poll(self) -> bool:
+        rc = self.eng.L.rpgpu_poll(self.h)
+        if rc == abi.PENDING:
+            return False
+        check(rc, self.eng.ctx, "rpgpu_poll")
+        return True
+
+    def wait(self):
+        check(self.eng.L.rpgpu_wait(self.h), self.eng.ctx, "rpgpu_wait")
+
+    def release(self):
+        if self.h:
+            self.eng.L.rpgpu_release(self.h)
+            self.h = None
+            self._keep = None
+
+    def __del__(self):
+        try:
+            if self.h:
+                self.wait()
+            self.release()
+        except Exception:
+            pass
 
 
 class HostJobC(C.Structure):

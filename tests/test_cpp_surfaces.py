@@ -313,15 +313,24 @@ def test_compressor_uncompress(driver, oracle, engine, tmp_path):
         else:
             assert line == "U runtime_error", ent["name"]
     # compression.cc:34-53: empty input and codec none throw runtime_error;
-    # gzip / zstd are not decoded by this engine (logic_error, documented)
+    # gzip / zstd run the reference's loops on the host (CPU fallback):
+    # malformed streams throw runtime_error, good ones decode
     empty = str(tmp_path / "empty.bin")
     open(empty, "wb").close()
     one = str(tmp_path / "one.bin")
     open(one, "wb").write(b"\x01\x02\x03")
     assert run(driver, "uncompress", abi.CODEC_GZIP, empty, out) == ["U runtime_error"]
     assert run(driver, "uncompress", abi.CODEC_NONE, one, out) == ["U runtime_error"]
-    assert run(driver, "uncompress", abi.CODEC_GZIP, one, out) == ["U logic_error"]
-    assert run(driver, "uncompress", abi.CODEC_ZSTD, one, out) == ["U logic_error"]
+    assert run(driver, "uncompress", abi.CODEC_GZIP, one, out) == ["U runtime_error"]
+    assert run(driver, "uncompress", abi.CODEC_ZSTD, one, out) == ["U runtime_error"]
+    import gzip
+    from tests.test_hostcodec import corpus, zstd_compress
+    gz, zs = str(tmp_path / "a.gz"), str(tmp_path / "a.zst")
+    open(gz, "wb").write(gzip.compress(corpus(20, 200000)))
+    open(zs, "wb").write(zstd_compress(corpus(21, 200000)))
+    o1, o2 = str(tmp_path / "a.gz.out"), str(tmp_path / "a.zst.out")
+    assert run(driver, "uncompress", abi.CODEC_GZIP, gz, o1, abi.CODEC_ZSTD, zs, o2) == ["U ok 200000"] * 2
+    assert open(o1, "rb").read() == corpus(20, 200000) and open(o2, "rb").read() == corpus(21, 200000)
 
 
 # ---------------------------------------------------------------------------

@@ -332,3 +332,56 @@ def test_host_path(engine, oracle, rplib, group_kib, recipe, monkeypatch):
     for k in ("n_batches", "n_records", "decoded_bytes"):
         assert int(t[k]) == int(ref.totals[k]), k
     assert int(t["overflow"]) == 0
+
+
+# ---------------------------------------------------------------------------
+# segment-engine boundary: async completion, capacity query,
+# batched uncompress
+# ---------------------------------------------------------------------------
+def test_async_poll_wait_and_capacity_query(engine, oracle, rplib):
+    """rpgpu_query_capacity sizes the outputs before the run (== the oracle
+    job's totals); rpgpu_submit_async + rpgpu_poll never block and the
+    results after completion equal the oracle's."""
+    import time
+
+    import torch
+    MIX = (1 << abi.CODEC_NONE) | (1 << abi.CODEC_LZ4) | (1 << abi.CODEC_SNAPPY)
+    segs = [gen(rplib, 3 << 20, i, seed=0xC5, batch_bytes=0, min_batch=200, max_batch=400000, codec_mix=MIX,
+                corrupt_payload_ppm=20000) for i in range(3)]
+    offs = np.cumsum([0] + [s.size for s in segs]).astype(np.uint64)
+    data = np.concatenate(segs)
+    flags = abi.JOB_CRC | abi.JOB_PARSE | abi.JOB_DECODE
+    ref = oracle.run_job(data, offs, flags)
+    d = torch.from_numpy(data).cuda()
+    nb, nrec, ndec = engine.query_capacity(d, offs, flags)
+    assert nb == len(ref.batches) and nrec == int(ref.totals["record_capacity_needed"])
+    assert ndec == int(ref.totals["decoded_capacity_needed"])
+    out = engine.alloc_outputs(len(segs), nb, nrec, ndec)  # exactly what the query said
+    p = engine.submit_async(d, offs, out, flags)
+    polls = 0
+    while not p.poll():
+        polls += 1
+        time.sleep(0.0005)
+    p.release()
+    got = out.to_host()
+    assert int(got.totals["overflow"]) == 0
+    assert_same(got, ref, flags)
+    p2 = engine.submit_async(d, offs, out, flags)
+    p2.wait()
+    assert p2.poll()
+    p2.release()
+    assert_same(out.to_host(), ref, flags)
+
+
+def test_uncompress_batch_matches_single(engine, oracle):
+    """rpgpu_uncompress_batch over every codec fixture at once (one device
+    round trip) == the oracle per payload, accept/reject and bytes."""
+    ents = json.load(open(os.path.join(G, "manifest.json")))["codecs"]
+    datas = [open(os.path.join(G, "codecs", e["name"] + ".bin"), "rb").read() for e in ents]
+    res = engine.uncompress_batch([e["codec"] for e in ents], datas)
+    for e, dat, (st, got) in zip(ents, datas, res):
+        rc, want = oracle.uncompress(e["codec"], dat, max(len(dat) * 300, 1 << 20))
+        if rc == 0:
+            assert st == 0 and got == want, e["name"]
+        else:
+            assert st == abi.E_CODEC, e["name"]
