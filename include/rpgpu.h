@@ -345,6 +345,28 @@ int rpgpu_segment_index(rpgpu_ctx* ctx, const rpgpu_batch_result* d_batches, uin
                         uint64_t* d_position, void* stream);
 
 /* ------------------------------------------------------------------------ */
+/* Write side: header stamping of batches about to be written (SURVEY.md     */
+/* §8(f) row 3)                                                              */
+/* ------------------------------------------------------------------------ */
+/* disk_log_appender::operator() (storage/disk_log_appender.cc:72-74): the
+ * batch gets the appender's next offset as base_offset, the appender moves
+ * on to last_offset + 1 (:113-119). */
+#define RPGPU_STAMP_OFFSETS (1u << 0)
+/* storage::internal::reset_size_checksum_metadata (storage/parser_utils.cc:
+ * 114-120): size_bytes = 61 + payload bytes, crc = crc_record_batch. */
+#define RPGPU_STAMP_CRC (1u << 1)
+
+/* n disk-layout batches in the device buffer d_data (16-byte aligned, with 16
+ * readable bytes past the last payload): batch i's 61-byte header at
+ * d_pos[i], its payload (d_payload_len[i] bytes) right after it.  In place,
+ * in batch order: RPGPU_STAMP_OFFSETS numbers them from next_offset,
+ * RPGPU_STAMP_CRC resets size and crc, and header_crc
+ * (model::internal_header_only_crc) is always recomputed last.  Batches must
+ * not overlap.  Asynchronous on `stream`. */
+int rpgpu_stamp(rpgpu_ctx* ctx, uint8_t* d_data, const uint64_t* d_pos, const uint32_t* d_payload_len, uint32_t n,
+                int64_t next_offset, uint32_t flags, void* stream);
+
+/* ------------------------------------------------------------------------ */
 /* compression::compressor::uncompress (compression/compression.h:21-24)     */
 /* ------------------------------------------------------------------------ */
 

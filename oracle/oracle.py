@@ -75,6 +75,8 @@ def lib():
         L.rpo_baseline_validate.restype = C.c_int64
         L.rpo_baseline_validate.argtypes = [C.c_void_p, C.c_void_p, C.c_uint32, C.c_int, C.c_int,
                                             C.POINTER(C.c_double), C.POINTER(C.c_uint64)]
+        L.rpo_stamp_batches.restype = None
+        L.rpo_stamp_batches.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32, C.c_int64, C.c_uint32]
         L.rpo_segment_index.restype = C.c_int
         L.rpo_segment_index.argtypes = [C.c_void_p, C.c_uint64, C.c_void_p, C.c_uint32, C.c_uint64,
                                         C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]
@@ -301,4 +303,15 @@ def segment_index(batches: np.ndarray, summaries: np.ndarray, base_offsets, step
     for s in st[:nseg]:
         a, n = int(s["first_entry"]), int(s["n_entries"])
         out.append((s, ro[a:a + n].copy(), rt[a:a + n].copy(), ps[a:a + n].copy()))
+    return out
+
+
+def stamp_batches(data: np.ndarray, positions, payload_lens, next_offset: int = 0, flags: int = 3) -> np.ndarray:
+    """Oracle of the write side (rpgpu_stamp): a stamped copy of `data`
+    (disk_log_appender::operator() + reset_size_checksum_metadata, in batch
+    order; flags 1 = offsets, 2 = size + crc; header_crc always)."""
+    out = np.array(data, dtype=np.uint8, copy=True)
+    pos = np.ascontiguousarray(np.asarray(positions, dtype=np.uint64))
+    pl = np.ascontiguousarray(np.asarray(payload_lens, dtype=np.uint32))
+    lib().rpo_stamp_batches(out.ctypes.data, pos.ctypes.data, pl.ctypes.data, len(pos), next_offset, flags)
     return out

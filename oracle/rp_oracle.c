@@ -1305,3 +1305,33 @@ int rpo_segment_index(const rpgpu_batch_result* batches, uint64_t batch_cap,
     }
     return 0;
 }
+
+/* ======================================================================== */
+/* Write side, in batch order, in place:            */
+/*   RPO_STAMP_OFFSETS: disk_log_appender::operator()                        */
+/*     (storage/disk_log_appender.cc:72-74): base_offset = _idx, then         */
+/*     _idx = last_offset + 1 (:113-119);                                     */
+/*   RPO_STAMP_CRC: storage::internal::reset_size_checksum_metadata          */
+/*     (storage/parser_utils.cc:114-120): size_bytes = 61 + payload,          */
+/*     crc = crc_record_batch(hdr, payload);                                  */
+/*   then header_crc = internal_header_only_crc (model/record_utils.cc:34-55).*/
+/* ======================================================================== */
+void rpo_stamp_batches(uint8_t* data, const uint64_t* pos, const uint32_t* plen, uint32_t n, int64_t next_offset,
+                       uint32_t flags) {
+    int64_t idx = next_offset;
+    for (uint32_t i = 0; i < n; i++) {
+        uint8_t* p = data + pos[i];
+        rpo_header h;
+        rpo_header_from_disk(p, &h);
+        if (flags & 1u) {
+            h.base_offset = idx;
+            idx = (int64_t)((uint64_t)h.base_offset + (uint64_t)(int64_t)h.last_offset_delta + 1u);
+        }
+        if (flags & 2u) {
+            h.size_bytes = (int32_t)(RPGPU_HEADER_SIZE + plen[i]);
+            h.crc = (int32_t)rpo_crc_record_batch(&h, p + RPGPU_HEADER_SIZE, plen[i]);
+        }
+        h.header_crc = rpo_internal_header_only_crc(&h);
+        rpo_header_to_disk(&h, p);
+    }
+}

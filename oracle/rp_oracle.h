@@ -155,6 +155,11 @@ int rpo_segment_index(const rpgpu_batch_result* batches, uint64_t batch_cap,
                       rpgpu_index_state* states, uint32_t* rel_offset, uint32_t* rel_time,
                       uint64_t* position);
 
+/* Write side: header stamping in batch order (flags: 1 offsets, 2 size+crc;
+ * header_crc always), see rp_oracle.c */
+void rpo_stamp_batches(uint8_t* data, const uint64_t* pos, const uint32_t* plen, uint32_t n, int64_t next_offset,
+                       uint32_t flags);
+
 #ifdef __cplusplus
 }
 #endif

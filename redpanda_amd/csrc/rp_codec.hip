@@ -42,6 +42,7 @@ __device__ unsigned long long g_dst[64];
 namespace rp {
 
 typedef __attribute__((address_space(1))) uint8_t g_u8;
+typedef __attribute__((address_space(3))) uint8_t lds_u8;
 
 // 16 bytes at any byte address (one global_load_dwordx4)
 DEV uint4 gld16(const uint8_t* p) {
@@ -58,6 +59,10 @@ struct Src {
     const uint8_t* p;  // stream start
     int64_t n;         // stream bytes
     int64_t rl;        // bytes readable from p (to the end of the job's data): 16-byte loads stay below
+    // optional LDS copy of stream bytes [wlo, whi) (k_lz_walk's staged walk of
+    // long pieces): 16-byte reads inside it come from LDS
+    const lds_u8* win = nullptr;
+    int64_t wlo = 0, whi = 0;
 };
 struct Dst {
     uint8_t* p;        // output position 0 of this unit
@@ -73,6 +78,15 @@ DEV uint32_t le32(const Src& s, int64_t i) { return le16(s, i) | (le16(s, i + 2)
 
 // 16 stream bytes from i; bytes past the job's data read as zero
 DEV uint4 ld16(const Src& s, int64_t i) {
+    if (s.win && i >= s.wlo && i + 16 <= s.whi) {
+        // five aligned dwords (the window has 16 spare bytes), then funnel shifts
+        typedef __attribute__((address_space(3))) const uint32_t lds_cu32;
+        const uint32_t o = (uint32_t)(i - s.wlo);
+        lds_cu32* w = (lds_cu32*)s.win + (o >> 2);
+        const uint32_t d0 = w[0], d1 = w[1], d2 = w[2], d3 = w[3], d4 = w[4], sh = o & 3;
+        return make_uint4(__builtin_amdgcn_alignbyte(d1, d0, sh), __builtin_amdgcn_alignbyte(d2, d1, sh),
+                          __builtin_amdgcn_alignbyte(d3, d2, sh), __builtin_amdgcn_alignbyte(d4, d3, sh));
+    }
     if (i + 16 <= s.rl) return gld16(s.p + i);
     uint32_t w0 = 0, w1 = 0, w2 = 0, w3 = 0;
 #pragma unroll
@@ -256,6 +270,68 @@ __device__ __attribute__((noinline)) uint32_t xxh32_lane(const uint8_t* p, uint6
     return h;
 }
 
+// XXH32 of n bytes at p by one wave.  The wave streams the input in 1 KiB
+// rows (coalesced, the next row in flight) through an LDS buffer; lanes 0..3
+// run the four accumulators, lane k folding dword k of each 16-byte stripe
+// (ds_read_b32, issued ahead of the serial rounds), so the serial chain is
+// plain VALU.  (A scalar-unit version, one readlane per dword, serialised
+// on the CU's one scalar unit across waves.)  lz4 1.9.3 xxhash.c XXH32.
+DEV uint32_t xxh32_wave(const uint8_t* p, uint64_t n, uint32_t seed, lds_u8* buf) {
+    typedef __attribute__((address_space(3))) uint32_t lds_u32;
+    const uint32_t P1 = 0x9E3779B1u, P2 = 0x85EBCA77u, P3 = 0xC2B2AE3Du, P4 = 0x27D4EB2Fu, P5 = 0x165667B1u;
+    const uint32_t l = lane();
+    const uint64_t ns = n >> 4;  // whole stripes
+    uint32_t h;
+    if (ns) {
+        uint32_t acc = l == 0 ? seed + P1 + P2 : l == 1 ? seed + P2 : l == 2 ? seed : seed - P1;
+        uint4 q = l < ns ? gld16(p + 16 * (uint64_t)l) : make_uint4(0, 0, 0, 0);
+        lds_u32* w = (lds_u32*)buf;
+        for (uint64_t r = 0; r < ns; r += 64) {
+            const uint64_t k = r + 64 + l;
+            const uint4 nq = k < ns ? gld16(p + 16 * k) : make_uint4(0, 0, 0, 0);
+            w[4 * l] = q.x;
+            w[4 * l + 1] = q.y;
+            w[4 * l + 2] = q.z;
+            w[4 * l + 3] = q.w;
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            const uint32_t cnt = ns - r < 64 ? (uint32_t)(ns - r) : 64u;
+            if (l < 4) {
+                uint32_t i = 0;
+                for (; i + 8 <= cnt; i += 8) {
+                    uint32_t x[8];
+#pragma unroll
+                    for (int u = 0; u < 8; u++) x[u] = w[4 * (i + u) + l];
+#pragma unroll
+                    for (int u = 0; u < 8; u++) acc = rotl32(acc + x[u] * P2, 13) * P1;
+                }
+                for (; i < cnt; i++) acc = rotl32(acc + w[4 * i + l] * P2, 13) * P1;
+            }
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            q = nq;
+        }
+        h = rotl32(rl(acc, 0), 1) + rotl32(rl(acc, 1), 7) + rotl32(rl(acc, 2), 12) + rotl32(rl(acc, 3), 18);
+    } else {
+        h = seed + P5;
+    }
+    h += (uint32_t)n;
+    // the last < 16 bytes: lane k holds byte k
+    uint64_t i = ns << 4;
+    const uint32_t t = (uint32_t)(n - i);
+    const uint32_t b = l < t ? (uint32_t)p[i + l] : 0u;
+    uint32_t k = 0;
+    for (; k + 4 <= t; k += 4) {
+        const uint32_t wd = rl(b, (int)k) | (rl(b, (int)k + 1) << 8) | (rl(b, (int)k + 2) << 16) | (rl(b, (int)k + 3) << 24);
+        h = rotl32(h + wd * P3, 17) * P4;
+    }
+    for (; k < t; k++) h = rotl32(h + rl(b, (int)k) * P5, 11) * P1;
+    h ^= h >> 15;
+    h *= P2;
+    h ^= h >> 13;
+    h *= P3;
+    h ^= h >> 16;
+    return h;
+}
+
 // ---------------------------------------------------------------------------
 // LZ4 block: rpo_lz4_block_decode (oracle) = lz4 1.9.3 LZ4_decompress_generic
 // for LZ4_decompress_safe_usingDict (fast loop + safe loop, every check).
@@ -280,27 +356,42 @@ struct PState {
     uint32_t safe;     // lz4: in the safe loop
 };
 
-// the input window: 16 stream bytes from wb, reloaded (one unaligned
-// 16-byte load) only when a read falls outside it; an LZ4 sequence of
-// short lengths spans 3-4 bytes, so one load serves several
+// the input window: 32 stream bytes from wb (two 16-byte loads issued
+// together), reloaded only when a read falls outside it; an LZ4 sequence of
+// short lengths spans 3-4 bytes, so one load round trip serves several
+// one 16-byte load per window (a 32-byte window, two loads, measured slower:
+// C2 walk 16.4 vs 13.8 ms, more VGPRs and fewer resident waves)
+#ifdef RPGPU_WIN32
+constexpr int32_t kWinSpan = 32;
+#else
+constexpr int32_t kWinSpan = 16;
+#endif
 struct Win {
-    uint4 w;
+    uint4 w, x;  // bytes [wb, wb + 16), [wb + 16, wb + 32)
     int32_t wb;
 };
+DEV void win_init(Win& W, const Src& s, int32_t p) {
+    W.w = ld16(s, p);
+    W.x = kWinSpan > 16 ? ld16(s, (int64_t)p + 16) : make_uint4(0, 0, 0, 0);
+    W.wb = p;
+}
 DEV void win_need(Win& W, const Src& s, int32_t p, int32_t nbytes) {
-    if (p < W.wb || p + nbytes > W.wb + 16) {
-        W.w = ld16(s, p);
-        W.wb = p;
-    }
+    if (p < W.wb || p + nbytes > W.wb + kWinSpan) win_init(W, s, p);
+}
+// dword i (0..7) of the window; 0 past it
+DEV uint32_t win_dw(const Win& W, uint32_t i) { return i < 4 ? dw(W.w, i) : dw(W.x, i - 4); }
+DEV uint32_t win_at32(const Win& W, uint32_t k) {
+    const uint32_t i = k >> 2;
+    return __builtin_amdgcn_alignbyte(win_dw(W, i + 1), win_dw(W, i), k & 3);
 }
 DEV uint32_t win_byte(Win& W, const Src& s, int32_t p) {
     win_need(W, s, p, 1);
     const uint32_t k = (uint32_t)(p - W.wb);
-    return (dw(W.w, k >> 2) >> (8 * (k & 3))) & 0xFFu;
+    return (win_dw(W, k >> 2) >> (8 * (k & 3))) & 0xFFu;
 }
 DEV uint32_t win_le16(Win& W, const Src& s, int32_t p) {
     win_need(W, s, p, 2);
-    return at32(W.w, (uint32_t)(p - W.wb)) & 0xFFFFu;
+    return win_at32(W, (uint32_t)(p - W.wb)) & 0xFFFFu;
 }
 
 DEV int32_t lz_read_var(Win& W, const Src& s, int32_t& ip, int32_t lencheck, bool loop_check, bool initial_check, int& err) {
@@ -357,8 +448,9 @@ struct RecSink {
     }
 };
 
+// stop_ip: suspend (st stays 0) before a sequence starting at or past it
 template <class Sink>
-DEV void lz4_run(const Src& s, int32_t oend, int32_t H, PState& ps, Sink& sink) {
+DEV void lz4_run(const Src& s, int32_t oend, int32_t H, PState& ps, Sink& sink, int32_t stop_ip = INT32_MAX) {
     if (ps.st) return;
     const int32_t iend = (int32_t)s.n;
     const int32_t shortiend = iend - 14 - 2, shortoend = oend - 14 - 18;
@@ -366,14 +458,20 @@ DEV void lz4_run(const Src& s, int32_t oend, int32_t H, PState& ps, Sink& sink) 
     int err;
     bool last = false, safe = ps.safe != 0;
     Win W;
-    W.w = ld16(s, ip);
-    W.wb = ip;
+    win_init(W, s, ip);
 #define LZ_FAIL() do { ps.st = -1; return; } while (0)
     // The two loops of LZ4_decompress_generic as one: `safe` is the safe
     // loop (entered for good at the first fast-loop exit); every path ends at
     // `emit` with the sequence's literal (lip, llen; op already past it) and
     // match (offset, ml).
     for (;;) {
+        if (ip >= stop_ip) {
+            ps.ip = ip;
+            ps.op = op;
+            ps.need = need;
+            ps.safe = safe;
+            return;
+        }
         const uint32_t token = win_byte(W, s, ip);
         ip++;
         length = (int32_t)(token >> 4);
@@ -663,14 +761,18 @@ DEV void snappy_begin(PState& ps, const Src& s, bool whole) {
 }
 
 template <class Sink>
-DEV void snappy_run(const Src& s, PState& ps, Sink& sink) {
+DEV void snappy_run(const Src& s, PState& ps, Sink& sink, int32_t stop_ip = INT32_MAX) {
     if (ps.st) return;
     const int64_t n = s.n, ulen = ps.ulen;
     int64_t ip = ps.ip, op = ps.op;
     Win W;
-    W.w = ld16(s, ip);
-    W.wb = (int32_t)ip;
+    win_init(W, s, (int32_t)ip);
     while (ip < n) {
+        if (ip >= stop_ip) {
+            ps.ip = (int32_t)ip;
+            ps.op = (int32_t)op;
+            return;
+        }
         const uint32_t c = win_byte(W, s, (int32_t)ip);
         const uint32_t t = c & 3;
         const int64_t extra = t == 0 ? (((c >> 2) >= 60) ? (int64_t)((c >> 2) - 59) : 0) : t == 1 ? 1 : t == 2 ? 2 : 4;
@@ -678,7 +780,7 @@ DEV void snappy_run(const Src& s, PState& ps, Sink& sink) {
         uint32_t x = 0;  // the tag's extra bytes (at most 4)
         if (extra) {
             win_need(W, s, (int32_t)ip + 1, (int32_t)extra);
-            x = at32(W.w, (uint32_t)(ip + 1 - W.wb));
+            x = win_at32(W, (uint32_t)(ip + 1 - W.wb));
         }
         bool go;
         if (t == 0) {
@@ -832,14 +934,15 @@ DEV int in_varint(In& in, int64_t pos, int64_t n, uint32_t& v) {
     return -1;
 }
 
-// Wave-uniform atomic fetch-add of `v` (lane 0's contribution; the other
-// lanes add 0).  Every lane executes the atomic: written as
-// `if (lane() == 0) x = atomicAdd(..)` followed by readfirstlane, the
-// compiler's divergence analysis took the claimed value for a per-lane one
-// and built a claim loop with a per-lane exit whose lanes never all left
-// (the round-2 wave decoder did not terminate).
-DEV uint32_t wave_fetch_add(uint32_t* p, uint32_t v) {
-    return uni32(atomicAdd(p, lane() == 0 ? v : 0u));
+
+DEV bool piece_is_long(uint32_t kind, uint32_t csize) {
+    return !(kind & kBlkRaw) && ((kind & kBlkWhole) || csize > 65536u);
+}
+
+// a long piece (walked by a wave in k_lz_walk): lane 0 appends it
+DEV void note_long(const DeviceJob& j, uint32_t idx) {
+    const uint32_t at = atomicAdd(&j.counters[11], 1u);
+    j.long_list[at] = idx;
 }
 
 // reserve `nb` items (wave-uniform); UINT32_MAX when the list is full
@@ -907,6 +1010,7 @@ DEV bool plan_lz4f(const DeviceJob& j, In& in, int64_t n, uint64_t src_abs, uint
             it.out = -1;
             it.cap = raw ? (uint32_t)bsz : (uint32_t)bmax;
             j.blocks[first + k] = it;
+            if (piece_is_long(it.kind, it.csize)) note_long(j, first + k);
         }
         plan += raw ? (uint64_t)bsz : (uint64_t)bmax;
         pos += 4 + bsz + (bcs ? 4 : 0);
@@ -967,6 +1071,7 @@ DEV bool plan_snappy_java(const DeviceJob& j, In& in, int64_t n, uint64_t src_ab
             it.out = -1;
             it.cap = ulen;
             j.blocks[first + k] = it;
+            if (piece_is_long(it.kind, it.csize)) note_long(j, first + k);
         }
         plan += ulen;
         pos += clen;
@@ -996,6 +1101,7 @@ DEV bool plan_snappy_whole(const DeviceJob& j, int64_t n, uint64_t src_abs, uint
         it.out = -1;
         it.cap = (uint32_t)cap;
         j.blocks[first] = it;
+        note_long(j, first);
     }
     fp.mode = 2;
     fp.first = first;
@@ -1074,7 +1180,6 @@ __global__ __launch_bounds__(256) void k_decode(DeviceJob j) {
 //   * Raw blocks are plain 16-byte-per-lane copies (through the ring in a
 //     linked frame, whose later blocks may copy from them).
 // ---------------------------------------------------------------------------
-typedef __attribute__((address_space(3))) uint8_t lds_u8;
 // The ring is small so that many waves share a CU: the execution is a chain
 // of LDS and load latencies per wave, and throughput scales with the waves
 // resident (16 KiB: 10 per CU; the 64 KiB ring of the first wave engine
@@ -1107,6 +1212,10 @@ struct XRing {
     uint32_t flushed;       // positions below are stored to dst
     bool linked;            // positions may pass the ring size (the ring wraps)
     bool hist;              // later pieces copy from this output (a linked frame): raw pieces go through the ring
+    bool fpend;             // flush stores issued since the last full wait
+    uint32_t safe;          // positions below are stored and the stores complete
+    const __attribute__((address_space(3))) uint32_t* pat;  // kPat.a then kPat.b in LDS (a constant-memory
+                                                          // load per short-offset match waited on HBM latency)
     __amdgpu_buffer_rsrc_t rs;  // dst window for far read-backs (linked)
 };
 
@@ -1166,6 +1275,7 @@ DEV void xflush(XRing& x, uint32_t upto) {
         }
     }
     x.flushed = upto;
+    x.fpend = true;
 }
 DEV void xflush_chunks(XRing& x) { xflush(x, x.op & ~1023u); }
 
@@ -1201,7 +1311,9 @@ DEV void xmatch(XRing& x, uint32_t d, uint32_t off, uint32_t ml, bool far) {
     uint32_t step = 16;
     if (off) {
         const uint4 v = xld16(x.r, s);  // bytes [s, s + off) are the pattern
-        const uint4 sa = *(const uint4*)&kPat.a[off][0], sb = *(const uint4*)&kPat.b[off][0];
+        const uint4 sa = make_uint4(x.pat[4 * off], x.pat[4 * off + 1], x.pat[4 * off + 2], x.pat[4 * off + 3]);
+        const uint4 sb = make_uint4(x.pat[64 + 4 * off], x.pat[64 + 4 * off + 1], x.pat[64 + 4 * off + 2],
+                                    x.pat[64 + 4 * off + 3]);
         p.x = __builtin_amdgcn_perm(v.y, v.x, sa.x) | __builtin_amdgcn_perm(v.w, v.z, sb.x);
         p.y = __builtin_amdgcn_perm(v.y, v.x, sa.y) | __builtin_amdgcn_perm(v.w, v.z, sb.y);
         p.z = __builtin_amdgcn_perm(v.y, v.x, sa.z) | __builtin_amdgcn_perm(v.w, v.z, sb.z);
@@ -1211,9 +1323,22 @@ DEV void xmatch(XRing& x, uint32_t d, uint32_t off, uint32_t ml, bool far) {
     for (uint32_t c = 0; c < ml; c += step) xst(x.r, d + c, p, ml - c < 16 ? ml - c : 16);
 }
 
-// the records of lanes [lo, hi) (none longer than kBig); lit0 = the first
-// 16 bytes of each lane's literal (loaded a window ahead)
-DEV void xbatch(XRing& x, const Src& s, const SeqRec& r, uint32_t lo, uint32_t hi_lane, const uint4& lit0) {
+// a lane's literal bytes (up to kBig), loaded a window ahead of its batch:
+// every load of a batch is then in flight before the batch starts
+struct Lit {
+    uint4 v[kBig / 16];
+};
+DEV Lit lit_load(const Src& s, const SeqRec& r) {
+    Lit L;
+#pragma unroll
+    for (uint32_t k = 0; k < kBig / 16; k++)
+        L.v[k] = (r.ll > 16 * k && r.ll <= kBig) ? ld16(s, (int64_t)r.lip + 16 * k) : make_uint4(0, 0, 0, 0);
+    return L;
+}
+
+// the records of lanes [lo, hi) (none longer than kBig); lit = each lane's
+// literal bytes (loaded a window ahead)
+DEV void xbatch(XRing& x, const Src& s, const SeqRec& r, uint32_t lo, uint32_t hi_lane, const Lit& lit) {
     const uint32_t l = lane();
 #ifdef RPGPU_DSTAMPS
     const uint64_t c0 = __builtin_amdgcn_s_memtime();
@@ -1227,9 +1352,9 @@ DEV void xbatch(XRing& x, const Src& s, const SeqRec& r, uint32_t lo, uint32_t h
     const uint32_t o = x.op + incl - len;
     const uint32_t hi = x.op + rl(incl, (int)hi_lane - 1);
     if (v && r.ll) {
-        xst(x.r, o, lit0, r.ll < 16 ? r.ll : 16);
-        for (uint32_t c = 16; c < r.ll; c += 16)
-            xst(x.r, o + c, ld16(s, (int64_t)r.lip + c), r.ll - c < 16 ? r.ll - c : 16);
+#pragma unroll
+        for (uint32_t k = 0; k < kBig / 16; k++)
+            if (r.ll > 16 * k) xst(x.r, o + 16 * k, lit.v[k], r.ll - 16 * k < 16 ? r.ll - 16 * k : 16);
     }
     const uint32_t d = o + r.ll, src = d - r.off;
     bool pend = v && r.ml > 0;
@@ -1239,7 +1364,13 @@ DEV void xbatch(XRing& x, const Src& s, const SeqRec& r, uint32_t lo, uint32_t h
 #endif
     // sources before (batch end - 64 KiB): their ring slots may be rewritten by this batch
     const bool far = x.linked && pend && hi > kXRing && src < hi - kXRing;
-    if (__ballot(far)) wait_vm();
+    // a far source was stored by an earlier flush: wait only while a flush
+    // may still be in flight (a wait drains every earlier memory op)
+    if (__ballot(far && src + r.ml > x.safe) && x.fpend) {
+        wait_vm();
+        x.fpend = false;
+        x.safe = x.flushed;
+    }
     for (;;) {
         const uint64_t pm = __ballot(pend);
         if (!pm) break;
@@ -1289,7 +1420,11 @@ DEV void xbig(XRing& x, const Src& s, uint32_t lip, uint32_t ll, uint32_t ml, ui
         // as the ring may no longer hold them
         const bool far = x.linked && off > kXRing - 1024;
         for (uint32_t c = 0; c < 64 * ((ml + 63) / 64); c += 64) {
-            if (far) wait_vm();
+            if (far && x.fpend && sp + c + 64 > x.safe) {
+                wait_vm();
+                x.fpend = false;
+                x.safe = x.flushed;
+            }
             uint32_t v = 0;
             if (off && c + l < ml)
                 v = far ? __builtin_amdgcn_raw_buffer_load_b8(x.rs, sp + c + l, 0, kSc1) : (uint32_t)x.r[(sp + c + l) & kXM];
@@ -1319,9 +1454,6 @@ DEV SeqRec rec_at(const SeqRec* recs, uint32_t k, uint32_t cnt) {
     if (k < cnt) r = recs[k];
     return r;
 }
-DEV uint4 lit_head(const Src& s, const SeqRec& r) {
-    return (r.ll && r.ll <= kBig) ? ld16(s, (int64_t)r.lip) : make_uint4(0, 0, 0, 0);
-}
 
 // records [0, cnt) in windows of 64 (lane k = record 64 w + k): records are
 // loaded two windows ahead and literal heads one window ahead, so the
@@ -1330,10 +1462,17 @@ DEV uint4 lit_head(const Src& s, const SeqRec& r) {
 DEV void xrecords(XRing& x, const Src& s, const SeqRec* recs, uint32_t cnt) {
     const uint32_t l = lane();
     SeqRec r0 = rec_at(recs, l, cnt), r1 = rec_at(recs, 64 + l, cnt);
-    uint4 lit0 = lit_head(s, r0);
+    Lit lit0 = lit_load(s, r0);
+    // vmcnt drains in issue order: once a batch has waited for its records
+    // (loaded two windows back), every flush issued before that load is
+    // complete, so far matches below that flush position need no wait
+    uint32_t fh0 = x.safe, fh1 = x.safe;
     for (uint32_t b = 0; b < cnt; b += 64) {
+        x.safe = fh1 > x.safe ? fh1 : x.safe;
+        fh1 = fh0;
+        fh0 = x.flushed;
         const SeqRec r2 = rec_at(recs, b + 128 + l, cnt);
-        const uint4 lit1 = lit_head(s, r1);
+        const Lit lit1 = lit_load(s, r1);
         const uint32_t n = cnt - b < 64 ? cnt - b : 64;
         const uint64_t bigm = __ballot(l < n && (r0.ll > kBig || r0.ml > kBig));
         uint32_t lo = 0;
@@ -1379,8 +1518,9 @@ struct Piece {
     uint32_t kind, cap;
 };
 
-// a piece's stream, block checksum and walk start (per lane)
-DEV void piece_begin(Piece& pc, const DeviceJob& j, const BlockItem& it) {
+// a piece's stream, block checksum and walk start (per lane; wave: the whole
+// wave works on this one piece and hashes the checksum together)
+DEV void piece_begin(Piece& pc, const DeviceJob& j, const BlockItem& it, lds_u8* xbuf = nullptr) {
     const uint64_t n = it.csize;
     pc.s = Src{j.data + it.src, (int64_t)n, (int64_t)(j.data_len - it.src)};
     pc.kind = it.kind;
@@ -1389,7 +1529,8 @@ DEV void piece_begin(Piece& pc, const DeviceJob& j, const BlockItem& it) {
     pc.ps.ulen = 0;
     pc.ps.safe = 0;
     pc.ps.st = 0;
-    if ((it.kind & kBlkChecksum) && le32(Src{pc.s.p, (int64_t)n + 4, pc.s.rl}, (int64_t)n) != xxh32_lane(pc.s.p, n, 0)) {
+    if ((it.kind & kBlkChecksum) &&
+        le32(Src{pc.s.p, (int64_t)n + 4, pc.s.rl}, (int64_t)n) != (xbuf ? xxh32_wave(pc.s.p, n, 0, xbuf) : xxh32_lane(pc.s.p, n, 0))) {
         pc.ps.st = -1;  // block checksum mismatch (LZ4F_decompress, checked before the block decodes)
         return;
     }
@@ -1403,56 +1544,142 @@ DEV void piece_begin(Piece& pc, const DeviceJob& j, const BlockItem& it) {
 }
 
 template <class Sink>
-DEV void piece_run(const Src& s, uint32_t kind, uint32_t cap, PState& ps, Sink& sink) {
-    if (kind & kBlkSnappy) snappy_run(s, ps, sink);
-    else lz4_run(s, (int32_t)cap, 65536, ps, sink);  // H = 64 KiB: the history check is `need` (see lz4_run)
+DEV void piece_run(const Src& s, uint32_t kind, uint32_t cap, PState& ps, Sink& sink, int32_t stop_ip = INT32_MAX) {
+    if (kind & kBlkSnappy) snappy_run(s, ps, sink, stop_ip);
+    else lz4_run(s, (int32_t)cap, 65536, ps, sink, stop_ip);  // H = 64 KiB: the history check is `need` (see lz4_run)
 }
 
 // records into slabs of the pool; false (suspend) once the pool is exhausted
+// records into slabs of the pool; false (suspend) once the pool is
+// exhausted.  Records are stored four at a time (64 contiguous bytes, one
+// store burst per line half): a lane storing one 16-byte record per
+// sequence left the L2 with partial lines of some 300 M scattered records.
 struct SlabSink {
     SeqRec* pool;
     uint32_t* slab_next;
     uint32_t* cursor;
     uint32_t pool_slabs;
     uint32_t slab, pos, n;
+    uint32_t cut;      // the pool ran out: the walk was suspended for good
+    uint4 r0, r1, r2;  // records (pos & ~3) .. pos - 1, not stored yet
     DEV bool seq(const uint4&, int32_t, int32_t lip, int32_t llen, int32_t, uint32_t off, int32_t ml) {
-        pool[(size_t)slab * kSlabRecs + pos] = SeqRec{(uint32_t)lip, (uint32_t)llen, (uint32_t)ml, off};
+#ifdef RPGPU_EXP_NOREC
+        // diagnostic: the walk without its record stores (nothing to execute)
+        n++;
+        return true;
+#endif
+        const uint4 r = make_uint4((uint32_t)lip, (uint32_t)llen, (uint32_t)ml, off);
+        const uint32_t k = pos & 3;
+        if (k == 3) {
+            uint4* q = (uint4*)(pool + (size_t)slab * kSlabRecs + pos - 3);
+            q[0] = r0;
+            q[1] = r1;
+            q[2] = r2;
+            q[3] = r;
+        } else if (k == 0) {
+            r0 = r;
+        } else if (k == 1) {
+            r1 = r;
+        } else {
+            r2 = r;
+        }
         n++;
         if (++pos < kSlabRecs) return true;
         const uint32_t ns = atomicAdd(cursor, 1u);
-        if (ns >= pool_slabs) return false;
+        if (ns >= pool_slabs) {
+            cut = 1;
+            return false;
+        }
         slab_next[slab] = ns;
         slab = ns;
         pos = 0;
         return true;
     }
+    // store the records still held (when the walk returns)
+    DEV void finish() {
+#ifdef RPGPU_EXP_NOREC
+        n = 0;
+        return;
+#endif
+        const uint32_t k = pos & 3;
+        uint4* q = (uint4*)(pool + (size_t)slab * kSlabRecs + (pos - k));
+        if (k > 0) q[0] = r0;
+        if (k > 1) q[1] = r1;
+        if (k > 2) q[2] = r2;
+    }
 };
 
 // ---------------------------------------------------------------------------
-// k_lz_walk: one lane per piece (every planned BlockItem, linked or not),
-// taken off counters[10]: block checksum, then the walk into slab records.
-// High occupancy: the walk is a chain of dependent loads per lane.
+// k_lz_walk: every planned BlockItem (linked or not) is walked into slab
+// records.  Long pieces (a raw snappy payload, an LZ4 block above 64 KiB
+// compressed: one serial chain of up to ~10^5 sequences) go first, one WAVE
+// each: the wave stages 4 KiB of the stream at a time in LDS (16 bytes per
+// lane per load, one memory latency per window) and lane 0 walks it from
+// there, where a lane walking the stream in HBM waits a memory latency per
+// sequence.  Then one LANE per remaining piece, taken off counters[10]:
+// block checksum, then the walk.  High occupancy: the lane walk is a chain
+// of dependent loads per lane.
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_lz_walk(DeviceJob j) {
-    const uint32_t reserved = j.counters[4];
-    const uint32_t nblk = reserved < j.block_capacity ? reserved : j.block_capacity;
-    for (;;) {
-        const uint32_t p = atomicAdd(&j.counters[10], 1u);
-        if (p >= nblk) break;
-        Piece pc;
-        piece_begin(pc, j, j.blocks[p]);
-        PieceState out;
-        out.nrec = 0;
-        out.first_slab = 0xFFFFFFFFu;
-        if (pc.ps.st == 0) {
-            const uint32_t fs = atomicAdd(&j.counters[9], 1u);
-            if (fs < j.pool_slabs) {
-                out.first_slab = fs;
-                SlabSink sink{j.pool, j.slab_next, &j.counters[9], j.pool_slabs, fs, 0, 0};
-                piece_run(pc.s, pc.kind, pc.cap, pc.ps, sink);
-                out.nrec = sink.n;
+constexpr uint32_t kWalkWin = 4096;  // staged stream bytes per wave (long pieces)
+
+
+DEV void walk_long(const DeviceJob& j, uint32_t p, lds_u8* win) {
+    const uint32_t l = lane();
+#ifdef RPGPU_DSTAMPS
+    const uint64_t t0 = wall_clock64();
+#endif
+    BlockItem it;
+    it.src = uni64(j.blocks[p].src);
+    it.dst = 0;
+    it.csize = uni32(j.blocks[p].csize);
+    it.kind = uni32(j.blocks[p].kind);
+    it.out = -1;
+    it.cap = uni32(j.blocks[p].cap);
+    Piece pc;
+    piece_begin(pc, j, it, win);  // (the window buffer hashes the block checksum first)
+    PieceState out;
+    out.nrec = 0;
+    out.first_slab = 0xFFFFFFFFu;
+    if (pc.ps.st == 0) {
+        const uint32_t fs = wave_fetch_add(&j.counters[9], 1u);
+        if (fs < j.pool_slabs) {
+            out.first_slab = fs;
+            SlabSink sink{j.pool, j.slab_next, &j.counters[9], j.pool_slabs, fs, 0, 0, 0, {}, {}, {}};
+            const int64_t n = pc.s.n;
+            for (;;) {
+                // stage [w0, w0 + 4 KiB) of the stream (w0 16-aligned below ip)
+                const int64_t w0 = (int64_t)pc.ps.ip & ~15ll;
+#pragma unroll
+                for (uint32_t k = 0; k < kWalkWin / 1024; k++) {
+                    const int64_t at = w0 + 1024 * k + 16 * l;
+                    const uint4 v = ld16(pc.s, at);
+                    __builtin_memcpy(win + 1024 * k + 16 * l, &v, 16);
+                }
+                asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+                Src ws = pc.s;
+                ws.win = win;
+                ws.wlo = w0;
+                ws.whi = w0 + kWalkWin;
+                // suspend before a sequence within 32 bytes of the window end
+                const int32_t stop = w0 + kWalkWin < n ? (int32_t)(w0 + kWalkWin - 32) : INT32_MAX;
+                if (l == 0) piece_run(ws, pc.kind, pc.cap, pc.ps, sink, stop);
+                // lane 0's walk state to every lane
+                pc.ps.ip = (int32_t)rl((uint32_t)pc.ps.ip, 0);
+                pc.ps.op = (int32_t)rl((uint32_t)pc.ps.op, 0);
+                pc.ps.need = (int32_t)rl((uint32_t)pc.ps.need, 0);
+                pc.ps.st = (int32_t)rl((uint32_t)pc.ps.st, 0);
+                pc.ps.safe = rl(pc.ps.safe, 0);
+                sink.slab = rl(sink.slab, 0);
+                sink.pos = rl(sink.pos, 0);
+                sink.n = rl(sink.n, 0);
+                sink.cut = rl(sink.cut, 0);
+                if (pc.ps.st != 0 || sink.cut) break;
             }
+            if (l == 0) sink.finish();
+            out.nrec = sink.n;
         }
+    }
+    if (l == 0) {
         out.ip = pc.ps.ip;
         out.op = pc.ps.op;
         out.need = pc.ps.need;
@@ -1460,6 +1687,103 @@ __global__ __launch_bounds__(256) void k_lz_walk(DeviceJob j) {
         out.ulen = pc.ps.ulen;
         out.safe = pc.ps.safe;
         j.pstate[p] = out;
+#ifdef RPGPU_DSTAMPS
+        const uint64_t dt = wall_clock64() - t0;
+        atomicAdd(&g_dst[24], dt);
+        atomicAdd(&g_dst[25], 1ull);
+        if (dt > atomicMax(&g_dst[26], dt)) { g_dst[32] = out.nrec; g_dst[33] = it.csize; }
+#endif
+    }
+}
+
+// a piece's walk result to the job (one lane)
+DEV void put_pstate(const DeviceJob& j, uint32_t p, const PState& ps, uint32_t nrec, uint32_t first_slab) {
+    PieceState out;
+    out.ip = ps.ip;
+    out.op = ps.op;
+    out.need = ps.need;
+    out.st = ps.st;
+    out.ulen = ps.ulen;
+    out.safe = ps.safe;
+    out.nrec = nrec;
+    out.first_slab = first_slab;
+    j.pstate[p] = out;
+}
+
+// Lane walk in rounds.  Every round, each lane with a piece stages the 64
+// stream bytes at its parse position in its LDS slot (four 16-byte loads,
+// issued by all lanes together: one memory latency per round for the whole
+// wave), then walks as many sequences as start within the first 48 of them.
+// A lane walking straight from HBM made the whole wave wait a memory
+// latency at nearly every sequence (some lane always needed a new window),
+// ~4 us per sequence on C2's JSON blocks.
+constexpr uint32_t kLaneWin = 64, kLaneSlot = kLaneWin + 16;  // + the spare bytes ld16's window reads need
+
+__global__ __launch_bounds__(256) void k_lz_walk(DeviceJob j) {
+    constexpr uint32_t kWaveLds = 64 * kLaneSlot > kWalkWin + 16 ? 64 * kLaneSlot : kWalkWin + 16;
+    __shared__ __attribute__((aligned(16))) uint8_t wwin[4][kWaveLds];
+    const uint32_t reserved = j.counters[4];
+    const uint32_t nblk = reserved < j.block_capacity ? reserved : j.block_capacity;
+    const uint32_t nlong = j.counters[11];
+    lds_u8* wl = (lds_u8*)wwin[threadIdx.x >> 6];
+    for (;;) {
+        const uint32_t k = wave_fetch_add(&j.counters[12], 1u);
+        if (k >= nlong) break;
+        walk_long(j, uni32(j.long_list[k]), wl);
+    }
+    lds_u8* slot = wl + kLaneSlot * lane();
+    bool active = false, drained = false;
+    uint32_t p = 0, first_slab = 0;
+    Piece pc;
+    SlabSink sink{j.pool, j.slab_next, &j.counters[9], j.pool_slabs, 0, 0, 0, 0, {}, {}, {}};
+    for (;;) {
+        // lanes without a piece take the next one (pieces that end at their
+        // begin, raw ones or a failed block checksum, are written at once)
+        while (!active && !drained) {
+            p = atomicAdd(&j.counters[10], 1u);
+            if (p >= nblk) {
+                drained = true;
+                break;
+            }
+            const BlockItem it = j.blocks[p];
+            if (piece_is_long(it.kind, it.csize)) continue;  // walked above
+            piece_begin(pc, j, it);
+            first_slab = 0xFFFFFFFFu;
+            if (pc.ps.st == 0) {
+                const uint32_t fs = atomicAdd(&j.counters[9], 1u);
+                if (fs < j.pool_slabs) {
+                    first_slab = fs;
+                    sink.slab = fs;
+                    sink.pos = sink.n = sink.cut = 0;
+                    active = true;
+                    break;
+                }
+            }
+            put_pstate(j, p, pc.ps, 0, first_slab);
+        }
+        if (!__ballot(active)) break;
+        // stage the window
+        const int64_t wb = (int64_t)pc.ps.ip & ~15ll;
+        if (active) {
+            uint4 v[kLaneWin / 16];
+#pragma unroll
+            for (uint32_t k = 0; k < kLaneWin / 16; k++) v[k] = ld16(pc.s, wb + 16 * k);
+#pragma unroll
+            for (uint32_t k = 0; k < kLaneWin / 16; k++) __builtin_memcpy(slot + 16 * k, &v[k], 16);
+        }
+        if (active) {
+            Src ws = pc.s;
+            ws.win = slot;
+            ws.wlo = wb;
+            ws.whi = wb + kLaneWin;
+            const int32_t stop = wb + kLaneWin < pc.s.n ? (int32_t)(wb + kLaneWin - 16) : INT32_MAX;
+            piece_run(ws, pc.kind, pc.cap, pc.ps, sink, stop);
+            if (pc.ps.st != 0 || sink.cut) {
+                sink.finish();
+                put_pstate(j, p, pc.ps, sink.n, first_slab);
+                active = false;
+            }
+        }
     }
 }
 
@@ -1482,6 +1806,7 @@ DEV int32_t exec_piece(XRing& x, const DeviceJob& j, uint32_t p, uint32_t hist, 
             xcopy_raw(x.dst + x.op, s, csize);
             x.op += csize;
             x.flushed = x.op;
+            x.fpend = true;
         }
         return (int32_t)csize;
     }
@@ -1524,23 +1849,28 @@ DEV int32_t exec_piece(XRing& x, const DeviceJob& j, uint32_t p, uint32_t hist, 
     return (int32_t)(x.op - start);
 }
 
-DEV void xring_init(XRing& x, const DeviceJob& j, lds_u8* ring, uint64_t dst, bool linked, bool hist) {
+DEV void xring_init(XRing& x, const DeviceJob& j, lds_u8* ring, uint64_t dst, bool linked, bool hist,
+                    const __attribute__((address_space(3))) uint32_t* pat) {
     x.r = ring;
+    x.pat = pat;
     x.dst = j.decoded + dst;
     x.op = 0;
     x.flushed = 0;
     x.linked = linked;
     x.hist = hist;
+    x.fpend = false;
+    x.safe = 0;
     const uint64_t room = j.decoded_capacity - dst;
     x.rs = __builtin_amdgcn_make_buffer_rsrc(x.dst, 0, (int)(room < 0x7FFFFFFFull ? room : 0x7FFFFFFFull), kBufFlags);
 }
 
 // the blocks of one linked LZ4F frame, in order, one position space
-DEV void exec_linked(const DeviceJob& j, lds_u8* ring, SeqRec* buf, uint32_t item) {
+DEV void exec_linked(const DeviceJob& j, lds_u8* ring, SeqRec* buf, uint32_t item,
+                     const __attribute__((address_space(3))) uint32_t* pat) {
     const uint32_t first = uni32(j.plans[item].first), nb = uni32(j.plans[item].nb);
     const uint64_t fdst = uni64(j.dcap[uni32(j.decode_list[item])]);
     XRing x;
-    xring_init(x, j, ring, fdst, true, true);
+    xring_init(x, j, ring, fdst, true, true, pat);
 #ifdef RPGPU_DSTAMPS
     const uint64_t t1 = wall_clock64();
 #endif
@@ -1561,7 +1891,8 @@ DEV void exec_linked(const DeviceJob& j, lds_u8* ring, SeqRec* buf, uint32_t ite
 }
 
 // up to 64 consecutive block items (independent pieces; linked ones skipped)
-DEV void exec_chunk(const DeviceJob& j, lds_u8* ring, SeqRec* buf, uint32_t base, uint32_t nblk) {
+DEV void exec_chunk(const DeviceJob& j, lds_u8* ring, SeqRec* buf, uint32_t base, uint32_t nblk,
+                    const __attribute__((address_space(3))) uint32_t* pat) {
     const uint32_t end = base + 64 < nblk ? base + 64 : nblk;
     for (uint32_t p = base; p < end; p++) {
         const uint32_t kind = uni32(j.blocks[p].kind);
@@ -1569,7 +1900,7 @@ DEV void exec_chunk(const DeviceJob& j, lds_u8* ring, SeqRec* buf, uint32_t base
         const uint64_t dst = uni64(j.blocks[p].dst);
         XRing x;
         // a piece longer than the ring wraps it: wrap-aware like a linked frame
-        xring_init(x, j, ring, dst, uni32(j.blocks[p].cap) > kXRing, false);
+        xring_init(x, j, ring, dst, uni32(j.blocks[p].cap) > kXRing, false, pat);
 #ifdef RPGPU_DSTAMPS
         const uint64_t e0 = wall_clock64();
 #endif
@@ -1595,7 +1926,12 @@ DEV void exec_chunk(const DeviceJob& j, lds_u8* ring, SeqRec* buf, uint32_t base
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(64) void k_lz_exec(DeviceJob j) {
     extern __shared__ __attribute__((aligned(16))) uint8_t xlds[];
+    __shared__ uint32_t spat[128];
     lds_u8* ring = (lds_u8*)xlds;
+    spat[threadIdx.x] = (&kPat.a[0][0])[threadIdx.x];
+    spat[64 + threadIdx.x] = (&kPat.b[0][0])[threadIdx.x];
+    __syncthreads();
+    const __attribute__((address_space(3))) uint32_t* pat = (const __attribute__((address_space(3))) uint32_t*)spat;
     SeqRec* buf = j.seqs + (size_t)blockIdx.x * kRecsPerLane;
     const uint32_t nlink = j.counters[7];
     const uint32_t reserved = j.counters[4];
@@ -1604,8 +1940,8 @@ __global__ __launch_bounds__(64) void k_lz_exec(DeviceJob j) {
     for (;;) {
         const uint32_t u = wave_fetch_add(&j.counters[8], 1u);
         if (u >= total) break;
-        if (u < nlink) exec_linked(j, ring, buf, uni32(j.link_list[u]));
-        else exec_chunk(j, ring, buf, (u - nlink) * 64, nblk);
+        if (u < nlink) exec_linked(j, ring, buf, uni32(j.link_list[u]), pat);
+        else exec_chunk(j, ring, buf, (u - nlink) * 64, nblk, pat);
     }
 }
 
@@ -1637,63 +1973,20 @@ __global__ __launch_bounds__(256) void k_decode_blocks(DeviceJob j) {
     }
 }
 
-// XXH32 of n bytes at p by one wave: lane l loads stripe l of each 1 KiB row
-// (the next row in flight while this one is folded) and the four
-// accumulators run on the scalar unit, one readlane per stripe dword, so a
-// 1 MiB content checksum is ~2M scalar cycles instead of a one-lane walk of
-// dependent vector loads (lz4 1.9.3 xxhash.c XXH32, as xxh32_lane)
-DEV uint32_t xxh32_wave(const uint8_t* p, uint64_t n, uint32_t seed) {
-    const uint32_t P1 = 0x9E3779B1u, P2 = 0x85EBCA77u, P3 = 0xC2B2AE3Du, P4 = 0x27D4EB2Fu, P5 = 0x165667B1u;
-    const uint32_t l = lane();
-    const uint64_t ns = n >> 4;  // whole stripes
-    uint32_t h;
-    if (ns) {
-        uint32_t v1 = seed + P1 + P2, v2 = seed + P2, v3 = seed, v4 = seed - P1;
-        uint4 q = l < ns ? gld16(p + 16 * (uint64_t)l) : make_uint4(0, 0, 0, 0);
-        for (uint64_t r = 0; r < ns; r += 64) {
-            const uint64_t k = r + 64 + l;
-            const uint4 nq = k < ns ? gld16(p + 16 * k) : make_uint4(0, 0, 0, 0);
-            const uint32_t cnt = ns - r < 64 ? (uint32_t)(ns - r) : 64u;
-            for (uint32_t i = 0; i < cnt; i++) {
-                v1 = rotl32(v1 + rl(q.x, (int)i) * P2, 13) * P1;
-                v2 = rotl32(v2 + rl(q.y, (int)i) * P2, 13) * P1;
-                v3 = rotl32(v3 + rl(q.z, (int)i) * P2, 13) * P1;
-                v4 = rotl32(v4 + rl(q.w, (int)i) * P2, 13) * P1;
-            }
-            q = nq;
-        }
-        h = rotl32(v1, 1) + rotl32(v2, 7) + rotl32(v3, 12) + rotl32(v4, 18);
-    } else {
-        h = seed + P5;
-    }
-    h += (uint32_t)n;
-    // the last < 16 bytes: lane k holds byte k
-    uint64_t i = ns << 4;
-    const uint32_t t = (uint32_t)(n - i);
-    const uint32_t b = l < t ? (uint32_t)p[i + l] : 0u;
-    uint32_t k = 0;
-    for (; k + 4 <= t; k += 4) {
-        const uint32_t wd = rl(b, (int)k) | (rl(b, (int)k + 1) << 8) | (rl(b, (int)k + 2) << 16) | (rl(b, (int)k + 3) << 24);
-        h = rotl32(h + wd * P3, 17) * P4;
-    }
-    for (; k < t; k++) h = rotl32(h + rl(b, (int)k) * P5, 11) * P1;
-    h ^= h >> 15;
-    h *= P2;
-    h ^= h >> 13;
-    h *= P3;
-    h ^= h >> 16;
-    return h;
-}
-
 // one wave per block-parallel frame: all pieces decoded, moved together
 // when an earlier one came out short (ascending 1 KiB steps, each loaded
 // whole before it is stored: safe for any gap), content size / checksum
 // checked
 __global__ __launch_bounds__(256) void k_decode_finish(DeviceJob j) {
+    __shared__ __attribute__((aligned(16))) uint8_t xb[4][1024];
+    lds_u8* xbuf = (lds_u8*)xb[threadIdx.x >> 6];
     const uint32_t count = j.counters[2];
-    const uint32_t nw = gridDim.x * (blockDim.x >> 6);
     const uint32_t l = lane();
-    for (uint32_t item = blockIdx.x * (blockDim.x >> 6) + uni32(threadIdx.x >> 6); item < count; item += nw) {
+    // frames claimed one at a time (counters[14]): the content checksums are
+    // long serial chains and only some frames carry one
+    for (;;) {
+        const uint32_t item = wave_fetch_add(&j.counters[14], 1u);
+        if (item >= count) break;
         const uint32_t mode = uni32(j.plans[item].mode);
         const uint32_t b = uni32(j.decode_list[item]);
         rpgpu_batch_result* R = &j.batches[b];
@@ -1731,7 +2024,7 @@ __global__ __launch_bounds__(256) void k_decode_finish(DeviceJob j) {
         const uint64_t total = run - d0;
         if (ok && mode == 1) {
             if (uni32(j.plans[item].csf) && total != uni64(j.plans[item].content_size)) ok = false;  // frameSize_wrong
-            if (ok && uni32(j.plans[item].ccs) && xxh32_wave(j.decoded + d0, total, 0) != uni32(j.plans[item].ccs_val))
+            if (ok && uni32(j.plans[item].ccs) && xxh32_wave(j.decoded + d0, total, 0, xbuf) != uni32(j.plans[item].ccs_val))
                 ok = false;
         }
         if (ok && l == 0) {
@@ -1774,10 +2067,15 @@ __global__ void k_print_dstamps() {
            g[3], g[2] / 1e5, g[5], g[4] / 1e5, g[7], g[6] / 1e5, g[9], g[10] / 1e5, g[11], g[12]);
     printf("RPGPU_DSTAMPS batches=%llu rounds=%llu | per batch clk: scan=%.0f lit=%.0f rounds=%.0f flush=%.0f\n", g[20], g[21],
            (double)g[16] / g[20], (double)g[17] / g[20], (double)g[18] / g[20], (double)g[19] / g[20]);
+    printf("RPGPU_DSTAMPS walk long=%llu sum_ms=%.1f max_ms=%.2f (nrec %llu csize %llu) | lane pieces=%llu sum_ms=%.1f "
+           "max_ms=%.2f (nrec %llu csize %llu kind %llu) | wave end spread ms=%.2f\n",
+           g[25], g[24] / 1e5, g[26] / 1e5, g[32], g[33], g[28], g[27] / 1e5, g[29] / 1e5, g[30], g[31] & 0xFFFFFFFFull,
+           g[31] >> 32, (double)(g[34] - g[35]) / 1e5);
     for (int i = 0; i < 64; i++) g_dst[i] = 0;
 }
 __global__ void k_init_dstamps() {
     for (int i = 0; i < 64; i++) g_dst[i] = 0;
+    g_dst[35] = ~0ull;
 }
 #endif
 
@@ -1794,6 +2092,9 @@ hipError_t launch_decode_blocks(const DeviceJob& j, hipStream_t s, uint32_t grid
 }
 
 hipError_t launch_lz_walk(const DeviceJob& j, hipStream_t s, uint32_t grid) {
+#ifdef RPGPU_DSTAMPS
+    hipLaunchKernelGGL(k_init_dstamps, dim3(1), dim3(1), 0, s);
+#endif
     hipLaunchKernelGGL(k_lz_walk, dim3(grid), dim3(256), 0, s, j);
     return hipGetLastError();
 }
@@ -1805,9 +2106,6 @@ hipError_t launch_lz_exec(const DeviceJob& j, hipStream_t s) {
         attr = true;
     }
     if (!j.exec_waves) return hipSuccess;
-#ifdef RPGPU_DSTAMPS
-    hipLaunchKernelGGL(k_init_dstamps, dim3(1), dim3(1), 0, s);
-#endif
     hipLaunchKernelGGL(k_lz_exec, dim3(j.exec_waves), dim3(64), kXRing, s, j);
 #ifdef RPGPU_DSTAMPS
     hipLaunchKernelGGL(k_print_dstamps, dim3(1), dim3(1), 0, s);

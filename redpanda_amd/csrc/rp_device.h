@@ -386,4 +386,14 @@ HD uint64_t decode_capacity_raw(int codec, const uint8_t* s, uint64_t n) {
 }
 
 
+// Wave-uniform atomic fetch-add of `v` (lane 0's contribution; the other
+// lanes add 0).  Every lane executes the atomic: written as
+// `if (lane() == 0) x = atomicAdd(..)` followed by readfirstlane, the
+// compiler's divergence analysis took the claimed value for a per-lane one
+// and built a claim loop with a per-lane exit whose lanes never all left
+// (the round-2 wave decoder did not terminate).
+DEV uint32_t wave_fetch_add(uint32_t* p, uint32_t v) {
+    return uni32(atomicAdd(p, lane() == 0 ? v : 0u));
+}
+
 }  // namespace rp

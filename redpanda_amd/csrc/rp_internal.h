@@ -145,10 +145,13 @@ struct DeviceJob {
     uint32_t* counters;           // [0] rewalks, [1] overflow bits, [2] decode items, [3] unused,
                                   // [4] block items reserved, [5] sequential-frame claim cursor,
                                   // [6] sequential frames, [7] linked frames, [8] k_lz_exec claim cursor,
-                                  // [9] slab pool cursor, [10] k_lz_walk claim cursor
+                                  // [9] slab pool cursor, [10] k_lz_walk claim cursor, [11] long pieces,
+                                  // [12] long-piece claim cursor, [13] k_validate_decoded claim cursor,
+                                  // [14] k_decode_finish claim cursor
     uint32_t* decode_list;        // batch_capacity: ordinals of batches to uncompress
     uint32_t* seq_list;           // batch_capacity: decode items decoded whole by one lane
     uint32_t* link_list;          // batch_capacity: decode items whose linked LZ4F blocks one wave decodes in order
+    uint32_t* long_list;          // block_capacity: pieces k_lz_walk walks one wave each ([11] count, [12] cursor)
     SeqRec* seqs;                 // k_lz_exec's own walks: kRecsPerLane per resident wave
     uint32_t exec_waves;          // k_lz_exec grid (one wave per workgroup; sizes `seqs`)
     PieceState* pstate;           // block_capacity: walk results
@@ -185,6 +188,11 @@ struct UncItem {
 hipError_t launch_uncompress_many(const UncItem* items, uint32_t count, const uint8_t* in, uint64_t in_total,
                                   uint8_t* out, int64_t* res, hipStream_t s);
 hipError_t launch_finalize(const DeviceJob& j, hipStream_t s);
+// rpgpu_stamp (rp_validate.hip): base offset of batch i = next + offs[i]
+// (RPGPU_STAMP_OFFSETS: offs = exclusive scan of the steps), cursor zeroed
+hipError_t launch_stamp_steps(const uint8_t* data, const uint64_t* pos, uint32_t n, uint64_t* steps, hipStream_t s);
+hipError_t launch_stamp(uint8_t* data, const uint64_t* pos, const uint32_t* plen, const uint64_t* offs, int64_t next,
+                        uint32_t n, uint32_t flags, const Tables* T, uint32_t* cursor, uint32_t grid, hipStream_t s);
 hipError_t scan_exclusive_u64(uint64_t* data, uint64_t n, void* temp, size_t temp_bytes, hipStream_t s);
 // n = min(*d_n, n_cap), read on the device
 hipError_t scan_exclusive_u64_devn(uint64_t* data, const uint64_t* d_n, uint64_t n_cap, void* temp, hipStream_t s);

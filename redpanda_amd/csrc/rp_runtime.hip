@@ -113,6 +113,9 @@ struct rpgpu_ctx {
     size_t bh_bytes = 0;
     void* bd = nullptr;
     size_t bd_bytes = 0;
+    // rpgpu_stamp workspace (offset steps, scan temporaries, claim cursor)
+    void* sws = nullptr;
+    size_t sws_bytes = 0;
     // rpgpu_segment_index workspace (piece tables), grow-only
     void* iws = nullptr;
     size_t iws_bytes = 0;
@@ -219,6 +222,7 @@ int rpgpu_destroy(rpgpu_ctx* c) {
     if (c->uws) hipFree(c->uws);
     if (c->iws) hipFree(c->iws);
     if (c->qws) hipFree(c->qws);
+    if (c->sws) hipFree(c->sws);
     if (c->bd) hipFree(c->bd);
     if (c->bh) hipHostFree(c->bh);
     if (c->seqs) hipFree(c->seqs);
@@ -397,6 +401,7 @@ int submit_impl(rpgpu_ctx* c, const rpgpu_job* job, void* stream, int stop, Plan
     const size_t o_blocks = take(bl_cap64 * sizeof(BlockItem));
     const size_t o_plans = take(dec ? (bcap + 1) * sizeof(FramePlan) : 0);
     const size_t o_pstate = take(bl_cap64 * sizeof(PieceState));
+    const size_t o_longl = take(bl_cap64 * 4);
     const size_t o_scan = take(scan_temp_bytes(std::max<uint64_t>(tc, bcap)) + 64);
     const size_t need = off;
     if (dec && !c->seqs) {
@@ -455,6 +460,7 @@ int submit_impl(rpgpu_ctx* c, const rpgpu_job* job, void* stream, int stop, Plan
     j.decode_list = (uint32_t*)(ws + o_dlist);
     j.seq_list = (uint32_t*)(ws + o_slist);
     j.link_list = (uint32_t*)(ws + o_llist);
+    j.long_list = (uint32_t*)(ws + o_longl);
     j.seqs = c->seqs;
     j.exec_waves = c->exec_waves;
     j.pstate = (PieceState*)(ws + o_pstate);
@@ -741,6 +747,37 @@ int rpgpu_uncompress(rpgpu_ctx* c, int codec, const void* in, size_t n, void* ou
     *out_len = (size_t)res[1];
     if ((size_t)res[1] > cap) return fail(c, RPGPU_E_OVERFLOW, "rpgpu_uncompress: output capacity too small");
     if (res[1]) HIPCHK(c, hipMemcpy(out, d_out, (size_t)res[1], hipMemcpyDeviceToHost));
+    return RPGPU_OK;
+}
+
+// Write side: stamp the headers of n batches in place (rp_validate.hip
+// k_stamp; disk_log_appender.cc:72-74 + parser_utils.cc:114-120).
+int rpgpu_stamp(rpgpu_ctx* c, uint8_t* d_data, const uint64_t* d_pos, const uint32_t* d_payload_len, uint32_t n,
+                int64_t next_offset, uint32_t flags, void* stream) {
+    if (!c) return RPGPU_E_INVALID;
+    if (n == 0) return RPGPU_OK;
+    if (!d_data || !d_pos || ((flags & RPGPU_STAMP_CRC) && !d_payload_len) ||
+        (flags & ~(RPGPU_STAMP_OFFSETS | RPGPU_STAMP_CRC)))
+        return fail(c, RPGPU_E_INVALID, "rpgpu_stamp: bad argument");
+    if (((uintptr_t)d_data & 15) != 0) return fail(c, RPGPU_E_INVALID, "rpgpu_stamp: d_data must be 16-byte aligned");
+    hipSetDevice(c->device);
+    hipStream_t s = pick(c, stream);
+    const size_t o_steps = 0, o_scan = align_up((size_t)(n + 1) * 8, 256);
+    const size_t o_cur = align_up(o_scan + scan_temp_bytes(n) + 64, 256), need = o_cur + 256;
+    if (need > c->sws_bytes) {
+        if (c->sws) { HIPCHK(c, hipStreamSynchronize(s)); HIPCHK(c, hipFree(c->sws)); c->sws = nullptr; c->sws_bytes = 0; }
+        if (hipMalloc(&c->sws, need) != hipSuccess) { c->sws = nullptr; return fail(c, RPGPU_E_NOMEM, "rpgpu_stamp workspace"); }
+        c->sws_bytes = need;
+    }
+    uint8_t* w = (uint8_t*)c->sws;
+    uint64_t* steps = (uint64_t*)(w + o_steps);
+    uint32_t* cursor = (uint32_t*)(w + o_cur);
+    HIPCHK(c, hipMemsetAsync(cursor, 0, 4, s));
+    if (flags & RPGPU_STAMP_OFFSETS) {
+        HIPCHK(c, launch_stamp_steps(d_data, d_pos, n, steps, s));
+        HIPCHK(c, scan_exclusive_u64(steps, n, w + o_scan, scan_temp_bytes(n) + 64, s));
+    }
+    HIPCHK(c, launch_stamp(d_data, d_pos, d_payload_len, steps, next_offset, n, flags, c->d_tables, cursor, c->cu_count, s));
     return RPGPU_OK;
 }
 

@@ -1290,8 +1290,11 @@ __global__ __launch_bounds__(1024) void k_validate_decoded(DeviceJob j) {
     const uint32_t l = lane_v();
     const Keys K = make_keys();
     const uint32_t c40 = uni32(T->c40);
-    const uint64_t nw = (uint64_t)gridDim.x * kVWaves;
-    for (uint64_t i = (uint64_t)blockIdx.x * kVWaves + uni32(threadIdx.x >> 6); i < count; i += nw) {
+    // items claimed one at a time (counters[13]): payloads run 200 B .. 1 MiB,
+    // and a static stride left waves holding several of the largest
+    for (;;) {
+        const uint32_t i = wave_fetch_add(&j.counters[13], 1u);
+        if (i >= count) break;
         const uint64_t b = uni32(j.decode_list[i]);
         rpgpu_batch_result* R = &j.batches[b];
         Desc d = desc_of(load_desc_raw(j, b));
@@ -1396,6 +1399,106 @@ __global__ __launch_bounds__(256) void k_walk(DeviceJob j) {
         // H is spent: its slot stages the entries
         coop_store(hslot, e, dst);
     }
+}
+
+// ---------------------------------------------------------------------------
+// Write side: stamp the headers of batches about to be
+// written, one wave per batch (claimed one at a time):
+//   * RPGPU_STAMP_OFFSETS — disk_log_appender::operator() (storage/
+//     disk_log_appender.cc:72-74, :113-119): base_offset = the appender's
+//     next offset, which then moves to last_offset + 1 (the caller's
+//     exclusive scan of last_offset_delta + 1 gives every batch its value);
+//   * RPGPU_STAMP_CRC — reset_size_checksum_metadata (storage/parser_utils.cc:
+//     114-120): size_bytes = 61 + payload, crc = crc_record_batch (BE40 prefix
+//     then the payload, the same braided window CRC as k_validate);
+//   * header_crc = internal_header_only_crc (model/record_utils.cc:34-55)
+//     over the final header, always.
+// ---------------------------------------------------------------------------
+// BE40 prefix byte k (model/record_utils.cc:68-80) = disk header byte be_src(k)
+DEV uint32_t be40_src(uint32_t k) {
+    // fields: attrs 2 @21, lod 4 @23, first_ts 8 @27, max_ts 8 @35, pid 8 @43,
+    // epoch 2 @51, base_seq 4 @53, record_count 4 @57 (each byte-reversed)
+    return k < 2 ? 22 - k : k < 6 ? 26 - (k - 2) : k < 14 ? 34 - (k - 6) : k < 22 ? 42 - (k - 14) : k < 30 ? 50 - (k - 22)
+         : k < 32 ? 52 - (k - 30) : k < 36 ? 56 - (k - 32) : 60 - (k - 36);
+}
+
+__global__ __launch_bounds__(1024) void k_stamp(uint8_t* data, const uint64_t* __restrict__ pos,
+                                                const uint32_t* __restrict__ plen,
+                                                const uint64_t* __restrict__ offs, int64_t next, uint32_t n,
+                                                uint32_t flags, const Tables* T, uint32_t* cursor) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    init_lds_tables(lds, T);
+    const uint32_t l = lane_v();
+    const Keys K = make_keys();
+    const uint32_t c40 = uni32(T->c40);
+    for (;;) {
+        const uint32_t i = wave_fetch_add(cursor, 1u);
+        if (i >= n) break;
+        const uint64_t p = uni64(pos[i]);
+        const uint32_t L = uni32(plen[i]);
+        uint8_t* h = data + p;
+        uint32_t b = l < RPGPU_HEADER_SIZE ? (uint32_t)h[l] : 0u;
+        if (flags & RPGPU_STAMP_OFFSETS) {
+            const uint64_t bo = (uint64_t)next + uni64(offs[i]);
+            if (l >= 8 && l < 16) b = (uint32_t)(bo >> (8 * (l - 8))) & 0xFFu;
+        }
+        if (flags & RPGPU_STAMP_CRC) {
+            const uint32_t size = RPGPU_HEADER_SIZE + L;
+            if (l >= 4 && l < 8) b = (size >> (8 * (l - 4))) & 0xFFu;
+            // raw CRC contribution of the BE40 prefix: lane k < 40 holds its byte
+            const uint32_t pb = (uint32_t)__shfl((int)b, (int)be40_src(l < 40 ? l : 0), 64);
+            uint32_t x = l < 40 ? T->hdr[39 - l][pb] : 0u;
+            x ^= swz_xor<1>(x);
+            x ^= swz_xor<2>(x);
+            x ^= swz_xor<4>(x);
+            x ^= swz_xor<8>(x);
+            x ^= swz_xor<16>(x);
+            const uint32_t praw = rl(x, 0) ^ rl(x, 32);
+            const Stream st = make_stream(data, p + RPGPU_HEADER_SIZE, p + RPGPU_HEADER_SIZE + L);
+            Win w;
+            load_window(st, 0, w);
+            const uint4 gt = load_tail(st);
+            const uint32_t crc = ~crc_stream(lds, K, st, w, gt, praw ^ c40);
+            if (l >= 17 && l < 21) b = (crc >> (8 * (l - 17))) & 0xFFu;
+        }
+        // header_crc over bytes 4..60 of the stamped header
+        uint32_t x = (l >= 4 && l < RPGPU_HEADER_SIZE) ? T->hdr[60 - l][b] : 0u;
+        x ^= swz_xor<1>(x);
+        x ^= swz_xor<2>(x);
+        x ^= swz_xor<4>(x);
+        x ^= swz_xor<8>(x);
+        x ^= swz_xor<16>(x);
+        const uint32_t hc = ~(T->c57 ^ rl(x, 0) ^ rl(x, 32));
+        if (l < 4) b = (hc >> (8 * l)) & 0xFFu;
+        if (l < 21) h[l] = (uint8_t)b;
+    }
+}
+
+// per batch last_offset_delta + 1 (the appender's offset step), scanned by the caller
+__global__ __launch_bounds__(256) void k_stamp_steps(const uint8_t* data, const uint64_t* __restrict__ pos, uint32_t n,
+                                                     uint64_t* steps) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint8_t* h = data + pos[i] + 23;
+    const int32_t lod = (int32_t)((uint32_t)h[0] | ((uint32_t)h[1] << 8) | ((uint32_t)h[2] << 16) | ((uint32_t)h[3] << 24));
+    steps[i] = (uint64_t)((int64_t)lod + 1);
+}
+
+hipError_t launch_stamp_steps(const uint8_t* data, const uint64_t* pos, uint32_t n, uint64_t* steps, hipStream_t s) {
+    if (n) hipLaunchKernelGGL(k_stamp_steps, dim3((n + 255) / 256), dim3(256), 0, s, data, pos, n, steps);
+    return hipGetLastError();
+}
+
+hipError_t launch_stamp(uint8_t* data, const uint64_t* pos, const uint32_t* plen, const uint64_t* offs, int64_t next,
+                        uint32_t n, uint32_t flags, const Tables* T, uint32_t* cursor, uint32_t grid, hipStream_t s) {
+    static bool attr = false;
+    if (!attr) {
+        (void)hipFuncSetAttribute((const void*)k_stamp, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsValidateBytes);
+        attr = true;
+    }
+    hipLaunchKernelGGL(k_stamp, dim3(grid), dim3(64 * kVWaves), kLdsValidateBytes, s, data, pos, plen, offs, next, n,
+                       flags, T, cursor);
+    return hipGetLastError();
 }
 
 hipError_t launch_walk(const DeviceJob& j, hipStream_t s, uint32_t grid) {

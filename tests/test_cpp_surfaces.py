@@ -322,7 +322,10 @@ def test_compressor_uncompress(driver, oracle, engine, tmp_path):
     assert run(driver, "uncompress", abi.CODEC_GZIP, empty, out) == ["U runtime_error"]
     assert run(driver, "uncompress", abi.CODEC_NONE, one, out) == ["U runtime_error"]
     assert run(driver, "uncompress", abi.CODEC_GZIP, one, out) == ["U runtime_error"]
-    assert run(driver, "uncompress", abi.CODEC_ZSTD, one, out) == ["U runtime_error"]
+    # three bytes are not a whole zstd frame header: ZSTD_decompressStream
+    # consumes them and asks for more, the reference loop ends with an empty
+    # result (stream_zstd.cc:160-176)
+    assert run(driver, "uncompress", abi.CODEC_ZSTD, one, out) == ["U ok 0"]
     import gzip
     from tests.test_hostcodec import corpus, zstd_compress
     gz, zs = str(tmp_path / "a.gz"), str(tmp_path / "a.zst")

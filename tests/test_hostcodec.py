@@ -133,6 +133,14 @@ def test_zstd_errors(rplib):
     assert rc == abi.E_OVERFLOW and need == 100000
 
 
+def test_zstd_short_input_is_an_empty_result(rplib):
+    """Fewer bytes than a frame header: ZSTD_decompressStream consumes them and
+    asks for more; the reference loop (stream_zstd.cc:160-176) then returns
+    what it has, nothing."""
+    assert uncompress(rplib, abi.CODEC_ZSTD, b"\x01\x02\x03") == (0, b"")
+    assert uncompress(rplib, abi.CODEC_ZSTD, zstd_compress(b"abc" * 1000)[:3]) == (0, b"")
+
+
 def test_empty_and_none_throw(rplib):
     assert uncompress(rplib, abi.CODEC_GZIP, b"")[0] == abi.E_CODEC
     assert uncompress(rplib, abi.CODEC_ZSTD, b"")[0] == abi.E_CODEC
