@@ -262,6 +262,17 @@ typedef struct rpgpu_job {
     rpgpu_segment_summary* d_summaries; /* n_segments entries */
     rpgpu_job_totals* d_totals;      /* one entry */
     uint64_t* d_valid_bitmap;        /* optional: 1 bit per batch, set = crc_ok && header_ok (&& parse_ok if PARSE) */
+    /* Optional chain seeds (the index-seeded mode of SURVEY.md §8(b)): known
+     * batch header positions of each segment, ascending, e.g. the
+     * position_index of its .base_index (storage/index_state.h:23-100,
+     * index_state::hydrate_from_buffer, storage/index_state.cc:104-186).
+     * Segment s's seeds are d_seeds[d_seed_offsets[s] .. d_seed_offsets[s+1]).
+     * Discovery then enters each chunk by following the chain from the last
+     * seed before it instead of scanning its bytes.  Seeds are verified like
+     * any discovered header (a wrong or stale index only costs re-walks);
+     * results are identical with or without them.  NULL = scan. */
+    const uint64_t* d_seeds;
+    const uint64_t* d_seed_offsets;  /* device, n_segments + 1 entries */
 } rpgpu_job;
 
 /* Enqueue the whole pipeline (discover -> resolve -> plan -> validate/decode)
@@ -365,6 +376,17 @@ int rpgpu_segment_index(rpgpu_ctx* ctx, const rpgpu_batch_result* d_batches, uin
  * not overlap.  Asynchronous on `stream`. */
 int rpgpu_stamp(rpgpu_ctx* ctx, uint8_t* d_data, const uint64_t* d_pos, const uint32_t* d_payload_len, uint32_t n,
                 int64_t next_offset, uint32_t flags, void* stream);
+
+/* kafka::writer_serialize_batch (kafka/protocol/response_writer.h:241-276)
+ * for batches [first, first + n) of a completed disk-layout job (its
+ * d_batches, over the job's d_data / d_seg_offsets): each batch's Kafka v2
+ * wire header (big endian; batch_length = size_bytes - 12, partition leader
+ * epoch 0, magic 2, the stored crc) followed by its payload, back to back in
+ * d_wire (capacity: the batches' size_bytes summed).  *d_total (a device
+ * u64) receives the record set's length.  Asynchronous on `stream`. */
+int rpgpu_serialize_wire(rpgpu_ctx* ctx, const uint8_t* d_data, const uint64_t* d_seg_offsets,
+                         const rpgpu_batch_result* d_batches, uint64_t first, uint32_t n, uint8_t* d_wire,
+                         uint64_t* d_total, void* stream);
 
 /* ------------------------------------------------------------------------ */
 /* compression::compressor::uncompress (compression/compression.h:21-24)     */

@@ -341,6 +341,51 @@ struct compressor {
 // ---------------------------------------------------------------------------
 namespace storage {
 
+namespace internal {
+// storage/parser_utils.cc:114-120 (host: one header at a time)
+inline void reset_size_checksum_metadata(model::record_batch_header& hdr, const rpgpu::iobuf& records) {
+    hdr.size_bytes = (int32_t)(RPGPU_HEADER_SIZE + records.size_bytes());
+    hdr.crc = model::crc_record_batch(hdr, records);
+    hdr.header_crc = model::internal_header_only_crc(hdr);
+}
+}  // namespace internal
+
+// The write side in bulk (rpgpu_stamp): a buffer of on-disk batches about to
+// be appended gets, on the device and in batch order, what
+// disk_log_appender::operator() (storage/disk_log_appender.cc:72-74,
+// :113-119) and reset_size_checksum_metadata give each one: base offsets
+// from `next_offset` (returns the appender's next offset after the last
+// batch), size_bytes and crc, then header_crc.  `buf` holds the batches
+// back to back; each payload runs to the next header (or the end).
+inline int64_t stamp_batches(uint8_t* buf, size_t len, const std::vector<size_t>& positions, int64_t next_offset,
+                             uint32_t flags = RPGPU_STAMP_OFFSETS | RPGPU_STAMP_CRC,
+                             rpgpu::engine& e = rpgpu::engine::local()) {
+    const size_t n = positions.size();
+    if (n == 0) return next_offset;
+    std::vector<uint64_t> pos(n);
+    std::vector<uint32_t> plen(n);
+    int64_t next = next_offset;
+    for (size_t i = 0; i < n; i++) {
+        const size_t end = i + 1 < n ? positions[i + 1] : len;
+        if (positions[i] + RPGPU_HEADER_SIZE > end) throw std::invalid_argument("stamp_batches: short batch");
+        pos[i] = positions[i];
+        plen[i] = (uint32_t)(end - positions[i] - RPGPU_HEADER_SIZE);
+        int32_t lod;
+        std::memcpy(&lod, buf + positions[i] + 23, 4);
+        next = (int64_t)((uint64_t)next + (uint64_t)(int64_t)lod + 1u);
+    }
+    rpgpu::dev_buffer d(e, len + 16), dp(e, n * 8), dl(e, n * 4);
+    e.check(rpgpu_memcpy_h2d(e.ctx(), d.get(), buf, len, nullptr), "rpgpu_memcpy_h2d");
+    e.check(rpgpu_memcpy_h2d(e.ctx(), dp.get(), pos.data(), n * 8, nullptr), "rpgpu_memcpy_h2d");
+    e.check(rpgpu_memcpy_h2d(e.ctx(), dl.get(), plen.data(), n * 4, nullptr), "rpgpu_memcpy_h2d");
+    e.check(rpgpu_stamp(e.ctx(), (uint8_t*)d.get(), (const uint64_t*)dp.get(), (const uint32_t*)dl.get(), (uint32_t)n,
+                        next_offset, flags, nullptr),
+            "rpgpu_stamp");
+    e.check(rpgpu_memcpy_d2h(e.ctx(), buf, d.get(), len, nullptr), "rpgpu_memcpy_d2h");
+    e.check(rpgpu_sync(e.ctx(), nullptr), "rpgpu_sync");
+    return (flags & RPGPU_STAMP_OFFSETS) ? next : next_offset;
+}
+
 // storage/parser_errc.h:18-25
 enum class parser_errc : int {
     none = RPGPU_ERRC_NONE,

@@ -31,6 +31,7 @@ class JobC(C.Structure):
         ("d_records", C.c_void_p), ("record_capacity", C.c_uint64),
         ("d_decoded", C.c_void_p), ("decoded_capacity", C.c_uint64),
         ("d_summaries", C.c_void_p), ("d_totals", C.c_void_p), ("d_valid_bitmap", C.c_void_p),
+        ("d_seeds", C.c_void_p), ("d_seed_offsets", C.c_void_p),
     ]
 
 
@@ -95,6 +96,8 @@ def load():
         "rpgpu_wait": (i32, [vp]),
         "rpgpu_release": (i32, [vp]),
         "rpgpu_query_capacity": (i32, [vp, C.POINTER(JobC), vp, C.POINTER(CapacityC)]),
+        "rpgpu_stamp": (i32, [vp, vp, vp, vp, u32, C.c_int64, u32, vp]),
+        "rpgpu_serialize_wire": (i32, [vp, vp, vp, vp, u64, u32, vp, vp, vp]),
         "rpgpu_validate_host": (i32, [vp, vp]),
         "rpgpu_segment_index": (i32, [vp, vp, u64, vp, u32, u64, vp, vp, vp, vp, vp]),
     }

@@ -12,6 +12,8 @@ CODEC_NONE, CODEC_GZIP, CODEC_SNAPPY, CODEC_LZ4, CODEC_ZSTD = 0, 1, 2, 3, 4
 # rpgpu_status
 OK, E_INVALID, E_NO_DEVICE, E_NOMEM, E_OVERFLOW, E_CODEC, E_UNSUPPORTED, E_HIP = 0, -1, -2, -3, -4, -5, -6, -7
 PENDING = 1
+# rpgpu_stamp flags
+STAMP_OFFSETS, STAMP_CRC = 1, 2
 
 ERRC_NONE = 0
 ERRC_END_OF_STREAM = 1

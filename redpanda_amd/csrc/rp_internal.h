@@ -162,6 +162,8 @@ struct DeviceJob {
     uint32_t block_capacity;
     FramePlan* plans;             // one per decode item
     uint32_t* seg_first_bad;      // n_segments: first chain ordinal failing complete && crc_ok (atomicMin)
+    const uint64_t* seeds;        // optional chain seeds (index-seeded discovery), per segment ascending
+    const uint64_t* seed_off;     // n_segments + 1
 };
 
 // kernel launchers (rp_kernels.hip)
@@ -188,6 +190,11 @@ struct UncItem {
 hipError_t launch_uncompress_many(const UncItem* items, uint32_t count, const uint8_t* in, uint64_t in_total,
                                   uint8_t* out, int64_t* res, hipStream_t s);
 hipError_t launch_finalize(const DeviceJob& j, hipStream_t s);
+// rpgpu_serialize_wire (rp_validate.hip): batches [first, first + n) of a job's
+// results; src/dst: n + 1 u64 each (dst ends as the exclusive scan, dst[n] = total)
+hipError_t launch_to_wire(const uint8_t* disk, uint8_t* wire, const rpgpu_batch_result* batches, const uint64_t* seg_off,
+                          uint64_t first, uint32_t n, uint64_t* src, uint64_t* dst, void* scan_tmp, size_t scan_bytes,
+                          uint32_t grid, hipStream_t s);
 // rpgpu_stamp (rp_validate.hip): base offset of batch i = next + offs[i]
 // (RPGPU_STAMP_OFFSETS: offs = exclusive scan of the steps), cursor zeroed
 hipError_t launch_stamp_steps(const uint8_t* data, const uint64_t* pos, uint32_t n, uint64_t* steps, hipStream_t s);

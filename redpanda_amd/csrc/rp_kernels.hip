@@ -158,18 +158,13 @@ DEV uint32_t scan_step(uint32_t layout, const uint8_t* __restrict__ seg, const S
     return m;
 }
 
-// One WORKGROUP per chunk: its four waves scan interleaved 1 KiB steps (wave
-// q takes steps q, q + 4, ...), so a round covers 4 KiB with four memory
-// latencies in flight, each wave's next step already loading.  After a
-// round the first verified header of the lowest wave that found one is the
-// chunk's entry.  A chunk inside a batch larger than the chunk holds no
-// header at all and is scanned to its end: with one wave per chunk those
-// scans (C2's 64 KiB..1 MiB batches) were a chain of 256 step latencies.
+// One wave per chunk, four chunks per workgroup.  (Four waves per chunk,
+// scanning interleaved steps, cut C2's discovery from 14.4 to 9.9 ms but
+// cost C1 0.2 ms of its 5 ms step: most C1 chunks find their entry within
+// a few steps, and four waves then scan four times the bytes.)
 __global__ __launch_bounds__(256) void k_discover(DeviceJob j) {
-    __shared__ uint64_t found[4];
-    const uint64_t g = blockIdx.x;
+    const uint64_t g = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
     if (g >= j.total_chunks) return;
-    const uint32_t wv = threadIdx.x >> 6;
     const uint32_t s = find_segment(j.chunk_base, j.n_segments, g);
     const uint64_t w = g - j.chunk_base[s];
     const uint64_t off = j.seg_off[s], len = j.seg_off[s + 1] - off;
@@ -177,43 +172,65 @@ __global__ __launch_bounds__(256) void k_discover(DeviceJob j) {
     const uint64_t cs = w * j.chunk_bytes;
     const uint64_t ce = (cs + j.chunk_bytes < len) ? cs + j.chunk_bytes : len;
     uint64_t entry = kNone;
+    bool scan = true;
     if (w == 0) {
         entry = 0;
-    } else {
-        // candidates in ascending order: lanes cover consecutive 16-byte
-        // spans, bits ascend within a lane, waves ascend within a round
-        const uint64_t a0 = (off + cs) & ~15ull;
-        uint64_t a = a0 + 1024ull * wv;
-        ScanWin cur, nxt;
-        if (a < off + ce) scan_load(j.data, j.data_len, a, cur);
-        for (uint64_t r0 = a0; r0 < off + ce; r0 += 4096, a += 4096) {
-            uint64_t mine = kNone;
-            if (a < off + ce) {
-                if (a + 4096 < off + ce) scan_load(j.data, j.data_len, a + 4096, nxt);
-                const uint32_t m = scan_step(j.layout, seg, cur, a, off, len, cs, ce);
-                uint64_t lanes = __ballot(m != 0);
-                while (lanes && mine == kNone) {
-                    const uint32_t l = __builtin_ctzll(lanes);
-                    lanes &= lanes - 1;
-                    uint32_t bits = rl(m, (int)l);
-                    while (bits) {
-                        const uint32_t i = __builtin_ctz(bits);
-                        bits &= bits - 1;
-                        const uint64_t qc = a + 16ull * l + i - off;
-                        Hdr h = wave_header_of(j.layout, seg, len, qc, j.tables);
-                        if (h.status < 0 && len - qc - RPGPU_HEADER_SIZE >= h.need) { mine = qc; break; }
-                    }
-                }
-                cur = nxt;
+        scan = false;
+    } else if (j.seeds) {
+        // index-seeded: follow the chain from the last seed at or before the
+        // chunk start (or the segment start) to the first header at or after
+        // it; every hop is a verified header, a failed one falls back to the scan
+        const uint64_t s0 = uni64(j.seed_off[s]), s1 = uni64(j.seed_off[s + 1]);
+        uint64_t lo = s0, hi = s1;  // first seed > cs
+        while (lo < hi) {
+            const uint64_t m = (lo + hi) >> 1;
+            if (uni64(j.seeds[m]) <= cs) lo = m + 1;
+            else hi = m;
+        }
+        uint64_t q = lo > s0 ? uni64(j.seeds[lo - 1]) : 0;
+        bool ok = q < len;
+        for (uint32_t hop = 0; ok && q < cs; hop++) {
+            const Hdr h = wave_header_of(j.layout, seg, len, q, j.tables);
+            if (hop >= 64 || h.status >= 0 || len - q - RPGPU_HEADER_SIZE < h.need) { ok = false; break; }
+            q += RPGPU_HEADER_SIZE + h.need;
+        }
+        if (ok && q >= cs) {
+            if (q < ce) {
+                const Hdr h = wave_header_of(j.layout, seg, len, q, j.tables);
+                ok = h.status < 0 && len - q - RPGPU_HEADER_SIZE >= h.need;
             }
-            if (lane() == 0) found[wv] = mine;
-            __syncthreads();
-            for (int q = 0; q < 4 && entry == kNone; q++) entry = found[q];
-            __syncthreads();
-            if (entry != kNone) break;
+            if (ok) {
+                entry = q < ce ? q : kNone;
+                scan = false;
+            }
         }
     }
-    if (threadIdx.x == 0) {
+    if (scan) {
+        // candidates in ascending order: lanes cover consecutive 16-byte
+        // spans, bits ascend within a lane
+        uint64_t a = (off + cs) & ~15ull;
+        ScanWin cur, nxt;
+        scan_load(j.data, j.data_len, a, cur);
+        for (; a < off + ce && entry == kNone; a += 1024) {
+            if (a + 1024 < off + ce) scan_load(j.data, j.data_len, a + 1024, nxt);
+            const uint32_t m = scan_step(j.layout, seg, cur, a, off, len, cs, ce);
+            uint64_t lanes = __ballot(m != 0);
+            while (lanes && entry == kNone) {
+                const uint32_t l = __builtin_ctzll(lanes);
+                lanes &= lanes - 1;
+                uint32_t bits = rl(m, (int)l);
+                while (bits) {
+                    const uint32_t i = __builtin_ctz(bits);
+                    bits &= bits - 1;
+                    const uint64_t qc = a + 16ull * l + i - off;
+                    Hdr h = wave_header_of(j.layout, seg, len, qc, j.tables);
+                    if (h.status < 0 && len - qc - RPGPU_HEADER_SIZE >= h.need) { entry = qc; break; }
+                }
+            }
+            cur = nxt;
+        }
+    }
+    if (lane() == 0) {
         ChunkRec r;
         r.entry = entry;
         r.exit = kNone;
@@ -746,7 +763,7 @@ hipError_t launch_chunk_base(const DeviceJob& j, hipStream_t s) {
 }
 
 hipError_t launch_discover(const DeviceJob& j, hipStream_t s) {
-    hipLaunchKernelGGL(k_discover, dim3(j.total_chunks), dim3(256), 0, s, j);
+    hipLaunchKernelGGL(k_discover, dim3((j.total_chunks + 3) / 4), dim3(256), 0, s, j);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k_chain, dim3((j.total_chunks + 255) / 256), dim3(256), kLdsHdrBytes, s, j);

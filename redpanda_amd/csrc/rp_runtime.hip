@@ -471,6 +471,8 @@ int submit_impl(rpgpu_ctx* c, const rpgpu_job* job, void* stream, int stop, Plan
     j.pool = (SeqRec*)c->pool;
     j.slab_next = (uint32_t*)((uint8_t*)c->pool + (size_t)j.pool_slabs * kSlabRecs * sizeof(SeqRec));
     j.seg_first_bad = (uint32_t*)(ws + o_fbad);
+    j.seeds = (job->d_seeds && job->d_seed_offsets) ? job->d_seeds : nullptr;
+    j.seed_off = j.seeds ? job->d_seed_offsets : nullptr;
     j.blocks = (BlockItem*)(ws + o_blocks);
     j.block_capacity = (uint32_t)bl_cap64;
     j.plans = (FramePlan*)(ws + o_plans);
@@ -778,6 +780,38 @@ int rpgpu_stamp(rpgpu_ctx* c, uint8_t* d_data, const uint64_t* d_pos, const uint
         HIPCHK(c, scan_exclusive_u64(steps, n, w + o_scan, scan_temp_bytes(n) + 64, s));
     }
     HIPCHK(c, launch_stamp(d_data, d_pos, d_payload_len, steps, next_offset, n, flags, c->d_tables, cursor, c->cu_count, s));
+    return RPGPU_OK;
+}
+
+// kafka::writer_serialize_batch over batches [first, first + n) of a
+// completed disk-layout job (kafka/protocol/response_writer.h:241-276):
+// the Kafka v2 record set, back to back in d_wire; *d_total (device) gets
+// its length.  Asynchronous on `stream`.
+int rpgpu_serialize_wire(rpgpu_ctx* c, const uint8_t* d_data, const uint64_t* d_seg_offsets,
+                         const rpgpu_batch_result* d_batches, uint64_t first, uint32_t n, uint8_t* d_wire,
+                         uint64_t* d_total, void* stream) {
+    if (!c) return RPGPU_E_INVALID;
+    if (!d_data || !d_seg_offsets || !d_batches || !d_wire || !d_total)
+        return fail(c, RPGPU_E_INVALID, "rpgpu_serialize_wire: missing argument");
+    hipSetDevice(c->device);
+    hipStream_t s = pick(c, stream);
+    const size_t o_dst = align_up((size_t)(n + 1) * 8, 256), o_scan = o_dst + align_up((size_t)(n + 1) * 8, 256);
+    const size_t need = o_scan + scan_temp_bytes(n) + 256;
+    if (need > c->sws_bytes) {
+        if (c->sws) { HIPCHK(c, hipStreamSynchronize(s)); HIPCHK(c, hipFree(c->sws)); c->sws = nullptr; c->sws_bytes = 0; }
+        if (hipMalloc(&c->sws, need) != hipSuccess) { c->sws = nullptr; return fail(c, RPGPU_E_NOMEM, "rpgpu_serialize_wire workspace"); }
+        c->sws_bytes = need;
+    }
+    uint8_t* w = (uint8_t*)c->sws;
+    uint64_t* src = (uint64_t*)w;
+    uint64_t* dst = (uint64_t*)(w + o_dst);
+    if (n == 0) {
+        HIPCHK(c, hipMemsetAsync(d_total, 0, 8, s));
+        return RPGPU_OK;
+    }
+    HIPCHK(c, launch_to_wire(d_data, d_wire, d_batches, d_seg_offsets, first, n, src, dst, w + o_scan,
+                             scan_temp_bytes(n) + 64, c->cu_count * 8, s));
+    HIPCHK(c, hipMemcpyAsync(d_total, dst + n, 8, hipMemcpyDeviceToDevice, s));
     return RPGPU_OK;
 }
 

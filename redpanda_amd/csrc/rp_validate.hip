@@ -1501,6 +1501,73 @@ hipError_t launch_stamp(uint8_t* data, const uint64_t* pos, const uint32_t* plen
     return hipGetLastError();
 }
 
+// ---------------------------------------------------------------------------
+// kafka::writer_serialize_batch (kafka/protocol/response_writer.h:241-276):
+// disk-layout batches -> a Kafka v2 record set, one wave per batch.  The
+// wire header is the disk header re-encoded big-endian: base_offset,
+// batch_length = size_bytes - 61 + 61 - 8 - 4, partition leader epoch 0,
+// magic 2, crc, attrs, last_offset_delta, first/max timestamp, producer id,
+// epoch, base_sequence, record_count; the payload follows unchanged.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_to_wire(const uint8_t* __restrict__ disk, uint8_t* __restrict__ wire,
+                                                 const uint64_t* __restrict__ src, const uint64_t* __restrict__ dst,
+                                                 uint32_t n) {
+    const uint32_t l = lane_v();
+    for (uint32_t i = blockIdx.x * 4 + (threadIdx.x >> 6); i < n; i += gridDim.x * 4) {
+        const uint8_t* h = disk + uni64(src[i]);
+        uint8_t* o = wire + uni64(dst[i]);
+        uint32_t b = l < RPGPU_HEADER_SIZE ? (uint32_t)h[l] : 0u;
+        const int32_t size = (int32_t)(rl(b, 4) | (rl(b, 5) << 8) | (rl(b, 6) << 16) | (rl(b, 7) << 24));
+        const uint32_t blen = (uint32_t)(size - 12);
+        // wire byte l <- disk byte src(l), reversed within each field
+        int from = -1;
+        uint32_t w = 0;
+        if (l < 8) from = 15 - (int)l;                        // base_offset (disk 8..15)
+        else if (l < 12) w = (blen >> (8 * (11 - l))) & 0xFFu;  // batch_length
+        else if (l < 16) w = 0;                               // partition leader epoch
+        else if (l == 16) w = 2;                              // magic
+        else if (l < 21) from = 20 - ((int)l - 17);           // crc (disk 17..20)
+        else if (l < RPGPU_HEADER_SIZE) from = (int)be40_src(l - 21);  // attrs .. record_count (the BE40 prefix)
+        const uint32_t v = (uint32_t)__shfl((int)b, from < 0 ? 0 : from, 64);
+        if (from >= 0) w = v;
+        if (l < RPGPU_HEADER_SIZE) o[l] = (uint8_t)w;
+        const uint32_t pl = (uint32_t)size - RPGPU_HEADER_SIZE;
+        const uint8_t* ps = h + RPGPU_HEADER_SIZE;
+        uint8_t* pd = o + RPGPU_HEADER_SIZE;
+        for (uint32_t c = 0; c < pl; c += 1024) {
+            const uint32_t k = c + 16 * l;
+            if (k + 16 <= pl) {
+                uint4 t;
+                __builtin_memcpy(&t, ps + k, 16);
+                __builtin_memcpy(pd + k, &t, 16);
+            } else if (k < pl) {
+                for (uint32_t e = k; e < pl; e++) pd[e] = ps[e];
+            }
+        }
+    }
+}
+
+__global__ __launch_bounds__(256) void k_wire_sizes(const rpgpu_batch_result* __restrict__ batches,
+                                                    const uint64_t* __restrict__ seg_off, uint64_t first, uint32_t n,
+                                                    uint64_t* src, uint64_t* sizes) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const rpgpu_batch_result& r = batches[first + i];
+    src[i] = seg_off[r.segment] + r.file_pos;
+    sizes[i] = (uint64_t)(uint32_t)r.size_bytes;
+}
+
+hipError_t launch_to_wire(const uint8_t* disk, uint8_t* wire, const rpgpu_batch_result* batches, const uint64_t* seg_off,
+                          uint64_t first, uint32_t n, uint64_t* src, uint64_t* dst, void* scan_tmp, size_t scan_bytes,
+                          uint32_t grid, hipStream_t s) {
+    if (!n) return hipSuccess;
+    hipLaunchKernelGGL(k_wire_sizes, dim3((n + 255) / 256), dim3(256), 0, s, batches, seg_off, first, n, src, dst);
+    hipError_t e = scan_exclusive_u64(dst, n, scan_tmp, scan_bytes, s);  // dst[n] = total
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_to_wire, dim3(grid), dim3(256), 0, s, disk, wire, src, dst, n);
+    return hipGetLastError();
+}
+
 hipError_t launch_walk(const DeviceJob& j, hipStream_t s, uint32_t grid) {
     if (j.flags & RPGPU_JOB_PARSE)
         hipLaunchKernelGGL(k_walk, dim3(grid), dim3(256), 4 * kWalkLdsWave, s, j);  // 48 KiB: 3 per CU

@@ -195,8 +195,58 @@ class Engine:
         check(self.L.rpgpu_uncompress_batch(self.ctx, n, ci, ip, il, op, oc, ol, st), self.ctx, "rpgpu_uncompress_batch")
         return [(int(st[i]), outs[i][: ol[i]].tobytes() if st[i] == 0 else int(ol[i])) for i in range(n)]
 
+    def stamp(self, data, positions, payload_lens, next_offset: int = 0,
+              flags: int = abi.STAMP_OFFSETS | abi.STAMP_CRC, stream=None):
+        """rpgpu_stamp: stamp the headers of disk-layout batches in `data` (a
+        torch uint8 CUDA tensor with 16 readable bytes past the last payload)
+        in place — appender offsets from next_offset, size/crc
+        (reset_size_checksum_metadata) and header_crc."""
+        torch = _torch()
+        dev = data.device
+        pos = torch.from_numpy(np.ascontiguousarray(np.asarray(positions, dtype=np.uint64)).view(np.int64)).to(dev)
+        pl = torch.from_numpy(np.ascontiguousarray(np.asarray(payload_lens, dtype=np.uint32)).view(np.int32)).to(dev)
+        s, finish = self._stream(dev, stream)
+        check(self.L.rpgpu_stamp(self.ctx, C.c_void_p(data.data_ptr()), C.c_void_p(pos.data_ptr()),
+                                 C.c_void_p(pl.data_ptr()), int(pos.numel()), int(next_offset), int(flags),
+                                 C.c_void_p(s.cuda_stream)), self.ctx, "rpgpu_stamp")
+        finish(data, pos, pl)
+        return data
+
+    @staticmethod
+    def seed_tensors(seeds, device):
+        """Per-segment ascending batch positions (e.g. an index's position
+        entries) -> (d_seeds, d_seed_offsets) for the index-seeded mode."""
+        torch = _torch()
+        arrs = [np.asarray(x, dtype=np.uint64).ravel() for x in seeds]
+        offs = np.cumsum([0] + [a.size for a in arrs]).astype(np.uint64)
+        flat = np.concatenate(arrs) if arrs and offs[-1] else np.zeros(1, dtype=np.uint64)
+        return (torch.from_numpy(flat.view(np.int64).copy()).to(device),
+                torch.from_numpy(offs.view(np.int64).copy()).to(device))
+
+    def serialize_wire(self, data, seg_offsets, out: DeviceResult, first: int = 0, n: int = None, stream=None):
+        """rpgpu_serialize_wire: batches [first, first + n) of a completed
+        disk-layout job as a Kafka v2 record set (device uint8 tensor)."""
+        torch = _torch()
+        dev = data.device
+        if n is None:
+            n = int(out.totals_host()["n_batches"]) - first
+        sizes = np.frombuffer(out.batches[first * abi.BATCH_RESULT.itemsize:(first + n) * abi.BATCH_RESULT.itemsize]
+                              .cpu().numpy().tobytes(), dtype=abi.BATCH_RESULT)["size_bytes"]
+        cap = int(np.sum(sizes.astype(np.int64))) + 16
+        wire = torch.empty(max(cap, 16), dtype=torch.uint8, device=dev)
+        total = torch.zeros(1, dtype=torch.int64, device=dev)
+        d_off = torch.from_numpy(np.ascontiguousarray(np.asarray(seg_offsets, dtype=np.uint64)).view(np.int64)).to(dev)
+        s, finish = self._stream(dev, stream)
+        check(self.L.rpgpu_serialize_wire(self.ctx, C.c_void_p(data.data_ptr()), C.c_void_p(d_off.data_ptr()),
+                                          C.c_void_p(out.batches.data_ptr()), int(first), int(n),
+                                          C.c_void_p(wire.data_ptr()), C.c_void_p(total.data_ptr()),
+                                          C.c_void_p(s.cuda_stream)), self.ctx, "rpgpu_serialize_wire")
+        finish(data, d_off, out.batches, wire, total)
+        s.synchronize()
+        return wire[: int(total.item())]
+
     def submit(self, data, seg_offsets, out: DeviceResult, flags: int = abi.JOB_CRC | abi.JOB_PARSE,
-               chunk_bytes: int = 0, stream=None, d_seg_offsets=None, layout: int = abi.LAYOUT_DISK):
+               chunk_bytes: int = 0, stream=None, d_seg_offsets=None, layout: int = abi.LAYOUT_DISK, seeds=None):
         """Enqueue one job ordered on `stream` (default: torch's current
         stream; the launch itself goes to a side stream when that is the
         legacy default stream, see _stream).  `data` is a torch uint8 CUDA
@@ -226,9 +276,14 @@ class Engine:
         job.d_summaries = out.summaries.data_ptr()
         job.d_totals = out.totals.data_ptr()
         job.d_valid_bitmap = out.bitmap.data_ptr() if out.bitmap is not None else 0
+        sd = so = None
+        if seeds is not None:
+            sd, so = seeds if isinstance(seeds, tuple) else self.seed_tensors(seeds, data.device)
+            job.d_seeds, job.d_seed_offsets = sd.data_ptr(), so.data_ptr()
+            self._keep_seeds = (sd, so)  # alive until the next submit
         s, finish = self._stream(data.device, stream)
         check(self.L.rpgpu_submit(self.ctx, C.byref(job), C.c_void_p(s.cuda_stream)), self.ctx, "rpgpu_submit")
-        finish(data, d_seg_offsets, out.batches, out.records, out.decoded, out.summaries, out.totals, out.bitmap)
+        finish(data, d_seg_offsets, out.batches, out.records, out.decoded, out.summaries, out.totals, out.bitmap, sd, so)
         return out
 
     def segment_index(self, out: DeviceResult, base_offsets, step: int = abi.INDEX_DEFAULT_STEP, stream=None,
@@ -299,7 +354,7 @@ class Engine:
 
     def validate(self, data, seg_offsets, flags: int = abi.JOB_CRC | abi.JOB_PARSE, batch_capacity=None,
                  record_capacity=None, decoded_capacity=None, chunk_bytes: int = 0,
-                 layout: int = abi.LAYOUT_DISK) -> HostResult:
+                 layout: int = abi.LAYOUT_DISK, seeds=None) -> HostResult:
         """Convenience: allocate outputs, run, synchronize, copy back."""
         torch = _torch()
         offs = np.asarray(seg_offsets, dtype=np.uint64)
@@ -312,7 +367,7 @@ class Engine:
         if decoded_capacity is None:
             decoded_capacity = max(total * 8, 1 << 16) if flags & abi.JOB_DECODE else 1
         out = self.alloc_outputs(nseg, batch_capacity, record_capacity, decoded_capacity)
-        self.submit(data, offs, out, flags, chunk_bytes, layout=layout)
+        self.submit(data, offs, out, flags, chunk_bytes, layout=layout, seeds=seeds)
         torch.cuda.synchronize(data.device)
         return out.to_host()
 

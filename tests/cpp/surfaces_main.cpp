@@ -259,6 +259,22 @@ int main(int argc, char** argv) {
             }
             return 0;
         }
+        if (mode == "stamp" && argc == 7) {
+            // stamp <in> <positions.txt> <out> <next_offset> <flags>: storage::stamp_batches
+            std::vector<uint8_t> buf = slurp(argv[2]);
+            std::vector<size_t> pos;
+            {
+                std::ifstream f(argv[3]);
+                size_t v;
+                while (f >> v) pos.push_back(v);
+            }
+            const int64_t next = storage::stamp_batches(buf.data(), buf.size(), pos, std::atoll(argv[5]),
+                                                        (uint32_t)std::atoi(argv[6]));
+            std::ofstream f(argv[4], std::ios::binary);
+            f.write((const char*)buf.data(), (std::streamsize)buf.size());
+            std::printf("S %lld\n", (long long)next);
+            return 0;
+        }
         if (mode == "uncompress" && argc >= 5 && (argc - 2) % 3 == 0) {
             // one or more (codec, in, out) triples: one line each
             for (int a = 2; a + 2 < argc; a += 3) {

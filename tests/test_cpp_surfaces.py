@@ -412,3 +412,34 @@ def test_kafka_batch_reader(driver, rplib, oracle, engine, tmp_path):
     for name, data in cases.items():
         got = run(driver, "wire", write(tmp_path, name, data))
         assert got == ref_batch_reader(data, oracle), name
+
+
+# ---------------------------------------------------------------------------
+# GPU: the write side (storage::stamp_batches over rpgpu_stamp)
+# ---------------------------------------------------------------------------
+@pytest.mark.gpu
+def test_stamp_batches_surface(driver, oracle, rplib, tmp_path):
+    """storage::stamp_batches (disk_log_appender offsets + reset_size_checksum_
+    metadata + header_crc) == the oracle, and returns the appender's next
+    offset (last_offset + 1)."""
+    import synth
+    a = np.zeros(3 << 20, dtype=np.uint8)
+    synth.gen_segment(a, 1, seed=0xC5, batch_bytes=0, min_batch=61, max_batch=400000, weights=[40, 0, 15, 30, 0, 15])
+    r = oracle.run_job(a, [0, a.size], abi.JOB_CRC)
+    b = r.batches
+    end = int(b["file_pos"][-1]) + int(b["size_bytes"][-1])
+    seg = a[:end].copy()
+    pos = b["file_pos"].astype(np.uint64)
+    pl = (b["size_bytes"] - abi.HEADER_SIZE).astype(np.uint32)
+    for p in pos:
+        seg[int(p):int(p) + 16] = 0
+        seg[int(p) + 17:int(p) + 21] = 0
+    src, posf, out = tmp_path / "in.bin", tmp_path / "pos.txt", tmp_path / "out.bin"
+    seg.tofile(src)
+    posf.write_text(" ".join(str(int(p)) for p in pos))
+    lines = run(driver, "stamp", str(src), str(posf), str(out), "1000", str(abi.STAMP_OFFSETS | abi.STAMP_CRC))
+    want = oracle.stamp_batches(seg, pos, pl, 1000, abi.STAMP_OFFSETS | abi.STAMP_CRC)
+    got = np.fromfile(out, dtype=np.uint8)
+    np.testing.assert_array_equal(got, want)
+    nxt = 1000 + int(np.sum(b["last_offset_delta"].astype(np.int64) + 1))
+    assert lines == [f"S {nxt}"]

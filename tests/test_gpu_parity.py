@@ -354,8 +354,10 @@ def test_async_poll_wait_and_capacity_query(engine, oracle, rplib):
     ref = oracle.run_job(data, offs, flags)
     d = torch.from_numpy(data).cuda()
     nb, nrec, ndec = engine.query_capacity(d, offs, flags)
-    assert nb == len(ref.batches) and nrec == int(ref.totals["record_capacity_needed"])
-    assert ndec == int(ref.totals["decoded_capacity_needed"])
+    # the oracle's job fills the capacities it used: n_records index slots,
+    # decoded_bytes of arena
+    assert nb == len(ref.batches) and nrec == int(ref.totals["n_records"])
+    assert ndec == int(ref.totals["decoded_bytes"])
     out = engine.alloc_outputs(len(segs), nb, nrec, ndec)  # exactly what the query said
     p = engine.submit_async(d, offs, out, flags)
     polls = 0
@@ -385,3 +387,76 @@ def test_uncompress_batch_matches_single(engine, oracle):
             assert st == 0 and got == want, e["name"]
         else:
             assert st == abi.E_CODEC, e["name"]
+
+
+# ---------------------------------------------------------------------------
+# index-seeded discovery (SURVEY §8(b) segment-engine row, §8(f) row 2)
+# ---------------------------------------------------------------------------
+@pytest.mark.parametrize("kind", ["index", "every_batch", "garbage", "stale", "partial"])
+def test_index_seeded_discovery(engine, oracle, rplib, kind):
+    """Seeds from the segment index (what hydrate_from_buffer gives), every
+    batch, garbage positions, positions past the chain end and seeds for
+    some segments only: results identical to the unseeded oracle run."""
+    import torch
+    rng = np.random.default_rng(len(kind))
+    MIX = (1 << abi.CODEC_NONE) | (1 << abi.CODEC_LZ4) | (1 << abi.CODEC_SNAPPY)
+    segs = [gen(rplib, 3 << 20, 0, seed=0xC1),
+            gen(rplib, 3 << 20, 1, seed=0xC5, batch_bytes=0, min_batch=200, max_batch=1 << 20, codec_mix=MIX,
+                corrupt_payload_ppm=20000),
+            gen(rplib, 2 << 20, 2, seed=0xC5, batch_bytes=0, min_batch=61, max_batch=3000)]
+    offs = np.cumsum([0] + [s.size for s in segs]).astype(np.uint64)
+    data = np.concatenate(segs)
+    flags = abi.JOB_CRC | abi.JOB_PARSE | abi.JOB_DECODE
+    ref = oracle.run_job(data, offs, flags)
+    b = ref.batches
+    seeds = []
+    for k in range(len(segs)):
+        pos = b["file_pos"][b["segment"] == k].astype(np.uint64)
+        if kind == "index":
+            ix = oracle.segment_index(ref.batches, ref.summaries, [0] * len(segs))[k]
+            seeds.append(np.sort(ix[3]))
+        elif kind == "every_batch":
+            seeds.append(pos)
+        elif kind == "garbage":
+            seeds.append(np.sort(rng.integers(1, segs[k].size, 200).astype(np.uint64)))
+        elif kind == "stale":
+            seeds.append(np.concatenate([pos[::3], np.array([segs[k].size + 5, segs[k].size + 1 << 20], np.uint64)]))
+        else:
+            seeds.append(pos[::2] if k == 1 else np.zeros(0, np.uint64))
+    for chunk in (0, 65536):
+        d = torch.from_numpy(data).cuda()
+        got = engine.validate(d, offs, flags, chunk_bytes=chunk, seeds=seeds)
+        assert_same(got, ref, flags)
+
+
+def test_serialize_wire(engine, oracle, rplib):
+    """rpgpu_serialize_wire (kafka::writer_serialize_batch, response_writer.h:
+    241-276) == the restatement in tests/batchgen.disk_to_wire over whole
+    segments and over a sub-range; the record set validates in the wire
+    layout with the same verdicts."""
+    import torch
+    from tests import batchgen as bg
+    MIX = (1 << abi.CODEC_NONE) | (1 << abi.CODEC_LZ4) | (1 << abi.CODEC_SNAPPY)
+    segs = [gen(rplib, 2 << 20, 0, seed=0xC1),
+            gen(rplib, 3 << 20, 1, seed=0xC5, batch_bytes=0, min_batch=61, max_batch=600000, codec_mix=MIX)]
+    offs = np.cumsum([0] + [s.size for s in segs]).astype(np.uint64)
+    data = np.concatenate(segs)
+    d = torch.from_numpy(np.concatenate([data, np.zeros(16, np.uint8)])).cuda()[: data.size]
+    out = engine.alloc_outputs(len(segs), 4096, 1 << 16, 1)
+    engine.submit(d, offs, out, abi.JOB_CRC)
+    torch.cuda.synchronize()
+    want = b"".join(bg.disk_to_wire(s.tobytes()) for s in segs)
+    got = engine.serialize_wire(d, offs, out).cpu().numpy().tobytes()
+    assert got == want
+    h = out.to_host()
+    nb0 = int(h.summaries["n_batches"][0])
+    sub = engine.serialize_wire(d, offs, out, first=nb0 - 3, n=7).cpu().numpy().tobytes()
+    b = h.batches
+    lo = int(sum(int(x) for x in b["size_bytes"][:nb0 - 3]))
+    assert sub == want[lo:lo + int(sum(int(x) for x in b["size_bytes"][nb0 - 3:nb0 + 4]))]
+    wire = np.frombuffer(got, dtype=np.uint8).copy()
+    wres = engine.validate(torch.from_numpy(wire).cuda(), [0, wire.size], abi.JOB_CRC | abi.JOB_PARSE,
+                           layout=abi.LAYOUT_WIRE)
+    assert len(wres.batches) == len(b)
+    assert np.all(wres.batches["flags"] & abi.F_CRC_OK)
+    np.testing.assert_array_equal(wres.batches["base_offset"], b["base_offset"])
