@@ -1623,6 +1623,80 @@ struct SlabSink {
 constexpr uint32_t kWalkWin = 4096;  // staged stream bytes per wave (long pieces)
 
 
+namespace {
+DEV uint64_t rl64(uint64_t v, int l) {
+    return (uint64_t)rl((uint32_t)v, l) | ((uint64_t)rl((uint32_t)(v >> 32), l) << 32);
+}
+}  // namespace
+
+// The serial walk of one long raw snappy stream, tight: lane 0 reads each
+// tag and its extra bytes with one 8-byte LDS read from the staged window
+// and emits its record; the wave restages 4 KiB when the next tag is not
+// wholly inside.  (snappy_run through the generic window costs ~1 us per
+// tag on one lane; its checks are the same: DecompressAllTags over the
+// stream, SnappyArrayWriter's limits, AppendFromSelf's offset rule.)
+DEV void walk_snappy_long(const DeviceJob& j, Piece& pc, SlabSink& sink, lds_u8* win) {
+    typedef __attribute__((address_space(3))) const uint32_t lds_cu32;
+    const uint32_t l = lane();
+    const int64_t n = pc.s.n;
+    const uint64_t ulen = pc.ps.ulen;
+    int64_t ip = pc.ps.ip;
+    uint64_t op = (uint32_t)pc.ps.op;
+    int32_t st = 0;
+    while (st == 0 && !sink.cut) {
+        if (ip >= n) {
+            st = op == ulen ? 1 : -1;
+            break;
+        }
+        const int64_t w0 = ip & ~15ll;
+#pragma unroll
+        for (uint32_t k = 0; k < kWalkWin / 1024; k++) {
+            const uint4 v = ld16(pc.s, w0 + 1024 * k + 16 * l);
+            __builtin_memcpy(win + 1024 * k + 16 * l, &v, 16);
+        }
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+        // tags whose 5 bytes lie in the window (or that end the stream)
+        const int64_t wend = w0 + kWalkWin - 8;
+        if (l == 0) {
+            lds_cu32* w32 = (lds_cu32*)win;
+            while (ip < n && ip < wend) {
+                const uint32_t o = (uint32_t)(ip - w0);
+                const uint64_t q = (((uint64_t)w32[(o >> 2) + 1] << 32) | w32[o >> 2]) >> (8 * (o & 3));
+                const uint32_t c = (uint32_t)q & 0xFFu, t = c & 3;
+                const uint32_t x = (uint32_t)(q >> 8);
+                const int64_t extra = t == 0 ? (((c >> 2) >= 60) ? (int64_t)((c >> 2) - 59) : 0) : t == 1 ? 1 : t == 2 ? 2 : 4;
+                if (n - ip < 1 + extra) { st = -1; break; }
+                if (t == 0) {
+                    int64_t lit = (int64_t)(c >> 2) + 1;
+                    if (lit >= 61) lit = (int64_t)(extra == 4 ? x : x & ((1u << (8 * extra)) - 1u)) + 1;
+                    const int64_t lip = ip + 1 + extra;
+                    if (n - lip < lit || (int64_t)(ulen - op) < lit) { st = -1; break; }
+                    if (!sink.seq(make_uint4(0, 0, 0, 0), 0, (int32_t)lip, (int32_t)lit, 0, 0u, 0)) { ip = lip + lit; op += lit; break; }
+                    op += lit;
+                    ip = lip + lit;
+                } else {
+                    const int64_t len = t == 1 ? 4 + ((c >> 2) & 7) : (int64_t)(c >> 2) + 1;
+                    const uint64_t off = t == 1 ? (((c >> 5) << 8) | (x & 0xFFu)) : t == 2 ? (x & 0xFFFFu) : x;
+                    ip += 1 + extra;
+                    if (off == 0 || op < off || (int64_t)(ulen - op) < len) { st = -1; break; }
+                    if (!sink.seq(make_uint4(0, 0, 0, 0), 0, 0, 0, 0, (uint32_t)off, (int32_t)len)) { op += len; break; }
+                    op += len;
+                }
+            }
+        }
+        ip = (int64_t)rl64((uint64_t)ip, 0);
+        op = rl64(op, 0);
+        st = (int32_t)rl((uint32_t)st, 0);
+        sink.slab = rl(sink.slab, 0);
+        sink.pos = rl(sink.pos, 0);
+        sink.n = rl(sink.n, 0);
+        sink.cut = rl(sink.cut, 0);
+    }
+    pc.ps.ip = (int32_t)ip;
+    pc.ps.op = (int32_t)op;
+    pc.ps.st = st;
+}
+
 DEV void walk_long(const DeviceJob& j, uint32_t p, lds_u8* win) {
     const uint32_t l = lane();
 #ifdef RPGPU_DSTAMPS
@@ -1646,7 +1720,8 @@ DEV void walk_long(const DeviceJob& j, uint32_t p, lds_u8* win) {
             out.first_slab = fs;
             SlabSink sink{j.pool, j.slab_next, &j.counters[9], j.pool_slabs, fs, 0, 0, 0, {}, {}, {}};
             const int64_t n = pc.s.n;
-            for (;;) {
+            if (pc.kind & kBlkSnappy) walk_snappy_long(j, pc, sink, win);
+            else for (;;) {
                 // stage [w0, w0 + 4 KiB) of the stream (w0 16-aligned below ip)
                 const int64_t w0 = (int64_t)pc.ps.ip & ~15ll;
 #pragma unroll

@@ -4,7 +4,7 @@ set -e
 cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
 TAG=${1:-dec}
-timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 240 --timeout-method thread -k "c2 or c5 or codec or decode or uncompress or smoke or host_path" > gpurun_out/pytest_$TAG.log 2>&1 || { tail -60 gpurun_out/pytest_$TAG.log; exit 1; }
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 240 --timeout-method thread -k "c2 or c5 or codec or decode or uncompress or smoke or host_path or snappy or seeded" > gpurun_out/pytest_$TAG.log 2>&1 || { tail -60 gpurun_out/pytest_$TAG.log; exit 1; }
 tail -2 gpurun_out/pytest_$TAG.log
 timeout -k 10 400 python -u bench.py --steps 5 --warmup 1 --no-cpu-baseline --no-index --workloads c2,c5 > gpurun_out/bench_$TAG.json 2> gpurun_out/bench_$TAG.err || { tail -30 gpurun_out/bench_$TAG.err; exit 1; }
 python - gpurun_out/bench_$TAG.json <<'PY'

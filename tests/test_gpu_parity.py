@@ -460,3 +460,17 @@ def test_serialize_wire(engine, oracle, rplib):
     assert len(wres.batches) == len(b)
     assert np.all(wres.batches["flags"] & abi.F_CRC_OK)
     np.testing.assert_array_equal(wres.batches["base_offset"], b["base_offset"])
+
+
+@pytest.mark.parametrize("seed", [0x51, 0x52, 0x53])
+def test_raw_snappy_long_streams(engine, oracle, rplib, seed):
+    """Raw (non-xerial) snappy payloads of 20 KiB .. 1 MiB, the speculative
+    parallel walk's case, with 10 % of them bit-flipped (every snappy error
+    path: premature end, zero offset, copy before the output start, length
+    mismatch): identical to the oracle, decoded bytes included."""
+    segs = [gen(rplib, 6 << 20, i, seed=seed, batch_bytes=0, min_batch=20000, max_batch=1 << 20,
+                weights=[0, 0, 0, 0, 0, 1], corrupt_payload_ppm=100000) for i in range(2)]
+    flags = abi.JOB_CRC | abi.JOB_PARSE | abi.JOB_DECODE
+    got, ref = run_both(engine, oracle, segs, flags=flags)
+    assert_same(got, ref, flags)
+    assert np.sum((ref.batches["flags"] & abi.F_CODEC_OK) != 0) > 4
