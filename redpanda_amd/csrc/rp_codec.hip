@@ -935,8 +935,11 @@ DEV int in_varint(In& in, int64_t pos, int64_t n, uint32_t& v) {
 }
 
 
+#ifndef RPGPU_LONG_LZ4
+#define RPGPU_LONG_LZ4 65536u
+#endif
 DEV bool piece_is_long(uint32_t kind, uint32_t csize) {
-    return !(kind & kBlkRaw) && ((kind & kBlkWhole) || csize > 65536u);
+    return !(kind & kBlkRaw) && ((kind & kBlkWhole) || csize > RPGPU_LONG_LZ4);
 }
 
 // a long piece (walked by a wave in k_lz_walk): lane 0 appends it
@@ -1772,6 +1775,182 @@ DEV void walk_snappy_long(const DeviceJob& j, Piece& pc, SlabSink& sink, lds_u8*
     sink.cut = cut;
 }
 
+// a stream byte for a lane of the window-parallel walks: from the staged
+// window when inside it, else from memory (0 past the job's data)
+DEV uint32_t wbyte(const Src& s, const lds_u8* win, int64_t w0, int64_t q) {
+    if (q >= w0 && q < w0 + (int64_t)kWalkWin) return win[q - w0];
+    return (q >= 0 && q < s.rl) ? (uint32_t)s.p[q] : 0u;
+}
+
+// the stored records [pos & ~3, pos) back into the sink's registers (the
+// window-parallel walks store records directly; the serial walk then goes on
+// through the sink's four-record buffer)
+DEV void sink_resync(SlabSink& sink) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const uint32_t k = sink.pos & 3;
+    const uint4* q = (const uint4*)(sink.pool + (size_t)sink.slab * kSlabRecs + (sink.pos - k));
+    if (k > 0) sink.r0 = q[0];
+    if (k > 1) sink.r1 = q[1];
+    if (k > 2) sink.r2 = q[2];
+}
+
+// Window-parallel LZ4 block walk (the wave's own piece): lane l decodes the
+// sequence that would start at ip + l the way LZ4_decompress_generic's fast
+// loop does (token, literal length, offset, match length, next token); the
+// true sequences are found by readlane hops from ip, their output positions
+// by a prefix sum.  Only sequences the fast loop would take without
+// leaving it are handled here (every condition that sends the reference to
+// its safe loop, or could fail the block, hands the rest of the block to
+// the serial walk: the block's last ~64 output bytes and ~32 input bytes,
+// and anything unusual).  The history check is the walk's `need` bound, as
+// in lz4_run.  Advances pc.ps and the sink.
+DEV void walk_lz4_wave(const DeviceJob& j, Piece& pc, SlabSink& sink, lds_u8* win) {
+    typedef __attribute__((address_space(3))) const uint32_t lds_cu32;
+    const uint32_t l = lane();
+    const int64_t iend = pc.s.n, oend = (int64_t)pc.cap;
+    if (pc.ps.st != 0 || pc.ps.safe) return;
+    int64_t ip = pc.ps.ip, op = pc.ps.op;
+    int32_t need = pc.ps.need;
+    uint32_t slab = sink.slab, pos = sink.pos, nrec = sink.n;
+    bool cut = false;
+    int64_t w0 = -1;
+    lds_cu32* w32 = (lds_cu32*)win;
+    for (;;) {
+        if (w0 < 0 || ip + 72 > w0 + kWalkWin) {
+            w0 = ip & ~15ll;
+#pragma unroll
+            for (uint32_t k = 0; k < kWalkWin / 1024; k++) {
+                const uint4 v = ld16(pc.s, w0 + 1024 * k + 16 * l);
+                __builtin_memcpy(win + 1024 * k + 16 * l, &v, 16);
+            }
+            asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+        }
+        // the sequence that would start at ip + l (fast-loop rules)
+        const int64_t p = ip + l;
+        bool ok = p < iend;
+        int64_t ll = 0, ml = 0, lip = 0, nxt = -1;
+        uint32_t off = 0;
+        if (ok) {
+            const uint32_t o = (uint32_t)(p - w0);
+            const uint32_t token = (w32[o >> 2] >> (8 * (o & 3))) & 0xFFu;
+            int64_t q = p + 1;
+            ll = token >> 4;
+            if (ll == 15) {
+                if (q >= iend - 15) ok = false;  // initial error / near the end: serial
+                uint32_t b = 255;
+                while (ok && b == 255) {
+                    b = wbyte(pc.s, win, w0, q);
+                    q++;
+                    ll += b;
+                    if (q >= iend - 15) ok = false;
+                }
+                if (ok && q + ll > iend - 32) ok = false;  // the fast loop would go safe
+            } else if (q > iend - 17) {
+                ok = false;
+            }
+            if (ok) {
+                lip = q;
+                q += ll;
+                off = wbyte(pc.s, win, w0, q) | (wbyte(pc.s, win, w0, q + 1) << 8);
+                q += 2;
+                ml = token & 15;
+                if (ml == 15) {
+                    uint32_t b = 255;
+                    while (ok && b == 255) {
+                        b = wbyte(pc.s, win, w0, q);
+                        q++;
+                        ml += b;
+                        if (q >= iend - kLastLiterals + 1) ok = false;
+                    }
+                }
+                ml += kMinMatch;
+                nxt = q;
+            }
+        }
+        // the true sequences among the 64, up to the first one not handled here
+        uint64_t chain = 0;
+        int64_t qn = ip;
+        bool stop = false;
+        while (qn - ip < 64) {
+            const int k = (int)(qn - ip);
+            if (!rl((uint32_t)ok, k)) {
+                stop = true;
+                break;
+            }
+            chain |= 1ull << k;
+            qn = (int64_t)rl64((uint64_t)nxt, k);
+        }
+        // output positions; the op-dependent fast-loop conditions
+        const bool on = (chain >> l) & 1;
+        const uint64_t len = on ? (uint64_t)(ll + ml) : 0ull;
+        uint64_t incl = len;
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint64_t v = shfl_up64(incl, d);
+            if (l >= (uint32_t)d) incl += v;
+        }
+        const int64_t opt = op + (int64_t)(incl - len);  // output at the sequence start
+        const bool go_safe = on && ((ll >= 15 && opt + ll > oend - 32) || opt + ll + ml >= oend - kFastSafeDistance);
+        const uint64_t gm = __ballot(go_safe);
+        if (gm) {
+            chain &= (1ull << __builtin_ctzll(gm)) - 1;  // the sequences before it
+            stop = true;
+        }
+        const bool mine = (chain >> l) & 1;
+        // records in chain order (the sink's slab rules)
+        const uint32_t cnt = (uint32_t)__builtin_popcountll(chain);
+        const uint32_t rank = (uint32_t)__builtin_popcountll(chain & ((1ull << l) - 1));
+        const uint32_t room = kSlabRecs - pos;
+        uint32_t ns = 0xFFFFFFFFu, emit = cnt;
+        if (cnt && cnt >= room) {
+            ns = wave_fetch_add(&j.counters[9], 1u);
+            if (ns >= j.pool_slabs) {
+                emit = room;
+                cut = true;
+            } else if (l == 0) {
+                j.slab_next[slab] = ns;
+            }
+        }
+        int32_t d = INT32_MIN;
+        if (mine && rank < emit) {
+            const SeqRec r{(uint32_t)lip, (uint32_t)ll, (uint32_t)ml, off};
+            if (rank < room) j.pool[(size_t)slab * kSlabRecs + pos + rank] = r;
+            else j.pool[(size_t)ns * kSlabRecs + (rank - room)] = r;
+            d = (int32_t)off - (int32_t)(opt + ll);  // offset - match position
+        }
+        for (int m = 32; m > 0; m >>= 1) {
+            const int32_t v = __shfl_xor(d, m, 64);
+            d = v > d ? v : d;
+        }
+        need = d > need ? d : need;
+        nrec += emit;
+        if (cnt && cnt >= room && !cut) {
+            slab = ns;
+            pos = cnt - room;
+        } else {
+            pos += emit;
+        }
+        if (emit == 0) break;  // nothing handled here: the serial walk takes over at ip
+        // state after the last stored sequence
+        uint64_t m2 = chain;
+        uint32_t kk = 0;
+        for (uint32_t e = 0; e < emit; e++) {
+            kk = (uint32_t)__builtin_ctzll(m2);
+            m2 &= m2 - 1;
+        }
+        op += (int64_t)rl64(incl, (int)kk);
+        ip = (int64_t)rl64((uint64_t)nxt, (int)kk);
+        if (stop || cut || emit < cnt) break;
+    }
+    pc.ps.ip = (int32_t)ip;
+    pc.ps.op = (int32_t)op;
+    pc.ps.need = need;
+    sink.slab = slab;
+    sink.pos = pos;
+    sink.n = nrec;
+    sink.cut = cut;
+    sink_resync(sink);
+}
+
 DEV void walk_long(const DeviceJob& j, uint32_t p, lds_u8* win) {
     const uint32_t l = lane();
 #ifdef RPGPU_DSTAMPS
@@ -1797,7 +1976,7 @@ DEV void walk_long(const DeviceJob& j, uint32_t p, lds_u8* win) {
             const int64_t n = pc.s.n;
             const bool lanes_store = (pc.kind & kBlkSnappy) != 0;  // records already stored by the lanes
             if (lanes_store) walk_snappy_long(j, pc, sink, win);
-            else for (;;) {
+            else if (!sink.cut && (walk_lz4_wave(j, pc, sink, win), !sink.cut)) for (;;) {
                 // stage [w0, w0 + 4 KiB) of the stream (w0 16-aligned below ip)
                 const int64_t w0 = (int64_t)pc.ps.ip & ~15ll;
 #pragma unroll
