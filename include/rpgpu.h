@@ -412,6 +412,30 @@ int rpgpu_uncompress_batch(rpgpu_ctx* ctx, uint32_t n, const int* codecs, const 
                            int* status);
 
 /* ------------------------------------------------------------------------ */
+/* compression::compressor::compress (compression/compression.cc:17-33): the */
+/* write side's storage::internal::compress_batch (storage/parser_utils.cc:   */
+/* 97-111).  SURVEY.md §8(f) row 3.                                          */
+/* ------------------------------------------------------------------------ */
+
+/* Bytes compressor::compress can produce for n input bytes: the LZ4 frame
+ * (lz4_frame_compressor.cc:72-113) or the snappy-java stream over frag-byte
+ * iobuf fragments (snappy_java_compressor.cc:58-75; frag 0 = one fragment).
+ * 0 for other codecs. */
+size_t rpgpu_compress_bound(int codec, size_t n, size_t frag);
+
+/* n payloads compressed on the device in one round trip (host pointers), the
+ * bytes liblz4 1.9.3 / libsnappy 1.1.8 produce through the reference's
+ * wrappers, bit for bit: RPGPU_CODEC_LZ4 -> LZ4 frame {independent 64 KiB
+ * blocks, content size, level 1}; RPGPU_CODEC_SNAPPY -> snappy-java with one
+ * chunk per frag[i]-byte fragment (frag may be NULL: one fragment, a
+ * contiguous iobuf).  status[i]: RPGPU_OK; RPGPU_E_OVERFLOW when cap[i] <
+ * the output (out_len[i] then holds its size); RPGPU_E_CODEC for
+ * RPGPU_CODEC_NONE (the reference throws "nothing to compress");
+ * RPGPU_E_UNSUPPORTED for gzip / zstd. */
+int rpgpu_compress_batch(rpgpu_ctx* ctx, uint32_t n, const int* codecs, const void* const* in, const size_t* in_len,
+                         const size_t* frag, void* const* out, const size_t* cap, size_t* out_len, int* status);
+
+/* ------------------------------------------------------------------------ */
 /* Host segment path: pinned, double-buffered H2D of host-resident segments  */
 /* (log_replayer over files).  Segments are copied in chunks on a copy       */
 /* stream while the previous chunk validates.  Outputs are HOST pointers.    */

@@ -154,6 +154,61 @@ size_t ref_snappy_compress(const uint8_t* src, size_t n, uint8_t* dst, size_t ca
 
 size_t ref_snappy_bound(size_t n) { return snappy_max_compressed_length(n); }
 
+/* lz4_frame_compressor::compress (lz4_frame_compressor.cc:72-113): Begin,
+ * one Update per iobuf fragment (frag bytes each; 0 = one fragment), End.
+ * Returns the frame size, 0 on an lz4 error. */
+size_t ref_lz4f_compress_stream(const uint8_t* src, size_t n, size_t frag, uint8_t* dst, size_t cap) {
+    LZ4F_cctx* ctx = NULL;
+    if (LZ4F_isError(LZ4F_createCompressionContext(&ctx, LZ4F_VERSION))) return 0;
+    LZ4F_preferences_t prefs;
+    memset(&prefs, 0, sizeof prefs);
+    prefs.compressionLevel = 1;
+    prefs.frameInfo.blockMode = LZ4F_blockIndependent;
+    prefs.frameInfo.contentSize = n;
+    size_t need = LZ4F_compressBound(n, &prefs) + 4 + 19;
+    size_t r = 0;
+    if (need > cap) goto out;
+    size_t o = LZ4F_compressBegin(ctx, dst, cap, &prefs);
+    if (LZ4F_isError(o)) goto out;
+    if (frag == 0) frag = n ? n : 1;
+    for (size_t f = 0; f < n; f += frag) {
+        size_t len = n - f < frag ? n - f : frag;
+        size_t c = LZ4F_compressUpdate(ctx, dst + o, cap - o, src + f, len, NULL);
+        if (LZ4F_isError(c)) goto out;
+        o += c;
+    }
+    {
+        size_t c = LZ4F_compressEnd(ctx, dst + o, cap - o, NULL);
+        if (LZ4F_isError(c)) goto out;
+        r = o + c;
+    }
+out:
+    LZ4F_freeCompressionContext(ctx);
+    return r;
+}
+
+/* snappy_java_compressor::compress (snappy_java_compressor.cc:58-75) over
+ * frag-byte fragments (0 = one fragment); snappy_compress = RawCompress. */
+size_t ref_snappy_java_compress(const uint8_t* src, size_t n, size_t frag, uint8_t* dst, size_t cap) {
+    static const uint8_t hdr[16] = {0x82, 'S', 'N', 'A', 'P', 'P', 'Y', 0, 1, 0, 0, 0, 1, 0, 0, 0};
+    if (cap < 16) return 0;
+    memcpy(dst, hdr, 16);
+    size_t o = 16;
+    if (frag == 0) frag = n ? n : 1;
+    for (size_t f = 0; f < n; f += frag) {
+        size_t len = n - f < frag ? n - f : frag;
+        if (o + 4 + snappy_max_compressed_length(len) > cap) return 0;
+        size_t c = snappy_max_compressed_length(len);
+        if (snappy_compress((const char*)src + f, len, (char*)dst + o + 4, &c) != SNAPPY_OK) return 0;
+        dst[o] = (uint8_t)(c >> 24);
+        dst[o + 1] = (uint8_t)(c >> 16);
+        dst[o + 2] = (uint8_t)(c >> 8);
+        dst[o + 3] = (uint8_t)c;
+        o += 4 + c;
+    }
+    return o;
+}
+
 /* ------------------------------------------------------------------------ */
 /* CPU baseline of the decode path (bench.py cpu_baseline, C2 / C5): per     */
 /* batch of a disk segment, what the reference does on recovery + decode:   */

@@ -77,6 +77,15 @@ def lib():
                                             C.POINTER(C.c_double), C.POINTER(C.c_uint64)]
         L.rpo_stamp_batches.restype = None
         L.rpo_stamp_batches.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32, C.c_int64, C.c_uint32]
+        for name in ("rpo_lz4f_compress_bound",):
+            getattr(L, name).restype = C.c_size_t
+            getattr(L, name).argtypes = [C.c_size_t]
+        L.rpo_snappy_java_compress_bound.restype = C.c_size_t
+        L.rpo_snappy_java_compress_bound.argtypes = [C.c_size_t, C.c_size_t]
+        L.rpo_lz4f_compress.restype = C.c_size_t
+        L.rpo_lz4f_compress.argtypes = [C.c_void_p, C.c_size_t, C.c_void_p]
+        L.rpo_snappy_java_compress.restype = C.c_size_t
+        L.rpo_snappy_java_compress.argtypes = [C.c_void_p, C.c_size_t, C.c_size_t, C.c_void_p]
         L.rpo_segment_index.restype = C.c_int
         L.rpo_segment_index.argtypes = [C.c_void_p, C.c_uint64, C.c_void_p, C.c_uint32, C.c_uint64,
                                         C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]
@@ -111,6 +120,10 @@ def ref():
         R.ref_snappy_compress.argtypes = [C.c_void_p, C.c_size_t, C.c_void_p, C.c_size_t]
         R.ref_snappy_bound.restype = C.c_size_t
         R.ref_snappy_bound.argtypes = [C.c_size_t]
+        R.ref_lz4f_compress_stream.restype = C.c_size_t
+        R.ref_lz4f_compress_stream.argtypes = [C.c_void_p, C.c_size_t, C.c_size_t, C.c_void_p, C.c_size_t]
+        R.ref_snappy_java_compress.restype = C.c_size_t
+        R.ref_snappy_java_compress.argtypes = [C.c_void_p, C.c_size_t, C.c_size_t, C.c_void_p, C.c_size_t]
         R.ref_baseline_decode.restype = C.c_double
         R.ref_baseline_decode.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64, C.c_int, C.POINTER(C.c_uint64),
                                           C.POINTER(C.c_uint64)]
@@ -315,3 +328,35 @@ def stamp_batches(data: np.ndarray, positions, payload_lens, next_offset: int = 
     pl = np.ascontiguousarray(np.asarray(payload_lens, dtype=np.uint32))
     lib().rpo_stamp_batches(out.ctypes.data, pos.ctypes.data, pl.ctypes.data, len(pos), next_offset, flags)
     return out
+
+
+def compress(codec: int, data: bytes, frag: int = 0) -> bytes:
+    """Oracle of the write side's compressor::compress (rp_oracle.c):
+    codec 3 = lz4 frame (lz4_frame_compressor.cc:72-113), 2 = snappy-java
+    over `frag`-byte iobuf fragments (snappy_java_compressor.cc:58-75)."""
+    src = np.frombuffer(bytes(data), dtype=np.uint8) if len(data) else np.zeros(1, np.uint8)
+    L = lib()
+    if codec == 3:
+        out = np.zeros(L.rpo_lz4f_compress_bound(len(data)), np.uint8)
+        n = L.rpo_lz4f_compress(src.ctypes.data, len(data), out.ctypes.data)
+    elif codec == 2:
+        out = np.zeros(L.rpo_snappy_java_compress_bound(len(data), frag), np.uint8)
+        n = L.rpo_snappy_java_compress(src.ctypes.data, len(data), frag, out.ctypes.data)
+    else:
+        raise ValueError(codec)
+    return out[:n].tobytes()
+
+
+def ref_compress(codec: int, data: bytes, frag: int = 0):
+    """The same through the reference's codec libraries (oracle/_ref), or
+    None when the harness is absent."""
+    R = ref()
+    if R is None:
+        return None
+    src = np.frombuffer(bytes(data), dtype=np.uint8) if len(data) else np.zeros(1, np.uint8)
+    cap = 2 * len(data) + (256 << 10)
+    out = np.zeros(cap, np.uint8)
+    f = R.ref_lz4f_compress_stream if codec == 3 else R.ref_snappy_java_compress
+    n = f(src.ctypes.data, len(data), frag, out.ctypes.data, cap)
+    assert n > 0
+    return out[:n].tobytes()

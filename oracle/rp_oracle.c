@@ -1335,3 +1335,316 @@ void rpo_stamp_batches(uint8_t* data, const uint64_t* pos, const uint32_t* plen,
         rpo_header_to_disk(&h, p);
     }
 }
+
+/* ========================================================================== */
+/* Write side: compression::compressor::compress for lz4 and snappy          */
+/* (compression/compression.cc:17-33).                                       */
+/*                                                                           */
+/* lz4: lz4_frame_compressor::compress (compression/internal/                */
+/* lz4_frame_compressor.cc:72-113): LZ4F_compressBegin / Update (one call    */
+/* per iobuf fragment) / End with prefs {compressionLevel 1, blockMode       */
+/* independent, contentSize = input size}, everything else 0.  liblz4 1.9.3  */
+/* (the reference's system dependency, compression/CMakeLists.txt) then      */
+/* frames the input as 64 KiB blocks (LZ4F_max64KB, the default block size   */
+/* id), whatever the fragmentation: Update buffers partial blocks.  Each     */
+/* block is LZ4F_makeBlock -> LZ4F_compressBlock ->                          */
+/* LZ4_compress_fast_extState_fastReset(acceleration 1, dstCapacity =        */
+/* srcSize - 1) on a table LZ4_prepareTable clears (every block is >= 4 KiB  */
+/* or follows a 64 KiB one), i.e. LZ4_compress_generic(byU16, noDict,        */
+/* noDictIssue, limitedOutput); 0 ("does not fit") makes a raw block.        */
+/*                                                                           */
+/* snappy: snappy_java_compressor::compress (compression/internal/           */
+/* snappy_java_compressor.cc:58-75): magic, version 1 and min version 1      */
+/* (little endian, as the reference appends them), then per iobuf fragment   */
+/* a big-endian int32 length and snappy::RawCompress of the fragment:        */
+/* libsnappy 1.1.8 Compress = varint length + CompressFragment per 64 KiB    */
+/* block with a fresh hash table of CalculateTableSize(block) entries.       */
+/*                                                                           */
+/* Pinned against the libraries through oracle/_ref (codec_ref.c            */
+/* ref_lz4f_compress_stream / ref_snappy_java_compress: the reference's      */
+/* driver loops) in tests/test_compress.py.                                  */
+/* ========================================================================== */
+enum { LZC_MINMATCH = 4, LZC_LASTLITERALS = 5, LZC_MFLIMIT = 12, LZC_MINLENGTH = 13, LZC_SKIPTRIGGER = 6,
+       LZC_HASHLOG_U16 = 13 };
+
+static inline uint32_t lz4_hash_u16(uint32_t seq) { return (seq * 2654435761u) >> (32 - LZC_HASHLOG_U16); }
+
+/* LZ4_count(pIn, pMatch, pInLimit) */
+static uint32_t lz4_count(const uint8_t* s, uint32_t in, uint32_t match, uint32_t limit) {
+    uint32_t start = in;
+    while (in < limit && s[in] == s[match]) { in++; match++; }
+    return in - start;
+}
+
+/* LZ4_compress_generic_validated (lz4 1.9.3 lz4.c), byU16 / noDict /
+ * noDictIssue / limitedOutput / acceleration 1, on a zeroed table: the
+ * compressed size, or 0 when it does not fit in cap bytes. */
+int rpo_lz4_compress_block(const uint8_t* s, int n, uint8_t* dst, int cap) {
+    uint16_t table[1 << LZC_HASHLOG_U16];
+    memset(table, 0, sizeof table);
+    if (n > 65547 - 1) return 0;
+    uint32_t ip = 0, anchor = 0;
+    const uint32_t iend = (uint32_t)n, mflimit_plus_one = iend - LZC_MFLIMIT + 1, matchlimit = iend - LZC_LASTLITERALS;
+    int64_t op = 0;
+    const int64_t olimit = cap;
+    uint32_t forward_h = 0, match = 0;
+    if (n < LZC_MINLENGTH) goto last_literals;
+    table[lz4_hash_u16(rd32(s + ip))] = (uint16_t)ip;
+    ip++;
+    forward_h = lz4_hash_u16(rd32(s + ip));
+    for (;;) {
+        int64_t token;
+        {
+            uint32_t forward_ip = ip;
+            int step = 1, search_match_nb = 1 << LZC_SKIPTRIGGER;
+            for (;;) {
+                const uint32_t h = forward_h, current = forward_ip;
+                const uint32_t match_index = table[h];
+                ip = forward_ip;
+                forward_ip += (uint32_t)step;
+                step = search_match_nb++ >> LZC_SKIPTRIGGER;
+                if (forward_ip > mflimit_plus_one) goto last_literals;
+                match = match_index;
+                forward_h = lz4_hash_u16(rd32(s + forward_ip));
+                table[h] = (uint16_t)current;
+                /* byU16 with LZ4_DISTANCE_MAX == 65535: no distance test */
+                if (rd32(s + match) == rd32(s + ip)) break;
+            }
+        }
+        /* catch up */
+        while (ip > anchor && match > 0 && s[ip - 1] == s[match - 1]) { ip--; match--; }
+        {
+            const uint32_t lit = ip - anchor;
+            token = op++;
+            if (op + lit + (2 + 1 + LZC_LASTLITERALS) + lit / 255 > olimit) return 0;
+            if (lit >= 15) {
+                int64_t len = (int64_t)lit - 15;
+                dst[token] = 15 << 4;
+                for (; len >= 255; len -= 255) dst[op++] = 255;
+                dst[op++] = (uint8_t)len;
+            } else {
+                dst[token] = (uint8_t)(lit << 4);
+            }
+            memcpy(dst + op, s + anchor, lit);
+            op += lit;
+        }
+    next_match:
+        dst[op] = (uint8_t)(ip - match);
+        dst[op + 1] = (uint8_t)((ip - match) >> 8);
+        op += 2;
+        {
+            uint32_t mc = lz4_count(s, ip + LZC_MINMATCH, match + LZC_MINMATCH, matchlimit);
+            ip += mc + LZC_MINMATCH;
+            if (op + (1 + LZC_LASTLITERALS) + (mc + 240) / 255 > olimit) return 0;
+            if (mc >= 15) {
+                dst[token] += 15;
+                mc -= 15;
+                /* LZ4_write32(0xFFFFFFFF) strides: 255 bytes, then mc % 255 */
+                while (mc >= 255) { dst[op++] = 255; mc -= 255; }
+                dst[op++] = (uint8_t)mc;
+            } else {
+                dst[token] += (uint8_t)mc;
+            }
+        }
+        anchor = ip;
+        if (ip >= mflimit_plus_one) break;
+        table[lz4_hash_u16(rd32(s + ip - 2))] = (uint16_t)(ip - 2);
+        {
+            const uint32_t h = lz4_hash_u16(rd32(s + ip));
+            const uint32_t match_index = table[h];
+            match = match_index;
+            table[h] = (uint16_t)ip;
+            if (rd32(s + match) == rd32(s + ip)) {
+                token = op++;
+                dst[token] = 0;
+                goto next_match;
+            }
+        }
+        forward_h = lz4_hash_u16(rd32(s + ++ip));
+    }
+last_literals: {
+        const uint64_t last = iend - anchor;
+        if (op + (int64_t)last + 1 + (int64_t)((last + 255 - 15) / 255) > olimit) return 0;
+        if (last >= 15) {
+            uint64_t acc = last - 15;
+            dst[op++] = 15 << 4;
+            for (; acc >= 255; acc -= 255) dst[op++] = 255;
+            dst[op++] = (uint8_t)acc;
+        } else {
+            dst[op++] = (uint8_t)(last << 4);
+        }
+        memcpy(dst + op, s + anchor, last);
+        op += (int64_t)last;
+    }
+    return (int)op;
+}
+
+/* bytes lz4_frame_compressor::compress produces at most */
+size_t rpo_lz4f_compress_bound(size_t n) {
+    const size_t nb = (n + 65535) / 65536;
+    return 15 + nb * (4 + 65536) + 4;
+}
+
+static void wr32le(uint8_t* p, uint32_t v) { p[0] = (uint8_t)v; p[1] = (uint8_t)(v >> 8); p[2] = (uint8_t)(v >> 16); p[3] = (uint8_t)(v >> 24); }
+
+/* the frame; returns its size (cap >= rpo_lz4f_compress_bound(n)) */
+size_t rpo_lz4f_compress(const uint8_t* s, size_t n, uint8_t* dst) {
+    size_t o = 0;
+    wr32le(dst, 0x184D2204u);
+    o = 4;
+    dst[o++] = (uint8_t)(0x40 | 0x20 | (n > 0 ? 0x08 : 0));  /* version 01, independent blocks, content size */
+    dst[o++] = 0x40;                                        /* max64KB */
+    if (n > 0) {
+        wr32le(dst + o, (uint32_t)n);
+        wr32le(dst + o + 4, (uint32_t)((uint64_t)n >> 32));
+        o += 8;
+    }
+    dst[o] = (uint8_t)((rpo_xxh32(dst + 4, o - 4, 0) >> 8) & 0xFF);
+    o++;
+    for (size_t b = 0; b < n; b += 65536) {
+        const int len = (int)(n - b < 65536 ? n - b : 65536);
+        const int c = rpo_lz4_compress_block(s + b, len, dst + o + 4, len - 1);
+        if (c == 0) {
+            wr32le(dst + o, (uint32_t)len | 0x80000000u);
+            memcpy(dst + o + 4, s + b, (size_t)len);
+            o += 4 + (size_t)len;
+        } else {
+            wr32le(dst + o, (uint32_t)c);
+            o += 4 + (size_t)c;
+        }
+    }
+    wr32le(dst + o, 0);
+    return o + 4;
+}
+
+/* snappy 1.1.8 */
+static inline uint32_t snappy_hash(uint32_t v, int shift) { return (v * 0x1e35a7bdu) >> shift; }
+static int log2_floor(uint32_t x) { int r = -1; while (x) { x >>= 1; r++; } return r; }
+
+static size_t snappy_emit_literal(uint8_t* op, const uint8_t* lit, uint32_t len) {
+    const uint32_t nn = len - 1;
+    size_t o = 0;
+    if (nn < 60) {
+        op[o++] = (uint8_t)(nn << 2);
+    } else {
+        const int count = (log2_floor(nn) >> 3) + 1;
+        op[o++] = (uint8_t)((59 + count) << 2);
+        for (int i = 0; i < count; i++) op[o++] = (uint8_t)(nn >> (8 * i));
+    }
+    memcpy(op + o, lit, len);
+    return o + len;
+}
+
+/* EmitCopyAtMost64 */
+static size_t snappy_copy64(uint8_t* op, uint32_t offset, uint32_t len) {
+    if (len < 12 && offset < 2048) {
+        op[0] = (uint8_t)(1 + ((len - 4) << 2) + ((offset >> 3) & 0xe0));
+        op[1] = (uint8_t)(offset & 0xff);
+        return 2;
+    }
+    op[0] = (uint8_t)(2 + ((len - 1) << 2));
+    op[1] = (uint8_t)offset;
+    op[2] = (uint8_t)(offset >> 8);
+    return 3;
+}
+
+static size_t snappy_emit_copy(uint8_t* op, uint32_t offset, uint32_t len) {
+    size_t o = 0;
+    if (len < 12) return snappy_copy64(op, offset, len);
+    while (len >= 68) { o += snappy_copy64(op + o, offset, 64); len -= 64; }
+    if (len > 64) { o += snappy_copy64(op + o, offset, 60); len -= 60; }
+    o += snappy_copy64(op + o, offset, len);
+    return o;
+}
+
+/* CompressFragment over one block of at most 64 KiB */
+size_t rpo_snappy_compress_block(const uint8_t* s, uint32_t n, uint8_t* op) {
+    uint16_t table[1 << 14];
+    uint32_t tsize = 256;
+    if (n > (1u << 14)) tsize = 1u << 14;
+    else if (n >= 256) tsize = 2u << log2_floor(n - 1);
+    if (tsize < 256) tsize = 256;
+    memset(table, 0, tsize * sizeof(uint16_t));
+    const int shift = 32 - log2_floor(tsize);
+    uint32_t ip = 0, next_emit = 0;
+    size_t o = 0;
+    if (n >= 15) {
+        const uint32_t ip_limit = n - 15;
+        uint32_t next_hash = snappy_hash(rd32(s + ++ip), shift);
+        for (;;) {
+            uint32_t skip = 32, next_ip = ip, candidate;
+            do {
+                ip = next_ip;
+                const uint32_t hash = next_hash;
+                const uint32_t between = skip >> 5;
+                skip += between;
+                next_ip = ip + between;
+                if (next_ip > ip_limit) goto emit_remainder;
+                next_hash = snappy_hash(rd32(s + next_ip), shift);
+                candidate = table[hash];
+                table[hash] = (uint16_t)ip;
+            } while (rd32(s + ip) != rd32(s + candidate));
+            o += snappy_emit_literal(op + o, s + next_emit, ip - next_emit);
+            uint32_t cand_bytes;
+            do {
+                const uint32_t base = ip;
+                uint32_t matched = 4;
+                while (ip + matched < n && s[candidate + matched] == s[ip + matched]) matched++;
+                ip += matched;
+                o += snappy_emit_copy(op + o, base - candidate, matched);
+                next_emit = ip;
+                if (ip >= ip_limit) goto emit_remainder;
+                table[snappy_hash(rd32(s + ip - 1), shift)] = (uint16_t)(ip - 1);
+                const uint32_t cur_hash = snappy_hash(rd32(s + ip), shift);
+                candidate = table[cur_hash];
+                cand_bytes = rd32(s + candidate);
+                table[cur_hash] = (uint16_t)ip;
+            } while (rd32(s + ip) == cand_bytes);
+            next_hash = snappy_hash(rd32(s + ip + 1), shift);
+            ++ip;
+        }
+    }
+emit_remainder:
+    if (next_emit < n) o += snappy_emit_literal(op + o, s + next_emit, n - next_emit);
+    return o;
+}
+
+/* snappy::RawCompress: varint length + the blocks */
+size_t rpo_snappy_raw_compress(const uint8_t* s, size_t n, uint8_t* dst) {
+    size_t o = 0;
+    uint32_t v = (uint32_t)n;
+    while (v >= 128) { dst[o++] = (uint8_t)(v | 128); v >>= 7; }
+    dst[o++] = (uint8_t)v;
+    for (size_t b = 0; b < n; b += 65536) {
+        const uint32_t len = (uint32_t)(n - b < 65536 ? n - b : 65536);
+        o += rpo_snappy_compress_block(s + b, len, dst + o);
+    }
+    return o;
+}
+
+/* snappy::MaxCompressedLength */
+static size_t snappy_max_len(size_t n) { return 32 + n + n / 6; }
+
+/* fragments of frag bytes (0: one fragment) */
+size_t rpo_snappy_java_compress_bound(size_t n, size_t frag) {
+    if (frag == 0 || frag > n) frag = n ? n : 1;
+    const size_t nf = n ? (n + frag - 1) / frag : 0;
+    return 16 + nf * (4 + snappy_max_len(frag));
+}
+
+size_t rpo_snappy_java_compress(const uint8_t* s, size_t n, size_t frag, uint8_t* dst) {
+    static const uint8_t hdr[16] = {0x82, 'S', 'N', 'A', 'P', 'P', 'Y', 0, 1, 0, 0, 0, 1, 0, 0, 0};
+    memcpy(dst, hdr, 16);
+    size_t o = 16;
+    if (frag == 0) frag = n ? n : 1;
+    for (size_t f = 0; f < n; f += frag) {
+        const size_t len = n - f < frag ? n - f : frag;
+        const size_t c = rpo_snappy_raw_compress(s + f, len, dst + o + 4);
+        dst[o] = (uint8_t)(c >> 24);
+        dst[o + 1] = (uint8_t)(c >> 16);
+        dst[o + 2] = (uint8_t)(c >> 8);
+        dst[o + 3] = (uint8_t)c;
+        o += 4 + c;
+    }
+    return o;
+}

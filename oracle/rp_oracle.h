@@ -160,6 +160,16 @@ int rpo_segment_index(const rpgpu_batch_result* batches, uint64_t batch_cap,
 void rpo_stamp_batches(uint8_t* data, const uint64_t* pos, const uint32_t* plen, uint32_t n, int64_t next_offset,
                        uint32_t flags);
 
+/* Write side: compression::compressor::compress (lz4 frame, snappy-java
+ * with `frag`-byte iobuf fragments, 0 = one fragment), see rp_oracle.c */
+int rpo_lz4_compress_block(const uint8_t* s, int n, uint8_t* dst, int cap);
+size_t rpo_lz4f_compress_bound(size_t n);
+size_t rpo_lz4f_compress(const uint8_t* s, size_t n, uint8_t* dst);
+size_t rpo_snappy_compress_block(const uint8_t* s, uint32_t n, uint8_t* op);
+size_t rpo_snappy_raw_compress(const uint8_t* s, size_t n, uint8_t* dst);
+size_t rpo_snappy_java_compress_bound(size_t n, size_t frag);
+size_t rpo_snappy_java_compress(const uint8_t* s, size_t n, size_t frag, uint8_t* dst);
+
 #ifdef __cplusplus
 }
 #endif

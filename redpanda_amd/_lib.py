@@ -91,6 +91,8 @@ def load():
         "rpgpu_set_timing": (i32, [vp, i32]),
         "rpgpu_uncompress": (i32, [vp, i32, vp, sz, vp, sz, C.POINTER(sz)]),
         "rpgpu_uncompress_batch": (i32, [vp, u32, vp, vp, vp, vp, vp, vp, vp]),
+        "rpgpu_compress_batch": (i32, [vp, u32, vp, vp, vp, vp, vp, vp, vp, vp]),
+        "rpgpu_compress_bound": (C.c_size_t, [C.c_int, C.c_size_t, C.c_size_t]),
         "rpgpu_submit_async": (i32, [vp, C.POINTER(JobC), vp, C.POINTER(vp)]),
         "rpgpu_poll": (i32, [vp]),
         "rpgpu_wait": (i32, [vp]),

@@ -187,6 +187,21 @@ struct UncItem {
     uint64_t dst, cap;  // output slot [dst, dst + cap) (cap includes 16 bytes of wild-copy room)
     int32_t codec, pad;
 };
+// compressor::compress (rp_compress.hip): 64 KiB blocks into scratch slots
+// of kCompSlot bytes (>= snappy::MaxCompressedLength(65536)), then one frame
+// per payload
+constexpr uint32_t kCompSlot = 76800;
+struct CompBlock {
+    uint64_t src;                    // staged input offset (4-byte aligned, 8 readable bytes past the block)
+    uint32_t n, codec;               // block bytes (<= 65536), RPGPU_CODEC_LZ4 / _SNAPPY
+    uint32_t frag_len, frag_blocks;  // snappy: on a fragment's first block, the fragment's bytes and blocks
+};
+struct CompPayload {
+    uint64_t n, out;                 // input bytes; output offset
+    uint32_t first, nblocks, codec, pad;
+};
+hipError_t launch_compress(const uint8_t* in, const CompBlock* blocks, uint32_t nb, const CompPayload* pay, uint32_t np,
+                           uint8_t* scratch, uint32_t* sizes, uint8_t* out, uint64_t* out_len, hipStream_t s);
 hipError_t launch_uncompress_many(const UncItem* items, uint32_t count, const uint8_t* in, uint64_t in_total,
                                   uint8_t* out, int64_t* res, hipStream_t s);
 hipError_t launch_finalize(const DeviceJob& j, hipStream_t s);

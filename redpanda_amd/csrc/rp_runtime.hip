@@ -888,6 +888,108 @@ int rpgpu_uncompress_batch(rpgpu_ctx* c, uint32_t n, const int* codecs, const vo
     return RPGPU_OK;
 }
 
+// compressor::compress for lz4 / snappy (rp_compress.hip)
+size_t rpgpu_compress_bound(int codec, size_t n, size_t frag) {
+    if (codec == RPGPU_CODEC_LZ4) return 15 + ((n + 65535) / 65536) * (4 + 65536) + 4;
+    if (codec == RPGPU_CODEC_SNAPPY) {
+        if (frag == 0 || frag > n) frag = n ? n : 1;
+        const size_t nf = n ? (n + frag - 1) / frag : 0;
+        return 16 + nf * (4 + 32 + frag + frag / 6);  // snappy::MaxCompressedLength per fragment
+    }
+    return 0;
+}
+
+int rpgpu_compress_batch(rpgpu_ctx* c, uint32_t n, const int* codecs, const void* const* in, const size_t* in_len,
+                         const size_t* frag, void* const* out, const size_t* cap, size_t* out_len, int* status) {
+    if (!c || (n && (!codecs || !in || !in_len || !out || !cap || !out_len || !status))) return RPGPU_E_INVALID;
+    std::vector<uint32_t> dev;
+    std::vector<CompPayload> pays;
+    std::vector<CompBlock> blocks;
+    std::vector<uint64_t> src_off;
+    uint64_t in_total = 0, out_total = 0;
+    for (uint32_t i = 0; i < n; i++) {
+        out_len[i] = 0;
+        const int codec = codecs[i];
+        if (codec < 0 || codec > RPGPU_CODEC_ZSTD || (!in[i] && in_len[i])) { status[i] = RPGPU_E_INVALID; continue; }
+        if (codec == RPGPU_CODEC_NONE) { status[i] = RPGPU_E_CODEC; continue; }
+        if (codec == RPGPU_CODEC_GZIP || codec == RPGPU_CODEC_ZSTD) { status[i] = RPGPU_E_UNSUPPORTED; continue; }
+        if (in_len[i] > (1ull << 32)) { status[i] = RPGPU_E_INVALID; continue; }
+        const uint64_t len = in_len[i];
+        CompPayload p;
+        p.n = len;
+        p.out = out_total;
+        p.first = (uint32_t)blocks.size();
+        p.codec = (uint32_t)codec;
+        p.pad = 0;
+        uint64_t fr = (codec == RPGPU_CODEC_SNAPPY && frag && frag[i]) ? frag[i] : len;
+        if (fr == 0) fr = 1;
+        for (uint64_t f = 0; f < len; f += (codec == RPGPU_CODEC_LZ4 ? len : fr)) {
+            // lz4: the frame's 64 KiB blocks whatever the fragmentation;
+            // snappy: each fragment is a RawCompress of its own
+            const uint64_t flen = codec == RPGPU_CODEC_LZ4 ? len : std::min<uint64_t>(fr, len - f);
+            const uint32_t nbk = (uint32_t)((flen + 65535) / 65536);
+            for (uint32_t k = 0; k < nbk; k++) {
+                CompBlock b;
+                b.src = in_total + f + (uint64_t)k * 65536;
+                b.n = (uint32_t)std::min<uint64_t>(65536, flen - (uint64_t)k * 65536);
+                b.codec = (uint32_t)codec;
+                b.frag_len = k == 0 ? (uint32_t)flen : 0;
+                b.frag_blocks = k == 0 ? nbk : 0;
+                blocks.push_back(b);
+            }
+        }
+        p.nblocks = (uint32_t)blocks.size() - p.first;
+        pays.push_back(p);
+        dev.push_back(i);
+        src_off.push_back(in_total);
+        in_total += align_up(len + 8, 16);
+        out_total += align_up(rpgpu_compress_bound(codec, len, fr), 16);
+        status[i] = RPGPU_E_CODEC;
+    }
+    if (pays.empty()) return RPGPU_OK;
+    hipSetDevice(c->device);
+    hipStream_t s = c->stream;
+    const uint32_t np = (uint32_t)pays.size(), nb = (uint32_t)blocks.size();
+    // device: [inputs][blocks][payloads] | [out_len][sizes][outputs][scratch];
+    // host (pinned): the first part, then out_len + outputs coming back
+    const size_t o_blk = align_up(in_total + 16, 256), o_pay = align_up(o_blk + (size_t)nb * sizeof(CompBlock), 256);
+    const size_t o_len = align_up(o_pay + (size_t)np * sizeof(CompPayload), 256);
+    const size_t o_sz = align_up(o_len + (size_t)np * 8, 256), o_out = align_up(o_sz + (size_t)nb * 4, 256);
+    const size_t o_scr = align_up(o_out + out_total, 256), total = o_scr + (size_t)nb * kCompSlot;
+    if (total > c->bd_bytes) {
+        if (c->bd) { HIPCHK(c, hipStreamSynchronize(s)); HIPCHK(c, hipFree(c->bd)); c->bd = nullptr; c->bd_bytes = 0; }
+        if (hipMalloc(&c->bd, total) != hipSuccess) { c->bd = nullptr; return fail(c, RPGPU_E_NOMEM, "compress staging"); }
+        c->bd_bytes = total;
+    }
+    if (o_scr > c->bh_bytes) {
+        if (c->bh) { HIPCHK(c, hipStreamSynchronize(s)); HIPCHK(c, hipHostFree(c->bh)); c->bh = nullptr; c->bh_bytes = 0; }
+        if (hipHostMalloc(&c->bh, o_scr, hipHostMallocDefault) != hipSuccess) { c->bh = nullptr; return fail(c, RPGPU_E_NOMEM, "compress pinned staging"); }
+        c->bh_bytes = o_scr;
+    }
+    uint8_t* h = (uint8_t*)c->bh;
+    uint8_t* d = (uint8_t*)c->bd;
+    std::memset(h, 0, o_blk);
+    for (uint32_t k = 0; k < np; k++)
+        if (pays[k].n) std::memcpy(h + src_off[k], in[dev[k]], pays[k].n);
+    std::memcpy(h + o_blk, blocks.data(), nb * sizeof(CompBlock));
+    std::memcpy(h + o_pay, pays.data(), np * sizeof(CompPayload));
+    HIPCHK(c, hipMemcpyAsync(d, h, o_len, hipMemcpyHostToDevice, s));
+    HIPCHK(c, launch_compress(d, (const CompBlock*)(d + o_blk), nb, (const CompPayload*)(d + o_pay), np, d + o_scr,
+                              (uint32_t*)(d + o_sz), d + o_out, (uint64_t*)(d + o_len), s));
+    HIPCHK(c, hipMemcpyAsync(h + o_len, d + o_len, np * 8, hipMemcpyDeviceToHost, s));
+    HIPCHK(c, hipMemcpyAsync(h + o_out, d + o_out, out_total, hipMemcpyDeviceToHost, s));
+    HIPCHK(c, hipStreamSynchronize(s));
+    const uint64_t* lens = (const uint64_t*)(h + o_len);
+    for (uint32_t k = 0; k < np; k++) {
+        const uint32_t i = dev[k];
+        out_len[i] = (size_t)lens[k];
+        if (out_len[i] > cap[i]) { status[i] = RPGPU_E_OVERFLOW; continue; }
+        std::memcpy(out[i], h + o_out + pays[k].out, out_len[i]);
+        status[i] = RPGPU_OK;
+    }
+    return RPGPU_OK;
+}
+
 // ---------------------------------------------------------------------------
 // Host segment path (log_replayer over files, storage/log_replayer.cc:95-114):
 // host-resident segments are grouped into staging groups of at most

@@ -195,6 +195,26 @@ class Engine:
         check(self.L.rpgpu_uncompress_batch(self.ctx, n, ci, ip, il, op, oc, ol, st), self.ctx, "rpgpu_uncompress_batch")
         return [(int(st[i]), outs[i][: ol[i]].tobytes() if st[i] == 0 else int(ol[i])) for i in range(n)]
 
+    def compress_batch(self, codecs, payloads, frags=None, caps=None):
+        """rpgpu_compress_batch (compressor::compress on the device): [(status,
+        bytes)] per payload — lz4 frames / snappy-java streams (frags[i]: the
+        iobuf fragment size, 0 = one fragment)."""
+        n = len(payloads)
+        srcs = [np.frombuffer(bytes(p), dtype=np.uint8) if len(p) else np.zeros(1, np.uint8) for p in payloads]
+        frags = list(frags) if frags is not None else [0] * n
+        caps = caps or [max(int(self.L.rpgpu_compress_bound(c, len(p), f)), 1) for c, p, f in zip(codecs, payloads, frags)]
+        outs = [np.zeros(max(c, 1), dtype=np.uint8) for c in caps]
+        ci = (C.c_int * max(n, 1))(*codecs)
+        ip = (C.c_void_p * max(n, 1))(*[s.ctypes.data for s in srcs])
+        il = (C.c_size_t * max(n, 1))(*[len(p) for p in payloads])
+        fr = (C.c_size_t * max(n, 1))(*frags)
+        op = (C.c_void_p * max(n, 1))(*[o.ctypes.data for o in outs])
+        oc = (C.c_size_t * max(n, 1))(*caps)
+        ol = (C.c_size_t * max(n, 1))()
+        st = (C.c_int * max(n, 1))()
+        check(self.L.rpgpu_compress_batch(self.ctx, n, ci, ip, il, fr, op, oc, ol, st), self.ctx, "rpgpu_compress_batch")
+        return [(int(st[i]), outs[i][: ol[i]].tobytes() if st[i] == 0 else int(ol[i])) for i in range(n)]
+
     def stamp(self, data, positions, payload_lens, next_offset: int = 0,
               flags: int = abi.STAMP_OFFSETS | abi.STAMP_CRC, stream=None):
         """rpgpu_stamp: stamp the headers of disk-layout batches in `data` (a
