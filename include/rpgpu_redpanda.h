@@ -333,6 +333,29 @@ struct compressor {
             throw std::runtime_error(rpgpu_last_error(e.ctx()));
         }
     }
+    // compression/compression.cc:17-33 (lz4: lz4_frame_compressor.cc:72-113,
+    // snappy: snappy_java_compressor.cc:58-75) on the device, byte for byte
+    // what liblz4 / libsnappy give through those wrappers.  `frag`: the
+    // size of the input iobuf's fragments (snappy-java writes one chunk per
+    // fragment; 0 = one contiguous fragment).  gzip / zstd compression is not
+    // provided (std::logic_error).
+    static rpgpu::iobuf compress(const rpgpu::iobuf& in, type t, rpgpu::engine& e = rpgpu::engine::local(),
+                                 size_t frag = 0) {
+        if (t == type::none) throw std::runtime_error("compressor: nothing to compress for 'none'");
+        if (t == type::gzip || t == type::zstd) throw std::logic_error("compressor: gzip/zstd compression not provided");
+        const int codec = (int)t;
+        size_t cap = rpgpu_compress_bound(codec, in.size_bytes(), frag), got = 0;
+        std::vector<uint8_t> out(cap ? cap : 1);
+        const void* src = in.data();
+        const size_t n = in.size_bytes();
+        void* dst = out.data();
+        int st = 0;
+        e.check(rpgpu_compress_batch(e.ctx(), 1, &codec, &src, &n, &frag, &dst, &cap, &got, &st),
+                "rpgpu_compress_batch");
+        if (st != RPGPU_OK) throw std::runtime_error("rpgpu_compress_batch: status " + std::to_string(st));
+        out.resize(got);
+        return rpgpu::iobuf(std::move(out));
+    }
 };
 }  // namespace compression
 
@@ -347,6 +370,18 @@ inline void reset_size_checksum_metadata(model::record_batch_header& hdr, const 
     hdr.size_bytes = (int32_t)(RPGPU_HEADER_SIZE + records.size_bytes());
     hdr.crc = model::crc_record_batch(hdr, records);
     hdr.header_crc = model::internal_header_only_crc(hdr);
+}
+
+// storage/parser_utils.cc:96-111: the payload compressed with c, the
+// compression bits set in attrs, then size, crc and header_crc reset
+inline std::pair<model::record_batch_header, rpgpu::iobuf>
+compress_batch(model::compression c, model::record_batch_header h, const rpgpu::iobuf& records,
+               rpgpu::engine& e = rpgpu::engine::local()) {
+    if (c == model::compression::none) throw std::invalid_argument("Asked to compress a batch with type `none`");
+    rpgpu::iobuf payload = compression::compressor::compress(records, c, e);
+    h.attrs |= c;  // compression bit must be set first
+    reset_size_checksum_metadata(h, payload);
+    return {h, std::move(payload)};
 }
 }  // namespace internal
 

@@ -52,6 +52,25 @@ static model::record_batch_header header_at(const uint8_t* p) {
     return h;
 }
 
+// the disk header back (header_at's inverse)
+template <class T>
+static void put_le(uint8_t* p, T v) { std::memcpy(p, &v, sizeof v); }
+static void header_to(const model::record_batch_header& h, uint8_t* p) {
+    put_le(p + 0, h.header_crc);
+    put_le(p + 4, h.size_bytes);
+    put_le(p + 8, h.base_offset);
+    p[16] = (uint8_t)h.type;
+    put_le(p + 17, h.crc);
+    put_le(p + 21, h.attrs.value());
+    put_le(p + 23, h.last_offset_delta);
+    put_le(p + 27, h.first_timestamp);
+    put_le(p + 35, h.max_timestamp);
+    put_le(p + 43, h.producer_id);
+    put_le(p + 51, h.producer_epoch);
+    put_le(p + 53, h.base_sequence);
+    put_le(p + 57, h.record_count);
+}
+
 static int self_checks() {
     // crc::crc32c: the standard check value, and extend() composes
     const char* s = "123456789";
@@ -273,6 +292,22 @@ int main(int argc, char** argv) {
             std::ofstream f(argv[4], std::ios::binary);
             f.write((const char*)buf.data(), (std::streamsize)buf.size());
             std::printf("S %lld\n", (long long)next);
+            return 0;
+        }
+        if (mode == "compress_batch" && argc == 5) {
+            // compress_batch <codec> <batch.bin> <out.bin>: one disk-layout
+            // batch (61-byte header + payload) through
+            // storage::internal::compress_batch, written back in disk layout
+            const std::vector<uint8_t> in = slurp(argv[3]);
+            model::record_batch_header h = header_at(in.data());
+            const rpgpu::iobuf records(in.data() + RPGPU_HEADER_SIZE, in.size() - RPGPU_HEADER_SIZE);
+            auto r = storage::internal::compress_batch((model::compression)std::atoi(argv[2]), h, records);
+            uint8_t hd[RPGPU_HEADER_SIZE];
+            header_to(r.first, hd);
+            std::ofstream f(argv[4], std::ios::binary);
+            f.write((const char*)hd, RPGPU_HEADER_SIZE);
+            f.write((const char*)r.second.data(), (std::streamsize)r.second.size_bytes());
+            std::printf("C %d %zu\n", r.first.size_bytes, r.second.size_bytes());
             return 0;
         }
         if (mode == "uncompress" && argc >= 5 && (argc - 2) % 3 == 0) {
