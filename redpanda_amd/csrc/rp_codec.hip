@@ -2047,7 +2047,10 @@ DEV void put_pstate(const DeviceJob& j, uint32_t p, const PState& ps, uint32_t n
 // A lane walking straight from HBM made the whole wave wait a memory
 // latency at nearly every sequence (some lane always needed a new window),
 // ~4 us per sequence on C2's JSON blocks.
-constexpr uint32_t kLaneWin = 64, kLaneSlot = kLaneWin + 16;  // + the spare bytes ld16's window reads need
+#ifndef RPGPU_LANE_WIN
+#define RPGPU_LANE_WIN 64
+#endif
+constexpr uint32_t kLaneWin = RPGPU_LANE_WIN, kLaneSlot = kLaneWin + 16;  // + the spare bytes ld16's window reads need
 
 __global__ __launch_bounds__(256) void k_lz_walk(DeviceJob j) {
     constexpr uint32_t kWaveLds = 64 * kLaneSlot > kWalkWin + 16 ? 64 * kLaneSlot : kWalkWin + 16;

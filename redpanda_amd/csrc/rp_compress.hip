@@ -72,27 +72,29 @@ DEV uint32_t lz_hash(uint32_t v) { return (v * 2654435761u) >> (32 - kLzHashLog)
 // byU16 / noDict / noDictIssue / limitedOutput / acceleration 1 on a zeroed
 // table; the size, or 0 when it does not fit in cap bytes
 DEV int32_t lz4c_block(const uint8_t* __restrict__ s, uint32_t n, uint8_t* __restrict__ d, int32_t cap, lds_u16* T) {
-    uint32_t ip = 0, anchor = 0, match = 0, fh = 0, tokv = 0;
+    uint32_t ip = 0, anchor = 0, match = 0, fh = 0, fv = 0, tokv = 0;
     const uint32_t mfl1 = n - 12 + 1, mlimit = n - 5;
     int32_t op = 0, token = 0;
     if (n < 13) goto last_literals;
     put16(T, lz_hash(g32(s, 0)), 0);
     ip = 1;
-    fh = lz_hash(g32(s, 1));
+    fv = g32(s, 1);  // the 4 bytes at the next probe position (kept: ip's bytes at the compare)
+    fh = lz_hash(fv);
     for (;;) {
         {
             uint32_t fip = ip, step = 1, nb = 64;
             for (;;) {
-                const uint32_t h = fh, cur = fip;
+                const uint32_t h = fh, cur = fip, iv = fv;
                 const uint32_t mi = T[h];
                 ip = fip;
                 fip += step;
                 step = nb++ >> 6;
                 if (fip > mfl1) goto last_literals;
                 match = mi;
-                fh = lz_hash(g32(s, fip));
+                fv = g32(s, fip);
+                fh = lz_hash(fv);
                 put16(T, h, cur);
-                if (g32(s, match) == g32(s, ip)) break;
+                if (g32(s, match) == iv) break;
             }
         }
         while (ip > anchor && match > 0 && s[ip - 1] == s[match - 1]) {
@@ -145,7 +147,8 @@ DEV int32_t lz4c_block(const uint8_t* __restrict__ s, uint32_t n, uint8_t* __res
                 goto next_match;
             }
         }
-        fh = lz_hash(g32(s, ++ip));
+        fv = g32(s, ++ip);
+        fh = lz_hash(fv);
     }
 last_literals : {
     const uint32_t last = n - anchor;
@@ -212,20 +215,23 @@ DEV uint32_t snappyc_block(const uint8_t* __restrict__ s, uint32_t n, uint8_t* _
     uint32_t ip = 0, next_emit = 0, op = 0;
     if (n >= 15) {
         const uint32_t ip_limit = n - 15;
-        uint32_t next_hash = sn_hash(g32(s, ++ip), shift);
+        uint32_t next_val = g32(s, ++ip);  // the bytes at next_ip (ip's at the compare)
+        uint32_t next_hash = sn_hash(next_val, shift);
         for (;;) {
-            uint32_t skip = 32, next_ip = ip, candidate;
+            uint32_t skip = 32, next_ip = ip, candidate, iv;
             do {
                 ip = next_ip;
+                iv = next_val;
                 const uint32_t hash = next_hash;
                 const uint32_t between = skip >> 5;
                 skip += between;
                 next_ip = ip + between;
                 if (next_ip > ip_limit) goto emit_remainder;
-                next_hash = sn_hash(g32(s, next_ip), shift);
+                next_val = g32(s, next_ip);
+                next_hash = sn_hash(next_val, shift);
                 candidate = T[hash];
                 put16(T, hash, ip);
-            } while (g32(s, ip) != g32(s, candidate));
+            } while (iv != g32(s, candidate));
             op = sn_literal(d, op, s + next_emit, ip - next_emit);
             uint32_t cand_bytes, cur;
             do {
@@ -242,7 +248,8 @@ DEV uint32_t snappyc_block(const uint8_t* __restrict__ s, uint32_t n, uint8_t* _
                 cand_bytes = g32(s, candidate);
                 put16(T, cur_hash, ip);
             } while (cur == cand_bytes);
-            next_hash = sn_hash(g32(s, ip + 1), shift);
+            next_val = g32(s, ip + 1);
+            next_hash = sn_hash(next_val, shift);
             ++ip;
         }
     }
@@ -251,20 +258,25 @@ emit_remainder:
     return op;
 }
 
+// one kernel per codec: the LDS table is 16 KiB for lz4 (10 waves per CU),
+// 32 KiB for snappy (5); a wave given the other codec's block leaves
+template <uint32_t kCodec>
 __global__ __launch_bounds__(64) void k_compress_blocks(const uint8_t* __restrict__ in, const CompBlock* __restrict__ blocks,
                                                         uint32_t nb, uint8_t* __restrict__ scratch,
                                                         uint32_t* __restrict__ sizes) {
-    __shared__ uint16_t table[16384];
+    __shared__ uint16_t table[kCodec == RPGPU_CODEC_SNAPPY ? 16384 : (1u << kLzHashLog)];
     lds_u16* T = (lds_u16*)table;
     const uint32_t b = blockIdx.x;
     if (b >= nb) return;
+    const uint32_t codec = uni32(blocks[b].codec);
+    if (codec != kCodec) return;
     const uint64_t src = uni64(blocks[b].src);
-    const uint32_t n = uni32(blocks[b].n), codec = uni32(blocks[b].codec);
+    const uint32_t n = uni32(blocks[b].n);
     const uint8_t* s = in + src;
     uint8_t* d = scratch + (uint64_t)b * kCompSlot;
     uint32_t tsize = 1u << kLzHashLog;
     int shift = 0;
-    if (codec == RPGPU_CODEC_SNAPPY) {
+    if (kCodec == RPGPU_CODEC_SNAPPY) {
         // CalculateTableSize
         tsize = n > 16384u ? 16384u : n < 256u ? 256u : 2u << log2f32(n - 1);
         shift = 32 - log2f32(tsize);
@@ -272,7 +284,7 @@ __global__ __launch_bounds__(64) void k_compress_blocks(const uint8_t* __restric
     for (uint32_t k = lane(); k < tsize; k += 64) T[k] = 0;
     __syncthreads();
     uint32_t r;
-    if (codec == RPGPU_CODEC_SNAPPY) r = snappyc_block(s, n, d, T, shift);
+    if (kCodec == RPGPU_CODEC_SNAPPY) r = snappyc_block(s, n, d, T, shift);
     else r = (uint32_t)lz4c_block(s, n, d, (int32_t)n - 1, T);
     if (lane() == 0) sizes[b] = r;
 }
@@ -392,7 +404,10 @@ __global__ __launch_bounds__(64) void k_compress_pack(const uint8_t* __restrict_
 
 hipError_t launch_compress(const uint8_t* in, const CompBlock* blocks, uint32_t nb, const CompPayload* pay, uint32_t np,
                            uint8_t* scratch, uint32_t* sizes, uint8_t* out, uint64_t* out_len, hipStream_t s) {
-    if (nb) hipLaunchKernelGGL(k_compress_blocks, dim3(nb), dim3(64), 0, s, in, blocks, nb, scratch, sizes);
+    if (nb) {
+        hipLaunchKernelGGL(k_compress_blocks<RPGPU_CODEC_LZ4>, dim3(nb), dim3(64), 0, s, in, blocks, nb, scratch, sizes);
+        hipLaunchKernelGGL(k_compress_blocks<RPGPU_CODEC_SNAPPY>, dim3(nb), dim3(64), 0, s, in, blocks, nb, scratch, sizes);
+    }
     if (np) hipLaunchKernelGGL(k_compress_pack, dim3(np), dim3(64), 0, s, in, pay, np, blocks, scratch, sizes, out, out_len);
     return hipGetLastError();
 }
