@@ -2040,15 +2040,17 @@ DEV void put_pstate(const DeviceJob& j, uint32_t p, const PState& ps, uint32_t n
     j.pstate[p] = out;
 }
 
-// Lane walk in rounds.  Every round, each lane with a piece stages the 64
-// stream bytes at its parse position in its LDS slot (four 16-byte loads,
-// issued by all lanes together: one memory latency per round for the whole
-// wave), then walks as many sequences as start within the first 48 of them.
-// A lane walking straight from HBM made the whole wave wait a memory
-// latency at nearly every sequence (some lane always needed a new window),
-// ~4 us per sequence on C2's JSON blocks.
+// Lane walk in rounds.  Every round, each lane with a piece stages the
+// kLaneWin stream bytes at its parse position in its LDS slot (16-byte
+// loads issued by all lanes together: one memory latency per round for the
+// whole wave), then walks as many sequences as start within the first
+// kLaneWin - 16 of them.  A lane walking straight from HBM made the whole
+// wave wait a memory latency at nearly every sequence (some lane always
+// needed a new window), ~4 us per sequence on C2's JSON blocks.  Window
+// size measured (C2 / C5 decode ms): 64 B 47.7 / 45.6, 192 B 44.4 / 43.9,
+// 256 B 43.4 / 40.4, 512 B 46.6 / 35.8 (fewer resident waves).
 #ifndef RPGPU_LANE_WIN
-#define RPGPU_LANE_WIN 64
+#define RPGPU_LANE_WIN 256
 #endif
 constexpr uint32_t kLaneWin = RPGPU_LANE_WIN, kLaneSlot = kLaneWin + 16;  // + the spare bytes ld16's window reads need
 
