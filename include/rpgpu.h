@@ -419,8 +419,8 @@ int rpgpu_uncompress_batch(rpgpu_ctx* ctx, uint32_t n, const int* codecs, const 
 
 /* Bytes compressor::compress can produce for n input bytes: the LZ4 frame
  * (lz4_frame_compressor.cc:72-113) or the snappy-java stream over frag-byte
- * iobuf fragments (snappy_java_compressor.cc:58-75; frag 0 = one fragment).
- * 0 for other codecs. */
+ * iobuf fragments (snappy_java_compressor.cc:58-75; frag 0 = one fragment),
+ * or a safe bound for the host gzip / zstd streams.  0 for RPGPU_CODEC_NONE. */
 size_t rpgpu_compress_bound(int codec, size_t n, size_t frag);
 
 /* n payloads compressed on the device in one round trip (host pointers), the
@@ -430,8 +430,10 @@ size_t rpgpu_compress_bound(int codec, size_t n, size_t frag);
  * chunk per frag[i]-byte fragment (frag may be NULL: one fragment, a
  * contiguous iobuf).  status[i]: RPGPU_OK; RPGPU_E_OVERFLOW when cap[i] <
  * the output (out_len[i] then holds its size); RPGPU_E_CODEC for
- * RPGPU_CODEC_NONE (the reference throws "nothing to compress");
- * RPGPU_E_UNSUPPORTED for gzip / zstd. */
+ * RPGPU_CODEC_NONE (the reference throws "nothing to compress").  gzip and
+ * zstd run on the host, the reference's loops over zlib / libzstd
+ * (gzip_compressor.cc:126-161, stream_zstd.cc:84-104; RPGPU_E_UNSUPPORTED
+ * when the library cannot be loaded). */
 int rpgpu_compress_batch(rpgpu_ctx* ctx, uint32_t n, const int* codecs, const void* const* in, const size_t* in_len,
                          const size_t* frag, void* const* out, const size_t* cap, size_t* out_len, int* status);
 

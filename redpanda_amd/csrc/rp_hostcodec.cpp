@@ -11,6 +11,14 @@
 //     with a static DCtx over ZSTD_estimateDStreamSize(8 MiB) of workspace
 //     (zstd_decompress_workspace_bytes, config/configuration.cc:911-916) and
 //     its 64 KiB output buffer (stream_zstd.cc:43-53).
+// And compressor::compress for the same two codecs (compression.cc:17-33):
+//   * gzip: gzip_compressor::compress (gzip_compressor.cc:126-161) with
+//     gzip_compression_codec::reset's deflateInit2(Z_DEFAULT_COMPRESSION,
+//     Z_DEFLATED, 15 + 16, 8, Z_DEFAULT_STRATEGY) (:51-62), one deflate
+//     (Z_NO_FLUSH) per iobuf fragment into a deflateBound buffer, Z_FINISH;
+//   * zstd: stream_zstd::do_compress (stream_zstd.cc:84-104): a fresh CCtx,
+//     pledged source size, one ZSTD_compressStream2(ZSTD_e_flush) per
+//     fragment into a ZSTD_compressBound buffer, ZSTD_endStream.
 // Host code only; no device work.  Status: 0 ok, kHostCodecError where the
 // reference throws std::runtime_error, kHostCodecMissing when the library is
 // absent, kHostCodecOverflow when cap is too small (*out_len = size needed).
@@ -36,6 +44,10 @@ struct ZApi {
     int (*inflateGetHeader)(z_streamp, gz_headerp);
     int (*inflate)(z_streamp, int);
     int (*inflateEnd)(z_streamp);
+    int (*deflateInit2_)(z_streamp, int, int, int, int, int, const char*, int);
+    uLong (*deflateBound)(z_streamp, uLong);
+    int (*deflate)(z_streamp, int);
+    int (*deflateEnd)(z_streamp);
 };
 
 const ZApi* zapi() {
@@ -47,7 +59,12 @@ const ZApi* zapi() {
         a.inflateGetHeader = (int (*)(z_streamp, gz_headerp))dlsym(h, "inflateGetHeader");
         a.inflate = (int (*)(z_streamp, int))dlsym(h, "inflate");
         a.inflateEnd = (int (*)(z_streamp))dlsym(h, "inflateEnd");
-        return a.inflateInit2_ && a.inflateGetHeader && a.inflate && a.inflateEnd;
+        a.deflateInit2_ = (int (*)(z_streamp, int, int, int, int, int, const char*, int))dlsym(h, "deflateInit2_");
+        a.deflateBound = (uLong(*)(z_streamp, uLong))dlsym(h, "deflateBound");
+        a.deflate = (int (*)(z_streamp, int))dlsym(h, "deflate");
+        a.deflateEnd = (int (*)(z_streamp))dlsym(h, "deflateEnd");
+        return a.inflateInit2_ && a.inflateGetHeader && a.inflate && a.inflateEnd && a.deflateInit2_ &&
+               a.deflateBound && a.deflate && a.deflateEnd;
     }();
     return ok ? &a : nullptr;
 }
@@ -144,6 +161,12 @@ struct ZstdApi {
     void* (*initStaticDCtx)(void*, size_t);
     size_t (*decompressStream)(void*, ZstdOut*, ZstdIn*);
     unsigned (*isError)(size_t);
+    void* (*createCCtx)();
+    size_t (*freeCCtx)(void*);
+    size_t (*setPledgedSrcSize)(void*, unsigned long long);
+    size_t (*compressBound)(size_t);
+    size_t (*compressStream2)(void*, ZstdOut*, ZstdIn*, int);
+    size_t (*endStream)(void*, ZstdOut*);
 };
 
 const ZstdApi* zstdapi() {
@@ -155,7 +178,14 @@ const ZstdApi* zstdapi() {
         a.initStaticDCtx = (void* (*)(void*, size_t))dlsym(h, "ZSTD_initStaticDCtx");
         a.decompressStream = (size_t(*)(void*, ZstdOut*, ZstdIn*))dlsym(h, "ZSTD_decompressStream");
         a.isError = (unsigned (*)(size_t))dlsym(h, "ZSTD_isError");
-        return a.estimateDStreamSize && a.initStaticDCtx && a.decompressStream && a.isError;
+        a.createCCtx = (void* (*)())dlsym(h, "ZSTD_createCCtx");
+        a.freeCCtx = (size_t(*)(void*))dlsym(h, "ZSTD_freeCCtx");
+        a.setPledgedSrcSize = (size_t(*)(void*, unsigned long long))dlsym(h, "ZSTD_CCtx_setPledgedSrcSize");
+        a.compressBound = (size_t(*)(size_t))dlsym(h, "ZSTD_compressBound");
+        a.compressStream2 = (size_t(*)(void*, ZstdOut*, ZstdIn*, int))dlsym(h, "ZSTD_compressStream2");
+        a.endStream = (size_t(*)(void*, ZstdOut*))dlsym(h, "ZSTD_endStream");
+        return a.estimateDStreamSize && a.initStaticDCtx && a.decompressStream && a.isError && a.createCCtx &&
+               a.freeCCtx && a.setPledgedSrcSize && a.compressBound && a.compressStream2 && a.endStream;
     }();
     return ok ? &a : nullptr;
 }
@@ -207,7 +237,75 @@ int zstd_uncompress(const uint8_t* in, size_t n, uint8_t* out, size_t cap, size_
     return total > cap ? kHostCodecOverflow : 0;
 }
 
+// gzip_compressor::compress; *out_len = the stream's size (also on overflow)
+int gzip_compress(const uint8_t* in, size_t n, size_t frag, uint8_t* out, size_t cap, size_t* out_len) {
+    const ZApi* z = zapi();
+    if (!z) return kHostCodecMissing;
+    if (n > 0xFFFFFFFFull) return kHostCodecError;
+    z_stream st;
+    memset(&st, 0, sizeof st);
+    if (z->deflateInit2_(&st, Z_DEFAULT_COMPRESSION, Z_DEFLATED, 15 + 16, 8, Z_DEFAULT_STRATEGY, ZLIB_VERSION,
+                         (int)sizeof(z_stream)) != Z_OK)
+        return kHostCodecError;
+    const size_t bound = z->deflateBound(&st, (uLong)n);
+    std::unique_ptr<uint8_t[]> buf(new (std::nothrow) uint8_t[bound ? bound : 1]);
+    int rc = 0;
+    if (!buf) rc = kHostCodecError;
+    if (rc == 0) {
+        st.next_out = buf.get();
+        st.avail_out = (uInt)bound;
+        if (frag == 0) frag = n ? n : 1;
+        for (size_t f = 0; f < n && rc == 0; f += frag) {
+            st.next_in = (unsigned char*)in + f;
+            st.avail_in = (uInt)(n - f < frag ? n - f : frag);
+            const int r = z->deflate(&st, Z_NO_FLUSH);
+            if (r != Z_OK && r != Z_STREAM_END && r != Z_BUF_ERROR) rc = kHostCodecError;
+        }
+        if (rc == 0 && z->deflate(&st, Z_FINISH) != Z_STREAM_END) rc = kHostCodecError;
+    }
+    if (rc == 0) {
+        *out_len = st.total_out;
+        if (st.total_out > cap) rc = kHostCodecOverflow;
+        else memcpy(out, buf.get(), st.total_out);
+    }
+    z->deflateEnd(&st);
+    return rc;
+}
+
+// stream_zstd::do_compress
+int zstd_compress(const uint8_t* in, size_t n, size_t frag, uint8_t* out, size_t cap, size_t* out_len) {
+    const ZstdApi* z = zstdapi();
+    if (!z) return kHostCodecMissing;
+    void* ctx = z->createCCtx();
+    if (!ctx) return kHostCodecError;
+    int rc = 0;
+    const size_t bound = z->compressBound(n);
+    std::unique_ptr<uint8_t[]> buf(new (std::nothrow) uint8_t[bound ? bound : 1]);
+    if (!buf || z->isError(z->setPledgedSrcSize(ctx, n))) rc = kHostCodecError;
+    ZstdOut o{buf.get(), bound, 0};
+    if (frag == 0) frag = n ? n : 1;
+    for (size_t f = 0; f < n && rc == 0; f += frag) {
+        ZstdIn i{in + f, n - f < frag ? n - f : frag, 0};
+        if (z->isError(z->compressStream2(ctx, &o, &i, 1 /* ZSTD_e_flush */))) rc = kHostCodecError;
+    }
+    if (rc == 0) {
+        z->endStream(ctx, &o);  // the reference does not check it
+        *out_len = o.pos;
+        if (o.pos > cap) rc = kHostCodecOverflow;
+        else memcpy(out, buf.get(), o.pos);
+    }
+    z->freeCCtx(ctx);
+    return rc;
+}
+
 }  // namespace
+
+int host_compress(int codec, const uint8_t* in, size_t n, size_t frag, uint8_t* out, size_t cap, size_t* out_len) {
+    *out_len = 0;
+    if (codec == kHostGzip) return gzip_compress(in, n, frag, out, cap, out_len);
+    if (codec == kHostZstd) return zstd_compress(in, n, frag, out, cap, out_len);
+    return kHostCodecMissing;
+}
 
 int host_uncompress(int codec, const uint8_t* in, size_t n, uint8_t* out, size_t cap, size_t* out_len) {
     *out_len = 0;

@@ -896,12 +896,19 @@ size_t rpgpu_compress_bound(int codec, size_t n, size_t frag) {
         const size_t nf = n ? (n + frag - 1) / frag : 0;
         return 16 + nf * (4 + 32 + frag + frag / 6);  // snappy::MaxCompressedLength per fragment
     }
+    // deflateBound / ZSTD_compressBound, generously (per-fragment flushes add
+    // a few bytes each)
+    if (codec == RPGPU_CODEC_GZIP || codec == RPGPU_CODEC_ZSTD) {
+        const size_t nf = frag ? (n + frag - 1) / frag : 1;
+        return n + n / 64 + 1024 + nf * 16;
+    }
     return 0;
 }
 
 int rpgpu_compress_batch(rpgpu_ctx* c, uint32_t n, const int* codecs, const void* const* in, const size_t* in_len,
                          const size_t* frag, void* const* out, const size_t* cap, size_t* out_len, int* status) {
-    if (!c || (n && (!codecs || !in || !in_len || !out || !cap || !out_len || !status))) return RPGPU_E_INVALID;
+    // ctx may be NULL when every payload is gzip / zstd (host work only)
+    if (n && (!codecs || !in || !in_len || !out || !cap || !out_len || !status)) return RPGPU_E_INVALID;
     std::vector<uint32_t> dev;
     std::vector<CompPayload> pays;
     std::vector<CompBlock> blocks;
@@ -912,8 +919,17 @@ int rpgpu_compress_batch(rpgpu_ctx* c, uint32_t n, const int* codecs, const void
         const int codec = codecs[i];
         if (codec < 0 || codec > RPGPU_CODEC_ZSTD || (!in[i] && in_len[i])) { status[i] = RPGPU_E_INVALID; continue; }
         if (codec == RPGPU_CODEC_NONE) { status[i] = RPGPU_E_CODEC; continue; }
-        if (codec == RPGPU_CODEC_GZIP || codec == RPGPU_CODEC_ZSTD) { status[i] = RPGPU_E_UNSUPPORTED; continue; }
-        if (in_len[i] > (1ull << 32)) { status[i] = RPGPU_E_INVALID; continue; }
+        if (codec == RPGPU_CODEC_GZIP || codec == RPGPU_CODEC_ZSTD) {
+            // the CPU fallback: the reference's loops over zlib / libzstd
+            const int r = host_compress(codec, (const uint8_t*)in[i], in_len[i], frag ? frag[i] : 0, (uint8_t*)out[i],
+                                        cap[i], &out_len[i]);
+            status[i] = r == 0 ? RPGPU_OK
+                        : r == kHostCodecOverflow ? RPGPU_E_OVERFLOW
+                        : r == kHostCodecMissing  ? RPGPU_E_UNSUPPORTED
+                                                  : RPGPU_E_CODEC;
+            continue;
+        }
+        if (!c || in_len[i] > (1ull << 32)) { status[i] = RPGPU_E_INVALID; continue; }
         const uint64_t len = in_len[i];
         CompPayload p;
         p.n = len;

@@ -81,7 +81,7 @@ def test_compress_bound(rplib, corpus):
             for frag in (0, 1000):
                 b = L.rpgpu_compress_bound(codec, len(data), frag)
                 assert b >= len(O.compress(codec, data, frag)), (name, codec, frag)
-    assert L.rpgpu_compress_bound(abi.CODEC_GZIP, 100, 0) == 0
+    assert L.rpgpu_compress_bound(abi.CODEC_NONE, 100, 0) == 0
 
 
 @pytest.mark.gpu
@@ -104,8 +104,9 @@ def test_gpu_compress_matches_oracle(engine, corpus):
 
 @pytest.mark.gpu
 def test_gpu_compress_round_trip_and_statuses(engine):
-    """Frames decode back on the device (rpgpu_uncompress_batch); none / gzip
-    / zstd statuses; a too-small capacity reports the size needed."""
+    """Frames decode back on the device (rpgpu_uncompress_batch); none throws,
+    gzip / zstd go to the host in the same call; a too-small capacity
+    reports the size needed."""
     data = [CC.json_like(1 << 20, 11), CC.text(200_000, 12), CC.random_bytes(70000, 13), b"abc" * 7]
     codecs = [3, 2, 3, 2]
     res = engine.compress_batch(codecs, data)
@@ -113,7 +114,8 @@ def test_gpu_compress_round_trip_and_statuses(engine):
     back = engine.uncompress_batch(codecs, [f for _, f in res], caps=[len(d) + 64 for d in data])
     assert [b for _, b in back] == data
     st = engine.compress_batch([abi.CODEC_NONE, abi.CODEC_GZIP, abi.CODEC_ZSTD], [b"x" * 10] * 3)
-    assert [s for s, _ in st] == [abi.E_CODEC, abi.E_UNSUPPORTED, abi.E_UNSUPPORTED]
+    assert [s for s, _ in st] == [abi.E_CODEC, abi.OK, abi.OK]
+    assert engine.uncompress_batch([abi.CODEC_GZIP, abi.CODEC_ZSTD], [st[1][1], st[2][1]]) == [(0, b"x" * 10)] * 2
     full = engine.compress_batch([3], [data[0]])[0][1]
     st, need = engine.compress_batch([3], [data[0]], caps=[100])[0]
     assert st == abi.E_OVERFLOW and need == len(full)
@@ -132,3 +134,61 @@ def test_gpu_compress_many_blocks(engine):
     res = engine.compress_batch(codecs, pays, frags)
     for (st, got), codec, data, frag in zip(res, codecs, pays, frags):
         assert st == 0 and got == O.compress(codec, data, frag)
+
+
+def _host_compress(rplib, codec, data, frag=0, cap=None):
+    """rpgpu_compress_batch with a NULL context (gzip / zstd are host work)."""
+    import ctypes as C
+    L = rplib.load()
+    src = np.frombuffer(bytes(data), dtype=np.uint8) if data else np.zeros(1, np.uint8)
+    cap = cap if cap is not None else L.rpgpu_compress_bound(codec, len(data), frag)
+    out = np.zeros(max(cap, 1), np.uint8)
+    ci, ip = (C.c_int * 1)(codec), (C.c_void_p * 1)(src.ctypes.data)
+    il, fr = (C.c_size_t * 1)(len(data)), (C.c_size_t * 1)(frag)
+    op, oc, ol, st = (C.c_void_p * 1)(out.ctypes.data), (C.c_size_t * 1)(cap), (C.c_size_t * 1)(), (C.c_int * 1)()
+    assert L.rpgpu_compress_batch(None, 1, ci, ip, il, fr, op, oc, ol, st) == 0
+    return int(st[0]), (out[: ol[0]].tobytes() if st[0] == 0 else int(ol[0]))
+
+
+def test_gzip_compress_host_fallback(rplib, corpus):
+    """gzip_compressor::compress (gzip_compressor.cc:126-161): deflateInit2(
+    Z_DEFAULT_COMPRESSION, Z_DEFLATED, 15 + 16, 8, Z_DEFAULT_STRATEGY), one
+    deflate per fragment, Z_FINISH — byte for byte what Python's zlib
+    (an independent driver of the same library, same parameters) gives."""
+    import zlib
+    for name, data in corpus:
+        for frag in (0, 1000):
+            st, got = _host_compress(rplib, abi.CODEC_GZIP, data, frag)
+            c = zlib.compressobj(-1, zlib.DEFLATED, 31, 8, 0)
+            want = b"".join(c.compress(data[f:f + (frag or len(data) or 1)])
+                            for f in range(0, len(data), frag or len(data) or 1)) + c.flush()
+            assert st == 0 and got == want, (name, frag)
+            assert zlib.decompress(got, 31) == data
+
+
+def test_zstd_compress_host_fallback(rplib, corpus):
+    """stream_zstd::do_compress (stream_zstd.cc:84-104): the frame carries the
+    content size and decodes back through libzstd and the host uncompress
+    path; per-fragment flushes make distinct (valid) frames."""
+    import test_hostcodec as H
+    Z = H.zstd_lib()
+    import ctypes as C
+    Z.ZSTD_getFrameContentSize.restype = C.c_ulonglong
+    Z.ZSTD_getFrameContentSize.argtypes = [C.c_void_p, C.c_size_t]
+    for name, data in corpus:
+        for frag in (0, 1000):
+            st, frame = _host_compress(rplib, abi.CODEC_ZSTD, data, frag)
+            assert st == 0, name
+            assert Z.ZSTD_getFrameContentSize(frame, len(frame)) == len(data)
+            rc, back = H.uncompress(rplib, abi.CODEC_ZSTD, frame, cap=len(data) + 1)
+            assert rc == 0 and back == data, (name, frag)
+
+
+def test_host_compress_overflow_and_none(rplib):
+    data = CC.text(50000, 3)
+    st, full = _host_compress(rplib, abi.CODEC_GZIP, data)
+    st2, need = _host_compress(rplib, abi.CODEC_GZIP, data, cap=10)
+    assert st == 0 and st2 == abi.E_OVERFLOW and need == len(full)
+    assert _host_compress(rplib, abi.CODEC_NONE, data, cap=100)[0] == abi.E_CODEC
+    # device codecs need a context
+    assert _host_compress(rplib, abi.CODEC_LZ4, data)[0] == abi.E_INVALID
