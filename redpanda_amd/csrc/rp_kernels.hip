@@ -82,6 +82,36 @@ struct ScanWin {
     uint32_t w[20];
 };
 
+#ifndef RPGPU_SCAN_LOADS
+// one 16-byte load per lane; the next 64 bytes come from lanes l + 1 .. l + 4
+// (DPP wave_shl:1, four hops), lane 63 loading what lies past the step.
+// (Five overlapping loads per lane, RPGPU_SCAN_LOADS, or plain instead of
+// non-temporal loads: C2 discovery 14.4 / 14.0 ms against 13.5 ms here; the
+// scan is bound by the per-position field checks, not by its loads.)
+DEV u32x4 scan_ld(const uint8_t* __restrict__ data, uint64_t data_len, uint64_t x) {
+    u32x4 v = {0, 0, 0, 0};
+    if (x + 16 <= data_len) v = __builtin_nontemporal_load((const u32x4*)(data + x));
+    return v;
+}
+DEV void scan_load(const uint8_t* __restrict__ data, uint64_t data_len, uint64_t a, ScanWin& sw) {
+    const uint32_t l = lane();
+    const uint64_t la = a + 16ull * l;
+    u32x4 v = scan_ld(data, data_len, la), d[4];
+#pragma unroll
+    for (int k = 1; k < 5; k++) {
+        d[k - 1] = (u32x4){0, 0, 0, 0};
+        if (l == 63) d[k - 1] = scan_ld(data, data_len, la + 16ull * k);
+    }
+    sw.w[0] = v.x; sw.w[1] = v.y; sw.w[2] = v.z; sw.w[3] = v.w;
+#pragma unroll
+    for (int k = 1; k < 5; k++) {
+#pragma unroll
+        for (int c = 0; c < 4; c++)
+            sw.w[4 * k + c] = (uint32_t)__builtin_amdgcn_update_dpp((int)d[k - 1][c], (int)sw.w[4 * (k - 1) + c], 0x130,
+                                                                   0xF, 0xF, false);
+    }
+}
+#else
 DEV void scan_load(const uint8_t* __restrict__ data, uint64_t data_len, uint64_t a, ScanWin& sw) {
     const uint64_t la = a + 16ull * lane();
 #pragma unroll
@@ -92,6 +122,7 @@ DEV void scan_load(const uint8_t* __restrict__ data, uint64_t data_len, uint64_t
         sw.w[4 * k] = v.x; sw.w[4 * k + 1] = v.y; sw.w[4 * k + 2] = v.z; sw.w[4 * k + 3] = v.w;
     }
 }
+#endif
 
 // Plausible header fields (disk or wire) given the 61 header bytes through
 // W32(o) / B(o); `rem` = bytes from the header to the segment end.  The
