@@ -142,16 +142,21 @@ struct DeviceJob {
     rpgpu_job_totals* totals;
     uint64_t* bitmap;
     const Tables* tables;
-    uint32_t* counters;           // [0] rewalks, [1] overflow bits, [2] decode items, [3] unused,
+    uint32_t* counters;           // [0] rewalks, [1] overflow bits, [2] decode items, [3] split batches,
                                   // [4] block items reserved, [5] sequential-frame claim cursor,
                                   // [6] sequential frames, [7] linked frames, [8] k_lz_exec claim cursor,
                                   // [9] slab pool cursor, [10] k_lz_walk claim cursor, [11] long pieces,
                                   // [12] long-piece claim cursor, [13] k_validate_decoded claim cursor,
-                                  // [14] k_decode_finish claim cursor
+                                  // [14] k_decode_finish claim cursor, [15] k_crc_split claim cursor
     uint32_t* decode_list;        // batch_capacity: ordinals of batches to uncompress
     uint32_t* seq_list;           // batch_capacity: decode items decoded whole by one lane
     uint32_t* link_list;          // batch_capacity: decode items whose linked LZ4F blocks one wave decodes in order
     uint32_t* long_list;          // block_capacity: pieces k_lz_walk walks one wave each ([11] count, [12] cursor)
+    uint32_t* split_list;         // split_capacity: stored payloads >= kSplitMin whose CRC runs in kSplitParts
+                                  // chunks on separate waves ([3] count)
+    uint32_t* split_part;         // split_capacity * kSplitParts: the chunks' linear CRCs
+    uint32_t split_capacity;
+    uint64_t split_min;           // payloads this large are split: max(kSplitMin, 2 x the job's bytes per k_validate wave)
     SeqRec* seqs;                 // k_lz_exec's own walks: kRecsPerLane per resident wave
     uint32_t exec_waves;          // k_lz_exec grid (one wave per workgroup; sizes `seqs`)
     PieceState* pstate;           // block_capacity: walk results
@@ -191,6 +196,14 @@ struct UncItem {
 // of kCompSlot bytes (>= snappy::MaxCompressedLength(65536)), then one frame
 // per payload
 constexpr uint32_t kCompSlot = 76800;
+// large stored payloads (disk layout): CRC in kSplitParts chunks, one wave
+// each, merged by GF(2) shifts (k_crc_split / k_crc_combine).  Only payloads
+// above twice a wave's share of the job are split (DeviceJob::split_min): a
+// job of many batches is balanced by k_validate's stride already, and
+// splitting C2 / C5's batches at 256 KiB measured slower (validate 8.8 ->
+// 9.9 ms), a separate pass where the stride overlapped them.
+constexpr uint64_t kSplitMin = 256u << 10;
+constexpr uint32_t kSplitParts = 16;
 struct CompBlock {
     uint64_t src;                    // staged input offset (4-byte aligned, 8 readable bytes past the block)
     uint32_t n, codec;               // block bytes (<= 65536), RPGPU_CODEC_LZ4 / _SNAPPY

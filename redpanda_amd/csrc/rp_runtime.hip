@@ -402,6 +402,12 @@ int submit_impl(rpgpu_ctx* c, const rpgpu_job* job, void* stream, int stop, Plan
     const size_t o_plans = take(dec ? (bcap + 1) * sizeof(FramePlan) : 0);
     const size_t o_pstate = take(bl_cap64 * sizeof(PieceState));
     const size_t o_longl = take(bl_cap64 * 4);
+    uint64_t split_min = std::max<uint64_t>(kSplitMin, 2 * data_len / ((uint64_t)c->cu_count * kVWaves));
+    // RPGPU_SPLIT_MIN_KIB: diagnostic override (scripts/bench_skew.py A/B)
+    if (const char* e = getenv("RPGPU_SPLIT_MIN_KIB")) split_min = std::max<uint64_t>(strtoull(e, nullptr, 10) << 10, 64);
+    const uint64_t split_cap = std::min<uint64_t>(data_len / split_min + 1, bcap + 1);
+    const size_t o_split = take(split_cap * 4);
+    const size_t o_spart = take(split_cap * kSplitParts * 4);
     const size_t o_scan = take(scan_temp_bytes(std::max<uint64_t>(tc, bcap)) + 64);
     const size_t need = off;
     if (dec && !c->seqs) {
@@ -461,6 +467,10 @@ int submit_impl(rpgpu_ctx* c, const rpgpu_job* job, void* stream, int stop, Plan
     j.seq_list = (uint32_t*)(ws + o_slist);
     j.link_list = (uint32_t*)(ws + o_llist);
     j.long_list = (uint32_t*)(ws + o_longl);
+    j.split_list = (uint32_t*)(ws + o_split);
+    j.split_part = (uint32_t*)(ws + o_spart);
+    j.split_capacity = (uint32_t)split_cap;
+    j.split_min = split_min;
     j.seqs = c->seqs;
     j.exec_waves = c->exec_waves;
     j.pstate = (PieceState*)(ws + o_pstate);

@@ -1217,16 +1217,26 @@ __global__ __launch_bounds__(1024) void k_validate(DeviceJob j) {
             // init ~0 = c40 ^ the prefix's raw contribution (from k_emit).
             // Half-way through, the first group's head and tail rows are
             // issued into the registers the CRC has freed.
-            const uint32_t crc = ~crc_stream(lds, K, st, v, gt, d.praw ^ c40);
-                record_regions(p0, (uint32_t)((uintptr_t)p0 & 15), n, g0.first && lane_v() < g0.m, g0.my_start,
-                               g0.my_end, g0.H, g0.T);
+            // a large stored payload (disk layout) has its CRC computed in
+            // kSplitParts chunks on other waves (k_crc_split) and merged by
+            // GF(2) shifts (k_crc_combine), which then sets the verdict
+            const bool split = !wire && d.n >= j.split_min;
+            uint32_t crc = 0;
+            if (!split) crc = ~crc_stream(lds, K, st, v, gt, d.praw ^ c40);
+            record_regions(p0, (uint32_t)((uintptr_t)p0 & 15), n, g0.first && lane_v() < g0.m, g0.my_start, g0.my_end,
+                           g0.H, g0.T);
             STAMP(tb2);
             STAMP_ADD(0, tb2 - tb);
             // on the wire valid_crc is only computed for v2 batches, and
             // adapt() parses records only after both checks passed
             // (kafka/protocol/kafka_batch_adapter.cc:157-181)
-            if (crc == d.crc && (!wire || (f & RPGPU_F_WIRE_V2))) f |= RPGPU_F_CRC_OK;
-            else if (!wire) note_bad(j, d.seg, b);
+            if (split) {
+                if (l == 0) j.split_list[atomicAdd(&j.counters[3], 1u)] = (uint32_t)b;
+            } else if (crc == d.crc && (!wire || (f & RPGPU_F_WIRE_V2))) {
+                f |= RPGPU_F_CRC_OK;
+            } else if (!wire) {
+                note_bad(j, d.seg, b);
+            }
             prefetch();
             if (walk && (!wire || (f & RPGPU_F_CRC_OK))) {
                 bool idx_ok;
@@ -1250,8 +1260,8 @@ __global__ __launch_bounds__(1024) void k_validate(DeviceJob j) {
                 R->records_parsed = parsed;
                 R->parse_err = (uint8_t)perr;
                 // a decoded payload is finished by k_validate_decoded, which
-                // still needs the prefix contribution
-                if (!(d.codec != 0 && (f & RPGPU_F_CODEC_OK))) R->reserved1 = 0;
+                // still needs the prefix contribution (so does k_crc_combine)
+                if (!(d.codec != 0 && (f & RPGPU_F_CODEC_OK)) && !split) R->reserved1 = 0;
             }
             STAMP(td);
             STAMP_ADD(5, td - tc);
@@ -1275,6 +1285,94 @@ __global__ void k_print_stamps() {
     for (int i = 0; i < 8; i++) g_stamps[i] = 0;
 }
 #endif
+
+// ---------------------------------------------------------------------------
+// Large stored payloads (north_star: "large batches are split into chunks
+// whose partial CRCs are merged with GF(2) crc-combine shifts").  A payload
+// of kSplitMin bytes or more would hold one k_validate wave for up to
+// 64 KiB-row windows in series while the other waves idle at the end of a
+// skewed job; instead k_validate lists it and k_crc_split spreads its
+// kSplitParts chunks over all waves (claimed one at a time).  Each chunk's
+// linear CRC L_k (zero initial state) is merged in k_crc_combine:
+//   state = x^(8 n) * S0  ^  sum_k x^(8 (n - end_k)) * L_k   (mod P)
+// with S0 the state after the BE40 prefix, the products in GF(2)[x] mod the
+// reflected CRC32C polynomial (zlib's multmodp / x2nmodp scheme).
+// ---------------------------------------------------------------------------
+DEV uint64_t split_cut(uint64_t n, uint32_t k) { return k >= kSplitParts ? n : (n * k / kSplitParts) & ~15ull; }
+
+__global__ __launch_bounds__(1024) void k_crc_split(DeviceJob j) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    const uint32_t count = j.counters[3];
+    if (count == 0) return;
+    init_lds_tables(lds, j.tables);
+    const Keys K = make_keys();
+    for (;;) {
+        const uint32_t i = wave_fetch_add(&j.counters[15], 1u);
+        if (i >= count * kSplitParts) break;
+        const uint32_t item = i / kSplitParts, part = i % kSplitParts;
+        const uint64_t b = uni32(j.split_list[item]);
+        const Desc d = desc_of(load_desc_raw(j, b));
+        // k_validate replaced index_base (the payload start) by the index
+        // slot: the payload follows the 61-byte header at file_pos
+        const uint64_t S = uni64(j.batches[b].file_pos) + uni64(j.seg_off[d.seg]) + RPGPU_HEADER_SIZE;
+        const Stream st = make_stream(j.data, S + split_cut(d.n, part), S + split_cut(d.n, part + 1));
+        Win v;
+        load_window(st, 0, v);
+        const uint4 gt = load_tail(st);
+        const uint32_t L = crc_stream(lds, K, st, v, gt, 0u);
+        if (lane_v() == 0) j.split_part[i] = L;
+    }
+}
+
+// x^(2^k) mod P, reflected CRC32C (k = 0..31)
+__constant__ uint32_t kX2n[32] = {
+    0x40000000u, 0x20000000u, 0x08000000u, 0x00800000u, 0x00008000u, 0x82F63B78u, 0x6EA2D55Cu, 0x18B8EA18u,
+    0x510AC59Au, 0xB82BE955u, 0xB8FDB1E7u, 0x88E56F72u, 0x74C360A4u, 0xE4172B16u, 0x0D65762Au, 0x35D73A62u,
+    0x28461564u, 0xBF455269u, 0xE2EA32DCu, 0xFE7740E6u, 0xF946610Bu, 0x3C204F8Fu, 0x538586E3u, 0x59726915u,
+    0x734D5309u, 0xBC1AC763u, 0x7D0722CCu, 0xD289CABEu, 0xE94CA9BCu, 0x05B74F3Fu, 0xA51E1F42u, 0x40000000u};
+
+// a * b mod P (reflected; a != 0)
+DEV uint32_t multmodp(uint32_t a, uint32_t b) {
+    uint32_t m = 1u << 31, p = 0;
+    for (;;) {
+        if (a & m) {
+            p ^= b;
+            if ((a & (m - 1)) == 0) break;
+        }
+        m >>= 1;
+        b = (b & 1) ? (b >> 1) ^ 0x82F63B78u : b >> 1;
+    }
+    return p;
+}
+// the state s advanced over n zero bytes: x^(8 n) * s mod P
+DEV uint32_t crc_shift(uint32_t s, uint64_t n) {
+    uint32_t p = 1u << 31;  // x^0
+    for (uint32_t k = 3; n; n >>= 1, k++)
+        if (n & 1) p = multmodp(kX2n[k & 31], p);
+    return multmodp(p, s);
+}
+
+// one wave per listed payload: lanes 0..15 shift the chunk CRCs, lane 16 the
+// prefix state, an xor over the wave merges them; then the verdict
+__global__ __launch_bounds__(256) void k_crc_combine(DeviceJob j) {
+    const uint32_t item = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (item >= j.counters[3]) return;
+    const uint32_t l = lane_v();
+    const uint64_t b = uni32(j.split_list[item]);
+    const Desc d = desc_of(load_desc_raw(j, b));
+    uint32_t t = 0;
+    if (l < kSplitParts) t = crc_shift(j.split_part[item * kSplitParts + l], d.n - split_cut(d.n, l + 1));
+    else if (l == kSplitParts) t = crc_shift(d.praw ^ j.tables->c40, d.n);
+    t = wave_xor(t);
+    const uint32_t crc = ~t;
+    if (crc != d.crc) note_bad(j, d.seg, b);
+    if (l == 0) {
+        rpgpu_batch_result* R = &j.batches[b];
+        R->crc_computed = crc;
+        if (crc == d.crc) R->flags = d.flags | RPGPU_F_CRC_OK;
+        if (!(d.codec != 0 && (d.flags & RPGPU_F_CODEC_OK))) R->reserved1 = 0;
+    }
+}
 
 // reset_size_checksum_metadata (storage/parser_utils.cc:114-120) and the
 // record walk over every payload k_decode uncompressed: one wave per
@@ -1580,12 +1678,18 @@ hipError_t launch_validate(const DeviceJob& j, hipStream_t s, uint32_t grid) {
         (void)hipFuncSetAttribute((const void*)k_validate, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsValidateBytes);
         (void)hipFuncSetAttribute((const void*)k_validate_decoded, hipFuncAttributeMaxDynamicSharedMemorySize,
                                   kLdsValidateBytes);
+        (void)hipFuncSetAttribute((const void*)k_crc_split, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  kLdsValidateBytes);
         attr = true;
     }
     hipLaunchKernelGGL(k_validate, dim3(grid), dim3(64 * kVWaves), kLdsValidateBytes, s, j);
 #ifdef RPGPU_STAMPS
     hipLaunchKernelGGL(k_print_stamps, dim3(1), dim3(1), 0, s);
 #endif
+    if (j.layout != RPGPU_LAYOUT_WIRE && j.data_len >= j.split_min) {
+        hipLaunchKernelGGL(k_crc_split, dim3(grid), dim3(64 * kVWaves), kLdsValidateBytes, s, j);
+        hipLaunchKernelGGL(k_crc_combine, dim3((j.split_capacity + 3) / 4), dim3(256), 0, s, j);
+    }
     if ((j.flags & RPGPU_JOB_DECODE) && j.decoded)
         hipLaunchKernelGGL(k_validate_decoded, dim3(grid), dim3(64 * kVWaves), kLdsValidateBytes, s, j);
     return hipGetLastError();

@@ -474,3 +474,16 @@ def test_raw_snappy_long_streams(engine, oracle, rplib, seed):
     got, ref = run_both(engine, oracle, segs, flags=flags)
     assert_same(got, ref, flags)
     assert np.sum((ref.batches["flags"] & abi.F_CODEC_OK) != 0) > 4
+
+
+@pytest.mark.parametrize("corrupt", [0, 300000])
+def test_large_batches_split_crc(engine, oracle, rplib, corrupt):
+    """A skewed job of few large batches (1..4 MiB): their stored-payload CRCs
+    run in kSplitParts chunks on separate waves (k_crc_split) merged by GF(2)
+    shifts (k_crc_combine); verdicts, crc_computed and checkpoints equal the
+    oracle's, corrupted payloads included."""
+    segs = [gen(rplib, 24 << 20, i, seed=0x5EED + i, batch_bytes=0, min_batch=1 << 20, max_batch=4 << 20,
+                corrupt_payload_ppm=corrupt) for i in range(2)]
+    got, ref = run_both(engine, oracle, segs, chunk=256 << 10)
+    assert_same(got, ref)
+    assert int(np.max(ref.batches["size_bytes"])) > 2 << 20
