@@ -2225,13 +2225,10 @@ DEV void exec_linked(const DeviceJob& j, lds_u8* ring, SeqRec* buf, uint32_t ite
 #endif
 }
 
-// up to 64 consecutive block items (independent pieces; linked ones skipped)
-DEV void exec_chunk(const DeviceJob& j, lds_u8* ring, SeqRec* buf, uint32_t base, uint32_t nblk,
-                    const __attribute__((address_space(3))) uint32_t* pat) {
-    const uint32_t end = base + 64 < nblk ? base + 64 : nblk;
-    for (uint32_t p = base; p < end; p++) {
-        const uint32_t kind = uni32(j.blocks[p].kind);
-        if (kind & kBlkLinked) continue;
+// one independent piece
+DEV void exec_one(const DeviceJob& j, lds_u8* ring, SeqRec* buf, uint32_t p, uint32_t kind,
+                  const __attribute__((address_space(3))) uint32_t* pat) {
+    {
         const uint64_t dst = uni64(j.blocks[p].dst);
         XRing x;
         // a piece longer than the ring wraps it: wrap-aware like a linked frame
@@ -2254,10 +2251,25 @@ DEV void exec_chunk(const DeviceJob& j, lds_u8* ring, SeqRec* buf, uint32_t base
     }
 }
 
+// up to 64 consecutive block items (independent pieces; linked ones and the
+// long ones, run first on their own, skipped)
+DEV void exec_chunk(const DeviceJob& j, lds_u8* ring, SeqRec* buf, uint32_t base, uint32_t nblk,
+                    const __attribute__((address_space(3))) uint32_t* pat) {
+    const uint32_t end = base + 64 < nblk ? base + 64 : nblk;
+    for (uint32_t p = base; p < end; p++) {
+        const uint32_t kind = uni32(j.blocks[p].kind);
+        if ((kind & kBlkLinked) || piece_is_long(kind, uni32(j.blocks[p].csize))) continue;
+        exec_one(j, ring, buf, p, kind, pat);
+    }
+}
+
 // ---------------------------------------------------------------------------
 // k_lz_exec: persistent, one wave per workgroup (64 KiB LDS ring each),
 // j.exec_waves of them; units by one agent-scope counter (counters[8]):
-// first the linked frames, then the block list in chunks of 64.
+// first the linked frames, then the long pieces one unit each (a 1 MiB raw
+// snappy payload is ~1000 record batches: taken first, and alone, it no
+// longer ends the kernel behind 63 other pieces of its chunk), then the
+// block list in chunks of 64.
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(64) void k_lz_exec(DeviceJob j) {
     extern __shared__ __attribute__((aligned(16))) uint8_t xlds[];
@@ -2271,12 +2283,20 @@ __global__ __launch_bounds__(64) void k_lz_exec(DeviceJob j) {
     const uint32_t nlink = j.counters[7];
     const uint32_t reserved = j.counters[4];
     const uint32_t nblk = reserved < j.block_capacity ? reserved : j.block_capacity;
-    const uint32_t total = nlink + (nblk + 63) / 64;
+    const uint32_t nlong = j.counters[11];
+    const uint32_t total = nlink + nlong + (nblk + 63) / 64;
     for (;;) {
         const uint32_t u = wave_fetch_add(&j.counters[8], 1u);
         if (u >= total) break;
-        if (u < nlink) exec_linked(j, ring, buf, uni32(j.link_list[u]), pat);
-        else exec_chunk(j, ring, buf, (u - nlink) * 64, nblk, pat);
+        if (u < nlink) {
+            exec_linked(j, ring, buf, uni32(j.link_list[u]), pat);
+        } else if (u < nlink + nlong) {
+            const uint32_t p = uni32(j.long_list[u - nlink]);
+            const uint32_t kind = uni32(j.blocks[p].kind);
+            if (!(kind & kBlkLinked)) exec_one(j, ring, buf, p, kind, pat);
+        } else {
+            exec_chunk(j, ring, buf, (u - nlink - nlong) * 64, nblk, pat);
+        }
     }
 }
 
