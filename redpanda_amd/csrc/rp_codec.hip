@@ -1703,23 +1703,22 @@ DEV void walk_snappy_long(const DeviceJob& j, Piece& pc, SlabSink& sink, lds_u8*
                 if (off == 0) bad = true;
             }
         }
-        // the true tags among the 64 (scalar hops)
+        // the true tags among the 64 (scalar hops; the bad bits one ballot)
+        const uint64_t badm = __ballot(bad);
         uint64_t chain = 0;
         uint32_t qn = ip;
         while (qn - ip < 64 && qn < n) {
             const int k = (int)(qn - ip);
             chain |= 1ull << k;
-            if (rl((uint32_t)bad, k)) break;
+            if ((badm >> k) & 1) break;
             qn = rl(nxt, k);
         }
         const bool on = (chain >> l) & 1;
-        // output before each chain tag
-        uint64_t incl = on ? out : 0;
-        for (int d = 1; d < 64; d <<= 1) {
-            const uint64_t v = shfl_up64(incl, d);
-            if (l >= (uint32_t)d) incl += v;
-        }
-        const uint64_t opt = op + incl - (on ? out : 0);
+        // output before each chain tag: a 32-bit DPP scan (a good chain tag's
+        // output is a literal inside the stream or a copy of <= 64 bytes)
+        const uint32_t o32 = on ? (uint32_t)out : 0u;
+        const uint32_t incl = wave_scan(o32);
+        const uint64_t opt = op + (incl - o32);
         const bool fail = on && (bad || (int64_t)(ulen - opt) < (int64_t)out || (t != 0 && opt < off));
         if (__ballot(fail)) {
             st = -1;
@@ -1760,10 +1759,10 @@ DEV void walk_snappy_long(const DeviceJob& j, Piece& pc, SlabSink& sink, lds_u8*
                 m &= m - 1;
             }
             ip = rl(nxt, (int)kk);
-            op = op + rl64(incl, (int)kk);
+            op = op + rl(incl, (int)kk);
             break;
         }
-        op += rl64(incl, 63);
+        op += rl(incl, 63);
         ip = qn;
     }
     pc.ps.ip = (int32_t)ip;
@@ -1868,26 +1867,24 @@ DEV void walk_lz4_wave(const DeviceJob& j, Piece& pc, SlabSink& sink, lds_u8* wi
             }
         }
         // the true sequences among the 64, up to the first one not handled here
+        const uint64_t okm = __ballot(ok);
         uint64_t chain = 0;
         int64_t qn = ip;
         bool stop = false;
         while (qn - ip < 64) {
             const int k = (int)(qn - ip);
-            if (!rl((uint32_t)ok, k)) {
+            if (!((okm >> k) & 1)) {
                 stop = true;
                 break;
             }
             chain |= 1ull << k;
             qn = (int64_t)rl64((uint64_t)nxt, k);
         }
-        // output positions; the op-dependent fast-loop conditions
+        // output positions (32-bit DPP scan: chain sequences lie inside the
+        // block); the op-dependent fast-loop conditions
         const bool on = (chain >> l) & 1;
-        const uint64_t len = on ? (uint64_t)(ll + ml) : 0ull;
-        uint64_t incl = len;
-        for (int d = 1; d < 64; d <<= 1) {
-            const uint64_t v = shfl_up64(incl, d);
-            if (l >= (uint32_t)d) incl += v;
-        }
+        const uint32_t len = on ? (uint32_t)(ll + ml) : 0u;
+        const uint32_t incl = wave_scan(len);
         const int64_t opt = op + (int64_t)(incl - len);  // output at the sequence start
         const bool go_safe = on && ((ll >= 15 && opt + ll > oend - 32) || opt + ll + ml >= oend - kFastSafeDistance);
         const uint64_t gm = __ballot(go_safe);
@@ -1937,7 +1934,7 @@ DEV void walk_lz4_wave(const DeviceJob& j, Piece& pc, SlabSink& sink, lds_u8* wi
             kk = (uint32_t)__builtin_ctzll(m2);
             m2 &= m2 - 1;
         }
-        op += (int64_t)rl64(incl, (int)kk);
+        op += (int64_t)rl(incl, (int)kk);
         ip = (int64_t)rl64((uint64_t)nxt, (int)kk);
         if (stop || cut || emit < cnt) break;
     }
