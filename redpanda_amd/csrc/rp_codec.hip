@@ -1651,16 +1651,28 @@ DEV uint64_t shfl_up64(uint64_t v, int d) {
 DEV void walk_snappy_long(const DeviceJob& j, Piece& pc, SlabSink& sink, lds_u8* win) {
     typedef __attribute__((address_space(3))) const uint32_t lds_cu32;
     const uint32_t l = lane();
-    const uint32_t n = (uint32_t)pc.s.n;
-    const uint64_t ulen = pc.ps.ulen;
-    uint32_t ip = (uint32_t)pc.ps.ip;
-    uint64_t op = (uint32_t)pc.ps.op;
+    // the walk state is wave-uniform: kept in SGPRs (readfirstlane), or the
+    // compiler runs the hop loop below as a divergent VGPR loop (~250 cycles
+    // per hop measured, against a few SALU instructions)
+    const uint32_t n = uni32((uint32_t)pc.s.n);
+    const uint64_t ulen = uni32(pc.ps.ulen);
+    uint32_t ip = uni32((uint32_t)pc.ps.ip);
+    uint64_t op = uni32((uint32_t)pc.ps.op);
     int32_t st = 0;
     uint32_t slab = sink.slab, pos = sink.pos, nrec = sink.n;
     bool cut = false;
     int64_t w0 = -1;
     lds_cu32* w32 = (lds_cu32*)win;
+#ifdef RPGPU_DSTAMPS
+    uint64_t ds_it = 0, ds_hops = 0, ds_c0 = 0, ds_c1 = 0, ds_c2 = 0;
+#endif
     while (st == 0 && !cut) {
+        ip = uni32(ip);
+        op = uni64(op);
+#ifdef RPGPU_DSTAMPS
+        const uint64_t q0 = __builtin_amdgcn_s_memtime();
+        ds_it++;
+#endif
         if (ip >= n) {
             st = op == ulen ? 1 : -1;
             break;
@@ -1703,16 +1715,39 @@ DEV void walk_snappy_long(const DeviceJob& j, Piece& pc, SlabSink& sink, lds_u8*
                 if (off == 0) bad = true;
             }
         }
-        // the true tags among the 64 (scalar hops; the bad bits one ballot)
-        const uint64_t badm = __ballot(bad);
-        uint64_t chain = 0;
-        uint32_t qn = ip;
-        while (qn - ip < 64 && qn < n) {
-            const int k = (int)(qn - ip);
-            chain |= 1ull << k;
-            if ((badm >> k) & 1) break;
-            qn = rl(nxt, k);
+#ifdef RPGPU_DSTAMPS
+        const uint64_t q1 = __builtin_amdgcn_s_memtime();
+#endif
+        // the true tags among the 64, by pointer doubling: J = the lane of
+        // the next tag (itself where the chain leaves the window, ends the
+        // stream or meets a bad tag), F = the lanes visited from here; after
+        // six rounds (F, J) <- (F | F[J], J[J]) lane 0's F is the chain.  (A
+        // scalar hop per tag, readlane -> SALU -> branch, cost ~130 cycles
+        // each.)
+        uint32_t J = l;
+        if (!bad && nxt != 0xFFFFFFFFu && nxt - ip < 64u && nxt < n) J = nxt - ip;
+        uint64_t F = 1ull << l;
+#pragma unroll
+        for (int t = 0; t < 6; t++) {
+            const uint32_t Jo = (uint32_t)__shfl((int)J, (int)J, 64);
+            const uint32_t flo = (uint32_t)__shfl((int)(uint32_t)F, (int)J, 64);
+            const uint32_t fhi = (uint32_t)__shfl((int)(uint32_t)(F >> 32), (int)J, 64);
+            F |= (uint64_t)flo | ((uint64_t)fhi << 32);
+            J = Jo;
         }
+        const uint64_t chain = (uint64_t)uni32((uint32_t)rl((uint32_t)F, 0)) |
+                               ((uint64_t)uni32(rl((uint32_t)(F >> 32), 0)) << 32);
+        // where the next iteration starts: the last chain tag's successor
+        const int last = 63 - __builtin_clzll(chain);
+        const uint32_t qn = uni32(rl(nxt, last));
+#ifdef RPGPU_DSTAMPS
+        ds_hops += (uint64_t)__builtin_popcountll(chain);
+#endif
+#ifdef RPGPU_DSTAMPS
+        const uint64_t q2 = __builtin_amdgcn_s_memtime();
+        ds_c0 += q1 - q0;
+        ds_c1 += q2 - q1;
+#endif
         const bool on = (chain >> l) & 1;
         // output before each chain tag: a 32-bit DPP scan (a good chain tag's
         // output is a literal inside the stream or a copy of <= 64 bytes)
@@ -1764,7 +1799,19 @@ DEV void walk_snappy_long(const DeviceJob& j, Piece& pc, SlabSink& sink, lds_u8*
         }
         op += rl(incl, 63);
         ip = qn;
+#ifdef RPGPU_DSTAMPS
+        ds_c2 += __builtin_amdgcn_s_memtime() - q2;
+#endif
     }
+#ifdef RPGPU_DSTAMPS
+    if (lane() == 0) {
+        atomicAdd(&g_dst[40], ds_it);
+        atomicAdd(&g_dst[41], ds_hops);
+        atomicAdd(&g_dst[42], ds_c0);
+        atomicAdd(&g_dst[43], ds_c1);
+        atomicAdd(&g_dst[44], ds_c2);
+    }
+#endif
     pc.ps.ip = (int32_t)ip;
     pc.ps.op = (int32_t)(uint32_t)op;
     pc.ps.st = st;
@@ -1806,15 +1853,18 @@ DEV void sink_resync(SlabSink& sink) {
 DEV void walk_lz4_wave(const DeviceJob& j, Piece& pc, SlabSink& sink, lds_u8* win) {
     typedef __attribute__((address_space(3))) const uint32_t lds_cu32;
     const uint32_t l = lane();
-    const int64_t iend = pc.s.n, oend = (int64_t)pc.cap;
+    const int64_t iend = (int64_t)uni64((uint64_t)pc.s.n), oend = (int64_t)uni32(pc.cap);
     if (pc.ps.st != 0 || pc.ps.safe) return;
-    int64_t ip = pc.ps.ip, op = pc.ps.op;
+    // wave-uniform walk state in SGPRs (see walk_snappy_long)
+    int64_t ip = (int32_t)uni32((uint32_t)pc.ps.ip), op = (int32_t)uni32((uint32_t)pc.ps.op);
     int32_t need = pc.ps.need;
     uint32_t slab = sink.slab, pos = sink.pos, nrec = sink.n;
     bool cut = false;
     int64_t w0 = -1;
     lds_cu32* w32 = (lds_cu32*)win;
     for (;;) {
+        ip = (int64_t)uni64((uint64_t)ip);
+        op = (int64_t)uni64((uint64_t)op);
         if (w0 < 0 || ip + 72 > w0 + kWalkWin) {
             w0 = ip & ~15ll;
 #pragma unroll
@@ -1878,7 +1928,7 @@ DEV void walk_lz4_wave(const DeviceJob& j, Piece& pc, SlabSink& sink, lds_u8* wi
                 break;
             }
             chain |= 1ull << k;
-            qn = (int64_t)rl64((uint64_t)nxt, k);
+            qn = (int64_t)uni64(rl64((uint64_t)nxt, k));
         }
         // output positions (32-bit DPP scan: chain sequences lie inside the
         // block); the op-dependent fast-loop conditions
@@ -2423,6 +2473,9 @@ __global__ void k_print_dstamps() {
            "max_ms=%.2f (nrec %llu csize %llu kind %llu) | wave end spread ms=%.2f\n",
            g[25], g[24] / 1e5, g[26] / 1e5, g[32], g[33], g[28], g[27] / 1e5, g[29] / 1e5, g[30], g[31] & 0xFFFFFFFFull,
            g[31] >> 32, (double)(g[34] - g[35]) / 1e5);
+    printf("RPGPU_DSTAMPS snappy-long iterations=%llu hops=%llu | per iteration clk: decode=%.0f hops=%.0f rest=%.0f\n",
+           g[40], g[41], (double)g[42] / (g[40] ? g[40] : 1), (double)g[43] / (g[40] ? g[40] : 1),
+           (double)g[44] / (g[40] ? g[40] : 1));
     for (int i = 0; i < 64; i++) g_dst[i] = 0;
 }
 __global__ void k_init_dstamps() {
