@@ -938,8 +938,16 @@ DEV int in_varint(In& in, int64_t pos, int64_t n, uint32_t& v) {
 #ifndef RPGPU_LONG_LZ4
 #define RPGPU_LONG_LZ4 65536u
 #endif
-DEV bool piece_is_long(uint32_t kind, uint32_t csize) {
-    return !(kind & kBlkRaw) && ((kind & kBlkWhole) || csize > RPGPU_LONG_LZ4);
+// dense pieces (decoded capacity >= RPGPU_DENSE_RATIO x compressed, at least
+// 4 KiB compressed: thousands of short sequences) are wave-walked too, where
+// the window-parallel parse takes ~13 sequences per step; literal-heavy ones
+// stay on the lane walk, whose 256-byte windows skip long literals
+#ifndef RPGPU_DENSE_RATIO
+#define RPGPU_DENSE_RATIO 3u
+#endif
+DEV bool piece_is_long(uint32_t kind, uint32_t csize, uint32_t cap) {
+    return !(kind & kBlkRaw) && ((kind & kBlkWhole) || csize > RPGPU_LONG_LZ4 ||
+                                 (RPGPU_DENSE_RATIO && csize >= 4096u && cap >= RPGPU_DENSE_RATIO * csize));
 }
 
 // a long piece (walked by a wave in k_lz_walk): lane 0 appends it
@@ -1013,7 +1021,7 @@ DEV bool plan_lz4f(const DeviceJob& j, In& in, int64_t n, uint64_t src_abs, uint
             it.out = -1;
             it.cap = raw ? (uint32_t)bsz : (uint32_t)bmax;
             j.blocks[first + k] = it;
-            if (piece_is_long(it.kind, it.csize)) note_long(j, first + k);
+            if (piece_is_long(it.kind, it.csize, it.cap)) note_long(j, first + k);
         }
         plan += raw ? (uint64_t)bsz : (uint64_t)bmax;
         pos += 4 + bsz + (bcs ? 4 : 0);
@@ -1074,7 +1082,7 @@ DEV bool plan_snappy_java(const DeviceJob& j, In& in, int64_t n, uint64_t src_ab
             it.out = -1;
             it.cap = ulen;
             j.blocks[first + k] = it;
-            if (piece_is_long(it.kind, it.csize)) note_long(j, first + k);
+            if (piece_is_long(it.kind, it.csize, it.cap)) note_long(j, first + k);
         }
         plan += ulen;
         pos += clen;
@@ -1917,18 +1925,27 @@ DEV void walk_lz4_wave(const DeviceJob& j, Piece& pc, SlabSink& sink, lds_u8* wi
             }
         }
         // the true sequences among the 64, up to the first one not handled here
+        // chain by pointer doubling (walk_snappy_long): J = the lane of the
+        // next sequence, itself where the chain leaves the window or at a
+        // sequence not handled here; the chain ends before the first such one
         const uint64_t okm = __ballot(ok);
-        uint64_t chain = 0;
-        int64_t qn = ip;
+        uint32_t J = l;
+        if (ok && nxt - ip < 64) J = (uint32_t)(nxt - ip);
+        uint64_t F = 1ull << l;
+#pragma unroll
+        for (int t = 0; t < 6; t++) {
+            const uint32_t Jo = (uint32_t)__shfl((int)J, (int)J, 64);
+            const uint32_t flo = (uint32_t)__shfl((int)(uint32_t)F, (int)J, 64);
+            const uint32_t fhi = (uint32_t)__shfl((int)(uint32_t)(F >> 32), (int)J, 64);
+            F |= (uint64_t)flo | ((uint64_t)fhi << 32);
+            J = Jo;
+        }
+        uint64_t chain = (uint64_t)uni32(rl((uint32_t)F, 0)) | ((uint64_t)uni32(rl((uint32_t)(F >> 32), 0)) << 32);
+        const uint64_t nok = chain & ~okm;
         bool stop = false;
-        while (qn - ip < 64) {
-            const int k = (int)(qn - ip);
-            if (!((okm >> k) & 1)) {
-                stop = true;
-                break;
-            }
-            chain |= 1ull << k;
-            qn = (int64_t)uni64(rl64((uint64_t)nxt, k));
+        if (nok) {
+            chain &= (1ull << __builtin_ctzll(nok)) - 1;
+            stop = true;
         }
         // output positions (32-bit DPP scan: chain sequences lie inside the
         // block); the op-dependent fast-loop conditions
@@ -2128,7 +2145,7 @@ __global__ __launch_bounds__(256) void k_lz_walk(DeviceJob j) {
                 break;
             }
             const BlockItem it = j.blocks[p];
-            if (piece_is_long(it.kind, it.csize)) continue;  // walked above
+            if (piece_is_long(it.kind, it.csize, it.cap)) continue;  // walked above
             piece_begin(pc, j, it);
             first_slab = 0xFFFFFFFFu;
             if (pc.ps.st == 0) {
@@ -2305,7 +2322,7 @@ DEV void exec_chunk(const DeviceJob& j, lds_u8* ring, SeqRec* buf, uint32_t base
     const uint32_t end = base + 64 < nblk ? base + 64 : nblk;
     for (uint32_t p = base; p < end; p++) {
         const uint32_t kind = uni32(j.blocks[p].kind);
-        if ((kind & kBlkLinked) || piece_is_long(kind, uni32(j.blocks[p].csize))) continue;
+        if ((kind & kBlkLinked) || piece_is_long(kind, uni32(j.blocks[p].csize), uni32(j.blocks[p].cap))) continue;
         exec_one(j, ring, buf, p, kind, pat);
     }
 }
