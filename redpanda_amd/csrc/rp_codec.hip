@@ -938,16 +938,22 @@ DEV int in_varint(In& in, int64_t pos, int64_t n, uint32_t& v) {
 #ifndef RPGPU_LONG_LZ4
 #define RPGPU_LONG_LZ4 65536u
 #endif
-// dense pieces (decoded capacity >= RPGPU_DENSE_RATIO x compressed, at least
-// 4 KiB compressed: thousands of short sequences) are wave-walked too, where
-// the window-parallel parse takes ~13 sequences per step; literal-heavy ones
-// stay on the lane walk, whose 256-byte windows skip long literals
-#ifndef RPGPU_DENSE_RATIO
-#define RPGPU_DENSE_RATIO 3u
+// dense pieces (decoded capacity >= RPGPU_DENSE_X10 / 10 x compressed, at least
+// RPGPU_DENSE_MIN compressed: thousands of short sequences) are wave-walked
+// too, where the window-parallel parse takes ~13 sequences per step;
+// literal-heavy ones stay on the lane walk, whose 256-byte windows skip long
+// literals.  Measured (step ms C2 / C5): off 65.4 / 38.4; x3 from 4 KiB
+// 65.4 / 23.1; x2 from 1 KiB 64.5 / 23.1.
+#ifndef RPGPU_DENSE_X10
+#define RPGPU_DENSE_X10 20u
+#endif
+#ifndef RPGPU_DENSE_MIN
+#define RPGPU_DENSE_MIN 1024u
 #endif
 DEV bool piece_is_long(uint32_t kind, uint32_t csize, uint32_t cap) {
-    return !(kind & kBlkRaw) && ((kind & kBlkWhole) || csize > RPGPU_LONG_LZ4 ||
-                                 (RPGPU_DENSE_RATIO && csize >= 4096u && cap >= RPGPU_DENSE_RATIO * csize));
+    return !(kind & kBlkRaw) &&
+           ((kind & kBlkWhole) || csize > RPGPU_LONG_LZ4 ||
+            (RPGPU_DENSE_X10 && csize >= RPGPU_DENSE_MIN && 10ull * cap >= (uint64_t)RPGPU_DENSE_X10 * csize));
 }
 
 // a long piece (walked by a wave in k_lz_walk): lane 0 appends it
