@@ -956,6 +956,13 @@ DEV bool piece_is_long(uint32_t kind, uint32_t csize, uint32_t cap) {
             (RPGPU_DENSE_X10 && csize >= RPGPU_DENSE_MIN && 10ull * cap >= (uint64_t)RPGPU_DENSE_X10 * csize));
 }
 
+// long pieces base + i for the set bits i of m (lane 0): one atomic per 64
+// blocks of a frame (one per piece cost the planner ~1 ms on C2's dense blocks)
+DEV void note_longs(const DeviceJob& j, uint32_t base, uint64_t m) {
+    if (!m) return;
+    uint32_t at = atomicAdd(&j.counters[11], (uint32_t)__builtin_popcountll(m));
+    for (; m; m &= m - 1) j.long_list[at++] = base + (uint32_t)__builtin_ctzll(m);
+}
 // a long piece (walked by a wave in k_lz_walk): lane 0 appends it
 DEV void note_long(const DeviceJob& j, uint32_t idx) {
     const uint32_t at = atomicAdd(&j.counters[11], 1u);
@@ -1013,7 +1020,7 @@ DEV bool plan_lz4f(const DeviceJob& j, In& in, int64_t n, uint64_t src_abs, uint
     const uint32_t first = reserve_blocks(j, nb);
     if (first == 0xFFFFFFFFu) return false;
     pos = hsize;
-    uint64_t plan = 0;
+    uint64_t plan = 0, lm = 0;
     for (uint32_t k = 0; k < nb; k++) {
         const uint32_t bh = in_le32(in, pos);
         const int64_t bsz = bh & 0x7FFFFFFFu;
@@ -1027,7 +1034,11 @@ DEV bool plan_lz4f(const DeviceJob& j, In& in, int64_t n, uint64_t src_abs, uint
             it.out = -1;
             it.cap = raw ? (uint32_t)bsz : (uint32_t)bmax;
             j.blocks[first + k] = it;
-            if (piece_is_long(it.kind, it.csize, it.cap)) note_long(j, first + k);
+            if (piece_is_long(it.kind, it.csize, it.cap)) lm |= 1ull << (k & 63);
+            if ((k & 63) == 63 || k + 1 == nb) {
+                note_longs(j, first + (k & ~63u), lm);
+                lm = 0;
+            }
         }
         plan += raw ? (uint64_t)bsz : (uint64_t)bmax;
         pos += 4 + bsz + (bcs ? 4 : 0);
@@ -1072,7 +1083,7 @@ DEV bool plan_snappy_java(const DeviceJob& j, In& in, int64_t n, uint64_t src_ab
     const uint32_t first = reserve_blocks(j, nb);
     if (first == 0xFFFFFFFFu) return false;
     pos = 16;
-    uint64_t plan = 0;
+    uint64_t plan = 0, lm = 0;
     for (uint32_t k = 0; k < nb; k++) {
         const int32_t clen = (int32_t)((in_byte(in, pos) << 24) | (in_byte(in, pos + 1) << 16) |
                                        (in_byte(in, pos + 2) << 8) | in_byte(in, pos + 3));
@@ -1088,7 +1099,11 @@ DEV bool plan_snappy_java(const DeviceJob& j, In& in, int64_t n, uint64_t src_ab
             it.out = -1;
             it.cap = ulen;
             j.blocks[first + k] = it;
-            if (piece_is_long(it.kind, it.csize, it.cap)) note_long(j, first + k);
+            if (piece_is_long(it.kind, it.csize, it.cap)) lm |= 1ull << (k & 63);
+            if ((k & 63) == 63 || k + 1 == nb) {
+                note_longs(j, first + (k & ~63u), lm);
+                lm = 0;
+            }
         }
         plan += ulen;
         pos += clen;
