@@ -955,6 +955,20 @@ DEV bool piece_is_long(uint32_t kind, uint32_t csize, uint32_t cap) {
            ((kind & kBlkWhole) || csize > RPGPU_LONG_LZ4 ||
             (RPGPU_DENSE_X10 && csize >= RPGPU_DENSE_MIN && 10ull * cap >= (uint64_t)RPGPU_DENSE_X10 * csize));
 }
+// Long pieces all run alone in k_lz_exec.  Dense ones are wave-walked only
+// when the job has few pieces for the lanes the walk keeps resident
+// (few_pieces): with many, the lane walk does them faster in aggregate (C2,
+// ~250 K pieces: step 63.7 -> 56.2 ms with its dense LZ4 blocks on the lane
+// walk); with few, lanes sit idle behind the slowest ones (C5, ~55 K pieces:
+// 23.1 -> 31.5 ms without the wave walk, 28.9 with only its snappy chunks on
+// it).  RPGPU_DENSE_WALK 1 / 0 force it on / off (diagnostics).
+#ifndef RPGPU_DENSE_WALK
+#define RPGPU_DENSE_WALK 2
+#endif
+DEV bool piece_wave_walked(uint32_t kind, uint32_t csize, uint32_t cap, bool few_pieces) {
+    if (RPGPU_DENSE_WALK == 1 || (RPGPU_DENSE_WALK == 2 && few_pieces)) return piece_is_long(kind, csize, cap);
+    return !(kind & kBlkRaw) && ((kind & kBlkWhole) || csize > RPGPU_LONG_LZ4);
+}
 
 // long pieces base + i for the set bits i of m (lane 0): one atomic per 64
 // blocks of a frame (one per piece cost the planner ~1 ms on C2's dense blocks)
@@ -2145,11 +2159,17 @@ __global__ __launch_bounds__(256) void k_lz_walk(DeviceJob j) {
     const uint32_t reserved = j.counters[4];
     const uint32_t nblk = reserved < j.block_capacity ? reserved : j.block_capacity;
     const uint32_t nlong = j.counters[11];
+    // few pieces: fewer than 512 per CU (the grid is 16 workgroups per CU, 2
+    // resident: 512 lanes)
+    const bool few = nblk < gridDim.x * 32u;
     lds_u8* wl = (lds_u8*)wwin[threadIdx.x >> 6];
     for (;;) {
         const uint32_t k = wave_fetch_add(&j.counters[12], 1u);
         if (k >= nlong) break;
-        walk_long(j, uni32(j.long_list[k]), wl);
+        const uint32_t p = uni32(j.long_list[k]);
+        if (!piece_wave_walked(uni32(j.blocks[p].kind), uni32(j.blocks[p].csize), uni32(j.blocks[p].cap), few))
+            continue;  // a dense piece: the lane walk takes it
+        walk_long(j, p, wl);
     }
     lds_u8* slot = wl + kLaneSlot * lane();
     bool active = false, drained = false;
@@ -2166,7 +2186,7 @@ __global__ __launch_bounds__(256) void k_lz_walk(DeviceJob j) {
                 break;
             }
             const BlockItem it = j.blocks[p];
-            if (piece_is_long(it.kind, it.csize, it.cap)) continue;  // walked above
+            if (piece_wave_walked(it.kind, it.csize, it.cap, few)) continue;  // walked above
             piece_begin(pc, j, it);
             first_slab = 0xFFFFFFFFu;
             if (pc.ps.st == 0) {
