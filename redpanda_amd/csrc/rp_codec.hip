@@ -950,10 +950,17 @@ DEV int in_varint(In& in, int64_t pos, int64_t n, uint32_t& v) {
 #ifndef RPGPU_DENSE_MIN
 #define RPGPU_DENSE_MIN 1024u
 #endif
+#ifndef RPGPU_ALONE_MIN
+#define RPGPU_ALONE_MIN 0u
+#endif
+DEV bool piece_dense(uint32_t csize, uint32_t cap) {
+    return RPGPU_DENSE_X10 && csize >= RPGPU_DENSE_MIN && 10ull * cap >= (uint64_t)RPGPU_DENSE_X10 * csize;
+}
+// the pieces k_lz_exec runs alone (the long list): long, dense, and (with
+// RPGPU_ALONE_MIN) every compressed piece of at least that many bytes
 DEV bool piece_is_long(uint32_t kind, uint32_t csize, uint32_t cap) {
-    return !(kind & kBlkRaw) &&
-           ((kind & kBlkWhole) || csize > RPGPU_LONG_LZ4 ||
-            (RPGPU_DENSE_X10 && csize >= RPGPU_DENSE_MIN && 10ull * cap >= (uint64_t)RPGPU_DENSE_X10 * csize));
+    return !(kind & kBlkRaw) && ((kind & kBlkWhole) || csize > RPGPU_LONG_LZ4 || piece_dense(csize, cap) ||
+                                 (RPGPU_ALONE_MIN && csize >= RPGPU_ALONE_MIN));
 }
 // Long pieces all run alone in k_lz_exec.  Dense ones are wave-walked only
 // when the job has few pieces for the lanes the walk keeps resident
@@ -966,8 +973,8 @@ DEV bool piece_is_long(uint32_t kind, uint32_t csize, uint32_t cap) {
 #define RPGPU_DENSE_WALK 2
 #endif
 DEV bool piece_wave_walked(uint32_t kind, uint32_t csize, uint32_t cap, bool few_pieces) {
-    if (RPGPU_DENSE_WALK == 1 || (RPGPU_DENSE_WALK == 2 && few_pieces)) return piece_is_long(kind, csize, cap);
-    return !(kind & kBlkRaw) && ((kind & kBlkWhole) || csize > RPGPU_LONG_LZ4);
+    const bool dense = RPGPU_DENSE_WALK == 1 || (RPGPU_DENSE_WALK == 2 && few_pieces);
+    return !(kind & kBlkRaw) && ((kind & kBlkWhole) || csize > RPGPU_LONG_LZ4 || (dense && piece_dense(csize, cap)));
 }
 
 // long pieces base + i for the set bits i of m (lane 0): one atomic per 64
