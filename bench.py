@@ -45,6 +45,41 @@ C2_PARTS, C2_SEG = 8, 3 << 29
 C5_PARTS, C5_SEG = 128, 64 << 20
 
 
+# index writes 48 B per record, result 64 B per batch
+IDX_BYTES_PER_RECORD = 48
+RESULT_BYTES_PER_BATCH = 64
+DECODE_KERNELS = ("k_decode", "k_decode_blocks", "k_lz_walk", "k_lz_exec", "k_decode_finish")
+
+
+def profiled_traffic(fname, workload, kernels):
+    """HBM bytes per launch from the committed PMC summary
+    (scripts/parse_traffic.py -> profiles/<fname>): the sum over `kernels`
+    and the per-kernel table (bytes, algorithmic bytes, ratio)."""
+    path = os.path.join(ROOT, "profiles", fname)
+    try:
+        tj = json.load(open(path)).get(workload)
+    except Exception:
+        return None, None
+    if not tj:
+        return None, None
+    ks = tj.get("kernels", {})
+    tot = [ks[k]["bytes"] for k in kernels if k in ks and ks[k].get("bytes") is not None]
+    return (int(sum(tot)) if tot else None), {"source": f"profiles/{fname} ({tj.get('tag')})", **ks}
+
+
+def write_stats(args, name, d):
+    """Merge one workload's byte counts into --stats-out (per-kernel
+    algorithmic bytes for the PMC summary, scripts/parse_traffic.py)."""
+    if not args.stats_out:
+        return
+    try:
+        cur = json.load(open(args.stats_out))
+    except Exception:
+        cur = {}
+    cur[name] = d
+    json.dump(cur, open(args.stats_out, "w"), indent=1)
+
+
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
@@ -195,6 +230,7 @@ def run_compressed(name, kw, n_parts, seg_bytes, args, torch, device, eng, abi, 
         "crc_ok": int(np.sum(crc_ok)),
         "parse_ok": int(np.sum((f & abi.F_PARSE_OK) != 0)),
         "overflow": int(h.totals["overflow"]),
+        "discovery_rewalks": int(h.totals["n_rewalks"]),
         "records_eq_sum_parsed": bool(n_rec >= int(np.sum(b["records_parsed"].astype(np.int64)))),
         "terminal_errc": {int(k): int(v) for k, v in zip(*np.unique(h.summaries["terminal_errc"], return_counts=True))},
     }
@@ -212,19 +248,22 @@ def run_compressed(name, kw, n_parts, seg_bytes, args, torch, device, eng, abi, 
     tm = eng.last_timings()
     eng.set_timing(False)
     dec_ms = tm["decode"]
+    # decode stage (k_decode .. k_decode_finish): compressed payload read
+    # once + decoded bytes written once
     dec_alg = comp_in + decoded
-    whole_alg = stored + comp_in + 2 * decoded + 64 * n_rec + 128 * len(b)
-    traffic = None
-    tfile = os.path.join(ROOT, "profiles", "decode_traffic.json")
-    if os.path.exists(tfile):
-        try:
-            tj = json.load(open(tfile)).get(name)
-            traffic = tj.get("bytes_per_step") if tj else None
-        except Exception:
-            traffic = None
+    # whole pipeline, SURVEY §8(d) C2/C5 bytes per unit: every stored byte
+    # read once (compressed payloads, uncompressed payloads, headers) +
+    # decoded bytes written once + the index (48 B per record, 64 B per
+    # batch result); the CRC / walk of the decoded bytes is not counted again
+    whole_alg = stored + decoded + IDX_BYTES_PER_RECORD * n_rec + RESULT_BYTES_PER_BATCH * len(b)
+    traffic, kernels_traffic = profiled_traffic("decode_traffic.json", name, DECODE_KERNELS)
     cpu = None
     if not args.no_cpu_baseline and len(positions):
         cpu = cpu_baseline_decode(host_first, positions)
+    write_stats(args, name, {"stored": stored, "stored_payload": int(np.sum(b["size_bytes"].astype(np.int64)
+                                                                          - abi.HEADER_SIZE)),
+                             "compressed_in": comp_in, "decoded": decoded, "batches": int(len(b)),
+                             "compressed_batches": int(np.sum(comp)), "records": n_rec})
     st = {
         "workload": desc,
         "partitions": n_parts,
@@ -239,17 +278,20 @@ def run_compressed(name, kw, n_parts, seg_bytes, args, torch, device, eng, abi, 
         "batches_per_s": round(len(b) / el, 1),
         "hbm_fraction_whole_pipeline": round(whole_alg / el / 1e9 / HBM_PEAK_GBS, 4),
         "whole_alg_bytes": whole_alg,
+        "whole_alg_def": "stored + decoded + 48 B/record + 64 B/batch (SURVEY §8(d))",
         "stage_ms": {k: round(v, 4) for k, v in tm.items()},
         "roofline": {
             "bound": "hbm",
-            "kernel": "decode stage (k_decode*)",
+            "kernel": "decode stage (k_decode .. k_decode_finish)",
             "achieved": round(dec_alg / (dec_ms * 1e-3) / 1e9, 1) if dec_ms > 0 else None,
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
             "frac": round(dec_alg / (dec_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4) if dec_ms > 0 else None,
             "traffic": traffic,
             "alg_bytes_per_launch": dec_alg,
+            "alg_def": "compressed payload read + decoded bytes written",
             "kernel_ms": round(dec_ms, 4),
+            "kernels_traffic": kernels_traffic,
         },
         "parity": parity,
         "cpu_baseline": cpu,
@@ -268,13 +310,18 @@ def main():
     ap.add_argument("--partitions", type=int, default=PARTITIONS_PER_GPU)
     ap.add_argument("--chunk-kib", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--gather", choices=["bitmap", "index"], default="bitmap")
+    ap.add_argument("--gather", choices=["bitmap", "index", "records"], default="bitmap",
+                    help="what travels to rank 0 each step at N > 1: bitmaps + summaries (default), + batch results, "
+                         "+ batch results and the per-record index")
     ap.add_argument("--no-parse", action="store_true", help="CRC only (diagnostic; not the headline workload)")
     ap.add_argument("--no-index", action="store_true", help="skip the segment-index rebuild measurement")
     ap.add_argument("--batch-bytes", type=int, default=BATCH_BYTES,
                     help="size_bytes per batch (diagnostic; the headline workload is 16 KiB)")
+    ap.add_argument("--stats-out", default="",
+                    help="write each workload's byte counts (JSON) here, for scripts/parse_traffic.py")
     ap.add_argument("--workloads", default="c1,c2,c5",
-                    help="c1 is the headline; c2/c5 stanzas run at N = 1 only")
+                    help="c1 is the headline; c2/c5 stanzas run at N = 1 only; a run without c1 is a diagnostic "
+                         "(per-workload profiles)")
     args = ap.parse_args()
     workloads = set(args.workloads.split(","))
 
@@ -282,7 +329,6 @@ def main():
     import torch.distributed as dist
     from redpanda_amd import abi
     from redpanda_amd.engine import Engine
-    from redpanda_amd.shard import as_bytes, gather_bytes, gather_job_verdicts, gather_sizes, partitions_for_rank
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -292,6 +338,54 @@ def main():
     device = torch.device("cuda", local)
     torch.cuda.set_device(device)
 
+    eng = Engine(local)
+    c1 = run_c1(args, torch, dist, device, eng, abi, world, rank) if "c1" in workloads else None
+    if c1 is None and world > 1:
+        raise SystemExit("--gpus N > 1 runs the headline workload (c1)")
+
+    extra = {}
+    if world == 1:
+        if "c2" in workloads:
+            extra["c2"] = run_compressed(
+                "c2", synth.C2, C2_PARTS, C2_SEG, args, torch, device, eng, abi,
+                "C2: 8 partitions x 1.5 GiB disk segments of LZ4 frames (64 KiB blocks, content size; 10% linked, "
+                "10% content checksum), decoded batches uniform 64 KiB..1 MiB, payload thirds random / alnum / "
+                "JSON-like (seed 0xC2): discover + header_crc + crc + LZ4F decode + decoded crc/header_crc + record walk")
+        if "c5" in workloads:
+            extra["c5"] = run_compressed(
+                "c5", synth.C5, C5_PARTS, C5_SEG, args, torch, device, eng, abi,
+                "C5: 128 partitions x 64 MiB, log-uniform 200 B..1 MiB batches, none 40 / lz4 30 / snappy-java 15 / "
+                "raw snappy 15, 1% payload + 0.2% header bit flips, 0.1% zeroed headers, truncated tails (seed 0xC5)")
+
+    if rank == 0:
+        line = {
+            "metric": "validated+decoded batch GB/s per GPU and whole node; % of HBM peak",
+            "value": c1["value"] if c1 else None,
+            "unit": "GB/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": c1["ms_per_step"] if c1 else None,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u8",
+            "data": "synthetic (seeded mt19937_64, reference random_batch recipe), device-resident",
+            "config": {**(c1["config"] if c1 else {"workload": "diagnostic run without the headline (c1) workload"}),
+                       **extra},
+            "roofline": c1["roofline"] if c1 else None,
+            "cpu_baseline": c1["cpu_baseline"] if c1 else None,
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def run_c1(args, torch, dist, device, eng, abi, world, rank):
+    """The headline workload (C1 per GPU; C3 across ranks): returns the
+    fields of the JSON line it owns."""
+    from redpanda_amd.shard import as_bytes, gather_bytes, gather_job_verdicts, gather_records, gather_sizes, \
+        partitions_for_rank
     seg_bytes = int(args.seg_gib * (1 << 30)) // BATCH_BYTES * BATCH_BYTES
     parts = partitions_for_rank(args.partitions * world, world, rank)
     t0 = time.time()
@@ -300,13 +394,23 @@ def main():
     n_batches = int(sum(counts))
     log(f"[rank {rank}] generated {len(parts)} x {seg_bytes >> 20} MiB, {n_batches} batches in {time.time() - t0:.1f}s")
 
-    eng = Engine(local)
     flags = abi.JOB_CRC | (0 if args.no_parse else abi.JOB_PARSE)
     rec_per_batch = 32
     out = eng.alloc_outputs(len(parts), n_batches + 16, n_batches * rec_per_batch, 1)
     d_offs = torch.from_numpy(offs.view(np.int64)).to(device)
     chunk = args.chunk_kib << 10
-    payload = [out.bitmap, out.summaries] + ([out.batches] if args.gather == "index" else [])
+    # the gather payload: validity bitmaps + segment summaries, plus the
+    # per-batch results (--gather index) or the results and the per-record
+    # index (--gather records)
+    payload = [out.bitmap, out.summaries]
+    if args.gather in ("index", "records"):
+        payload.append(out.batches[: n_batches * abi.BATCH_RESULT.itemsize])
+    n_records_est = None
+    if args.gather == "records":
+        eng.submit(data, offs, out, flags, chunk, d_seg_offsets=d_offs)
+        torch.cuda.synchronize(device)
+        n_records_est = int(out.totals_host()["n_records"])
+        payload.append(out.records[: n_records_est * abi.RECORD_INDEX.itemsize])
     # the gather's per-rank lengths are fixed for the run: negotiated once,
     # outside the timed loop (no host sync per step)
     sizes = [gather_sizes(as_bytes(t), world, dist) for t in payload] if world > 1 else None
@@ -314,7 +418,7 @@ def main():
     def step():
         eng.submit(data, offs, out, flags, chunk, d_seg_offsets=d_offs)
         if world > 1:
-            # the one exchange: validity bitmaps + segment summaries to rank 0
+            # the one exchange: to rank 0
             for t, sz in zip(payload, sizes):
                 gather_bytes(as_bytes(t), rank, world, dist, sizes=sz)
 
@@ -328,15 +432,30 @@ def main():
                   and np.all(h.batches["flags"] & abi.F_CRC_OK) and h.totals["overflow"] == 0)
     bm_ok = bool(np.all(h.bitmap[: nb // 64] == np.uint64(0xFFFFFFFFFFFFFFFF)))
     n_records = int(h.totals["n_records"])
+    gathered = None
     if world > 1:
         # the gathered job picture on rank 0: every partition checkpointed at its end
         g = gather_job_verdicts(out.summaries, out.bitmap, nb, parts, rank, world, dist)
         if rank == 0:
             all_ok = bool(all_ok and np.all(g["summaries"]["has_checkpoint"] == 1)
                           and np.all(g["summaries"]["first_bad"] == g["summaries"]["n_batches"]))
+        if args.gather == "records":
+            gr = gather_records(out.batches[: nb * abi.BATCH_RESULT.itemsize],
+                                out.records[: n_records * abi.RECORD_INDEX.itemsize], out.summaries, parts, rank,
+                                world, dist)
+            if rank == 0:
+                b, r = gr["batches"], gr["records"]
+                ok = bool(len(r) == int(np.sum(b["records_parsed"].astype(np.int64)))
+                          and np.all(np.diff(b["index_base"].astype(np.int64)) >= 0)
+                          and np.all(np.diff(r["batch"].astype(np.int64)) >= 0))
+                gathered = {"batches": int(len(b)), "records": int(len(r)), "consistent": ok,
+                            "bytes_per_step": int(sum(max(sz) * world for sz in sizes))}
     payload_bytes = int(np.sum(h.batches["size_bytes"].astype(np.int64) - abi.HEADER_SIZE))
     seg_total = int(np.sum(h.batches["size_bytes"].astype(np.int64)))
     del h
+    if rank == 0:
+        write_stats(args, "c1", {"stored": seg_total, "stored_payload": payload_bytes, "compressed_in": 0, "decoded": 0,
+                                 "batches": n_batches, "compressed_batches": 0, "records": n_records})
 
     eng.set_timing(True)
     if world > 1:
@@ -374,17 +493,11 @@ def main():
     achieved = alg / (v_ms * 1e-3) / 1e9
     walk_alg = 64 * n_records + 128 * n_batches
     w_ms = tm.get("walk", 0.0)
-    whole_alg = seg_total + 64 * n_records + 64 * n_batches  # SURVEY §8(d) C1 bytes per unit
-    traffic = None
-    tfile = os.path.join(ROOT, "profiles", "validate_traffic.json")  # refreshed by scripts/parse_profile.py
-    if os.path.exists(tfile):
-        try:
-            tj = json.load(open(tfile))
-            # only a profile of the same kernel split counts
-            if tj.get("alg_def") == "payload+128B/batch":
-                traffic = tj.get("bytes_per_launch")
-        except Exception:
-            traffic = None
+    # SURVEY §8(d) C1 bytes per unit: segment bytes read once + 48 B per
+    # record + 64 B per batch
+    whole_alg = seg_total + IDX_BYTES_PER_RECORD * n_records + RESULT_BYTES_PER_BATCH * n_batches
+    _, c1_traffic = profiled_traffic("validate_traffic.json", "c1", ("k_validate", "k_walk"))
+    traffic = c1_traffic.get("k_validate", {}).get("bytes") if c1_traffic else None
 
     # segment sparse-index rebuild (segment_index::maybe_track over the
     # recovered batches, §8(f) row 2): timed separately on its own stream,
@@ -405,16 +518,16 @@ def main():
         st.synchronize()
         ix = eng.index_to_host(*res, n_segments=len(parts))
         n_entries = int(sum(int(r[0]["n_entries"]) for r in ix))
-        gathered = None
+        gidx = None
         if world > 1:
             # the job's indexes at rank 0 (RCCL gather of the used entries only)
             from redpanda_amd.shard import gather_segment_index
             g = gather_segment_index(*res, parts, rank, world, dist)
             if rank == 0:
-                gathered = {"partitions": len(g), "entries": int(sum(int(v[0]["n_entries"]) for v in g.values()))}
+                gidx = {"partitions": len(g), "entries": int(sum(int(v[0]["n_entries"]) for v in g.values()))}
         index = {"kernel": "k_idx_cut+k_idx_cand+k_idx_resolve+k_idx_emit", "ms": round(e0.elapsed_time(e1) / reps, 4),
                  "step": abi.INDEX_DEFAULT_STEP, "entries": n_entries,
-                 "tracked": int(sum(int(r[0]["tracked"]) for r in ix)), "gathered_at_rank0": gathered,
+                 "tracked": int(sum(int(r[0]["tracked"]) for r in ix)), "gathered_at_rank0": gidx,
                  "note": "piece-parallel (1024-batch pieces, candidate first entries, serial resolve); "
                          "outputs preallocated, timed region = the four kernels + workspace memset"}
         del ix, res
@@ -425,70 +538,45 @@ def main():
     # release the C1 job before the compressed workloads
     del out, data, d_offs, payload
     torch.cuda.empty_cache()
-
-    extra = {}
-    if world == 1:
-        if "c2" in workloads:
-            extra["c2"] = run_compressed(
-                "c2", synth.C2, C2_PARTS, C2_SEG, args, torch, device, eng, abi,
-                "C2: 8 partitions x 1.5 GiB disk segments of LZ4 frames (64 KiB blocks, content size; 10% linked, "
-                "10% content checksum), decoded batches uniform 64 KiB..1 MiB, payload thirds random / alnum / "
-                "JSON-like (seed 0xC2): discover + header_crc + crc + LZ4F decode + decoded crc/header_crc + record walk")
-        if "c5" in workloads:
-            extra["c5"] = run_compressed(
-                "c5", synth.C5, C5_PARTS, C5_SEG, args, torch, device, eng, abi,
-                "C5: 128 partitions x 64 MiB, log-uniform 200 B..1 MiB batches, none 40 / lz4 30 / snappy-java 15 / "
-                "raw snappy 15, 1% payload + 0.2% header bit flips, 0.1% zeroed headers, truncated tails (seed 0xC5)")
-
-    if rank == 0:
-        line = {
-            "metric": "validated+decoded batch GB/s per GPU and whole node; % of HBM peak",
-            "value": round(value, 2),
+    gather_desc = {"bitmap": "bitmaps+summaries", "index": "bitmaps+summaries+batch results",
+                   "records": "bitmaps+summaries+batch results+record index"}[args.gather]
+    return {
+        "value": round(value, 2),
+        "ms_per_step": round(ms_per_step, 4),
+        "config": {
+            "workload": "C1/C3: per GPU 8 partitions x 2 GiB disk segments of uncompressed 16 KiB batches "
+                        "(seed 0xC1): chain discovery + header_crc + CRC32C + record walk/index + checkpoint",
+            "segment_bytes": seg_bytes,
+            "partitions_per_gpu": len(parts),
+            "batches_per_gpu": n_batches,
+            "records_per_gpu": n_records,
+            "batch_bytes": args.batch_bytes,
+            "batches_per_s": round(job_batches * args.steps / elapsed, 1),
+            "parallelism": f"partition-sharded x{world}, RCCL gather of {gather_desc}",
+            "gathered_records": gathered,
+            "parity": {"all_batches_valid": all_ok, "bitmap_all_ones": bm_ok},
+            "stage_ms": {k: round(v, 4) for k, v in tm.items()},
+            "hbm_fraction_whole_pipeline": round(value / world / HBM_PEAK_GBS, 4),
+            "hbm_fraction_whole_pipeline_alg": round(whole_alg / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+            "whole_alg_def": "segment bytes + 48 B/record + 64 B/batch (SURVEY §8(d))",
+            "segment_index": index,
+        },
+        "roofline": {
+            "bound": "hbm",
+            "kernel": "k_validate",
+            "achieved": round(achieved, 1),
+            "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
-            "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": round(ms_per_step, 4),
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": None,
-            "dtype": "u8",
-            "data": "synthetic (seeded mt19937_64, reference random_batch recipe), device-resident",
-            "config": {
-                "workload": "C1/C3: per GPU 8 partitions x 2 GiB disk segments of uncompressed 16 KiB batches "
-                            "(seed 0xC1): chain discovery + header_crc + CRC32C + record walk/index + checkpoint",
-                "segment_bytes": seg_bytes,
-                "partitions_per_gpu": len(parts),
-                "batches_per_gpu": n_batches,
-                "records_per_gpu": n_records,
-                "batch_bytes": args.batch_bytes,
-                "batches_per_s": round(job_batches * args.steps / elapsed, 1),
-                "parallelism": f"partition-sharded x{world}, RCCL gather of bitmaps+summaries",
-                "parity": {"all_batches_valid": all_ok, "bitmap_all_ones": bm_ok},
-                "stage_ms": {k: round(v, 4) for k, v in tm.items()},
-                "hbm_fraction_whole_pipeline": round(value / world / HBM_PEAK_GBS, 4),
-                "hbm_fraction_whole_pipeline_alg": round(whole_alg / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
-                "segment_index": index,
-                **extra,
-            },
-            "roofline": {
-                "bound": "hbm",
-                "kernel": "k_validate",
-                "achieved": round(achieved, 1),
-                "peak": HBM_PEAK_GBS,
-                "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 4),
-                "traffic": traffic,
-                "alg_bytes_per_launch": alg,
-                "kernel_ms": round(v_ms, 4),
-                "walk": {"kernel": "k_walk", "kernel_ms": round(w_ms, 4), "alg_bytes_per_launch": walk_alg,
-                         "achieved": round(walk_alg / (w_ms * 1e-3) / 1e9, 1) if w_ms > 0 else None},
-            },
-            "cpu_baseline": cpu,
-        }
-        print(json.dumps(line), flush=True)
-    if world > 1:
-        dist.destroy_process_group()
+            "frac": round(achieved / HBM_PEAK_GBS, 4),
+            "traffic": traffic,
+            "alg_bytes_per_launch": alg,
+            "kernel_ms": round(v_ms, 4),
+            "walk": {"kernel": "k_walk", "kernel_ms": round(w_ms, 4), "alg_bytes_per_launch": walk_alg,
+                     "achieved": round(walk_alg / (w_ms * 1e-3) / 1e9, 1) if w_ms > 0 else None},
+            "kernels_traffic": c1_traffic,
+        },
+        "cpu_baseline": cpu,
+    }
 
 
 if __name__ == "__main__":

@@ -448,7 +448,9 @@ typedef struct rpgpu_host_job {
     uint32_t n_segments;
     uint32_t layout;
     uint32_t flags;
-    uint32_t reserved;
+    uint32_t group_kib;              /* staging group size in KiB (0 = 256 MiB): segments are copied and
+                                        validated in groups of at most this many bytes (a larger segment
+                                        is a group of its own) */
     rpgpu_batch_result* batches;     /* host, capacity batch_capacity */
     uint64_t batch_capacity;
     rpgpu_segment_summary* summaries; /* host, n_segments */

@@ -50,6 +50,8 @@ VARIANTS = {
     "": (OUT, BUILD, []),
     "checked": (os.path.join(HERE, "librpgpu_checked.so"), BUILD + "_checked", ["-DRPGPU_CHECKED"]),
     "stamps": (os.path.join(HERE, "librpgpu_stamps.so"), BUILD + "_stamps", ["-DRPGPU_STAMPS"]),
+    # environment overrides (RPGPU_DEBUG_SYNC, RPGPU_POOL_SLABS, ...): diagnostics only
+    "diag": (os.path.join(HERE, "librpgpu_diag.so"), BUILD + "_diag", ["-DRPGPU_DIAG"]),
 }
 
 
@@ -108,5 +110,6 @@ def build_surfaces_test(force: bool = False) -> str:
 
 
 if __name__ == "__main__":
-    v = "checked" if "--checked" in sys.argv else "stamps" if "--stamps" in sys.argv else ""
+    v = "checked" if "--checked" in sys.argv else "stamps" if "--stamps" in sys.argv else \
+        "diag" if "--diag" in sys.argv else ""
     print(build(force="--force" in sys.argv, verbose=True, variant=v))

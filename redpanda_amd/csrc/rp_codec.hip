@@ -112,9 +112,6 @@ DEV uint4 shr1(const uint4& w) {
 
 // 16 bytes (the first len of them significant, 1..16) at output o
 DEV void put(const Dst& d, int64_t o, const uint4& v, uint32_t len) {
-#ifdef RPGPU_EXP_NOCOPY
-    return;
-#endif
     if (o + 16 <= d.lim) {
         gst16(d.p + o, v);
         return;
@@ -126,9 +123,6 @@ DEV void put(const Dst& d, int64_t o, const uint4& v, uint32_t len) {
 
 // len stream bytes from ip to output o (64 bytes in flight per step)
 DEV void copy_in(const Src& s, int64_t ip, const Dst& d, int64_t o, int64_t len) {
-#ifdef RPGPU_EXP_NOCOPY
-    return;
-#endif
     int64_t c = 0;
     for (; c + 64 <= len && ip + c + 64 <= s.rl && o + c + 64 <= d.lim; c += 64) {
         const uint4 a = gld16(s.p + ip + c), b = gld16(s.p + ip + c + 16), e = gld16(s.p + ip + c + 32),
@@ -170,13 +164,6 @@ constexpr PatTab make_pat() {
 __constant__ PatTab kPat = make_pat();
 
 DEV void copy_match(const Dst& d, int64_t o, uint32_t off, int64_t ml) {
-#ifdef RPGPU_EXP_NOCOPY
-    return;
-#endif
-#ifdef RPGPU_EXP_NOMATCHLOAD
-    for (int64_t c = 0; c < ml; c += 16) put(d, o + c, make_uint4(off, 0, 0, 0), (uint32_t)(ml - c < 16 ? ml - c : 16));
-    return;
-#endif
     if (off >= 16) {
         const uint8_t* s = d.p + o - off;
         int64_t c = 0;
@@ -361,11 +348,7 @@ struct PState {
 // short lengths spans 3-4 bytes, so one load round trip serves several
 // one 16-byte load per window (a 32-byte window, two loads, measured slower:
 // C2 walk 16.4 vs 13.8 ms, more VGPRs and fewer resident waves)
-#ifdef RPGPU_WIN32
-constexpr int32_t kWinSpan = 32;
-#else
 constexpr int32_t kWinSpan = 16;
-#endif
 struct Win {
     uint4 w, x;  // bytes [wb, wb + 16), [wb + 16, wb + 32)
     int32_t wb;
@@ -1616,11 +1599,6 @@ struct SlabSink {
     uint32_t cut;      // the pool ran out: the walk was suspended for good
     uint4 r0, r1, r2;  // records (pos & ~3) .. pos - 1, not stored yet
     DEV bool seq(const uint4&, int32_t, int32_t lip, int32_t llen, int32_t, uint32_t off, int32_t ml) {
-#ifdef RPGPU_EXP_NOREC
-        // diagnostic: the walk without its record stores (nothing to execute)
-        n++;
-        return true;
-#endif
         const uint4 r = make_uint4((uint32_t)lip, (uint32_t)llen, (uint32_t)ml, off);
         const uint32_t k = pos & 3;
         if (k == 3) {
@@ -1650,10 +1628,6 @@ struct SlabSink {
     }
     // store the records still held (when the walk returns)
     DEV void finish() {
-#ifdef RPGPU_EXP_NOREC
-        n = 0;
-        return;
-#endif
         const uint32_t k = pos & 3;
         uint4* q = (uint4*)(pool + (size_t)slab * kSlabRecs + (pos - k));
         if (k > 0) q[0] = r0;

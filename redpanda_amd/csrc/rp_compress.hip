@@ -33,7 +33,8 @@ namespace {
 
 typedef __attribute__((address_space(3))) uint16_t lds_u16;
 
-// 4 bytes at s + i (s 4-byte aligned; reads up to 7 bytes past i)
+// 4 bytes at s + i (s = a block of a fragment staged 16-byte aligned; reads
+// up to 7 bytes past i)
 DEV uint32_t g32(const uint8_t* __restrict__ s, uint32_t i) {
     const uint32_t* w = (const uint32_t*)(s + (i & ~3u));
     return __builtin_amdgcn_alignbyte(w[1], w[0], i & 3);

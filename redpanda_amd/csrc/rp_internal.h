@@ -205,7 +205,7 @@ constexpr uint32_t kCompSlot = 76800;
 constexpr uint64_t kSplitMin = 256u << 10;
 constexpr uint32_t kSplitParts = 16;
 struct CompBlock {
-    uint64_t src;                    // staged input offset (4-byte aligned, 8 readable bytes past the block)
+    uint64_t src;                    // staged input offset (a fragment starts 16-byte aligned; 8 readable bytes past it)
     uint32_t n, codec;               // block bytes (<= 65536), RPGPU_CODEC_LZ4 / _SNAPPY
     uint32_t frag_len, frag_blocks;  // snappy: on a fragment's first block, the fragment's bytes and blocks
 };

@@ -82,12 +82,11 @@ struct ScanWin {
     uint32_t w[20];
 };
 
-#ifndef RPGPU_SCAN_LOADS
 // one 16-byte load per lane; the next 64 bytes come from lanes l + 1 .. l + 4
 // (DPP wave_shl:1, four hops), lane 63 loading what lies past the step.
-// (Five overlapping loads per lane, RPGPU_SCAN_LOADS, or plain instead of
-// non-temporal loads: C2 discovery 14.4 / 14.0 ms against 13.5 ms here; the
-// scan is bound by the per-position field checks, not by its loads.)
+// (Five overlapping loads per lane, or plain instead of non-temporal loads:
+// C2 discovery 14.4 / 14.0 ms against 13.5 ms here; the scan is bound by the
+// per-position field checks, not by its loads.)
 DEV u32x4 scan_ld(const uint8_t* __restrict__ data, uint64_t data_len, uint64_t x) {
     u32x4 v = {0, 0, 0, 0};
     if (x + 16 <= data_len) v = __builtin_nontemporal_load((const u32x4*)(data + x));
@@ -111,18 +110,6 @@ DEV void scan_load(const uint8_t* __restrict__ data, uint64_t data_len, uint64_t
                                                                    0xF, 0xF, false);
     }
 }
-#else
-DEV void scan_load(const uint8_t* __restrict__ data, uint64_t data_len, uint64_t a, ScanWin& sw) {
-    const uint64_t la = a + 16ull * lane();
-#pragma unroll
-    for (int k = 0; k < 5; k++) {
-        const uint64_t x = la + 16ull * k;
-        u32x4 v = {0, 0, 0, 0};
-        if (x + 16 <= data_len) v = __builtin_nontemporal_load((const u32x4*)(data + x));
-        sw.w[4 * k] = v.x; sw.w[4 * k + 1] = v.y; sw.w[4 * k + 2] = v.z; sw.w[4 * k + 3] = v.w;
-    }
-}
-#endif
 
 // Plausible header fields (disk or wire) given the 61 header bytes through
 // W32(o) / B(o); `rem` = bytes from the header to the segment end.  The
@@ -189,10 +176,34 @@ DEV uint32_t scan_step(uint32_t layout, const uint8_t* __restrict__ seg, const S
     return m;
 }
 
+// Scan budget: a chunk is scanned for its first header over at most its
+// first kScanBudget bytes.  A chunk that lies inside a large batch holds no
+// header start at all and was scanned to its end (C2: 1 MiB batches over
+// 256 KiB chunks, discovery 13.5 ms of a 56 ms step); with the budget such a
+// chunk is marked kExhausted instead, and k_chain carries the chain of the
+// nearest earlier chunk with an entry through it (storage/parser.cc:139-176
+// semantics are unchanged: k_resolve verifies every chunk's entry against
+// the true chain and re-walks any it cannot confirm).
+// A chunk then holds a header start within its first kScanBudget bytes about
+// kScanBudget / (mean batch bytes) of the time: C2's ~420 KB batches leave
+// runs of tens of spent chunks between two entries (up to ~150 at 16 KiB),
+// each carried by one k_chain lane at ~0.6 header hops per chunk.  (32 KiB:
+// C2 discover 3.0 ms, a 32-chunk carry limit made k_resolve re-walk the
+// rest of the longer runs serially, 0.86 ms.)
+constexpr uint64_t kScanBudget = 16u << 10;
+constexpr uint64_t kExhausted = kNone - 1;
+// chunks one k_chain lane carries its chain through: unbounded in practice
+// (a run is as long as the gap between two entries); the serial cost is the
+// headers in the run, which k_resolve would otherwise re-walk serially
+constexpr uint32_t kMaxCarry = 1u << 30;
+
 // One wave per chunk, four chunks per workgroup.  (Four waves per chunk,
 // scanning interleaved steps, cut C2's discovery from 14.4 to 9.9 ms but
 // cost C1 0.2 ms of its 5 ms step: most C1 chunks find their entry within
 // a few steps, and four waves then scan four times the bytes.)
+// Output: the default (no entry) ChunkRec, and the discovered entry in
+// chunk_entry[g] (a position, kNone: scanned to the chunk end without a
+// header, kExhausted: budget spent); k_resolve overwrites chunk_entry later.
 __global__ __launch_bounds__(256) void k_discover(DeviceJob j) {
     const uint64_t g = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
     if (g >= j.total_chunks) return;
@@ -236,14 +247,16 @@ __global__ __launch_bounds__(256) void k_discover(DeviceJob j) {
             }
         }
     }
+    bool exhausted = false;
     if (scan) {
         // candidates in ascending order: lanes cover consecutive 16-byte
         // spans, bits ascend within a lane
         uint64_t a = (off + cs) & ~15ull;
+        const uint64_t se = (cs + kScanBudget < ce) ? cs + kScanBudget : ce;
         ScanWin cur, nxt;
         scan_load(j.data, j.data_len, a, cur);
-        for (; a < off + ce && entry == kNone; a += 1024) {
-            if (a + 1024 < off + ce) scan_load(j.data, j.data_len, a + 1024, nxt);
+        for (; a < off + se && entry == kNone; a += 1024) {
+            if (a + 1024 < off + se) scan_load(j.data, j.data_len, a + 1024, nxt);
             const uint32_t m = scan_step(j.layout, seg, cur, a, off, len, cs, ce);
             uint64_t lanes = __ballot(m != 0);
             while (lanes && entry == kNone) {
@@ -260,15 +273,17 @@ __global__ __launch_bounds__(256) void k_discover(DeviceJob j) {
             }
             cur = nxt;
         }
+        exhausted = entry == kNone && se < ce;
     }
     if (lane() == 0) {
         ChunkRec r;
-        r.entry = entry;
+        r.entry = kNone;
         r.exit = kNone;
         r.count = 0;
         r.term = -1;
         r.tpos = 0;
         j.chunks[g] = r;
+        j.chunk_entry[g] = entry != kNone ? entry : exhausted ? kExhausted : kNone;
     }
 }
 
@@ -299,26 +314,45 @@ DEV WalkOut lane_walk(uint32_t layout, const uint8_t* __restrict__ seg, uint64_t
 // Speculative chain of every chunk from the entry k_discover found, one chunk
 // per LANE: a chunk's headers are a dependent chain, so 64 chains per wave
 // keep 64 header reads in flight where a wave-cooperative walk had one.
+// The chain then runs on through the following chunks whose scan budget
+// was spent (kExhausted, up to kMaxCarry of them), recording each one's
+// speculative entry / exit / count as a scan would have: such a chunk is
+// written by this lane only (runs of kExhausted chunks after an entry are
+// disjoint), and chunk_entry is read-only here.
 __global__ __launch_bounds__(256) void k_chain(DeviceJob j) {
     extern __shared__ uint32_t th[];
     init_lds_hdr(th, j.tables);
     const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (g >= j.total_chunks) return;
-    const uint64_t entry = j.chunks[g].entry;
-    if (entry == kNone) return;
+    const uint64_t entry = j.chunk_entry[g];
+    if (entry >= kExhausted) return;
     const uint32_t s = find_segment(j.chunk_base, j.n_segments, g);
     const uint64_t w = g - j.chunk_base[s];
+    const uint64_t W = j.chunk_base[s + 1] - j.chunk_base[s];
     const uint64_t off = j.seg_off[s], len = j.seg_off[s + 1] - off;
-    const uint64_t cs = w * j.chunk_bytes;
-    const uint64_t ce = (cs + j.chunk_bytes < len) ? cs + j.chunk_bytes : len;
-    const WalkOut o = lane_walk(j.layout, j.data + off, len, entry, ce, th, j.tables->c57);
-    ChunkRec r;
-    r.entry = entry;
-    r.exit = o.exit;
-    r.count = o.count;
-    r.term = o.term;
-    r.tpos = o.tpos;
-    j.chunks[g] = r;
+    uint64_t p = entry;
+    for (uint32_t k = 0;; k++) {
+        const uint64_t cs = (w + k) * j.chunk_bytes;
+        const uint64_t ce = (cs + j.chunk_bytes < len) ? cs + j.chunk_bytes : len;
+        ChunkRec r;
+        r.entry = kNone;
+        r.exit = kNone;
+        r.count = 0;
+        r.term = -1;
+        r.tpos = 0;
+        if (p < ce) {
+            // p >= cs: the first chain position at or after the chunk start
+            const WalkOut o = lane_walk(j.layout, j.data + off, len, p, ce, th, j.tables->c57);
+            r.entry = p;
+            r.exit = o.exit;
+            r.count = o.count;
+            r.term = o.term;
+            r.tpos = o.tpos;
+            p = o.exit;
+        }
+        j.chunks[g + k] = r;
+        if (r.term >= 0 || k + 1 >= kMaxCarry || w + k + 1 >= W || j.chunk_entry[g + k + 1] != kExhausted) break;
+    }
 }
 
 // ---------------------------------------------------------------------------

@@ -127,6 +127,13 @@ struct rpgpu_ctx {
     void* pool = nullptr;
     size_t pool_bytes = 0;
     std::string err;
+    // Context scratch (ws, pool, seqs, sws, iws) is shared by every job on
+    // the context, whichever stream it is launched on: each async entry
+    // point makes its stream wait for the previous job's last event (a
+    // device-side wait, no host sync) and records its own at the end, and a
+    // scratch buffer is only freed for growth once that event completed.
+    hipEvent_t ws_ev = nullptr;
+    bool ws_live = false;
     // rpgpu_validate_host: a copy stream and two staging slots (segment
     // bytes in, per-batch results out), used alternately so the H2D copy of
     // group g + 1 runs while group g validates
@@ -170,7 +177,34 @@ int fail(rpgpu_ctx* c, int code, const char* what, hipError_t e = hipSuccess) {
         if (_e != hipSuccess) return fail((ctx), RPGPU_E_HIP, #call, _e);   \
     } while (0)
 
+// ordering of jobs that share the context scratch (see rpgpu_ctx::ws_ev)
+int ws_acquire(rpgpu_ctx* c, hipStream_t s) {
+    if (c->ws_live) HIPCHK(c, hipStreamWaitEvent(s, c->ws_ev, 0));
+    return RPGPU_OK;
+}
+int ws_release(rpgpu_ctx* c, hipStream_t s) {
+    if (!c->ws_ev) HIPCHK(c, hipEventCreateWithFlags(&c->ws_ev, hipEventDisableTiming));
+    HIPCHK(c, hipEventRecord(c->ws_ev, s));
+    c->ws_live = true;
+    return RPGPU_OK;
+}
+// before freeing scratch for growth: the previous job (any stream) is done
+int ws_drain(rpgpu_ctx* c, hipStream_t s) {
+    if (c->ws_live) HIPCHK(c, hipEventSynchronize(c->ws_ev));
+    HIPCHK(c, hipStreamSynchronize(s));
+    return RPGPU_OK;
+}
+
 size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
+
+// Environment overrides exist in the diagnostic build only
+// (librpgpu_diag.so, -DRPGPU_DIAG, loaded with RPGPU_VARIANT=diag): the
+// product library reads no environment.
+#ifdef RPGPU_DIAG
+const char* diag_env(const char* name) { return getenv(name); }
+#else
+const char* diag_env(const char*) { return nullptr; }
+#endif
 
 // gzip / zstd: the CPU fallback behind compressor::uncompress (rp_hostcodec.cpp)
 int host_codec(rpgpu_ctx* c, int codec, const void* in, size_t n, void* out, size_t cap, size_t* out_len) {
@@ -218,6 +252,7 @@ int rpgpu_destroy(rpgpu_ctx* c) {
     if (!c) return RPGPU_E_INVALID;
     hipSetDevice(c->device);
     if (c->stream) hipStreamSynchronize(c->stream);
+    if (c->ws_live) (void)hipEventSynchronize(c->ws_ev);
     if (c->ws) hipFree(c->ws);
     if (c->uws) hipFree(c->uws);
     if (c->iws) hipFree(c->iws);
@@ -229,6 +264,7 @@ int rpgpu_destroy(rpgpu_ctx* c) {
     if (c->pool) hipFree(c->pool);
     if (c->pin) hipHostFree(c->pin);
     if (c->d_tables) hipFree(c->d_tables);
+    if (c->ws_ev) { (void)hipEventSynchronize(c->ws_ev); (void)hipEventDestroy(c->ws_ev); }
     for (auto& set : c->ev_sets)
         for (auto& e : set) hipEventDestroy(e);
     if (c->stream) hipStreamDestroy(c->stream);
@@ -321,13 +357,12 @@ int rpgpu_last_timings(rpgpu_ctx* c, float* ms, int n) {
     for (size_t i = 0; i < c->ev_used; i++) {
         auto& e = c->ev_sets[i];
         HIPCHK(c, hipEventSynchronize(e[6]));
-        float t;
-        hipEventElapsedTime(&t, e[0], e[6]); acc[0] += t;
-        hipEventElapsedTime(&t, e[0], e[1]); acc[1] += t;
-        hipEventElapsedTime(&t, e[1], e[2]); acc[2] += t;
-        hipEventElapsedTime(&t, e[3], e[4]); acc[3] += t;
-        hipEventElapsedTime(&t, e[2], e[3]); acc[4] += t;
-        hipEventElapsedTime(&t, e[4], e[5]); acc[5] += t;
+        const int pairs[6][2] = {{0, 6}, {0, 1}, {1, 2}, {3, 4}, {2, 3}, {4, 5}};
+        for (int k = 0; k < 6; k++) {
+            float t = 0;
+            HIPCHK(c, hipEventElapsedTime(&t, e[pairs[k][0]], e[pairs[k][1]]));
+            acc[k] += t;
+        }
     }
     for (int i = 0; i < n && i < 6; i++) ms[i] = (float)(acc[i] / (double)c->ev_used);
     c->ev_used = 0;
@@ -357,7 +392,20 @@ int rpgpu_submit(rpgpu_ctx* c, const rpgpu_job* job, void* stream) { return subm
 }  // extern "C"
 
 namespace {
+int submit_body(rpgpu_ctx* c, const rpgpu_job* job, hipStream_t s, int stop, PlanPtrs* plan);
+
+// every job on a context is ordered after the previous one (rpgpu_ctx::ws_ev)
 int submit_impl(rpgpu_ctx* c, const rpgpu_job* job, void* stream, int stop, PlanPtrs* plan) {
+    if (!c) return RPGPU_E_INVALID;
+    hipSetDevice(c->device);
+    hipStream_t s = pick(c, stream);
+    if (int rc = ws_acquire(c, s)) return rc;
+    const int rc = submit_body(c, job, s, stop, plan);
+    const int rr = ws_release(c, s);
+    return rc ? rc : rr;
+}
+
+int submit_body(rpgpu_ctx* c, const rpgpu_job* job, hipStream_t s, int stop, PlanPtrs* plan) {
     if (!c || !job || !job->d_data || !job->d_seg_offsets || !job->h_seg_offsets || job->n_segments == 0 ||
         !job->d_batches || !job->d_summaries || !job->d_totals)
         return fail(c, RPGPU_E_INVALID, "rpgpu_submit: missing argument");
@@ -366,8 +414,6 @@ int submit_impl(rpgpu_ctx* c, const rpgpu_job* job, void* stream, int stop, Plan
         return fail(c, RPGPU_E_INVALID, "rpgpu_submit: unknown layout");
     if ((job->flags & RPGPU_JOB_PARSE) && !job->d_records && job->record_capacity)
         return fail(c, RPGPU_E_INVALID, "rpgpu_submit: PARSE needs d_records");
-    hipSetDevice(c->device);
-    hipStream_t s = pick(c, stream);
     const uint32_t nseg = job->n_segments;
     const uint32_t cs = job->chunk_bytes ? job->chunk_bytes : (256u << 10);
     // chunk table from the host offsets
@@ -403,8 +449,8 @@ int submit_impl(rpgpu_ctx* c, const rpgpu_job* job, void* stream, int stop, Plan
     const size_t o_pstate = take(bl_cap64 * sizeof(PieceState));
     const size_t o_longl = take(bl_cap64 * 4);
     uint64_t split_min = std::max<uint64_t>(kSplitMin, 2 * data_len / ((uint64_t)c->cu_count * kVWaves));
-    // RPGPU_SPLIT_MIN_KIB: diagnostic override (scripts/bench_skew.py A/B)
-    if (const char* e = getenv("RPGPU_SPLIT_MIN_KIB")) split_min = std::max<uint64_t>(strtoull(e, nullptr, 10) << 10, 64);
+    // RPGPU_SPLIT_MIN_KIB (diagnostic build): override (scripts/bench_skew.py A/B)
+    if (const char* e = diag_env("RPGPU_SPLIT_MIN_KIB")) split_min = std::max<uint64_t>(strtoull(e, nullptr, 10) << 10, 64);
     const uint64_t split_cap = std::min<uint64_t>(data_len / split_min + 1, bcap + 1);
     const size_t o_split = take(split_cap * 4);
     const size_t o_spart = take(split_cap * kSplitParts * 4);
@@ -425,12 +471,21 @@ int submit_impl(rpgpu_ctx* c, const rpgpu_job* job, void* stream, int stop, Plan
     const size_t slab_bytes = kSlabRecs * sizeof(SeqRec) + 4;
     const size_t pool_want = dec ? std::min<size_t>(std::max<size_t>(data_len / 2, 256ull << 20), 8ull << 30) : 0;
     if (pool_want > c->pool_bytes) {
-        if (c->pool) { hipStreamSynchronize(s); hipFree(c->pool); c->pool = nullptr; c->pool_bytes = 0; }
+        if (c->pool) {
+            if (int rc = ws_drain(c, s)) return rc;
+            hipFree(c->pool);
+            c->pool = nullptr;
+            c->pool_bytes = 0;
+        }
         if (hipMalloc(&c->pool, pool_want) != hipSuccess) { c->pool = nullptr; return fail(c, RPGPU_E_NOMEM, "decode record pool"); }
         c->pool_bytes = pool_want;
     }
     if (need > c->ws_bytes) {
-        if (c->ws) { hipStreamSynchronize(s); hipFree(c->ws); c->ws = nullptr; }
+        if (c->ws) {
+            if (int rc = ws_drain(c, s)) return rc;
+            hipFree(c->ws);
+            c->ws = nullptr;
+        }
         if (hipMalloc(&c->ws, need) != hipSuccess) { c->ws_bytes = 0; return fail(c, RPGPU_E_NOMEM, "workspace"); }
         c->ws_bytes = need;
     }
@@ -475,9 +530,9 @@ int submit_impl(rpgpu_ctx* c, const rpgpu_job* job, void* stream, int stop, Plan
     j.exec_waves = c->exec_waves;
     j.pstate = (PieceState*)(ws + o_pstate);
     j.pool_slabs = (uint32_t)std::min<size_t>(c->pool_bytes / slab_bytes, 0xFFFFFFF0ull);
-    // RPGPU_POOL_SLABS: test override shrinking the record pool (exercises
+    // RPGPU_POOL_SLABS (diagnostic build): shrinks the record pool (exercises
     // k_lz_exec's own walk of the pieces the pool cuts short)
-    if (const char* e = getenv("RPGPU_POOL_SLABS")) j.pool_slabs = std::min<uint32_t>(j.pool_slabs, (uint32_t)atoi(e));
+    if (const char* e = diag_env("RPGPU_POOL_SLABS")) j.pool_slabs = std::min<uint32_t>(j.pool_slabs, (uint32_t)atoi(e));
     j.pool = (SeqRec*)c->pool;
     j.slab_next = (uint32_t*)((uint8_t*)c->pool + (size_t)j.pool_slabs * kSlabRecs * sizeof(SeqRec));
     j.seg_first_bad = (uint32_t*)(ws + o_fbad);
@@ -489,9 +544,9 @@ int submit_impl(rpgpu_ctx* c, const rpgpu_job* job, void* stream, int stop, Plan
     if (((uintptr_t)job->d_decoded & 15) != 0) return fail(c, RPGPU_E_INVALID, "rpgpu_submit: d_decoded must be 16-byte aligned");
     uint64_t* scan_tmp = (uint64_t*)(ws + o_scan);
 
-    // RPGPU_DEBUG_SYNC=1: synchronize after every stage and name the stage
-    // that failed (fault localisation; never set in measured runs)
-    static const bool dbg = [] { const char* e = getenv("RPGPU_DEBUG_SYNC"); return e && *e == '1'; }();
+    // RPGPU_DEBUG_SYNC=1 (diagnostic build): synchronize after every stage and
+    // name the stage that failed (fault localisation)
+    static const bool dbg = [] { const char* e = diag_env("RPGPU_DEBUG_SYNC"); return e && *e == '1'; }();
 #define STAGE(name, call)                                                                  \
     do {                                                                                   \
         HIPCHK(c, (call));                                                                 \
@@ -502,7 +557,9 @@ int submit_impl(rpgpu_ctx* c, const rpgpu_job* job, void* stream, int stop, Plan
             if (_e != hipSuccess) return fail(c, RPGPU_E_HIP, "stage " name " failed", _e); \
         }                                                                                  \
     } while (0)
-    const bool tm = c->timing;
+    // timed submits only: rpgpu_query_capacity's planning runs stop early
+    // and record no timings
+    const bool tm = c->timing && stop == kRunAll;
     hipEvent_t* ev = nullptr;
     if (tm) {
         if (c->ev_used == c->ev_sets.size()) {
@@ -543,8 +600,8 @@ int submit_impl(rpgpu_ctx* c, const rpgpu_job* job, void* stream, int stop, Plan
     if (tm) HIPCHK(c, hipEventRecord(ev[3], s));
     STAGE("validate", launch_validate(j, s, c->cu_count));
     if (tm) HIPCHK(c, hipEventRecord(ev[4], s));
-    // RPGPU_WALK_WGS: diagnostic override of k_walk's grid (workgroups per CU)
-    static const uint32_t walk_wgs = [] { const char* e = getenv("RPGPU_WALK_WGS"); return e ? (uint32_t)atoi(e) : 8u; }();
+    // RPGPU_WALK_WGS (diagnostic build): k_walk's grid (workgroups per CU)
+    static const uint32_t walk_wgs = [] { const char* e = diag_env("RPGPU_WALK_WGS"); return e ? (uint32_t)atoi(e) : 8u; }();
     STAGE("walk", launch_walk(j, s, c->cu_count * walk_wgs));
     if (tm) HIPCHK(c, hipEventRecord(ev[5], s));
     STAGE("finalize", launch_finalize(j, s));
@@ -572,7 +629,12 @@ int rpgpu_query_capacity(rpgpu_ctx* c, const rpgpu_job* job, void* stream, rpgpu
     const uint32_t nseg = job->n_segments;
     auto grow = [&](void** p, size_t* have, size_t want) -> int {
         if (want <= *have) return RPGPU_OK;
-        if (*p) { HIPCHK(c, hipStreamSynchronize(s)); HIPCHK(c, hipFree(*p)); *p = nullptr; *have = 0; }
+        if (*p) {
+            if (int rc = ws_drain(c, s)) return rc;
+            HIPCHK(c, hipFree(*p));
+            *p = nullptr;
+            *have = 0;
+        }
         if (hipMalloc(p, want) != hipSuccess) { *p = nullptr; return fail(c, RPGPU_E_NOMEM, "rpgpu_query_capacity: scratch"); }
         *have = want;
         return RPGPU_OK;
@@ -703,8 +765,8 @@ int rpgpu_segment_index(rpgpu_ctx* c, const rpgpu_batch_result* d_batches, uint6
     if (n_segments > 0x7FFFFFFFu) return fail(c, RPGPU_E_INVALID, "rpgpu_segment_index: too many segments");
     hipSetDevice(c->device);
     hipStream_t s = pick(c, stream);
-    // RPGPU_INDEX_SERIAL=1: the one-wave-per-segment walk (A/B reference)
-    static const bool serial = [] { const char* e = getenv("RPGPU_INDEX_SERIAL"); return e && e[0] == '1'; }();
+    // RPGPU_INDEX_SERIAL=1 (diagnostic build): the one-wave-per-segment walk (A/B reference)
+    static const bool serial = [] { const char* e = diag_env("RPGPU_INDEX_SERIAL"); return e && e[0] == '1'; }();
     if (serial) {
         HIPCHK(c, launch_segment_index(d_batches, batch_capacity, d_summaries, n_segments, step, d_states, d_rel_offset,
                                        d_rel_time, d_position, s));
@@ -713,7 +775,7 @@ int rpgpu_segment_index(rpgpu_ctx* c, const rpgpu_batch_result* d_batches, uint6
     const size_t need = segment_index_ws_bytes(n_segments, batch_capacity);
     if (need > c->iws_bytes) {
         if (c->iws) {
-            HIPCHK(c, hipDeviceSynchronize());  // the old tables may still be in use on any stream
+            if (int rc = ws_drain(c, s)) return rc;  // the old tables may still be in use on another stream
             HIPCHK(c, hipFree(c->iws));
             c->iws = nullptr;
             c->iws_bytes = 0;
@@ -721,9 +783,10 @@ int rpgpu_segment_index(rpgpu_ctx* c, const rpgpu_batch_result* d_batches, uint6
         HIPCHK(c, hipMalloc(&c->iws, need));
         c->iws_bytes = need;
     }
+    if (int rc = ws_acquire(c, s)) return rc;
     HIPCHK(c, launch_segment_index_pieces(d_batches, batch_capacity, d_summaries, n_segments, step, d_states,
                                           d_rel_offset, d_rel_time, d_position, c->iws, s));
-    return RPGPU_OK;
+    return ws_release(c, s);
 }
 
 int rpgpu_uncompress(rpgpu_ctx* c, int codec, const void* in, size_t n, void* out, size_t cap, size_t* out_len) {
@@ -777,10 +840,16 @@ int rpgpu_stamp(rpgpu_ctx* c, uint8_t* d_data, const uint64_t* d_pos, const uint
     const size_t o_steps = 0, o_scan = align_up((size_t)(n + 1) * 8, 256);
     const size_t o_cur = align_up(o_scan + scan_temp_bytes(n) + 64, 256), need = o_cur + 256;
     if (need > c->sws_bytes) {
-        if (c->sws) { HIPCHK(c, hipStreamSynchronize(s)); HIPCHK(c, hipFree(c->sws)); c->sws = nullptr; c->sws_bytes = 0; }
+        if (c->sws) {
+            if (int rc = ws_drain(c, s)) return rc;
+            HIPCHK(c, hipFree(c->sws));
+            c->sws = nullptr;
+            c->sws_bytes = 0;
+        }
         if (hipMalloc(&c->sws, need) != hipSuccess) { c->sws = nullptr; return fail(c, RPGPU_E_NOMEM, "rpgpu_stamp workspace"); }
         c->sws_bytes = need;
     }
+    if (int rc = ws_acquire(c, s)) return rc;
     uint8_t* w = (uint8_t*)c->sws;
     uint64_t* steps = (uint64_t*)(w + o_steps);
     uint32_t* cursor = (uint32_t*)(w + o_cur);
@@ -790,7 +859,7 @@ int rpgpu_stamp(rpgpu_ctx* c, uint8_t* d_data, const uint64_t* d_pos, const uint
         HIPCHK(c, scan_exclusive_u64(steps, n, w + o_scan, scan_temp_bytes(n) + 64, s));
     }
     HIPCHK(c, launch_stamp(d_data, d_pos, d_payload_len, steps, next_offset, n, flags, c->d_tables, cursor, c->cu_count, s));
-    return RPGPU_OK;
+    return ws_release(c, s);
 }
 
 // kafka::writer_serialize_batch over batches [first, first + n) of a
@@ -808,21 +877,27 @@ int rpgpu_serialize_wire(rpgpu_ctx* c, const uint8_t* d_data, const uint64_t* d_
     const size_t o_dst = align_up((size_t)(n + 1) * 8, 256), o_scan = o_dst + align_up((size_t)(n + 1) * 8, 256);
     const size_t need = o_scan + scan_temp_bytes(n) + 256;
     if (need > c->sws_bytes) {
-        if (c->sws) { HIPCHK(c, hipStreamSynchronize(s)); HIPCHK(c, hipFree(c->sws)); c->sws = nullptr; c->sws_bytes = 0; }
+        if (c->sws) {
+            if (int rc = ws_drain(c, s)) return rc;
+            HIPCHK(c, hipFree(c->sws));
+            c->sws = nullptr;
+            c->sws_bytes = 0;
+        }
         if (hipMalloc(&c->sws, need) != hipSuccess) { c->sws = nullptr; return fail(c, RPGPU_E_NOMEM, "rpgpu_serialize_wire workspace"); }
         c->sws_bytes = need;
     }
+    if (int rc = ws_acquire(c, s)) return rc;
     uint8_t* w = (uint8_t*)c->sws;
     uint64_t* src = (uint64_t*)w;
     uint64_t* dst = (uint64_t*)(w + o_dst);
     if (n == 0) {
         HIPCHK(c, hipMemsetAsync(d_total, 0, 8, s));
-        return RPGPU_OK;
+        return ws_release(c, s);
     }
     HIPCHK(c, launch_to_wire(d_data, d_wire, d_batches, d_seg_offsets, first, n, src, dst, w + o_scan,
                              scan_temp_bytes(n) + 64, c->cu_count * 8, s));
     HIPCHK(c, hipMemcpyAsync(d_total, dst + n, 8, hipMemcpyDeviceToDevice, s));
-    return RPGPU_OK;
+    return ws_release(c, s);
 }
 
 // Many payloads per GPU round trip (the per-batch call sites of
@@ -922,7 +997,11 @@ int rpgpu_compress_batch(rpgpu_ctx* c, uint32_t n, const int* codecs, const void
     std::vector<uint32_t> dev;
     std::vector<CompPayload> pays;
     std::vector<CompBlock> blocks;
-    std::vector<uint64_t> src_off;
+    // staged input pieces: (host bytes, length, staged offset); every snappy
+    // fragment (each a RawCompress of its own) starts 16-byte aligned, as
+    // the block kernels' dword reads assume
+    struct Stage { const uint8_t* src; uint64_t n, off; };
+    std::vector<Stage> stage;
     uint64_t in_total = 0, out_total = 0;
     for (uint32_t i = 0; i < n; i++) {
         out_len[i] = 0;
@@ -939,16 +1018,26 @@ int rpgpu_compress_batch(rpgpu_ctx* c, uint32_t n, const int* codecs, const void
                                                   : RPGPU_E_CODEC;
             continue;
         }
-        if (!c || in_len[i] > (1ull << 32)) { status[i] = RPGPU_E_INVALID; continue; }
+        // 32-bit frame fields (CompBlock::frag_len, the snappy length varint
+        // and BE32 chunk length) hold lengths below 4 GiB only
+        if (!c || in_len[i] >= (1ull << 32)) { status[i] = RPGPU_E_INVALID; continue; }
         const uint64_t len = in_len[i];
+        uint64_t fr = (codec == RPGPU_CODEC_SNAPPY && frag && frag[i]) ? frag[i] : len;
+        if (fr == 0) fr = 1;
+        // snappy_java_compressor::compress writes int32_t(omax) per fragment
+        // (compression/internal/snappy_java_compressor.cc:58-75): a fragment
+        // whose bound does not fit int32 cannot be framed
+        if (codec == RPGPU_CODEC_SNAPPY && 32 + std::min<uint64_t>(fr, len) + std::min<uint64_t>(fr, len) / 6 > 0x7FFFFFFFull) {
+            status[i] = RPGPU_E_INVALID;
+            continue;
+        }
         CompPayload p;
         p.n = len;
         p.out = out_total;
         p.first = (uint32_t)blocks.size();
         p.codec = (uint32_t)codec;
         p.pad = 0;
-        uint64_t fr = (codec == RPGPU_CODEC_SNAPPY && frag && frag[i]) ? frag[i] : len;
-        if (fr == 0) fr = 1;
+        const uint8_t* src = (const uint8_t*)in[i];
         for (uint64_t f = 0; f < len; f += (codec == RPGPU_CODEC_LZ4 ? len : fr)) {
             // lz4: the frame's 64 KiB blocks whatever the fragmentation;
             // snappy: each fragment is a RawCompress of its own
@@ -956,19 +1045,19 @@ int rpgpu_compress_batch(rpgpu_ctx* c, uint32_t n, const int* codecs, const void
             const uint32_t nbk = (uint32_t)((flen + 65535) / 65536);
             for (uint32_t k = 0; k < nbk; k++) {
                 CompBlock b;
-                b.src = in_total + f + (uint64_t)k * 65536;
+                b.src = in_total + (uint64_t)k * 65536;
                 b.n = (uint32_t)std::min<uint64_t>(65536, flen - (uint64_t)k * 65536);
                 b.codec = (uint32_t)codec;
                 b.frag_len = k == 0 ? (uint32_t)flen : 0;
                 b.frag_blocks = k == 0 ? nbk : 0;
                 blocks.push_back(b);
             }
+            stage.push_back({src + f, flen, in_total});
+            in_total += align_up(flen + 8, 16);
         }
         p.nblocks = (uint32_t)blocks.size() - p.first;
         pays.push_back(p);
         dev.push_back(i);
-        src_off.push_back(in_total);
-        in_total += align_up(len + 8, 16);
         out_total += align_up(rpgpu_compress_bound(codec, len, fr), 16);
         status[i] = RPGPU_E_CODEC;
     }
@@ -995,8 +1084,8 @@ int rpgpu_compress_batch(rpgpu_ctx* c, uint32_t n, const int* codecs, const void
     uint8_t* h = (uint8_t*)c->bh;
     uint8_t* d = (uint8_t*)c->bd;
     std::memset(h, 0, o_blk);
-    for (uint32_t k = 0; k < np; k++)
-        if (pays[k].n) std::memcpy(h + src_off[k], in[dev[k]], pays[k].n);
+    for (const Stage& st : stage)
+        if (st.n) std::memcpy(h + st.off, st.src, st.n);
     std::memcpy(h + o_blk, blocks.data(), nb * sizeof(CompBlock));
     std::memcpy(h + o_pay, pays.data(), np * sizeof(CompPayload));
     HIPCHK(c, hipMemcpyAsync(d, h, o_len, hipMemcpyHostToDevice, s));
@@ -1034,12 +1123,10 @@ int rpgpu_compress_batch(rpgpu_ctx* c, uint32_t n, const int* codecs, const void
 namespace {
 constexpr uint64_t kHostGroupBytes = 256ull << 20;
 
-// RPGPU_HOST_GROUP_KIB: staging-group size override (tests use small groups
-// to exercise the double buffering on small inputs)
-uint64_t host_group_bytes() {
-    const char* e = getenv("RPGPU_HOST_GROUP_KIB");
-    const uint64_t kib = e ? strtoull(e, nullptr, 10) : 0;
-    return kib ? kib << 10 : kHostGroupBytes;
+// staging-group size: rpgpu_host_job.group_kib, 0 = kHostGroupBytes (tests
+// use small groups to exercise the double buffering on small inputs)
+uint64_t host_group_bytes(const rpgpu_host_job* job) {
+    return job->group_kib ? (uint64_t)job->group_kib << 10 : kHostGroupBytes;
 }
 
 template <class T>
@@ -1125,7 +1212,7 @@ int rpgpu_validate_host(rpgpu_ctx* c, const rpgpu_host_job* job) {
         if (!h.d_tot) HIPCHK(c, hipMalloc((void**)&h.d_tot, sizeof(rpgpu_job_totals)));
     }
     std::vector<HostGroup> groups;
-    const uint64_t gbytes = host_group_bytes();
+    const uint64_t gbytes = host_group_bytes(job);
     for (uint32_t i = 0; i < job->n_segments; i++) {
         const uint64_t sz = job->seg_sizes[i];
         if (!job->segments[i] && sz) return fail(c, RPGPU_E_INVALID, "rpgpu_validate_host: null segment");

@@ -392,7 +392,7 @@ class Engine:
         return out.to_host()
 
     def validate_host(self, segments, flags: int = abi.JOB_CRC | abi.JOB_PARSE, layout: int = abi.LAYOUT_DISK,
-                      batch_capacity=None):
+                      batch_capacity=None, group_kib: int = 0):
         """rpgpu_validate_host: host-resident segments (numpy uint8 arrays,
         pinned or pageable) copied to the device in double-buffered groups
         and validated there.  Returns (batches, summaries, totals) as numpy
@@ -406,7 +406,7 @@ class Engine:
         batches = np.zeros(max(batch_capacity, 1), dtype=abi.BATCH_RESULT)
         sums = np.zeros(max(n, 1), dtype=abi.SEGMENT_SUMMARY)
         tot = np.zeros(1, dtype=abi.JOB_TOTALS)
-        job = HostJobC(C.cast(ptrs, C.c_void_p), C.cast(sizes, C.c_void_p), n, layout, flags, 0,
+        job = HostJobC(C.cast(ptrs, C.c_void_p), C.cast(sizes, C.c_void_p), n, layout, flags, group_kib,
                        batches.ctypes.data, batch_capacity, sums.ctypes.data, tot.ctypes.data)
         rc = self.L.rpgpu_validate_host(self.ctx, C.byref(job))
         check(rc, self.ctx, "rpgpu_validate_host")
@@ -448,6 +448,6 @@ class Pending:
 class HostJobC(C.Structure):
     """rpgpu_host_job (include/rpgpu.h)."""
     _fields_ = [("segments", C.c_void_p), ("seg_sizes", C.c_void_p), ("n_segments", C.c_uint32),
-                ("layout", C.c_uint32), ("flags", C.c_uint32), ("reserved", C.c_uint32),
+                ("layout", C.c_uint32), ("flags", C.c_uint32), ("group_kib", C.c_uint32),
                 ("batches", C.c_void_p), ("batch_capacity", C.c_uint64), ("summaries", C.c_void_p),
                 ("totals", C.c_void_p)]

@@ -95,6 +95,59 @@ def gather_job_verdicts(summaries, bitmap, n_batches: int, parts: Sequence[int],
     return {"summaries": out, "bitmaps": bits}
 
 
+def gather_records(batches, records, summaries, parts: Sequence[int], rank: int, world: int, dist):
+    """Gather each rank's per-batch results (rpgpu_batch_result[n_batches] as
+    bytes) and per-record offset index (rpgpu_record_index[n_records] as
+    bytes) to rank 0, and lay them out as ONE job over every partition in
+    global partition order would have (the offset index at
+    rank 0; what storage/log_replayer.cc:62-79 and the index rebuild need).
+
+    On rank 0 the result is what a single-process job over all partitions
+    (segment s = partition s) returns: batch `segment` = the partition id,
+    batch ordinals and `index_base` continue across partitions, record
+    `batch` = the global batch ordinal.  `decoded_off` stays rank-local (the
+    decoded arena is not gathered).  None on other ranks."""
+    import torch
+    from . import abi
+    meta = torch.tensor(list(parts), dtype=torch.int64, device=batches.device)
+    got = [gather_bytes(as_bytes(t), rank, world, dist) for t in (meta, summaries[: len(parts) * abi.SEGMENT_SUMMARY.itemsize],
+                                                               batches, records)]
+    if rank != 0:
+        return None
+    per_part = {}
+    for r in range(world):
+        rp = got[0][r].cpu().numpy().view(np.int64)
+        rs = got[1][r].cpu().numpy().view(abi.SEGMENT_SUMMARY)
+        rb = got[2][r].cpu().numpy().view(abi.BATCH_RESULT)
+        rr = got[3][r].cpu().numpy().view(abi.RECORD_INDEX)
+        if len(rs) != len(rp):
+            raise RuntimeError(f"rank {r}: {len(rs)} summaries for {len(rp)} partitions")
+        rec0 = 0
+        for p, s in zip(rp, rs):
+            b0, nb, nrec = int(s["first_batch"]), int(s["n_batches"]), int(s["n_records"])
+            if b0 + nb > len(rb) or rec0 + nrec > len(rr):
+                raise RuntimeError(f"rank {r} partition {p}: results shorter than its summary")
+            per_part[int(p)] = (rb[b0:b0 + nb], rr[rec0:rec0 + nrec], b0, rec0)
+            rec0 += nrec
+    bs, rs_ = [], []
+    gb = gr = 0
+    for p in sorted(per_part):
+        b, rec, b0, r0 = per_part[p]
+        b = b.copy()
+        rec = rec.copy()
+        b["segment"] = p
+        # index_base: the record slot of the batch's first index entry
+        b["index_base"] = b["index_base"] - np.uint64(r0) + np.uint64(gr)
+        rec["batch"] = (rec["batch"].astype(np.int64) - b0 + gb).astype(np.uint32)
+        bs.append(b)
+        rs_.append(rec)
+        gb += len(b)
+        gr += len(rec)
+    return {"batches": np.concatenate(bs) if bs else np.zeros(0, abi.BATCH_RESULT),
+            "records": np.concatenate(rs_) if rs_ else np.zeros(0, abi.RECORD_INDEX),
+            "partitions": sorted(per_part)}
+
+
 def gather_segment_index(states, rel_off, rel_time, pos, parts: Sequence[int], rank: int, world: int, dist):
     """Gather each rank's rebuilt segment indexes (the outputs of
     Engine.segment_index: rpgpu_index_state[len(parts)] as bytes plus the three

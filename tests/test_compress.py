@@ -92,7 +92,9 @@ def test_gpu_compress_matches_oracle(engine, corpus):
     codecs, pays, frags = [], [], []
     for name, data in corpus:
         for codec in (3, 2):
-            for frag in ((0, 1000, 100_000) if codec == 2 else (0,)):
+            # odd fragment sizes (1001, 4097) put fragment starts at every
+            # byte alignment of the caller's buffer
+            for frag in ((0, 1000, 1001, 4097, 100_000) if codec == 2 else (0,)):
                 codecs.append(codec)
                 pays.append(data)
                 frags.append(frag)

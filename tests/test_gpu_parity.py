@@ -177,6 +177,33 @@ def test_prefilter_misses_at_scale(engine, oracle, rplib, chunk):
     assert_same(got, ref)
 
 
+@pytest.mark.parametrize("chunk", [32 << 10, 64 << 10, 256 << 10])
+def test_spent_scan_budget_carry(engine, oracle, rplib, chunk):
+    """Large batches (20 KiB..600 KiB) over chunks larger than the discovery
+    scan budget: most chunks spend it without a header and are carried by
+    the chain of the nearest earlier chunk with an entry, through chunks the
+    chain jumps over, through prefilter-miss headers, and up to a header
+    corruption or a zeroed header that ends the chain inside a carried run."""
+    segs = [gen(rplib, 6 << 20, i, seed=0x5B + i, batch_bytes=0, min_batch=20 << 10, max_batch=600 << 10)
+            for i in range(4)]
+    edits = [dict(btype=0), dict(base=-7), dict(record_count=-1)]
+    for k, seg in enumerate(segs):
+        r = oracle.run_job(seg, [0, seg.size], FLAGS)
+        pos = [int(p) for p in r.batches["file_pos"]]
+        for i, p in enumerate(pos):
+            if i % 4 == 1:
+                restamp(seg, p, **edits[i % len(edits)])
+        if k == 2:
+            seg[pos[len(pos) // 2] + 30] ^= 0x10  # header_crc mismatch mid-segment
+        if k == 3:
+            seg[pos[2 * len(pos) // 3]:pos[2 * len(pos) // 3] + 61] = 0  # a zeroed header
+    got, ref = run_both(engine, oracle, segs, chunk=chunk)
+    assert len(ref.batches) > 40
+    assert set(int(x) for x in ref.summaries["terminal_errc"]) >= {abi.ERRC_HEADER_ONLY_CRC_MISSMATCH,
+                                                                   abi.ERRC_FALLOCATED_FILE_READ_ZERO_BYTES_FOR_HEADER}
+    assert_same(got, ref)
+
+
 def test_golden_segments(engine, oracle):
     man = json.load(open(os.path.join(G, "manifest.json")))
     segs = [np.frombuffer(open(os.path.join(G, "segments", e["name"] + ".bin"), "rb").read(), dtype=np.uint8)
@@ -305,14 +332,12 @@ def test_wire_layout_codec_mix(engine, oracle, rplib):
 
 @pytest.mark.parametrize("group_kib", [0, 1024, 3000])
 @pytest.mark.parametrize("recipe", ["mix", "c5"])
-def test_host_path(engine, oracle, rplib, group_kib, recipe, monkeypatch):
+def test_host_path(engine, oracle, rplib, group_kib, recipe):
     """rpgpu_validate_host (pinned/pageable host segments, double-buffered
     H2D groups): per-batch results and summaries equal the oracle's over the
     same segments.  Small staging groups exercise the slot alternation; the
     LZ4/snappy mix with DECODE makes groups overflow the first-try decode
     capacity and re-run."""
-    if group_kib:
-        monkeypatch.setenv("RPGPU_HOST_GROUP_KIB", str(group_kib))
     if recipe == "c5":
         segs = [gen(rplib, 3 << 20, i, **synth.C5) for i in range(4)]
     else:
@@ -321,7 +346,7 @@ def test_host_path(engine, oracle, rplib, group_kib, recipe, monkeypatch):
     segs.append(gen(rplib, 4 << 20, 9, seed=0xC1))
     offs = np.cumsum([0] + [s.size for s in segs]).astype(np.uint64)
     ref = oracle.run_job(np.concatenate(segs), offs, DFLAGS)
-    b, s, t = engine.validate_host(segs, DFLAGS)
+    b, s, t = engine.validate_host(segs, DFLAGS, group_kib=group_kib)
     assert len(b) == len(ref.batches)
     for f in abi.BATCH_COMPARE_FIELDS:
         if f in ("index_base", "decoded_off"):  # device-side arena positions, per staging group
@@ -373,6 +398,39 @@ def test_async_poll_wait_and_capacity_query(engine, oracle, rplib):
     assert p2.poll()
     p2.release()
     assert_same(out.to_host(), ref, flags)
+
+
+def test_async_then_submit_on_another_stream(engine, oracle, rplib):
+    """A job still running from rpgpu_submit_async (the context's stream)
+    and a second job submitted on torch's stream share the context scratch:
+    the second waits for the first on the device, and a bigger second job
+    (scratch growth) frees nothing the first still uses.  Both results ==
+    the oracle."""
+    import torch
+    MIX = (1 << abi.CODEC_NONE) | (1 << abi.CODEC_LZ4) | (1 << abi.CODEC_SNAPPY)
+    flags = abi.JOB_CRC | abi.JOB_PARSE | abi.JOB_DECODE
+    jobs = []
+    for k, (n, nseg) in enumerate(((2 << 20, 2), (6 << 20, 5))):
+        segs = [gen(rplib, n, i, seed=0xA5 + k, batch_bytes=0, min_batch=200, max_batch=300000, codec_mix=MIX,
+                    corrupt_payload_ppm=20000) for i in range(nseg)]
+        offs = np.cumsum([0] + [s.size for s in segs]).astype(np.uint64)
+        data = np.concatenate(segs)
+        ref = oracle.run_job(data, offs, flags)
+        d = torch.from_numpy(data).cuda()
+        out = engine.alloc_outputs(nseg, len(ref.batches) + 8, int(ref.totals["n_records"]) + 8,
+                                   int(ref.totals["decoded_bytes"]) + 4096)
+        jobs.append((d, offs, out, ref))
+    torch.cuda.synchronize()
+    (d0, o0, out0, ref0), (d1, o1, out1, ref1) = jobs
+    p = engine.submit_async(d0, o0, out0, flags)
+    s = torch.cuda.Stream()
+    with torch.cuda.stream(s):
+        engine.submit(d1, o1, out1, flags, stream=s)
+    s.synchronize()
+    p.wait()
+    p.release()
+    assert_same(out0.to_host(), ref0, flags)
+    assert_same(out1.to_host(), ref1, flags)
 
 
 def test_uncompress_batch_matches_single(engine, oracle):

@@ -144,3 +144,117 @@ def test_gloo_world2_index_gather_matches_single_process(rplib, oracle, tmp_path
         g = got[str(p)]
         assert g["n"] == int(s["n_entries"]) > 0 and g["max_offset"] == int(s["max_offset"])
         assert g["ro"] == ro.tolist() and g["ps"] == ps.tolist()
+
+
+# ---------------------------------------------------------------------------
+# The whole gather (verdicts, segment index, per-batch results and the
+# per-record offset index) over per-rank job outputs saved as host arrays:
+# by the oracle here, by the HIP engine on cuda:0 in the -m gpu test.  The
+# gloo workers never touch the GPU; rank 0 must hold exactly what ONE
+# single-process oracle job over every partition (global order) returns.
+# ---------------------------------------------------------------------------
+INDEX_STEP = 4096
+
+
+def _save_rank(path, res, ix, parts):
+    st = np.zeros(len(parts), dtype=abi.INDEX_STATE)
+    cap = max(len(res.batches), 1)
+    ro, rt, ps = np.zeros(cap, np.uint32), np.zeros(cap, np.uint32), np.zeros(cap, np.uint64)
+    for k, (s, a, b, c) in enumerate(ix):
+        st[k] = s
+        f, n = int(s["first_entry"]), int(s["n_entries"])
+        ro[f:f + n], rt[f:f + n], ps[f:f + n] = a, b, c
+    np.savez(path, batches=res.batches.view(np.uint8), records=res.records.view(np.uint8),
+             summaries=res.summaries.view(np.uint8), bitmap=res.bitmap.view(np.uint8), n_batches=len(res.batches),
+             parts=np.asarray(parts, np.int64), states=st.view(np.uint8), ro=ro, rt=rt, ps=ps)
+
+
+def _full_gather_worker(rank, world, port, in_dir, out_path):
+    import torch
+    import torch.distributed as dist
+    from redpanda_amd.shard import gather_job_verdicts, gather_records, gather_segment_index
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        z = np.load(os.path.join(in_dir, f"rank{rank}.npz"))
+        parts = [int(p) for p in z["parts"]]
+        t = lambda a: torch.from_numpy(np.ascontiguousarray(a))  # noqa: E731
+        v = gather_job_verdicts(t(z["summaries"]), t(z["bitmap"]), int(z["n_batches"]), parts, rank, world, dist)
+        ix = gather_segment_index(t(z["states"]), t(z["ro"].view(np.int32)), t(z["rt"].view(np.int32)),
+                                  t(z["ps"].view(np.int64)), parts, rank, world, dist)
+        rec = gather_records(t(z["batches"]), t(z["records"]), t(z["summaries"]), parts, rank, world, dist)
+        if rank == 0:
+            np.savez(out_path, summaries=v["summaries"].view(np.uint8),
+                     bits=np.concatenate([v["bitmaps"][k] for k in sorted(v["bitmaps"])]),
+                     batches=rec["batches"].view(np.uint8), records=rec["records"].view(np.uint8),
+                     ix_n=np.asarray([int(ix[p][0]["n_entries"]) for p in range(N_PARTS)]),
+                     ix_ro=np.concatenate([ix[p][1] for p in range(N_PARTS)]),
+                     ix_ps=np.concatenate([ix[p][3] for p in range(N_PARTS)]))
+        else:
+            assert v is None and ix is None and rec is None
+    finally:
+        dist.destroy_process_group()
+
+
+def _check_full_gather(out_path, oracle):
+    import torch.multiprocessing as mp  # noqa: F401
+    z = np.load(out_path)
+    ref = _oracle_job(_segments(list(range(N_PARTS))))
+    got_s = z["summaries"].view(abi.SEGMENT_SUMMARY)
+    for f in SUMMARY_FIELDS:
+        assert np.array_equal(got_s[f], ref.summaries[f]), f
+    gb = z["batches"].view(abi.BATCH_RESULT)
+    gr = z["records"].view(abi.RECORD_INDEX)
+    assert len(gb) == len(ref.batches) > 0 and len(gr) == len(ref.records) > 0
+    for f in abi.BATCH_COMPARE_FIELDS:
+        if f != "decoded_off":
+            assert np.array_equal(gb[f], ref.batches[f]), f"batches.{f}"
+    for f in abi.RECORD_COMPARE_FIELDS:
+        assert np.array_equal(gr[f], ref.records[f]), f"records.{f}"
+    # per-rank bitmaps, rank order = sorted parts tuples
+    assert not np.all(z["bits"] == 1), "corruption should clear some bits"
+    ixr = oracle.segment_index(ref.batches, ref.summaries, [0] * N_PARTS, step=INDEX_STEP)
+    assert z["ix_n"].tolist() == [int(s["n_entries"]) for s, _, _, _ in ixr]
+    assert np.array_equal(z["ix_ro"], np.concatenate([r[1] for r in ixr]))
+    assert np.array_equal(z["ix_ps"], np.concatenate([r[3] for r in ixr]))
+
+
+def test_gloo_world2_full_gather_oracle_outputs(rplib, oracle, tmp_path):
+    import torch.multiprocessing as mp
+    for r in range(2):
+        parts = partitions_for_rank(N_PARTS, 2, r)
+        res = _oracle_job(_segments(parts))
+        ix = oracle.segment_index(res.batches, res.summaries, [0] * len(parts), step=INDEX_STEP)
+        _save_rank(str(tmp_path / f"rank{r}.npz"), res, ix, parts)
+    out = str(tmp_path / "rank0_full.npz")
+    mp.spawn(_full_gather_worker, args=(2, _free_port(), str(tmp_path), out), nprocs=2, join=True)
+    _check_full_gather(out, oracle)
+
+
+@pytest.mark.gpu
+def test_gloo_world2_full_gather_gpu_outputs(rplib, oracle, tmp_path):
+    """Config C3 in miniature: the HIP engine validates each rank's
+    partitions on cuda:0 (records, summaries, bitmap, segment index), the
+    CPU-only gloo ranks gather those outputs to rank 0."""
+    import torch
+    import torch.multiprocessing as mp
+    from redpanda_amd.engine import Engine
+    eng = Engine(0)
+    for r in range(2):
+        parts = partitions_for_rank(N_PARTS, 2, r)
+        segs = _segments(parts)
+        offs = np.cumsum([0] + [s.size for s in segs]).astype(np.uint64)
+        data = torch.from_numpy(np.concatenate(segs)).cuda()
+        flags = abi.JOB_CRC | abi.JOB_PARSE
+        total = int(offs[-1])
+        out = eng.alloc_outputs(len(parts), total // abi.HEADER_SIZE + 16, total // 4, 1)
+        eng.submit(data, offs, out, flags)
+        torch.cuda.synchronize()
+        res = out.to_host()
+        ix = eng.index_to_host(*eng.segment_index(out, [0] * len(parts), step=INDEX_STEP), n_segments=len(parts))
+        _save_rank(str(tmp_path / f"rank{r}.npz"), res, ix, parts)
+    eng.close()
+    out = str(tmp_path / "rank0_full.npz")
+    mp.spawn(_full_gather_worker, args=(2, _free_port(), str(tmp_path), out), nprocs=2, join=True)
+    _check_full_gather(out, oracle)
