@@ -438,9 +438,13 @@ int rpgpu_compress_batch(rpgpu_ctx* ctx, uint32_t n, const int* codecs, const vo
                          const size_t* frag, void* const* out, const size_t* cap, size_t* out_len, int* status);
 
 /* ------------------------------------------------------------------------ */
-/* Host segment path: pinned, double-buffered H2D of host-resident segments  */
-/* (log_replayer over files).  Segments are copied in chunks on a copy       */
-/* stream while the previous chunk validates.  Outputs are HOST pointers.    */
+/* Host segment path (log_replayer over files, storage/log_replayer.cc:       */
+/* 95-114): pinned, double-buffered H2D of host-resident segments.  Segments */
+/* are copied in staging groups on a copy stream while the previous group    */
+/* validates, and each group's outputs come back while the next one runs.    */
+/* Outputs are HOST pointers and hold exactly what ONE rpgpu_submit over all */
+/* the segments returns: job-wide batch ordinals (record_index.batch),       */
+/* index_base, decoded_off and summary.first_batch.                          */
 /* ------------------------------------------------------------------------ */
 typedef struct rpgpu_host_job {
     const uint8_t* const* segments;  /* host pointers (pinned or pageable) */
@@ -455,9 +459,40 @@ typedef struct rpgpu_host_job {
     uint64_t batch_capacity;
     rpgpu_segment_summary* summaries; /* host, n_segments */
     rpgpu_job_totals* totals;        /* host */
+    /* optional (NULL / 0: not returned): the per-record index
+     * (RPGPU_JOB_PARSE) and the decoded arena (RPGPU_JOB_DECODE); a capacity
+     * that is too small sets totals.overflow bit 2 / 4, as on the device */
+    rpgpu_record_index* records;
+    uint64_t record_capacity;
+    uint8_t* decoded;
+    uint64_t decoded_capacity;
+    /* optional segment index rebuild (rpgpu_segment_index over each group's
+     * results, disk layout): index_step != 0 fills index_states[n_segments]
+     * (base_offset is an IN field) and the three entry arrays (batch_capacity
+     * entries each; segment s's entries at [first_entry, first_entry +
+     * n_entries), first_entry == its summary.first_batch) */
+    uint64_t index_step;
+    rpgpu_index_state* index_states;
+    uint32_t* rel_offset;
+    uint32_t* rel_time;
+    uint64_t* position;
 } rpgpu_host_job;
 
 int rpgpu_validate_host(rpgpu_ctx* ctx, const rpgpu_host_job* job);
+
+/* Decoded-size plan of one lz4 / snappy payload from its frame structure
+ * alone (the arena rule rpgpu_submit reserves per batch): an upper bound of
+ * what compressor::uncompress returns for a payload it accepts; 0 for an
+ * empty, unplannable or gzip / zstd payload (the caller then grows on
+ * RPGPU_E_OVERFLOW).  Host only, no context. */
+uint64_t rpgpu_uncompress_bound(int codec, const void* in, size_t n);
+
+/* rpgpu_stamp over a HOST buffer, in place (storage::stamp_batches): staged
+ * through the context's pinned and device scratch (grow-only), one H2D, the
+ * kernels, one D2H.  Synchronous.  d_pos / d_payload_len as rpgpu_stamp,
+ * but host arrays. */
+int rpgpu_stamp_host(rpgpu_ctx* ctx, uint8_t* buf, size_t len, const uint64_t* pos, const uint32_t* payload_len,
+                     uint32_t n, int64_t next_offset, uint32_t flags);
 
 #ifdef __cplusplus
 } /* extern "C" */

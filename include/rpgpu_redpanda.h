@@ -21,7 +21,8 @@
  * Differences forced by leaving Seastar: futures become synchronous calls,
  * ss::input_stream becomes a byte span of a whole segment, iobuf a
  * contiguous byte buffer.  The parser validates the whole segment on the GPU
- * in one rpgpu_submit, then replays the per-batch verdicts into the consumer
+ * through rpgpu_validate_host (pinned, double-buffered host -> device
+ * staging in the context), then replays the per-batch verdicts into the consumer
  * in chain order, so accept / skip / stop decisions and byte accounting
  * follow continuous_batch_parser::consume exactly.  No exception crosses the
  * C-ABI; these wrappers rethrow where the reference throws.
@@ -317,7 +318,12 @@ namespace compression {
 using type = model::compression;
 struct compressor {
     static rpgpu::iobuf uncompress(const rpgpu::iobuf& in, type t, rpgpu::engine& e = rpgpu::engine::local()) {
-        size_t cap = in.size_bytes() * 8 + 4096, got = 0;
+        // the frame's planned size (LZ4F block sizes / content size, snappy
+        // length varints), as the batch pipeline reserves it; gzip / zstd
+        // (no plan) start at 4x and grow on RPGPU_E_OVERFLOW to the size the
+        // decoder reports
+        const uint64_t plan = rpgpu_uncompress_bound((int)t, in.data(), in.size_bytes());
+        size_t cap = plan ? (size_t)plan : in.size_bytes() * 4 + 64, got = 0;
         for (;;) {
             std::vector<uint8_t> out(cap);
             const int rc = rpgpu_uncompress(e.ctx(), (int)t, in.data(), in.size_bytes(), out.data(), cap, &got);
@@ -325,8 +331,8 @@ struct compressor {
                 out.resize(got);
                 return rpgpu::iobuf(std::move(out));
             }
-            if (rc == RPGPU_E_OVERFLOW && got > cap) {
-                cap = got;
+            if (rc == RPGPU_E_OVERFLOW) {
+                cap = got > cap ? got : cap * 2;
                 continue;
             }
             if (rc == RPGPU_E_UNSUPPORTED) throw std::logic_error(rpgpu_last_error(e.ctx()));
@@ -408,15 +414,10 @@ inline int64_t stamp_batches(uint8_t* buf, size_t len, const std::vector<size_t>
         std::memcpy(&lod, buf + positions[i] + 23, 4);
         next = (int64_t)((uint64_t)next + (uint64_t)(int64_t)lod + 1u);
     }
-    rpgpu::dev_buffer d(e, len + 16), dp(e, n * 8), dl(e, n * 4);
-    e.check(rpgpu_memcpy_h2d(e.ctx(), d.get(), buf, len, nullptr), "rpgpu_memcpy_h2d");
-    e.check(rpgpu_memcpy_h2d(e.ctx(), dp.get(), pos.data(), n * 8, nullptr), "rpgpu_memcpy_h2d");
-    e.check(rpgpu_memcpy_h2d(e.ctx(), dl.get(), plen.data(), n * 4, nullptr), "rpgpu_memcpy_h2d");
-    e.check(rpgpu_stamp(e.ctx(), (uint8_t*)d.get(), (const uint64_t*)dp.get(), (const uint32_t*)dl.get(), (uint32_t)n,
-                        next_offset, flags, nullptr),
-            "rpgpu_stamp");
-    e.check(rpgpu_memcpy_d2h(e.ctx(), buf, d.get(), len, nullptr), "rpgpu_memcpy_d2h");
-    e.check(rpgpu_sync(e.ctx(), nullptr), "rpgpu_sync");
+    // through the context's grow-only pinned + device staging: one H2D, the
+    // kernels, one D2H
+    e.check(rpgpu_stamp_host(e.ctx(), buf, len, pos.data(), plen.data(), (uint32_t)n, next_offset, flags),
+            "rpgpu_stamp_host");
     return (flags & RPGPU_STAMP_OFFSETS) ? next : next_offset;
 }
 
@@ -478,67 +479,50 @@ struct index_request {
 inline segment_scan scan_segment(rpgpu::engine& e, const uint8_t* seg, size_t len,
                                  uint32_t layout = RPGPU_LAYOUT_DISK, uint32_t flags = RPGPU_JOB_CRC,
                                  const index_request* want_index = nullptr) {
+    // rpgpu_validate_host: the context's pinned, double-buffered staging
+    // (256 MiB groups copied while the previous group validates), no
+    // per-call device allocation.  The result arrays are sized for the
+    // worst case (a batch per 61 bytes) but left uninitialised, so only the
+    // entries the job writes are touched.
     segment_scan out;
     const size_t cap = len / RPGPU_HEADER_SIZE + 2;
-    const size_t rcap = (flags & RPGPU_JOB_PARSE) ? len / 4 + 64 : 1;
-    const size_t padded = ((len + 15) / 16 + 1) * 16;
-    rpgpu::dev_buffer d_data(e, padded), d_offs(e, 16), d_b(e, cap * sizeof(rpgpu_batch_result)),
-        d_s(e, sizeof(rpgpu_segment_summary)), d_t(e, sizeof(rpgpu_job_totals)),
-        d_r(e, rcap * sizeof(rpgpu_record_index));
-    const uint64_t offs[2] = {0, (uint64_t)len};
-    e.check(rpgpu_memset(e.ctx(), d_data.get(), 0, padded, nullptr), "rpgpu_memset");
-    if (len) e.check(rpgpu_memcpy_h2d(e.ctx(), d_data.get(), seg, len, nullptr), "rpgpu_memcpy_h2d");
-    e.check(rpgpu_memcpy_h2d(e.ctx(), d_offs.get(), offs, sizeof offs, nullptr), "rpgpu_memcpy_h2d");
-    rpgpu_job j{};
-    j.d_data = (const uint8_t*)d_data.get();
-    j.d_seg_offsets = (const uint64_t*)d_offs.get();
-    j.h_seg_offsets = offs;
+    std::unique_ptr<rpgpu_batch_result[]> b(new rpgpu_batch_result[cap]);
+    std::unique_ptr<uint32_t[]> ro, rt;
+    std::unique_ptr<uint64_t[]> ps;
+    const uint8_t* segs[1] = {seg};
+    const uint64_t sizes[1] = {(uint64_t)len};
+    rpgpu_job_totals t{};
+    rpgpu_host_job j{};
+    j.segments = segs;
+    j.seg_sizes = sizes;
     j.n_segments = 1;
     j.layout = layout;
     j.flags = flags;
-    j.d_records = (rpgpu_record_index*)d_r.get();
-    j.record_capacity = rcap;
-    j.d_batches = (rpgpu_batch_result*)d_b.get();
+    j.batches = b.get();
     j.batch_capacity = cap;
-    j.d_summaries = (rpgpu_segment_summary*)d_s.get();
-    j.d_totals = (rpgpu_job_totals*)d_t.get();
-    e.check(rpgpu_submit(e.ctx(), &j, nullptr), "rpgpu_submit");
+    j.summaries = &out.summary;
+    j.totals = &t;
     if (want_index) {
-        // segment_index::maybe_track over the crc-good prefix, on the same stream
-        rpgpu::dev_buffer d_st(e, sizeof(rpgpu_index_state)), d_ro(e, cap * 4), d_rt(e, cap * 4), d_ps(e, cap * 8);
+        ro.reset(new uint32_t[cap]);
+        rt.reset(new uint32_t[cap]);
+        ps.reset(new uint64_t[cap]);
         out.index = rpgpu_index_state{};
         out.index.base_offset = want_index->base_offset;
-        e.check(rpgpu_memcpy_h2d(e.ctx(), d_st.get(), &out.index, sizeof out.index, nullptr), "rpgpu_memcpy_h2d");
-        e.check(rpgpu_segment_index(e.ctx(), (const rpgpu_batch_result*)d_b.get(), cap,
-                                    (const rpgpu_segment_summary*)d_s.get(), 1, want_index->step,
-                                    (rpgpu_index_state*)d_st.get(), (uint32_t*)d_ro.get(), (uint32_t*)d_rt.get(),
-                                    (uint64_t*)d_ps.get(), nullptr),
-                "rpgpu_segment_index");
-        e.check(rpgpu_memcpy_d2h(e.ctx(), &out.index, d_st.get(), sizeof out.index, nullptr), "rpgpu_memcpy_d2h");
-        e.check(rpgpu_sync(e.ctx(), nullptr), "rpgpu_sync");
-        const size_t n = (size_t)out.index.n_entries;
-        out.rel_offset.resize(n);
-        out.rel_time.resize(n);
-        out.position.resize(n);
-        if (n) {
-            e.check(rpgpu_memcpy_d2h(e.ctx(), out.rel_offset.data(), (uint32_t*)d_ro.get() + out.index.first_entry,
-                                     n * 4, nullptr), "rpgpu_memcpy_d2h");
-            e.check(rpgpu_memcpy_d2h(e.ctx(), out.rel_time.data(), (uint32_t*)d_rt.get() + out.index.first_entry,
-                                     n * 4, nullptr), "rpgpu_memcpy_d2h");
-            e.check(rpgpu_memcpy_d2h(e.ctx(), out.position.data(), (uint64_t*)d_ps.get() + out.index.first_entry,
-                                     n * 8, nullptr), "rpgpu_memcpy_d2h");
-        }
-        e.check(rpgpu_sync(e.ctx(), nullptr), "rpgpu_sync");
+        j.index_step = want_index->step;
+        j.index_states = &out.index;
+        j.rel_offset = ro.get();
+        j.rel_time = rt.get();
+        j.position = ps.get();
     }
-    rpgpu_job_totals t{};
-    e.check(rpgpu_memcpy_d2h(e.ctx(), &t, d_t.get(), sizeof t, nullptr), "rpgpu_memcpy_d2h");
-    e.check(rpgpu_memcpy_d2h(e.ctx(), &out.summary, d_s.get(), sizeof out.summary, nullptr), "rpgpu_memcpy_d2h");
-    e.check(rpgpu_sync(e.ctx(), nullptr), "rpgpu_sync");
-    out.batches.resize((size_t)t.n_batches);
-    if (t.n_batches)
-        e.check(rpgpu_memcpy_d2h(e.ctx(), out.batches.data(), d_b.get(), t.n_batches * sizeof(rpgpu_batch_result), nullptr),
-                "rpgpu_memcpy_d2h");
-    e.check(rpgpu_sync(e.ctx(), nullptr), "rpgpu_sync");
+    e.check(rpgpu_validate_host(e.ctx(), &j), "rpgpu_validate_host");
+    const size_t nb = (size_t)std::min<uint64_t>(t.n_batches, cap);
+    out.batches.assign(b.get(), b.get() + nb);
+    if (want_index) {
+        const size_t a = (size_t)out.index.first_entry, n = (size_t)out.index.n_entries;
+        out.rel_offset.assign(ro.get() + a, ro.get() + a + n);
+        out.rel_time.assign(rt.get() + a, rt.get() + a + n);
+        out.position.assign(ps.get() + a, ps.get() + a + n);
+    }
     return out;
 }
 }  // namespace detail

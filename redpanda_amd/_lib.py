@@ -102,6 +102,8 @@ def load():
         "rpgpu_serialize_wire": (i32, [vp, vp, vp, vp, u64, u32, vp, vp, vp]),
         "rpgpu_validate_host": (i32, [vp, vp]),
         "rpgpu_segment_index": (i32, [vp, vp, u64, vp, u32, u64, vp, vp, vp, vp, vp]),
+        "rpgpu_uncompress_bound": (u64, [i32, vp, sz]),
+        "rpgpu_stamp_host": (i32, [vp, vp, sz, vp, vp, u32, C.c_int64, u32]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)

@@ -153,9 +153,22 @@ struct rpgpu_ctx {
         uint64_t sums_n = 0;
         rpgpu_job_totals* d_tot = nullptr;
         rpgpu_job_totals* h_tot = nullptr;  // pinned
+        // segment index rebuild (rpgpu_host_job.index_step)
+        rpgpu_index_state* d_ist = nullptr;
+        uint64_t ist_n = 0;
+        uint32_t* d_ro = nullptr;
+        uint32_t* d_rt = nullptr;
+        uint64_t* d_ps = nullptr;
+        uint64_t ix_n = 0;
         hipEvent_t h2d = nullptr, done = nullptr;
         std::vector<uint64_t> h_offs;
+        std::vector<rpgpu_index_state> h_ist;
     } hs[2];
+    // rpgpu_stamp_host staging (pinned host + device), grow-only
+    void* sth = nullptr;
+    size_t sth_bytes = 0;
+    void* std_ = nullptr;
+    size_t std_bytes = 0;
 };
 
 namespace {
@@ -263,6 +276,8 @@ int rpgpu_destroy(rpgpu_ctx* c) {
     if (c->seqs) hipFree(c->seqs);
     if (c->pool) hipFree(c->pool);
     if (c->pin) hipHostFree(c->pin);
+    if (c->sth) hipHostFree(c->sth);
+    if (c->std_) hipFree(c->std_);
     if (c->d_tables) hipFree(c->d_tables);
     if (c->ws_ev) { (void)hipEventSynchronize(c->ws_ev); (void)hipEventDestroy(c->ws_ev); }
     for (auto& set : c->ev_sets)
@@ -273,6 +288,7 @@ int rpgpu_destroy(rpgpu_ctx* c) {
         (void)hipFree(h.d_data); (void)hipFree(h.d_offs); (void)hipFree(h.d_batches); (void)hipFree(h.d_records);
         (void)hipFree(h.d_decoded);
         (void)hipFree(h.d_sums); (void)hipFree(h.d_tot);
+        (void)hipFree(h.d_ist); (void)hipFree(h.d_ro); (void)hipFree(h.d_rt); (void)hipFree(h.d_ps);
         if (h.h_tot) (void)hipHostFree(h.h_tot);
         if (h.h2d) hipEventDestroy(h.h2d);
         if (h.done) hipEventDestroy(h.done);
@@ -1132,6 +1148,7 @@ uint64_t host_group_bytes(const rpgpu_host_job* job) {
 template <class T>
 int grow(rpgpu_ctx* c, T*& p, uint64_t& have, uint64_t need) {
     if (need <= have && p) return RPGPU_OK;
+    // hipFree waits for the device work still using the old buffer
     if (p) hipFree(p);
     p = nullptr;
     have = 0;
@@ -1187,6 +1204,27 @@ int host_issue(rpgpu_ctx* c, rpgpu_ctx::HostSlot& h, const rpgpu_host_job* job, 
     j.d_summaries = h.d_sums;
     j.d_totals = h.d_tot;
     if (int rc = rpgpu_submit(c, &j, c->stream)) return rc;
+    if (job->index_step && job->layout == RPGPU_LAYOUT_DISK) {
+        // segment_index::maybe_track over the group's crc-good prefixes
+        // (storage/log_replayer.cc:62-74), base offsets from the caller
+        if (int rc = grow(c, h.d_ist, h.ist_n, (uint64_t)g.nseg)) return rc;
+        if (h.ix_n < h.bcap || !h.d_ro) {
+            uint64_t have = 0;
+            if (int rc = grow(c, h.d_ro, have, h.bcap)) return rc;
+            have = 0;
+            if (int rc = grow(c, h.d_rt, have, h.bcap)) return rc;
+            have = 0;
+            if (int rc = grow(c, h.d_ps, have, h.bcap)) return rc;
+            h.ix_n = h.bcap;
+        }
+        h.h_ist.assign(g.nseg, rpgpu_index_state{});
+        for (uint32_t i = 0; i < g.nseg; i++) h.h_ist[i].base_offset = job->index_states[g.seg0 + i].base_offset;
+        HIPCHK(c, hipMemcpyAsync(h.d_ist, h.h_ist.data(), g.nseg * sizeof(rpgpu_index_state), hipMemcpyHostToDevice,
+                                 c->stream));
+        if (int rc = rpgpu_segment_index(c, h.d_batches, h.bcap, h.d_sums, g.nseg, job->index_step, h.d_ist, h.d_ro, h.d_rt,
+                                         h.d_ps, c->stream))
+            return rc;
+    }
     HIPCHK(c, hipMemcpyAsync(h.h_tot, h.d_tot, sizeof(rpgpu_job_totals), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipEventRecord(h.done, c->stream));
     return RPGPU_OK;
@@ -1197,8 +1235,12 @@ extern "C" {
 
 int rpgpu_validate_host(rpgpu_ctx* c, const rpgpu_host_job* job) {
     if (!c || !job || (job->n_segments && (!job->segments || !job->seg_sizes)) || !job->totals ||
-        (job->n_segments && !job->summaries) || (job->batch_capacity && !job->batches))
+        (job->n_segments && !job->summaries) || (job->batch_capacity && !job->batches) ||
+        (job->record_capacity && !job->records) || (job->decoded_capacity && !job->decoded) ||
+        (job->index_step && (!job->index_states || (job->batch_capacity && (!job->rel_offset || !job->rel_time ||
+                                                                             !job->position)))))
         return fail(c, RPGPU_E_INVALID, "rpgpu_validate_host: missing argument");
+    if (job->index_step >= (1ull << 62)) return fail(c, RPGPU_E_INVALID, "rpgpu_validate_host: index step out of range");
     if (job->layout != RPGPU_LAYOUT_DISK && job->layout != RPGPU_LAYOUT_WIRE)
         return fail(c, RPGPU_E_INVALID, "rpgpu_validate_host: unknown layout");
     hipSetDevice(c->device);
@@ -1242,18 +1284,51 @@ int rpgpu_validate_host(rpgpu_ctx* c, const rpgpu_host_job* job) {
         const uint64_t nb = t.n_batches;
         const uint64_t room = job->batch_capacity > out_b ? job->batch_capacity - out_b : 0;
         const uint64_t take = std::min(nb, room);
+        // this group's positions in the job: its records and decoded bytes
+        // follow the earlier groups' (the index slots and arena bytes one
+        // rpgpu_submit over every segment would have reserved before them)
+        const uint64_t rec_base = T.n_records, dec_base = T.decoded_bytes;
+        const uint64_t nrec = (job->flags & RPGPU_JOB_PARSE) ? t.n_records : 0;
+        const uint64_t ndec = (job->flags & RPGPU_JOB_DECODE) ? t.decoded_bytes : 0;
+        const uint64_t rroom = job->record_capacity > rec_base ? job->record_capacity - rec_base : 0;
+        const uint64_t droom = job->decoded_capacity > dec_base ? job->decoded_capacity - dec_base : 0;
+        const uint64_t rtake = job->records ? std::min(nrec, rroom) : 0;
+        const uint64_t dtake = job->decoded ? std::min(ndec, droom) : 0;
+        const bool ix = job->index_step && job->layout == RPGPU_LAYOUT_DISK;
         // results back on the copy stream: the compute stream already holds
         // the next group's pipeline, which must not be waited for here
         if (take) {
             HIPCHK(c, hipMemcpyAsync(job->batches + out_b, h.d_batches, take * sizeof(rpgpu_batch_result),
                                      hipMemcpyDeviceToHost, c->copy));
+            if (ix) {
+                HIPCHK(c, hipMemcpyAsync(job->rel_offset + out_b, h.d_ro, take * 4, hipMemcpyDeviceToHost, c->copy));
+                HIPCHK(c, hipMemcpyAsync(job->rel_time + out_b, h.d_rt, take * 4, hipMemcpyDeviceToHost, c->copy));
+                HIPCHK(c, hipMemcpyAsync(job->position + out_b, h.d_ps, take * 8, hipMemcpyDeviceToHost, c->copy));
+            }
         }
+        if (rtake)
+            HIPCHK(c, hipMemcpyAsync(job->records + rec_base, h.d_records, rtake * sizeof(rpgpu_record_index),
+                                     hipMemcpyDeviceToHost, c->copy));
+        if (dtake) HIPCHK(c, hipMemcpyAsync(job->decoded + dec_base, h.d_decoded, dtake, hipMemcpyDeviceToHost, c->copy));
         HIPCHK(c, hipMemcpyAsync(job->summaries + g.seg0, h.d_sums, g.nseg * sizeof(rpgpu_segment_summary),
                                  hipMemcpyDeviceToHost, c->copy));
+        if (ix)
+            HIPCHK(c, hipMemcpyAsync(job->index_states + g.seg0, h.d_ist, g.nseg * sizeof(rpgpu_index_state),
+                                     hipMemcpyDeviceToHost, c->copy));
         HIPCHK(c, hipStreamSynchronize(c->copy));
-        // group-relative -> job-wide ordinals
-        for (uint64_t i = 0; i < take; i++) job->batches[out_b + i].segment += g.seg0;
+        // group-relative -> job-wide ordinals and positions
+        for (uint64_t i = 0; i < take; i++) {
+            rpgpu_batch_result& r = job->batches[out_b + i];
+            r.segment += g.seg0;
+            r.index_base += rec_base;
+            r.decoded_off += dec_base;
+        }
+        for (uint64_t i = 0; i < rtake; i++) job->records[rec_base + i].batch += (uint32_t)out_b;
         for (uint32_t i = 0; i < g.nseg; i++) job->summaries[g.seg0 + i].first_batch += out_b;
+        if (ix)
+            for (uint32_t i = 0; i < g.nseg; i++) job->index_states[g.seg0 + i].first_entry += out_b;
+        if (nrec > rtake && job->records) T.overflow |= 2u;
+        if (ndec > dtake && job->decoded) T.overflow |= 4u;
         T.n_batches += nb;
         T.n_records += t.n_records;
         T.decoded_bytes += t.decoded_bytes;
@@ -1273,6 +1348,56 @@ int rpgpu_validate_host(rpgpu_ctx* c, const rpgpu_host_job* job) {
     }
     if (int rc = finish(groups.size() - 1)) return rc;
     T.batch_capacity_needed = T.n_batches;
+    return RPGPU_OK;
+}
+
+uint64_t rpgpu_uncompress_bound(int codec, const void* in, size_t n) {
+    if (!in || n == 0 || (codec != RPGPU_CODEC_LZ4 && codec != RPGPU_CODEC_SNAPPY)) return 0;
+    return decode_capacity_dev(codec, (const uint8_t*)in, n);
+}
+
+int rpgpu_stamp_host(rpgpu_ctx* c, uint8_t* buf, size_t len, const uint64_t* pos, const uint32_t* payload_len,
+                     uint32_t n, int64_t next_offset, uint32_t flags) {
+    if (!c) return RPGPU_E_INVALID;
+    if (n == 0) return RPGPU_OK;
+    if (!buf || !pos || ((flags & RPGPU_STAMP_CRC) && !payload_len))
+        return fail(c, RPGPU_E_INVALID, "rpgpu_stamp_host: missing argument");
+    hipSetDevice(c->device);
+    hipStream_t s = c->stream;
+    // device: [batches + 16][pos][plen]; host (pinned): the same
+    const size_t o_pos = align_up(len + 16, 256), o_len = align_up(o_pos + (size_t)n * 8, 256);
+    const size_t total = align_up(o_len + (size_t)n * 4, 256);
+    if (total > c->std_bytes) {
+        if (c->std_) {
+            if (int rc = ws_drain(c, s)) return rc;
+            HIPCHK(c, hipFree(c->std_));
+            c->std_ = nullptr;
+            c->std_bytes = 0;
+        }
+        if (hipMalloc(&c->std_, total) != hipSuccess) { c->std_ = nullptr; return fail(c, RPGPU_E_NOMEM, "stamp staging"); }
+        c->std_bytes = total;
+    }
+    if (total > c->sth_bytes) {
+        if (c->sth) { HIPCHK(c, hipStreamSynchronize(s)); HIPCHK(c, hipHostFree(c->sth)); c->sth = nullptr; c->sth_bytes = 0; }
+        if (hipHostMalloc(&c->sth, total, hipHostMallocDefault) != hipSuccess) {
+            c->sth = nullptr;
+            return fail(c, RPGPU_E_NOMEM, "stamp pinned staging");
+        }
+        c->sth_bytes = total;
+    }
+    uint8_t* h = (uint8_t*)c->sth;
+    uint8_t* d = (uint8_t*)c->std_;
+    std::memcpy(h, buf, len);
+    std::memset(h + len, 0, 16);
+    std::memcpy(h + o_pos, pos, (size_t)n * 8);
+    if (payload_len) std::memcpy(h + o_len, payload_len, (size_t)n * 4);
+    HIPCHK(c, hipMemcpyAsync(d, h, total, hipMemcpyHostToDevice, s));
+    if (int rc = rpgpu_stamp(c, d, (const uint64_t*)(d + o_pos), payload_len ? (const uint32_t*)(d + o_len) : nullptr, n,
+                             next_offset, flags, s))
+        return rc;
+    HIPCHK(c, hipMemcpyAsync(h, d, len, hipMemcpyDeviceToHost, s));
+    HIPCHK(c, hipStreamSynchronize(s));
+    std::memcpy(buf, h, len);
     return RPGPU_OK;
 }
 

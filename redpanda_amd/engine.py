@@ -392,26 +392,57 @@ class Engine:
         return out.to_host()
 
     def validate_host(self, segments, flags: int = abi.JOB_CRC | abi.JOB_PARSE, layout: int = abi.LAYOUT_DISK,
-                      batch_capacity=None, group_kib: int = 0):
+                      batch_capacity=None, group_kib: int = 0, record_capacity=None, decoded_capacity=None,
+                      index_step: int = 0, base_offsets=None):
         """rpgpu_validate_host: host-resident segments (numpy uint8 arrays,
         pinned or pageable) copied to the device in double-buffered groups
-        and validated there.  Returns (batches, summaries, totals) as numpy
-        structured arrays; the record index stays on the device."""
+        and validated there.  Returns a HostResult (batches, records, decoded
+        arena, summaries, totals; bitmap None) holding what one device job
+        over all the segments returns, plus `.index` (per segment:
+        index_state row, relative_offset, relative_time, position) when
+        index_step is set."""
         segs = [np.ascontiguousarray(s, dtype=np.uint8) for s in segments]
         n = len(segs)
+        total = sum(s.size for s in segs)
         if batch_capacity is None:
-            batch_capacity = sum(s.size for s in segs) // abi.HEADER_SIZE + n + 1
+            batch_capacity = total // abi.HEADER_SIZE + n + 1
+        if record_capacity is None:
+            record_capacity = max(total // 4, 64) if flags & abi.JOB_PARSE else 0
+        if decoded_capacity is None:
+            decoded_capacity = max(total * 8, 1 << 16) if flags & abi.JOB_DECODE else 0
         ptrs = (C.c_void_p * max(n, 1))(*[s.ctypes.data for s in segs])
         sizes = (C.c_uint64 * max(n, 1))(*[s.size for s in segs])
         batches = np.zeros(max(batch_capacity, 1), dtype=abi.BATCH_RESULT)
+        recs = np.zeros(max(record_capacity, 1), dtype=abi.RECORD_INDEX)
+        dec = np.zeros(max(decoded_capacity, 1), dtype=np.uint8)
         sums = np.zeros(max(n, 1), dtype=abi.SEGMENT_SUMMARY)
         tot = np.zeros(1, dtype=abi.JOB_TOTALS)
+        st = np.zeros(max(n, 1), dtype=abi.INDEX_STATE)
+        if base_offsets is not None:
+            st["base_offset"][:n] = np.asarray(base_offsets, dtype=np.int64)
+        ro = np.zeros(max(batch_capacity, 1), np.uint32)
+        rt = np.zeros(max(batch_capacity, 1), np.uint32)
+        ps = np.zeros(max(batch_capacity, 1), np.uint64)
         job = HostJobC(C.cast(ptrs, C.c_void_p), C.cast(sizes, C.c_void_p), n, layout, flags, group_kib,
-                       batches.ctypes.data, batch_capacity, sums.ctypes.data, tot.ctypes.data)
+                       batches.ctypes.data, batch_capacity, sums.ctypes.data, tot.ctypes.data,
+                       recs.ctypes.data if record_capacity else None, record_capacity,
+                       dec.ctypes.data if decoded_capacity else None, decoded_capacity,
+                       index_step, st.ctypes.data if index_step else None, ro.ctypes.data if index_step else None,
+                       rt.ctypes.data if index_step else None, ps.ctypes.data if index_step else None)
         rc = self.L.rpgpu_validate_host(self.ctx, C.byref(job))
         check(rc, self.ctx, "rpgpu_validate_host")
-        nb = int(min(tot[0]["n_batches"], batch_capacity))
-        return batches[:nb], sums[:n], tot[0]
+        t = tot[0]
+        nb = int(min(t["n_batches"], batch_capacity))
+        nr = int(min(t["n_records"], record_capacity))
+        nd = int(min(t["decoded_bytes"], decoded_capacity))
+        res = HostResult(batches[:nb], recs[:nr], dec[:nd], sums[:n], t, None)
+        res.index = None
+        if index_step:
+            res.index = []
+            for k in range(n):
+                a, m = int(st[k]["first_entry"]), int(st[k]["n_entries"])
+                res.index.append((st[k], ro[a:a + m].copy(), rt[a:a + m].copy(), ps[a:a + m].copy()))
+        return res
 
 
 class Pending:
@@ -450,4 +481,7 @@ class HostJobC(C.Structure):
     _fields_ = [("segments", C.c_void_p), ("seg_sizes", C.c_void_p), ("n_segments", C.c_uint32),
                 ("layout", C.c_uint32), ("flags", C.c_uint32), ("group_kib", C.c_uint32),
                 ("batches", C.c_void_p), ("batch_capacity", C.c_uint64), ("summaries", C.c_void_p),
-                ("totals", C.c_void_p)]
+                ("totals", C.c_void_p), ("records", C.c_void_p), ("record_capacity", C.c_uint64),
+                ("decoded", C.c_void_p), ("decoded_capacity", C.c_uint64), ("index_step", C.c_uint64),
+                ("index_states", C.c_void_p), ("rel_offset", C.c_void_p), ("rel_time", C.c_void_p),
+                ("position", C.c_void_p)]

@@ -6,10 +6,12 @@
 //   surfaces_test cpu <segment>                 host walk: model:: crc helpers
 //   surfaces_test parse <segment> M R S E       continuous_batch_parser replay
 //   surfaces_test recover <segment>             log_replayer checkpoint
+//   surfaces_test recover_bench <reps> <seg>... log_replayer::recover timing (host path)
 //   surfaces_test index <segment> <base> <q>... log_replayer recovery + segment_index rebuild,
 //                                               find_nearest(offset) for each q
 //   surfaces_test uncompress (<codec> <in> <out>)+  compressor::uncompress
 //   surfaces_test wire <record_set>             kafka::batch_reader
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <fstream>
@@ -193,6 +195,27 @@ int main(int argc, char** argv) {
             const storage::log_replayer::checkpoint c = storage::log_replayer::recover(seg.data(), seg.size());
             if (c.last_offset) std::printf("CKPT 1 %lld %zu\n", (long long)*c.last_offset, *c.truncate_file_pos);
             else std::printf("CKPT 0\n");
+            return 0;
+        }
+        if (mode == "recover_bench" && argc >= 4) {
+            // log_replayer::recover over host segments (the pinned,
+            // double-buffered host path): wall time per pass after a warm-up
+            std::vector<std::vector<uint8_t>> segs;
+            for (int a = 3; a < argc; a++) segs.push_back(slurp(argv[a]));
+            const int reps = std::atoi(argv[2]);
+            size_t bytes = 0;
+            for (auto& sg : segs) bytes += sg.size();
+            for (auto& sg : segs) (void)storage::log_replayer::recover(sg.data(), sg.size());  // warm-up
+            const auto t0 = std::chrono::steady_clock::now();
+            long long ck = 0;
+            for (int r = 0; r < reps; r++)
+                for (auto& sg : segs) {
+                    const storage::log_replayer::checkpoint c = storage::log_replayer::recover(sg.data(), sg.size());
+                    ck += c.last_offset ? *c.last_offset : -1;
+                }
+            const double sec = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+            std::printf("RECOVER_BENCH bytes=%zu reps=%d seconds=%.4f GBps=%.2f ckpt_sum=%lld\n", bytes, reps, sec,
+                        (double)bytes * reps / sec / 1e9, ck);
             return 0;
         }
         if (mode == "xxh64") {  // host only: the .base_index checksum primitive

@@ -22,13 +22,29 @@ G = os.path.join(HERE, "golden")
 FLAGS = abi.JOB_CRC | abi.JOB_PARSE
 
 
-def assert_same(got, ref, flags=0):
+def written_records(res):
+    """Record-index slots the ABI defines: [index_base, index_base +
+    records_parsed) of every batch with RPGPU_F_INDEX_WRITTEN (rpgpu.h); the
+    rest of a reserved range is undefined."""
+    mask = np.zeros(len(res.records), dtype=bool)
+    b = res.batches
+    w = (b["flags"] & abi.F_INDEX_WRITTEN) != 0
+    for ib, n in zip(b["index_base"][w], b["records_parsed"][w]):
+        mask[int(ib):int(ib) + int(n)] = True
+    return mask
+
+
+def assert_same(got, ref, flags=0, defined_only=False):
+    """defined_only: compare the record index on the slots the ABI defines
+    (buffers reused across jobs, as the host path's staging slots are, keep
+    older entries in the undefined ones)."""
     assert len(got.batches) == len(ref.batches)
     for f in abi.BATCH_COMPARE_FIELDS:
         np.testing.assert_array_equal(got.batches[f], ref.batches[f], err_msg=f"batches.{f}")
     assert len(got.records) == len(ref.records)
+    rm = written_records(ref) if defined_only else slice(None)
     for f in abi.RECORD_COMPARE_FIELDS:
-        np.testing.assert_array_equal(got.records[f], ref.records[f], err_msg=f"records.{f}")
+        np.testing.assert_array_equal(got.records[f][rm], ref.records[f][rm], err_msg=f"records.{f}")
     for f in abi.SUMMARY_COMPARE_FIELDS:
         np.testing.assert_array_equal(got.summaries[f], ref.summaries[f], err_msg=f"summaries.{f}")
     for k in ("n_batches", "n_records", "decoded_bytes", "overflow"):
@@ -334,10 +350,12 @@ def test_wire_layout_codec_mix(engine, oracle, rplib):
 @pytest.mark.parametrize("recipe", ["mix", "c5"])
 def test_host_path(engine, oracle, rplib, group_kib, recipe):
     """rpgpu_validate_host (pinned/pageable host segments, double-buffered
-    H2D groups): per-batch results and summaries equal the oracle's over the
-    same segments.  Small staging groups exercise the slot alternation; the
-    LZ4/snappy mix with DECODE makes groups overflow the first-try decode
-    capacity and re-run."""
+    H2D groups) returns exactly what one device job over the same segments
+    returns: batch results, the record index, the decoded arena, summaries,
+    totals, and the rebuilt segment indexes, all job-wide, == the oracle.
+    Small staging groups exercise the slot alternation and the group-to-job
+    rebasing; the LZ4/snappy mix with DECODE makes groups overflow the
+    first-try decode capacity and re-run."""
     if recipe == "c5":
         segs = [gen(rplib, 3 << 20, i, **synth.C5) for i in range(4)]
     else:
@@ -346,17 +364,31 @@ def test_host_path(engine, oracle, rplib, group_kib, recipe):
     segs.append(gen(rplib, 4 << 20, 9, seed=0xC1))
     offs = np.cumsum([0] + [s.size for s in segs]).astype(np.uint64)
     ref = oracle.run_job(np.concatenate(segs), offs, DFLAGS)
-    b, s, t = engine.validate_host(segs, DFLAGS, group_kib=group_kib)
-    assert len(b) == len(ref.batches)
-    for f in abi.BATCH_COMPARE_FIELDS:
-        if f in ("index_base", "decoded_off"):  # device-side arena positions, per staging group
-            continue
-        np.testing.assert_array_equal(b[f], ref.batches[f], err_msg=f"batches.{f}")
-    for f in abi.SUMMARY_COMPARE_FIELDS:
-        np.testing.assert_array_equal(s[f], ref.summaries[f], err_msg=f"summaries.{f}")
-    for k in ("n_batches", "n_records", "decoded_bytes"):
-        assert int(t[k]) == int(ref.totals[k]), k
-    assert int(t["overflow"]) == 0
+    bases = [1000 * (k + 1) for k in range(len(segs))]
+    got = engine.validate_host(segs, DFLAGS, group_kib=group_kib, index_step=8192, base_offsets=bases)
+    assert_same(got, ref, DFLAGS, defined_only=True)
+    rix = oracle.segment_index(ref.batches, ref.summaries, bases, step=8192)
+    assert len(got.index) == len(rix)
+    for (gs, gro, grt, gps), (rs, rro, rrt, rps) in zip(got.index, rix):
+        assert all(int(gs[f]) == int(rs[f]) for f in abi.INDEX_STATE.names), (gs, rs)
+        assert np.array_equal(gro, rro) and np.array_equal(grt, rrt) and np.array_equal(gps, rps)
+
+
+def test_host_path_small_host_capacities(engine, oracle, rplib):
+    """Host output arrays smaller than the job: what fits is returned and
+    totals.overflow says which ones were short (bits 2 / 4)."""
+    segs = [gen(rplib, 2 << 20, i, seed=0xC2 + i, batch_bytes=0, min_batch=4096, max_batch=200000, codec_mix=MIX)
+            for i in range(3)]
+    offs = np.cumsum([0] + [s.size for s in segs]).astype(np.uint64)
+    ref = oracle.run_job(np.concatenate(segs), offs, DFLAGS)
+    nrec, ndec = int(ref.totals["n_records"]), int(ref.totals["decoded_bytes"])
+    got = engine.validate_host(segs, DFLAGS, group_kib=1024, record_capacity=nrec // 2, decoded_capacity=ndec // 3)
+    assert int(got.totals["overflow"]) & 6 == 6
+    assert len(got.batches) == len(ref.batches)
+    n = len(got.records)
+    rm = written_records(ref)[:n]
+    for f in abi.RECORD_COMPARE_FIELDS:
+        np.testing.assert_array_equal(got.records[f][rm], ref.records[f][:n][rm], err_msg=f"records.{f}")
 
 
 # ---------------------------------------------------------------------------
