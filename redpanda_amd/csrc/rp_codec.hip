@@ -1037,6 +1037,7 @@ DEV bool plan_lz4f(const DeviceJob& j, In& in, int64_t n, uint64_t src_abs, uint
             it.kind = (raw ? kBlkRaw : 0u) | (bcs ? kBlkChecksum : 0u) | (linked ? kBlkLinked : 0u);
             it.out = -1;
             it.cap = raw ? (uint32_t)bsz : (uint32_t)bmax;
+            it.crc = it.pad = 0;
             j.blocks[first + k] = it;
             if (piece_is_long(it.kind, it.csize, it.cap)) lm |= 1ull << (k & 63);
             if ((k & 63) == 63 || k + 1 == nb) {
@@ -1102,6 +1103,7 @@ DEV bool plan_snappy_java(const DeviceJob& j, In& in, int64_t n, uint64_t src_ab
             it.kind = kBlkSnappy;
             it.out = -1;
             it.cap = ulen;
+            it.crc = it.pad = 0;
             j.blocks[first + k] = it;
             if (piece_is_long(it.kind, it.csize, it.cap)) lm |= 1ull << (k & 63);
             if ((k & 63) == 63 || k + 1 == nb) {
@@ -1136,6 +1138,7 @@ DEV bool plan_snappy_whole(const DeviceJob& j, int64_t n, uint64_t src_abs, uint
         it.kind = kBlkSnappy | kBlkWhole;
         it.out = -1;
         it.cap = (uint32_t)cap;
+        it.crc = it.pad = 0;
         j.blocks[first] = it;
         note_long(j, first);
     }
@@ -1238,14 +1241,42 @@ constexpr uint32_t kFlushLag = kXRing >= 65536 ? (24u << 10) : kXRing / 4;
 // below the flushed position; xbig's far reads need ring >= lag + 2 KiB + 64
 static_assert(kFlushLag + 1024 + 128 * kBig + kBig <= kXRing, "ring too small for the flush lag and a batch");
 static_assert(kXRing >= kFlushLag + 2048 + 128, "ring too small for xbig's far reads");
+// Workgroup layout: kExecWaves independent waves (each claims its own work)
+// share one LDS image: their rings, then the CRC tables of the streaming
+// decoded-payload CRC (braid T1023..T1020 and slice T3..T0, 1 KiB each, a
+// single copy) and the short-offset pattern selectors.  (One wave per
+// workgroup left no room for shared tables; 9 rings + 8.5 KiB fit 160 KiB,
+// as many waves per CU as the 10 one-wave workgroups that were resident.)
+constexpr uint32_t kExecWaves = (160u * 1024u - 8704u) / kXRing;
+constexpr uint32_t kXCrcOff = kExecWaves * kXRing;
+constexpr uint32_t kXPatOff = kXCrcOff + 8192u;
+constexpr uint32_t kXLds = kXPatOff + 512u;
+static_assert(kExecWaves >= 1 && kXLds <= 160u * 1024u, "k_lz_exec LDS image exceeds 160 KiB");
 constexpr uint32_t kBufFlags = 0x00020000u;    // buffer resource word 3 (raw, 32-bit data format)
 constexpr int kSc1 = 16;                       // cache policy: sc1 (L2-coherent, bypasses the vector L1)
+
+typedef const __attribute__((address_space(3))) uint32_t lds_cu32;
+
+struct CrcState {
+    uint32_t bp[4], bq[4];  // braid k's state is bp[k] ^ bq[k]
+    uint4 pend;             // the pending row
+    uint32_t crow;          // end of the rows taken in
+    uint32_t hp;            // a row is pending
+};
 
 struct XRing {
     lds_u8* r;
     uint8_t* dst;           // arena address of position 0
     uint32_t op;            // next output position (uniform)
     uint32_t flushed;       // positions below are stored to dst
+    // streaming CRC of the output (reset_size_checksum_metadata's new crc,
+    // computed as flushed rows pass instead of re-reading the arena): rows
+    // of 1 KiB from position 0, lane l holding bytes [16 l, +16); braid k of
+    // a lane accumulates its dword k of every row (state bp ^ bq); the last
+    // row seen stays pending (un-braided) until the next one arrives or the
+    // output ends, where it is folded (crc_finish)
+    lds_cu32* ct;           // T1023..T1020 (4 x 256), then T3..T0
+    CrcState cs;
     bool linked;            // positions may pass the ring size (the ring wraps)
     bool hist;              // later pieces copy from this output (a linked frame): raw pieces go through the ring
     bool fpend;             // flush stores issued since the last full wait
@@ -1256,6 +1287,56 @@ struct XRing {
 };
 
 DEV void wait_vm() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
+DEV uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) { return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96); }
+
+// one braid step of braid k with word w: the CRC of (state ^ w) over the
+// word and the 1020 bytes of the other braids of the row
+DEV void xbraid(CrcState& c, lds_cu32* ct, int k, uint32_t w) {
+    const uint32_t v = xor3(c.bp[k], c.bq[k], w);
+    const uint32_t a = ct[v & 255u], b = ct[256u + ((v >> 8) & 255u)], d = ct[512u + ((v >> 16) & 255u)];
+    c.bq[k] = ct[768u + (v >> 24)];
+    c.bp[k] = xor3(a, b, d);
+}
+// slice-by-4 word step from v = state ^ word, xored with e
+DEV uint32_t xword(lds_cu32* ct, uint32_t v, uint32_t e) {
+    return xor3(xor3(ct[1024u + (v & 255u)], ct[1280u + ((v >> 8) & 255u)], ct[1536u + ((v >> 16) & 255u)]),
+                ct[1792u + (v >> 24)], e);
+}
+DEV void crc_init(CrcState& c) {
+#pragma unroll
+    for (int k = 0; k < 4; k++) c.bp[k] = c.bq[k] = 0u;
+    c.pend = make_uint4(0u, 0u, 0u, 0u);
+    c.crow = 0;
+    c.hp = 0;
+}
+// the next 1 KiB row of the output (this lane's 16 bytes; zero past the end)
+DEV void crc_row(CrcState& c, lds_cu32* ct, const uint4& v) {
+    if (c.hp) {
+        xbraid(c, ct, 0, c.pend.x);
+        xbraid(c, ct, 1, c.pend.y);
+        xbraid(c, ct, 2, c.pend.z);
+        xbraid(c, ct, 3, c.pend.w);
+    }
+    c.pend = v;
+    c.hp = 1;
+    c.crow += 1024u;
+}
+DEV void crc_row(XRing& x, const uint4& v) { crc_row(x.cs, x.ct, v); }
+// linear CRC (zero state, no final xor) of output [0, n), every row up to n
+// taken in: the pending row folded with word steps, the lane states moved
+// to the row end (x^(8 * 16 (63 - l))) and merged, then moved back over the
+// zero padding of the last row (x^(-8 z))
+DEV uint32_t crc_finish(const XRing& x, const Tables* __restrict__ T, uint32_t n) {
+    const CrcState& c = x.cs;
+    if (!c.hp) return 0u;
+    uint32_t w = xword(x.ct, xor3(c.bp[0], c.bq[0], c.pend.x), c.bp[1] ^ c.bq[1]);
+    w = xword(x.ct, w ^ c.pend.y, c.bp[2] ^ c.bq[2]);
+    w = xword(x.ct, w ^ c.pend.z, c.bp[3] ^ c.bq[3]);
+    const uint32_t s0 = xword(x.ct, w ^ c.pend.w, 0u);
+    const uint32_t acc = wave_xor(multmodp(T->lane_rowend[lane()], s0));
+    return multmodp(uni32(T->inv_shift[(c.crow - n) & 1023u]), uni32(acc));
+}
 
 // 16 ring bytes at position p (wrapping)
 DEV uint4 xld16(const lds_u8* r, uint32_t p) {
@@ -1294,6 +1375,8 @@ DEV void xst(lds_u8* r, uint32_t p, const uint4& v, uint32_t len) {
 // store ring positions [x.flushed, upto) to the arena: whole 16-byte pieces
 // as one ds_read_b128 + global_store_dwordx4 per lane, edge pieces byte by
 // byte.  Uniform trip count.
+// Every flush but a piece's last one ends on a 1 KiB boundary, so each
+// flushed row is taken into the streaming CRC whole, in order, once.
 DEV void xflush(XRing& x, uint32_t upto) {
     const uint32_t f = x.flushed;
     if (f >= upto) return;
@@ -1302,13 +1385,22 @@ DEV void xflush(XRing& x, uint32_t upto) {
     const uint32_t nch = (((upto + 1023u) & ~1023u) - c0) >> 10;
     for (uint32_t i = 0; i < nch; i++) {
         const uint32_t a = c0 + (i << 10) + 16u * l;
+        uint4 v = make_uint4(0u, 0u, 0u, 0u);
         if (a >= f && a + 16 <= upto) {
-            gst16(x.dst + a, xld16(x.r, a));
+            v = xld16(x.r, a);
+            gst16(x.dst + a, v);
         } else if (a + 16 > f && a < upto) {
+            uint32_t w[4] = {0u, 0u, 0u, 0u};
 #pragma unroll
             for (uint32_t b = 0; b < 16; b++)
-                if (a + b >= f && a + b < upto) x.dst[a + b] = x.r[(a + b) & kXM];
+                if (a + b >= f && a + b < upto) {
+                    const uint32_t y = x.r[(a + b) & kXM];
+                    x.dst[a + b] = (uint8_t)y;
+                    w[b >> 2] |= y << (8 * (b & 3));
+                }
+            v = make_uint4(w[0], w[1], w[2], w[3]);
         }
+        crc_row(x, v);
     }
     x.flushed = upto;
     x.fpend = true;
@@ -1529,23 +1621,43 @@ DEV void xrecords(XRing& x, const Src& s, const SeqRec* recs, uint32_t cnt) {
 
 // raw bytes straight from the stream to the arena (an independent raw
 // block): 16 bytes per lane, 4 KiB per step
-DEV void xcopy_raw(uint8_t* dst, const Src& s, uint32_t len) {
+// (the rows also feed the streaming CRC).  Not inlined: inlined into
+// k_lz_exec, its unrolled rows of CRC table loads pushed the kernel past the
+// 168 VGPRs its 9-wave workgroups allow; a call per raw piece is cheap.
+__device__ __noinline__ CrcState raw_copy(uint8_t* dst, const uint8_t* src, int64_t rl, uint32_t len, lds_cu32* ct,
+                                          CrcState c) {
+    const Src s{src, (int64_t)len, rl};
     const uint32_t l = lane();
-    uint32_t c = 0;
-    for (; c + 4096 <= len; c += 4096) {
+    uint32_t k = 0;
+    for (; k + 4096 <= len; k += 4096) {
         uint4 v[4];
 #pragma unroll
-        for (int u = 0; u < 4; u++) v[u] = ld16(s, (int64_t)c + 1024 * u + 16 * l);
+        for (int u = 0; u < 4; u++) v[u] = ld16(s, (int64_t)k + 1024 * u + 16 * l);
 #pragma unroll
-        for (int u = 0; u < 4; u++) gst16(dst + c + 1024 * u + 16 * l, v[u]);
+        for (int u = 0; u < 4; u++) gst16(dst + k + 1024 * u + 16 * l, v[u]);
+#pragma unroll
+        for (int u = 0; u < 4; u++) crc_row(c, ct, v[u]);
     }
-    for (; c < len; c += 1024) {
-        const uint32_t k = c + 16 * l;
-        if (k + 16 <= len) gst16(dst + k, ld16(s, k));
-        else if (k < len)
-            for (uint32_t b = k; b < len; b++) dst[b] = s.p[b];
+    for (; k < len; k += 1024) {
+        const uint32_t q = k + 16 * l;
+        uint4 v = make_uint4(0u, 0u, 0u, 0u);
+        if (q + 16 <= len) {
+            v = ld16(s, q);
+            gst16(dst + q, v);
+        } else if (q < len) {
+            uint32_t w[4] = {0u, 0u, 0u, 0u};
+            for (uint32_t b = q; b < len; b++) {
+                const uint32_t y = src[b];
+                dst[b] = (uint8_t)y;
+                w[(b - q) >> 2] |= y << (8 * ((b - q) & 3));
+            }
+            v = make_uint4(w[0], w[1], w[2], w[3]);
+        }
+        crc_row(c, ct, v);
     }
+    return c;
 }
+DEV void xcopy_raw(XRing& x, const Src& s, uint32_t len) { x.cs = raw_copy(x.dst, s.p, s.rl, len, x.ct, x.cs); }
 
 // A piece's stream and walk state (one lane)
 struct Piece {
@@ -2043,6 +2155,7 @@ DEV void walk_long(const DeviceJob& j, uint32_t p, lds_u8* win) {
     it.kind = uni32(j.blocks[p].kind);
     it.out = -1;
     it.cap = uni32(j.blocks[p].cap);
+    it.crc = it.pad = 0;
     Piece pc;
     piece_begin(pc, j, it, win);  // (the window buffer hashes the block checksum first)
     PieceState out;
@@ -2224,7 +2337,7 @@ DEV int32_t exec_piece(XRing& x, const DeviceJob& j, uint32_t p, uint32_t hist, 
     if (kind & kBlkRaw) {
         if (x.hist) xbig(x, s, 0, csize, 0, 0);
         else {
-            xcopy_raw(x.dst + x.op, s, csize);
+            xcopy_raw(x, s, csize);
             x.op += csize;
             x.flushed = x.op;
             x.fpend = true;
@@ -2271,9 +2384,11 @@ DEV int32_t exec_piece(XRing& x, const DeviceJob& j, uint32_t p, uint32_t hist, 
 }
 
 DEV void xring_init(XRing& x, const DeviceJob& j, lds_u8* ring, uint64_t dst, bool linked, bool hist,
-                    const __attribute__((address_space(3))) uint32_t* pat) {
+                    const __attribute__((address_space(3))) uint32_t* pat, lds_cu32* ct) {
     x.r = ring;
     x.pat = pat;
+    x.ct = ct;
+    crc_init(x.cs);
     x.dst = j.decoded + dst;
     x.op = 0;
     x.flushed = 0;
@@ -2287,11 +2402,11 @@ DEV void xring_init(XRing& x, const DeviceJob& j, lds_u8* ring, uint64_t dst, bo
 
 // the blocks of one linked LZ4F frame, in order, one position space
 DEV void exec_linked(const DeviceJob& j, lds_u8* ring, SeqRec* buf, uint32_t item,
-                     const __attribute__((address_space(3))) uint32_t* pat) {
+                     const __attribute__((address_space(3))) uint32_t* pat, lds_cu32* ct) {
     const uint32_t first = uni32(j.plans[item].first), nb = uni32(j.plans[item].nb);
     const uint64_t fdst = uni64(j.dcap[uni32(j.decode_list[item])]);
     XRing x;
-    xring_init(x, j, ring, fdst, true, true, pat);
+    xring_init(x, j, ring, fdst, true, true, pat, ct);
 #ifdef RPGPU_DSTAMPS
     const uint64_t t1 = wall_clock64();
 #endif
@@ -2306,6 +2421,9 @@ DEV void exec_linked(const DeviceJob& j, lds_u8* ring, SeqRec* buf, uint32_t ite
         }
     }
     xflush(x, x.op);
+    // the frame's whole output, one stream (its blocks are contiguous)
+    const uint32_t fcrc = ok ? crc_finish(x, j.tables, x.op) : 0u;
+    if (lane() == 0) j.blocks[first].crc = fcrc;
 #ifdef RPGPU_DSTAMPS
     if (lane() == 0) { atomicAdd(&g_dst[10], wall_clock64() - t1); atomicAdd(&g_dst[9], 1ull); }
 #endif
@@ -2313,18 +2431,22 @@ DEV void exec_linked(const DeviceJob& j, lds_u8* ring, SeqRec* buf, uint32_t ite
 
 // one independent piece
 DEV void exec_one(const DeviceJob& j, lds_u8* ring, SeqRec* buf, uint32_t p, uint32_t kind,
-                  const __attribute__((address_space(3))) uint32_t* pat) {
+                  const __attribute__((address_space(3))) uint32_t* pat, lds_cu32* ct) {
     {
         const uint64_t dst = uni64(j.blocks[p].dst);
         XRing x;
         // a piece longer than the ring wraps it: wrap-aware like a linked frame
-        xring_init(x, j, ring, dst, uni32(j.blocks[p].cap) > kXRing, false, pat);
+        xring_init(x, j, ring, dst, uni32(j.blocks[p].cap) > kXRing, false, pat, ct);
 #ifdef RPGPU_DSTAMPS
         const uint64_t e0 = wall_clock64();
 #endif
         const int32_t dd = exec_piece(x, j, p, 0, buf);
         if (dd >= 0) xflush(x, x.op);
-        if (lane() == 0) j.blocks[p].out = dd;
+        const uint32_t pcrc = dd >= 0 ? crc_finish(x, j.tables, x.op) : 0u;
+        if (lane() == 0) {
+            j.blocks[p].out = dd;
+            j.blocks[p].crc = pcrc;
+        }
 #ifdef RPGPU_DSTAMPS
         if (lane() == 0) {
             const int k = (kind & kBlkRaw) ? 4 : (kind & kBlkSnappy) ? 6 : 2;
@@ -2340,32 +2462,40 @@ DEV void exec_one(const DeviceJob& j, lds_u8* ring, SeqRec* buf, uint32_t p, uin
 // up to 64 consecutive block items (independent pieces; linked ones and the
 // long ones, run first on their own, skipped)
 DEV void exec_chunk(const DeviceJob& j, lds_u8* ring, SeqRec* buf, uint32_t base, uint32_t nblk,
-                    const __attribute__((address_space(3))) uint32_t* pat) {
+                    const __attribute__((address_space(3))) uint32_t* pat, lds_cu32* ct) {
     const uint32_t end = base + 64 < nblk ? base + 64 : nblk;
     for (uint32_t p = base; p < end; p++) {
         const uint32_t kind = uni32(j.blocks[p].kind);
         if ((kind & kBlkLinked) || piece_is_long(kind, uni32(j.blocks[p].csize), uni32(j.blocks[p].cap))) continue;
-        exec_one(j, ring, buf, p, kind, pat);
+        exec_one(j, ring, buf, p, kind, pat, ct);
     }
 }
 
 // ---------------------------------------------------------------------------
-// k_lz_exec: persistent, one wave per workgroup (64 KiB LDS ring each),
-// j.exec_waves of them; units by one agent-scope counter (counters[8]):
+// k_lz_exec: persistent, kExecWaves independent waves per workgroup (a
+// 16 KiB LDS ring each), one workgroup per CU; units by one agent-scope
+// counter (counters[8]):
 // first the linked frames, then the long pieces one unit each (a 1 MiB raw
 // snappy payload is ~1000 record batches: taken first, and alone, it no
 // longer ends the kernel behind 63 other pieces of its chunk), then the
 // block list in chunks of 64.
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(64) void k_lz_exec(DeviceJob j) {
+__global__ __launch_bounds__(64 * kExecWaves) void k_lz_exec(DeviceJob j) {
     extern __shared__ __attribute__((aligned(16))) uint8_t xlds[];
-    __shared__ uint32_t spat[128];
-    lds_u8* ring = (lds_u8*)xlds;
-    spat[threadIdx.x] = (&kPat.a[0][0])[threadIdx.x];
-    spat[64 + threadIdx.x] = (&kPat.b[0][0])[threadIdx.x];
+    const uint32_t wi = threadIdx.x >> 6;
+    lds_u8* ring = (lds_u8*)(xlds + wi * kXRing);
+    uint32_t* ct_w = (uint32_t*)(xlds + kXCrcOff);
+    uint32_t* pat_w = (uint32_t*)(xlds + kXPatOff);
+    for (uint32_t i = threadIdx.x; i < 1024u; i += blockDim.x) {
+        ct_w[i] = j.tables->braid[i >> 8][i & 255u];               // T1023, T1022, T1021, T1020
+        ct_w[1024u + i] = j.tables->hdr[3u - (i >> 8)][i & 255u];  // T3, T2, T1, T0
+    }
+    for (uint32_t i = threadIdx.x; i < 128u; i += blockDim.x)
+        pat_w[i] = i < 64u ? (&kPat.a[0][0])[i] : (&kPat.b[0][0])[i - 64u];
     __syncthreads();
-    const __attribute__((address_space(3))) uint32_t* pat = (const __attribute__((address_space(3))) uint32_t*)spat;
-    SeqRec* buf = j.seqs + (size_t)blockIdx.x * kRecsPerLane;
+    const __attribute__((address_space(3))) uint32_t* pat = (const __attribute__((address_space(3))) uint32_t*)pat_w;
+    lds_cu32* ct = (lds_cu32*)ct_w;
+    SeqRec* buf = j.seqs + ((size_t)blockIdx.x * kExecWaves + wi) * kRecsPerLane;
     const uint32_t nlink = j.counters[7];
     const uint32_t reserved = j.counters[4];
     const uint32_t nblk = reserved < j.block_capacity ? reserved : j.block_capacity;
@@ -2375,13 +2505,13 @@ __global__ __launch_bounds__(64) void k_lz_exec(DeviceJob j) {
         const uint32_t u = wave_fetch_add(&j.counters[8], 1u);
         if (u >= total) break;
         if (u < nlink) {
-            exec_linked(j, ring, buf, uni32(j.link_list[u]), pat);
+            exec_linked(j, ring, buf, uni32(j.link_list[u]), pat, ct);
         } else if (u < nlink + nlong) {
             const uint32_t p = uni32(j.long_list[u - nlink]);
             const uint32_t kind = uni32(j.blocks[p].kind);
-            if (!(kind & kBlkLinked)) exec_one(j, ring, buf, p, kind, pat);
+            if (!(kind & kBlkLinked)) exec_one(j, ring, buf, p, kind, pat, ct);
         } else {
-            exec_chunk(j, ring, buf, (u - nlink - nlong) * 64, nblk, pat);
+            exec_chunk(j, ring, buf, (u - nlink - nlong) * 64, nblk, pat, ct);
         }
     }
 }
@@ -2468,9 +2598,35 @@ __global__ __launch_bounds__(256) void k_decode_finish(DeviceJob j) {
             if (ok && uni32(j.plans[item].ccs) && xxh32_wave(j.decoded + d0, total, 0, xbuf) != uni32(j.plans[item].ccs_val))
                 ok = false;
         }
+        uint32_t dcrc = 0;
+        if (ok) {
+            // reset_size_checksum_metadata's new crc (storage/parser_utils.cc:
+            // 114-120) from the streaming CRCs k_lz_exec took of each piece:
+            // the BE40 prefix with the codec bits of attrs cleared (BE byte
+            // 1), then the pieces in order, each moved to the payload end by
+            // GF(2) shifts (a linked frame is one stream already)
+            const uint32_t codec = uni32((uint32_t)(uint16_t)R->attrs) & 7u;
+            const uint32_t S0 = uni32((uint32_t)R->reserved1) ^ j.tables->hdr[38][codec] ^ j.tables->c40;
+            uint32_t acc = 0;
+            if (uni32(j.blocks[first].kind) & kBlkLinked) {
+                if (l == 0) acc = j.blocks[first].crc;
+            } else {
+                uint64_t carry = 0;
+                for (uint32_t b0 = 0; b0 < nb; b0 += 64) {
+                    const uint32_t k = b0 + l;
+                    const uint32_t o = k < nb ? (uint32_t)j.blocks[first + k].out : 0u;
+                    const uint32_t incl = wave_scan(o);
+                    if (k < nb) acc ^= crc_shift(j.blocks[first + k].crc, total - (carry + incl));
+                    carry += rl(incl, 63);
+                }
+            }
+            dcrc = ~(crc_shift(S0, total) ^ wave_xor(acc));
+        }
         if (ok && l == 0) {
             R->flags = R->flags | RPGPU_F_CODEC_OK;
             R->decoded_len = (uint32_t)total;
+            R->decoded_crc = dcrc;
+            R->reserved0 = 1;  // decoded crc done (k_validate_decoded skips its CRC pass)
         }
     }
 }
@@ -2523,7 +2679,7 @@ __global__ void k_init_dstamps() {
 }
 #endif
 
-uint32_t lz_exec_wgs_per_cu() { return (160u * 1024u) / kXRing; }
+uint32_t lz_exec_wgs_per_cu() { return kExecWaves; }
 
 hipError_t launch_decode(const DeviceJob& j, hipStream_t s, uint32_t grid) {
     hipLaunchKernelGGL(k_decode, dim3(grid), dim3(256), 0, s, j);
@@ -2546,11 +2702,11 @@ hipError_t launch_lz_walk(const DeviceJob& j, hipStream_t s, uint32_t grid) {
 hipError_t launch_lz_exec(const DeviceJob& j, hipStream_t s) {
     static bool attr = false;
     if (!attr) {
-        (void)hipFuncSetAttribute((const void*)k_lz_exec, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kXRing);
+        (void)hipFuncSetAttribute((const void*)k_lz_exec, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kXLds);
         attr = true;
     }
     if (!j.exec_waves) return hipSuccess;
-    hipLaunchKernelGGL(k_lz_exec, dim3(j.exec_waves), dim3(64), kXRing, s, j);
+    hipLaunchKernelGGL(k_lz_exec, dim3(j.exec_waves / kExecWaves), dim3(64 * kExecWaves), kXLds, s, j);
 #ifdef RPGPU_DSTAMPS
     hipLaunchKernelGGL(k_print_dstamps, dim3(1), dim3(1), 0, s);
 #endif

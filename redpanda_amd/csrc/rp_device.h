@@ -386,6 +386,39 @@ HD uint64_t decode_capacity_raw(int codec, const uint8_t* s, uint64_t n) {
 }
 
 
+// ---------------------------------------------------------------------------
+// GF(2) arithmetic modulo the reflected CRC32C polynomial (zlib's multmodp /
+// x2nmodp scheme; bit 31 is x^0): merging partial CRCs (k_crc_combine) and
+// the pieces of a decoded payload (k_decode_finish).  x has order 2^31 - 1
+// modulo this polynomial, so x^(2^k) repeats with period 31.
+// ---------------------------------------------------------------------------
+static __constant__ uint32_t kX2n[31] = {
+    0x40000000u, 0x20000000u, 0x08000000u, 0x00800000u, 0x00008000u, 0x82F63B78u, 0x6EA2D55Cu, 0x18B8EA18u,
+    0x510AC59Au, 0xB82BE955u, 0xB8FDB1E7u, 0x88E56F72u, 0x74C360A4u, 0xE4172B16u, 0x0D65762Au, 0x35D73A62u,
+    0x28461564u, 0xBF455269u, 0xE2EA32DCu, 0xFE7740E6u, 0xF946610Bu, 0x3C204F8Fu, 0x538586E3u, 0x59726915u,
+    0x734D5309u, 0xBC1AC763u, 0x7D0722CCu, 0xD289CABEu, 0xE94CA9BCu, 0x05B74F3Fu, 0xA51E1F42u};
+
+// a * b mod P (a != 0)
+DEV uint32_t multmodp(uint32_t a, uint32_t b) {
+    uint32_t m = 1u << 31, p = 0;
+    for (;;) {
+        if (a & m) {
+            p ^= b;
+            if ((a & (m - 1)) == 0) break;
+        }
+        m >>= 1;
+        b = (b & 1) ? (b >> 1) ^ kCrcPoly : b >> 1;
+    }
+    return p;
+}
+// the raw state s advanced over n zero bytes: x^(8 n) * s mod P
+DEV uint32_t crc_shift(uint32_t s, uint64_t n) {
+    uint32_t p = 1u << 31;  // x^0
+    for (uint32_t k = 3; n; n >>= 1, k = (k == 30u) ? 0u : k + 1u)
+        if (n & 1) p = multmodp(kX2n[k], p);
+    return multmodp(p, s);
+}
+
 // Wave-uniform atomic fetch-add of `v` (lane 0's contribution; the other
 // lanes add 0).  Every lane executes the atomic: written as
 // `if (lane() == 0) x = atomicAdd(..)` followed by readfirstlane, the

@@ -48,6 +48,12 @@ struct Tables {
     uint32_t c57;                    // state 0xFFFFFFFF advanced over 57 zero bytes
     uint32_t c40;                    // state 0xFFFFFFFF advanced over 40 zero bytes
     uint32_t pad[2];
+    // streaming CRC of decoded output (k_lz_exec): lane l's 16-byte state
+    // moved to its 1 KiB row end, x^(8 * 16 (63 - l)); and the inverse
+    // shifts x^(-8 z) (z = 0..1023) that take a zero-padded last row back to
+    // the true end
+    uint32_t lane_rowend[64];
+    uint32_t inv_shift[1024];
 };
 
 // Discovery record per chunk (speculative walk), 32 bytes.
@@ -77,6 +83,9 @@ struct BlockItem {
     uint32_t kind;   // kBlk* bits
     int32_t out;     // decoded bytes, -1 on failure (written by k_lz_exec)
     uint32_t cap;    // bytes reserved at dst (LZ4: the block maximum = the decoder's output bound)
+    uint32_t crc;    // linear CRC32C (zero state, no final xor) of the decoded bytes, from k_lz_exec's
+                     // flush; a linked frame's whole output on its first block
+    uint32_t pad;
 };
 // kBlkWhole: a raw (non-xerial) snappy payload, snappy_standard_compressor
 // semantics (length 0 is an empty result whatever follows)
@@ -93,8 +102,8 @@ struct SeqRec {
 // one pool (bump counter); slab_next chains a piece's slabs
 constexpr uint32_t kSlabRecs = 512;
 constexpr uint32_t kRecsPerLane = 256;                // k_lz_exec's own walk (pool exhausted): records per pass
-// k_lz_exec workgroups (one wave, one LDS ring each) resident per CU, as
-// compiled into rp_codec.hip (its ring size decides it)
+// k_lz_exec waves (one LDS ring each) per CU: one workgroup of that many
+// waves per CU, as compiled into rp_codec.hip (its ring size decides it)
 uint32_t lz_exec_wgs_per_cu();
 
 // A piece's walk result (k_lz_walk -> k_lz_exec)
@@ -158,7 +167,7 @@ struct DeviceJob {
     uint32_t split_capacity;
     uint64_t split_min;           // payloads this large are split: max(kSplitMin, 2 x the job's bytes per k_validate wave)
     SeqRec* seqs;                 // k_lz_exec's own walks: kRecsPerLane per resident wave
-    uint32_t exec_waves;          // k_lz_exec grid (one wave per workgroup; sizes `seqs`)
+    uint32_t exec_waves;          // k_lz_exec waves (lz_exec_wgs_per_cu() per workgroup; sizes `seqs`)
     PieceState* pstate;           // block_capacity: walk results
     SeqRec* pool;                 // record slabs
     uint32_t* slab_next;          // pool_slabs: next slab of the same piece

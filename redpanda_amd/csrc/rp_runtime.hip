@@ -68,6 +68,19 @@ static void build_tables(Tables* T) {
     for (int z = 40; z < 57; z++) c = raw_step_zero(c, t0);
     T->c57 = c;
     T->pad[0] = T->pad[1] = 0;
+    // x^(8 * 16 k) (reflected, bit 31 = x^0): mulx multiplies by x
+    auto mulx = [](uint32_t a) { return (a & 1u) ? (a >> 1) ^ kCrcPoly : a >> 1; };
+    auto invx = [](uint32_t a) { return (a & 0x80000000u) ? ((a ^ kCrcPoly) << 1) | 1u : a << 1; };
+    uint32_t e = 0x80000000u;
+    for (uint32_t k = 0; k < 64; k++) {
+        T->lane_rowend[63 - k] = e;
+        for (int b = 0; b < 128; b++) e = mulx(e);
+    }
+    e = 0x80000000u;
+    for (uint32_t z = 0; z < 1024; z++) {
+        T->inv_shift[z] = e;
+        for (int b = 0; b < 8; b++) e = invx(e);
+    }
 }
 
 // the combine tables take ~2^13 * 1024 zero-steps; build them once per process

@@ -1324,34 +1324,6 @@ __global__ __launch_bounds__(1024) void k_crc_split(DeviceJob j) {
     }
 }
 
-// x^(2^k) mod P, reflected CRC32C (k = 0..31)
-__constant__ uint32_t kX2n[32] = {
-    0x40000000u, 0x20000000u, 0x08000000u, 0x00800000u, 0x00008000u, 0x82F63B78u, 0x6EA2D55Cu, 0x18B8EA18u,
-    0x510AC59Au, 0xB82BE955u, 0xB8FDB1E7u, 0x88E56F72u, 0x74C360A4u, 0xE4172B16u, 0x0D65762Au, 0x35D73A62u,
-    0x28461564u, 0xBF455269u, 0xE2EA32DCu, 0xFE7740E6u, 0xF946610Bu, 0x3C204F8Fu, 0x538586E3u, 0x59726915u,
-    0x734D5309u, 0xBC1AC763u, 0x7D0722CCu, 0xD289CABEu, 0xE94CA9BCu, 0x05B74F3Fu, 0xA51E1F42u, 0x40000000u};
-
-// a * b mod P (reflected; a != 0)
-DEV uint32_t multmodp(uint32_t a, uint32_t b) {
-    uint32_t m = 1u << 31, p = 0;
-    for (;;) {
-        if (a & m) {
-            p ^= b;
-            if ((a & (m - 1)) == 0) break;
-        }
-        m >>= 1;
-        b = (b & 1) ? (b >> 1) ^ 0x82F63B78u : b >> 1;
-    }
-    return p;
-}
-// the state s advanced over n zero bytes: x^(8 n) * s mod P
-DEV uint32_t crc_shift(uint32_t s, uint64_t n) {
-    uint32_t p = 1u << 31;  // x^0
-    for (uint32_t k = 3; n; n >>= 1, k++)
-        if (n & 1) p = multmodp(kX2n[k & 31], p);
-    return multmodp(p, s);
-}
-
 // one wave per listed payload: lanes 0..15 shift the chunk CRCs, lane 16 the
 // prefix state, an xor over the wave merges them; then the verdict
 __global__ __launch_bounds__(256) void k_crc_combine(DeviceJob j) {
@@ -1401,11 +1373,19 @@ __global__ __launch_bounds__(1024) void k_validate_decoded(DeviceJob j) {
         // slot; the header sits at file_pos in its segment
         const uint64_t hdr = uni64(R->file_pos) + uni64(j.seg_off[d.seg]);
         const uint64_t dl = d.dlen;
-        const Stream ds = make_stream(j.decoded, d.doff, d.doff + dl);
-        Win dv;
-        load_window(ds, 0, dv);
-        const uint4 dgt = load_tail(ds);
-        const uint32_t dcrc = ~crc_stream(lds, K, ds, dv, dgt, d.praw ^ T->hdr[38][d.codec] ^ c40);
+        // block-parallel frames: k_decode_finish merged the streaming CRCs
+        // of k_lz_exec's flushes (reserved0 = 1); frames decoded whole (the
+        // sequential list) are read back here
+        uint32_t dcrc;
+        if (uni32((uint32_t)R->reserved0) == 1u) {
+            dcrc = uni32(R->decoded_crc);
+        } else {
+            const Stream ds = make_stream(j.decoded, d.doff, d.doff + dl);
+            Win dv;
+            load_window(ds, 0, dv);
+            const uint4 dgt = load_tail(ds);
+            dcrc = ~crc_stream(lds, K, ds, dv, dgt, d.praw ^ T->hdr[38][d.codec] ^ c40);
+        }
         const uint32_t dhcrc = decoded_header_crc(T, j.data + hdr, (uint32_t)(RPGPU_HEADER_SIZE + dl), dcrc,
                                                   j.layout == RPGPU_LAYOUT_WIRE);
         uint32_t f = d.flags, perr = 0, parsed = 0;
@@ -1423,6 +1403,7 @@ __global__ __launch_bounds__(1024) void k_validate_decoded(DeviceJob j) {
             R->parse_err = (uint8_t)perr;
             R->decoded_crc = dcrc;
             R->decoded_header_crc = dhcrc;
+            R->reserved0 = 0;
             R->reserved1 = 0;
         }
     }
