@@ -823,11 +823,384 @@ int rpo_snappy_java_uncompress(const uint8_t* s, size_t n, uint8_t* dst, size_t 
     return 0;
 }
 
+/* ======================================================================== */
+/* gzip: zlib 1.2.11 inflate as gzip_compressor::uncompress drives it         */
+/* ======================================================================== */
+/* The reference (compression/internal/gzip_compressor.cc:161-230) runs
+ * inflateInit2(15 + 32) twice over the whole payload: a sizing pass through a
+ * 512-byte buffer (buffer_for_input: total_out), then the real pass into a
+ * buffer of exactly that size.  Its loop only throws on Z_STREAM_ERROR /
+ * Z_NEED_DICT / Z_DATA_ERROR / Z_MEM_ERROR, so:
+ *   - an error anywhere before the end of the first member throws;
+ *   - a stream that runs out of input is NOT an error: the output is every
+ *     symbol zlib could decode from the bytes present (a literal as soon as
+ *     its code is complete, a match once its length, distance and extra bits
+ *     are), stored blocks byte by byte;
+ *   - bytes after the first member are ignored.
+ * The state machine below follows zlib's inflate() (inflate.c HEAD ..
+ * DONE) and inflate_table()'s acceptance rules (over-subscribed codes are
+ * errors, incomplete ones only allowed for a single 1-bit literal/length or
+ * distance code; an all-zero code-length code decodes 1 bit per symbol as
+ * length 0, zlib's "wait for decoding to report error" table).  Bits are
+ * pulled one byte at a time exactly when zlib's NEEDBITS / PULLBYTE would,
+ * so truncation is detected at the same symbol.  gz_header fields are not
+ * kept (the reference passes an uninitialised gz_header to inflateGetHeader;
+ * the name / extra / comment copies it would make are undefined there and
+ * have no effect on the output here). */
+typedef struct {
+    const uint8_t* s;
+    size_t n, pos;     /* input and bytes pulled */
+    uint64_t hold;
+    unsigned bits;
+} rpo_zbits;
+
+static int zb_need(rpo_zbits* b, unsigned k) {
+    while (b->bits < k) {
+        if (b->pos >= b->n) return 0;
+        b->hold |= (uint64_t)b->s[b->pos++] << b->bits;
+        b->bits += 8;
+    }
+    return 1;
+}
+static unsigned zb_peek(const rpo_zbits* b, unsigned k) { return (unsigned)(b->hold & ((1ull << k) - 1)); }
+static void zb_drop(rpo_zbits* b, unsigned k) { b->hold >>= k; b->bits -= k; }
+
+static uint32_t g_crc32_table[256];
+static void crc32_ieee_init(void) {
+    if (g_crc32_table[1]) return;
+    for (uint32_t i = 0; i < 256; i++) {
+        uint32_t c = i;
+        for (int k = 0; k < 8; k++) c = (c & 1) ? (c >> 1) ^ 0xEDB88320u : c >> 1;
+        g_crc32_table[i] = c;
+    }
+}
+/* zlib crc32(crc, p, n) */
+static uint32_t crc32_ieee(uint32_t crc, const uint8_t* p, size_t n) {
+    crc32_ieee_init();
+    crc = ~crc;
+    for (size_t i = 0; i < n; i++) crc = g_crc32_table[(crc ^ p[i]) & 0xFF] ^ (crc >> 8);
+    return ~crc;
+}
+/* zlib adler32(adler, p, n) */
+static uint32_t adler32_z(uint32_t adler, const uint8_t* p, size_t n) {
+    uint32_t a = adler & 0xFFFF, b = adler >> 16;
+    for (size_t i = 0; i < n; i++) {
+        a = (a + p[i]) % 65521u;
+        b = (b + a) % 65521u;
+    }
+    return (b << 16) | a;
+}
+
+/* canonical Huffman code (deflate's bit-reversed packing) */
+typedef struct {
+    uint16_t count[16];   /* codes per length */
+    uint16_t sym[320];    /* symbols ordered by (length, value) */
+    int empty;            /* no codes at all (zlib's max == 0 table) */
+} rpo_huff;
+
+/* inflate_table acceptance (zlib 1.2.11 inftrees.c): 0 ok, -1 error.
+ * type: 0 CODES, 1 LENS, 2 DISTS */
+static int huff_build(rpo_huff* h, const uint16_t* lens, unsigned n, int type) {
+    memset(h->count, 0, sizeof h->count);
+    for (unsigned i = 0; i < n; i++) h->count[lens[i]]++;
+    unsigned max = 15;
+    while (max >= 1 && h->count[max] == 0) max--;
+    h->empty = max == 0;
+    if (max == 0) return 0;
+    int left = 1;
+    for (unsigned len = 1; len <= 15; len++) {
+        left <<= 1;
+        left -= h->count[len];
+        if (left < 0) return -1;             /* over-subscribed */
+    }
+    if (left > 0 && (type == 0 || max != 1)) return -1;  /* incomplete */
+    uint16_t offs[16];
+    offs[1] = 0;
+    for (unsigned len = 1; len < 15; len++) offs[len + 1] = offs[len] + h->count[len];
+    for (unsigned i = 0; i < n; i++)
+        if (lens[i]) h->sym[offs[lens[i]]++] = (uint16_t)i;
+    return 0;
+}
+
+/* Decode one symbol: 1 decoded (*sym, bits dropped), 0 needs more input,
+ * -1 an invalid code (bits dropped).  zlib looks codes up with the bits it
+ * holds (missing ones read as zero) and pulls a byte whenever the entry
+ * found needs more bits than it holds; that is: the shortest code matching
+ * the zero-extended bits decodes once all its bits are present. */
+static int huff_decode(const rpo_huff* h, rpo_zbits* b, unsigned* sym) {
+    for (;;) {
+        if (h->empty) {  /* zlib's table for no codes: op 64, bits 1 */
+            if (!zb_need(b, 1)) return 0;
+            zb_drop(b, 1);
+            *sym = 0;
+            return -1;
+        }
+        /* canonical decode over the bits held */
+        int code = 0, first = 0, index = 0;
+        unsigned len;
+        for (len = 1; len <= 15; len++) {
+            code |= (len <= b->bits) ? (int)((b->hold >> (len - 1)) & 1) : 0;
+            int count = h->count[len];
+            if (code - count < first) {
+                if (len > b->bits) break;  /* the code needs bits not held yet */
+                *sym = h->sym[index + (code - first)];
+                zb_drop(b, len);
+                return 1;
+            }
+            index += count;
+            first += count;
+            first <<= 1;
+            code <<= 1;
+        }
+        if (len > 15) {
+            /* no code matches: only possible for an incomplete single 1-bit
+             * code (zlib fills the hole with op 64, bits 1) */
+            if (b->bits < 1 && !zb_need(b, 1)) return 0;
+            zb_drop(b, 1);
+            return -1;
+        }
+        if (b->pos >= b->n) return 0;
+        b->hold |= (uint64_t)b->s[b->pos++] << b->bits;
+        b->bits += 8;
+    }
+}
+
+static const uint16_t k_len_base[29] = {3, 4, 5, 6, 7, 8, 9, 10, 11, 13, 15, 17, 19, 23, 27, 31,
+                                        35, 43, 51, 59, 67, 83, 99, 115, 131, 163, 195, 227, 258};
+static const uint8_t k_len_extra[29] = {0, 0, 0, 0, 0, 0, 0, 0, 1, 1, 1, 1, 2, 2, 2, 2,
+                                        3, 3, 3, 3, 4, 4, 4, 4, 5, 5, 5, 5, 0};
+static const uint16_t k_dist_base[30] = {1, 2, 3, 4, 5, 7, 9, 13, 17, 25, 33, 49, 65, 97, 129,
+                                         193, 257, 385, 513, 769, 1025, 1537, 2049, 3073, 4097,
+                                         6145, 8193, 12289, 16385, 24577};
+static const uint8_t k_dist_extra[30] = {0, 0, 0, 0, 1, 1, 2, 2, 3, 3, 4, 4, 5, 5, 6,
+                                         6, 7, 7, 8, 8, 9, 9, 10, 10, 11, 11, 12, 12, 13, 13};
+static const uint8_t k_clen_order[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12, 3, 13, 2, 14, 1, 15};
+
+/* emit a byte (counted always, stored while it fits) */
+#define ZOUT(byte)                                   \
+    do {                                             \
+        const uint8_t zb_ = (uint8_t)(byte);         \
+        if (total < cap) dst[total] = zb_;           \
+        total++;                                     \
+    } while (0)
+
+
+int rpo_gzip_uncompress(const uint8_t* src, size_t n, uint8_t* dst, size_t cap, size_t* out_len) {
+    rpo_zbits b = {src, n, 0, 0, 0};
+    size_t total = 0;
+    int err = 0, gz = 0;
+    unsigned flags = 0;
+    uint32_t hcheck = 0;
+    rpo_huff lencode, distcode, codecode;
+    rpo_huff* L = &lencode; rpo_huff* D = &distcode; rpo_huff* C = &codecode;
+    *out_len = 0;
+    /* HEAD */
+    if (!zb_need(&b, 16)) goto done;
+    if ((b.hold & 0xFFFF) == 0x8b1f) {
+        gz = 1;
+        hcheck = crc32_ieee(0, src, 2);
+        zb_drop(&b, 16);
+        /* FLAGS */
+        if (!zb_need(&b, 16)) goto done;
+        flags = (unsigned)(b.hold & 0xFFFF);
+        if ((flags & 0xff) != 8) { err = 1; goto done; }     /* unknown compression method */
+        if (flags & 0xe000) { err = 1; goto done; }           /* unknown header flags set */
+        if (flags & 0x0200) hcheck = crc32_ieee(hcheck, src + b.pos - 2, 2);
+        zb_drop(&b, 16);
+        /* TIME, OS */
+        if (!zb_need(&b, 32)) goto done;
+        if (flags & 0x0200) hcheck = crc32_ieee(hcheck, src + b.pos - 4, 4);
+        zb_drop(&b, 32);
+        if (!zb_need(&b, 16)) goto done;
+        if (flags & 0x0200) hcheck = crc32_ieee(hcheck, src + b.pos - 2, 2);
+        zb_drop(&b, 16);
+        if (flags & 0x0400) {  /* EXLEN, EXTRA */
+            if (!zb_need(&b, 16)) goto done;
+            size_t xlen = (size_t)(b.hold & 0xFFFF);
+            if (flags & 0x0200) hcheck = crc32_ieee(hcheck, src + b.pos - 2, 2);
+            zb_drop(&b, 16);
+            size_t have = n - b.pos, copy = xlen < have ? xlen : have;
+            if (flags & 0x0200) hcheck = crc32_ieee(hcheck, src + b.pos, copy);
+            b.pos += copy;
+            if (copy < xlen) goto done;
+        }
+        for (unsigned f = 0x0800; f <= 0x1000; f <<= 1) {  /* NAME, COMMENT */
+            if (!(flags & f)) continue;
+            if (b.pos >= n) goto done;
+            size_t start = b.pos;
+            uint8_t c;
+            do c = src[b.pos++]; while (c && b.pos < n);
+            if (flags & 0x0200) hcheck = crc32_ieee(hcheck, src + start, b.pos - start);
+            if (c) goto done;
+        }
+        if (flags & 0x0200) {  /* HCRC */
+            if (!zb_need(&b, 16)) goto done;
+            if ((b.hold & 0xFFFF) != (hcheck & 0xFFFF)) { err = 1; goto done; }  /* header crc mismatch */
+            zb_drop(&b, 16);
+        }
+    } else {
+        /* zlib wrapper */
+        const unsigned hold = (unsigned)(b.hold & 0xFFFF);
+        if ((((hold & 0xFF) << 8) + (hold >> 8)) % 31) { err = 1; goto done; }  /* incorrect header check */
+        if ((hold & 0x0F) != 8) { err = 1; goto done; }                          /* unknown compression method */
+        if (((hold >> 4) & 0x0F) + 8 > 15) { err = 1; goto done; }              /* invalid window size */
+        zb_drop(&b, 16);
+        if (hold & 0x2000) {  /* FDICT: DICTID then Z_NEED_DICT */
+            if (!zb_need(&b, 32)) goto done;
+            err = 1;
+            goto done;
+        }
+    }
+    /* blocks */
+    for (;;) {
+        if (!zb_need(&b, 3)) goto done;
+        const unsigned last = zb_peek(&b, 1);
+        const unsigned type = (unsigned)((b.hold >> 1) & 3);
+        zb_drop(&b, 3);
+        if (type == 0) {  /* STORED */
+            zb_drop(&b, b.bits & 7);
+            if (!zb_need(&b, 32)) goto done;
+            if ((b.hold & 0xFFFF) != (((b.hold >> 16) & 0xFFFF) ^ 0xFFFF)) { err = 1; goto done; }
+            size_t length = (size_t)(b.hold & 0xFFFF);
+            zb_drop(&b, 32);  /* INITBITS: the hold is empty (whole bytes were pulled exactly) */
+            while (length) {
+                if (b.pos >= n) goto done;
+                ZOUT(src[b.pos++]);
+                length--;
+            }
+        } else if (type == 3) {
+            err = 1;  /* invalid block type */
+            goto done;
+        } else {
+            if (type == 1) {  /* fixed codes */
+                uint16_t lens[320];
+                unsigned i = 0;
+                for (; i < 144; i++) lens[i] = 8;
+                for (; i < 256; i++) lens[i] = 9;
+                for (; i < 280; i++) lens[i] = 7;
+                for (; i < 288; i++) lens[i] = 8;
+                huff_build(L, lens, 288, 1);
+                for (i = 0; i < 32; i++) lens[i] = 5;
+                huff_build(D, lens, 32, 2);
+            } else {  /* TABLE */
+                if (!zb_need(&b, 14)) goto done;
+                const unsigned nlen = zb_peek(&b, 5) + 257;
+                zb_drop(&b, 5);
+                const unsigned ndist = zb_peek(&b, 5) + 1;
+                zb_drop(&b, 5);
+                const unsigned ncode = zb_peek(&b, 4) + 4;
+                zb_drop(&b, 4);
+                if (nlen > 286 || ndist > 30) { err = 1; goto done; }  /* too many length or distance symbols */
+                uint16_t lens[320];
+                unsigned have = 0;
+                while (have < ncode) {
+                    if (!zb_need(&b, 3)) goto done;
+                    lens[k_clen_order[have++]] = (uint16_t)zb_peek(&b, 3);
+                    zb_drop(&b, 3);
+                }
+                while (have < 19) lens[k_clen_order[have++]] = 0;
+                if (huff_build(C, lens, 19, 0)) { err = 1; goto done; }  /* invalid code lengths set */
+                have = 0;
+                while (have < nlen + ndist) {
+                    unsigned sym;
+                    int r = huff_decode(C, &b, &sym);
+                    if (r == 0) goto done;
+                    if (r < 0) sym = 0;  /* zlib's CODELENS does not check op: an invalid entry is length 0 */
+                    if (sym < 16) {
+                        lens[have++] = (uint16_t)sym;
+                        continue;
+                    }
+                    /* the code's bits are already dropped; zlib needs code + extra bits
+                     * together (NEEDBITS(here.bits + k)) before dropping the code: the
+                     * same truncation point, since the code bits were present */
+                    unsigned len = 0, copy;
+                    if (sym == 16) {
+                        if (!zb_need(&b, 2)) goto done;
+                        if (have == 0) { err = 1; goto done; }  /* invalid bit length repeat */
+                        len = lens[have - 1];
+                        copy = 3 + zb_peek(&b, 2);
+                        zb_drop(&b, 2);
+                    } else if (sym == 17) {
+                        if (!zb_need(&b, 3)) goto done;
+                        copy = 3 + zb_peek(&b, 3);
+                        zb_drop(&b, 3);
+                    } else {
+                        if (!zb_need(&b, 7)) goto done;
+                        copy = 11 + zb_peek(&b, 7);
+                        zb_drop(&b, 7);
+                    }
+                    if (have + copy > nlen + ndist) { err = 1; goto done; }  /* invalid bit length repeat */
+                    while (copy--) lens[have++] = (uint16_t)len;
+                }
+                if (lens[256] == 0) { err = 1; goto done; }  /* invalid code -- missing end-of-block */
+                if (huff_build(L, lens, nlen, 1)) { err = 1; goto done; }       /* invalid literal/lengths set */
+                if (huff_build(D, lens + nlen, ndist, 2)) { err = 1; goto done; } /* invalid distances set */
+            }
+            /* LEN .. MATCH */
+            for (;;) {
+                unsigned sym;
+                int r = huff_decode(L, &b, &sym);
+                if (r == 0) goto done;
+                if (r < 0 || sym > 285) { err = 1; goto done; }  /* invalid literal/length code */
+                if (sym < 256) { ZOUT(sym); continue; }
+                if (sym == 256) break;
+                sym -= 257;
+                unsigned length = k_len_base[sym];
+                if (k_len_extra[sym]) {
+                    if (!zb_need(&b, k_len_extra[sym])) goto done;
+                    length += zb_peek(&b, k_len_extra[sym]);
+                    zb_drop(&b, k_len_extra[sym]);
+                }
+                r = huff_decode(D, &b, &sym);
+                if (r == 0) goto done;
+                if (r < 0 || sym > 29) { err = 1; goto done; }  /* invalid distance code */
+                unsigned dist = k_dist_base[sym];
+                if (k_dist_extra[sym]) {
+                    if (!zb_need(&b, k_dist_extra[sym])) goto done;
+                    dist += zb_peek(&b, k_dist_extra[sym]);
+                    zb_drop(&b, k_dist_extra[sym]);
+                }
+                if (dist > total) { err = 1; goto done; }  /* invalid distance too far back */
+                for (unsigned k = 0; k < length; k++) {
+                    const size_t from = total - dist;
+                    ZOUT(from < cap ? dst[from] : 0);
+                }
+            }
+        }
+        if (last) break;
+    }
+    /* CHECK, LENGTH */
+    zb_drop(&b, b.bits & 7);
+    if (!zb_need(&b, 32)) goto done;
+    {
+        const uint32_t w = (uint32_t)(b.hold & 0xFFFFFFFFu);
+        if (gz) {
+            if (total <= cap && w != crc32_ieee(0, dst, total)) { err = 1; goto done; }   /* incorrect data check */
+        } else {
+            const uint32_t be = (w >> 24) | ((w >> 8) & 0xFF00u) | ((w << 8) & 0xFF0000u) | (w << 24);
+            if (total <= cap && be != adler32_z(1, dst, total)) { err = 1; goto done; }
+        }
+        if (total > cap) err = 2;  /* the check needs the bytes: the caller resizes and retries */
+        zb_drop(&b, 32);
+    }
+    if (gz && err == 0) {
+        if (!zb_need(&b, 32)) goto done;
+        if ((uint32_t)(b.hold & 0xFFFFFFFFu) != (uint32_t)total) { err = 1; goto done; }  /* incorrect length check */
+    }
+done:
+    *out_len = total;
+    if (err == 1) { *out_len = 0; return -1; }
+    if (total > cap) return -2;
+    return 0;
+}
+#undef ZOUT
+
 int rpo_uncompress(int codec, const uint8_t* s, size_t n, uint8_t* dst, size_t cap, size_t* out_len) {
     /* compression/compression.cc:34-55 */
     *out_len = 0;
     if (n == 0) return -1;
     switch (codec) {
+    case RPGPU_CODEC_GZIP: return rpo_gzip_uncompress(s, n, dst, cap, out_len);
     case RPGPU_CODEC_SNAPPY: return rpo_snappy_java_uncompress(s, n, dst, cap, out_len);
     case RPGPU_CODEC_LZ4: return rpo_lz4f_uncompress(s, n, dst, cap, out_len);
     default: return -1;

@@ -89,6 +89,14 @@ int rpo_lz4f_uncompress(const uint8_t* src, size_t n, uint8_t* dst, size_t cap, 
 int rpo_snappy_raw_uncompress(const uint8_t* src, size_t n, uint8_t* dst, size_t cap, size_t* out_len);
 int rpo_snappy_java_uncompress(const uint8_t* src, size_t n, uint8_t* dst, size_t cap, size_t* out_len);
 int rpo_uncompress(int codec, const uint8_t* src, size_t n, uint8_t* dst, size_t cap, size_t* out_len);
+/* gzip_compressor::uncompress (compression/internal/gzip_compressor.cc:
+ * 161-230) over zlib 1.2.11 inflate (inflateInit2(15 + 32): gzip or zlib
+ * wrapper): a restatement of zlib's inflate state machine.  *out_len = the
+ * bytes the stream yields (the reference's sizing pass: everything decoded
+ * before the end of the first member, an error, or the end of the input);
+ * at most cap of them are written.  0 ok, -1 where the reference throws
+ * (Z_DATA_ERROR / Z_NEED_DICT), -2 when cap is too small. */
+int rpo_gzip_uncompress(const uint8_t* src, size_t n, uint8_t* dst, size_t cap, size_t* out_len);
 /* LZ4 block (lz4 1.9.3 LZ4_decompress_safe_usingDict): history = bytes
  * immediately before dst that matches may reference (0 for independent). */
 int rpo_lz4_block_decode(const uint8_t* src, size_t n, uint8_t* dst, size_t dst_cap,

@@ -79,9 +79,14 @@ struct GzDec {
     ~GzDec() {
         if (init) z->inflateEnd(&s);
     }
-    // reset(): inflateInit2(15 + 32) then inflateGetHeader; false = throw
+    // reset(): inflateInit2(15 + 32) then inflateGetHeader; false = throw.
+    // The header struct is zeroed: the reference hands zlib an uninitialised
+    // gz_header, whose extra / name / comment pointers zlib then writes
+    // through for FEXTRA / FNAME / FCOMMENT members (undefined behaviour
+    // there; with null pointers zlib skips the copies, output unchanged)
     bool reset(const uint8_t* src, size_t n) {
         memset(&s, 0, sizeof(s));
+        memset(&hdr, 0, sizeof(hdr));
         s.zalloc = Z_NULL;
         s.zfree = Z_NULL;
         s.opaque = Z_NULL;
