@@ -681,27 +681,34 @@ struct index_state {
         return out;
     }
 
-    // index_state::hydrate_from_buffer (storage/index_state.cc:95-186): nullopt
+    // index_state::hydrate_from_buffer (storage/index_state.cc:104-186): nullopt
     // on an unknown version, a size mismatch or a bad checksum (the reference
-    // then rebuilds the index from the log)
+    // then rebuilds the index from the log); a read past the buffer throws
+    // std::out_of_range, as the reference's iobuf_parser does
+    // (bytes/details/io_iterator_consumer.h:64-84)
     static std::optional<index_state> hydrate_from_buffer(const uint8_t* p, size_t n) {
         size_t at = 0;
         auto take = [&](auto& v) {
-            if (n - at < sizeof(v)) return false;
+            if (n - at < sizeof(v)) throw std::out_of_range("index_state: short read");
             std::memcpy(&v, p + at, sizeof(v));
             at += sizeof(v);
-            return true;
         };
         int8_t version;
         uint32_t size, vsize;
         uint64_t checksum;
         index_state r;
-        if (!take(version) || version != ondisk_version) return std::nullopt;
-        if (!take(size) || n - at != size) return std::nullopt;
-        if (!take(checksum) || !take(r.bitflags) || !take(r.base_offset) || !take(r.max_offset) ||
-            !take(r.base_timestamp) || !take(r.max_timestamp) || !take(vsize))
-            return std::nullopt;
-        if ((n - at) / 16 < vsize) return std::nullopt;  // the reference's parser throws on a short read
+        take(version);
+        if (version != ondisk_version) return std::nullopt;
+        take(size);
+        if (n - at != size) return std::nullopt;
+        take(checksum);
+        take(r.bitflags);
+        take(r.base_offset);
+        take(r.max_offset);
+        take(r.base_timestamp);
+        take(r.max_timestamp);
+        take(vsize);
+        if ((n - at) / 16 < vsize) throw std::out_of_range("index_state: short read");
         r.relative_offset_index.resize(vsize);
         r.relative_time_index.resize(vsize);
         r.position_index.resize(vsize);

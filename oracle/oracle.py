@@ -87,6 +87,8 @@ def lib():
         L.rpo_snappy_java_compress.restype = C.c_size_t
         L.rpo_snappy_java_compress.argtypes = [C.c_void_p, C.c_size_t, C.c_size_t, C.c_void_p]
         L.rpo_segment_index.restype = C.c_int
+        L.rpo_serialize_wire.restype = C.c_uint64
+        L.rpo_serialize_wire.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64, C.c_uint64, C.c_void_p]
         L.rpo_segment_index.argtypes = [C.c_void_p, C.c_uint64, C.c_void_p, C.c_uint32, C.c_uint64,
                                         C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]
         _lib = L
@@ -288,6 +290,20 @@ def baseline_decode(seg: np.ndarray, positions, threads: int):
     secs = R.ref_baseline_decode(seg.ctypes.data_as(C.c_void_p), pos.ctypes.data_as(C.c_void_p), pos.size, threads,
                                  C.byref(s), C.byref(d))
     return secs, s.value, d.value
+
+
+def serialize_wire(data: np.ndarray, seg_offsets, batches: np.ndarray, first: int = 0, n: int = None) -> bytes:
+    """kafka::writer_serialize_batch (kafka/protocol/response_writer.h:241-276)
+    over batches [first, first + n) of a job's results."""
+    data = np.ascontiguousarray(data, dtype=np.uint8)
+    offs = np.ascontiguousarray(np.asarray(seg_offsets, dtype=np.uint64))
+    b = np.ascontiguousarray(batches, dtype=abi.BATCH_RESULT)
+    n = b.size - first if n is None else n
+    args = (data.ctypes.data_as(C.c_void_p), offs.ctypes.data_as(C.c_void_p), b.ctypes.data_as(C.c_void_p), first, n)
+    size = lib().rpo_serialize_wire(*args, None)
+    out = np.zeros(max(size, 1), dtype=np.uint8)
+    lib().rpo_serialize_wire(*args, out.ctypes.data_as(C.c_void_p))
+    return out[:size].tobytes()
 
 
 def segment_index(batches: np.ndarray, summaries: np.ndarray, base_offsets, step: int = abi.INDEX_DEFAULT_STEP,

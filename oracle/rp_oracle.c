@@ -1207,6 +1207,17 @@ int rpo_uncompress(int codec, const uint8_t* s, size_t n, uint8_t* dst, size_t c
     }
 }
 
+/* Engine plan rule for a gzip member (not reference semantics; the reference
+ * sizes its buffer with the same decode, gzip_compressor.cc:187-195): the
+ * bytes the sizing pass yields rounded up to 16, 0 when it rejects.  The
+ * sizing pass holds no output, so it stops short of the trailer checks. */
+uint64_t rpo_gzip_plan(const uint8_t* s, size_t n) {
+    size_t total = 0;
+    if (n == 0) return 0;
+    if (rpo_gzip_uncompress(s, n, NULL, 0, &total) == -1) return 0;
+    return ((uint64_t)total + 15) & ~(uint64_t)15;
+}
+
 static uint64_t decode_capacity_raw(int codec, const uint8_t* s, size_t n);
 
 /* Engine plan rule (not reference semantics): bytes reserved in the decoded
@@ -1376,7 +1387,7 @@ int64_t rpo_scan_segment_layout(const uint8_t* seg, uint64_t len, uint32_t segme
         const int may_walk = !wire || (r->flags & RPGPU_F_CRC_OK);
         if (codec) r->flags |= RPGPU_F_COMPRESSED;
         if (codec >= 5) r->flags |= RPGPU_F_CODEC_INVALID;
-        if (codec == RPGPU_CODEC_GZIP || codec == RPGPU_CODEC_ZSTD) r->flags |= RPGPU_F_CODEC_UNSUPPORTED;
+        if (codec == RPGPU_CODEC_ZSTD) r->flags |= RPGPU_F_CODEC_UNSUPPORTED;
 
         /* Plan (engine rule, see DESIGN.md "index and arena planning"): the
          * record-index slots and decode-arena bytes of a batch are reserved
@@ -1384,12 +1395,13 @@ int64_t rpo_scan_segment_layout(const uint8_t* seg, uint64_t len, uint32_t segme
          * the GPU can assign them with prefix sums.  Reservations never depend
          * on whether the decode or the walk later succeed. */
         uint64_t slots = 0, cap = 0;
-        int decodable = (codec == RPGPU_CODEC_LZ4 || codec == RPGPU_CODEC_SNAPPY) && (job_flags & RPGPU_JOB_DECODE);
+        int decodable = (codec == RPGPU_CODEC_LZ4 || codec == RPGPU_CODEC_SNAPPY || codec == RPGPU_CODEC_GZIP) &&
+                        (job_flags & RPGPU_JOB_DECODE);
         if (codec == 0) {
             if ((job_flags & RPGPU_JOB_PARSE) && h.record_count > 0 && (uint64_t)h.record_count <= need)
                 slots = (uint64_t)h.record_count;
         } else if (decodable) {
-            cap = rpo_decode_capacity((int)codec, payload, need);
+            cap = codec == RPGPU_CODEC_GZIP ? rpo_gzip_plan(payload, need) : rpo_decode_capacity((int)codec, payload, need);
             if ((job_flags & RPGPU_JOB_PARSE) && h.record_count > 0 && (uint64_t)h.record_count <= cap)
                 slots = (uint64_t)h.record_count;
         }
@@ -2020,4 +2032,48 @@ size_t rpo_snappy_java_compress(const uint8_t* s, size_t n, size_t frag, uint8_t
         o += 4 + c;
     }
     return o;
+}
+
+
+/* ======================================================================== */
+/* kafka::writer_serialize_batch (kafka/protocol/response_writer.h:241-276)  */
+/* ======================================================================== */
+/* Batches [first, first + n) of a job's results as a Kafka v2 record set:
+ * base_offset, batch_length = size_bytes - 61 + 61 - 8 - 4, partition leader
+ * epoch 0, magic 2, crc, attrs, last_offset_delta, first / max timestamp,
+ * producer id / epoch, base_sequence, record_count (each big endian), then
+ * the payload as stored.  Returns the bytes written (out may be NULL to
+ * size). */
+static size_t put_be(uint8_t* o, uint64_t v, int k) {
+    if (o)
+        for (int i = 0; i < k; i++) o[i] = (uint8_t)(v >> (8 * (k - 1 - i)));
+    return (size_t)k;
+}
+
+uint64_t rpo_serialize_wire(const uint8_t* data, const uint64_t* seg_offsets, const rpgpu_batch_result* batches,
+                            uint64_t first, uint64_t n, uint8_t* out) {
+    uint64_t at = 0;
+    for (uint64_t i = first; i < first + n; i++) {
+        const rpgpu_batch_result* b = &batches[i];
+        uint8_t* o = out ? out + at : NULL;
+        size_t k = 0;
+        const int32_t size = b->size_bytes - RPGPU_HEADER_SIZE + RPGPU_HEADER_SIZE - 8 - 4;
+        k += put_be(o ? o + k : NULL, (uint64_t)b->base_offset, 8);
+        k += put_be(o ? o + k : NULL, (uint32_t)size, 4);
+        k += put_be(o ? o + k : NULL, 0, 4);
+        k += put_be(o ? o + k : NULL, 2, 1);
+        k += put_be(o ? o + k : NULL, b->crc, 4);
+        k += put_be(o ? o + k : NULL, (uint16_t)b->attrs, 2);
+        k += put_be(o ? o + k : NULL, (uint32_t)b->last_offset_delta, 4);
+        k += put_be(o ? o + k : NULL, (uint64_t)b->first_timestamp, 8);
+        k += put_be(o ? o + k : NULL, (uint64_t)b->max_timestamp, 8);
+        k += put_be(o ? o + k : NULL, (uint64_t)b->producer_id, 8);
+        k += put_be(o ? o + k : NULL, (uint16_t)b->producer_epoch, 2);
+        k += put_be(o ? o + k : NULL, (uint32_t)b->base_sequence, 4);
+        k += put_be(o ? o + k : NULL, (uint32_t)b->record_count, 4);
+        const uint64_t plen = (uint64_t)(uint32_t)(b->size_bytes - RPGPU_HEADER_SIZE);
+        if (o) memcpy(o + k, data + seg_offsets[b->segment] + b->file_pos + RPGPU_HEADER_SIZE, plen);
+        at += k + plen;
+    }
+    return at;
 }

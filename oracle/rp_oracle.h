@@ -104,6 +104,8 @@ int rpo_lz4_block_decode(const uint8_t* src, size_t n, uint8_t* dst, size_t dst_
 /* decode-arena reservation for one compressed payload (engine plan rule,
  * shared with the GPU planner; see DESIGN.md "decode arena") */
 uint64_t rpo_decode_capacity(int codec, const uint8_t* src, size_t n);
+/* the same for a gzip member (the engine's sizing pass) */
+uint64_t rpo_gzip_plan(const uint8_t* src, size_t n);
 
 /* --- segment pipeline: continuous_batch_parser::consume
  *     (storage/parser.cc:96-254) driving checksumming_consumer
@@ -130,6 +132,11 @@ int rpo_run_job(const uint8_t* data, const uint64_t* seg_offsets, uint32_t n_seg
                 rpgpu_record_index* index, uint64_t index_cap, uint8_t* decoded,
                 uint64_t decoded_cap, rpgpu_segment_summary* summaries,
                 rpgpu_job_totals* totals, uint64_t* valid_bitmap);
+
+/* kafka::writer_serialize_batch (kafka/protocol/response_writer.h:241-276)
+ * over batches [first, first + n) of a job's results; out NULL sizes */
+uint64_t rpo_serialize_wire(const uint8_t* data, const uint64_t* seg_offsets, const rpgpu_batch_result* batches,
+                            uint64_t first, uint64_t n, uint8_t* out);
 
 /* validity rule behind rpgpu_job.d_valid_bitmap */
 int rpo_batch_valid(const rpgpu_batch_result* b, uint32_t job_flags);

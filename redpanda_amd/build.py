@@ -19,7 +19,7 @@ OUT = os.path.join(HERE, "librpgpu.so")
 BUILD = os.path.join(HERE, "_build")
 ARCH = os.environ.get("RPGPU_ARCH", "gfx950")
 
-HIP_SOURCES = ["rp_kernels.hip", "rp_validate.hip", "rp_codec.hip", "rp_compress.hip", "rp_index.hip", "rp_runtime.hip"]
+HIP_SOURCES = ["rp_kernels.hip", "rp_validate.hip", "rp_codec.hip", "rp_inflate.hip", "rp_compress.hip", "rp_index.hip", "rp_runtime.hip"]
 CXX_SOURCES = ["rp_hostcodec.cpp"]
 
 

@@ -1,0 +1,660 @@
+// rp_inflate.hip — gzip_compressor::uncompress on the device
+// (compression/internal/gzip_compressor.cc:161-230): zlib 1.2.11 inflate
+// with inflateInit2(15 + 32) (a gzip member or a zlib stream), as the
+// reference's loop drives it.  The accept/reject rules are the oracle's
+// restatement (oracle/rp_oracle.c rpo_gzip_uncompress), which is pinned
+// against zlib itself:
+//   * an error anywhere before the end of the first member rejects;
+//   * input that runs out is not an error: the output is what inflate could
+//     decode from the bytes present (a code decodes once all its bits are
+//     there; stored blocks byte by byte);
+//   * bytes after the first member are ignored.
+//
+// The reference decodes every payload twice (buffer_for_input sizes the
+// output with a pass through a 512-byte buffer, then decodes into a buffer of
+// exactly that size).  The engine does the same: k_inflate_plan runs the
+// decoder without output to size each member's arena slot before the slot
+// scan, and k_inflate decodes into the slot.
+//
+// Execution model: one wave per member.  Deflate is a serial bit stream, so
+// the decoder state is wave-uniform (scalar registers); the wave's lanes
+// build the Huffman codes (ballots over the code lengths), find a code's
+// length with one compare per lane (lane L holds the left-justified limit of
+// the length-L codes: canonical codes make that the whole decode), copy
+// matches 64 bytes per step, and flush, CRC32 and Adler-32 1 KiB of output
+// per step.  Output goes through a 32 KiB LDS ring (deflate distances reach
+// 32768 back) and leaves in coalesced 16-byte stores.
+// Integer work only: no MFMA.
+#include "rp_device.h"
+
+namespace rp {
+
+typedef __attribute__((address_space(3))) uint8_t inf_lds_u8;
+
+constexpr uint32_t kInfRing = 32768, kInfMask = kInfRing - 1;
+// per-wave LDS: the code tables (symbols in canonical order, code lengths of
+// a dynamic header) and, for the decode pass, the output ring
+struct InfTabs {
+    uint16_t lsym[288];
+    uint16_t dsym[32];
+    uint16_t csym[19];
+    uint16_t pad0;
+    uint8_t lens[320];
+    uint32_t crc_tab[256];  // CRC32 (IEEE, reflected 0xEDB88320) byte table
+};
+constexpr uint32_t kInfTabBytes = (sizeof(InfTabs) + 15u) & ~15u;
+constexpr uint32_t kInfLdsDecode = kInfRing + kInfTabBytes;
+
+// x^(2^k) mod the reflected CRC32 polynomial 0xEDB88320 (period 32)
+static __constant__ uint32_t kX2nIeee[32] = {
+    0x40000000u, 0x20000000u, 0x08000000u, 0x00800000u, 0x00008000u, 0xEDB88320u, 0xB1E6B092u, 0xA06A2517u,
+    0xED627DAEu, 0x88D14467u, 0xD7BBFE6Au, 0xEC447F11u, 0x8E7EA170u, 0x6427800Eu, 0x4D47BAE0u, 0x09FE548Fu,
+    0x83852D0Fu, 0x30362F1Au, 0x7B5A9CC3u, 0x31FEC169u, 0x9FEC022Au, 0x6C8DEDC4u, 0x15D6874Du, 0x5FDE7A4Eu,
+    0xBAD90E37u, 0x2E4E5EEFu, 0x4EABA214u, 0xA8A472C0u, 0x429A969Eu, 0x148D302Au, 0xC40BA6D0u, 0xC4E22C3Cu};
+
+DEV uint32_t ieee_mulmod(uint32_t a, uint32_t b) {
+    uint32_t p = 0;
+    for (uint32_t m = 1u << 31; m; m >>= 1) {
+        if (a & m) p ^= b;
+        b = (b & 1) ? (b >> 1) ^ 0xEDB88320u : b >> 1;
+    }
+    return p;
+}
+// x^(8 n) mod P
+DEV uint32_t ieee_xpow8(uint32_t n) {
+    uint32_t p = 1u << 31;
+    for (uint32_t k = 3; n; n >>= 1, k = (k + 1) & 31u)
+        if (n & 1) p = ieee_mulmod(kX2nIeee[k], p);
+    return p;
+}
+
+// deflate's length / distance bases and extra bits (RFC 1951 3.2.5)
+static __constant__ uint16_t kLenBase[29] = {3, 4, 5, 6, 7, 8, 9, 10, 11, 13, 15, 17, 19, 23, 27, 31,
+                                              35, 43, 51, 59, 67, 83, 99, 115, 131, 163, 195, 227, 258};
+static __constant__ uint8_t kLenExtra[29] = {0, 0, 0, 0, 0, 0, 0, 0, 1, 1, 1, 1, 2, 2, 2, 2,
+                                              3, 3, 3, 3, 4, 4, 4, 4, 5, 5, 5, 5, 0};
+static __constant__ uint16_t kDistBase[30] = {1, 2, 3, 4, 5, 7, 9, 13, 17, 25, 33, 49, 65, 97, 129,
+                                               193, 257, 385, 513, 769, 1025, 1537, 2049, 3073, 4097,
+                                               6145, 8193, 12289, 16385, 24577};
+static __constant__ uint8_t kDistExtra[30] = {0, 0, 0, 0, 1, 1, 2, 2, 3, 3, 4, 4, 5, 5, 6,
+                                               6, 7, 7, 8, 8, 9, 9, 10, 10, 11, 11, 12, 12, 13, 13};
+static __constant__ uint8_t kClenOrder[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12, 3, 13, 2, 14, 1, 15};
+
+// ---------------------------------------------------------------------------
+// Input: the member's bytes through a 512-byte window held one dword per
+// lane (two rows); reads are wave-uniform.  Bytes past the member read as 0.
+// ---------------------------------------------------------------------------
+struct InfIn {
+    const uint8_t* src;  // the member's first byte
+    const uint8_t* al;   // src rounded down to 4 bytes: window dwords are read from here
+    uint64_t n, nphys;   // member bytes; n + mis
+    uint32_t mis;        // src & 3
+    uint64_t base;       // window start (4-aligned offset from al)
+    uint32_t w0, w1;     // lane l: dwords base + 4 l, base + 256 + 4 l
+};
+
+DEV InfIn inf_in(const uint8_t* src, uint64_t n) {
+    InfIn in;
+    in.src = src;
+    in.mis = (uint32_t)((uintptr_t)src & 3);
+    in.al = src - in.mis;
+    in.n = n;
+    in.nphys = n + in.mis;
+    in.base = ~0ull >> 1;
+    in.w0 = in.w1 = 0;
+    return in;
+}
+// an aligned dword that starts inside the member never crosses a page, so
+// reading its bytes past the member end is safe (they are masked)
+DEV uint32_t inf_ld(const InfIn& in, uint64_t a) { return a < in.nphys ? *(const uint32_t*)(in.al + a) : 0u; }
+DEV uint32_t inf_dw(InfIn& in, uint64_t a) {  // a: 4-aligned, wave-uniform
+    uint64_t o = a - in.base;
+    if (a < in.base || o >= 512) {
+        in.base = a;
+        in.w0 = inf_ld(in, a + 4u * lane());
+        in.w1 = inf_ld(in, a + 256u + 4u * lane());
+        o = 0;
+    }
+    const int li = (int)((o >> 2) & 63);
+    return o < 256 ? rl(in.w0, li) : rl(in.w1, li);
+}
+DEV uint32_t inf_byte(InfIn& in, uint64_t i) {
+    if (i >= in.n) return 0u;
+    const uint64_t p = i + in.mis;
+    return (inf_dw(in, p & ~3ull) >> (8u * (uint32_t)(p & 3))) & 0xFFu;
+}
+// 32 bits of the stream from bit position bp (LSB first), zero past the end
+DEV uint32_t inf_peek(InfIn& in, uint64_t bp) {
+    const uint64_t pb = bp + 8ull * in.mis, b = pb >> 3, a = b & ~3ull;
+    const uint32_t sh = (uint32_t)(((b & 3) << 3) | (pb & 7));
+    const uint32_t d0 = inf_dw(in, a), d1 = inf_dw(in, a + 4);
+    const uint32_t v = sh ? __builtin_amdgcn_alignbit(d1, d0, sh) : d0;
+    const uint64_t avail = in.n * 8 - bp;
+    return avail < 32 ? v & ((1u << avail) - 1u) : v;
+}
+// 64 bits from bp (two peeks)
+DEV uint64_t inf_peek64(InfIn& in, uint64_t bp) {
+    return (uint64_t)inf_peek(in, bp) | ((uint64_t)(bp + 32 < in.n * 8 ? inf_peek(in, bp + 32) : 0u) << 32);
+}
+
+// ---------------------------------------------------------------------------
+// Canonical Huffman code: lane L (1..15) holds the left-justified 15-bit
+// limit of the codes of length <= L, the first code of length L and the
+// canonical index of that code; symbols in LDS in canonical order.
+// ---------------------------------------------------------------------------
+struct InfCode {
+    uint32_t lim, first, offs;  // lane L
+};
+
+// inflate_table acceptance (zlib 1.2.11 inftrees.c, the oracle's
+// huff_build): over-subscribed -> error; incomplete -> error unless a single
+// 1-bit literal/length or distance code; no codes at all -> an empty code
+// (any decode reports an invalid code after one bit).  type: 0 code-length
+// code, 1 literal/length, 2 distance.  Returns 0 ok, -1 error.
+DEV int inf_build(const inf_lds_u8* lens, uint32_t m, int type, uint16_t* syms, InfCode& c) {
+    const uint32_t l = lane();
+    uint32_t cnt = 0;
+    for (uint32_t ch = 0; ch < m; ch += 64) {
+        const uint32_t s = ch + l;
+        const uint32_t len = s < m ? (uint32_t)lens[s] : 0u;
+#pragma unroll
+        for (uint32_t L = 1; L <= 15; L++) {
+            const uint32_t k = (uint32_t)__builtin_popcountll(__ballot(len == L));
+            if (l == L) cnt += k;
+        }
+    }
+    int left = 1;
+    uint32_t code = 0, offs = 0, max = 0;
+    c.lim = c.first = c.offs = 0;
+    for (uint32_t L = 1; L <= 15; L++) {
+        const uint32_t cL = rl(cnt, (int)L);
+        left = 2 * left - (int)cL;
+        if (left < 0) return -1;  // over-subscribed
+        if (l == L) {
+            c.first = code;
+            c.offs = offs;
+            c.lim = (code + cL) << (15 - L);
+        }
+        code = (code + cL) << 1;
+        offs += cL;
+        if (cL) max = L;
+    }
+    if (max == 0) {  // no codes: every lookup is the invalid entry
+        c.lim = 0;
+        return 0;
+    }
+    if (left > 0 && (type == 0 || max != 1)) return -1;  // incomplete
+    // symbols in canonical order: (length, value), ranks by ballot
+    uint32_t next = c.offs;  // lane L: next slot for length L
+    for (uint32_t ch = 0; ch < m; ch += 64) {
+        const uint32_t s = ch + l;
+        const uint32_t len = s < m ? (uint32_t)lens[s] : 0u;
+        uint32_t pos = 0;
+#pragma unroll
+        for (uint32_t L = 1; L <= 15; L++) {
+            const uint64_t mask = __ballot(len == L);
+            if (len == L) pos = rl(next, (int)L) + (uint32_t)__builtin_popcountll(mask & ((1ull << l) - 1ull));
+            if (l == L) next += (uint32_t)__builtin_popcountll(mask);
+        }
+        if (len) syms[pos] = (uint16_t)s;
+    }
+    return 0;
+}
+
+// One symbol from the 32 peeked bits v, `avail` bits left in the stream:
+// 1 decoded (sym, len), 0 the code needs bits past the end (truncated), -1
+// an invalid code (one bit).  The shortest code matching the zero-extended
+// bits decodes once all its bits are present: zlib's table lookup.
+DEV int inf_decode(uint32_t v, uint64_t avail, const InfCode& c, const uint16_t* syms, uint32_t& sym, uint32_t& len) {
+    const uint32_t r = __builtin_bitreverse32(v) >> 17;  // next 15 bits, first bit most significant
+    const uint64_t m = __ballot(r < c.lim);
+    if (m == 0) return avail >= 1 ? -1 : 0;
+    const uint32_t L = (uint32_t)__builtin_ctzll(m);
+    if (L > avail) return 0;
+    const uint32_t idx = rl(c.offs, (int)L) + (r >> (15 - L)) - rl(c.first, (int)L);
+    sym = uni32((uint32_t)syms[idx]);
+    len = L;
+    return 1;
+}
+
+// ---------------------------------------------------------------------------
+// Output (decode pass): ring in LDS, 1 KiB chunks flushed to the slot with
+// their CRC32 / Adler-32 folded into the running check.
+// ---------------------------------------------------------------------------
+struct InfOut {
+    inf_lds_u8* ring;
+    const uint32_t* tab;  // CRC32 byte table (LDS)
+    uint8_t* dst;         // slot start (16-byte aligned)
+    uint64_t flushed;     // bytes flushed (multiple of 1024 until the end)
+    uint32_t crc;         // raw register (init 0xFFFFFFFF)
+    uint32_t ada, adb;    // Adler-32 sums
+    bool gz;
+};
+
+// flush output bytes [o.flushed, o.flushed + len) (len <= 1024, the start
+// 1 KiB aligned) from the ring and fold them into the check
+DEV void inf_flush(InfOut& o, uint32_t len) {
+    const uint32_t l = lane();
+    const uint32_t at = (uint32_t)(o.flushed & kInfMask) + 16u * l;
+    const uint32_t t = 16u * l < len ? min(16u, len - 16u * l) : 0u;  // this lane's bytes
+    uint4 v = make_uint4(0, 0, 0, 0);
+    if (t) {
+        v = *(const uint4*)(o.ring + at);
+        *(uint4*)(o.dst + o.flushed + 16u * l) = v;  // the slot is rounded up to 16: a whole piece fits
+    }
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+    if (o.gz) {
+        uint32_t c = 0;
+#pragma unroll
+        for (uint32_t k = 0; k < 16; k++)
+            if (k < t) c = o.tab[(c ^ (w[k >> 2] >> (8 * (k & 3)))) & 0xFFu] ^ (c >> 8);
+        // lane l's raw CRC moved to the end of the piece: x^(8 (len - 16 l - t))
+        uint32_t x = t ? ieee_mulmod(ieee_xpow8(len - 16u * l - t), c) : 0u;
+        x = wave_xor(x);
+        o.crc = ieee_mulmod(ieee_xpow8(len), o.crc) ^ uni32(x);
+    } else {
+        uint32_t s1 = 0, s2 = 0;
+#pragma unroll
+        for (uint32_t k = 0; k < 16; k++)
+            if (k < t) {
+                const uint32_t d = (w[k >> 2] >> (8 * (k & 3))) & 0xFFu;
+                s1 += d;
+                s2 += (len - 16u * l - k) * d;  // weight: bytes from it to the chunk end
+            }
+        for (int off = 32; off > 0; off >>= 1) {
+            s1 += __shfl_xor(s1, off, 64);
+            s2 += __shfl_xor(s2, off, 64);
+        }
+        s1 = uni32(s1);
+        s2 = uni32(s2);
+        o.adb = (uint32_t)(((uint64_t)o.adb + (uint64_t)len * o.ada + s2) % 65521u);
+        o.ada = (o.ada + s1) % 65521u;
+    }
+    o.flushed += len;
+}
+
+// every complete 1 KiB chunk below op
+DEV void inf_flush_upto(InfOut& o, uint64_t op) {
+    while ((op >> 10) > (o.flushed >> 10)) inf_flush(o, 1024u);
+}
+
+// match: ml bytes from dist back (dist <= op, checked)
+DEV void inf_copy(InfOut& o, uint64_t op, uint32_t dist, uint32_t ml) {
+    const uint32_t l = lane();
+    uint32_t b[5];
+#pragma unroll
+    for (uint32_t i = 0; i < 5; i++) {
+        const uint32_t k = 64u * i + l;
+        const uint32_t from = (uint32_t)(op - dist) + (dist >= ml ? k : k % dist);
+        b[i] = k < ml ? (uint32_t)o.ring[from & kInfMask] : 0u;  // every read before any write
+    }
+#pragma unroll
+    for (uint32_t i = 0; i < 5; i++) {
+        const uint32_t k = 64u * i + l;
+        if (k < ml) o.ring[(uint32_t)(op + k) & kInfMask] = (uint8_t)b[i];
+    }
+}
+
+// ---------------------------------------------------------------------------
+// The member decoder.  kWrite = false: the sizing pass (no output, no data
+// check); true: the decode pass into `o`.  Returns -1 rejected, 0 accepted;
+// `total` = bytes produced.
+// ---------------------------------------------------------------------------
+template <bool kWrite>
+DEV int inflate_member(InfIn& in, InfTabs* T, InfOut& o, uint64_t& total) {
+    const uint32_t l = lane();
+    const uint64_t nbits = in.n * 8;
+    uint64_t bp = 0, op = 0;
+    total = 0;
+    bool gz = false;
+    uint32_t v, sym, len;
+    InfCode LC, DC, CC;
+#define NEED(k) \
+    if (nbits - bp < (uint64_t)(k)) goto done
+    // HEAD
+    NEED(16);
+    v = inf_peek(in, bp);
+    if ((v & 0xFFFFu) == 0x8b1fu) {
+        gz = true;
+        // FLAGS, TIME, OS, EXLEN, EXTRA, NAME, COMMENT, HCRC
+        uint32_t hc = 0xFFFFFFFFu;  // header CRC register (FHCRC)
+        auto hcrc = [&](uint64_t from, uint64_t cnt) __attribute__((always_inline)) {
+            for (uint64_t i = 0; i < cnt; i++) hc = T->crc_tab[(hc ^ inf_byte(in, from + i)) & 0xFFu] ^ (hc >> 8);
+        };
+        hcrc(0, 2);
+        bp = 16;
+        NEED(16);
+        const uint32_t flags = inf_peek(in, bp) & 0xFFFFu;
+        if ((flags & 0xFFu) != 8u) return -1;  // unknown compression method
+        if (flags & 0xe000u) return -1;        // unknown header flags set
+        const bool fh = (flags & 0x0200u) != 0;
+        if (fh) hcrc(2, 2);
+        bp = 32;
+        NEED(32);
+        if (fh) hcrc(4, 4);
+        bp = 64;
+        NEED(16);
+        if (fh) hcrc(8, 2);
+        bp = 80;
+        if (flags & 0x0400u) {
+            NEED(16);
+            const uint64_t xlen = inf_peek(in, bp) & 0xFFFFu;
+            if (fh) hcrc(10, 2);
+            bp += 16;
+            const uint64_t have = in.n - (bp >> 3), copy = xlen < have ? xlen : have;
+            if (fh) hcrc(bp >> 3, copy);
+            bp += 8 * copy;
+            if (copy < xlen) goto done;
+        }
+        for (uint32_t f = 0x0800u; f <= 0x1000u; f <<= 1) {
+            if (!(flags & f)) continue;
+            uint64_t p = bp >> 3;
+            if (p >= in.n) goto done;
+            const uint64_t start = p;
+            uint32_t c;
+            do c = inf_byte(in, p++); while (c && p < in.n);
+            if (fh) hcrc(start, p - start);
+            bp = 8 * p;
+            if (c) goto done;
+        }
+        if (fh) {
+            NEED(16);
+            if ((inf_peek(in, bp) & 0xFFFFu) != (~hc & 0xFFFFu)) return -1;  // header crc mismatch
+            bp += 16;
+        }
+    } else {
+        const uint32_t hold = v & 0xFFFFu;
+        if ((((hold & 0xFFu) << 8) + (hold >> 8)) % 31u) return -1;  // incorrect header check
+        if ((hold & 0x0Fu) != 8u) return -1;                         // unknown compression method
+        if (((hold >> 4) & 0x0Fu) + 8u > 15u) return -1;             // invalid window size
+        bp = 16;
+        if (hold & 0x2000u) {  // FDICT: DICTID, then Z_NEED_DICT
+            NEED(32);
+            return -1;
+        }
+    }
+    if (kWrite) {
+        o.gz = gz;
+        o.crc = 0xFFFFFFFFu;
+        o.ada = 1;
+        o.adb = 0;
+    }
+    // blocks
+    for (;;) {
+        NEED(3);
+        v = inf_peek(in, bp);
+        const uint32_t last = v & 1u, type = (v >> 1) & 3u;
+        bp += 3;
+        if (type == 0) {  // STORED
+            bp = (bp + 7) & ~7ull;
+            NEED(32);
+            v = inf_peek(in, bp);
+            if ((v & 0xFFFFu) != ((v >> 16) ^ 0xFFFFu)) return -1;  // invalid stored block lengths
+            bp += 32;
+            uint64_t length = v & 0xFFFFu;
+            const uint64_t p = bp >> 3, have = in.n - p, copy = length < have ? length : have;
+            if (kWrite) {
+                // 1 KiB per step: lane l's 16 bytes, byte loads (any alignment)
+                for (uint64_t c = 0; c < copy; c += 1024) {
+                    uint32_t w[4] = {0, 0, 0, 0};
+#pragma unroll
+                    for (uint32_t k = 0; k < 16; k++) {
+                        const uint64_t i = c + 16u * l + k;
+                        if (i < copy) w[k >> 2] |= (uint32_t)in.src[p + i] << (8 * (k & 3));
+                    }
+#pragma unroll
+                    for (uint32_t k = 0; k < 16; k++) {
+                        const uint64_t i = c + 16u * l + k;
+                        if (i < copy) o.ring[(uint32_t)(op + i - c) & kInfMask] = (uint8_t)(w[k >> 2] >> (8 * (k & 3)));
+                    }
+                    const uint64_t step = copy - c < 1024 ? copy - c : 1024;
+                    op += step;
+                    inf_flush_upto(o, op);
+                }
+            } else {
+                op += copy;
+            }
+            bp += 8 * copy;
+            if (copy < length) goto done;
+        } else if (type == 3) {
+            return -1;  // invalid block type
+        } else {
+            inf_lds_u8* lens = (inf_lds_u8*)T->lens;
+            if (type == 1) {  // fixed codes
+                for (uint32_t s = l; s < 288; s += 64) lens[s] = s < 144 ? 8 : s < 256 ? 9 : s < 280 ? 7 : 8;
+                inf_build(lens, 288, 1, T->lsym, LC);
+                if (l < 32) lens[l] = 5;
+                inf_build(lens, 32, 2, T->dsym, DC);
+            } else {  // TABLE
+                NEED(14);
+                v = inf_peek(in, bp);
+                const uint32_t nlen = (v & 31u) + 257, ndist = ((v >> 5) & 31u) + 1, ncode = ((v >> 10) & 15u) + 4;
+                bp += 14;
+                if (nlen > 286 || ndist > 30) return -1;  // too many length or distance symbols
+                // code-length code lengths (3 bits each, permuted)
+                const uint64_t need = 3ull * ncode;
+                const bool all = nbits - bp >= need;
+                const uint32_t got = all ? ncode : (uint32_t)((nbits - bp) / 3);
+                // lane i < 19: its code length (0 when past ncode); 57 bits at most
+                const uint64_t w57 = inf_peek64(in, bp);
+                const uint32_t cl = l < got ? (uint32_t)(w57 >> (3 * (l < 19 ? l : 0))) & 7u : 0u;
+                if (!all) goto done;
+                bp += need;
+                if (l < 19) lens[kClenOrder[l]] = (uint8_t)(l < ncode ? cl : 0u);
+                if (inf_build(lens, 19, 0, T->csym, CC)) return -1;  // invalid code lengths set
+                uint32_t have = 0;
+                while (have < nlen + ndist) {
+                    v = inf_peek(in, bp);
+                    const int r = inf_decode(v, nbits - bp, CC, T->csym, sym, len);
+                    if (r == 0) goto done;
+                    if (r < 0) { sym = 0; len = 1; }  // zlib's CODELENS reads an invalid entry as length 0
+                    bp += len;
+                    if (sym < 16) {
+                        if (l == 0) lens[have] = (uint8_t)sym;
+                        have++;
+                        continue;
+                    }
+                    uint32_t rep = 0, cnt;
+                    v = inf_peek(in, bp);
+                    if (sym == 16) {
+                        NEED(2);
+                        if (have == 0) return -1;  // invalid bit length repeat
+                        rep = uni32((uint32_t)lens[have - 1]);
+                        cnt = 3 + (v & 3u);
+                        bp += 2;
+                    } else if (sym == 17) {
+                        NEED(3);
+                        cnt = 3 + (v & 7u);
+                        bp += 3;
+                    } else {
+                        NEED(7);
+                        cnt = 11 + (v & 127u);
+                        bp += 7;
+                    }
+                    if (have + cnt > nlen + ndist) return -1;  // invalid bit length repeat
+                    if (l < cnt) lens[have + l] = (uint8_t)rep;  // cnt <= 138: lanes, twice
+                    if (l + 64 < cnt) lens[have + l + 64] = (uint8_t)rep;
+                    if (l + 128 < cnt) lens[have + l + 128] = (uint8_t)rep;
+                    have += cnt;
+                }
+                if (lens[256] == 0) return -1;                             // invalid code -- missing end-of-block
+                if (inf_build(lens, nlen, 1, T->lsym, LC)) return -1;      // invalid literal/lengths set
+                if (inf_build(lens + nlen, ndist, 2, T->dsym, DC)) return -1;  // invalid distances set
+            }
+            // LEN .. MATCH
+            for (;;) {
+                v = inf_peek(in, bp);
+                int r = inf_decode(v, nbits - bp, LC, T->lsym, sym, len);
+                if (r == 0) goto done;
+                if (r < 0 || sym > 285) return -1;  // invalid literal/length code
+                bp += len;
+                if (sym < 256) {
+                    if (kWrite) {
+                        if (l == 0) o.ring[(uint32_t)op & kInfMask] = (uint8_t)sym;
+                        op++;
+                        if ((op & 1023) == 0) inf_flush(o, 1024u);
+                    } else {
+                        op++;
+                    }
+                    continue;
+                }
+                if (sym == 256) break;
+                sym -= 257;
+                uint32_t ml = kLenBase[sym];
+                const uint32_t le = kLenExtra[sym];
+                v >>= len;  // the extra bits follow the code (len + le <= 20 < 32)
+                if (le) {
+                    NEED(le);
+                    ml += v & ((1u << le) - 1u);
+                    bp += le;
+                }
+                v = inf_peek(in, bp);
+                r = inf_decode(v, nbits - bp, DC, T->dsym, sym, len);
+                if (r == 0) goto done;
+                if (r < 0 || sym > 29) return -1;  // invalid distance code
+                bp += len;
+                uint32_t dist = kDistBase[sym];
+                const uint32_t de = kDistExtra[sym];
+                if (de) {
+                    NEED(de);
+                    dist += (v >> len) & ((1u << de) - 1u);  // len + de <= 28
+                    bp += de;
+                }
+                if (dist > op) return -1;  // invalid distance too far back
+                if (kWrite) {
+                    inf_copy(o, op, dist, ml);
+                    op += ml;
+                    inf_flush_upto(o, op);
+                } else {
+                    op += ml;
+                }
+            }
+        }
+        if (last) break;
+    }
+    // CHECK, LENGTH (the sizing pass stops before them: it holds no bytes to
+    // check, and the plan depends only on what decodes)
+    if (kWrite) {
+        bp = (bp + 7) & ~7ull;
+        NEED(32);
+        if (op > o.flushed) inf_flush(o, (uint32_t)(op - o.flushed));
+        const uint32_t w = inf_peek(in, bp);
+        if (gz) {
+            if (w != ~o.crc) return -1;  // incorrect data check
+        } else {
+            const uint32_t be = __builtin_bswap32(w);
+            if (be != ((o.adb << 16) | o.ada)) return -1;
+        }
+        bp += 32;
+        if (gz) {
+            NEED(32);
+            if (inf_peek(in, bp) != (uint32_t)op) return -1;  // incorrect length check
+        }
+        total = op;
+        return 0;
+    }
+done:
+    if (kWrite && op > o.flushed) inf_flush(o, (uint32_t)(op - o.flushed));
+    total = op;
+    return 0;
+#undef NEED
+}
+
+// ---------------------------------------------------------------------------
+// Job kernels.  k_emit lists the gzip batches of RPGPU_JOB_DECODE jobs
+// (inf_list, counters[16] items).
+//   k_inflate_plan: the sizing pass, one wave per member, before the slot
+//     scans: the member's arena reservation (dcap: its output rounded up to
+//     16, 0 when it is rejected) and index slots (the same record_count rule
+//     as every codec), and the pass's verdict (inf_state);
+//   k_inflate: the decode pass into the slot: CODEC_OK, decoded_len.
+// k_validate_decoded then computes the new crc / header_crc and walks it.
+// ---------------------------------------------------------------------------
+DEV void inf_load_tab(uint32_t* tab) {
+    for (uint32_t i = lane(); i < 256; i += 64) {
+        uint32_t c = i;
+        for (int k = 0; k < 8; k++) c = (c & 1) ? (c >> 1) ^ 0xEDB88320u : c >> 1;
+        tab[i] = c;
+    }
+}
+
+DEV InfIn inf_batch(const DeviceJob& j, const rpgpu_batch_result* R) {
+    const uint64_t S = uni64(j.seg_off[uni32(R->segment)]) + uni64(R->file_pos) + RPGPU_HEADER_SIZE;
+    const uint64_t n = (uint64_t)uni32((uint32_t)(R->size_bytes - (int32_t)RPGPU_HEADER_SIZE));
+    return inf_in(j.data + S, n);
+}
+
+// one wave per workgroup: the tables (and the ring) are the wave's own
+__global__ __launch_bounds__(64) void k_inflate_plan(DeviceJob j) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    InfTabs* T = (InfTabs*)lds;
+    inf_load_tab(T->crc_tab);
+    const uint32_t count = j.counters[16];
+    for (;;) {
+        const uint32_t i = wave_fetch_add(&j.counters[17], 1u);
+        if (i >= count) break;
+        const uint32_t b = uni32(j.inf_list[i]);
+        const rpgpu_batch_result* R = &j.batches[b];
+        InfIn in = inf_batch(j, R);
+        InfOut o;
+        uint64_t total = 0;
+        // compressor::uncompress throws on an empty payload (compression/compression.cc:34-55)
+        const int rc = in.n ? inflate_member<false>(in, T, o, total) : -1;
+        const uint64_t cap = rc ? 0 : (total + 15) & ~15ull;
+        if (lane() == 0) {
+            const int32_t rcount = R->record_count;
+            j.dcap[b] = cap;
+            j.slots[b] = ((j.flags & RPGPU_JOB_PARSE) && rcount > 0 && (uint64_t)rcount <= cap) ? (uint64_t)rcount : 0;
+            j.inf_state[i] = rc ? 1u : 0u;
+        }
+    }
+}
+
+__global__ __launch_bounds__(64) void k_inflate(DeviceJob j) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    InfTabs* T = (InfTabs*)(lds + kInfRing);
+    inf_load_tab(T->crc_tab);
+    const uint32_t count = j.counters[16];
+    for (;;) {
+        const uint32_t i = wave_fetch_add(&j.counters[18], 1u);
+        if (i >= count) break;
+        if (uni32(j.inf_state[i])) continue;  // rejected by the sizing pass
+        const uint32_t b = uni32(j.inf_list[i]);
+        rpgpu_batch_result* R = &j.batches[b];
+        const uint64_t dst = uni64(j.dcap[b]), cap = uni64(j.dcap[b + 1]) - dst;
+        if (dst + cap > j.decoded_capacity) {
+            if (lane() == 0) R->flags = R->flags | RPGPU_F_DECODE_OVERFLOW;
+            continue;
+        }
+        InfIn in = inf_batch(j, R);
+        InfOut o;
+        o.ring = (inf_lds_u8*)lds;
+        o.tab = T->crc_tab;
+        o.dst = j.decoded + dst;
+        o.flushed = 0;
+        uint64_t total = 0;
+        const int rc = inflate_member<true>(in, T, o, total);
+        if (rc == 0 && lane() == 0) {
+            R->flags = R->flags | RPGPU_F_CODEC_OK;
+            R->decoded_len = (uint32_t)total;
+            R->reserved0 = 0;  // k_validate_decoded computes the decoded crc
+        }
+    }
+}
+
+hipError_t launch_inflate_plan(const DeviceJob& j, hipStream_t s, uint32_t grid) {
+    hipLaunchKernelGGL(k_inflate_plan, dim3(grid), dim3(64), kInfTabBytes, s, j);
+    return hipGetLastError();
+}
+
+hipError_t launch_inflate(const DeviceJob& j, hipStream_t s, uint32_t grid) {
+    static bool attr = false;
+    if (!attr) {
+        (void)hipFuncSetAttribute((const void*)k_inflate, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kInfLdsDecode);
+        attr = true;
+    }
+    hipLaunchKernelGGL(k_inflate, dim3(grid), dim3(64), kInfLdsDecode, s, j);
+    return hipGetLastError();
+}
+
+}  // namespace rp

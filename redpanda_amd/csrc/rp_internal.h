@@ -125,6 +125,9 @@ struct FramePlan {
     uint32_t csf;           // LZ4F: content size present
 };
 
+// job counters (DeviceJob::counters), zeroed per submit
+constexpr size_t kCounterBytes = 128;
+
 struct DeviceJob {
     const uint8_t* data;
     uint64_t data_len;            // bytes of d_data (= h_seg_offsets[n_segments])
@@ -156,7 +159,8 @@ struct DeviceJob {
                                   // [6] sequential frames, [7] linked frames, [8] k_lz_exec claim cursor,
                                   // [9] slab pool cursor, [10] k_lz_walk claim cursor, [11] long pieces,
                                   // [12] long-piece claim cursor, [13] k_validate_decoded claim cursor,
-                                  // [14] k_decode_finish claim cursor, [15] k_crc_split claim cursor
+                                  // [14] k_decode_finish claim cursor, [15] k_crc_split claim cursor,
+                                  // [16] gzip members (inf_list), [17] k_inflate_plan / [18] k_inflate claim cursors
     uint32_t* decode_list;        // batch_capacity: ordinals of batches to uncompress
     uint32_t* seq_list;           // batch_capacity: decode items decoded whole by one lane
     uint32_t* link_list;          // batch_capacity: decode items whose linked LZ4F blocks one wave decodes in order
@@ -178,6 +182,8 @@ struct DeviceJob {
     uint32_t* seg_first_bad;      // n_segments: first chain ordinal failing complete && crc_ok (atomicMin)
     const uint64_t* seeds;        // optional chain seeds (index-seeded discovery), per segment ascending
     const uint64_t* seed_off;     // n_segments + 1
+    uint32_t* inf_list;           // batch_capacity: ordinals of gzip batches (k_inflate_plan / k_inflate)
+    uint32_t* inf_state;          // batch_capacity: 1 = rejected by the sizing pass
 };
 
 // kernel launchers (rp_kernels.hip)
@@ -192,6 +198,9 @@ hipError_t launch_decode_blocks(const DeviceJob& j, hipStream_t s, uint32_t grid
 hipError_t launch_lz_walk(const DeviceJob& j, hipStream_t s, uint32_t grid);
 hipError_t launch_lz_exec(const DeviceJob& j, hipStream_t s);
 hipError_t launch_decode_finish(const DeviceJob& j, hipStream_t s, uint32_t grid);
+// gzip members (rp_inflate.hip): sizing pass before the slot scans, decode pass
+hipError_t launch_inflate_plan(const DeviceJob& j, hipStream_t s, uint32_t grid);
+hipError_t launch_inflate(const DeviceJob& j, hipStream_t s, uint32_t grid);
 // one payload, one wave (rpgpu_uncompress); res[0] = rc (0 / -1 / -2), res[1] = out_len
 hipError_t launch_uncompress_one(int codec, const uint8_t* src, uint64_t n, uint8_t* dst, uint64_t cap,
                                  int64_t* res, hipStream_t s);

@@ -572,7 +572,7 @@ __global__ __launch_bounds__(256) void k_emit(DeviceJob j) {
             if (complete) f |= RPGPU_F_COMPLETE;
             if (codec) f |= RPGPU_F_COMPRESSED;
             if (codec >= 5) f |= RPGPU_F_CODEC_INVALID;
-            if (complete && (codec == RPGPU_CODEC_GZIP || codec == RPGPU_CODEC_ZSTD)) f |= RPGPU_F_CODEC_UNSUPPORTED;
+            if (complete && codec == RPGPU_CODEC_ZSTD) f |= RPGPU_F_CODEC_UNSUPPORTED;
             r.flags = f;
             r.segment = s;
             // scratch for k_validate: absolute payload start (overwritten with
@@ -594,6 +594,9 @@ __global__ __launch_bounds__(256) void k_emit(DeviceJob j) {
             // decode work list for k_decode (order is irrelevant: every item
             // writes only its own batch and its own reserved arena slot)
             if (complete && decodable) j.decode_list[atomicAdd(&j.counters[2], 1u)] = (uint32_t)ord;
+            // gzip members: sized by k_inflate_plan (dcap / slots above are 0 until then)
+            if (complete && codec == RPGPU_CODEC_GZIP && (j.flags & RPGPU_JOB_DECODE))
+                j.inf_list[atomicAdd(&j.counters[16], 1u)] = (uint32_t)ord;
         }
         if (!complete) break;
         p += RPGPU_HEADER_SIZE + h.need;

@@ -464,11 +464,14 @@ int submit_body(rpgpu_ctx* c, const rpgpu_job* job, hipStream_t s, int stop, Pla
     const size_t o_segterm = take(nseg * sizeof(SegTerm));
     const size_t o_slots = take((bcap + 1) * 8);
     const size_t o_dcap = take((bcap + 1) * 8);
-    const size_t o_counters = take(64);
+    const size_t o_counters = take(kCounterBytes);
     const size_t o_dlist = take((bcap + 1) * 4);
     const size_t o_slist = take((bcap + 1) * 4);
     const size_t o_llist = take((bcap + 1) * 4);
     const size_t o_fbad = take((size_t)nseg * 4);
+    const bool decode_job = (job->flags & RPGPU_JOB_DECODE) != 0;
+    const size_t o_ilist = take(decode_job ? (bcap + 1) * 4 : 0);
+    const size_t o_istate = take(decode_job ? (bcap + 1) * 4 : 0);
     // block-parallel decode: one item per LZ4F block / snappy-java chunk
     const bool dec = (job->flags & RPGPU_JOB_DECODE) && job->d_decoded;
     const uint64_t data_len = job->h_seg_offsets[nseg];
@@ -567,6 +570,8 @@ int submit_body(rpgpu_ctx* c, const rpgpu_job* job, hipStream_t s, int stop, Pla
     j.seg_first_bad = (uint32_t*)(ws + o_fbad);
     j.seeds = (job->d_seeds && job->d_seed_offsets) ? job->d_seeds : nullptr;
     j.seed_off = j.seeds ? job->d_seed_offsets : nullptr;
+    j.inf_list = (uint32_t*)(ws + o_ilist);
+    j.inf_state = (uint32_t*)(ws + o_istate);
     j.blocks = (BlockItem*)(ws + o_blocks);
     j.block_capacity = (uint32_t)bl_cap64;
     j.plans = (FramePlan*)(ws + o_plans);
@@ -600,7 +605,7 @@ int submit_body(rpgpu_ctx* c, const rpgpu_job* job, hipStream_t s, int stop, Pla
         HIPCHK(c, hipEventRecord(ev[0], s));
     }
     STAGE("chunk_base", launch_chunk_base(j, s));
-    HIPCHK(c, hipMemsetAsync(j.counters, 0, 64, s));
+    HIPCHK(c, hipMemsetAsync(j.counters, 0, kCounterBytes, s));
     HIPCHK(c, hipMemsetAsync(j.seg_first_bad, 0xFF, (size_t)nseg * 4, s));
     STAGE("discover", launch_discover(j, s));
     if (tm) HIPCHK(c, hipEventRecord(ev[1], s));
@@ -613,6 +618,8 @@ int submit_body(rpgpu_ctx* c, const rpgpu_job* job, hipStream_t s, int stop, Pla
     }
     if (stop == kStopAfterCount) return RPGPU_OK;
     STAGE("emit", launch_emit(j, s));
+    // gzip members: the sizing pass (their arena bytes and index slots) before the scans
+    if (decode_job) STAGE("inflate_plan", launch_inflate_plan(j, s, c->cu_count * 16));
     const uint64_t* d_nb = j.chunk_count + tc;
     STAGE("scan_slots", scan_exclusive_u64_devn(j.slots, d_nb, bcap, scan_tmp, s));
     STAGE("scan_dcap", scan_exclusive_u64_devn(j.dcap, d_nb, bcap, scan_tmp, s));
@@ -625,6 +632,7 @@ int submit_body(rpgpu_ctx* c, const rpgpu_job* job, hipStream_t s, int stop, Pla
         STAGE("lz_walk", launch_lz_walk(j, s, c->cu_count * 16));
         STAGE("lz_exec", launch_lz_exec(j, s));
         STAGE("decode_finish", launch_decode_finish(j, s, c->cu_count * 8));
+        STAGE("inflate", launch_inflate(j, s, c->cu_count * 4));
     }
     if (tm) HIPCHK(c, hipEventRecord(ev[3], s));
     STAGE("validate", launch_validate(j, s, c->cu_count));

@@ -1353,7 +1353,8 @@ __global__ __launch_bounds__(256) void k_crc_combine(DeviceJob j) {
 // (BE40 byte 1) followed by the decoded bytes.
 __global__ __launch_bounds__(1024) void k_validate_decoded(DeviceJob j) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-    const uint32_t count = j.counters[2];
+    // the LZ4 / snappy decode list, then the gzip members
+    const uint32_t nlz = j.counters[2], count = nlz + j.counters[16];
     if (count == 0) return;
     const Tables* T = j.tables;
     init_lds_tables(lds, T);
@@ -1365,7 +1366,7 @@ __global__ __launch_bounds__(1024) void k_validate_decoded(DeviceJob j) {
     for (;;) {
         const uint32_t i = wave_fetch_add(&j.counters[13], 1u);
         if (i >= count) break;
-        const uint64_t b = uni32(j.decode_list[i]);
+        const uint64_t b = uni32(i < nlz ? j.decode_list[i] : j.inf_list[i - nlz]);
         rpgpu_batch_result* R = &j.batches[b];
         Desc d = desc_of(load_desc_raw(j, b));
         if (!(d.flags & RPGPU_F_CODEC_OK)) continue;

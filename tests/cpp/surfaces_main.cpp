@@ -252,8 +252,29 @@ int main(int argc, char** argv) {
                                   back->position_index == st.position_index && back->max_offset == st.max_offset &&
                                   back->max_timestamp == st.max_timestamp;
                 ser[ser.size() / 2] ^= 0x40;  // a flipped bit: checksum mismatch -> rebuild
-                const bool rejected = !storage::index_state::hydrate_from_buffer(ser.data(), ser.size());
+                bool rejected;  // nullopt, or a short read (the flip may land in a length field)
+                try {
+                    rejected = !storage::index_state::hydrate_from_buffer(ser.data(), ser.size());
+                } catch (const std::out_of_range&) {
+                    rejected = true;
+                }
                 std::printf("HYDRATE %d %d\n", same ? 1 : 0, rejected ? 1 : 0);
+                // short reads throw (the reference's iobuf_parser): an empty
+                // buffer, and a vsize past the bytes present
+                auto outcome = [](const std::vector<uint8_t>& b) {
+                    try {
+                        return storage::index_state::hydrate_from_buffer(b.data(), b.size()) ? "value" : "nullopt";
+                    } catch (const std::out_of_range&) {
+                        return "out_of_range";
+                    }
+                };
+                std::vector<uint8_t> shortv = st.checksum_and_serialize();
+                const size_t vs_at = 1 + 4 + 8 + 4 + 8 * 4;  // version, size, checksum, bitflags, 4 x i64
+                uint32_t vsz;
+                std::memcpy(&vsz, shortv.data() + vs_at, 4);
+                vsz += 1000;
+                std::memcpy(shortv.data() + vs_at, &vsz, 4);
+                std::printf("HYDRATE_SHORT %s %s\n", outcome(std::vector<uint8_t>()), outcome(shortv));
             }
             const storage::segment_index idx(std::move(st));
             for (int a = 4; a < argc; a++) {

@@ -521,9 +521,10 @@ def test_index_seeded_discovery(engine, oracle, rplib, kind):
 
 def test_serialize_wire(engine, oracle, rplib):
     """rpgpu_serialize_wire (kafka::writer_serialize_batch, response_writer.h:
-    241-276) == the restatement in tests/batchgen.disk_to_wire over whole
-    segments and over a sub-range; the record set validates in the wire
-    layout with the same verdicts."""
+    241-276) == the oracle's restatement (rpo_serialize_wire, over the
+    oracle's own job results) and the independent one in
+    tests/batchgen.disk_to_wire, over whole segments and over a sub-range;
+    the record set validates in the wire layout with the same verdicts."""
     import torch
     from tests import batchgen as bg
     MIX = (1 << abi.CODEC_NONE) | (1 << abi.CODEC_LZ4) | (1 << abi.CODEC_SNAPPY)
@@ -536,6 +537,8 @@ def test_serialize_wire(engine, oracle, rplib):
     engine.submit(d, offs, out, abi.JOB_CRC)
     torch.cuda.synchronize()
     want = b"".join(bg.disk_to_wire(s.tobytes()) for s in segs)
+    ref = oracle.run_job(data, offs, abi.JOB_CRC)
+    assert oracle.serialize_wire(data, offs, ref.batches) == want
     got = engine.serialize_wire(d, offs, out).cpu().numpy().tobytes()
     assert got == want
     h = out.to_host()
@@ -544,6 +547,7 @@ def test_serialize_wire(engine, oracle, rplib):
     b = h.batches
     lo = int(sum(int(x) for x in b["size_bytes"][:nb0 - 3]))
     assert sub == want[lo:lo + int(sum(int(x) for x in b["size_bytes"][nb0 - 3:nb0 + 4]))]
+    assert sub == oracle.serialize_wire(data, offs, ref.batches, first=nb0 - 3, n=7)
     wire = np.frombuffer(got, dtype=np.uint8).copy()
     wres = engine.validate(torch.from_numpy(wire).cuda(), [0, wire.size], abi.JOB_CRC | abi.JOB_PARSE,
                            layout=abi.LAYOUT_WIRE)
@@ -577,3 +581,59 @@ def test_large_batches_split_crc(engine, oracle, rplib, corrupt):
     got, ref = run_both(engine, oracle, segs, chunk=256 << 10)
     assert_same(got, ref)
     assert int(np.max(ref.batches["size_bytes"])) > 2 << 20
+
+
+# ---------------------------------------------------------------------------
+# gzip members decoded on the device (rp_inflate.hip): sizing pass + decode
+# pass against the oracle's zlib restatement (itself pinned against zlib by
+# tests/test_inflate_oracle.py)
+# ---------------------------------------------------------------------------
+GZ_WEIGHTS = [3, 3, 1, 2, 1, 1]  # none, gzip, snappy-java, lz4, zstd, raw snappy
+
+
+@pytest.mark.parametrize("seed", [0xC6, 31])
+def test_gzip_mix_decode(engine, oracle, rplib, seed):
+    """Segments mixing gzip with every other codec (zstd stays flagged
+    CODEC_UNSUPPORTED), payload corruptions: flags, new crc/header_crc,
+    index and arena bit-exact."""
+    segs = [gen(rplib, 3 << 20, i, seed=seed, batch_bytes=0, min_batch=200, max_batch=600000,
+                weights=GZ_WEIGHTS, corrupt_payload_ppm=(20000 if i == 1 else 0)) for i in range(3)]
+    got, ref = run_both(engine, oracle, segs, flags=DFLAGS, chunk=64 << 10)
+    codec = got.batches["attrs"] & 7
+    ok = (got.batches["flags"] & abi.F_CODEC_OK) != 0
+    assert np.any(ok & (codec == abi.CODEC_GZIP))
+    assert_same(got, ref, DFLAGS)
+
+
+def _gzip_batches(payloads, base=0):
+    """One disk batch per gzip payload, records = the decoded record count
+    when the payload decodes (else 3)."""
+    import zlib
+    from tests import batchgen as BG
+    out = bytearray()
+    for k, p in enumerate(payloads):
+        d = zlib.decompressobj(47)
+        try:
+            plain = d.decompress(p)
+        except zlib.error:
+            plain = b""
+        rc = max(1, plain.count(b"\x00") // 50) if plain else 3
+        out += BG.batch(p, rc, base_offset=base + 100 * k, attrs=abi.CODEC_GZIP)
+    return np.frombuffer(bytes(out), dtype=np.uint8).copy()
+
+
+def test_gzip_members_corpus(engine, oracle):
+    """Every corpus member (clean gzip / zlib of every deflate strategy, FHCRC /
+    FEXTRA / FNAME / FCOMMENT headers, truncations, bit flips, trailing data,
+    two members) as a batch payload: accept/reject, decoded bytes and the
+    decoded batch's crc / header_crc as the oracle's, walk included."""
+    from tests import batchgen as BG
+    from tests.gzip_corpus import clean_streams, gzip_member, mutated_streams
+    recs = [BG.simple_records(n, vlen=v, seed=n) for n, v in [(1, 10), (30, 40), (200, 300), (900, 900)]]
+    good = [gzip_member(r, lvl, strat, flags=fl) for r in recs for lvl, strat, fl in
+            [(6, 0, 0), (9, 1, 2), (1, 2, 8), (6, 3, 30), (0, 0, 0), (6, 4, 4)]]
+    segs = [_gzip_batches(good), _gzip_batches(clean_streams(9, 40, 40000)),
+            _gzip_batches(mutated_streams(13, 150)), _gzip_batches(mutated_streams(14, 150)[::-1])]
+    got, ref = run_both(engine, oracle, segs, flags=DFLAGS)
+    assert np.any((got.batches["flags"] & abi.F_PARSE_OK) != 0)
+    assert_same(got, ref, DFLAGS)
