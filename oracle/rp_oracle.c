@@ -8,6 +8,7 @@
 #define _GNU_SOURCE
 #include "rp_oracle.h"
 
+#include <dlfcn.h>
 #include <pthread.h>
 #include <stdlib.h>
 #include <string.h>
@@ -1195,6 +1196,71 @@ done:
 }
 #undef ZOUT
 
+/* ======================================================================== */
+/* zstd: stream_zstd::do_uncompress (compression/stream_zstd.cc:152-178)      */
+/* over libzstd (a system dependency; dlopen'd, the library not restated)     */
+/* ======================================================================== */
+typedef struct { const void* src; size_t size, pos; } rpo_zin;
+typedef struct { void* dst; size_t size, pos; } rpo_zout;
+static struct {
+    int tried;
+    size_t (*estimate)(size_t);
+    void* (*init_static)(void*, size_t);
+    size_t (*decompress_stream)(void*, rpo_zout*, rpo_zin*);
+    unsigned (*is_error)(size_t);
+} g_zstd;
+
+static int zstd_load(void) {
+    if (!g_zstd.tried) {
+        g_zstd.tried = 1;
+        void* h = dlopen("libzstd.so.1", RTLD_NOW | RTLD_LOCAL);
+        if (h) {
+            g_zstd.estimate = (size_t(*)(size_t))dlsym(h, "ZSTD_estimateDStreamSize");
+            g_zstd.init_static = (void* (*)(void*, size_t))dlsym(h, "ZSTD_initStaticDCtx");
+            g_zstd.decompress_stream = (size_t(*)(void*, rpo_zout*, rpo_zin*))dlsym(h, "ZSTD_decompressStream");
+            g_zstd.is_error = (unsigned (*)(size_t))dlsym(h, "ZSTD_isError");
+        }
+    }
+    return g_zstd.estimate && g_zstd.init_static && g_zstd.decompress_stream && g_zstd.is_error;
+}
+
+/* The reference's loop: a static DCtx over ZSTD_estimateDStreamSize(8 MiB)
+ * of workspace (zstd_decompress_workspace_bytes, config/configuration.cc:
+ * 911-916), a 64 KiB output buffer appended whenever it fills while input
+ * remains; an error only counts when the output buffer is not full. */
+int rpo_zstd_uncompress(const uint8_t* src, size_t n, uint8_t* dst, size_t cap, size_t* out_len) {
+    *out_len = 0;
+    if (!zstd_load()) return -3;
+    const size_t ws = g_zstd.estimate((size_t)8 << 20);
+    void* mem = malloc(ws + (64u << 10));
+    if (!mem) return -1;
+    uint8_t* obuf = (uint8_t*)mem + ws;
+    void* dctx = g_zstd.init_static(mem, ws);
+    int rc = dctx ? 0 : -1;
+    size_t total = 0;
+    rpo_zout o = {obuf, 64u << 10, 0};
+    rpo_zin i = {src, n, 0};
+    while (rc == 0 && i.pos != i.size) {
+        const size_t err = g_zstd.decompress_stream(dctx, &o, &i);
+        if (i.pos != i.size && o.pos == o.size) {
+            if (total + o.size <= cap) memcpy(dst + total, obuf, o.size);
+            total += o.size;
+            o.size = 64u << 10;
+            o.pos = 0;
+        } else if (g_zstd.is_error(err)) {
+            rc = -1;
+        }
+    }
+    if (rc == 0) {
+        if (total + o.pos <= cap) memcpy(dst + total, obuf, o.pos);
+        total += o.pos;
+        *out_len = total;
+        if (total > cap) rc = -2;
+    }
+    free(mem);
+    return rc;
+}
+
 int rpo_uncompress(int codec, const uint8_t* s, size_t n, uint8_t* dst, size_t cap, size_t* out_len) {
     /* compression/compression.cc:34-55 */
     *out_len = 0;
@@ -1203,6 +1269,7 @@ int rpo_uncompress(int codec, const uint8_t* s, size_t n, uint8_t* dst, size_t c
     case RPGPU_CODEC_GZIP: return rpo_gzip_uncompress(s, n, dst, cap, out_len);
     case RPGPU_CODEC_SNAPPY: return rpo_snappy_java_uncompress(s, n, dst, cap, out_len);
     case RPGPU_CODEC_LZ4: return rpo_lz4f_uncompress(s, n, dst, cap, out_len);
+    case RPGPU_CODEC_ZSTD: return rpo_zstd_uncompress(s, n, dst, cap, out_len);
     default: return -1;
     }
 }
@@ -1215,6 +1282,16 @@ uint64_t rpo_gzip_plan(const uint8_t* s, size_t n) {
     size_t total = 0;
     if (n == 0) return 0;
     if (rpo_gzip_uncompress(s, n, NULL, 0, &total) == -1) return 0;
+    return ((uint64_t)total + 15) & ~(uint64_t)15;
+}
+
+/* ... and for a host-decoded zstd payload: its decoded size rounded up to
+ * 16, 0 when the reference throws */
+uint64_t rpo_zstd_plan(const uint8_t* s, size_t n) {
+    size_t total = 0;
+    if (n == 0) return 0;
+    const int rc = rpo_zstd_uncompress(s, n, NULL, 0, &total);
+    if (rc != 0 && rc != -2) return 0;
     return ((uint64_t)total + 15) & ~(uint64_t)15;
 }
 
@@ -1387,7 +1464,9 @@ int64_t rpo_scan_segment_layout(const uint8_t* seg, uint64_t len, uint32_t segme
         const int may_walk = !wire || (r->flags & RPGPU_F_CRC_OK);
         if (codec) r->flags |= RPGPU_F_COMPRESSED;
         if (codec >= 5) r->flags |= RPGPU_F_CODEC_INVALID;
-        if (codec == RPGPU_CODEC_ZSTD) r->flags |= RPGPU_F_CODEC_UNSUPPORTED;
+        /* zstd: decoded on the host with RPGPU_JOB_HOST_CODECS, else not at all */
+        const int host_codec = (job_flags & RPGPU_JOB_DECODE) && (job_flags & RPGPU_JOB_HOST_CODECS);
+        if (codec == RPGPU_CODEC_ZSTD && !host_codec) r->flags |= RPGPU_F_CODEC_UNSUPPORTED;
 
         /* Plan (engine rule, see DESIGN.md "index and arena planning"): the
          * record-index slots and decode-arena bytes of a batch are reserved
@@ -1395,13 +1474,16 @@ int64_t rpo_scan_segment_layout(const uint8_t* seg, uint64_t len, uint32_t segme
          * the GPU can assign them with prefix sums.  Reservations never depend
          * on whether the decode or the walk later succeed. */
         uint64_t slots = 0, cap = 0;
-        int decodable = (codec == RPGPU_CODEC_LZ4 || codec == RPGPU_CODEC_SNAPPY || codec == RPGPU_CODEC_GZIP) &&
-                        (job_flags & RPGPU_JOB_DECODE);
+        int decodable = ((codec == RPGPU_CODEC_LZ4 || codec == RPGPU_CODEC_SNAPPY || codec == RPGPU_CODEC_GZIP) &&
+                         (job_flags & RPGPU_JOB_DECODE)) ||
+                        (codec == RPGPU_CODEC_ZSTD && host_codec);
         if (codec == 0) {
             if ((job_flags & RPGPU_JOB_PARSE) && h.record_count > 0 && (uint64_t)h.record_count <= need)
                 slots = (uint64_t)h.record_count;
         } else if (decodable) {
-            cap = codec == RPGPU_CODEC_GZIP ? rpo_gzip_plan(payload, need) : rpo_decode_capacity((int)codec, payload, need);
+            cap = codec == RPGPU_CODEC_GZIP ? rpo_gzip_plan(payload, need)
+                : codec == RPGPU_CODEC_ZSTD ? rpo_zstd_plan(payload, need)
+                : rpo_decode_capacity((int)codec, payload, need);
             if ((job_flags & RPGPU_JOB_PARSE) && h.record_count > 0 && (uint64_t)h.record_count <= cap)
                 slots = (uint64_t)h.record_count;
         }

@@ -104,8 +104,13 @@ int rpo_lz4_block_decode(const uint8_t* src, size_t n, uint8_t* dst, size_t dst_
 /* decode-arena reservation for one compressed payload (engine plan rule,
  * shared with the GPU planner; see DESIGN.md "decode arena") */
 uint64_t rpo_decode_capacity(int codec, const uint8_t* src, size_t n);
-/* the same for a gzip member (the engine's sizing pass) */
+/* the same for a gzip member (the engine's sizing pass) and a host-decoded
+ * zstd payload */
 uint64_t rpo_gzip_plan(const uint8_t* src, size_t n);
+uint64_t rpo_zstd_plan(const uint8_t* src, size_t n);
+/* stream_zstd::do_uncompress (compression/stream_zstd.cc:152-178) over
+ * libzstd (dlopen'd); -3 when libzstd is absent */
+int rpo_zstd_uncompress(const uint8_t* src, size_t n, uint8_t* dst, size_t cap, size_t* out_len);
 
 /* --- segment pipeline: continuous_batch_parser::consume
  *     (storage/parser.cc:96-254) driving checksumming_consumer

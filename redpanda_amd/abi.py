@@ -46,6 +46,7 @@ PARSE_ERR_INDEX_CAPACITY = 5
 JOB_CRC = 1 << 0
 JOB_PARSE = 1 << 1
 JOB_DECODE = 1 << 2
+JOB_HOST_CODECS = 1 << 3
 
 LAYOUT_DISK = 0
 LAYOUT_WIRE = 1

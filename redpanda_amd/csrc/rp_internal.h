@@ -160,7 +160,8 @@ struct DeviceJob {
                                   // [9] slab pool cursor, [10] k_lz_walk claim cursor, [11] long pieces,
                                   // [12] long-piece claim cursor, [13] k_validate_decoded claim cursor,
                                   // [14] k_decode_finish claim cursor, [15] k_crc_split claim cursor,
-                                  // [16] gzip members (inf_list), [17] k_inflate_plan / [18] k_inflate claim cursors
+                                  // [16] gzip members (inf_list), [17] k_inflate_plan / [18] k_inflate claim cursors,
+                                  // [19] host-decoded members (host_list)
     uint32_t* decode_list;        // batch_capacity: ordinals of batches to uncompress
     uint32_t* seq_list;           // batch_capacity: decode items decoded whole by one lane
     uint32_t* link_list;          // batch_capacity: decode items whose linked LZ4F blocks one wave decodes in order
@@ -184,7 +185,26 @@ struct DeviceJob {
     const uint64_t* seed_off;     // n_segments + 1
     uint32_t* inf_list;           // batch_capacity: ordinals of gzip batches (k_inflate_plan / k_inflate)
     uint32_t* inf_state;          // batch_capacity: 1 = rejected by the sizing pass
+    uint32_t* host_list;          // batch_capacity: ordinals of host-decoded (zstd) batches (RPGPU_JOB_HOST_CODECS)
 };
+
+// one host-decoded batch (RPGPU_JOB_HOST_CODECS): its payload, the host's
+// verdict and where its bytes sit in the staging buffers
+struct HostItem {
+    uint64_t src;        // payload offset in d_data
+    uint64_t stage;      // offset in the payload / decoded staging
+    uint64_t out_len;    // decoded bytes
+    uint64_t cap;        // arena reservation (0 when rejected)
+    uint32_t n;          // payload bytes
+    uint32_t ord;        // batch ordinal
+    int32_t record_count;
+    int32_t status;      // 0 decoded, -1 the reference throws
+};
+hipError_t launch_host_desc(const DeviceJob& j, HostItem* items, uint32_t n, hipStream_t s);
+hipError_t launch_host_gather(const DeviceJob& j, const HostItem* items, uint32_t n, uint8_t* stage, hipStream_t s);
+hipError_t launch_host_patch(const DeviceJob& j, const HostItem* items, uint32_t n, hipStream_t s);
+hipError_t launch_host_scatter(const DeviceJob& j, const HostItem* items, uint32_t n, const uint8_t* stage,
+                               hipStream_t s);
 
 // kernel launchers (rp_kernels.hip)
 hipError_t launch_chunk_base(const DeviceJob& j, hipStream_t s);

@@ -572,7 +572,8 @@ __global__ __launch_bounds__(256) void k_emit(DeviceJob j) {
             if (complete) f |= RPGPU_F_COMPLETE;
             if (codec) f |= RPGPU_F_COMPRESSED;
             if (codec >= 5) f |= RPGPU_F_CODEC_INVALID;
-            if (complete && codec == RPGPU_CODEC_ZSTD) f |= RPGPU_F_CODEC_UNSUPPORTED;
+            const bool host_codec = (j.flags & RPGPU_JOB_DECODE) && (j.flags & RPGPU_JOB_HOST_CODECS);
+            if (complete && codec == RPGPU_CODEC_ZSTD && !host_codec) f |= RPGPU_F_CODEC_UNSUPPORTED;
             r.flags = f;
             r.segment = s;
             // scratch for k_validate: absolute payload start (overwritten with
@@ -597,6 +598,9 @@ __global__ __launch_bounds__(256) void k_emit(DeviceJob j) {
             // gzip members: sized by k_inflate_plan (dcap / slots above are 0 until then)
             if (complete && codec == RPGPU_CODEC_GZIP && (j.flags & RPGPU_JOB_DECODE))
                 j.inf_list[atomicAdd(&j.counters[16], 1u)] = (uint32_t)ord;
+            // zstd members with RPGPU_JOB_HOST_CODECS: decoded by the host step
+            if (complete && codec == RPGPU_CODEC_ZSTD && host_codec)
+                j.host_list[atomicAdd(&j.counters[19], 1u)] = (uint32_t)ord;
         }
         if (!complete) break;
         p += RPGPU_HEADER_SIZE + h.need;
@@ -790,6 +794,89 @@ __global__ void k_finalize_totals(DeviceJob j) {
     t.n_rewalks = j.counters[0];
     t.reserved[0] = t.reserved[1] = 0;
     *j.totals = t;
+}
+
+// ---------------------------------------------------------------------------
+// Host-decoded batches (RPGPU_JOB_HOST_CODECS: zstd).  The runtime reads the
+// host list's descriptors, gathers the payloads into staging, decodes them
+// on the host and hands the results back; these kernels do the device side.
+// ---------------------------------------------------------------------------
+// descriptor of host item i: payload offset in d_data, bytes, batch ordinal,
+// record_count
+__global__ __launch_bounds__(256) void k_host_desc(DeviceJob j, HostItem* items) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= j.counters[19]) return;
+    const uint32_t b = j.host_list[i];
+    const rpgpu_batch_result& R = j.batches[b];
+    HostItem it;
+    it.src = j.seg_off[R.segment] + R.file_pos + RPGPU_HEADER_SIZE;
+    it.n = (uint32_t)(R.size_bytes - (int32_t)RPGPU_HEADER_SIZE);
+    it.ord = b;
+    it.record_count = R.record_count;
+    it.status = 0;
+    it.stage = 0;
+    it.out_len = 0;
+    it.cap = 0;
+    items[i] = it;
+}
+
+// payload of item i to staging + items[i].stage (one wave per item)
+__global__ __launch_bounds__(256) void k_host_gather(DeviceJob j, const HostItem* items, uint32_t n, uint8_t* stage) {
+    const uint32_t i = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (i >= n) return;
+    const uint8_t* s = j.data + items[i].src;
+    uint8_t* d = stage + items[i].stage;
+    for (uint64_t k = threadIdx.x & 63; k < items[i].n; k += 64) d[k] = s[k];
+}
+
+// the host's verdicts: arena reservation and index slots, before the scans
+__global__ __launch_bounds__(256) void k_host_patch(DeviceJob j, const HostItem* items, uint32_t n) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const HostItem it = items[i];
+    j.dcap[it.ord] = it.cap;
+    j.slots[it.ord] = ((j.flags & RPGPU_JOB_PARSE) && it.record_count > 0 && (uint64_t)it.record_count <= it.cap)
+                          ? (uint64_t)it.record_count
+                          : 0;
+}
+
+// decoded bytes from staging into the arena slots (one wave per item)
+__global__ __launch_bounds__(256) void k_host_scatter(DeviceJob j, const HostItem* items, uint32_t n,
+                                                      const uint8_t* stage) {
+    const uint32_t i = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (i >= n) return;
+    const HostItem it = items[i];
+    if (it.status != 0) return;
+    rpgpu_batch_result* R = &j.batches[it.ord];
+    const uint64_t dst = j.dcap[it.ord];
+    if (dst + it.cap > j.decoded_capacity) {
+        if ((threadIdx.x & 63) == 0) R->flags = R->flags | RPGPU_F_DECODE_OVERFLOW;
+        return;
+    }
+    for (uint64_t k = threadIdx.x & 63; k < it.out_len; k += 64) j.decoded[dst + k] = stage[it.stage + k];
+    if ((threadIdx.x & 63) == 0) {
+        R->flags = R->flags | RPGPU_F_CODEC_OK;
+        R->decoded_len = (uint32_t)it.out_len;
+        R->reserved0 = 0;
+    }
+}
+
+hipError_t launch_host_desc(const DeviceJob& j, HostItem* items, uint32_t n, hipStream_t s) {
+    if (n) hipLaunchKernelGGL(k_host_desc, dim3((n + 255) / 256), dim3(256), 0, s, j, items);
+    return hipGetLastError();
+}
+hipError_t launch_host_gather(const DeviceJob& j, const HostItem* items, uint32_t n, uint8_t* stage, hipStream_t s) {
+    if (n) hipLaunchKernelGGL(k_host_gather, dim3((n + 3) / 4), dim3(256), 0, s, j, items, n, stage);
+    return hipGetLastError();
+}
+hipError_t launch_host_patch(const DeviceJob& j, const HostItem* items, uint32_t n, hipStream_t s) {
+    if (n) hipLaunchKernelGGL(k_host_patch, dim3((n + 255) / 256), dim3(256), 0, s, j, items, n);
+    return hipGetLastError();
+}
+hipError_t launch_host_scatter(const DeviceJob& j, const HostItem* items, uint32_t n, const uint8_t* stage,
+                               hipStream_t s) {
+    if (n) hipLaunchKernelGGL(k_host_scatter, dim3((n + 3) / 4), dim3(256), 0, s, j, items, n, stage);
+    return hipGetLastError();
 }
 
 // ---------------------------------------------------------------------------

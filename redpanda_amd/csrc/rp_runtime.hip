@@ -182,6 +182,14 @@ struct rpgpu_ctx {
     size_t sth_bytes = 0;
     void* std_ = nullptr;
     size_t std_bytes = 0;
+    // RPGPU_JOB_HOST_CODECS: the host step's items and staging (device and
+    // pinned host, grow-only); hc_n = items of the job being enqueued
+    struct Grow {
+        void* p = nullptr;
+        size_t bytes = 0;
+        bool pinned = false;
+    } hc_items, hc_items_h, hc_in, hc_in_h, hc_out, hc_out_h, hc_small;
+    uint32_t hc_n = 0;
 };
 
 namespace {
@@ -292,6 +300,8 @@ int rpgpu_destroy(rpgpu_ctx* c) {
     if (c->sth) hipHostFree(c->sth);
     if (c->std_) hipFree(c->std_);
     if (c->d_tables) hipFree(c->d_tables);
+    for (auto* g : {&c->hc_items, &c->hc_items_h, &c->hc_in, &c->hc_in_h, &c->hc_out, &c->hc_out_h, &c->hc_small})
+        if (g->p) (void)(g->pinned ? hipHostFree(g->p) : hipFree(g->p));
     if (c->ws_ev) { (void)hipEventSynchronize(c->ws_ev); (void)hipEventDestroy(c->ws_ev); }
     for (auto& set : c->ev_sets)
         for (auto& e : set) hipEventDestroy(e);
@@ -434,6 +444,107 @@ int submit_impl(rpgpu_ctx* c, const rpgpu_job* job, void* stream, int stop, Plan
     return rc ? rc : rr;
 }
 
+// grow-only device or pinned host buffer (the stream is drained before a
+// device buffer is replaced: earlier work on the context may still use it)
+int grow_buf(rpgpu_ctx* c, rpgpu_ctx::Grow& g, size_t want, bool pinned, hipStream_t s) {
+    if (want <= g.bytes && g.p) return RPGPU_OK;
+    if (g.p) {
+        if (int rc = ws_drain(c, s)) return rc;
+        (void)(g.pinned ? hipHostFree(g.p) : hipFree(g.p));
+        g.p = nullptr;
+        g.bytes = 0;
+    }
+    want = std::max<size_t>(align_up(want + want / 4, 4096), 4096);
+    const hipError_t e = pinned ? hipHostMalloc(&g.p, want, hipHostMallocDefault) : hipMalloc(&g.p, want);
+    if (e != hipSuccess) { g.p = nullptr; return fail(c, RPGPU_E_NOMEM, "host codec staging"); }
+    g.bytes = want;
+    g.pinned = pinned;
+    return RPGPU_OK;
+}
+
+// RPGPU_JOB_HOST_CODECS: the batches k_emit put on the host list (zstd) cross
+// to the host, are decoded by stream_zstd::do_uncompress's loop over libzstd
+// (rp_hostcodec.cpp; compression/stream_zstd.cc:152-178) on a few threads,
+// and come back: their arena reservations and index slots are patched in
+// before the scans (the same rule as every codec: the decoded size rounded up
+// to 16, 0 when the reference throws), the bytes wait in device staging for
+// k_host_scatter.  Synchronizes the stream three times.
+int host_codec_step(rpgpu_ctx* c, const DeviceJob& j, hipStream_t s) {
+    if (int rc = grow_buf(c, c->hc_small, 64, true, s)) return rc;
+    uint32_t* cnt = (uint32_t*)c->hc_small.p;
+    HIPCHK(c, hipMemcpyAsync(cnt, j.counters + 19, 4, hipMemcpyDeviceToHost, s));
+    HIPCHK(c, hipStreamSynchronize(s));
+    const uint32_t n = *cnt;
+    if (n == 0) return RPGPU_OK;
+    const size_t ib = (size_t)n * sizeof(HostItem);
+    if (int rc = grow_buf(c, c->hc_items, ib, false, s)) return rc;
+    if (int rc = grow_buf(c, c->hc_items_h, ib, true, s)) return rc;
+    HostItem* dit = (HostItem*)c->hc_items.p;
+    HostItem* hit = (HostItem*)c->hc_items_h.p;
+    HIPCHK(c, launch_host_desc(j, dit, n, s));
+    HIPCHK(c, hipMemcpyAsync(hit, dit, ib, hipMemcpyDeviceToHost, s));
+    HIPCHK(c, hipStreamSynchronize(s));
+    uint64_t in_total = 0;
+    for (uint32_t i = 0; i < n; i++) {
+        hit[i].stage = in_total;
+        in_total += align_up(hit[i].n, 16);
+    }
+    if (int rc = grow_buf(c, c->hc_in, in_total + 16, false, s)) return rc;
+    if (int rc = grow_buf(c, c->hc_in_h, in_total + 16, true, s)) return rc;
+    HIPCHK(c, hipMemcpyAsync(dit, hit, ib, hipMemcpyHostToDevice, s));
+    HIPCHK(c, launch_host_gather(j, dit, n, (uint8_t*)c->hc_in.p, s));
+    HIPCHK(c, hipMemcpyAsync(c->hc_in_h.p, c->hc_in.p, in_total, hipMemcpyDeviceToHost, s));
+    HIPCHK(c, hipStreamSynchronize(s));
+    // decode: compressor::uncompress throws on an empty payload
+    // (compression/compression.cc:34-55), then the reference loop
+    std::vector<std::vector<uint8_t>> outs(n);
+    const uint8_t* in = (const uint8_t*)c->hc_in_h.p;
+    std::atomic<uint32_t> next{0};
+    auto work = [&]() {
+        for (uint32_t i; (i = next.fetch_add(1)) < n;) {
+            HostItem& it = hit[i];
+            it.status = -1;
+            it.out_len = 0;
+            if (it.n == 0) continue;
+            std::vector<uint8_t>& o = outs[i];
+            o.resize((size_t)it.n * 4 + 4096);
+            size_t len = 0;
+            int rc = host_uncompress(kHostZstd, in + it.stage, it.n, o.data(), o.size(), &len);
+            if (rc == kHostCodecOverflow) {
+                o.resize(len);
+                rc = host_uncompress(kHostZstd, in + it.stage, it.n, o.data(), o.size(), &len);
+            }
+            if (rc == 0) {
+                it.status = 0;
+                it.out_len = len;
+            }
+        }
+    };
+    const uint32_t nt = std::min<uint32_t>(std::max(1u, std::min(16u, std::thread::hardware_concurrency())), n);
+    std::vector<std::thread> pool;
+    for (uint32_t t = 1; t < nt; t++) pool.emplace_back(work);
+    work();
+    for (auto& t : pool) t.join();
+    uint64_t out_total = 0;
+    for (uint32_t i = 0; i < n; i++) {
+        HostItem& it = hit[i];
+        it.cap = it.status == 0 ? align_up(it.out_len, 16) : 0;
+        it.stage = out_total;
+        out_total += it.cap;
+    }
+    if (int rc = grow_buf(c, c->hc_out, out_total + 16, false, s)) return rc;
+    if (int rc = grow_buf(c, c->hc_out_h, out_total + 16, true, s)) return rc;
+    for (uint32_t i = 0; i < n; i++)
+        if (hit[i].status == 0) memcpy((uint8_t*)c->hc_out_h.p + hit[i].stage, outs[i].data(), hit[i].out_len);
+    HIPCHK(c, hipMemcpyAsync(c->hc_out.p, c->hc_out_h.p, out_total, hipMemcpyHostToDevice, s));
+    HIPCHK(c, hipMemcpyAsync(dit, hit, ib, hipMemcpyHostToDevice, s));
+    HIPCHK(c, launch_host_patch(j, dit, n, s));
+    // the pinned copies are read by the copies just queued: done before this
+    // context's next host step rewrites them (it syncs the stream first)
+    c->hc_n = n;
+    return RPGPU_OK;
+}
+
 int submit_body(rpgpu_ctx* c, const rpgpu_job* job, hipStream_t s, int stop, PlanPtrs* plan) {
     if (!c || !job || !job->d_data || !job->d_seg_offsets || !job->h_seg_offsets || job->n_segments == 0 ||
         !job->d_batches || !job->d_summaries || !job->d_totals)
@@ -472,6 +583,8 @@ int submit_body(rpgpu_ctx* c, const rpgpu_job* job, hipStream_t s, int stop, Pla
     const bool decode_job = (job->flags & RPGPU_JOB_DECODE) != 0;
     const size_t o_ilist = take(decode_job ? (bcap + 1) * 4 : 0);
     const size_t o_istate = take(decode_job ? (bcap + 1) * 4 : 0);
+    const bool host_job = decode_job && (job->flags & RPGPU_JOB_HOST_CODECS);
+    const size_t o_hlist = take(host_job ? (bcap + 1) * 4 : 0);
     // block-parallel decode: one item per LZ4F block / snappy-java chunk
     const bool dec = (job->flags & RPGPU_JOB_DECODE) && job->d_decoded;
     const uint64_t data_len = job->h_seg_offsets[nseg];
@@ -572,6 +685,8 @@ int submit_body(rpgpu_ctx* c, const rpgpu_job* job, hipStream_t s, int stop, Pla
     j.seed_off = j.seeds ? job->d_seed_offsets : nullptr;
     j.inf_list = (uint32_t*)(ws + o_ilist);
     j.inf_state = (uint32_t*)(ws + o_istate);
+    j.host_list = (uint32_t*)(ws + o_hlist);
+    c->hc_n = 0;
     j.blocks = (BlockItem*)(ws + o_blocks);
     j.block_capacity = (uint32_t)bl_cap64;
     j.plans = (FramePlan*)(ws + o_plans);
@@ -620,6 +735,10 @@ int submit_body(rpgpu_ctx* c, const rpgpu_job* job, hipStream_t s, int stop, Pla
     STAGE("emit", launch_emit(j, s));
     // gzip members: the sizing pass (their arena bytes and index slots) before the scans
     if (decode_job) STAGE("inflate_plan", launch_inflate_plan(j, s, c->cu_count * 16));
+    // zstd members (RPGPU_JOB_HOST_CODECS): decoded on the host now, sized
+    // before the scans like every other payload
+    if (host_job)
+        if (int rc = host_codec_step(c, j, s)) return rc;
     const uint64_t* d_nb = j.chunk_count + tc;
     STAGE("scan_slots", scan_exclusive_u64_devn(j.slots, d_nb, bcap, scan_tmp, s));
     STAGE("scan_dcap", scan_exclusive_u64_devn(j.dcap, d_nb, bcap, scan_tmp, s));
@@ -633,6 +752,8 @@ int submit_body(rpgpu_ctx* c, const rpgpu_job* job, hipStream_t s, int stop, Pla
         STAGE("lz_exec", launch_lz_exec(j, s));
         STAGE("decode_finish", launch_decode_finish(j, s, c->cu_count * 8));
         STAGE("inflate", launch_inflate(j, s, c->cu_count * 4));
+        if (c->hc_n) STAGE("host_scatter", launch_host_scatter(j, (const HostItem*)c->hc_items.p, c->hc_n,
+                                                               (const uint8_t*)c->hc_out.p, s));
     }
     if (tm) HIPCHK(c, hipEventRecord(ev[3], s));
     STAGE("validate", launch_validate(j, s, c->cu_count));

@@ -832,8 +832,17 @@ DEV void note_bad_lane(const J& j, uint32_t seg, uint64_t b) {
 // instruction).  Row r of lane w's region lands at slot + 96 w + 16 r.  Two
 // slots per wave alternate by step parity: H (C_{k-1}, the record's head)
 // and C_k (loaded this step).
-constexpr uint32_t kRegionRows = 6u;
+// 6 rows: 48 bytes before the guessed end (record k's headers) and 48 after
+// it (record k + 1's length .. value length).  5-row regions (48 / 32: 10 KiB
+// of LDS per wave, four workgroups per CU instead of three) measured slower
+// on C1 (walk 1.34 -> 1.49 ms): the walk is not short of walks in flight.
+#ifndef RPGPU_WALK_ROWS
+#define RPGPU_WALK_ROWS 6
+#endif
+constexpr uint32_t kRegionRows = RPGPU_WALK_ROWS;
 constexpr uint32_t kRegionBytes = 16u * kRegionRows;
+constexpr uint32_t kRegionBefore = 48u;  // bytes of C_k before the 16-aligned guessed end
+static_assert(kRegionBytes > kRegionBefore && 64u * kRegionBytes >= 4096u, "region / staging geometry");
 constexpr uint32_t kRegionReach = kRegionBytes - 16u;  // a read needs 16 bytes from its offset
 constexpr uint32_t kSlotBytes = 64u * kRegionBytes;
 constexpr uint32_t kWalkLdsWave = 2u * kSlotBytes;
@@ -1028,7 +1037,7 @@ DEV uint32_t lane_c_base(const LaneWalk& w, const uint8_t* H) {
         if (len >= 0 && (uint64_t)len <= n) guess = start + br + (uint32_t)len;
     }
     const uint32_t e16 = (guess + mis + 15u) & ~15u;
-    return (guess != 0xFFFFFFFFu && e16 >= w.h_base + kRegionBytes / 2u) ? e16 - kRegionBytes / 2u : w.h_base;
+    return (guess != 0xFFFFFFFFu && e16 >= w.h_base + kRegionBefore) ? e16 - kRegionBefore : w.h_base;
 }
 
 // One record of a lane walk (w.total > 0), H and C_k in LDS: parse the record
@@ -1354,7 +1363,7 @@ __global__ __launch_bounds__(256) void k_crc_combine(DeviceJob j) {
 __global__ __launch_bounds__(1024) void k_validate_decoded(DeviceJob j) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     // the LZ4 / snappy decode list, then the gzip members
-    const uint32_t nlz = j.counters[2], count = nlz + j.counters[16];
+    const uint32_t nlz = j.counters[2], ngz = j.counters[16], count = nlz + ngz + j.counters[19];
     if (count == 0) return;
     const Tables* T = j.tables;
     init_lds_tables(lds, T);
@@ -1366,7 +1375,7 @@ __global__ __launch_bounds__(1024) void k_validate_decoded(DeviceJob j) {
     for (;;) {
         const uint32_t i = wave_fetch_add(&j.counters[13], 1u);
         if (i >= count) break;
-        const uint64_t b = uni32(i < nlz ? j.decode_list[i] : j.inf_list[i - nlz]);
+        const uint64_t b = uni32(i < nlz ? j.decode_list[i] : i < nlz + ngz ? j.inf_list[i - nlz] : j.host_list[i - nlz - ngz]);
         rpgpu_batch_result* R = &j.batches[b];
         Desc d = desc_of(load_desc_raw(j, b));
         if (!(d.flags & RPGPU_F_CODEC_OK)) continue;

@@ -637,3 +637,24 @@ def test_gzip_members_corpus(engine, oracle):
     got, ref = run_both(engine, oracle, segs, flags=DFLAGS)
     assert np.any((got.batches["flags"] & abi.F_PARSE_OK) != 0)
     assert_same(got, ref, DFLAGS)
+
+
+@pytest.mark.parametrize("host", [False, True])
+def test_zstd_host_codec_job(engine, oracle, rplib, host):
+    """zstd batches inside a job: with RPGPU_JOB_HOST_CODECS decoded on the
+    host (stream_zstd::do_uncompress over libzstd) into the same arena, then
+    CRC'd and walked on the device; without it flagged CODEC_UNSUPPORTED.
+    Bit flips in some payloads exercise the reject path."""
+    weights = [2, 1, 1, 1, 4, 1]
+    segs = [gen(rplib, 2 << 20, i, seed=0x25D + i, batch_bytes=0, min_batch=200, max_batch=400000,
+                weights=weights, corrupt_payload_ppm=(30000 if i == 1 else 0)) for i in range(3)]
+    flags = DFLAGS | (abi.JOB_HOST_CODECS if host else 0)
+    got, ref = run_both(engine, oracle, segs, flags=flags, chunk=64 << 10)
+    z = (got.batches["attrs"] & 7) == abi.CODEC_ZSTD
+    assert np.any(z)
+    if host:
+        assert np.any(z & ((got.batches["flags"] & abi.F_CODEC_OK) != 0))
+        assert not np.any(got.batches["flags"] & abi.F_CODEC_UNSUPPORTED)
+    else:
+        assert np.all((got.batches["flags"][z] & abi.F_CODEC_UNSUPPORTED) != 0)
+    assert_same(got, ref, flags)
