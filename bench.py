@@ -201,12 +201,12 @@ def sized_outputs(eng, data, offs, flags, nseg, est_batches, torch, device):
     raise RuntimeError("output sizing did not converge")
 
 
-def run_compressed(name, kw, n_parts, seg_bytes, args, torch, device, eng, abi, desc):
-    """One compressed workload stanza (C2 / C5) on this GPU."""
+def run_compressed(name, kw, n_parts, seg_bytes, args, torch, device, eng, abi, desc, extra_flags=0):
+    """One compressed workload stanza (C2 / C5 / C6) on this GPU."""
     t0 = time.time()
     data, offs, counts, host_first = gen_partitions(list(range(n_parts)), seg_bytes, kw, torch, device)
     log(f"[{name}] generated {n_parts} x {seg_bytes >> 20} MiB ({sum(counts)} batches) in {time.time() - t0:.1f}s")
-    flags = abi.JOB_CRC | abi.JOB_PARSE | abi.JOB_DECODE
+    flags = abi.JOB_CRC | abi.JOB_PARSE | abi.JOB_DECODE | extra_flags
     d_offs = torch.from_numpy(offs.view(np.int64)).to(device)
     out = sized_outputs(eng, data, offs, flags, n_parts, int(offs[-1]) // 4096 + 4096, torch, device)
     for _ in range(args.warmup):
@@ -258,7 +258,7 @@ def run_compressed(name, kw, n_parts, seg_bytes, args, torch, device, eng, abi, 
     whole_alg = stored + decoded + IDX_BYTES_PER_RECORD * n_rec + RESULT_BYTES_PER_BATCH * len(b)
     traffic, kernels_traffic = profiled_traffic("decode_traffic.json", name, DECODE_KERNELS)
     cpu = None
-    if not args.no_cpu_baseline and len(positions):
+    if not args.no_cpu_baseline and len(positions) and name != "c6":
         cpu = cpu_baseline_decode(host_first, positions)
     write_stats(args, name, {"stored": stored, "stored_payload": int(np.sum(b["size_bytes"].astype(np.int64)
                                                                           - abi.HEADER_SIZE)),
@@ -296,6 +296,12 @@ def run_compressed(name, kw, n_parts, seg_bytes, args, torch, device, eng, abi, 
         "parity": parity,
         "cpu_baseline": cpu,
     }
+    if name == "c6":
+        codec = b["attrs"] & 7
+        st["per_codec"] = {str(c): {"batches": int(np.sum(codec == c)), "codec_ok": int(np.sum(dec_ok & (codec == c))),
+                                    "decoded_bytes": int(np.sum(b["decoded_len"].astype(np.int64)[dec_ok & (codec == c)]))}
+                           for c in (1, 2, 3, 4)}
+        st["cpu_baseline"] = None  # the liblz4 / libsnappy baseline does not cover gzip / zstd
     del out, data, d_offs
     torch.cuda.empty_cache()
     return st
@@ -351,6 +357,12 @@ def main():
                 "C2: 8 partitions x 1.5 GiB disk segments of LZ4 frames (64 KiB blocks, content size; 10% linked, "
                 "10% content checksum), decoded batches uniform 64 KiB..1 MiB, payload thirds random / alnum / "
                 "JSON-like (seed 0xC2): discover + header_crc + crc + LZ4F decode + decoded crc/header_crc + record walk")
+        if "c6" in workloads:
+            extra["c6"] = run_compressed(
+                "c6", synth.C6, C5_PARTS, C5_SEG, args, torch, device, eng, abi,
+                "C6 (C5 + gzip / zstd): 128 partitions x 64 MiB, log-uniform 200 B..1 MiB batches, none 32 / gzip 10 / "
+                "lz4 24 / snappy-java 12 / raw snappy 12 / zstd 10 (host, RPGPU_JOB_HOST_CODECS), 1% payload + 0.2% "
+                "header bit flips, 0.1% zeroed headers, truncated tails (seed 0xC6)", extra_flags=abi.JOB_HOST_CODECS)
         if "c5" in workloads:
             extra["c5"] = run_compressed(
                 "c5", synth.C5, C5_PARTS, C5_SEG, args, torch, device, eng, abi,

@@ -60,11 +60,17 @@ DEV uint32_t ieee_mulmod(uint32_t a, uint32_t b) {
     }
     return p;
 }
-// x^(8 n) mod P
-DEV uint32_t ieee_xpow8(uint32_t n) {
+// x^(8 n) mod P; x2n = kX2nIeee held one entry per lane (lane k: x^(2^k)):
+// a constant-memory table read per step is a vector load and a wait each
+// n may differ per lane: the loop runs wave-uniformly (a lane that has
+// finished its bits must still be there when the table is read across lanes)
+DEV uint32_t ieee_xpow8(uint32_t n, uint32_t x2n) {
     uint32_t p = 1u << 31;
-    for (uint32_t k = 3; n; n >>= 1, k = (k + 1) & 31u)
-        if (n & 1) p = ieee_mulmod(kX2nIeee[k], p);
+    for (uint32_t i = 0; i < 32; i++) {
+        if (__ballot((n >> i) != 0) == 0) break;
+        const uint32_t f = rl(x2n, (int)((3 + i) & 31u));
+        if ((n >> i) & 1) p = ieee_mulmod(f, p);
+    }
     return p;
 }
 
@@ -229,6 +235,9 @@ struct InfOut {
     uint32_t crc;         // raw register (init 0xFFFFFFFF)
     uint32_t ada, adb;    // Adler-32 sums
     bool gz;
+    uint32_t x2n;         // lane k: x^(2^k) mod P
+    uint32_t lane_mul;    // lane l: x^(8 (1024 - 16 (l + 1))): its 16 bytes moved to a full chunk's end
+    uint32_t chunk_mul;   // x^(8 * 1024)
 };
 
 // flush output bytes [o.flushed, o.flushed + len) (len <= 1024, the start
@@ -249,9 +258,10 @@ DEV void inf_flush(InfOut& o, uint32_t len) {
         for (uint32_t k = 0; k < 16; k++)
             if (k < t) c = o.tab[(c ^ (w[k >> 2] >> (8 * (k & 3)))) & 0xFFu] ^ (c >> 8);
         // lane l's raw CRC moved to the end of the piece: x^(8 (len - 16 l - t))
-        uint32_t x = t ? ieee_mulmod(ieee_xpow8(len - 16u * l - t), c) : 0u;
+        const bool full = len == 1024u;
+        uint32_t x = t ? ieee_mulmod(full ? o.lane_mul : ieee_xpow8(len - 16u * l - t, o.x2n), c) : 0u;
         x = wave_xor(x);
-        o.crc = ieee_mulmod(ieee_xpow8(len), o.crc) ^ uni32(x);
+        o.crc = ieee_mulmod(full ? o.chunk_mul : ieee_xpow8(len, o.x2n), o.crc) ^ uni32(x);
     } else {
         uint32_t s1 = 0, s2 = 0;
 #pragma unroll
@@ -300,8 +310,21 @@ DEV void inf_copy(InfOut& o, uint64_t op, uint32_t dist, uint32_t ml) {
 // check); true: the decode pass into `o`.  Returns -1 rejected, 0 accepted;
 // `total` = bytes produced.
 // ---------------------------------------------------------------------------
+// deflate's length / distance tables held one symbol per lane (base | extra
+// << 16): a v_readlane per symbol instead of a vector load and its wait
+struct InfSymTabs {
+    uint32_t len, dist;
+};
+DEV InfSymTabs inf_sym_tabs() {
+    const uint32_t l = lane();
+    InfSymTabs t;
+    t.len = l < 29 ? (uint32_t)kLenBase[l] | ((uint32_t)kLenExtra[l] << 16) : 0u;
+    t.dist = l < 30 ? (uint32_t)kDistBase[l] | ((uint32_t)kDistExtra[l] << 16) : 0u;
+    return t;
+}
+
 template <bool kWrite>
-DEV int inflate_member(InfIn& in, InfTabs* T, InfOut& o, uint64_t& total) {
+DEV int inflate_member(InfIn& in, InfTabs* T, InfOut& o, const InfSymTabs& ST, uint64_t& total) {
     const uint32_t l = lane();
     const uint64_t nbits = in.n * 8;
     uint64_t bp = 0, op = 0;
@@ -500,8 +523,9 @@ DEV int inflate_member(InfIn& in, InfTabs* T, InfOut& o, uint64_t& total) {
                 }
                 if (sym == 256) break;
                 sym -= 257;
-                uint32_t ml = kLenBase[sym];
-                const uint32_t le = kLenExtra[sym];
+                const uint32_t lt = rl(ST.len, (int)sym);
+                uint32_t ml = lt & 0xFFFFu;
+                const uint32_t le = lt >> 16;
                 v >>= len;  // the extra bits follow the code (len + le <= 20 < 32)
                 if (le) {
                     NEED(le);
@@ -513,8 +537,9 @@ DEV int inflate_member(InfIn& in, InfTabs* T, InfOut& o, uint64_t& total) {
                 if (r == 0) goto done;
                 if (r < 0 || sym > 29) return -1;  // invalid distance code
                 bp += len;
-                uint32_t dist = kDistBase[sym];
-                const uint32_t de = kDistExtra[sym];
+                const uint32_t dt = rl(ST.dist, (int)sym);
+                uint32_t dist = dt & 0xFFFFu;
+                const uint32_t de = dt >> 16;
                 if (de) {
                     NEED(de);
                     dist += (v >> len) & ((1u << de) - 1u);  // len + de <= 28
@@ -589,6 +614,7 @@ __global__ __launch_bounds__(64) void k_inflate_plan(DeviceJob j) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     InfTabs* T = (InfTabs*)lds;
     inf_load_tab(T->crc_tab);
+    const InfSymTabs ST = inf_sym_tabs();
     const uint32_t count = j.counters[16];
     for (;;) {
         const uint32_t i = wave_fetch_add(&j.counters[17], 1u);
@@ -599,7 +625,7 @@ __global__ __launch_bounds__(64) void k_inflate_plan(DeviceJob j) {
         InfOut o;
         uint64_t total = 0;
         // compressor::uncompress throws on an empty payload (compression/compression.cc:34-55)
-        const int rc = in.n ? inflate_member<false>(in, T, o, total) : -1;
+        const int rc = in.n ? inflate_member<false>(in, T, o, ST, total) : -1;
         const uint64_t cap = rc ? 0 : (total + 15) & ~15ull;
         if (lane() == 0) {
             const int32_t rcount = R->record_count;
@@ -614,6 +640,10 @@ __global__ __launch_bounds__(64) void k_inflate(DeviceJob j) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     InfTabs* T = (InfTabs*)(lds + kInfRing);
     inf_load_tab(T->crc_tab);
+    const InfSymTabs ST = inf_sym_tabs();
+    const uint32_t l = lane();
+    const uint32_t x2n = l < 32 ? kX2nIeee[l] : 0u;
+    const uint32_t lane_mul = ieee_xpow8(1024u - 16u * (l + 1), x2n), chunk_mul = ieee_xpow8(1024u, x2n);
     const uint32_t count = j.counters[16];
     for (;;) {
         const uint32_t i = wave_fetch_add(&j.counters[18], 1u);
@@ -632,8 +662,11 @@ __global__ __launch_bounds__(64) void k_inflate(DeviceJob j) {
         o.tab = T->crc_tab;
         o.dst = j.decoded + dst;
         o.flushed = 0;
+        o.x2n = x2n;
+        o.lane_mul = lane_mul;
+        o.chunk_mul = chunk_mul;
         uint64_t total = 0;
-        const int rc = inflate_member<true>(in, T, o, total);
+        const int rc = inflate_member<true>(in, T, o, ST, total);
         if (rc == 0 && lane() == 0) {
             R->flags = R->flags | RPGPU_F_CODEC_OK;
             R->decoded_len = (uint32_t)total;
