@@ -782,14 +782,15 @@ __global__ void k_finalize_totals(DeviceJob j) {
     rpgpu_job_totals t;
     t.n_batches = nb_total;
     t.n_records = j.slots[nb];
-    t.decoded_bytes = j.dcap[nb];
+    const uint64_t dtot = (j.flags & RPGPU_JOB_DECODE) ? j.dcap[nb] : 0;  // unscanned without DECODE
+    t.decoded_bytes = dtot;
     t.batch_capacity_needed = nb_total;
     t.record_capacity_needed = j.slots[nb];
-    t.decoded_capacity_needed = j.dcap[nb];
+    t.decoded_capacity_needed = dtot;
     uint32_t ov = j.counters[1];
     if (nb_total > j.batch_capacity) ov |= 1;
     if (j.slots[nb] > j.record_capacity) ov |= 2;
-    if (j.dcap[nb] > j.decoded_capacity) ov |= 4;
+    if (dtot > j.decoded_capacity) ov |= 4;
     t.overflow = ov;
     t.n_rewalks = j.counters[0];
     t.reserved[0] = t.reserved[1] = 0;

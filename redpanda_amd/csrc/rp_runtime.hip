@@ -741,7 +741,9 @@ int submit_body(rpgpu_ctx* c, const rpgpu_job* job, hipStream_t s, int stop, Pla
         if (int rc = host_codec_step(c, j, s)) return rc;
     const uint64_t* d_nb = j.chunk_count + tc;
     STAGE("scan_slots", scan_exclusive_u64_devn(j.slots, d_nb, bcap, scan_tmp, s));
-    STAGE("scan_dcap", scan_exclusive_u64_devn(j.dcap, d_nb, bcap, scan_tmp, s));
+    // without DECODE every reservation is 0 (k_emit): the scan would write
+    // zeros over zeros; k_finalize_totals reads no total then
+    if (job->flags & RPGPU_JOB_DECODE) STAGE("scan_dcap", scan_exclusive_u64_devn(j.dcap, d_nb, bcap, scan_tmp, s));
     if (stop == kStopAfterPlan) return RPGPU_OK;
     if (tm) HIPCHK(c, hipEventRecord(ev[2], s));
     // decode first: k_validate checksums and walks the decoded payloads
