@@ -238,11 +238,18 @@ struct InfOut {
     uint32_t x2n;         // lane k: x^(2^k) mod P
     uint32_t lane_mul;    // lane l: x^(8 (1024 - 16 (l + 1))): its 16 bytes moved to a full chunk's end
     uint32_t chunk_mul;   // x^(8 * 1024)
+    uint64_t cap;         // bytes dst holds (16-byte multiple); past it the pass only counts
+    bool over;            // the output outgrew dst: no more stores, no check
 };
 
 // flush output bytes [o.flushed, o.flushed + len) (len <= 1024, the start
 // 1 KiB aligned) from the ring and fold them into the check
 DEV void inf_flush(InfOut& o, uint32_t len) {
+    if (o.over || o.flushed + len > o.cap) {  // the slot is full: count only
+        o.over = true;
+        o.flushed += len;
+        return;
+    }
     const uint32_t l = lane();
     const uint32_t at = (uint32_t)(o.flushed & kInfMask) + 16u * l;
     const uint32_t t = 16u * l < len ? min(16u, len - 16u * l) : 0u;  // this lane's bytes
@@ -559,23 +566,26 @@ DEV int inflate_member(InfIn& in, InfTabs* T, InfOut& o, const InfSymTabs& ST, u
     }
     // CHECK, LENGTH (the sizing pass stops before them: it holds no bytes to
     // check, and the plan depends only on what decodes)
+    // a check that fails returns -2: the stream decoded (its plan stands),
+    // the reference still throws
     if (kWrite) {
         bp = (bp + 7) & ~7ull;
         NEED(32);
         if (op > o.flushed) inf_flush(o, (uint32_t)(op - o.flushed));
+        total = op;
+        if (o.over) return 0;  // no bytes held to check: a second pass decides
         const uint32_t w = inf_peek(in, bp);
         if (gz) {
-            if (w != ~o.crc) return -1;  // incorrect data check
+            if (w != ~o.crc) return -2;  // incorrect data check
         } else {
             const uint32_t be = __builtin_bswap32(w);
-            if (be != ((o.adb << 16) | o.ada)) return -1;
+            if (be != ((o.adb << 16) | o.ada)) return -2;
         }
         bp += 32;
         if (gz) {
             NEED(32);
-            if (inf_peek(in, bp) != (uint32_t)op) return -1;  // incorrect length check
+            if (inf_peek(in, bp) != (uint32_t)op) return -2;  // incorrect length check
         }
-        total = op;
         return 0;
     }
 done:
@@ -588,11 +598,19 @@ done:
 // ---------------------------------------------------------------------------
 // Job kernels.  k_emit lists the gzip batches of RPGPU_JOB_DECODE jobs
 // (inf_list, counters[16] items).
-//   k_inflate_plan: the sizing pass, one wave per member, before the slot
-//     scans: the member's arena reservation (dcap: its output rounded up to
-//     16, 0 when it is rejected) and index slots (the same record_count rule
-//     as every codec), and the pass's verdict (inf_state);
-//   k_inflate: the decode pass into the slot: CODEC_OK, decoded_len.
+//   k_inflate_first (after k_emit, before the slot scans): one wave per
+//     member decodes it into a scratch slot of the context's pool, sized
+//     from the member's ISIZE trailer (capped by deflate's 1032:1 ratio);
+//     it sets the member's arena reservation (dcap: the output rounded up to
+//     16, 0 when the stream is rejected, the same plan rule as the
+//     reference's sizing pass: a failed data / length check still reserves)
+//     and index slots, and its state: 0 decoded and checked (the bytes wait
+//     in scratch), 1 rejected, 2 the output outgrew the scratch slot (or the
+//     pool ran out): only sized, decoded again by k_inflate;
+//   k_inflate_copy: state 0 members from scratch into their arena slots;
+//   k_inflate: the second pass for state 2 members, into the slot.
+// The reference decodes every payload twice (buffer_for_input, then the real
+// pass); here a well-formed member is decoded once.
 // k_validate_decoded then computes the new crc / header_crc and walks it.
 // ---------------------------------------------------------------------------
 DEV void inf_load_tab(uint32_t* tab) {
@@ -609,12 +627,40 @@ DEV InfIn inf_batch(const DeviceJob& j, const rpgpu_batch_result* R) {
     return inf_in(j.data + S, n);
 }
 
-// one wave per workgroup: the tables (and the ring) are the wave's own
-__global__ __launch_bounds__(64) void k_inflate_plan(DeviceJob j) {
+// per-wave constants of the decode passes
+struct InfWave {
+    InfSymTabs ST;
+    uint32_t x2n, lane_mul, chunk_mul;
+};
+DEV InfWave inf_wave() {
+    InfWave w;
+    w.ST = inf_sym_tabs();
+    const uint32_t l = lane();
+    w.x2n = l < 32 ? kX2nIeee[l] : 0u;
+    w.lane_mul = ieee_xpow8(1024u - 16u * (l + 1), w.x2n);
+    w.chunk_mul = ieee_xpow8(1024u, w.x2n);
+    return w;
+}
+DEV InfOut inf_out(uint8_t* lds, const InfTabs* T, const InfWave& w, uint8_t* dst, uint64_t cap) {
+    InfOut o;
+    o.ring = (inf_lds_u8*)lds;
+    o.tab = T->crc_tab;
+    o.dst = dst;
+    o.flushed = 0;
+    o.x2n = w.x2n;
+    o.lane_mul = w.lane_mul;
+    o.chunk_mul = w.chunk_mul;
+    o.cap = cap;
+    o.over = false;
+    return o;
+}
+
+// one wave per workgroup: the tables and the ring are the wave's own
+__global__ __launch_bounds__(64) void k_inflate_first(DeviceJob j) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-    InfTabs* T = (InfTabs*)lds;
+    InfTabs* T = (InfTabs*)(lds + kInfRing);
     inf_load_tab(T->crc_tab);
-    const InfSymTabs ST = inf_sym_tabs();
+    const InfWave W = inf_wave();
     const uint32_t count = j.counters[16];
     for (;;) {
         const uint32_t i = wave_fetch_add(&j.counters[17], 1u);
@@ -622,33 +668,71 @@ __global__ __launch_bounds__(64) void k_inflate_plan(DeviceJob j) {
         const uint32_t b = uni32(j.inf_list[i]);
         const rpgpu_batch_result* R = &j.batches[b];
         InfIn in = inf_batch(j, R);
-        InfOut o;
         uint64_t total = 0;
-        // compressor::uncompress throws on an empty payload (compression/compression.cc:34-55)
-        const int rc = in.n ? inflate_member<false>(in, T, o, ST, total) : -1;
-        const uint64_t cap = rc ? 0 : (total + 15) & ~15ull;
+        int rc = -1;  // compressor::uncompress throws on an empty payload (compression/compression.cc:34-55)
+        bool over = true;
+        uint64_t soff = 0;
+        if (in.n) {
+            // scratch slot from the ISIZE trailer (a guess: a truncated or
+            // padded member's last bytes are something else)
+            const uint64_t isize = in.n >= 4 ? (uint64_t)(inf_byte(in, in.n - 4) | (inf_byte(in, in.n - 3) << 8) |
+                                                          (inf_byte(in, in.n - 2) << 16) | (inf_byte(in, in.n - 1) << 24))
+                                             : 0;
+            const uint64_t bound = 1032ull * in.n + 64;  // deflate's expansion limit
+            const uint64_t guess = ((isize < bound ? isize : bound) + 15) & ~15ull;
+            soff = uni64(atomicAdd((unsigned long long*)j.inf_scratch_used, lane() == 0 ? (unsigned long long)guess : 0ull));
+            const uint64_t cap = soff + guess <= j.inf_scratch_bytes ? guess : 0;
+            InfOut o = inf_out(lds, T, W, j.inf_scratch + soff, cap);
+            rc = inflate_member<true>(in, T, o, W.ST, total);
+            over = o.over;
+        }
+        // the plan: the output rounded up to 16 unless the stream is rejected
+        const uint64_t cap = rc == -1 ? 0 : (total + 15) & ~15ull;
         if (lane() == 0) {
             const int32_t rcount = R->record_count;
             j.dcap[b] = cap;
             j.slots[b] = ((j.flags & RPGPU_JOB_PARSE) && rcount > 0 && (uint64_t)rcount <= cap) ? (uint64_t)rcount : 0;
-            j.inf_state[i] = rc ? 1u : 0u;
+            j.inf_state[i] = rc != 0 ? 1u : over ? 2u : 0u;
+            j.inf_off[i] = soff;
+            j.inf_total[i] = total;
         }
     }
 }
 
+// decoded members from scratch into their arena slots (one wave per member)
+__global__ __launch_bounds__(256) void k_inflate_copy(DeviceJob j) {
+    const uint32_t count = j.counters[16];
+    const uint32_t l = lane();
+    for (uint32_t i = blockIdx.x * 4 + (threadIdx.x >> 6); i < count; i += gridDim.x * 4) {
+        if (uni32(j.inf_state[i]) != 0) continue;
+        const uint32_t b = uni32(j.inf_list[i]);
+        rpgpu_batch_result* R = &j.batches[b];
+        const uint64_t dst = uni64(j.dcap[b]), cap = uni64(j.dcap[b + 1]) - dst, total = uni64(j.inf_total[i]);
+        if (dst + cap > j.decoded_capacity) {
+            if (l == 0) R->flags = R->flags | RPGPU_F_DECODE_OVERFLOW;
+            continue;
+        }
+        const uint8_t* src = j.inf_scratch + uni64(j.inf_off[i]);
+        for (uint64_t c = 16ull * l; c < total; c += 1024) *(uint4*)(j.decoded + dst + c) = *(const uint4*)(src + c);
+        if (l == 0) {
+            R->flags = R->flags | RPGPU_F_CODEC_OK;
+            R->decoded_len = (uint32_t)total;
+            R->reserved0 = 0;  // k_validate_decoded computes the decoded crc
+        }
+    }
+}
+
+// the second pass, for members whose output outgrew their scratch slot
 __global__ __launch_bounds__(64) void k_inflate(DeviceJob j) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     InfTabs* T = (InfTabs*)(lds + kInfRing);
     inf_load_tab(T->crc_tab);
-    const InfSymTabs ST = inf_sym_tabs();
-    const uint32_t l = lane();
-    const uint32_t x2n = l < 32 ? kX2nIeee[l] : 0u;
-    const uint32_t lane_mul = ieee_xpow8(1024u - 16u * (l + 1), x2n), chunk_mul = ieee_xpow8(1024u, x2n);
+    const InfWave W = inf_wave();
     const uint32_t count = j.counters[16];
     for (;;) {
         const uint32_t i = wave_fetch_add(&j.counters[18], 1u);
         if (i >= count) break;
-        if (uni32(j.inf_state[i])) continue;  // rejected by the sizing pass
+        if (uni32(j.inf_state[i]) != 2) continue;
         const uint32_t b = uni32(j.inf_list[i]);
         rpgpu_batch_result* R = &j.batches[b];
         const uint64_t dst = uni64(j.dcap[b]), cap = uni64(j.dcap[b + 1]) - dst;
@@ -657,26 +741,25 @@ __global__ __launch_bounds__(64) void k_inflate(DeviceJob j) {
             continue;
         }
         InfIn in = inf_batch(j, R);
-        InfOut o;
-        o.ring = (inf_lds_u8*)lds;
-        o.tab = T->crc_tab;
-        o.dst = j.decoded + dst;
-        o.flushed = 0;
-        o.x2n = x2n;
-        o.lane_mul = lane_mul;
-        o.chunk_mul = chunk_mul;
+        InfOut o = inf_out(lds, T, W, j.decoded + dst, cap);
         uint64_t total = 0;
-        const int rc = inflate_member<true>(in, T, o, ST, total);
-        if (rc == 0 && lane() == 0) {
+        const int rc = inflate_member<true>(in, T, o, W.ST, total);
+        if (rc == 0 && !o.over && lane() == 0) {
             R->flags = R->flags | RPGPU_F_CODEC_OK;
             R->decoded_len = (uint32_t)total;
-            R->reserved0 = 0;  // k_validate_decoded computes the decoded crc
+            R->reserved0 = 0;
         }
     }
 }
 
 hipError_t launch_inflate_plan(const DeviceJob& j, hipStream_t s, uint32_t grid) {
-    hipLaunchKernelGGL(k_inflate_plan, dim3(grid), dim3(64), kInfTabBytes, s, j);
+    static bool attr = false;
+    if (!attr) {
+        (void)hipFuncSetAttribute((const void*)k_inflate_first, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)kInfLdsDecode);
+        attr = true;
+    }
+    hipLaunchKernelGGL(k_inflate_first, dim3(grid), dim3(64), kInfLdsDecode, s, j);
     return hipGetLastError();
 }
 
@@ -686,6 +769,7 @@ hipError_t launch_inflate(const DeviceJob& j, hipStream_t s, uint32_t grid) {
         (void)hipFuncSetAttribute((const void*)k_inflate, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kInfLdsDecode);
         attr = true;
     }
+    hipLaunchKernelGGL(k_inflate_copy, dim3(grid), dim3(256), 0, s, j);
     hipLaunchKernelGGL(k_inflate, dim3(grid), dim3(64), kInfLdsDecode, s, j);
     return hipGetLastError();
 }

@@ -184,7 +184,12 @@ struct DeviceJob {
     const uint64_t* seeds;        // optional chain seeds (index-seeded discovery), per segment ascending
     const uint64_t* seed_off;     // n_segments + 1
     uint32_t* inf_list;           // batch_capacity: ordinals of gzip batches (k_inflate_plan / k_inflate)
-    uint32_t* inf_state;          // batch_capacity: 1 = rejected by the sizing pass
+    uint32_t* inf_state;          // batch_capacity: 0 decoded into scratch, 1 rejected, 2 decode again (k_inflate)
+    uint64_t* inf_off;            // batch_capacity: scratch offset of each member's first-pass output
+    uint64_t* inf_total;          // batch_capacity: decoded bytes of each member
+    uint8_t* inf_scratch;         // first-pass output pool (context scratch)
+    uint64_t inf_scratch_bytes;
+    uint64_t* inf_scratch_used;   // bump allocator of the pool (zeroed per job)
     uint32_t* host_list;          // batch_capacity: ordinals of host-decoded (zstd) batches (RPGPU_JOB_HOST_CODECS)
 };
 
@@ -218,7 +223,8 @@ hipError_t launch_decode_blocks(const DeviceJob& j, hipStream_t s, uint32_t grid
 hipError_t launch_lz_walk(const DeviceJob& j, hipStream_t s, uint32_t grid);
 hipError_t launch_lz_exec(const DeviceJob& j, hipStream_t s);
 hipError_t launch_decode_finish(const DeviceJob& j, hipStream_t s, uint32_t grid);
-// gzip members (rp_inflate.hip): sizing pass before the slot scans, decode pass
+// gzip members (rp_inflate.hip): first pass (into scratch) before the slot
+// scans, then the copy into the arena and the second pass where needed
 hipError_t launch_inflate_plan(const DeviceJob& j, hipStream_t s, uint32_t grid);
 hipError_t launch_inflate(const DeviceJob& j, hipStream_t s, uint32_t grid);
 // one payload, one wave (rpgpu_uncompress); res[0] = rc (0 / -1 / -2), res[1] = out_len

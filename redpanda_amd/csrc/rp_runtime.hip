@@ -190,6 +190,9 @@ struct rpgpu_ctx {
         bool pinned = false;
     } hc_items, hc_items_h, hc_in, hc_in_h, hc_out, hc_out_h, hc_small;
     uint32_t hc_n = 0;
+    // gzip first-pass output pool (k_inflate_first), grow-only
+    void* gz_pool = nullptr;
+    size_t gz_pool_bytes = 0;
 };
 
 namespace {
@@ -300,6 +303,7 @@ int rpgpu_destroy(rpgpu_ctx* c) {
     if (c->sth) hipHostFree(c->sth);
     if (c->std_) hipFree(c->std_);
     if (c->d_tables) hipFree(c->d_tables);
+    if (c->gz_pool) hipFree(c->gz_pool);
     for (auto* g : {&c->hc_items, &c->hc_items_h, &c->hc_in, &c->hc_in_h, &c->hc_out, &c->hc_out_h, &c->hc_small})
         if (g->p) (void)(g->pinned ? hipHostFree(g->p) : hipFree(g->p));
     if (c->ws_ev) { (void)hipEventSynchronize(c->ws_ev); (void)hipEventDestroy(c->ws_ev); }
@@ -444,6 +448,20 @@ int submit_impl(rpgpu_ctx* c, const rpgpu_job* job, void* stream, int stop, Plan
     return rc ? rc : rr;
 }
 
+// grow-only device pool (drained before it is replaced)
+int grow_pool(rpgpu_ctx* c, void*& p, size_t& have, size_t want, hipStream_t s) {
+    if (want <= have && p) return RPGPU_OK;
+    if (p) {
+        if (int rc = ws_drain(c, s)) return rc;
+        (void)hipFree(p);
+        p = nullptr;
+        have = 0;
+    }
+    if (hipMalloc(&p, want) != hipSuccess) { p = nullptr; return fail(c, RPGPU_E_NOMEM, "gzip first-pass pool"); }
+    have = want;
+    return RPGPU_OK;
+}
+
 // grow-only device or pinned host buffer (the stream is drained before a
 // device buffer is replaced: earlier work on the context may still use it)
 int grow_buf(rpgpu_ctx* c, rpgpu_ctx::Grow& g, size_t want, bool pinned, hipStream_t s) {
@@ -583,6 +601,8 @@ int submit_body(rpgpu_ctx* c, const rpgpu_job* job, hipStream_t s, int stop, Pla
     const bool decode_job = (job->flags & RPGPU_JOB_DECODE) != 0;
     const size_t o_ilist = take(decode_job ? (bcap + 1) * 4 : 0);
     const size_t o_istate = take(decode_job ? (bcap + 1) * 4 : 0);
+    const size_t o_ioff = take(decode_job ? (bcap + 1) * 8 : 0);
+    const size_t o_itot = take(decode_job ? (bcap + 1) * 8 : 0);
     const bool host_job = decode_job && (job->flags & RPGPU_JOB_HOST_CODECS);
     const size_t o_hlist = take(host_job ? (bcap + 1) * 4 : 0);
     // block-parallel decode: one item per LZ4F block / snappy-java chunk
@@ -685,6 +705,19 @@ int submit_body(rpgpu_ctx* c, const rpgpu_job* job, hipStream_t s, int stop, Pla
     j.seed_off = j.seeds ? job->d_seed_offsets : nullptr;
     j.inf_list = (uint32_t*)(ws + o_ilist);
     j.inf_state = (uint32_t*)(ws + o_istate);
+    j.inf_off = (uint64_t*)(ws + o_ioff);
+    j.inf_total = (uint64_t*)(ws + o_itot);
+    // gzip first-pass pool: twice the job's bytes, 256 MiB .. 2 GiB (members
+    // that do not fit are decoded again, straight into the arena)
+    j.inf_scratch = nullptr;
+    j.inf_scratch_bytes = 0;
+    j.inf_scratch_used = (uint64_t*)(j.counters + 24);  // zeroed with the counters
+    if (decode_job) {
+        const size_t want = std::min<size_t>(std::max<size_t>(2 * data_len, 256ull << 20), 2ull << 30);
+        if (int rc = grow_pool(c, c->gz_pool, c->gz_pool_bytes, want, s)) return rc;
+        j.inf_scratch = (uint8_t*)c->gz_pool;
+        j.inf_scratch_bytes = c->gz_pool_bytes;
+    }
     j.host_list = (uint32_t*)(ws + o_hlist);
     c->hc_n = 0;
     j.blocks = (BlockItem*)(ws + o_blocks);
@@ -733,8 +766,9 @@ int submit_body(rpgpu_ctx* c, const rpgpu_job* job, hipStream_t s, int stop, Pla
     }
     if (stop == kStopAfterCount) return RPGPU_OK;
     STAGE("emit", launch_emit(j, s));
-    // gzip members: the sizing pass (their arena bytes and index slots) before the scans
-    if (decode_job) STAGE("inflate_plan", launch_inflate_plan(j, s, c->cu_count * 16));
+    // gzip members: the first pass (their arena bytes, index slots and, when
+    // they fit the pool, their output) before the scans
+    if (decode_job) STAGE("inflate_plan", launch_inflate_plan(j, s, c->cu_count * 4));
     // zstd members (RPGPU_JOB_HOST_CODECS): decoded on the host now, sized
     // before the scans like every other payload
     if (host_job)
