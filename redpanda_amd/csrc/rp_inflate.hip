@@ -41,6 +41,10 @@ struct InfTabs {
     uint16_t pad0;
     uint8_t lens[320];
     uint32_t crc_tab[256];  // CRC32 (IEEE, reflected 0xEDB88320) byte table
+    // root tables of the literal/length and distance codes: the next 9
+    // stream bits -> symbol | length << 9 for codes of at most 9 bits, 0 for
+    // a longer (or invalid) code
+    uint16_t lroot[512], droot[512];
 };
 constexpr uint32_t kInfTabBytes = (sizeof(InfTabs) + 15u) & ~15u;
 constexpr uint32_t kInfLdsDecode = kInfRing + kInfTabBytes;
@@ -221,6 +225,28 @@ DEV int inf_decode(uint32_t v, uint64_t avail, const InfCode& c, const uint16_t*
     sym = uni32((uint32_t)syms[idx]);
     len = L;
     return 1;
+}
+
+// the root table of a built code (lanes fill 8 entries each): entry idx =
+// the next 9 stream bits; the shortest length L <= 9 whose left-justified
+// limit exceeds them gives the symbol (inf_decode's rule on a prefix)
+DEV void inf_root(const InfCode& c, const uint16_t* syms, uint16_t* root) {
+    const uint32_t l = lane();
+#pragma unroll
+    for (uint32_t k = 0; k < 8; k++) {
+        const uint32_t idx = 64u * k + l;
+        const uint32_t r9 = __builtin_bitreverse32(idx) >> 23;  // first stream bit most significant
+        const uint32_t r15 = r9 << 6;
+        uint32_t e = 0;
+        for (uint32_t L = 1; L <= 9; L++) {
+            const uint32_t lim = rl(c.lim, (int)L);
+            if (e == 0 && r15 < lim) {
+                const uint32_t sidx = rl(c.offs, (int)L) + (r9 >> (9 - L)) - rl(c.first, (int)L);
+                e = (uint32_t)syms[sidx] | (L << 9);
+            }
+        }
+        root[idx] = (uint16_t)e;
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -455,6 +481,8 @@ DEV int inflate_member(InfIn& in, InfTabs* T, InfOut& o, const InfSymTabs& ST, u
                 inf_build(lens, 288, 1, T->lsym, LC);
                 if (l < 32) lens[l] = 5;
                 inf_build(lens, 32, 2, T->dsym, DC);
+                inf_root(LC, T->lsym, T->lroot);
+                inf_root(DC, T->dsym, T->droot);
             } else {  // TABLE
                 NEED(14);
                 v = inf_peek(in, bp);
@@ -510,6 +538,83 @@ DEV int inflate_member(InfIn& in, InfTabs* T, InfOut& o, const InfSymTabs& ST, u
                 if (lens[256] == 0) return -1;                             // invalid code -- missing end-of-block
                 if (inf_build(lens, nlen, 1, T->lsym, LC)) return -1;      // invalid literal/lengths set
                 if (inf_build(lens + nlen, ndist, 2, T->dsym, DC)) return -1;  // invalid distances set
+                inf_root(LC, T->lsym, T->lroot);
+                inf_root(DC, T->dsym, T->droot);
+            }
+            // fast loop: far from the end of the member every code's bits are
+            // present, so no truncation test; a 64-bit bit buffer refilled a
+            // dword at a time from the window, codes of <= 9 bits from the
+            // root tables, longer ones by the limit compare.  It hands over to
+            // the exact loop below near the end (and at the block end).
+            if (kWrite) {
+                const uint64_t pb = bp + 8ull * in.mis;
+                uint64_t pq = (pb >> 5) << 2;                 // next dword to load (physical byte offset)
+                uint32_t sh = (uint32_t)(pb & 31);
+                uint64_t bb = (uint64_t)(inf_dw(in, pq) >> sh);
+                uint32_t bc = 32 - sh;
+                pq += 4;
+                bool eob = false;
+                // safe while the next two refills stay inside the member
+                while (pq + 12 <= in.nphys) {
+                    while (bc <= 32) {
+                        bb |= (uint64_t)inf_dw(in, pq) << bc;
+                        bc += 32;
+                        pq += 4;
+                    }
+                    uint32_t e = uni32((uint32_t)T->lroot[(uint32_t)bb & 511u]);
+                    if (e == 0) {  // a code longer than 9 bits
+                        const int r = inf_decode((uint32_t)bb, 64, LC, T->lsym, sym, len);
+                        if (r < 0) return -1;  // invalid literal/length code
+                        e = sym | (len << 9);
+                    }
+                    sym = e & 511u;
+                    len = e >> 9;
+                    bb >>= len;
+                    bc -= len;
+                    if (sym < 256) {
+                        if (l == 0) o.ring[(uint32_t)op & kInfMask] = (uint8_t)sym;
+                        op++;
+                        if ((op & 1023) == 0) inf_flush(o, 1024u);
+                        continue;
+                    }
+                    if (sym == 256) { eob = true; break; }
+                    if (sym > 285) return -1;  // invalid literal/length code
+                    const uint32_t lt = rl(ST.len, (int)(sym - 257));
+                    const uint32_t le = lt >> 16;
+                    const uint32_t ml = (lt & 0xFFFFu) + ((uint32_t)bb & ((1u << le) - 1u));
+                    bb >>= le;
+                    bc -= le;
+                    if (bc <= 32) {  // the distance code and its extra bits need <= 28
+                        bb |= (uint64_t)inf_dw(in, pq) << bc;
+                        bc += 32;
+                        pq += 4;
+                    }
+                    e = uni32((uint32_t)T->droot[(uint32_t)bb & 511u]);
+                    if (e == 0) {
+                        const int r = inf_decode((uint32_t)bb, 64, DC, T->dsym, sym, len);
+                        if (r < 0) return -1;  // invalid distance code
+                        e = sym | (len << 9);
+                    }
+                    sym = e & 511u;
+                    len = e >> 9;
+                    if (sym > 29) return -1;  // invalid distance code
+                    bb >>= len;
+                    bc -= len;
+                    const uint32_t dt = rl(ST.dist, (int)sym);
+                    const uint32_t de = dt >> 16;
+                    const uint32_t dist = (dt & 0xFFFFu) + ((uint32_t)bb & ((1u << de) - 1u));
+                    bb >>= de;
+                    bc -= de;
+                    if (dist > op) return -1;  // invalid distance too far back
+                    inf_copy(o, op, dist, ml);
+                    op += ml;
+                    inf_flush_upto(o, op);
+                }
+                bp = 8 * (pq - in.mis) - bc;  // the bits consumed
+                if (eob) {
+                    if (last) break;
+                    continue;
+                }
             }
             // LEN .. MATCH
             for (;;) {
