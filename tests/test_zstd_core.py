@@ -1,0 +1,95 @@
+"""The device zstd decoder's logic (redpanda_amd/csrc/rp_zstd_core.h) built
+for the host by the test (tests/cpp/zstd_core_host.cpp) and compared with the
+reference -- stream_zstd::do_uncompress's loop over libzstd 1.4.8, the
+oracle's rpo_zstd_uncompress -- on libzstd frames and thousands of seeded
+mutations: same accept / reject, same output bytes.  The GPU tests then pin
+the device build of the same logic against the same oracle.  CPU only."""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import random
+import subprocess
+
+import pytest
+
+from tests import zstd_corpus as Z
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+@pytest.fixture(scope="module")
+def host(tmp_path_factory):
+    out = str(tmp_path_factory.mktemp("zs") / "libzshost.so")
+    subprocess.run(["g++", "-O2", "-std=c++17", "-shared", "-fPIC", "-o", out,
+                    os.path.join(HERE, "cpp", "zstd_core_host.cpp")], check=True)
+    L = C.CDLL(out)
+    L.zs_host_decode.argtypes = [C.c_char_p, C.c_uint64, C.c_void_p, C.c_uint64, C.POINTER(C.c_uint64)]
+    L.zs_host_xxh64.argtypes = [C.c_char_p, C.c_uint64]
+    L.zs_host_xxh64.restype = C.c_uint64
+
+    def decode(b: bytes, cap: int = 1 << 24):
+        dst = C.create_string_buffer(cap)
+        t = C.c_uint64(0)
+        rc = L.zs_host_decode(b, len(b), dst, cap, C.byref(t))
+        assert rc in (0, -1), rc
+        return dst.raw[: t.value] if rc == 0 else None
+    decode.xxh64 = lambda b: L.zs_host_xxh64(b, len(b))
+    return decode
+
+
+def test_xxh64_matches_xxhash(host):
+    import xxhash
+    rng = random.Random(3)
+    for n in [0, 1, 3, 4, 7, 8, 31, 32, 33, 63, 64, 100, 1000, 4096 + 17]:
+        b = bytes(rng.getrandbits(8) for _ in range(n))
+        assert host.xxh64(b) == xxhash.xxh64(b).intdigest()
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3])
+def test_core_matches_libzstd_loop(host, seed):
+    rng = random.Random(seed)
+    frames = Z.random_frames(rng, 40)
+    for data, f in frames:
+        assert host(f) == Z.ref_decode(f)
+    bad = []
+    cases = Z.mutations(rng, frames)
+    for c in cases:
+        if host(c) != Z.ref_decode(c):
+            bad.append(c[:24].hex())
+    assert not bad, (len(bad), len(cases), bad[:4])
+
+
+def test_core_edge_frames(host):
+    """Hand-built frames for the loop's rules (probed against libzstd):
+    block-size limit in the streaming path only, trailing bytes, skippable
+    frames, dictionary ids, reserved bits, window limit of the static DCtx,
+    content checksum, raw-block streaming, the output-room shortcut."""
+    import struct
+    M = struct.pack("<I", 0xFD2FB528)
+
+    def bh(last, typ, size):
+        return struct.pack("<I", last | (typ << 1) | (size << 3))[:3]
+
+    ok = M + bytes([0x20, 10]) + bh(1, 0, 10) + b"0123456789"
+    B = M + bytes([0x80, 0]) + struct.pack("<I", 4096) + bh(0, 1, 2048) + b"a" + bh(1, 1, 2048) + b"b"
+    A62 = M + bytes([0xA0]) + struct.pack("<I", 62000) + bh(1, 0, 62000) + b"r" * 62000
+    A60 = M + bytes([0xA0]) + struct.pack("<I", 60000) + bh(1, 0, 60000) + b"r" * 60000
+    raw2 = M + bytes([0xA0]) + struct.pack("<I", 20) + bh(0, 0, 10) + b"0" * 10 + bh(1, 0, 10)
+    cases = [ok, ok + b"\x11" * 4, ok + b"\x11" * 5, B, A60 + B, A62 + B,
+             M + bytes([0x00, 0]) + bh(1, 1, 1500) + b"z", M + bytes([0x00, 0]) + bh(1, 0, 2000) + b"A" * 10,
+             M + bytes([0x00, 0x68]) + bh(1, 0, 10) + b"A" * 10, M + bytes([0x00, 0x70]) + bh(1, 0, 10) + b"A" * 10,
+             M + bytes([0x28, 10]) + bh(1, 0, 10) + b"A" * 10, M + bytes([0x21, 5, 10]) + bh(1, 0, 10) + b"A" * 10,
+             M + bytes([0x21, 0, 10]) + bh(1, 0, 10) + b"A" * 10, M + bytes([0x20, 10]) + bh(1, 3, 10) + b"A" * 10,
+             struct.pack("<II", 0x184D2A53, 3) + b"xyz" + ok, raw2, raw2 + b"1" * 5,
+             M + bytes([0x24, 10]) + bh(1, 0, 10) + b"0123456789" + b"\0\0\0\0",
+             M + bytes([0x24, 10]) + bh(1, 0, 10) + b"0123456789" + b"\0\0",
+             # empty blocks: skipped by the streaming path (a last one skips the content-size check)
+             M + bytes([0x80, 0]) + struct.pack("<I", 300000) + bh(0, 2, 0) + bh(1, 0, 10) + b"x" * 10,
+             M + bytes([0x80, 0x58]) + struct.pack("<I", 10) + bh(0, 2, 0) + bh(1, 0, 10) + b"x" * 10,
+             M + bytes([0x00, 0x58]) + bh(0, 2, 0) + bh(1, 0, 10) + b"x" * 10,
+             M + bytes([0x80, 0x58]) + struct.pack("<I", 300000) + bh(0, 0, 10) + b"x" * 10 + bh(1, 2, 0),
+             M + bytes([0x84, 0x58]) + struct.pack("<I", 300000) + bh(0, 0, 10) + b"x" * 10 + bh(1, 2, 0) + b"\0" * 4,
+             M + bytes([0x80, 0x58]) + struct.pack("<I", 300000) + bh(0, 0, 10) + b"x" * 10 + bh(1, 0, 0)]
+    for c in cases:
+        assert host(c) == Z.ref_decode(c), c[:16].hex()
