@@ -77,7 +77,7 @@ enum rpgpu_status {
 #define RPGPU_F_CRC_OK (1u << 2)         /* (uint32)hdr.crc == crc32c(BE hdr40 ++ stored payload) (storage/log_replayer.cc:62-79, model/record_utils.cc:68-91) */
 #define RPGPU_F_COMPRESSED (1u << 3)     /* attrs codec != none */
 #define RPGPU_F_CODEC_INVALID (1u << 4)  /* codec value 5..7: record_batch_attributes::compression() throws (model/record.h:283-300) */
-#define RPGPU_F_CODEC_UNSUPPORTED (1u << 5) /* zstd in a job without RPGPU_JOB_HOST_CODECS: not decoded (rpgpu_uncompress decodes it on the host) */
+#define RPGPU_F_CODEC_UNSUPPORTED (1u << 5) /* zstd in a job without RPGPU_JOB_DECODE (kept from the host-only zstd path) */
 #define RPGPU_F_CODEC_OK (1u << 6)       /* compressor::uncompress succeeded (compression/compression.cc:34-55) */
 #define RPGPU_F_PARSED (1u << 7)         /* a record walk was run over the (decoded) payload */
 #define RPGPU_F_PARSE_ASYNC_OK (1u << 8) /* model::for_each_record completed without throwing (model/record.h:680-697) */
@@ -239,14 +239,14 @@ enum rpgpu_layout {
 
 #define RPGPU_JOB_CRC (1u << 0)     /* compute the payload crc (always on in recovery) */
 #define RPGPU_JOB_PARSE (1u << 1)   /* walk records into the index */
-#define RPGPU_JOB_DECODE (1u << 2)  /* uncompress lz4/snappy/gzip payloads into the arena (on the device) */
-/* With RPGPU_JOB_DECODE: also decode zstd batches, on the host (SURVEY.md
- * §8(b): zstd falls back to the CPU; stream_zstd::do_uncompress over libzstd,
+#define RPGPU_JOB_DECODE (1u << 2)  /* uncompress lz4/snappy/gzip/zstd payloads into the arena (on the device) */
+/* With RPGPU_JOB_DECODE: decode zstd batches on the host instead (SURVEY.md
+ * §8(b)'s CPU fallback: stream_zstd::do_uncompress over libzstd,
  * compression/stream_zstd.cc:152-178), into the same arena, then CRC and walk
- * them on the device like every other decoded payload.  The submit then
- * synchronizes on its stream once the chain is planned (the payloads' sizes
- * and bytes cross to the host and back), so rpgpu_submit_async returns after
- * that point.  Without it zstd batches are flagged RPGPU_F_CODEC_UNSUPPORTED. */
+ * them on the device like every other decoded payload.  Same plan and
+ * verdicts as the device decoder; the submit then synchronizes on its stream
+ * once the chain is planned (the payloads' sizes and bytes cross to the host
+ * and back), so rpgpu_submit_async returns after that point. */
 #define RPGPU_JOB_HOST_CODECS (1u << 3)
 
 /* All pointers are DEVICE pointers, caller-owned.  Segments are concatenated

@@ -1464,9 +1464,9 @@ int64_t rpo_scan_segment_layout(const uint8_t* seg, uint64_t len, uint32_t segme
         const int may_walk = !wire || (r->flags & RPGPU_F_CRC_OK);
         if (codec) r->flags |= RPGPU_F_COMPRESSED;
         if (codec >= 5) r->flags |= RPGPU_F_CODEC_INVALID;
-        /* zstd: decoded on the host with RPGPU_JOB_HOST_CODECS, else not at all */
-        const int host_codec = (job_flags & RPGPU_JOB_DECODE) && (job_flags & RPGPU_JOB_HOST_CODECS);
-        if (codec == RPGPU_CODEC_ZSTD && !host_codec) r->flags |= RPGPU_F_CODEC_UNSUPPORTED;
+        /* zstd: decoded in DECODE jobs (on the device, or on the host with
+         * RPGPU_JOB_HOST_CODECS: the same plan and verdicts) */
+        if (codec == RPGPU_CODEC_ZSTD && !(job_flags & RPGPU_JOB_DECODE)) r->flags |= RPGPU_F_CODEC_UNSUPPORTED;
 
         /* Plan (engine rule, see DESIGN.md "index and arena planning"): the
          * record-index slots and decode-arena bytes of a batch are reserved
@@ -1474,9 +1474,9 @@ int64_t rpo_scan_segment_layout(const uint8_t* seg, uint64_t len, uint32_t segme
          * the GPU can assign them with prefix sums.  Reservations never depend
          * on whether the decode or the walk later succeed. */
         uint64_t slots = 0, cap = 0;
-        int decodable = ((codec == RPGPU_CODEC_LZ4 || codec == RPGPU_CODEC_SNAPPY || codec == RPGPU_CODEC_GZIP) &&
-                         (job_flags & RPGPU_JOB_DECODE)) ||
-                        (codec == RPGPU_CODEC_ZSTD && host_codec);
+        int decodable = (codec == RPGPU_CODEC_LZ4 || codec == RPGPU_CODEC_SNAPPY || codec == RPGPU_CODEC_GZIP ||
+                         codec == RPGPU_CODEC_ZSTD) &&
+                        (job_flags & RPGPU_JOB_DECODE);
         if (codec == 0) {
             if ((job_flags & RPGPU_JOB_PARSE) && h.record_count > 0 && (uint64_t)h.record_count <= need)
                 slots = (uint64_t)h.record_count;

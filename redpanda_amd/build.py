@@ -63,7 +63,8 @@ def build(force: bool = False, verbose: bool = False, checked: bool = False, var
     out, bdir, extra = VARIANTS[variant]
     os.makedirs(bdir, exist_ok=True)
     hipcc = _hipcc()
-    headers = [os.path.join(INC, "rpgpu.h"), os.path.join(CSRC, "rp_internal.h"), os.path.join(CSRC, "rp_device.h")]
+    headers = [os.path.join(INC, "rpgpu.h"), os.path.join(CSRC, "rp_internal.h"), os.path.join(CSRC, "rp_device.h"),
+               os.path.join(CSRC, "rp_zstd_core.h")]
     objs = []
     for src in HIP_SOURCES:
         s = os.path.join(CSRC, src)

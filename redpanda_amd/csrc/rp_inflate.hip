@@ -25,7 +25,16 @@
 // per step.  Output goes through a 32 KiB LDS ring (deflate distances reach
 // 32768 back) and leaves in coalesced 16-byte stores.
 // Integer work only: no MFMA.
+//
+// zstd (stream_zstd::do_uncompress, compression/stream_zstd.cc:152-178) runs
+// here too, on the same member list, scratch slots and passes: the decoder
+// logic is rp_zstd_core.h (libzstd 1.4.8's acceptance rules as the
+// reference's loop sees them), instantiated over ZDev below.
 #include "rp_device.h"
+
+#define ZS_FN DEV
+#define ZS_CONST static __constant__
+#include "rp_zstd_core.h"
 
 namespace rp {
 
@@ -772,6 +781,7 @@ __global__ __launch_bounds__(64) void k_inflate_first(DeviceJob j) {
         if (i >= count) break;
         const uint32_t b = uni32(j.inf_list[i]);
         const rpgpu_batch_result* R = &j.batches[b];
+        if ((uni32((uint32_t)(uint16_t)R->attrs) & 7u) != RPGPU_CODEC_GZIP) continue;  // zstd: k_zstd_first
         InfIn in = inf_batch(j, R);
         uint64_t total = 0;
         int rc = -1;  // compressor::uncompress throws on an empty payload (compression/compression.cc:34-55)
@@ -840,6 +850,7 @@ __global__ __launch_bounds__(64) void k_inflate(DeviceJob j) {
         if (uni32(j.inf_state[i]) != 2) continue;
         const uint32_t b = uni32(j.inf_list[i]);
         rpgpu_batch_result* R = &j.batches[b];
+        if ((uni32((uint32_t)(uint16_t)R->attrs) & 7u) != RPGPU_CODEC_GZIP) continue;  // zstd: k_zstd
         const uint64_t dst = uni64(j.dcap[b]), cap = uni64(j.dcap[b + 1]) - dst;
         if (dst + cap > j.decoded_capacity) {
             if (lane() == 0) R->flags = R->flags | RPGPU_F_DECODE_OVERFLOW;
@@ -857,14 +868,356 @@ __global__ __launch_bounds__(64) void k_inflate(DeviceJob j) {
     }
 }
 
+// ---------------------------------------------------------------------------
+// zstd: the decoder of rp_zstd_core.h over a wave environment.  State is
+// wave-uniform (every lane runs the same scalar logic; table reads are made
+// uniform with readfirstlane); the input is read through the member's 512-byte
+// window (headers, tables) and a 256-byte register window per backward bit
+// stream (the sequence stream and each Huffman stream: one load per ~248
+// bytes consumed); output goes through the 32 KiB LDS ring in 256-byte
+// lane-parallel pieces and leaves in 1 KiB flushes (16 bytes per lane), as
+// the inflate output does.  Matches reaching past the ring read the slot
+// (L2-coherent loads once the flushes have completed).  A frame's XXH64
+// content checksum is computed by the wave over its bytes (slot + ring).
+// ---------------------------------------------------------------------------
+constexpr int kBufFlagsZs = 0x00020000;  // buffer resource word 3 (raw, 32-bit data format)
+DEV void zs_wait_vm() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+constexpr int kZsSc1 = 16;  // cache policy sc1: L2-coherent, bypasses the vector L1
+constexpr uint32_t kZsTabBytes = (sizeof(zs::Tabs) + 15u) & ~15u;
+constexpr uint32_t kZsLds = kInfRing + kZsTabBytes;
+constexpr uint64_t kZsFarOff = kInfRing - 1024 - 256;  // offsets up to this read the ring
+
+constexpr uint64_t kXP1 = 0x9E3779B185EBCA87ull, kXP2 = 0xC2B2AE3D27D4EB4Full, kXP3 = 0x165667B19E3779F9ull,
+                   kXP4 = 0x85EBCA77C2B2AE63ull, kXP5 = 0x27D4EB2F165667C5ull;
+DEV uint64_t xrotl(uint64_t x, int r) { return (x << r) | (x >> (64 - r)); }
+DEV uint64_t xround(uint64_t acc, uint64_t in) { return xrotl(acc + in * kXP2, 31) * kXP1; }
+
+struct ZDev {
+    InfIn in;
+    inf_lds_u8* ring;
+    uint8_t* dst;
+    uint64_t cap;      // bytes the slot holds (a multiple of 16)
+    uint64_t op;       // output position
+    uint64_t flushed;  // output below left the ring (1 KiB aligned until the end)
+    uint64_t stored;   // output below is in the slot
+    bool over;         // the output outgrew the slot: only counted from then on
+    uint64_t fstart;   // the current frame's first output byte
+    __amdgpu_buffer_rsrc_t rs;
+
+    DEV uint32_t b(uint64_t i) { return inf_byte(in, i); }
+    DEV uint64_t le(uint64_t i, uint32_t k) {  // k (<= 8) bytes at i, inside the member
+        const uint64_t p = i + in.mis, a = p & ~3ull;
+        const uint32_t sh = (uint32_t)(p & 3) * 8u;
+        const uint32_t d0 = inf_dw(in, a), d1 = inf_dw(in, a + 4);
+        const uint64_t lo = (uint64_t)d0 | ((uint64_t)d1 << 32);
+        uint64_t v = lo;
+        if (sh) v = (lo >> sh) | ((uint64_t)inf_dw(in, a + 8) << (64 - sh));
+        return k >= 8 ? v : v & ((1ull << (8 * k)) - 1ull);
+    }
+    // 8 bytes at pos for backward bit stream s: its own register window,
+    // placed to end just past the read (the stream moves down)
+    DEV uint64_t lb(zs::Bits& s, uint64_t pos) {
+        const uint64_t p = pos + in.mis;
+        if (p < s.wbase || p + 12 > s.wbase + 256) {
+            const uint64_t nb = (p + 12 > 256 ? p + 12 - 256 : 0) & ~3ull;
+            s.wbase = nb;
+            s.wreg = inf_ld(in, nb + 4u * lane());
+        }
+        const uint32_t o = (uint32_t)(p - s.wbase), li = o >> 2, sh = (o & 3) * 8u;
+        const uint64_t lo = (uint64_t)rl(s.wreg, (int)li) | ((uint64_t)rl(s.wreg, (int)li + 1) << 32);
+        return sh ? (lo >> sh) | ((uint64_t)rl(s.wreg, (int)li + 2) << (64 - sh)) : lo;
+    }
+    DEV uint32_t U(uint32_t x) { return uni32(x); }
+    DEV zs::SeqSym sym(const zs::SeqSym& t) {
+        uint64_t v;
+        __builtin_memcpy(&v, &t, 8);
+        v = uni64(v);
+        zs::SeqSym r;
+        __builtin_memcpy(&r, &v, 8);
+        return r;
+    }
+    // [flushed, flushed + len) out of the ring (flushed 1 KiB aligned, len <= 1 KiB)
+    DEV void flush(uint32_t len) {
+        if (!over) {
+            const uint64_t room = cap > flushed ? cap - flushed : 0;
+            const uint32_t at = 16u * lane();
+            if (at < len && at < room) {
+                const uint4 v = *(const uint4*)(ring + ((uint32_t)(flushed + at) & kInfMask));
+                *(uint4*)(dst + flushed + at) = v;
+            }
+            const uint64_t end = flushed + len;
+            stored = end < cap ? end : cap;
+            if (end > cap) over = true;
+        }
+        flushed += len;
+    }
+    DEV void flush_upto(uint64_t p) {
+        while ((p >> 10) > (flushed >> 10)) flush(1024u);
+    }
+    DEV void flush_all() {
+        flush_upto(op);
+        if (op > flushed) flush((uint32_t)(op - flushed));
+    }
+    DEV void raw(uint64_t pos, uint64_t k) {
+        const uint32_t l = lane();
+        for (uint64_t c = 0; c < k; c += 256) {
+            const uint32_t m = k - c < 256 ? (uint32_t)(k - c) : 256u;
+            if (!over) {
+#pragma unroll
+                for (uint32_t t = 0; t < 4; t++) {
+                    const uint32_t x = 4u * l + t;
+                    if (x < m) ring[(uint32_t)(op + x) & kInfMask] = in.src[pos + c + x];
+                }
+            }
+            op += m;
+            flush_upto(op);
+        }
+    }
+    DEV void fill(uint32_t v, uint64_t k) {
+        const uint32_t l = lane();
+        for (uint64_t c = 0; c < k; c += 256) {
+            const uint32_t m = k - c < 256 ? (uint32_t)(k - c) : 256u;
+            if (!over) {
+#pragma unroll
+                for (uint32_t t = 0; t < 4; t++) {
+                    const uint32_t x = 4u * l + t;
+                    if (x < m) ring[(uint32_t)(op + x) & kInfMask] = (uint8_t)v;
+                }
+            }
+            op += m;
+            flush_upto(op);
+        }
+    }
+    DEV void lit(uint32_t v) {
+        if (!over && lane() == 0) ring[(uint32_t)op & kInfMask] = (uint8_t)v;
+        op++;
+        if ((op & 1023) == 0) flush(1024u);
+    }
+    DEV void match(uint64_t off, uint64_t ml) {
+        const uint32_t l = lane();
+        if (over) {
+            op += ml;
+            flush_upto(op);
+            return;
+        }
+        const bool far = off > kZsFarOff;
+        for (uint64_t c = 0; c < ml; c += 256) {
+            const uint32_t m = ml - c < 256 ? (uint32_t)(ml - c) : 256u;
+            uint32_t v[4];
+            if (far) zs_wait_vm();  // the slot bytes read below were stored by this wave's flushes
+#pragma unroll
+            for (uint32_t t = 0; t < 4; t++) {
+                const uint32_t x = 4u * l + t;
+                v[t] = 0;
+                if (x < m) {
+                    if (far) {
+                        v[t] = __builtin_amdgcn_raw_buffer_load_b8(rs, (int)(op + x - off), 0, kZsSc1);
+                    } else {
+                        const uint64_t sx = off >= 256 ? (uint64_t)x : (uint64_t)(x % (uint32_t)off);
+                        v[t] = ring[(uint32_t)(op - off + sx) & kInfMask];
+                    }
+                }
+            }
+#pragma unroll
+            for (uint32_t t = 0; t < 4; t++) {
+                const uint32_t x = 4u * l + t;
+                if (x < m) ring[(uint32_t)(op + x) & kInfMask] = (uint8_t)v[t];
+            }
+            op += m;
+            flush_upto(op);
+        }
+    }
+    DEV void frame_begin() { fstart = op; }
+    // output byte q of this member (the slot below `flushed`, else the ring)
+    DEV uint32_t byte_at(uint64_t q) {
+        return q < flushed ? (uint32_t)__builtin_amdgcn_raw_buffer_load_b8(rs, (int)q, 0, kZsSc1)
+                           : (uint32_t)ring[(uint32_t)q & kInfMask];
+    }
+    // XXH64 of the frame's output [fstart, op) vs the trailer's low 32 bits:
+    // 1 equal, 0 not, 2 unknown (the bytes outgrew the slot)
+    DEV int check(uint32_t want) {
+        if (over || stored < flushed) return 2;
+        zs_wait_vm();
+        const uint32_t l = lane();
+        const uint64_t len = op - fstart, body = len & ~31ull;
+        uint64_t h;
+        if (len >= 32) {
+            // lanes 0..3 hold the four accumulators; a 1 KiB piece at a time
+            uint64_t acc = l == 0 ? kXP1 + kXP2 : l == 1 ? kXP2 : l == 2 ? 0ull : 0ull - kXP1;
+            for (uint64_t c = 0; c < body; c += 1024) {
+                const uint32_t m = body - c < 1024 ? (uint32_t)(body - c) : 1024u;
+                uint32_t w[4] = {0u, 0u, 0u, 0u};
+                if (16u * l < m) {
+#pragma unroll
+                    for (uint32_t t = 0; t < 16; t++) w[t >> 2] |= byte_at(fstart + c + 16u * l + t) << (8 * (t & 3));
+                }
+                for (uint32_t i = 0; i < m / 32; i++) {
+                    // accumulator k takes bytes [32 i + 8 k, +8): lane 2 i + k / 2, half k & 1
+                    const int src = (int)(2 * i + ((l & 3) >> 1));
+                    const uint32_t x0 = (uint32_t)__shfl((int)w[0], src, 64), x1 = (uint32_t)__shfl((int)w[1], src, 64);
+                    const uint32_t x2 = (uint32_t)__shfl((int)w[2], src, 64), x3 = (uint32_t)__shfl((int)w[3], src, 64);
+                    const uint64_t word = (l & 1) ? ((uint64_t)x2 | ((uint64_t)x3 << 32)) : ((uint64_t)x0 | ((uint64_t)x1 << 32));
+                    if (l < 4) acc = xround(acc, word);
+                }
+            }
+            const uint64_t v1 = (uint64_t)rl((uint32_t)acc, 0) | ((uint64_t)rl((uint32_t)(acc >> 32), 0) << 32);
+            const uint64_t v2 = (uint64_t)rl((uint32_t)acc, 1) | ((uint64_t)rl((uint32_t)(acc >> 32), 1) << 32);
+            const uint64_t v3 = (uint64_t)rl((uint32_t)acc, 2) | ((uint64_t)rl((uint32_t)(acc >> 32), 2) << 32);
+            const uint64_t v4 = (uint64_t)rl((uint32_t)acc, 3) | ((uint64_t)rl((uint32_t)(acc >> 32), 3) << 32);
+            h = xrotl(v1, 1) + xrotl(v2, 7) + xrotl(v3, 12) + xrotl(v4, 18);
+            h = (h ^ xround(0, v1)) * kXP1 + kXP4;
+            h = (h ^ xround(0, v2)) * kXP1 + kXP4;
+            h = (h ^ xround(0, v3)) * kXP1 + kXP4;
+            h = (h ^ xround(0, v4)) * kXP1 + kXP4;
+        } else {
+            h = kXP5;
+        }
+        h += len;
+        uint64_t q = fstart + body;
+        const uint64_t e = op;
+        while (q + 8 <= e) {
+            uint64_t k = 0;
+            for (uint32_t t = 0; t < 8; t++) k |= (uint64_t)uni32(byte_at(q + t)) << (8 * t);
+            h ^= xround(0, k);
+            h = xrotl(h, 27) * kXP1 + kXP4;
+            q += 8;
+        }
+        if (q + 4 <= e) {
+            uint64_t k = 0;
+            for (uint32_t t = 0; t < 4; t++) k |= (uint64_t)uni32(byte_at(q + t)) << (8 * t);
+            h ^= k * kXP1;
+            h = xrotl(h, 23) * kXP2 + kXP3;
+            q += 4;
+        }
+        while (q < e) {
+            h ^= (uint64_t)uni32(byte_at(q)) * kXP5;
+            h = xrotl(h, 11) * kXP1;
+            q++;
+        }
+        h ^= h >> 33;
+        h *= kXP2;
+        h ^= h >> 29;
+        h *= kXP3;
+        h ^= h >> 32;
+        return (uint32_t)h == want ? 1 : 0;
+    }
+};
+
+DEV ZDev zdev(const InfIn& in, uint8_t* lds, uint8_t* dst, uint64_t cap) {
+    ZDev e;
+    e.in = in;
+    e.ring = (inf_lds_u8*)lds;
+    e.dst = dst;
+    e.cap = cap;
+    e.op = e.flushed = e.stored = 0;
+    e.over = false;
+    e.fstart = 0;
+    e.rs = __builtin_amdgcn_make_buffer_rsrc(dst, 0, (int)(cap < 0x7FFFFFFFull ? cap : 0x7FFFFFFFull), kBufFlagsZs);
+    return e;
+}
+
+// the scratch slot of the first pass: the first frame's content size when
+// its header carries one (exact for a one-frame payload), else 8 x the input
+DEV uint64_t zs_guess(InfIn& in) {
+    const uint64_t n = in.n;
+    uint64_t g = 8 * n + 4096;
+    if (n >= 6 && (inf_byte(in, 0) | (inf_byte(in, 1) << 8) | (inf_byte(in, 2) << 16) | (inf_byte(in, 3) << 24)) ==
+                      0xFD2FB528u) {
+        const uint32_t fhd = inf_byte(in, 4);
+        const uint32_t single = (fhd >> 5) & 1, fcsid = fhd >> 6, did = fhd & 3;
+        const uint64_t at = 5 + (single ? 0 : 1) + (did == 3 ? 4 : did);
+        const uint32_t sz = fcsid == 0 ? (single ? 1 : 0) : fcsid == 1 ? 2 : fcsid == 2 ? 4 : 8;
+        if (sz && at + sz <= n) {
+            uint64_t f = 0;
+            for (uint32_t k = 0; k < sz; k++) f |= (uint64_t)inf_byte(in, at + k) << (8 * k);
+            if (fcsid == 1) f += 256;
+            if (f < (1ull << 32)) g = f + 64;
+        }
+    }
+    return (g + 15) & ~15ull;
+}
+
+// first pass over the zstd members of inf_list (the gzip ones are
+// k_inflate_first's): same plan / state rules as the inflate passes; a
+// payload whose content checksum could not be checked in the slot (it
+// outgrew it) is decoded again by k_zstd
+__global__ __launch_bounds__(64) void k_zstd_first(DeviceJob j) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    zs::Tabs* T = (zs::Tabs*)(lds + kInfRing);
+    const uint32_t count = j.counters[16];
+    for (;;) {
+        const uint32_t i = wave_fetch_add(&j.counters[20], 1u);
+        if (i >= count) break;
+        const uint32_t b = uni32(j.inf_list[i]);
+        const rpgpu_batch_result* R = &j.batches[b];
+        if ((uni32((uint32_t)(uint16_t)R->attrs) & 7u) != RPGPU_CODEC_ZSTD) continue;
+        InfIn in = inf_batch(j, R);
+        uint64_t total = 0, soff = 0;
+        int rc = -1;  // compressor::uncompress throws on an empty payload (compression/compression.cc:34-55)
+        bool again = true;
+        if (in.n) {
+            const uint64_t guess = zs_guess(in);
+            soff = uni64(atomicAdd((unsigned long long*)j.inf_scratch_used, lane() == 0 ? (unsigned long long)guess : 0ull));
+            const uint64_t cap = soff + guess <= j.inf_scratch_bytes ? guess : 0;
+            ZDev e = zdev(in, lds, j.inf_scratch + soff, cap);
+            bool unsure = false;
+            rc = zs::payload(e, T, in.n, total, unsure);
+            e.flush_all();
+            again = unsure || e.stored < total;
+        }
+        const uint64_t cap = rc != 0 ? 0 : (total + 15) & ~15ull;
+        if (lane() == 0) {
+            const int32_t rcount = R->record_count;
+            j.dcap[b] = cap;
+            j.slots[b] = ((j.flags & RPGPU_JOB_PARSE) && rcount > 0 && (uint64_t)rcount <= cap) ? (uint64_t)rcount : 0;
+            j.inf_state[i] = rc != 0 ? 1u : again ? 2u : 0u;
+            j.inf_off[i] = soff;
+            j.inf_total[i] = total;
+        }
+    }
+}
+
+// second pass: zstd members that outgrew their scratch slot, into the arena
+__global__ __launch_bounds__(64) void k_zstd(DeviceJob j) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    zs::Tabs* T = (zs::Tabs*)(lds + kInfRing);
+    const uint32_t count = j.counters[16];
+    for (;;) {
+        const uint32_t i = wave_fetch_add(&j.counters[21], 1u);
+        if (i >= count) break;
+        if (uni32(j.inf_state[i]) != 2) continue;
+        const uint32_t b = uni32(j.inf_list[i]);
+        rpgpu_batch_result* R = &j.batches[b];
+        if ((uni32((uint32_t)(uint16_t)R->attrs) & 7u) != RPGPU_CODEC_ZSTD) continue;
+        const uint64_t dst = uni64(j.dcap[b]), cap = uni64(j.dcap[b + 1]) - dst;
+        if (dst + cap > j.decoded_capacity) {
+            if (lane() == 0) R->flags = R->flags | RPGPU_F_DECODE_OVERFLOW;
+            continue;
+        }
+        InfIn in = inf_batch(j, R);
+        ZDev e = zdev(in, lds, j.decoded + dst, cap);
+        uint64_t total = 0;
+        bool unsure = false;
+        const int rc = zs::payload(e, T, in.n, total, unsure);
+        e.flush_all();
+        if (rc == 0 && !unsure && e.stored >= total && lane() == 0) {
+            R->flags = R->flags | RPGPU_F_CODEC_OK;
+            R->decoded_len = (uint32_t)total;
+            R->reserved0 = 0;
+        }
+    }
+}
+
 hipError_t launch_inflate_plan(const DeviceJob& j, hipStream_t s, uint32_t grid) {
     static bool attr = false;
     if (!attr) {
         (void)hipFuncSetAttribute((const void*)k_inflate_first, hipFuncAttributeMaxDynamicSharedMemorySize,
                                   (int)kInfLdsDecode);
+        (void)hipFuncSetAttribute((const void*)k_zstd_first, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kZsLds);
         attr = true;
     }
     hipLaunchKernelGGL(k_inflate_first, dim3(grid), dim3(64), kInfLdsDecode, s, j);
+    hipLaunchKernelGGL(k_zstd_first, dim3(grid), dim3(64), kZsLds, s, j);
     return hipGetLastError();
 }
 
@@ -872,10 +1225,12 @@ hipError_t launch_inflate(const DeviceJob& j, hipStream_t s, uint32_t grid) {
     static bool attr = false;
     if (!attr) {
         (void)hipFuncSetAttribute((const void*)k_inflate, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kInfLdsDecode);
+        (void)hipFuncSetAttribute((const void*)k_zstd, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kZsLds);
         attr = true;
     }
     hipLaunchKernelGGL(k_inflate_copy, dim3(grid), dim3(256), 0, s, j);
     hipLaunchKernelGGL(k_inflate, dim3(grid), dim3(64), kInfLdsDecode, s, j);
+    hipLaunchKernelGGL(k_zstd, dim3(grid), dim3(64), kZsLds, s, j);
     return hipGetLastError();
 }
 

@@ -573,7 +573,7 @@ __global__ __launch_bounds__(256) void k_emit(DeviceJob j) {
             if (codec) f |= RPGPU_F_COMPRESSED;
             if (codec >= 5) f |= RPGPU_F_CODEC_INVALID;
             const bool host_codec = (j.flags & RPGPU_JOB_DECODE) && (j.flags & RPGPU_JOB_HOST_CODECS);
-            if (complete && codec == RPGPU_CODEC_ZSTD && !host_codec) f |= RPGPU_F_CODEC_UNSUPPORTED;
+            if (complete && codec == RPGPU_CODEC_ZSTD && !(j.flags & RPGPU_JOB_DECODE)) f |= RPGPU_F_CODEC_UNSUPPORTED;
             r.flags = f;
             r.segment = s;
             // scratch for k_validate: absolute payload start (overwritten with
@@ -595,8 +595,10 @@ __global__ __launch_bounds__(256) void k_emit(DeviceJob j) {
             // decode work list for k_decode (order is irrelevant: every item
             // writes only its own batch and its own reserved arena slot)
             if (complete && decodable) j.decode_list[atomicAdd(&j.counters[2], 1u)] = (uint32_t)ord;
-            // gzip members: sized by k_inflate_plan (dcap / slots above are 0 until then)
-            if (complete && codec == RPGPU_CODEC_GZIP && (j.flags & RPGPU_JOB_DECODE))
+            // gzip and zstd members: sized by k_inflate_first / k_zstd_first (dcap /
+            // slots above are 0 until then)
+            if (complete && (j.flags & RPGPU_JOB_DECODE) &&
+                (codec == RPGPU_CODEC_GZIP || (codec == RPGPU_CODEC_ZSTD && !host_codec)))
                 j.inf_list[atomicAdd(&j.counters[16], 1u)] = (uint32_t)ord;
             // zstd members with RPGPU_JOB_HOST_CODECS: decoded by the host step
             if (complete && codec == RPGPU_CODEC_ZSTD && host_codec)

@@ -593,9 +593,9 @@ GZ_WEIGHTS = [3, 3, 1, 2, 1, 1]  # none, gzip, snappy-java, lz4, zstd, raw snapp
 
 @pytest.mark.parametrize("seed", [0xC6, 31])
 def test_gzip_mix_decode(engine, oracle, rplib, seed):
-    """Segments mixing gzip with every other codec (zstd stays flagged
-    CODEC_UNSUPPORTED), payload corruptions: flags, new crc/header_crc,
-    index and arena bit-exact."""
+    """Segments mixing gzip with every other codec (zstd decoded on the
+    device too), payload corruptions: flags, new crc/header_crc, index and
+    arena bit-exact."""
     segs = [gen(rplib, 3 << 20, i, seed=seed, batch_bytes=0, min_batch=200, max_batch=600000,
                 weights=GZ_WEIGHTS, corrupt_payload_ppm=(20000 if i == 1 else 0)) for i in range(3)]
     got, ref = run_both(engine, oracle, segs, flags=DFLAGS, chunk=64 << 10)
@@ -641,10 +641,11 @@ def test_gzip_members_corpus(engine, oracle):
 
 @pytest.mark.parametrize("host", [False, True])
 def test_zstd_host_codec_job(engine, oracle, rplib, host):
-    """zstd batches inside a job: with RPGPU_JOB_HOST_CODECS decoded on the
-    host (stream_zstd::do_uncompress over libzstd) into the same arena, then
-    CRC'd and walked on the device; without it flagged CODEC_UNSUPPORTED.
-    Bit flips in some payloads exercise the reject path."""
+    """zstd batches inside a job: decoded on the device (rp_zstd_core.h over
+    the wave environment), or with RPGPU_JOB_HOST_CODECS on the host
+    (stream_zstd::do_uncompress over libzstd); either way into the same
+    arena, then CRC'd and walked on the device, with the oracle's plan and
+    verdicts.  Bit flips in some payloads exercise the reject path."""
     weights = [2, 1, 1, 1, 4, 1]
     segs = [gen(rplib, 2 << 20, i, seed=0x25D + i, batch_bytes=0, min_batch=200, max_batch=400000,
                 weights=weights, corrupt_payload_ppm=(30000 if i == 1 else 0)) for i in range(3)]
@@ -652,9 +653,61 @@ def test_zstd_host_codec_job(engine, oracle, rplib, host):
     got, ref = run_both(engine, oracle, segs, flags=flags, chunk=64 << 10)
     z = (got.batches["attrs"] & 7) == abi.CODEC_ZSTD
     assert np.any(z)
-    if host:
-        assert np.any(z & ((got.batches["flags"] & abi.F_CODEC_OK) != 0))
-        assert not np.any(got.batches["flags"] & abi.F_CODEC_UNSUPPORTED)
-    else:
-        assert np.all((got.batches["flags"][z] & abi.F_CODEC_UNSUPPORTED) != 0)
+    assert np.any(z & ((got.batches["flags"] & abi.F_CODEC_OK) != 0))
+    assert not np.any(got.batches["flags"] & abi.F_CODEC_UNSUPPORTED)
     assert_same(got, ref, flags)
+
+
+def _zstd_batches(payloads, counts=None, base=0):
+    """One disk batch per zstd payload; records = the given count, else a
+    guess from the decoded bytes (the walk then accepts or rejects)."""
+    from tests import batchgen as BG
+    from tests import zstd_corpus as ZC
+    out = bytearray()
+    for k, p in enumerate(payloads):
+        if counts is not None:
+            rc = counts[k]
+        else:
+            plain = ZC.ref_decode(p)
+            rc = max(1, plain.count(b"\x00") // 50) if plain else 3
+        out += BG.batch(p, rc, base_offset=base + 100 * k, attrs=abi.CODEC_ZSTD)
+    return np.frombuffer(bytes(out), dtype=np.uint8).copy()
+
+
+def test_zstd_members_corpus(engine, oracle):
+    """zstd payloads from libzstd itself as batch payloads decoded on the
+    device: clean frames of every level class, with and without content
+    size / checksum, streaming flushes, no pledged size; matches reaching past
+    the 32 KiB ring (read back from the slot); frames whose output outgrows
+    the first pass's slot (no content size: the second pass); concatenated
+    and skippable frames; and seeded mutations (truncations, header and body
+    bit flips, trailing bytes).  Accept/reject, decoded bytes, crc /
+    header_crc, index and walk as the oracle's (stream_zstd::do_uncompress
+    over libzstd)."""
+    import random
+    import struct
+    from tests import batchgen as BG
+    from tests import zstd_corpus as ZC
+    rng = random.Random(0x257)
+    recs = [(n, BG.simple_records(n, vlen=v, seed=n)) for n, v in [(1, 10), (30, 40), (200, 300), (900, 900)]]
+    good, counts = [], []
+    for n, r in recs:
+        for kw in [dict(level=3), dict(level=19, checksum=1), dict(level=1, checksum=1, content_size=0),
+                   dict(level=-3, flushes=[len(r) // 3, len(r) // 2]), dict(level=9, pledged=False)]:
+            good.append(ZC.frame(r, **kw))
+            counts.append(n)
+    far_src = bytes(rng.getrandbits(8) for _ in range(40000))
+    special = [ZC.frame(far_src * 3, level=19, wlog=17, checksum=1),           # 40 KB-back matches
+               ZC.frame(b"\0" * (1 << 20), level=3, content_size=0, checksum=1),  # outgrows 8 x input
+               ZC.frame(b"abc" * 50000, level=5, pledged=False),
+               ZC.frame(b"hello " * 1000) + ZC.frame(b"world " * 2000, checksum=1),
+               struct.pack("<II", 0x184D2A50, 5) + b"skip!" + ZC.frame(b"after the skippable frame " * 30)]
+    frames = ZC.random_frames(rng, 24, sizes=(0, 1, 40, 1000, 5000, 20000, 70000, 140000))
+    mutated = ZC.mutations(rng, frames, per=4)
+    segs = [_zstd_batches(good, counts), _zstd_batches(special), _zstd_batches(mutated[: len(mutated) // 2]),
+            _zstd_batches(mutated[len(mutated) // 2:])]
+    got, ref = run_both(engine, oracle, segs, flags=DFLAGS)
+    assert np.any((got.batches["flags"] & abi.F_PARSE_OK) != 0)
+    ok = (got.batches["flags"] & abi.F_CODEC_OK) != 0
+    assert int(np.sum(ok)) > len(good)
+    assert_same(got, ref, DFLAGS)
