@@ -34,6 +34,15 @@
 
 #define ZS_FN DEV
 #define ZS_CONST static __constant__
+#ifdef RPGPU_ZSTAMPS  // diagnostic build: wall-clock totals per decoder phase (scripts/build_exp.py)
+#define ZS_PROF(k, stmt)                        \
+    {                                           \
+        const uint64_t t0_ = wall_clock64();    \
+        stmt;                                   \
+        e.prof[k] += wall_clock64() - t0_;      \
+    }
+__device__ unsigned long long g_zst[8];
+#endif
 #include "rp_zstd_core.h"
 
 namespace rp {
@@ -710,21 +719,22 @@ done:
 }
 
 // ---------------------------------------------------------------------------
-// Job kernels.  k_emit lists the gzip batches of RPGPU_JOB_DECODE jobs
-// (inf_list, counters[16] items).
-//   k_inflate_first (after k_emit, before the slot scans): one wave per
-//     member decodes it into a scratch slot of the context's pool, sized
-//     from the member's ISIZE trailer (capped by deflate's 1032:1 ratio);
-//     it sets the member's arena reservation (dcap: the output rounded up to
-//     16, 0 when the stream is rejected, the same plan rule as the
-//     reference's sizing pass: a failed data / length check still reserves)
-//     and index slots, and its state: 0 decoded and checked (the bytes wait
-//     in scratch), 1 rejected, 2 the output outgrew the scratch slot (or the
-//     pool ran out): only sized, decoded again by k_inflate;
+// Job passes.  k_emit lists the gzip and zstd batches of RPGPU_JOB_DECODE
+// jobs (inf_list, counters[16] items).
+//   first pass (k_members_first, after k_emit, before the slot scans): one
+//     wave per member decodes it into a scratch slot of the context's pool,
+//     sized from the member's ISIZE trailer (gzip, capped by deflate's 1032:1
+//     ratio) or first frame's content size (zstd); it sets the member's arena
+//     reservation (dcap: the output rounded up to 16, 0 when the stream is
+//     rejected, the plan rule of the reference's sizing pass: for gzip a
+//     failed data / length check still reserves) and index slots, and its
+//     state: 0 decoded and checked (the bytes wait in scratch), 1 rejected,
+//     2 the output outgrew the scratch slot (or the pool ran out): decoded
+//     again by the second pass;
 //   k_inflate_copy: state 0 members from scratch into their arena slots;
-//   k_inflate: the second pass for state 2 members, into the slot.
-// The reference decodes every payload twice (buffer_for_input, then the real
-// pass); here a well-formed member is decoded once.
+//   second pass (k_members): state 2 members, into the slot.
+// The reference decodes every gzip payload twice (buffer_for_input, then the
+// real pass); here a well-formed member is decoded once.
 // k_validate_decoded then computes the new crc / header_crc and walks it.
 // ---------------------------------------------------------------------------
 DEV void inf_load_tab(uint32_t* tab) {
@@ -769,48 +779,38 @@ DEV InfOut inf_out(uint8_t* lds, const InfTabs* T, const InfWave& w, uint8_t* ds
     return o;
 }
 
-// one wave per workgroup: the tables and the ring are the wave's own
-__global__ __launch_bounds__(64) void k_inflate_first(DeviceJob j) {
-    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-    InfTabs* T = (InfTabs*)(lds + kInfRing);
-    inf_load_tab(T->crc_tab);
-    const InfWave W = inf_wave();
-    const uint32_t count = j.counters[16];
-    for (;;) {
-        const uint32_t i = wave_fetch_add(&j.counters[17], 1u);
-        if (i >= count) break;
-        const uint32_t b = uni32(j.inf_list[i]);
-        const rpgpu_batch_result* R = &j.batches[b];
-        if ((uni32((uint32_t)(uint16_t)R->attrs) & 7u) != RPGPU_CODEC_GZIP) continue;  // zstd: k_zstd_first
-        InfIn in = inf_batch(j, R);
-        uint64_t total = 0;
-        int rc = -1;  // compressor::uncompress throws on an empty payload (compression/compression.cc:34-55)
-        bool over = true;
-        uint64_t soff = 0;
-        if (in.n) {
-            // scratch slot from the ISIZE trailer (a guess: a truncated or
-            // padded member's last bytes are something else)
-            const uint64_t isize = in.n >= 4 ? (uint64_t)(inf_byte(in, in.n - 4) | (inf_byte(in, in.n - 3) << 8) |
-                                                          (inf_byte(in, in.n - 2) << 16) | (inf_byte(in, in.n - 1) << 24))
-                                             : 0;
-            const uint64_t bound = 1032ull * in.n + 64;  // deflate's expansion limit
-            const uint64_t guess = ((isize < bound ? isize : bound) + 15) & ~15ull;
-            soff = uni64(atomicAdd((unsigned long long*)j.inf_scratch_used, lane() == 0 ? (unsigned long long)guess : 0ull));
-            const uint64_t cap = soff + guess <= j.inf_scratch_bytes ? guess : 0;
-            InfOut o = inf_out(lds, T, W, j.inf_scratch + soff, cap);
-            rc = inflate_member<true>(in, T, o, W.ST, total);
-            over = o.over;
-        }
-        // the plan: the output rounded up to 16 unless the stream is rejected
-        const uint64_t cap = rc == -1 ? 0 : (total + 15) & ~15ull;
-        if (lane() == 0) {
-            const int32_t rcount = R->record_count;
-            j.dcap[b] = cap;
-            j.slots[b] = ((j.flags & RPGPU_JOB_PARSE) && rcount > 0 && (uint64_t)rcount <= cap) ? (uint64_t)rcount : 0;
-            j.inf_state[i] = rc != 0 ? 1u : over ? 2u : 0u;
-            j.inf_off[i] = soff;
-            j.inf_total[i] = total;
-        }
+// first pass of gzip member i (batch b): decode into a scratch slot sized
+// from the ISIZE trailer, set the plan and the state
+DEV void gzip_first_item(const DeviceJob& j, uint8_t* lds, InfTabs* T, const InfWave& W, uint32_t i, uint32_t b,
+                         const rpgpu_batch_result* R) {
+    InfIn in = inf_batch(j, R);
+    uint64_t total = 0;
+    int rc = -1;  // compressor::uncompress throws on an empty payload (compression/compression.cc:34-55)
+    bool over = true;
+    uint64_t soff = 0;
+    if (in.n) {
+        // scratch slot from the ISIZE trailer (a guess: a truncated or
+        // padded member's last bytes are something else)
+        const uint64_t isize = in.n >= 4 ? (uint64_t)(inf_byte(in, in.n - 4) | (inf_byte(in, in.n - 3) << 8) |
+                                                      (inf_byte(in, in.n - 2) << 16) | (inf_byte(in, in.n - 1) << 24))
+                                         : 0;
+        const uint64_t bound = 1032ull * in.n + 64;  // deflate's expansion limit
+        const uint64_t guess = ((isize < bound ? isize : bound) + 15) & ~15ull;
+        soff = uni64(atomicAdd((unsigned long long*)j.inf_scratch_used, lane() == 0 ? (unsigned long long)guess : 0ull));
+        const uint64_t cap = soff + guess <= j.inf_scratch_bytes ? guess : 0;
+        InfOut o = inf_out(lds, T, W, j.inf_scratch + soff, cap);
+        rc = inflate_member<true>(in, T, o, W.ST, total);
+        over = o.over;
+    }
+    // the plan: the output rounded up to 16 unless the stream is rejected
+    const uint64_t cap = rc == -1 ? 0 : (total + 15) & ~15ull;
+    if (lane() == 0) {
+        const int32_t rcount = R->record_count;
+        j.dcap[b] = cap;
+        j.slots[b] = ((j.flags & RPGPU_JOB_PARSE) && rcount > 0 && (uint64_t)rcount <= cap) ? (uint64_t)rcount : 0;
+        j.inf_state[i] = rc != 0 ? 1u : over ? 2u : 0u;
+        j.inf_off[i] = soff;
+        j.inf_total[i] = total;
     }
 }
 
@@ -837,34 +837,17 @@ __global__ __launch_bounds__(256) void k_inflate_copy(DeviceJob j) {
     }
 }
 
-// the second pass, for members whose output outgrew their scratch slot
-__global__ __launch_bounds__(64) void k_inflate(DeviceJob j) {
-    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-    InfTabs* T = (InfTabs*)(lds + kInfRing);
-    inf_load_tab(T->crc_tab);
-    const InfWave W = inf_wave();
-    const uint32_t count = j.counters[16];
-    for (;;) {
-        const uint32_t i = wave_fetch_add(&j.counters[18], 1u);
-        if (i >= count) break;
-        if (uni32(j.inf_state[i]) != 2) continue;
-        const uint32_t b = uni32(j.inf_list[i]);
-        rpgpu_batch_result* R = &j.batches[b];
-        if ((uni32((uint32_t)(uint16_t)R->attrs) & 7u) != RPGPU_CODEC_GZIP) continue;  // zstd: k_zstd
-        const uint64_t dst = uni64(j.dcap[b]), cap = uni64(j.dcap[b + 1]) - dst;
-        if (dst + cap > j.decoded_capacity) {
-            if (lane() == 0) R->flags = R->flags | RPGPU_F_DECODE_OVERFLOW;
-            continue;
-        }
-        InfIn in = inf_batch(j, R);
-        InfOut o = inf_out(lds, T, W, j.decoded + dst, cap);
-        uint64_t total = 0;
-        const int rc = inflate_member<true>(in, T, o, W.ST, total);
-        if (rc == 0 && !o.over && lane() == 0) {
-            R->flags = R->flags | RPGPU_F_CODEC_OK;
-            R->decoded_len = (uint32_t)total;
-            R->reserved0 = 0;
-        }
+// the second pass of gzip member i (its output outgrew the scratch slot)
+DEV void gzip_item(const DeviceJob& j, uint8_t* lds, InfTabs* T, const InfWave& W, rpgpu_batch_result* R,
+                   uint64_t dst, uint64_t cap) {
+    InfIn in = inf_batch(j, R);
+    InfOut o = inf_out(lds, T, W, j.decoded + dst, cap);
+    uint64_t total = 0;
+    const int rc = inflate_member<true>(in, T, o, W.ST, total);
+    if (rc == 0 && !o.over && lane() == 0) {
+        R->flags = R->flags | RPGPU_F_CODEC_OK;
+        R->decoded_len = (uint32_t)total;
+        R->reserved0 = 0;
     }
 }
 
@@ -902,7 +885,12 @@ struct ZDev {
     uint64_t stored;   // output below is in the slot
     bool over;         // the output outgrew the slot: only counted from then on
     uint64_t fstart;   // the current frame's first output byte
+    uint32_t lbuf;     // Huffman literals gathered one per lane before they go to the ring
+    uint32_t nlit;
     __amdgpu_buffer_rsrc_t rs;
+#ifdef RPGPU_ZSTAMPS
+    uint64_t prof[4];  // literals, matches, stream ends, whole compressed blocks
+#endif
 
     DEV uint32_t b(uint64_t i) { return inf_byte(in, i); }
     DEV uint64_t le(uint64_t i, uint32_t k) {  // k (<= 8) bytes at i, inside the member
@@ -954,11 +942,20 @@ struct ZDev {
     DEV void flush_upto(uint64_t p) {
         while ((p >> 10) > (flushed >> 10)) flush(1024u);
     }
+    DEV void lit_spill() {
+        if (!nlit) return;
+        if (!over && lane() < nlit) ring[(uint32_t)(op + lane()) & kInfMask] = (uint8_t)lbuf;
+        op += nlit;
+        nlit = 0;
+        flush_upto(op);
+    }
     DEV void flush_all() {
+        lit_spill();
         flush_upto(op);
         if (op > flushed) flush((uint32_t)(op - flushed));
     }
     DEV void raw(uint64_t pos, uint64_t k) {
+        lit_spill();
         const uint32_t l = lane();
         for (uint64_t c = 0; c < k; c += 256) {
             const uint32_t m = k - c < 256 ? (uint32_t)(k - c) : 256u;
@@ -974,6 +971,7 @@ struct ZDev {
         }
     }
     DEV void fill(uint32_t v, uint64_t k) {
+        lit_spill();
         const uint32_t l = lane();
         for (uint64_t c = 0; c < k; c += 256) {
             const uint32_t m = k - c < 256 ? (uint32_t)(k - c) : 256u;
@@ -989,11 +987,11 @@ struct ZDev {
         }
     }
     DEV void lit(uint32_t v) {
-        if (!over && lane() == 0) ring[(uint32_t)op & kInfMask] = (uint8_t)v;
-        op++;
-        if ((op & 1023) == 0) flush(1024u);
+        lbuf = lane() == nlit ? v : lbuf;
+        if (++nlit == 64) lit_spill();
     }
     DEV void match(uint64_t off, uint64_t ml) {
+        lit_spill();
         const uint32_t l = lane();
         if (over) {
             op += ml;
@@ -1001,6 +999,11 @@ struct ZDev {
             return;
         }
         const bool far = off > kZsFarOff;
+        // a match overlapping its own output repeats the off bytes before it:
+        // byte x of a piece is x mod off into them (off < 256: a multiply by
+        // the rounded-up reciprocal is exact for x < 256)
+        const bool rep = off < 256 && off < ml;
+        const uint64_t mg = rep ? 0xFFFFFFFFull / off + 1ull : 0ull;  // 2^32 for off = 1
         for (uint64_t c = 0; c < ml; c += 256) {
             const uint32_t m = ml - c < 256 ? (uint32_t)(ml - c) : 256u;
             uint32_t v[4];
@@ -1013,7 +1016,7 @@ struct ZDev {
                     if (far) {
                         v[t] = __builtin_amdgcn_raw_buffer_load_b8(rs, (int)(op + x - off), 0, kZsSc1);
                     } else {
-                        const uint64_t sx = off >= 256 ? (uint64_t)x : (uint64_t)(x % (uint32_t)off);
+                        const uint64_t sx = rep ? x - (((uint64_t)x * mg) >> 32) * off : (uint64_t)x;
                         v[t] = ring[(uint32_t)(op - off + sx) & kInfMask];
                     }
                 }
@@ -1027,7 +1030,10 @@ struct ZDev {
             flush_upto(op);
         }
     }
-    DEV void frame_begin() { fstart = op; }
+    DEV void frame_begin() {
+        lit_spill();
+        fstart = op;
+    }
     // output byte q of this member (the slot below `flushed`, else the ring)
     DEV uint32_t byte_at(uint64_t q) {
         return q < flushed ? (uint32_t)__builtin_amdgcn_raw_buffer_load_b8(rs, (int)q, 0, kZsSc1)
@@ -1036,6 +1042,7 @@ struct ZDev {
     // XXH64 of the frame's output [fstart, op) vs the trailer's low 32 bits:
     // 1 equal, 0 not, 2 unknown (the bytes outgrew the slot)
     DEV int check(uint32_t want) {
+        lit_spill();
         if (over || stored < flushed) return 2;
         zs_wait_vm();
         const uint32_t l = lane();
@@ -1112,6 +1119,11 @@ DEV ZDev zdev(const InfIn& in, uint8_t* lds, uint8_t* dst, uint64_t cap) {
     e.op = e.flushed = e.stored = 0;
     e.over = false;
     e.fstart = 0;
+    e.lbuf = 0;
+    e.nlit = 0;
+#ifdef RPGPU_ZSTAMPS
+    e.prof[0] = e.prof[1] = e.prof[2] = e.prof[3] = 0;
+#endif
     e.rs = __builtin_amdgcn_make_buffer_rsrc(dst, 0, (int)(cap < 0x7FFFFFFFull ? cap : 0x7FFFFFFFull), kBufFlagsZs);
     return e;
 }
@@ -1137,100 +1149,160 @@ DEV uint64_t zs_guess(InfIn& in) {
     return (g + 15) & ~15ull;
 }
 
-// first pass over the zstd members of inf_list (the gzip ones are
-// k_inflate_first's): same plan / state rules as the inflate passes; a
+// first pass of zstd member i: the same plan / state rules as gzip's; a
 // payload whose content checksum could not be checked in the slot (it
-// outgrew it) is decoded again by k_zstd
-__global__ __launch_bounds__(64) void k_zstd_first(DeviceJob j) {
-    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+// outgrew it) is decoded again by the second pass
+DEV void zstd_first_item(const DeviceJob& j, uint8_t* lds, uint32_t i, uint32_t b, const rpgpu_batch_result* R) {
     zs::Tabs* T = (zs::Tabs*)(lds + kInfRing);
+    InfIn in = inf_batch(j, R);
+    uint64_t total = 0, soff = 0;
+    int rc = -1;  // compressor::uncompress throws on an empty payload (compression/compression.cc:34-55)
+    bool again = true;
+    if (in.n) {
+        const uint64_t guess = zs_guess(in);
+        soff = uni64(atomicAdd((unsigned long long*)j.inf_scratch_used, lane() == 0 ? (unsigned long long)guess : 0ull));
+        const uint64_t cap = soff + guess <= j.inf_scratch_bytes ? guess : 0;
+        ZDev e = zdev(in, lds, j.inf_scratch + soff, cap);
+        bool unsure = false;
+#ifdef RPGPU_ZSTAMPS
+        const uint64_t t0 = wall_clock64();
+#endif
+        rc = zs::payload(e, T, in.n, total, unsure);
+        e.flush_all();
+        again = unsure || e.stored < total;
+#ifdef RPGPU_ZSTAMPS
+        if (lane() == 0) {
+            for (int k = 0; k < 4; k++) atomicAdd(&g_zst[k], (unsigned long long)e.prof[k]);
+            atomicAdd(&g_zst[4], (unsigned long long)(wall_clock64() - t0));
+            atomicAdd(&g_zst[5], 1ull);
+            atomicAdd(&g_zst[6], (unsigned long long)total);
+            atomicMax(&g_zst[7], (unsigned long long)(wall_clock64() - t0));
+        }
+#endif
+    }
+    const uint64_t cap = rc != 0 ? 0 : (total + 15) & ~15ull;
+    if (lane() == 0) {
+        const int32_t rcount = R->record_count;
+        j.dcap[b] = cap;
+        j.slots[b] = ((j.flags & RPGPU_JOB_PARSE) && rcount > 0 && (uint64_t)rcount <= cap) ? (uint64_t)rcount : 0;
+        j.inf_state[i] = rc != 0 ? 1u : again ? 2u : 0u;
+        j.inf_off[i] = soff;
+        j.inf_total[i] = total;
+    }
+}
+
+// the second pass of zstd member i, into its arena slot
+DEV void zstd_item(const DeviceJob& j, uint8_t* lds, rpgpu_batch_result* R, uint64_t dst, uint64_t cap) {
+    zs::Tabs* T = (zs::Tabs*)(lds + kInfRing);
+    InfIn in = inf_batch(j, R);
+    ZDev e = zdev(in, lds, j.decoded + dst, cap);
+    uint64_t total = 0;
+    bool unsure = false;
+    const int rc = zs::payload(e, T, in.n, total, unsure);
+    e.flush_all();
+    if (rc == 0 && !unsure && e.stored >= total && lane() == 0) {
+        R->flags = R->flags | RPGPU_F_CODEC_OK;
+        R->decoded_len = (uint32_t)total;
+        R->reserved0 = 0;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// The member kernels: one wave per workgroup (the ring and the tables are the
+// wave's own LDS, sized for the larger decoder), members claimed one at a
+// time from inf_list, gzip and zstd alike, so both codecs' members run side
+// by side.  The gzip CRC table shares LDS with the zstd tables: it is
+// reloaded before a gzip member that follows a zstd one.
+//   k_members_first (after k_emit, before the slot scans): the first pass;
+//   k_inflate_copy: state-0 members from scratch into the arena;
+//   k_members: the second pass of state-2 members.
+// ---------------------------------------------------------------------------
+constexpr uint32_t kMemLds = kZsLds > kInfLdsDecode ? kZsLds : kInfLdsDecode;
+
+__global__ __launch_bounds__(64) void k_members_first(DeviceJob j) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    InfTabs* T = (InfTabs*)(lds + kInfRing);
+    const InfWave W = inf_wave();
+    bool tab = false;
     const uint32_t count = j.counters[16];
     for (;;) {
-        const uint32_t i = wave_fetch_add(&j.counters[20], 1u);
+        const uint32_t i = wave_fetch_add(&j.counters[17], 1u);
         if (i >= count) break;
         const uint32_t b = uni32(j.inf_list[i]);
         const rpgpu_batch_result* R = &j.batches[b];
-        if ((uni32((uint32_t)(uint16_t)R->attrs) & 7u) != RPGPU_CODEC_ZSTD) continue;
-        InfIn in = inf_batch(j, R);
-        uint64_t total = 0, soff = 0;
-        int rc = -1;  // compressor::uncompress throws on an empty payload (compression/compression.cc:34-55)
-        bool again = true;
-        if (in.n) {
-            const uint64_t guess = zs_guess(in);
-            soff = uni64(atomicAdd((unsigned long long*)j.inf_scratch_used, lane() == 0 ? (unsigned long long)guess : 0ull));
-            const uint64_t cap = soff + guess <= j.inf_scratch_bytes ? guess : 0;
-            ZDev e = zdev(in, lds, j.inf_scratch + soff, cap);
-            bool unsure = false;
-            rc = zs::payload(e, T, in.n, total, unsure);
-            e.flush_all();
-            again = unsure || e.stored < total;
-        }
-        const uint64_t cap = rc != 0 ? 0 : (total + 15) & ~15ull;
-        if (lane() == 0) {
-            const int32_t rcount = R->record_count;
-            j.dcap[b] = cap;
-            j.slots[b] = ((j.flags & RPGPU_JOB_PARSE) && rcount > 0 && (uint64_t)rcount <= cap) ? (uint64_t)rcount : 0;
-            j.inf_state[i] = rc != 0 ? 1u : again ? 2u : 0u;
-            j.inf_off[i] = soff;
-            j.inf_total[i] = total;
+        if ((uni32((uint32_t)(uint16_t)R->attrs) & 7u) == RPGPU_CODEC_GZIP) {
+            if (!tab) inf_load_tab(T->crc_tab);
+            tab = true;
+            gzip_first_item(j, lds, T, W, i, b, R);
+        } else {
+            tab = false;
+            zstd_first_item(j, lds, i, b, R);
         }
     }
 }
 
-// second pass: zstd members that outgrew their scratch slot, into the arena
-__global__ __launch_bounds__(64) void k_zstd(DeviceJob j) {
+__global__ __launch_bounds__(64) void k_members(DeviceJob j) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-    zs::Tabs* T = (zs::Tabs*)(lds + kInfRing);
+    InfTabs* T = (InfTabs*)(lds + kInfRing);
+    const InfWave W = inf_wave();
+    bool tab = false;
     const uint32_t count = j.counters[16];
     for (;;) {
-        const uint32_t i = wave_fetch_add(&j.counters[21], 1u);
+        const uint32_t i = wave_fetch_add(&j.counters[18], 1u);
         if (i >= count) break;
         if (uni32(j.inf_state[i]) != 2) continue;
         const uint32_t b = uni32(j.inf_list[i]);
         rpgpu_batch_result* R = &j.batches[b];
-        if ((uni32((uint32_t)(uint16_t)R->attrs) & 7u) != RPGPU_CODEC_ZSTD) continue;
         const uint64_t dst = uni64(j.dcap[b]), cap = uni64(j.dcap[b + 1]) - dst;
         if (dst + cap > j.decoded_capacity) {
             if (lane() == 0) R->flags = R->flags | RPGPU_F_DECODE_OVERFLOW;
             continue;
         }
-        InfIn in = inf_batch(j, R);
-        ZDev e = zdev(in, lds, j.decoded + dst, cap);
-        uint64_t total = 0;
-        bool unsure = false;
-        const int rc = zs::payload(e, T, in.n, total, unsure);
-        e.flush_all();
-        if (rc == 0 && !unsure && e.stored >= total && lane() == 0) {
-            R->flags = R->flags | RPGPU_F_CODEC_OK;
-            R->decoded_len = (uint32_t)total;
-            R->reserved0 = 0;
+        if ((uni32((uint32_t)(uint16_t)R->attrs) & 7u) == RPGPU_CODEC_GZIP) {
+            if (!tab) inf_load_tab(T->crc_tab);
+            tab = true;
+            gzip_item(j, lds, T, W, R, dst, cap);
+        } else {
+            tab = false;
+            zstd_item(j, lds, R, dst, cap);
         }
     }
 }
 
+#ifdef RPGPU_ZSTAMPS
+__global__ void k_zstamps(int print) {
+    if (print)
+        printf("RPGPU_ZSTAMPS payloads=%llu out=%llu wall_ms(sum) lits=%.1f match=%.1f ends=%.1f blocks=%.1f total=%.1f max_payload_ms=%.2f\n",
+               g_zst[5], g_zst[6], g_zst[0] * 1e-5, g_zst[1] * 1e-5, g_zst[2] * 1e-5, g_zst[3] * 1e-5,
+               g_zst[4] * 1e-5, g_zst[7] * 1e-5);
+    for (int k = 0; k < 8; k++) g_zst[k] = 0;
+}
+#endif
+
 hipError_t launch_inflate_plan(const DeviceJob& j, hipStream_t s, uint32_t grid) {
     static bool attr = false;
     if (!attr) {
-        (void)hipFuncSetAttribute((const void*)k_inflate_first, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  (int)kInfLdsDecode);
-        (void)hipFuncSetAttribute((const void*)k_zstd_first, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kZsLds);
+        (void)hipFuncSetAttribute((const void*)k_members_first, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kMemLds);
         attr = true;
     }
-    hipLaunchKernelGGL(k_inflate_first, dim3(grid), dim3(64), kInfLdsDecode, s, j);
-    hipLaunchKernelGGL(k_zstd_first, dim3(grid), dim3(64), kZsLds, s, j);
+#ifdef RPGPU_ZSTAMPS
+    hipLaunchKernelGGL(k_zstamps, dim3(1), dim3(1), 0, s, 0);
+#endif
+    hipLaunchKernelGGL(k_members_first, dim3(grid), dim3(64), kMemLds, s, j);
+#ifdef RPGPU_ZSTAMPS
+    hipLaunchKernelGGL(k_zstamps, dim3(1), dim3(1), 0, s, 1);
+#endif
     return hipGetLastError();
 }
 
 hipError_t launch_inflate(const DeviceJob& j, hipStream_t s, uint32_t grid) {
     static bool attr = false;
     if (!attr) {
-        (void)hipFuncSetAttribute((const void*)k_inflate, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kInfLdsDecode);
-        (void)hipFuncSetAttribute((const void*)k_zstd, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kZsLds);
+        (void)hipFuncSetAttribute((const void*)k_members, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kMemLds);
         attr = true;
     }
-    hipLaunchKernelGGL(k_inflate_copy, dim3(grid), dim3(256), 0, s, j);
-    hipLaunchKernelGGL(k_inflate, dim3(grid), dim3(64), kInfLdsDecode, s, j);
-    hipLaunchKernelGGL(k_zstd, dim3(grid), dim3(64), kZsLds, s, j);
+    hipLaunchKernelGGL(k_inflate_copy, dim3(grid), dim3(64 * 4), 0, s, j);
+    hipLaunchKernelGGL(k_members, dim3(grid), dim3(64), kMemLds, s, j);
     return hipGetLastError();
 }
 

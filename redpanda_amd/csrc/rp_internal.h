@@ -160,8 +160,8 @@ struct DeviceJob {
                                   // [9] slab pool cursor, [10] k_lz_walk claim cursor, [11] long pieces,
                                   // [12] long-piece claim cursor, [13] k_validate_decoded claim cursor,
                                   // [14] k_decode_finish claim cursor, [15] k_crc_split claim cursor,
-                                  // [16] gzip / zstd members (inf_list), [17] k_inflate_first / [18] k_inflate claim cursors,
-                                  // [19] host-decoded members (host_list), [20] k_zstd_first / [21] k_zstd claim cursors
+                                  // [16] gzip / zstd members (inf_list), [17] k_members_first / [18] k_members claim cursors,
+                                  // [19] host-decoded members (host_list)
     uint32_t* decode_list;        // batch_capacity: ordinals of batches to uncompress
     uint32_t* seq_list;           // batch_capacity: decode items decoded whole by one lane
     uint32_t* link_list;          // batch_capacity: decode items whose linked LZ4F blocks one wave decodes in order
@@ -183,7 +183,7 @@ struct DeviceJob {
     uint32_t* seg_first_bad;      // n_segments: first chain ordinal failing complete && crc_ok (atomicMin)
     const uint64_t* seeds;        // optional chain seeds (index-seeded discovery), per segment ascending
     const uint64_t* seed_off;     // n_segments + 1
-    uint32_t* inf_list;           // batch_capacity: ordinals of gzip / zstd batches (k_inflate* / k_zstd*)
+    uint32_t* inf_list;           // batch_capacity: ordinals of gzip / zstd batches (k_members_first / k_members)
     uint32_t* inf_state;          // batch_capacity: 0 decoded into scratch, 1 rejected, 2 decode again (k_inflate)
     uint64_t* inf_off;            // batch_capacity: scratch offset of each member's first-pass output
     uint64_t* inf_total;          // batch_capacity: decoded bytes of each member

@@ -595,7 +595,7 @@ __global__ __launch_bounds__(256) void k_emit(DeviceJob j) {
             // decode work list for k_decode (order is irrelevant: every item
             // writes only its own batch and its own reserved arena slot)
             if (complete && decodable) j.decode_list[atomicAdd(&j.counters[2], 1u)] = (uint32_t)ord;
-            // gzip and zstd members: sized by k_inflate_first / k_zstd_first (dcap /
+            // gzip and zstd members: sized by k_members_first (dcap /
             // slots above are 0 until then)
             if (complete && (j.flags & RPGPU_JOB_DECODE) &&
                 (codec == RPGPU_CODEC_GZIP || (codec == RPGPU_CODEC_ZSTD && !host_codec)))

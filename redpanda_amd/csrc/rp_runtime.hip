@@ -190,7 +190,7 @@ struct rpgpu_ctx {
         bool pinned = false;
     } hc_items, hc_items_h, hc_in, hc_in_h, hc_out, hc_out_h, hc_small;
     uint32_t hc_n = 0;
-    // gzip first-pass output pool (k_inflate_first), grow-only
+    // gzip / zstd first-pass output pool (k_members_first), grow-only
     void* gz_pool = nullptr;
     size_t gz_pool_bytes = 0;
 };

@@ -39,6 +39,10 @@
 #ifndef ZS_TRACE
 #define ZS_TRACE(...)
 #endif
+// per-phase timing hook of diagnostic builds (RPGPU_ZSTAMPS)
+#ifndef ZS_PROF
+#define ZS_PROF(k, stmt) stmt
+#endif
 
 namespace rp {
 namespace zs {
@@ -468,7 +472,7 @@ struct Lits {
     Bits s[4];
     uint32_t cnt[4], dec[4];
     bool x2;           // the streams decode through libzstd's double-symbol table (HUF_decompress4X2)
-    uint32_t pend[4];  // X2: the next symbol is the second of a double-symbol step
+    uint32_t pend[4];  // X2: code length of the symbol that opened the current step, 0 if none is open
 };
 
 // HUF_selectDecoder (huf_decompress.c): the double-symbol decoder for a
@@ -495,32 +499,43 @@ ZS_FN bool huf_select_x2(uint32_t dsize, uint64_t csize) {
 // when it starts a step alone (HUF_decodeLastSymbolX2): a double entry there
 // consumes both codes, clamped to the container, or nothing once the
 // container is spent.
+// n literals of one stream (left = the stream's symbols not yet decoded).
+// X1 (single-symbol table): each symbol's code is consumed.  X2 (libzstd's
+// double-symbol table, 12-bit lookups): a step decodes two symbols when the
+// second code fits the 12 bits after the first, so the symbols are the same;
+// only the stream's last symbol differs when it starts a step alone
+// (HUF_decodeLastSymbolX2): a double entry there consumes both codes,
+// clamped to the container, or nothing once the container is spent.  The
+// container is refilled only when the next lookup could run past it (the
+// decoded values and the end check do not depend on when libzstd refills),
+// and always before a stream's last symbol (whose X2 clamp does).
 template <class E>
-ZS_FN uint32_t huf_sym(E& e, Tabs* T, Bits& s, uint32_t& pend, uint32_t left, bool x2, uint32_t hlog) {
-    bits_reload(e, s);
-    const uint32_t v = e.U((uint32_t)((s.c << (s.used & 63)) >> ((64 - hlog) & 63)));
-    const uint32_t d = e.U(T->huf[v]);
-    const uint32_t l1 = d >> 8;
-    if (x2) {
-        if (pend) {
-            pend = 0;
-        } else {
-            const uint32_t w = e.U((uint32_t)((s.c << ((s.used + l1) & 63)) >> ((64 - hlog) & 63)));
-            const uint32_t l2 = e.U(T->huf[w]) >> 8;
-            const bool pair = l1 + l2 <= 12;
-            if (left >= 2) {
-                pend = pair ? 1u : 0u;
-            } else if (pair) {
-                if (s.used < 64) s.used = s.used + l1 + l2 > 64 ? 64u : s.used + l1 + l2;
-                return d & 0xFFu;
+ZS_FN void huf_run(E& e, Tabs* T, Bits& s, uint32_t& open, uint32_t left, uint32_t n, bool x2, uint32_t hlog,
+                   bool emit) {
+    for (uint32_t i = 0; i < n; i++, left--) {
+        if (left == 1 || s.used > 64 - hlog) bits_reload(e, s);
+        const uint32_t v = e.U((uint32_t)((s.c << (s.used & 63)) >> ((64 - hlog) & 63)));
+        const uint32_t d = e.U(T->huf[v]);
+        const uint32_t l1 = d >> 8;
+        if (x2) {
+            const bool paired = open && open + l1 <= 12;
+            if (left == 1 && !paired) {
+                const uint32_t w = e.U((uint32_t)((s.c << ((s.used + l1) & 63)) >> ((64 - hlog) & 63)));
+                const uint32_t l2 = e.U(T->huf[w]) >> 8;
+                if (l1 + l2 <= 12) {  // a double entry for the lone last symbol
+                    if (s.used < 64) s.used = s.used + l1 + l2 > 64 ? 64u : s.used + l1 + l2;
+                    if (emit) e.lit(d & 0xFFu);
+                    continue;
+                }
             }
+            open = paired ? 0u : l1;
         }
+        s.used += l1;
+        if (emit) e.lit(d & 0xFFu);
     }
-    s.used += l1;
-    return d & 0xFFu;
 }
 // stream K (a constant: the per-stream state stays in registers on the device)
-#define ZS_HUF(K) huf_sym(e, T, L.s[K], L.pend[K], L.cnt[K] - L.dec[K], L.x2, hlog)
+#define ZS_RUN(K, N, EMIT) huf_run(e, T, L.s[K], L.pend[K], L.cnt[K] - L.dec[K], N, L.x2, hlog, EMIT)
 
 template <class E>
 ZS_FN void lits_emit(E& e, Tabs* T, Lits& L, uint32_t k, uint32_t hlog) {
@@ -531,27 +546,27 @@ ZS_FN void lits_emit(E& e, Tabs* T, Lits& L, uint32_t k, uint32_t hlog) {
         e.fill(L.rle, k);
         L.used += k;
     } else {
-        for (uint32_t i = 0; i < k; i++) {
+        while (k) {
             while (L.used == L.curend) {  // the next stream's segment
                 L.cur++;
                 L.curend += L.seg;
             }
-            uint32_t v;
+            const uint32_t m = L.curend - L.used < k ? L.curend - L.used : k;
             if (L.cur == 0) {
-                v = ZS_HUF(0);
-                L.dec[0]++;
+                ZS_RUN(0, m, true);
+                L.dec[0] += m;
             } else if (L.cur == 1) {
-                v = ZS_HUF(1);
-                L.dec[1]++;
+                ZS_RUN(1, m, true);
+                L.dec[1] += m;
             } else if (L.cur == 2) {
-                v = ZS_HUF(2);
-                L.dec[2]++;
+                ZS_RUN(2, m, true);
+                L.dec[2] += m;
             } else {
-                v = ZS_HUF(3);
-                L.dec[3]++;
+                ZS_RUN(3, m, true);
+                L.dec[3] += m;
             }
-            e.lit(v);
-            L.used++;
+            L.used += m;
+            k -= m;
         }
     }
 }
@@ -560,12 +575,12 @@ ZS_FN void lits_emit(E& e, Tabs* T, Lits& L, uint32_t k, uint32_t hlog) {
 template <class E>
 ZS_FN bool lits_finish(E& e, Tabs* T, Lits& L, uint32_t hlog) {
     if (L.kind != 2) return true;
-#define ZS_FIN(K)                       \
-    while (L.dec[K] < L.cnt[K]) {       \
-        ZS_HUF(K);                      \
-        L.dec[K]++;                     \
-    }                                   \
-    bits_reload(e, L.s[K]);             \
+#define ZS_FIN(K)                                   \
+    if (L.dec[K] < L.cnt[K]) {                      \
+        ZS_RUN(K, L.cnt[K] - L.dec[K], false);      \
+        L.dec[K] = L.cnt[K];                        \
+    }                                               \
+    bits_reload(e, L.s[K]);                         \
     if (!bits_end(L.s[K])) return false;
     ZS_FIN(0)
     if (L.ns == 4) {
@@ -576,7 +591,7 @@ ZS_FN bool lits_finish(E& e, Tabs* T, Lits& L, uint32_t hlog) {
 #undef ZS_FIN
     return true;
 }
-#undef ZS_HUF
+#undef ZS_RUN
 
 // ---------------------------------------------------------------------------
 // Frame state and one compressed block
@@ -777,11 +792,11 @@ ZS_FN int64_t block(E& e, Tabs* T, Frame& F, uint64_t bp, uint64_t bn, uint64_t 
             // ZSTD_execSequence's checks, then the copies
             if (ll + ml > capb - bo) return -1;
             if (ll > (uint64_t)(L.size - L.used)) return -1;
-            if (ll) lits_emit(e, T, L, (uint32_t)ll, F.hlog);
+            if (ll) ZS_PROF(0, lits_emit(e, T, L, (uint32_t)ll, F.hlog));
             bo += ll;
             F.fo += ll;
             if (off > F.fo - F.seg0 + F.prevlen) return -1;  // beyond the prefix and the previous segment
-            e.match(off, ml);
+            ZS_PROF(1, e.match(off, ml));
             bo += ml;
             F.fo += ml;
             bits_reload(e, d);
@@ -794,10 +809,12 @@ ZS_FN int64_t block(E& e, Tabs* T, Frame& F, uint64_t bp, uint64_t bn, uint64_t 
     }
     const uint32_t last = L.size - L.used;
     if (last > capb - bo) return -1;
-    if (last) lits_emit(e, T, L, last, F.hlog);
+    if (last) ZS_PROF(0, lits_emit(e, T, L, last, F.hlog));
     bo += last;
     F.fo += last;
-    if (!lits_finish(e, T, L, F.hlog)) return -1;
+    bool fin = false;
+    ZS_PROF(2, fin = lits_finish(e, T, L, F.hlog));
+    if (!fin) return -1;
     return (int64_t)bo;
 }
 
@@ -971,7 +988,8 @@ ZS_FN int payload(E& e, Tabs* T, uint64_t n, uint64_t& total, bool& unsure) {
             } else {
                 if (avail < bsz) return 0;
                 if (bsz >= kBlockMax) return -1;
-                const int64_t o = block(e, T, F, ip, bsz, capb);
+                int64_t o = -1;
+                ZS_PROF(3, o = block(e, T, F, ip, bsz, capb));
                 if (o < 0) return -1;
                 r = (uint64_t)o;
             }

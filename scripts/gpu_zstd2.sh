@@ -1,0 +1,10 @@
+# zstd on the device: parity + microbench + C6
+set -e
+cd "$GRAFT_REPO_ROOT"
+export TMPDIR=/tmp
+timeout -k 10 400 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -v --timeout 300 --timeout-method thread \
+  -k "zstd or gzip" > gpurun_out/pytest_zstd.log 2>&1 || { tail -60 gpurun_out/pytest_zstd.log; exit 1; }
+tail -3 gpurun_out/pytest_zstd.log
+timeout -k 10 300 python -u scripts/mb_inflate.py
+timeout -k 10 400 python -u bench.py --workloads c6 --steps 5 --warmup 1 --no-index --no-cpu-baseline > gpurun_out/bench_c6.json 2> gpurun_out/bench_c6.err || { tail -30 gpurun_out/bench_c6.err; exit 1; }
+python -c "import json; d=json.load(open('gpurun_out/bench_c6.json')); c=d['config']['c6']; print(c['ms_per_step'], c['stage_ms'], c['parity'])"

@@ -11,12 +11,16 @@ from redpanda_amd.engine import Engine
 
 eng = Engine(0)
 F = abi.JOB_CRC | abi.JOB_PARSE | abi.JOB_DECODE
-for nseg, seg_mib, bmin, bmax in [(1, 2, 1 << 20, 1 << 20), (1, 2, 64 << 10, 64 << 10), (16, 16, 1 << 20, 1 << 20),
-                                  (64, 16, 64 << 10, 256 << 10)]:
+for codec, nseg, seg_mib, bmin, bmax in [(1, 1, 2, 1 << 20, 1 << 20), (1, 1, 2, 64 << 10, 64 << 10),
+                                         (1, 16, 16, 1 << 20, 1 << 20), (1, 64, 16, 64 << 10, 256 << 10),
+                                         (4, 1, 2, 1 << 20, 1 << 20), (4, 1, 2, 64 << 10, 64 << 10),
+                                         (4, 16, 16, 1 << 20, 1 << 20), (4, 64, 16, 64 << 10, 256 << 10)]:
+    w = [0] * 6
+    w[codec] = 1
     segs = []
     for i in range(nseg):
         a = np.zeros(seg_mib << 20, np.uint8)
-        synth.gen_segment(a, i, seed=77 + i, batch_bytes=0, min_batch=bmin, max_batch=bmax, weights=[0, 1, 0, 0, 0, 0],
+        synth.gen_segment(a, i, seed=77 + i, batch_bytes=0, min_batch=bmin, max_batch=bmax, weights=w,
                           size_uniform=True)
         segs.append(a)
     offs = np.cumsum([0] + [s.size for s in segs]).astype(np.uint64)
@@ -33,5 +37,5 @@ for nseg, seg_mib, bmin, bmax in [(1, 2, 1 << 20, 1 << 20), (1, 2, 64 << 10, 64 
     torch.cuda.synchronize()
     tm = eng.last_timings()
     eng.set_timing(False)
-    print(f"{nseg}x{seg_mib}MiB batches {len(f)} ok {ok} decoded {dec/1e6:.1f} MB: plan+resolve {tm['resolve_plan']:.2f} ms "
+    print(f"{'gzip' if codec == 1 else 'zstd'} {nseg}x{seg_mib}MiB batches {len(f)} ok {ok} decoded {dec/1e6:.1f} MB: plan+resolve {tm['resolve_plan']:.2f} ms "
           f"decode {tm['decode']:.2f} ms -> {dec / (tm['decode'] * 1e-3) / 1e9:.2f} GB/s decode pass", flush=True)

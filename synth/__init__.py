@@ -100,7 +100,7 @@ C2 = dict(seed=0xC2, batch_bytes=0, min_batch=64 << 10, max_batch=1 << 20, weigh
           size_uniform=True, lz4_linked_ppm=100000, lz4_content_checksum_ppm=100000)
 C5 = dict(seed=0xC5, batch_bytes=0, min_batch=200, max_batch=1 << 20, weights=[40, 0, 15, 30, 0, 15],
           corrupt_payload_ppm=10000, corrupt_header_ppm=2000, corrupt_zero_ppm=1000, truncate_tail=True)
-# C5 with 10% gzip and 10% zstd: gzip on the device,
-# zstd through RPGPU_JOB_HOST_CODECS
+# C5 with 10% gzip and 10% zstd: both decoded on the
+# device (zstd through the host with RPGPU_JOB_HOST_CODECS)
 C6 = dict(seed=0xC6, batch_bytes=0, min_batch=200, max_batch=1 << 20, weights=[32, 10, 12, 24, 10, 12],
           corrupt_payload_ppm=10000, corrupt_header_ppm=2000, corrupt_zero_ppm=1000, truncate_tail=True)
