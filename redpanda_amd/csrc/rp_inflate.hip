@@ -339,20 +339,26 @@ DEV void inf_flush_upto(InfOut& o, uint64_t op) {
     while ((op >> 10) > (o.flushed >> 10)) inf_flush(o, 1024u);
 }
 
-// match: ml bytes from dist back (dist <= op, checked)
+// match: ml bytes from dist back (dist <= op, checked).  A match overlapping
+// its own output (dist < ml) repeats the dist bytes before it: byte k is
+// k mod dist into them, by a multiply with the rounded-up reciprocal (exact
+// for k < 2^32 / dist); every read is issued before any write.
 DEV void inf_copy(InfOut& o, uint64_t op, uint32_t dist, uint32_t ml) {
     const uint32_t l = lane();
+    const bool rep = dist < ml;
+    const uint64_t mg = rep ? 0xFFFFFFFFull / dist + 1ull : 0ull;
+    const uint32_t n = (ml + 63) >> 6;  // deflate: ml <= 258, at most 5 rows
     uint32_t b[5];
 #pragma unroll
     for (uint32_t i = 0; i < 5; i++) {
         const uint32_t k = 64u * i + l;
-        const uint32_t from = (uint32_t)(op - dist) + (dist >= ml ? k : k % dist);
-        b[i] = k < ml ? (uint32_t)o.ring[from & kInfMask] : 0u;  // every read before any write
+        const uint32_t x = rep ? k - (uint32_t)(((uint64_t)k * mg) >> 32) * dist : k;
+        b[i] = (i < n && k < ml) ? (uint32_t)o.ring[((uint32_t)(op - dist) + x) & kInfMask] : 0u;
     }
 #pragma unroll
     for (uint32_t i = 0; i < 5; i++) {
         const uint32_t k = 64u * i + l;
-        if (k < ml) o.ring[(uint32_t)(op + k) & kInfMask] = (uint8_t)b[i];
+        if (i < n && k < ml) o.ring[(uint32_t)(op + k) & kInfMask] = (uint8_t)b[i];
     }
 }
 
@@ -572,6 +578,18 @@ DEV int inflate_member(InfIn& in, InfTabs* T, InfOut& o, const InfSymTabs& ST, u
                 uint32_t bc = 32 - sh;
                 pq += 4;
                 bool eob = false;
+                // literals gathered one per lane, written to the ring 64 at a
+                // time (a single-lane LDS store per literal was an exec-mask
+                // round trip each)
+                uint32_t lb = 0, nl = 0;
+                auto spill = [&]() __attribute__((always_inline)) {
+                    if (nl) {
+                        if (l < nl) o.ring[(uint32_t)(op + l) & kInfMask] = (uint8_t)lb;
+                        op += nl;
+                        nl = 0;
+                        inf_flush_upto(o, op);
+                    }
+                };
                 // safe while the next two refills stay inside the member
                 while (pq + 12 <= in.nphys) {
                     while (bc <= 32) {
@@ -590,11 +608,11 @@ DEV int inflate_member(InfIn& in, InfTabs* T, InfOut& o, const InfSymTabs& ST, u
                     bb >>= len;
                     bc -= len;
                     if (sym < 256) {
-                        if (l == 0) o.ring[(uint32_t)op & kInfMask] = (uint8_t)sym;
-                        op++;
-                        if ((op & 1023) == 0) inf_flush(o, 1024u);
+                        lb = l == nl ? sym : lb;
+                        if (++nl == 64) spill();
                         continue;
                     }
+                    spill();
                     if (sym == 256) { eob = true; break; }
                     if (sym > 285) return -1;  // invalid literal/length code
                     const uint32_t lt = rl(ST.len, (int)(sym - 257));
@@ -628,6 +646,7 @@ DEV int inflate_member(InfIn& in, InfTabs* T, InfOut& o, const InfSymTabs& ST, u
                     op += ml;
                     inf_flush_upto(o, op);
                 }
+                spill();
                 bp = 8 * (pq - in.mis) - bc;  // the bits consumed
                 if (eob) {
                     if (last) break;
