@@ -898,12 +898,14 @@ struct ZDev {
     InfIn in;
     inf_lds_u8* ring;
     uint8_t* dst;
-    uint64_t cap;      // bytes the slot holds (a multiple of 16)
-    uint64_t op;       // output position
-    uint64_t flushed;  // output below left the ring (1 KiB aligned until the end)
-    uint64_t stored;   // output below is in the slot
+    // output positions are 32-bit (SALU compares; the slot is < 2 GiB, and
+    // output past 2^32 only counts: the core's totals are 64-bit)
+    uint32_t cap;      // bytes the slot holds (a multiple of 16)
+    uint32_t op;       // output position
+    uint32_t flushed;  // output below left the ring (1 KiB aligned until the end)
+    uint32_t stored;   // output below is in the slot
     bool over;         // the output outgrew the slot: only counted from then on
-    uint64_t fstart;   // the current frame's first output byte
+    uint32_t fstart;   // the current frame's first output byte
     uint32_t lbuf;     // Huffman literals gathered one per lane before they go to the ring
     uint32_t nlit;
     __amdgpu_buffer_rsrc_t rs;
@@ -946,19 +948,19 @@ struct ZDev {
     // [flushed, flushed + len) out of the ring (flushed 1 KiB aligned, len <= 1 KiB)
     DEV void flush(uint32_t len) {
         if (!over) {
-            const uint64_t room = cap > flushed ? cap - flushed : 0;
+            const uint32_t room = cap > flushed ? cap - flushed : 0u;
             const uint32_t at = 16u * lane();
             if (at < len && at < room) {
                 const uint4 v = *(const uint4*)(ring + ((uint32_t)(flushed + at) & kInfMask));
                 *(uint4*)(dst + flushed + at) = v;
             }
-            const uint64_t end = flushed + len;
-            stored = end < cap ? end : cap;
+            const uint64_t end = (uint64_t)flushed + len;
+            stored = end < cap ? (uint32_t)end : cap;
             if (end > cap) over = true;
         }
         flushed += len;
     }
-    DEV void flush_upto(uint64_t p) {
+    DEV void flush_upto(uint32_t p) {
         while ((p >> 10) > (flushed >> 10)) flush(1024u);
     }
     DEV void lit_spill() {
@@ -1013,7 +1015,7 @@ struct ZDev {
         lit_spill();
         const uint32_t l = lane();
         if (over) {
-            op += ml;
+            op += (uint32_t)ml;
             flush_upto(op);
             return;
         }
@@ -1033,10 +1035,10 @@ struct ZDev {
                 v[t] = 0;
                 if (x < m) {
                     if (far) {
-                        v[t] = __builtin_amdgcn_raw_buffer_load_b8(rs, (int)(op + x - off), 0, kZsSc1);
+                        v[t] = __builtin_amdgcn_raw_buffer_load_b8(rs, (int)(op + x - (uint32_t)off), 0, kZsSc1);
                     } else {
                         const uint64_t sx = rep ? x - (((uint64_t)x * mg) >> 32) * off : (uint64_t)x;
-                        v[t] = ring[(uint32_t)(op - off + sx) & kInfMask];
+                        v[t] = ring[(op - (uint32_t)off + (uint32_t)sx) & kInfMask];
                     }
                 }
             }
@@ -1054,9 +1056,9 @@ struct ZDev {
         fstart = op;
     }
     // output byte q of this member (the slot below `flushed`, else the ring)
-    DEV uint32_t byte_at(uint64_t q) {
+    DEV uint32_t byte_at(uint32_t q) {
         return q < flushed ? (uint32_t)__builtin_amdgcn_raw_buffer_load_b8(rs, (int)q, 0, kZsSc1)
-                           : (uint32_t)ring[(uint32_t)q & kInfMask];
+                           : (uint32_t)ring[q & kInfMask];
     }
     // XXH64 of the frame's output [fstart, op) vs the trailer's low 32 bits:
     // 1 equal, 0 not, 2 unknown (the bytes outgrew the slot)
@@ -1065,13 +1067,13 @@ struct ZDev {
         if (over || stored < flushed) return 2;
         zs_wait_vm();
         const uint32_t l = lane();
-        const uint64_t len = op - fstart, body = len & ~31ull;
+        const uint32_t len = op - fstart, body = len & ~31u;
         uint64_t h;
         if (len >= 32) {
             // lanes 0..3 hold the four accumulators; a 1 KiB piece at a time
             uint64_t acc = l == 0 ? kXP1 + kXP2 : l == 1 ? kXP2 : l == 2 ? 0ull : 0ull - kXP1;
-            for (uint64_t c = 0; c < body; c += 1024) {
-                const uint32_t m = body - c < 1024 ? (uint32_t)(body - c) : 1024u;
+            for (uint32_t c = 0; c < body; c += 1024) {
+                const uint32_t m = body - c < 1024 ? body - c : 1024u;
                 uint32_t w[4] = {0u, 0u, 0u, 0u};
                 if (16u * l < m) {
 #pragma unroll
@@ -1099,8 +1101,8 @@ struct ZDev {
             h = kXP5;
         }
         h += len;
-        uint64_t q = fstart + body;
-        const uint64_t e = op;
+        uint32_t q = fstart + body;
+        const uint32_t e = op;
         while (q + 8 <= e) {
             uint64_t k = 0;
             for (uint32_t t = 0; t < 8; t++) k |= (uint64_t)uni32(byte_at(q + t)) << (8 * t);
@@ -1134,7 +1136,7 @@ DEV ZDev zdev(const InfIn& in, uint8_t* lds, uint8_t* dst, uint64_t cap) {
     e.in = in;
     e.ring = (inf_lds_u8*)lds;
     e.dst = dst;
-    e.cap = cap;
+    e.cap = cap < (1ull << 31) ? (uint32_t)cap : 0u;  // a slot past 2 GiB: count only (never one real batch)
     e.op = e.flushed = e.stored = 0;
     e.over = false;
     e.fstart = 0;
