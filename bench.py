@@ -152,10 +152,11 @@ def cpu_baseline_c1(host_seg, seconds_budget=15.0):
     }
 
 
-def cpu_baseline_decode(host_seg, positions, seconds_budget=12.0):
-    """liblz4 1.9.3 / libsnappy 1.1.8 (the reference's codec libraries) over
-    the complete batches of one segment: stored crc + uncompress (the
-    reference's driver loops) + decoded crc, one thread per core."""
+def cpu_baseline_decode(host_seg, positions, seconds_budget=12.0, gz_zstd=False):
+    """liblz4 1.9.3 / libsnappy 1.1.8 (the reference's codec libraries; for
+    C6 also zlib 1.2.11 and libzstd 1.4) over the complete batches of one
+    segment: stored crc + uncompress (the reference's driver loops) + decoded
+    crc, one thread per core."""
     from oracle import oracle as O
     cores = host_threads()
     pos = np.asarray(positions, dtype=np.uint64)
@@ -176,8 +177,10 @@ def cpu_baseline_decode(host_seg, positions, seconds_budget=12.0):
         "kind": "reference",
         "sample": f"{len(pos)} batches ({tb // max(reps, 1) >> 20} MiB stored) of partition 0: stored crc + "
                   f"liblz4 LZ4F_decompress / libsnappy RawUncompress (lz4_frame_compressor.cc:123-200 / "
-                  f"snappy_java_compressor.cc:76-129 loops) + decoded crc, {cores} threads x {reps} reps; "
-                  "record walk not included",
+                  f"snappy_java_compressor.cc:76-129 loops)"
+                  + (" / zlib inflate twice (gzip_compressor.cc:161-230) / libzstd ZSTD_decompressStream "
+                     "(stream_zstd.cc:152-178)" if gz_zstd else "")
+                  + f" + decoded crc, {cores} threads x {reps} reps; record walk not included",
         "one_core_GBs": round(b1 / s1 / 1e9, 3),
         "one_core_decoded_GBs": round(d1 / s1 / 1e9, 3),
         "host_logical_cpus": os.cpu_count(),
@@ -260,8 +263,8 @@ def run_compressed(name, kw, n_parts, seg_bytes, args, torch, device, eng, abi, 
     whole_alg = stored + decoded + IDX_BYTES_PER_RECORD * n_rec + RESULT_BYTES_PER_BATCH * len(b)
     traffic, kernels_traffic = profiled_traffic("decode_traffic.json", name, DECODE_KERNELS)
     cpu = None
-    if not args.no_cpu_baseline and len(positions) and name != "c6":
-        cpu = cpu_baseline_decode(host_first, positions)
+    if not args.no_cpu_baseline and len(positions):
+        cpu = cpu_baseline_decode(host_first, positions, gz_zstd=(name == "c6"))
     write_stats(args, name, {"stored": stored, "stored_payload": int(np.sum(b["size_bytes"].astype(np.int64)
                                                                           - abi.HEADER_SIZE)),
                              "compressed_in": comp_in, "decoded": decoded, "batches": int(len(b)),
@@ -304,7 +307,6 @@ def run_compressed(name, kw, n_parts, seg_bytes, args, torch, device, eng, abi, 
         st["per_codec"] = {str(c): {"batches": int(np.sum(codec == c)), "codec_ok": int(np.sum(dec_ok & (codec == c))),
                                     "decoded_bytes": int(np.sum(b["decoded_len"].astype(np.int64)[dec_ok & (codec == c)]))}
                            for c in (1, 2, 3, 4)}
-        st["cpu_baseline"] = None  # the liblz4 / libsnappy baseline does not cover gzip / zstd
         # gzip / zstd members decode in the member pass, which runs inside the
         # resolve_plan stage (it sizes their arena slots, as the reference's
         # buffer_for_input does); one wave per member

@@ -9,12 +9,22 @@
  *   ref_lz4f_uncompress   <- lz4_frame_compressor.cc:115-200 (do_uncompressed)
  *   ref_snappy_java       <- snappy_java_compressor.cc:76-129
  *   ref_snappy_raw        <- snappy_standard_compressor.cc:43-65
+ *   ref_gzip_uncompress   <- gzip_compressor.cc:161-230 (zlib 1.2.11: a sizing
+ *                            pass through a 512-byte buffer, then the decode)
+ *   ref_zstd_uncompress   <- stream_zstd.cc:152-178 (libzstd 1.4.8: static
+ *                            DCtx over estimateDStreamSize(8 MiB), 64 KiB
+ *                            output buffer appended when full)
+ * (gzip / zstd are used by the C6 CPU baseline only; their verdicts are
+ * pinned by the oracle's own tests.)
  * Return 0 ok, -1 where the reference throws, -2 output capacity too small.
  */
 #define _POSIX_C_SOURCE 199309L
 #include <lz4.h>
 #include <lz4frame.h>
 #include <snappy-c.h>
+#include <zlib.h>
+#define ZSTD_STATIC_LINKING_ONLY
+#include <zstd.h>
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
@@ -248,6 +258,70 @@ static void be40(const uint8_t* h, uint8_t* be) {
         for (int i = 0; i < f[k][1]; i++) be[o++] = h[f[k][0] + f[k][1] - 1 - i];
 }
 
+/* gzip_compressor::uncompress: inflateInit2(15 + 32) twice, the first pass
+ * only counting total_out through a 512-byte buffer (buffer_for_input) */
+int ref_gzip_uncompress(const uint8_t* src, size_t n, uint8_t* dst, size_t cap, size_t* out_len) {
+    *out_len = 0;
+    uint8_t small[512];
+    size_t total = 0;
+    for (int pass = 0; pass < 2; pass++) {
+        z_stream z;
+        memset(&z, 0, sizeof(z));
+        if (inflateInit2(&z, 15 + 32) != Z_OK) return -1;
+        z.next_in = (Bytef*)src;
+        z.avail_in = (uInt)n;
+        int rc = Z_OK;
+        if (pass == 0) {
+            do {
+                z.next_out = small;
+                z.avail_out = sizeof(small);
+                rc = inflate(&z, Z_NO_FLUSH);
+            } while (rc == Z_OK && z.avail_in > 0);
+            total = z.total_out;
+        } else {
+            if (total > cap) { inflateEnd(&z); return -2; }
+            z.next_out = dst;
+            z.avail_out = (uInt)total;
+            rc = inflate(&z, Z_NO_FLUSH);
+            *out_len = z.total_out;
+        }
+        inflateEnd(&z);
+        if (rc == Z_DATA_ERROR || rc == Z_NEED_DICT || rc == Z_STREAM_ERROR || rc == Z_MEM_ERROR) return -1;
+    }
+    return 0;
+}
+
+/* stream_zstd::do_uncompress */
+int ref_zstd_uncompress(const uint8_t* src, size_t n, uint8_t* dst, size_t cap, size_t* out_len) {
+    static __thread void* ws = NULL;
+    static __thread size_t ws_size = 0;
+    *out_len = 0;
+    if (!ws) {
+        ws_size = ZSTD_estimateDStreamSize((size_t)8 << 20);
+        ws = malloc(ws_size + (64u << 10));
+    }
+    uint8_t* obuf = (uint8_t*)ws + ws_size;
+    ZSTD_DCtx* d = ZSTD_initStaticDCtx(ws, ws_size);
+    if (!d) return -1;
+    ZSTD_outBuffer o = {obuf, 64u << 10, 0};
+    ZSTD_inBuffer i = {src, n, 0};
+    size_t total = 0;
+    while (i.pos != i.size) {
+        const size_t err = ZSTD_decompressStream(d, &o, &i);
+        if (i.pos != i.size && o.pos == o.size) {
+            if (total + o.size <= cap) memcpy(dst + total, obuf, o.size);
+            total += o.size;
+            o.pos = 0;
+        } else if (ZSTD_isError(err)) {
+            return -1;
+        }
+    }
+    if (total + o.pos <= cap) memcpy(dst + total, obuf, o.pos);
+    total += o.pos;
+    *out_len = total;
+    return total > cap ? -2 : 0;
+}
+
 typedef struct {
     const uint8_t* seg;
     const uint64_t* pos;
@@ -275,6 +349,8 @@ static void* dec_worker(void* arg) {
         int rc = -1;
         if (codec == 3) rc = ref_lz4f_uncompress(h + 61, n, buf, cap, &out);
         else if (codec == 2) rc = ref_snappy_java(h + 61, n, buf, cap, &out);
+        else if (codec == 1) rc = ref_gzip_uncompress(h + 61, n, buf, cap, &out);
+        else if (codec == 4) rc = ref_zstd_uncompress(h + 61, n, buf, cap, &out);
         else if (codec == 0) { rc = 0; out = 0; }
         if (rc == 0 && codec) {
             be[1] &= (uint8_t)~7u; /* codec bits cleared */
