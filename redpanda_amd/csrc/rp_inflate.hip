@@ -1246,18 +1246,24 @@ __global__ __launch_bounds__(64) void k_members_first(DeviceJob j) {
     const InfWave W = inf_wave();
     bool tab = false;
     const uint32_t count = j.counters[16];
-    for (;;) {
-        const uint32_t i = wave_fetch_add(&j.counters[17], 1u);
-        if (i >= count) break;
-        const uint32_t b = uni32(j.inf_list[i]);
-        const rpgpu_batch_result* R = &j.batches[b];
-        if ((uni32((uint32_t)(uint16_t)R->attrs) & 7u) == RPGPU_CODEC_GZIP) {
-            if (!tab) inf_load_tab(T->crc_tab);
-            tab = true;
-            gzip_first_item(j, lds, T, W, i, b, R);
-        } else {
-            tab = false;
-            zstd_first_item(j, lds, i, b, R);
+    // largest first (a member decodes serially, so a big one claimed last
+    // would set the pass's tail): members of >= 128 KiB stored, then the rest
+    for (uint32_t phase = 0; phase < 2; phase++) {
+        for (;;) {
+            const uint32_t i = wave_fetch_add(&j.counters[phase ? 20 : 17], 1u);
+            if (i >= count) break;
+            const uint32_t b = uni32(j.inf_list[i]);
+            const rpgpu_batch_result* R = &j.batches[b];
+            const bool big = uni32((uint32_t)R->size_bytes) >= (128u << 10);
+            if (big != (phase == 0)) continue;
+            if ((uni32((uint32_t)(uint16_t)R->attrs) & 7u) == RPGPU_CODEC_GZIP) {
+                if (!tab) inf_load_tab(T->crc_tab);
+                tab = true;
+                gzip_first_item(j, lds, T, W, i, b, R);
+            } else {
+                tab = false;
+                zstd_first_item(j, lds, i, b, R);
+            }
         }
     }
 }

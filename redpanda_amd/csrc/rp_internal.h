@@ -161,7 +161,7 @@ struct DeviceJob {
                                   // [12] long-piece claim cursor, [13] k_validate_decoded claim cursor,
                                   // [14] k_decode_finish claim cursor, [15] k_crc_split claim cursor,
                                   // [16] gzip / zstd members (inf_list), [17] k_members_first / [18] k_members claim cursors,
-                                  // [19] host-decoded members (host_list)
+                                  // [19] host-decoded members (host_list), [20] k_members_first's second claim cursor
     uint32_t* decode_list;        // batch_capacity: ordinals of batches to uncompress
     uint32_t* seq_list;           // batch_capacity: decode items decoded whole by one lane
     uint32_t* link_list;          // batch_capacity: decode items whose linked LZ4F blocks one wave decodes in order
