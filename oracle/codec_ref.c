@@ -291,15 +291,12 @@ int ref_gzip_uncompress(const uint8_t* src, size_t n, uint8_t* dst, size_t cap, 
     return 0;
 }
 
-/* stream_zstd::do_uncompress */
-int ref_zstd_uncompress(const uint8_t* src, size_t n, uint8_t* dst, size_t cap, size_t* out_len) {
-    static __thread void* ws = NULL;
-    static __thread size_t ws_size = 0;
+/* stream_zstd::do_uncompress; ws: ZSTD_estimateDStreamSize(8 MiB) + 64 KiB
+ * bytes of the caller's (the reference keeps one static workspace) */
+size_t ref_zstd_workspace(void) { return ZSTD_estimateDStreamSize((size_t)8 << 20) + (64u << 10); }
+int ref_zstd_uncompress(void* ws, const uint8_t* src, size_t n, uint8_t* dst, size_t cap, size_t* out_len) {
+    const size_t ws_size = ZSTD_estimateDStreamSize((size_t)8 << 20);
     *out_len = 0;
-    if (!ws) {
-        ws_size = ZSTD_estimateDStreamSize((size_t)8 << 20);
-        ws = malloc(ws_size + (64u << 10));
-    }
     uint8_t* obuf = (uint8_t*)ws + ws_size;
     ZSTD_DCtx* d = ZSTD_initStaticDCtx(ws, ws_size);
     if (!d) return -1;
@@ -325,7 +322,8 @@ int ref_zstd_uncompress(const uint8_t* src, size_t n, uint8_t* dst, size_t cap, 
 typedef struct {
     const uint8_t* seg;
     const uint64_t* pos;
-    uint64_t n, first, stride;
+    uint64_t n;
+    uint64_t* next;  /* shared claim cursor over pos (largest batches first) */
     uint64_t stored, decoded, ok;
 } dec_task;
 
@@ -333,7 +331,10 @@ static void* dec_worker(void* arg) {
     dec_task* t = (dec_task*)arg;
     size_t cap = 4u << 20;
     uint8_t* buf = (uint8_t*)malloc(cap);
-    for (uint64_t i = t->first; i < t->n; i += t->stride) {
+    void* zws = malloc(ref_zstd_workspace());
+    for (;;) {
+        const uint64_t i = __atomic_fetch_add(t->next, 1, __ATOMIC_RELAXED);
+        if (i >= t->n) break;
         const uint8_t* h = t->seg + t->pos[i];
         int32_t size;
         memcpy(&size, h + 4, 4);
@@ -350,7 +351,7 @@ static void* dec_worker(void* arg) {
         if (codec == 3) rc = ref_lz4f_uncompress(h + 61, n, buf, cap, &out);
         else if (codec == 2) rc = ref_snappy_java(h + 61, n, buf, cap, &out);
         else if (codec == 1) rc = ref_gzip_uncompress(h + 61, n, buf, cap, &out);
-        else if (codec == 4) rc = ref_zstd_uncompress(h + 61, n, buf, cap, &out);
+        else if (codec == 4) rc = ref_zstd_uncompress(zws, h + 61, n, buf, cap, &out);
         else if (codec == 0) { rc = 0; out = 0; }
         if (rc == 0 && codec) {
             be[1] &= (uint8_t)~7u; /* codec bits cleared */
@@ -359,8 +360,17 @@ static void* dec_worker(void* arg) {
         }
         t->ok += (c != stored_crc) ? 1u : 0u; /* keeps both CRCs live */
     }
+    free(zws);
     free(buf);
     return NULL;
+}
+
+static const uint8_t* g_sort_seg;
+static int by_size_desc(const void* a, const void* b) {
+    int32_t sa, sb;
+    memcpy(&sa, g_sort_seg + *(const uint64_t*)a + 4, 4);
+    memcpy(&sb, g_sort_seg + *(const uint64_t*)b + 4, 4);
+    return sa < sb ? 1 : sa > sb ? -1 : 0;
 }
 
 /* pos[n]: file positions of the batches to process (all complete, in one
@@ -370,14 +380,20 @@ double ref_baseline_decode(const uint8_t* seg, const uint64_t* pos, uint64_t n, 
     if (threads < 1) threads = 1;
     dec_task* t = (dec_task*)calloc((size_t)threads, sizeof(dec_task));
     pthread_t* th = (pthread_t*)calloc((size_t)threads, sizeof(pthread_t));
+    /* largest batches first, claimed dynamically: a 1 MiB gzip batch takes
+     * milliseconds and would otherwise set the tail */
+    uint64_t* order = (uint64_t*)malloc((size_t)(n ? n : 1) * sizeof(uint64_t));
+    memcpy(order, pos, (size_t)n * sizeof(uint64_t));
+    g_sort_seg = seg;
+    qsort(order, (size_t)n, sizeof(uint64_t), by_size_desc);
+    uint64_t next = 0;
     struct timespec t0, t1;
     clock_gettime(CLOCK_MONOTONIC, &t0);
     for (int i = 0; i < threads; i++) {
         t[i].seg = seg;
-        t[i].pos = pos;
+        t[i].pos = order;
         t[i].n = n;
-        t[i].first = (uint64_t)i;
-        t[i].stride = (uint64_t)threads;
+        t[i].next = &next;
         pthread_create(&th[i], NULL, dec_worker, &t[i]);
     }
     uint64_t s = 0, d = 0;
@@ -387,6 +403,7 @@ double ref_baseline_decode(const uint8_t* seg, const uint64_t* pos, uint64_t n, 
         d += t[i].decoded;
     }
     clock_gettime(CLOCK_MONOTONIC, &t1);
+    free(order);
     free(t);
     free(th);
     *stored = s;
