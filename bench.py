@@ -11,13 +11,19 @@ checkpoint, validity bitmap.  With --gpus N (torchrun, one rank per GPU)
 partitions are sharded p -> p % N and the only collective is the final RCCL
 gather of bitmaps + segment summaries to rank 0 (weak scaling).
 
-At N = 1 two more stanzas ride on the same JSON line (configs[2] and [4],
+At N = 1 three more stanzas ride on the same JSON line (configs[2] and [4],
 SURVEY.md §8(d)): `c2` (LZ4 frames, 64 KiB..1 MiB decoded batches, decode +
-CRC + parse) and `c5` (skewed 200 B..1 MiB, none/lz4/snappy-java/raw snappy,
-corruptions), each with its own decode-kernel roofline and a liblz4 /
-libsnappy CPU baseline.
+CRC + parse), `c5` (skewed 200 B..1 MiB, none/lz4/snappy-java/raw snappy,
+corruptions) and `c6` (C5 plus gzip / zstd), each with its own decode-stage
+roofline and a CPU baseline over the reference's codec libraries.
 
-Prints ONE JSON line on rank 0 (contract in the task statement).
+Prints ONE JSON line on rank 0 (contract in the task statement).  Only the
+headline's own timed region can cost that line: every stanza, baseline,
+index measurement and gather check reports its failure inside its own field.
+
+The device layer is `CudaPlatform` (torch-ROCm); tests/test_bench.py runs
+this file's whole control flow (every stanza, and the N > 1 gather with gloo
+at world size 2) on the CPU through a stand-in platform.
 """
 from __future__ import annotations
 
@@ -27,6 +33,7 @@ import os
 import sys
 import threading
 import time
+import traceback
 
 import numpy as np
 
@@ -40,15 +47,76 @@ PARTITIONS_PER_GPU = 8
 BATCH_BYTES = 16384
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 # C2: 8 partitions x 1.5 GiB of LZ4 segments (~16 GiB decoded per GPU);
-# C5: 128 partitions x 64 MiB (skewed batches, corruptions end chains early)
+# C5 / C6: 128 partitions x 64 MiB (skewed batches, corruptions end chains early)
 C2_PARTS, C2_SEG = 8, 3 << 29
 C5_PARTS, C5_SEG = 128, 64 << 20
-
+# C6's CPU sample: the first C6_CPU_PARTS partitions (1 MiB gzip / zstd
+# batches take the reference's loops milliseconds each)
+C6_CPU_PARTS = 8
+CPU_C1_SAMPLE = 1 << 30
 
 # index writes 48 B per record, result 64 B per batch
 IDX_BYTES_PER_RECORD = 48
 RESULT_BYTES_PER_BATCH = 64
 DECODE_KERNELS = ("k_decode", "k_decode_blocks", "k_lz_walk", "k_lz_exec", "k_decode_finish")
+MEMBER_KERNELS = ("k_members_first", "k_members", "k_inflate_copy")
+# segment-summary fields that do not depend on where a partition sits in a job
+SUMMARY_JOB_FIELDS = ("n_batches", "terminal_pos", "bytes_consumed", "terminal_errc", "terminal_eof",
+                      "has_checkpoint", "first_bad", "ckpt_last_offset", "ckpt_truncate_pos", "n_records")
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def failure(where, e):
+    """A stanza / leg that failed: logged in full, reported in its field."""
+    log(f"[{where}] failed: {e!r}\n{traceback.format_exc()}")
+    return {"error": repr(e)}
+
+
+class CudaPlatform:
+    """The device layer the bench drives: torch-ROCm on an MI355X, one rank
+    per GPU (LOCAL_RANK modulo the visible devices, so several ranks may
+    share one card for a rehearsal of the N > 1 path)."""
+
+    def __init__(self, local: int):
+        import torch
+        self.torch = torch
+        n = torch.cuda.device_count()
+        self.device = torch.device("cuda", local % max(n, 1))
+        torch.cuda.set_device(self.device)
+
+    def engine(self):
+        from redpanda_amd.engine import Engine
+        return Engine(self.device.index)
+
+    def sync(self):
+        self.torch.cuda.synchronize(self.device)
+
+    def empty_cache(self):
+        self.torch.cuda.empty_cache()
+
+    def comm_device(self, backend: str):
+        """Where collective tensors live: device memory for nccl (RCCL), the
+        host for gloo."""
+        return self.device if backend == "nccl" else self.torch.device("cpu")
+
+    def time_on_side_stream(self, first, again, reps: int):
+        """first(stream) once untimed, then `reps` x again(stream, prev)
+        between HIP events recorded on that stream: (ms per call, result)."""
+        torch = self.torch
+        st = torch.cuda.Stream(self.device)
+        self.sync()
+        with torch.cuda.stream(st):
+            res = first(st)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(st)
+            for _ in range(reps):
+                res = again(st, res)
+            e1.record(st)
+        st.synchronize()
+        return e0.elapsed_time(e1) / reps, res
 
 
 def profiled_traffic(fname, workload, kernels):
@@ -57,7 +125,8 @@ def profiled_traffic(fname, workload, kernels):
     and the per-kernel table (bytes, algorithmic bytes, ratio)."""
     path = os.path.join(ROOT, "profiles", fname)
     try:
-        tj = json.load(open(path)).get(workload)
+        with open(path) as f:
+            tj = json.load(f).get(workload)
     except Exception:
         return None, None
     if not tj:
@@ -73,15 +142,13 @@ def write_stats(args, name, d):
     if not args.stats_out:
         return
     try:
-        cur = json.load(open(args.stats_out))
+        with open(args.stats_out) as f:
+            cur = json.load(f)
     except Exception:
         cur = {}
     cur[name] = d
-    json.dump(cur, open(args.stats_out, "w"), indent=1)
-
-
-def log(*a):
-    print(*a, file=sys.stderr, flush=True)
+    with open(args.stats_out, "w") as f:
+        json.dump(cur, f, indent=1)
 
 
 def host_threads() -> int:
@@ -94,30 +161,36 @@ def host_threads() -> int:
 
 def gen_partitions(partitions, seg_bytes, kw, torch, device, threads=None):
     """Generate each partition's segment on the host (parallel, the GIL is
-    released inside librpgen) and copy it into one device buffer."""
+    released inside librpgen) and copy it into one device buffer.  Returns
+    (data, offsets, batch counts, partition 0's host copy)."""
     n = len(partitions)
     data = torch.empty(n * seg_bytes + 256, dtype=torch.uint8, device=device)
     counts = [0] * n
-    host_first = None
+    host_first = [None]
     lock = threading.Lock()
     sem = threading.Semaphore(threads or host_threads())
+    errors = []
 
     def work(i, p):
-        nonlocal host_first
-        with sem:
-            buf = np.empty(seg_bytes, dtype=np.uint8)
-            counts[i] = synth.gen_segment(buf, p, **kw)
-            with lock:
-                data[i * seg_bytes:(i + 1) * seg_bytes].copy_(torch.from_numpy(buf), non_blocking=False)
-                if i == 0:
-                    host_first = buf
+        try:
+            with sem:
+                buf = np.empty(seg_bytes, dtype=np.uint8)
+                counts[i] = synth.gen_segment(buf, p, **kw)
+                with lock:
+                    data[i * seg_bytes:(i + 1) * seg_bytes].copy_(torch.from_numpy(buf), non_blocking=False)
+                    if i == 0:
+                        host_first[0] = buf
+        except Exception as e:  # surfaced after the join
+            errors.append(e)
     ths = [threading.Thread(target=work, args=(i, p)) for i, p in enumerate(partitions)]
     for t in ths:
         t.start()
     for t in ths:
         t.join()
+    if errors:
+        raise errors[0]
     offs = np.arange(n + 1, dtype=np.uint64) * np.uint64(seg_bytes)
-    return data, offs, counts, host_first
+    return data, offs, counts, host_first[0]
 
 
 def cpu_baseline_c1(host_seg, seconds_budget=15.0):
@@ -125,9 +198,10 @@ def cpu_baseline_c1(host_seg, seconds_budget=15.0):
     this box's host cores over a bounded sample of the same workload."""
     from oracle import oracle as O
     cores = host_threads()
-    sample = host_seg[: 1 << 30]  # 1 GiB sample = 65,536 batches
+    sample = host_seg[:CPU_C1_SAMPLE]
     # split the sample into `cores` slices on batch boundaries (16 KiB grid)
-    per = (sample.size // BATCH_BYTES) // cores * BATCH_BYTES
+    per = max((sample.size // BATCH_BYTES) // cores, 1) * BATCH_BYTES
+    cores = max(1, min(cores, sample.size // per))
     offs = np.arange(cores + 1, dtype=np.uint64) * np.uint64(per)
     sample = np.ascontiguousarray(sample[: int(offs[-1])])
     one = np.ascontiguousarray(sample[:per])
@@ -138,9 +212,9 @@ def cpu_baseline_c1(host_seg, seconds_budget=15.0):
         total_b += b
         total_s += s
         reps += 1
-    one_core = b1 / s1 / 1e9
+    one_core = b1 / max(s1, 1e-9) / 1e9
     return {
-        "value": round(total_b / total_s / 1e9, 3),
+        "value": round(total_b / max(total_s, 1e-9) / 1e9, 3),
         "unit": "GB/s",
         "cores": cores,
         "kind": "port",
@@ -170,31 +244,31 @@ def cpu_baseline_decode(host_seg, positions, seconds_budget=12.0, gz_zstd=False)
         s, b, d = O.baseline_decode(host_seg, sub, 1)
         b1, d1, s1, r1 = b1 + b, d1 + d, s1 + s, r1 + 1
     return {
-        "value": round(tb / ts / 1e9, 3),
+        "value": round(tb / max(ts, 1e-9) / 1e9, 3),
         "unit": "GB/s (stored bytes)",
-        "decoded_GBs": round(td / ts / 1e9, 3),
+        "decoded_GBs": round(td / max(ts, 1e-9) / 1e9, 3),
         "cores": cores,
         "kind": "reference",
         "sample": f"{len(pos)} batches ({tb // max(reps, 1) >> 20} MiB stored) of partition 0"
-                  + ("-7" if gz_zstd else "") + ": stored crc + "
+                  + (f"-{C6_CPU_PARTS - 1}" if gz_zstd else "") + ": stored crc + "
                   f"liblz4 LZ4F_decompress / libsnappy RawUncompress (lz4_frame_compressor.cc:123-200 / "
                   f"snappy_java_compressor.cc:76-129 loops)"
                   + (" / zlib inflate twice (gzip_compressor.cc:161-230) / libzstd ZSTD_decompressStream "
                      "(stream_zstd.cc:152-178)" if gz_zstd else "")
                   + f" + decoded crc, {cores} threads x {reps} reps; record walk not included",
-        "one_core_GBs": round(b1 / s1 / 1e9, 3),
-        "one_core_decoded_GBs": round(d1 / s1 / 1e9, 3),
+        "one_core_GBs": round(b1 / max(s1, 1e-9) / 1e9, 3),
+        "one_core_decoded_GBs": round(d1 / max(s1, 1e-9) / 1e9, 3),
         "host_logical_cpus": os.cpu_count(),
     }
 
 
-def sized_outputs(eng, data, offs, flags, nseg, est_batches, torch, device):
+def sized_outputs(eng, plat, data, offs, flags, nseg, est_batches):
     """Outputs sized from the job's own totals (a probe run)."""
     nb, nrec, ndec = est_batches, est_batches * 8, int(offs[-1]) * 2
     for _ in range(4):
         out = eng.alloc_outputs(nseg, nb + 16, nrec + 16, ndec + 4096)
         eng.submit(data, offs, out, flags)
-        torch.cuda.synchronize(device)
+        plat.sync()
         t = out.totals_host()
         if int(t["overflow"]) == 0:
             return out
@@ -205,19 +279,20 @@ def sized_outputs(eng, data, offs, flags, nseg, est_batches, torch, device):
     raise RuntimeError("output sizing did not converge")
 
 
-def run_compressed(name, kw, n_parts, seg_bytes, args, torch, device, eng, abi, desc, extra_flags=0):
+def run_compressed(name, kw, n_parts, seg_bytes, args, plat, eng, abi, desc, extra_flags=0):
     """One compressed workload stanza (C2 / C5 / C6) on this GPU."""
+    torch, device = plat.torch, plat.device
     t0 = time.time()
     data, offs, counts, host_first = gen_partitions(list(range(n_parts)), seg_bytes, kw, torch, device)
     log(f"[{name}] generated {n_parts} x {seg_bytes >> 20} MiB ({sum(counts)} batches) in {time.time() - t0:.1f}s")
     flags = abi.JOB_CRC | abi.JOB_PARSE | abi.JOB_DECODE | extra_flags
     d_offs = torch.from_numpy(offs.view(np.int64)).to(device)
-    out = sized_outputs(eng, data, offs, flags, n_parts, int(offs[-1]) // 4096 + 4096, torch, device)
-    # C6's step is ~0.5 s (serial gzip / zstd members): fewer timed steps
-    steps = min(args.steps, 5) if name == "c6" else args.steps
+    out = sized_outputs(eng, plat, data, offs, flags, n_parts, int(offs[-1]) // 4096 + 4096)
+    # C6's step is ~0.3 s (serial gzip / zstd members): fewer timed steps
+    steps = max(1, min(args.steps, 5) if name == "c6" else args.steps)
     for _ in range(min(args.warmup, 1) if name == "c6" else args.warmup):
         eng.submit(data, offs, out, flags, d_seg_offsets=d_offs)
-    torch.cuda.synchronize(device)
+    plat.sync()
     h = out.to_host()
     b = h.batches
     f = b["flags"]
@@ -243,21 +318,26 @@ def run_compressed(name, kw, n_parts, seg_bytes, args, torch, device, eng, abi, 
     if name == "c2":
         parity["all_valid"] = bool(np.all(crc_ok) and np.all(dec_ok) and np.all(f & abi.F_PARSE_OK))
     positions = b["file_pos"][(b["segment"] == 0) & ((f & abi.F_COMPLETE) != 0)]
-    host_base = host_first
-    if name == "c6" and n_parts >= 8:
-        # C6's 1 MiB gzip / zstd batches take the reference's loops
-        # milliseconds each: one 64 MiB partition keeps only a few cores
-        # busy, so the CPU sample is the first 8 partitions
-        host_base = data[: int(offs[8])].cpu().numpy()
-        sel = (b["segment"] < 8) & ((f & abi.F_COMPLETE) != 0)
+    cpu_host = host_first
+    if name == "c6" and n_parts >= C6_CPU_PARTS:
+        cpu_host = data[: int(offs[C6_CPU_PARTS])].cpu().numpy()
+        sel = (b["segment"] < C6_CPU_PARTS) & ((f & abi.F_COMPLETE) != 0)
         positions = b["file_pos"][sel] + offs[b["segment"][sel].astype(np.int64)]
-    del h
+    per_codec = None
+    if name == "c6":
+        codec = b["attrs"] & 7
+        per_codec = {str(c): {"batches": int(np.sum(codec == c)), "codec_ok": int(np.sum(dec_ok & (codec == c))),
+                              "decoded_bytes": int(np.sum(b["decoded_len"].astype(np.int64)[dec_ok & (codec == c)]))}
+                     for c in (1, 2, 3, 4)}
+    n_batches = int(len(b))
+    stored_payload = int(np.sum(b["size_bytes"].astype(np.int64) - abi.HEADER_SIZE))
+    del h, b, f
     eng.set_timing(True)
-    torch.cuda.synchronize(device)
+    plat.sync()
     t1 = time.perf_counter()
     for _ in range(steps):
         eng.submit(data, offs, out, flags, d_seg_offsets=d_offs)
-    torch.cuda.synchronize(device)
+    plat.sync()
     el = (time.perf_counter() - t1) / steps
     tm = eng.last_timings()
     eng.set_timing(False)
@@ -269,32 +349,31 @@ def run_compressed(name, kw, n_parts, seg_bytes, args, torch, device, eng, abi, 
     # read once (compressed payloads, uncompressed payloads, headers) +
     # decoded bytes written once + the index (48 B per record, 64 B per
     # batch result); the CRC / walk of the decoded bytes is not counted again
-    whole_alg = stored + decoded + IDX_BYTES_PER_RECORD * n_rec + RESULT_BYTES_PER_BATCH * len(b)
-    traffic, kernels_traffic = profiled_traffic("decode_traffic.json", name, DECODE_KERNELS)
+    whole_alg = stored + decoded + IDX_BYTES_PER_RECORD * n_rec + RESULT_BYTES_PER_BATCH * n_batches
+    traffic, kernels_traffic = profiled_traffic("decode_traffic.json", name,
+                                                DECODE_KERNELS + (MEMBER_KERNELS if name == "c6" else ()))
     cpu = None
     if not args.no_cpu_baseline and len(positions):
         try:
-            cpu = cpu_baseline_decode(host_base, positions, gz_zstd=(name == "c6"))
+            cpu = cpu_baseline_decode(cpu_host, positions, gz_zstd=(name == "c6"))
         except Exception as e:  # a baseline failure must not cost the GPU measurement
-            log(f"[{name}] cpu baseline failed: {e!r}")
-            cpu = {"error": repr(e)}
-    write_stats(args, name, {"stored": stored, "stored_payload": int(np.sum(b["size_bytes"].astype(np.int64)
-                                                                          - abi.HEADER_SIZE)),
-                             "compressed_in": comp_in, "decoded": decoded, "batches": int(len(b)),
-                             "compressed_batches": int(np.sum(comp)), "records": n_rec})
+            cpu = failure(f"{name} cpu baseline", e)
+    write_stats(args, name, {"stored": stored, "stored_payload": stored_payload, "compressed_in": comp_in,
+                             "decoded": decoded, "batches": n_batches,
+                             "compressed_batches": parity["compressed"], "records": n_rec})
     st = {
         "workload": desc,
         "partitions": n_parts,
         "segment_bytes": seg_bytes,
         "stored_bytes": stored,
         "decoded_bytes": decoded,
-        "batches": int(len(b)),
+        "batches": n_batches,
         "records": n_rec,
         "ms_per_step": round(el * 1e3, 3),
         "steps": steps,
         "stored_GBps": round(stored / el / 1e9, 2),
         "decoded_GBps": round(decoded / el / 1e9, 2),
-        "batches_per_s": round(len(b) / el, 1),
+        "batches_per_s": round(n_batches / el, 1),
         "hbm_fraction_whole_pipeline": round(whole_alg / el / 1e9 / HBM_PEAK_GBS, 4),
         "whole_alg_bytes": whole_alg,
         "whole_alg_def": "stored + decoded + 48 B/record + 64 B/batch (SURVEY §8(d))",
@@ -315,35 +394,46 @@ def run_compressed(name, kw, n_parts, seg_bytes, args, torch, device, eng, abi, 
         "parity": parity,
         "cpu_baseline": cpu,
     }
-    if name == "c6":
-        codec = b["attrs"] & 7
-        st["per_codec"] = {str(c): {"batches": int(np.sum(codec == c)), "codec_ok": int(np.sum(dec_ok & (codec == c))),
-                                    "decoded_bytes": int(np.sum(b["decoded_len"].astype(np.int64)[dec_ok & (codec == c)]))}
-                           for c in (1, 2, 3, 4)}
+    if per_codec is not None:
+        st["per_codec"] = per_codec
         # gzip / zstd members decode in the member pass, which runs inside the
         # resolve_plan stage (it sizes their arena slots, as the reference's
-        # buffer_for_input does); one wave per member
-        gz_zs = sum(st["per_codec"][c]["decoded_bytes"] for c in ("1", "4"))
+        # buffer_for_input does)
+        gz_zs = sum(per_codec[c]["decoded_bytes"] for c in ("1", "4"))
+        rp = tm["resolve_plan"]
         st["member_pass"] = {"stage": "resolve_plan (k_members_first + k_inflate_copy; k_members for outgrown slots)",
-                             "ms": round(tm["resolve_plan"], 3), "decoded_bytes": gz_zs,
-                             "decoded_GBps": round(gz_zs / (tm["resolve_plan"] * 1e-3) / 1e9, 3)
-                             if tm["resolve_plan"] > 0 else None}
-    del out, data, d_offs, host_base
-    torch.cuda.empty_cache()
+                             "ms": round(rp, 3), "decoded_bytes": gz_zs,
+                             "decoded_GBps": round(gz_zs / (rp * 1e-3) / 1e9, 3) if rp > 0 else None}
+    del out, data, d_offs, cpu_host
+    plat.empty_cache()
     return st
 
 
-def run_compressed_safe(name, *a, **kw):
-    """The opt-in-turned-default C6 stanza: a failure there is reported in
-    its stanza instead of costing the headline line."""
+def run_stanza(name, *a, **kw):
+    """A compressed-workload stanza: a failure there is reported in its
+    stanza instead of costing the headline line."""
     try:
         return run_compressed(name, *a, **kw)
     except Exception as e:
-        log(f"[{name}] stanza failed: {e!r}")
-        return {"error": repr(e)}
+        return failure(name, e)
 
 
-def main():
+STANZAS = {
+    "c2": (lambda: synth.C2, lambda: (C2_PARTS, C2_SEG),
+           "C2: 8 partitions x 1.5 GiB disk segments of LZ4 frames (64 KiB blocks, content size; 10% linked, "
+           "10% content checksum), decoded batches uniform 64 KiB..1 MiB, payload thirds random / alnum / "
+           "JSON-like (seed 0xC2): discover + header_crc + crc + LZ4F decode + decoded crc/header_crc + record walk"),
+    "c6": (lambda: synth.C6, lambda: (C5_PARTS, C5_SEG),
+           "C6 (C5 + gzip / zstd): 128 partitions x 64 MiB, log-uniform 200 B..1 MiB batches, none 32 / gzip 10 / "
+           "lz4 24 / snappy-java 12 / raw snappy 12 / zstd 10, every codec decoded on the device, 1% payload + "
+           "0.2% header bit flips, 0.1% zeroed headers, truncated tails (seed 0xC6)"),
+    "c5": (lambda: synth.C5, lambda: (C5_PARTS, C5_SEG),
+           "C5: 128 partitions x 64 MiB, log-uniform 200 B..1 MiB batches, none 40 / lz4 30 / snappy-java 15 / "
+           "raw snappy 15, 1% payload + 0.2% header bit flips, 0.1% zeroed headers, truncated tails (seed 0xC5)"),
+}
+
+
+def parse_args(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
@@ -355,6 +445,12 @@ def main():
     ap.add_argument("--gather", choices=["bitmap", "index", "records"], default="bitmap",
                     help="what travels to rank 0 each step at N > 1: bitmaps + summaries (default), + batch results, "
                          "+ batch results and the per-record index")
+    ap.add_argument("--dist-backend", choices=["nccl", "gloo"], default="nccl",
+                    help="nccl (RCCL over xGMI, the product path); gloo stages the gather through host memory "
+                         "(a rehearsal of the N > 1 path, e.g. several ranks on one card)")
+    ap.add_argument("--check-gather", action="store_true",
+                    help="at N > 1, after the timed region: rank 0 runs ONE job over every partition and compares the "
+                         "gathered verdicts, bitmaps, batch results, record index and segment indexes with it")
     ap.add_argument("--no-parse", action="store_true", help="CRC only (diagnostic; not the headline workload)")
     ap.add_argument("--no-index", action="store_true", help="skip the segment-index rebuild measurement")
     ap.add_argument("--batch-bytes", type=int, default=BATCH_BYTES,
@@ -364,76 +460,120 @@ def main():
     ap.add_argument("--workloads", default="c1,c2,c5,c6",
                     help="c1 is the headline; c2/c5/c6 stanzas run at N = 1 only; a run without c1 is a diagnostic "
                          "(per-workload profiles)")
-    args = ap.parse_args()
-    workloads = set(args.workloads.split(","))
+    return ap.parse_args(argv)
 
-    import torch
+
+def main(argv=None, platform=None):
+    args = parse_args(argv)
+    workloads = [w for w in args.workloads.split(",") if w]
+
     import torch.distributed as dist
     from redpanda_amd import abi
-    from redpanda_amd.engine import Engine
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    plat = (platform or CudaPlatform)(local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    device = torch.device("cuda", local)
-    torch.cuda.set_device(device)
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=plat.device)
+        else:
+            dist.init_process_group("gloo")
+    try:
+        eng = plat.engine()
+        c1 = run_c1(args, plat, dist, eng, abi, world, rank) if "c1" in workloads else None
+        if c1 is None and world > 1:
+            raise SystemExit("--gpus N > 1 runs the headline workload (c1)")
 
-    eng = Engine(local)
-    c1 = run_c1(args, torch, dist, device, eng, abi, world, rank) if "c1" in workloads else None
-    if c1 is None and world > 1:
-        raise SystemExit("--gpus N > 1 runs the headline workload (c1)")
+        extra = {}
+        if world == 1:
+            for name in ("c2", "c6", "c5"):
+                if name in workloads:
+                    kw, size, desc = STANZAS[name]
+                    parts, seg = size()
+                    extra[name] = run_stanza(name, kw(), parts, seg, args, plat, eng, abi, desc)
 
-    extra = {}
-    if world == 1:
-        if "c2" in workloads:
-            extra["c2"] = run_compressed(
-                "c2", synth.C2, C2_PARTS, C2_SEG, args, torch, device, eng, abi,
-                "C2: 8 partitions x 1.5 GiB disk segments of LZ4 frames (64 KiB blocks, content size; 10% linked, "
-                "10% content checksum), decoded batches uniform 64 KiB..1 MiB, payload thirds random / alnum / "
-                "JSON-like (seed 0xC2): discover + header_crc + crc + LZ4F decode + decoded crc/header_crc + record walk")
-        if "c6" in workloads:
-            extra["c6"] = run_compressed_safe(
-                "c6", synth.C6, C5_PARTS, C5_SEG, args, torch, device, eng, abi,
-                "C6 (C5 + gzip / zstd): 128 partitions x 64 MiB, log-uniform 200 B..1 MiB batches, none 32 / gzip 10 / "
-                "lz4 24 / snappy-java 12 / raw snappy 12 / zstd 10, every codec decoded on the device, 1% payload + "
-                "0.2% header bit flips, 0.1% zeroed headers, truncated tails (seed 0xC6)")
-        if "c5" in workloads:
-            extra["c5"] = run_compressed(
-                "c5", synth.C5, C5_PARTS, C5_SEG, args, torch, device, eng, abi,
-                "C5: 128 partitions x 64 MiB, log-uniform 200 B..1 MiB batches, none 40 / lz4 30 / snappy-java 15 / "
-                "raw snappy 15, 1% payload + 0.2% header bit flips, 0.1% zeroed headers, truncated tails (seed 0xC5)")
-
-    if rank == 0:
-        line = {
-            "metric": "validated+decoded batch GB/s per GPU and whole node; % of HBM peak",
-            "value": c1["value"] if c1 else None,
-            "unit": "GB/s",
-            "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": c1["ms_per_step"] if c1 else None,
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": None,
-            "dtype": "u8",
-            "data": "synthetic (seeded mt19937_64, reference random_batch recipe), device-resident",
-            "config": {**(c1["config"] if c1 else {"workload": "diagnostic run without the headline (c1) workload"}),
-                       **extra},
-            "roofline": c1["roofline"] if c1 else None,
-            "cpu_baseline": c1["cpu_baseline"] if c1 else None,
-        }
-        print(json.dumps(line), flush=True)
-    if world > 1:
-        dist.destroy_process_group()
+        if rank == 0:
+            line = {
+                "metric": "validated+decoded batch GB/s per GPU and whole node; % of HBM peak",
+                "value": c1["value"] if c1 else None,
+                "unit": "GB/s",
+                "n_gpus": world,
+                "steps": args.steps,
+                "warmup": args.warmup,
+                "ms_per_step": c1["ms_per_step"] if c1 else None,
+                "higher_is_better": True,
+                "scaling": "weak",
+                "vs_baseline": None,
+                "dtype": "u8",
+                "data": "synthetic (seeded mt19937_64, reference random_batch recipe), device-resident",
+                "config": {**(c1["config"] if c1 else {"workload": "diagnostic run without the headline (c1) workload"}),
+                           **extra},
+                "roofline": c1["roofline"] if c1 else None,
+                "cpu_baseline": c1["cpu_baseline"] if c1 else None,
+            }
+            print(json.dumps(line), flush=True)
+    finally:
+        if world > 1:
+            dist.destroy_process_group()
 
 
-def run_c1(args, torch, dist, device, eng, abi, world, rank):
+def check_gather(args, plat, dist, eng, abi, out, index_res, parts, nb, n_records, world, rank, flags, seg_bytes):
+    """--check-gather: the gathered job at rank 0 against ONE single-process
+    job over every partition (global partition order) on rank 0's device.
+    Every rank takes part in the gathers; rank 0 returns the comparison."""
+    from redpanda_amd.shard import gather_job_verdicts, gather_records, gather_segment_index
+    v = gather_job_verdicts(out.summaries, out.bitmap, nb, parts, rank, world, dist)
+    g = gather_records(out.batches[: nb * abi.BATCH_RESULT.itemsize],
+                       out.records[: n_records * abi.RECORD_INDEX.itemsize], out.summaries, parts, rank, world, dist)
+    gi = gather_segment_index(*index_res, parts, rank, world, dist) if index_res is not None else None
+    if rank != 0:
+        return None
+    all_parts = list(range(args.partitions * world))
+    data, offs, counts, _ = gen_partitions(all_parts, seg_bytes, dict(synth.C1, batch_bytes=args.batch_bytes),
+                                           plat.torch, plat.device)
+    n_all = int(sum(counts))
+    ref = eng.alloc_outputs(len(all_parts), n_all + 16, n_all * 32 + 16, 1)
+    eng.submit(data, offs, ref, flags)
+    plat.sync()
+    r = ref.to_host()
+    res = {"partitions": len(all_parts)}
+    res["summaries"] = bool(all(np.array_equal(v["summaries"][fld], r.summaries[fld]) for fld in SUMMARY_JOB_FIELDS))
+    bits = np.unpackbits(r.bitmap.view(np.uint8), bitorder="little") if r.bitmap is not None else None
+    ok_bits = bits is not None
+    for key, got in v["bitmaps"].items():
+        if not ok_bits:
+            break
+        want = np.concatenate([bits[int(r.summaries["first_batch"][p]):
+                                    int(r.summaries["first_batch"][p]) + int(r.summaries["n_batches"][p])]
+                               for p in key])
+        ok_bits = np.array_equal(got, want)
+    res["bitmaps"] = bool(ok_bits)
+    gb, gr = g["batches"], g["records"]
+    res["batches"] = bool(len(gb) == len(r.batches) and all(
+        np.array_equal(gb[fld], r.batches[fld]) for fld in abi.BATCH_COMPARE_FIELDS if fld != "decoded_off"))
+    res["records"] = bool(len(gr) == len(r.records) and all(
+        np.array_equal(gr[fld], r.records[fld]) for fld in abi.RECORD_COMPARE_FIELDS))
+    res["n_batches"], res["n_records"] = int(len(gb)), int(len(gr))
+    if gi is not None:
+        ri = eng.index_to_host(*eng.segment_index(ref, [0] * len(all_parts)), n_segments=len(all_parts))
+        res["index"] = bool(sorted(gi) == all_parts and all(
+            all(int(gi[p][0][fld]) == int(ri[p][0][fld]) for fld in abi.INDEX_STATE.names if fld != "first_entry")
+            and all(np.array_equal(gi[p][k], ri[p][k]) for k in (1, 2, 3)) for p in all_parts))
+    res["consistent"] = bool(all(res[k] for k in ("summaries", "bitmaps", "batches", "records"))
+                             and res.get("index", True))
+    del ref, data, r
+    plat.empty_cache()
+    return res
+
+
+def run_c1(args, plat, dist, eng, abi, world, rank):
     """The headline workload (C1 per GPU; C3 across ranks): returns the
     fields of the JSON line it owns."""
     from redpanda_amd.shard import as_bytes, gather_bytes, gather_job_verdicts, gather_records, gather_sizes, \
         partitions_for_rank
+    torch, device = plat.torch, plat.device
+    comm = plat.comm_device(args.dist_backend)
     seg_bytes = int(args.seg_gib * (1 << 30)) // BATCH_BYTES * BATCH_BYTES
     parts = partitions_for_rank(args.partitions * world, world, rank)
     t0 = time.time()
@@ -453,14 +593,13 @@ def run_c1(args, torch, dist, device, eng, abi, world, rank):
     payload = [out.bitmap, out.summaries]
     if args.gather in ("index", "records"):
         payload.append(out.batches[: n_batches * abi.BATCH_RESULT.itemsize])
-    n_records_est = None
     if args.gather == "records":
         eng.submit(data, offs, out, flags, chunk, d_seg_offsets=d_offs)
-        torch.cuda.synchronize(device)
+        plat.sync()
         n_records_est = int(out.totals_host()["n_records"])
         payload.append(out.records[: n_records_est * abi.RECORD_INDEX.itemsize])
     # the gather's per-rank lengths are fixed for the run: negotiated once,
-    # outside the timed loop (no host sync per step)
+    # outside the timed loop (no host sync per step with nccl)
     sizes = [gather_sizes(as_bytes(t), world, dist) for t in payload] if world > 1 else None
 
     def step():
@@ -472,7 +611,7 @@ def run_c1(args, torch, dist, device, eng, abi, world, rank):
 
     for _ in range(args.warmup):
         step()
-    torch.cuda.synchronize(device)
+    plat.sync()
     # correctness of the measured workload (size-independent properties)
     h = out.to_host()
     nb = len(h.batches)
@@ -496,8 +635,10 @@ def run_c1(args, torch, dist, device, eng, abi, world, rank):
                 ok = bool(len(r) == int(np.sum(b["records_parsed"].astype(np.int64)))
                           and np.all(np.diff(b["index_base"].astype(np.int64)) >= 0)
                           and np.all(np.diff(r["batch"].astype(np.int64)) >= 0))
-                gathered = {"batches": int(len(b)), "records": int(len(r)), "consistent": ok,
-                            "bytes_per_step": int(sum(max(sz) * world for sz in sizes))}
+                gathered = {"batches": int(len(b)), "records": int(len(r)), "consistent": ok}
+        if rank == 0:
+            gathered = dict(gathered or {}, bytes_per_step=int(sum(max(sz) * world for sz in sizes)),
+                            backend=args.dist_backend)
     payload_bytes = int(np.sum(h.batches["size_bytes"].astype(np.int64) - abi.HEADER_SIZE))
     seg_total = int(np.sum(h.batches["size_bytes"].astype(np.int64)))
     del h
@@ -508,11 +649,11 @@ def run_c1(args, torch, dist, device, eng, abi, world, rank):
     eng.set_timing(True)
     if world > 1:
         dist.barrier()
-    torch.cuda.synchronize(device)
+    plat.sync()
     t1 = time.perf_counter()
     for _ in range(args.steps):
         step()
-    torch.cuda.synchronize(device)
+    plat.sync()
     if world > 1:
         dist.barrier()
     t2 = time.perf_counter()
@@ -520,10 +661,10 @@ def run_c1(args, torch, dist, device, eng, abi, world, rank):
     tm = eng.last_timings()
     elapsed = t2 - t1
     if world > 1:
-        tt = torch.tensor([elapsed], dtype=torch.float64, device=device)
+        tt = torch.tensor([elapsed], dtype=torch.float64, device=comm)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
-        tb = torch.tensor([seg_total, n_batches], dtype=torch.float64, device=device)
+        tb = torch.tensor([seg_total, n_batches], dtype=torch.float64, device=comm)
         dist.all_reduce(tb, op=dist.ReduceOp.SUM)
         job_bytes, job_batches = float(tb[0].item()), float(tb[1].item())
     else:
@@ -531,15 +672,18 @@ def run_c1(args, torch, dist, device, eng, abi, world, rank):
     ms_per_step = elapsed / args.steps * 1e3
     value = job_bytes * args.steps / elapsed / 1e9
 
+    # Everything below is after the headline's timed region: each leg
+    # reports a failure in its own field instead of costing the line.
+
     # roofline of the dominant kernel (k_validate: CRC32C of every stored
     # payload): algorithmic bytes per launch = payload read once + 128 B per
     # batch result (descriptor read + verdict written, counted once).  The
-    # record walk runs in k_walk (index writes: 64 B per record + the result
-    # struct), reported beside it.
+    # record walk runs in k_walk (index writes + the result struct), reported
+    # beside it.
     alg = payload_bytes + 128 * n_batches
     v_ms = tm["validate"]
-    achieved = alg / (v_ms * 1e-3) / 1e9
-    walk_alg = 64 * n_records + 128 * n_batches
+    achieved = alg / (v_ms * 1e-3) / 1e9 if v_ms > 0 else None
+    walk_alg = abi.RECORD_INDEX.itemsize * n_records + 128 * n_batches
     w_ms = tm.get("walk", 0.0)
     # SURVEY §8(d) C1 bytes per unit: segment bytes read once + 48 B per
     # record + 64 B per batch
@@ -550,44 +694,50 @@ def run_c1(args, torch, dist, device, eng, abi, world, rank):
     # segment sparse-index rebuild (segment_index::maybe_track over the
     # recovered batches, §8(f) row 2): timed separately on its own stream,
     # after the headline region; not part of `value`
-    index = None
+    index, index_res = None, None
     if not args.no_index:
-        st = torch.cuda.Stream(device)
-        bases = [0] * len(parts)
-        torch.cuda.synchronize(device)
-        with torch.cuda.stream(st):
-            res = eng.segment_index(out, bases, stream=st)
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            reps = 5
-            e0.record(st)
-            for _ in range(reps):
-                res = eng.segment_index(out, bases, stream=st, outputs=res)
-            e1.record(st)
-        st.synchronize()
-        ix = eng.index_to_host(*res, n_segments=len(parts))
-        n_entries = int(sum(int(r[0]["n_entries"]) for r in ix))
-        gidx = None
-        if world > 1:
-            # the job's indexes at rank 0 (RCCL gather of the used entries only)
-            from redpanda_amd.shard import gather_segment_index
-            g = gather_segment_index(*res, parts, rank, world, dist)
-            if rank == 0:
-                gidx = {"partitions": len(g), "entries": int(sum(int(v[0]["n_entries"]) for v in g.values()))}
-        index = {"kernel": "k_idx_cut+k_idx_cand+k_idx_resolve+k_idx_emit", "ms": round(e0.elapsed_time(e1) / reps, 4),
-                 "step": abi.INDEX_DEFAULT_STEP, "entries": n_entries,
-                 "tracked": int(sum(int(r[0]["tracked"]) for r in ix)), "gathered_at_rank0": gidx,
-                 "note": "piece-parallel (1024-batch pieces, candidate first entries, serial resolve); "
-                         "outputs preallocated, timed region = the four kernels + workspace memset"}
-        del ix, res
+        try:
+            bases = [0] * len(parts)
+            ms, index_res = plat.time_on_side_stream(
+                lambda st: eng.segment_index(out, bases, stream=st),
+                lambda st, prev: eng.segment_index(out, bases, stream=st, outputs=prev), 5)
+            ix = eng.index_to_host(*index_res, n_segments=len(parts))
+            n_entries = int(sum(int(r[0]["n_entries"]) for r in ix))
+            gidx = None
+            if world > 1:
+                # the job's indexes at rank 0 (gather of the used entries only)
+                from redpanda_amd.shard import gather_segment_index
+                gi = gather_segment_index(*index_res, parts, rank, world, dist)
+                if rank == 0:
+                    gidx = {"partitions": len(gi), "entries": int(sum(int(v[0]["n_entries"]) for v in gi.values()))}
+            index = {"kernel": "k_idx_cut+k_idx_cand+k_idx_resolve+k_idx_emit", "ms": round(ms, 4),
+                     "step": abi.INDEX_DEFAULT_STEP, "entries": n_entries,
+                     "tracked": int(sum(int(r[0]["tracked"]) for r in ix)), "gathered_at_rank0": gidx,
+                     "note": "piece-parallel (1024-batch pieces, candidate first entries, serial resolve); "
+                             "outputs preallocated, timed region = the four kernels + workspace memset"}
+            del ix
+        except Exception as e:
+            index = failure("segment index", e)
+            if world > 1:
+                raise  # a rank that left the gather would hang the others
+
+    gcheck = None
+    if world > 1 and args.check_gather:
+        gcheck = check_gather(args, plat, dist, eng, abi, out, index_res, parts, nb, n_records, world, rank, flags,
+                              seg_bytes)
 
     cpu = None
     if rank == 0 and not args.no_cpu_baseline and host_first is not None:
-        cpu = cpu_baseline_c1(host_first)
+        try:
+            cpu = cpu_baseline_c1(host_first)
+        except Exception as e:
+            cpu = failure("c1 cpu baseline", e)
     # release the C1 job before the compressed workloads
-    del out, data, d_offs, host_base, payload
-    torch.cuda.empty_cache()
+    del out, data, d_offs, payload, index_res
+    plat.empty_cache()
     gather_desc = {"bitmap": "bitmaps+summaries", "index": "bitmaps+summaries+batch results",
                    "records": "bitmaps+summaries+batch results+record index"}[args.gather]
+    coll = "RCCL" if args.dist_backend == "nccl" else "gloo (host-staged)"
     return {
         "value": round(value, 2),
         "ms_per_step": round(ms_per_step, 4),
@@ -600,8 +750,9 @@ def run_c1(args, torch, dist, device, eng, abi, world, rank):
             "records_per_gpu": n_records,
             "batch_bytes": args.batch_bytes,
             "batches_per_s": round(job_batches * args.steps / elapsed, 1),
-            "parallelism": f"partition-sharded x{world}, RCCL gather of {gather_desc}",
+            "parallelism": f"partition-sharded x{world}, {coll} gather of {gather_desc}",
             "gathered_records": gathered,
+            "gather_check": gcheck,
             "parity": {"all_batches_valid": all_ok, "bitmap_all_ones": bm_ok},
             "stage_ms": {k: round(v, 4) for k, v in tm.items()},
             "hbm_fraction_whole_pipeline": round(value / world / HBM_PEAK_GBS, 4),
@@ -612,10 +763,10 @@ def run_c1(args, torch, dist, device, eng, abi, world, rank):
         "roofline": {
             "bound": "hbm",
             "kernel": "k_validate",
-            "achieved": round(achieved, 1),
+            "achieved": round(achieved, 1) if achieved else None,
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
-            "frac": round(achieved / HBM_PEAK_GBS, 4),
+            "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
             "traffic": traffic,
             "alg_bytes_per_launch": alg,
             "kernel_ms": round(v_ms, 4),

@@ -8,7 +8,9 @@ summaries (checkpoints) and validity bitmaps to rank 0, where a caller such
 as log recovery wants the whole job's picture.
 
 Everything here takes `dist` (torch.distributed) and works with the nccl
-(RCCL) backend on device tensors and with gloo on host tensors.
+(RCCL) backend on device tensors and with gloo on host tensors; under gloo a
+device payload is staged through host memory (gloo's gather has no device
+path), which lets several ranks rehearse the N > 1 path on one card.
 """
 from __future__ import annotations
 
@@ -24,12 +26,20 @@ def partitions_for_rank(n_partitions: int, world: int, rank: int) -> List[int]:
     return [p for p in range(n_partitions) if p % world == rank]
 
 
+def _comm(t, dist):
+    """`t` where the backend moves it: device tensors for nccl, host tensors
+    for gloo."""
+    if t.is_cuda and dist.get_backend() == "gloo":
+        return t.cpu()
+    return t
+
+
 def gather_sizes(t, world: int, dist) -> List[int]:
     """Every rank's length of `t` (one small all_gather and a host sync):
     negotiate once, then pass the result to gather_bytes for repeated gathers
     of same-shaped payloads."""
     import torch
-    n = torch.tensor([t.numel()], dtype=torch.int64, device=t.device)
+    n = _comm(torch.tensor([t.numel()], dtype=torch.int64, device=t.device), dist)
     sizes = [torch.zeros_like(n) for _ in range(world)]
     dist.all_gather(sizes, n)
     return [int(s.item()) for s in sizes]
@@ -44,6 +54,7 @@ def gather_bytes(t, rank: int, world: int, dist, dst: int = 0, sizes: Sequence[i
     if sizes is None:
         sizes = gather_sizes(t, world, dist)
     m = max(sizes) if sizes else 0
+    t = _comm(t, dist)
     buf = t
     if t.numel() < m:
         buf = torch.zeros(m, dtype=t.dtype, device=t.device)
