@@ -10,6 +10,7 @@ import os
 import shutil
 import subprocess
 import sys
+from concurrent.futures import ThreadPoolExecutor
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
@@ -65,26 +66,28 @@ def build(force: bool = False, verbose: bool = False, checked: bool = False, var
     hipcc = _hipcc()
     headers = [os.path.join(INC, "rpgpu.h"), os.path.join(CSRC, "rp_internal.h"), os.path.join(CSRC, "rp_device.h"),
                os.path.join(CSRC, "rp_zstd_core.h")]
-    objs = []
+    objs, cmds = [], []
     for src in HIP_SOURCES:
         s = os.path.join(CSRC, src)
         o = os.path.join(bdir, src + ".o")
         if force or _stale(o, [s] + headers):
-            cmd = [hipcc, f"--offload-arch={ARCH}", "-O3", "-fPIC", "-std=c++17", "-I", INC, "-I", CSRC,
-                   "-Wall", "-Wno-unused-function", "-Wno-unused-variable", "-Wno-unused-label"] + extra + ["-c", s, "-o", o]
-            if verbose:
-                print(" ".join(cmd))
-            _run(cmd)
+            cmds.append([hipcc, f"--offload-arch={ARCH}", "-O3", "-fPIC", "-std=c++17", "-I", INC, "-I", CSRC,
+                         "-Wall", "-Wno-unused-function", "-Wno-unused-variable", "-Wno-unused-label"] + extra
+                        + ["-c", s, "-o", o])
         objs.append(o)
     for src in CXX_SOURCES:
         s = os.path.join(CSRC, src)
         o = os.path.join(bdir, src + ".o")
         if force or _stale(o, [s] + headers):
-            cmd = ["g++", "-O2", "-fPIC", "-std=c++17", "-I", INC, "-Wall", "-c", s, "-o", o]
-            if verbose:
-                print(" ".join(cmd))
-            _run(cmd)
+            cmds.append(["g++", "-O2", "-fPIC", "-std=c++17", "-I", INC, "-Wall"] + extra + ["-c", s, "-o", o])
         objs.append(o)
+    if verbose:
+        for cmd in cmds:
+            print(" ".join(cmd))
+    # one compiler per source, in parallel (each hipcc is single-threaded)
+    jobs = max(1, min(len(cmds), int(os.environ.get("MAX_JOBS", "0") or 0) or (os.cpu_count() or 1), 8))
+    with ThreadPoolExecutor(jobs) as ex:
+        list(ex.map(_run, cmds))
     if force or _stale(out, objs):
         cmd = [hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", out] + objs + ["-ldl", "-lpthread"]
         if verbose:

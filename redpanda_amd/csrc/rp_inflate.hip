@@ -798,6 +798,20 @@ DEV InfOut inf_out(uint8_t* lds, const InfTabs* T, const InfWave& w, uint8_t* ds
     return o;
 }
 
+// a member's first-pass scratch slot: the size its trailer / frame header
+// claims (payload-controlled), capped by deflate's 1032:1 expansion limit, by
+// 64x the input (above that a member is decoded again by the second pass) and
+// by 1/8 of the pool, so one hostile trailer cannot starve the members
+// claimed after it
+DEV uint64_t scratch_guess(const DeviceJob& j, uint64_t claimed, uint64_t n) {
+    uint64_t g = claimed;
+    g = g < 1032ull * n + 64 ? g : 1032ull * n + 64;
+    const uint64_t ratio = 64ull * n > (64ull << 10) ? 64ull * n : (64ull << 10);
+    g = g < ratio ? g : ratio;
+    g = g < j.inf_scratch_bytes / 8 ? g : j.inf_scratch_bytes / 8;
+    return (g + 15) & ~15ull;
+}
+
 // first pass of gzip member i (batch b): decode into a scratch slot sized
 // from the ISIZE trailer, set the plan and the state
 DEV void gzip_first_item(const DeviceJob& j, uint8_t* lds, InfTabs* T, const InfWave& W, uint32_t i, uint32_t b,
@@ -813,8 +827,7 @@ DEV void gzip_first_item(const DeviceJob& j, uint8_t* lds, InfTabs* T, const Inf
         const uint64_t isize = in.n >= 4 ? (uint64_t)(inf_byte(in, in.n - 4) | (inf_byte(in, in.n - 3) << 8) |
                                                       (inf_byte(in, in.n - 2) << 16) | (inf_byte(in, in.n - 1) << 24))
                                          : 0;
-        const uint64_t bound = 1032ull * in.n + 64;  // deflate's expansion limit
-        const uint64_t guess = ((isize < bound ? isize : bound) + 15) & ~15ull;
+        const uint64_t guess = scratch_guess(j, isize, in.n);
         soff = uni64(atomicAdd((unsigned long long*)j.inf_scratch_used, lane() == 0 ? (unsigned long long)guess : 0ull));
         const uint64_t cap = soff + guess <= j.inf_scratch_bytes ? guess : 0;
         InfOut o = inf_out(lds, T, W, j.inf_scratch + soff, cap);
@@ -1180,7 +1193,7 @@ DEV void zstd_first_item(const DeviceJob& j, uint8_t* lds, uint32_t i, uint32_t 
     int rc = -1;  // compressor::uncompress throws on an empty payload (compression/compression.cc:34-55)
     bool again = true;
     if (in.n) {
-        const uint64_t guess = zs_guess(in);
+        const uint64_t guess = scratch_guess(j, zs_guess(in), in.n);
         soff = uni64(atomicAdd((unsigned long long*)j.inf_scratch_used, lane() == 0 ? (unsigned long long)guess : 0ull));
         const uint64_t cap = soff + guess <= j.inf_scratch_bytes ? guess : 0;
         ZDev e = zdev(in, lds, j.inf_scratch + soff, cap);

@@ -457,7 +457,13 @@ int grow_pool(rpgpu_ctx* c, void*& p, size_t& have, size_t want, hipStream_t s) 
         p = nullptr;
         have = 0;
     }
-    if (hipMalloc(&p, want) != hipSuccess) { p = nullptr; return fail(c, RPGPU_E_NOMEM, "gzip first-pass pool"); }
+    if (hipMalloc(&p, want) != hipSuccess) {
+        // not an error: without the pool every member is decoded by the
+        // second pass, straight into its arena slot
+        (void)hipGetLastError();
+        p = nullptr;
+        return RPGPU_OK;
+    }
     have = want;
     return RPGPU_OK;
 }
@@ -518,6 +524,10 @@ int host_codec_step(rpgpu_ctx* c, const DeviceJob& j, hipStream_t s) {
     std::vector<std::vector<uint8_t>> outs(n);
     const uint8_t* in = (const uint8_t*)c->hc_in_h.p;
     std::atomic<uint32_t> next{0};
+    std::atomic<bool> missing{false};
+    // RPGPU_HOST_CODEC_MISSING=1 (diagnostic build): act as if libzstd could
+    // not be loaded (tests the unsupported path)
+    static const bool force_missing = [] { const char* e = diag_env("RPGPU_HOST_CODEC_MISSING"); return e && *e == '1'; }();
     auto work = [&]() {
         for (uint32_t i; (i = next.fetch_add(1)) < n;) {
             HostItem& it = hit[i];
@@ -527,11 +537,13 @@ int host_codec_step(rpgpu_ctx* c, const DeviceJob& j, hipStream_t s) {
             std::vector<uint8_t>& o = outs[i];
             o.resize((size_t)it.n * 4 + 4096);
             size_t len = 0;
-            int rc = host_uncompress(kHostZstd, in + it.stage, it.n, o.data(), o.size(), &len);
+            int rc = force_missing ? kHostCodecMissing
+                                   : host_uncompress(kHostZstd, in + it.stage, it.n, o.data(), o.size(), &len);
             if (rc == kHostCodecOverflow) {
                 o.resize(len);
                 rc = host_uncompress(kHostZstd, in + it.stage, it.n, o.data(), o.size(), &len);
             }
+            if (rc == kHostCodecMissing) missing = true;
             if (rc == 0) {
                 it.status = 0;
                 it.out_len = len;
@@ -543,6 +555,9 @@ int host_codec_step(rpgpu_ctx* c, const DeviceJob& j, hipStream_t s) {
     for (uint32_t t = 1; t < nt; t++) pool.emplace_back(work);
     work();
     for (auto& t : pool) t.join();
+    // a payload libzstd never saw is not corrupt: the job is unsupported here
+    // (rpgpu_uncompress answers RPGPU_E_UNSUPPORTED the same way)
+    if (missing) return fail(c, RPGPU_E_UNSUPPORTED, "RPGPU_JOB_HOST_CODECS: libzstd not loadable");
     uint64_t out_total = 0;
     for (uint32_t i = 0; i < n; i++) {
         HostItem& it = hit[i];
@@ -712,11 +727,18 @@ int submit_body(rpgpu_ctx* c, const rpgpu_job* job, hipStream_t s, int stop, Pla
     j.inf_scratch = nullptr;
     j.inf_scratch_bytes = 0;
     j.inf_scratch_used = (uint64_t*)(j.counters + 24);  // zeroed with the counters
-    if (decode_job) {
-        const size_t want = std::min<size_t>(std::max<size_t>(2 * data_len, 256ull << 20), 2ull << 30);
+    // Only a job that writes decoded bytes uses it (a planning run only sizes
+    // members); failing to get it costs a second pass, never the job.
+    if (dec && stop == kRunAll) {
+        size_t want = std::min<size_t>(std::max<size_t>(2 * data_len, 256ull << 20), 2ull << 30);
+        // RPGPU_INF_POOL_KIB (diagnostic build): a small pool (exercises members
+        // that do not get a scratch slot)
+        if (const char* e = diag_env("RPGPU_INF_POOL_KIB")) want = std::max<size_t>(strtoull(e, nullptr, 10) << 10, 4096);
         if (int rc = grow_pool(c, c->gz_pool, c->gz_pool_bytes, want, s)) return rc;
-        j.inf_scratch = (uint8_t*)c->gz_pool;
-        j.inf_scratch_bytes = c->gz_pool_bytes;
+        if (c->gz_pool) {
+            j.inf_scratch = (uint8_t*)c->gz_pool;
+            j.inf_scratch_bytes = std::min<size_t>(c->gz_pool_bytes, want);
+        }
     }
     j.host_list = (uint32_t*)(ws + o_hlist);
     c->hc_n = 0;

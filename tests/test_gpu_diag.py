@@ -1,0 +1,29 @@
+"""GPU cases run on the diagnostic library variant in a child process
+(tests/diag_cases.py): the gzip / zstd first-pass pool exhausted by hostile
+ISIZE trailers, and RPGPU_JOB_HOST_CODECS without a loadable libzstd."""
+import os
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _run(case, **env):
+    lib = os.path.join(ROOT, "redpanda_amd", "librpgpu_diag.so")
+    assert os.path.exists(lib), "librpgpu_diag.so missing: __graft_entry__.build() builds it"
+    e = dict(os.environ, RPGPU_VARIANT="diag", **env)
+    r = subprocess.run([sys.executable, "-m", "tests.diag_cases", case], cwd=ROOT, env=e, capture_output=True,
+                       text=True, timeout=180)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    return r.stdout
+
+
+def test_member_pool_exhausted_hostile_isize():
+    assert "small_pool ok" in _run("small_pool", RPGPU_INF_POOL_KIB="64")
+
+
+def test_host_codec_missing_is_unsupported():
+    assert "host_codec_missing ok" in _run("host_codec_missing", RPGPU_HOST_CODEC_MISSING="1")
