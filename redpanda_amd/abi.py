@@ -100,6 +100,7 @@ assert JOB_TOTALS.itemsize == 72
 # bit-exactly against the oracle (reserved fields excluded)
 BATCH_COMPARE_FIELDS = [n for n in BATCH_RESULT.names if not n.startswith("reserved")]
 RECORD_COMPARE_FIELDS = [n for n in RECORD_INDEX.names if n != "pad"]
+SUMMARY_COMPARE_FIELDS = [n for n in SEGMENT_SUMMARY.names if n != "reserved"]
 
 
 def _record_slots(batches: np.ndarray, n_records: int):

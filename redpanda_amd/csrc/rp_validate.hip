@@ -1257,12 +1257,18 @@ __global__ __launch_bounds__(1024) void k_validate(DeviceJob j) {
             STAMP_ADD(1, tc - tb2);
             if (l == 0) {
                 R->crc_computed = crc;
-                R->flags = f;
+                // OR-ed: k_walk may be adding its parse bits to this word
+                // at the same time (it runs concurrently on the disk
+                // layout); the parse fields are written by whichever kernel
+                // walked the batch (k_emit zeroed them)
+                atomicOr(&R->flags, f);
                 R->index_base = d.ib;
                 R->decoded_off = d.doff;
-                R->records_parsed = parsed;
-                R->walk_end = wend;
-                R->parse_err = (uint8_t)perr;
+                if (walk) {
+                    R->records_parsed = parsed;
+                    R->walk_end = wend;
+                    R->parse_err = (uint8_t)perr;
+                }
                 // a decoded payload is finished by k_validate_decoded, which
                 // still needs the prefix contribution (so does k_crc_combine)
                 if (!(d.codec != 0 && (f & RPGPU_F_CODEC_OK)) && !split) R->reserved1 = 0;
@@ -1345,7 +1351,7 @@ __global__ __launch_bounds__(256) void k_crc_combine(DeviceJob j) {
     if (l == 0) {
         rpgpu_batch_result* R = &j.batches[b];
         R->crc_computed = crc;
-        if (crc == d.crc) R->flags = d.flags | RPGPU_F_CRC_OK;
+        if (crc == d.crc) atomicOr(&R->flags, RPGPU_F_CRC_OK);  // k_walk may be OR-ing its bits concurrently
         if (!(d.codec != 0 && (d.flags & RPGPU_F_CODEC_OK))) R->reserved1 = 0;
     }
 }

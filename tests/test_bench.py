@@ -297,3 +297,15 @@ def test_bench_world2_gloo_gather_check(rplib, tmp_path, gather):
     if gather == "records":
         assert c["gathered_records"]["consistent"]
     assert c["segment_index"]["gathered_at_rank0"]["partitions"] == 4
+
+
+def test_test_helpers_resolve_abi_names():
+    """Attribute reads of the abi module by the GPU tests and the smoke exist
+    (the -m gpu suite is the only other place that would notice)."""
+    import re
+    from redpanda_amd import abi
+    for rel in ["tests/test_gpu_parity.py", "tests/diag_cases.py", "tests/test_shard.py", "__graft_entry__.py",
+                "bench.py", "redpanda_amd/shard.py", "redpanda_amd/engine.py"]:
+        with open(os.path.join(ROOT, rel)) as f:
+            for name in set(re.findall(r"\babi\.([A-Za-z_][A-Za-z0-9_]*)", f.read())):
+                assert hasattr(abi, name), (rel, name)
