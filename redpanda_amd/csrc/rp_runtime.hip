@@ -193,13 +193,6 @@ struct rpgpu_ctx {
     // gzip / zstd first-pass output pool (k_members_first), grow-only
     void* gz_pool = nullptr;
     size_t gz_pool_bytes = 0;
-    // concurrent CRC / record walk (disk layout): k_validate and k_walk on two
-    // streams whose CU masks split the device (split_k eighths of the CUs
-    // walk), forked from and joined back into the job's stream
-    hipStream_t split_v = nullptr, split_w = nullptr;
-    uint32_t split_k = 0, split_vcus = 0, split_wcus = 0;
-    hipEvent_t ev_fork = nullptr, ev_vdone = nullptr, ev_wdone = nullptr;
-    std::vector<uint8_t> ev_conc;  // per timing set: validate and walk overlapped
 };
 
 namespace {
@@ -318,10 +311,6 @@ int rpgpu_destroy(rpgpu_ctx* c) {
         for (auto& e : set) hipEventDestroy(e);
     if (c->stream) hipStreamDestroy(c->stream);
     if (c->copy) { (void)hipStreamSynchronize(c->copy); (void)hipStreamDestroy(c->copy); }
-    for (hipStream_t q : {c->split_v, c->split_w})
-        if (q) { (void)hipStreamSynchronize(q); (void)hipStreamDestroy(q); }
-    for (hipEvent_t e : {c->ev_fork, c->ev_vdone, c->ev_wdone})
-        if (e) (void)hipEventDestroy(e);
     for (auto& h : c->hs) {
         (void)hipFree(h.d_data); (void)hipFree(h.d_offs); (void)hipFree(h.d_batches); (void)hipFree(h.d_records);
         (void)hipFree(h.d_decoded);
@@ -411,10 +400,7 @@ int rpgpu_last_timings(rpgpu_ctx* c, float* ms, int n) {
     for (size_t i = 0; i < c->ev_used; i++) {
         auto& e = c->ev_sets[i];
         HIPCHK(c, hipEventSynchronize(e[6]));
-        // an overlapped set recorded the walk's end on its own stream: the
-        // walk runs from the fork (3) to it (5)
-        const bool conc = i < c->ev_conc.size() && c->ev_conc[i];
-        const int pairs[6][2] = {{0, 6}, {0, 1}, {1, 2}, {3, 4}, {2, 3}, {conc ? 3 : 4, 5}};
+        const int pairs[6][2] = {{0, 6}, {0, 1}, {1, 2}, {3, 4}, {2, 3}, {4, 5}};
         for (int k = 0; k < 6; k++) {
             float t = 0;
             HIPCHK(c, hipEventElapsedTime(&t, e[pairs[k][0]], e[pairs[k][1]]));
@@ -461,40 +447,6 @@ int submit_impl(rpgpu_ctx* c, const rpgpu_job* job, void* stream, int stop, Plan
     const int rr = ws_release(c, s);
     return rc ? rc : rr;
 }
-
-// The CU-masked stream pair of the concurrent CRC / walk (k8 eighths of the
-// CUs walk).  CUs are picked by a hash of their index, so either placement
-// of logical CU ids over the 8 XCDs (round-robin or contiguous) gives every
-// XCD its share of both kernels.
-int split_streams(rpgpu_ctx* c, uint32_t k8) {
-    if (c->split_k == k8 && c->split_v) return RPGPU_OK;
-    for (hipStream_t* q : {&c->split_v, &c->split_w})
-        if (*q) {
-            HIPCHK(c, hipStreamSynchronize(*q));
-            HIPCHK(c, hipStreamDestroy(*q));
-            *q = nullptr;
-        }
-    const uint32_t n = c->cu_count, words = (n + 31) / 32;
-    std::vector<uint32_t> mv(words, 0u), mw(words, 0u);
-    uint32_t nv = 0, nw = 0;
-    for (uint32_t i = 0; i < n; i++) {
-        const bool walk = ((i ^ (i >> 3) ^ (i >> 6)) & 7u) < k8;
-        (walk ? mw : mv)[i / 32] |= 1u << (i % 32);
-        (walk ? nw : nv)++;
-    }
-    if (nv == 0 || nw == 0) return fail(c, RPGPU_E_INVALID, "concurrent walk: empty CU mask");
-    HIPCHK(c, hipExtStreamCreateWithCUMask(&c->split_v, words, mv.data()));
-    HIPCHK(c, hipExtStreamCreateWithCUMask(&c->split_w, words, mw.data()));
-    for (hipEvent_t* e : {&c->ev_fork, &c->ev_vdone, &c->ev_wdone})
-        if (!*e) HIPCHK(c, hipEventCreateWithFlags(e, hipEventDisableTiming));
-    c->split_k = k8;
-    c->split_vcus = nv;
-    c->split_wcus = nw;
-    return RPGPU_OK;
-}
-
-// Default share of the concurrent walk (eighths of the CUs; 0 = serial)
-constexpr uint32_t kWalkSplitEighths = 0;
 
 // grow-only device pool (drained before it is replaced)
 int grow_pool(rpgpu_ctx* c, void*& p, size_t& have, size_t want, hipStream_t s) {
@@ -819,8 +771,6 @@ int submit_body(rpgpu_ctx* c, const rpgpu_job* job, hipStream_t s, int stop, Pla
             for (auto& e : set) HIPCHK(c, hipEventCreate(&e));
             c->ev_sets.push_back(set);
         }
-        if (c->ev_conc.size() < c->ev_sets.size()) c->ev_conc.resize(c->ev_sets.size(), 0);
-        c->ev_conc[c->ev_used] = 0;
         ev = c->ev_sets[c->ev_used++].data();
         HIPCHK(c, hipEventRecord(ev[0], s));
     }
@@ -865,41 +815,11 @@ int submit_body(rpgpu_ctx* c, const rpgpu_job* job, hipStream_t s, int stop, Pla
     }
     // RPGPU_WALK_WGS (diagnostic build): k_walk's grid (workgroups per CU)
     static const uint32_t walk_wgs = [] { const char* e = diag_env("RPGPU_WALK_WGS"); return e ? (uint32_t)atoi(e) : 8u; }();
-    // RPGPU_WALK_SPLIT (diagnostic build): eighths of the CUs that run the
-    // lane record walk concurrently with the CRC (0: one after the other)
-    static const uint32_t split_k = [] {
-        const char* e = diag_env("RPGPU_WALK_SPLIT");
-        return e ? (uint32_t)atoi(e) : kWalkSplitEighths;
-    }();
-    // k_walk needs no CRC verdict on the disk layout (the wire layout walks
-    // crc-good batches only): there the two kernels overlap, the CRC stream
-    // (HBM-bound) on most CUs and the latency-bound walk on the rest
-    const bool conc = split_k > 0 && split_k < 8 && (job->flags & RPGPU_JOB_PARSE) && job->layout == RPGPU_LAYOUT_DISK;
-    if (conc) {
-        if (int rc = split_streams(c, split_k)) return rc;
-        hipStream_t v = c->split_v, w = c->split_w;
-        HIPCHK(c, hipEventRecord(c->ev_fork, s));
-        HIPCHK(c, hipStreamWaitEvent(v, c->ev_fork, 0));
-        HIPCHK(c, hipStreamWaitEvent(w, c->ev_fork, 0));
-        if (tm) {
-            c->ev_conc[c->ev_used - 1] = 1;
-            HIPCHK(c, hipEventRecord(ev[3], v));
-        }
-        STAGE("validate", launch_validate(j, v, c->split_vcus));
-        if (tm) HIPCHK(c, hipEventRecord(ev[4], v));
-        STAGE("walk", launch_walk(j, w, c->split_wcus * walk_wgs));
-        if (tm) HIPCHK(c, hipEventRecord(ev[5], w));
-        HIPCHK(c, hipEventRecord(c->ev_vdone, v));
-        HIPCHK(c, hipEventRecord(c->ev_wdone, w));
-        HIPCHK(c, hipStreamWaitEvent(s, c->ev_vdone, 0));
-        HIPCHK(c, hipStreamWaitEvent(s, c->ev_wdone, 0));
-    } else {
-        if (tm) HIPCHK(c, hipEventRecord(ev[3], s));
-        STAGE("validate", launch_validate(j, s, c->cu_count));
-        if (tm) HIPCHK(c, hipEventRecord(ev[4], s));
-        STAGE("walk", launch_walk(j, s, c->cu_count * walk_wgs));
-        if (tm) HIPCHK(c, hipEventRecord(ev[5], s));
-    }
+    if (tm) HIPCHK(c, hipEventRecord(ev[3], s));
+    STAGE("validate", launch_validate(j, s, c->cu_count));
+    if (tm) HIPCHK(c, hipEventRecord(ev[4], s));
+    STAGE("walk", launch_walk(j, s, c->cu_count * walk_wgs));
+    if (tm) HIPCHK(c, hipEventRecord(ev[5], s));
     STAGE("finalize", launch_finalize(j, s));
     if (tm) HIPCHK(c, hipEventRecord(ev[6], s));
 #undef STAGE

@@ -7,9 +7,11 @@ set -e
 cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
 TAG=${1:-r03}
+if [ -z "${NO_TRACE:-}" ]; then
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$TAG -o $TAG --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-index > gpurun_out/prof_$TAG.log 2>&1
 echo "trace ok"
-for W in c1 c2 c5; do
+fi
+for W in ${WORKLOADS:-c1 c2 c5 c6}; do
 timeout -s KILL 240 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_fetch_${TAG}_$W -o f --output-format csv -- python3 bench.py --workloads $W --steps 2 --warmup 1 --no-cpu-baseline --no-index --stats-out gpurun_out/stats_${TAG}_$W.json > gpurun_out/pmc_fetch_${TAG}_$W.log 2>&1
 echo "fetch $W ok"
 timeout -s KILL 240 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc_write_${TAG}_$W -o w --output-format csv -- python3 bench.py --workloads $W --steps 2 --warmup 1 --no-cpu-baseline --no-index > gpurun_out/pmc_write_${TAG}_$W.log 2>&1

@@ -50,10 +50,10 @@ def alg_bytes(w, st):
         "k_validate": st["stored_payload"] + 128 * st["batches"],
         "k_lz_walk": st["compressed_in"],
         "k_lz_exec": st["decoded"],
-        "k_validate_decoded": st["decoded"] + 64 * st["records"],
+        "k_validate_decoded": st["decoded"] + 48 * st["records"],
     }
     if w == "c1":
-        a["k_walk"] = 64 * st["records"] + 128 * st["batches"]
+        a["k_walk"] = 48 * st["records"] + 128 * st["batches"]
     return a
 
 
@@ -86,11 +86,15 @@ def one(tag, w):
 
 def main():
     tag = sys.argv[1] if len(sys.argv) > 1 else "r03"
-    res = {w: one(tag, w) for w in ("c1", "c2", "c5")}
+    res = {w: one(tag, w) for w in ("c1", "c2", "c5", "c6")
+           if os.path.isdir(os.path.join(out, f"pmc_fetch_{tag}_{w}"))}
     for w, r in res.items():
         print(w, json.dumps({k: (v["bytes"], v.get("ratio")) for k, v in r["kernels"].items()}))
-    json.dump({"c1": res["c1"]}, open(os.path.join(prof, "validate_traffic.json"), "w"), indent=1)
-    json.dump({"c2": res["c2"], "c5": res["c5"]}, open(os.path.join(prof, "decode_traffic.json"), "w"), indent=1)
+    if "c1" in res:
+        json.dump({"c1": res["c1"]}, open(os.path.join(prof, "validate_traffic.json"), "w"), indent=1)
+    dec = {w: res[w] for w in ("c2", "c5", "c6") if w in res}
+    if dec:
+        json.dump(dec, open(os.path.join(prof, "decode_traffic.json"), "w"), indent=1)
     json.dump(res, open(os.path.join(prof, f"{tag}_traffic.json"), "w"), indent=1)
 
 
