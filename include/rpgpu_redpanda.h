@@ -31,6 +31,7 @@
 #define RPGPU_REDPANDA_H_
 
 #include <cstddef>
+#include <cstdio>
 #include <cstdint>
 #include <cstring>
 #include <memory>
@@ -527,22 +528,75 @@ inline segment_scan scan_segment(rpgpu::engine& e, const uint8_t* seg, size_t le
 }
 }  // namespace detail
 
-// storage/parser.h:94-136.  The input stream is one whole segment in host
-// memory (a file's bytes from position 0, as log_replayer reads it).
+// ss::input_stream<char> as the parser reads it: successive reads from
+// file position 0, 0 bytes at the end of the stream.
+class input_stream {
+public:
+    virtual ~input_stream() = default;
+    // up to n bytes into dst; 0 = end of stream
+    virtual size_t read(uint8_t* dst, size_t n) = 0;
+};
+
+// a file read from position 0 (log_replayer::recover opens the segment with
+// make_file_input_stream at 0, storage/log_replayer.cc:95-114)
+class file_input_stream final : public input_stream {
+public:
+    explicit file_input_stream(const char* path) : _f(std::fopen(path, "rb")) {
+        if (!_f) throw std::runtime_error(std::string("file_input_stream: cannot open ") + path);
+    }
+    ~file_input_stream() override {
+        if (_f) std::fclose(_f);
+    }
+    size_t read(uint8_t* dst, size_t n) override { return std::fread(dst, 1, n, _f); }
+
+private:
+    std::FILE* _f;
+};
+
+// bytes already in host memory, read in pieces of at most `piece`
+class memory_input_stream final : public input_stream {
+public:
+    memory_input_stream(const uint8_t* p, size_t n, size_t piece = SIZE_MAX) : _p(p), _n(n), _piece(piece) {}
+    size_t read(uint8_t* dst, size_t n) override {
+        const size_t k = std::min(std::min(n, _piece), _n - _at);
+        std::memcpy(dst, _p + _at, k);
+        _at += k;
+        return k;
+    }
+
+private:
+    const uint8_t* _p;
+    size_t _n, _piece, _at = 0;
+};
+
+// storage/parser.h:94-136.  Two inputs: a whole segment in host memory (a
+// file's bytes from position 0, as log_replayer reads it), or an
+// input_stream read ahead in windows (default 64 MiB).  A window is
+// validated on the GPU in one job; the chain's stop inside it is final
+// unless the window merely ended there (a short header or payload at its
+// end while the stream has more): then the bytes from that batch on are
+// kept, the window refilled and validated again from there, so the events
+// are exactly those of one job over the whole stream.  A batch larger than
+// the window doubles it.
 class continuous_batch_parser {
 public:
+    static constexpr size_t default_readahead = 64u << 20;
+
     continuous_batch_parser(std::unique_ptr<batch_consumer> consumer, const uint8_t* segment, size_t len,
                             rpgpu::engine& e = rpgpu::engine::local()) noexcept
-      : _consumer(std::move(consumer)), _seg(segment), _len(len), _e(e) {}
+      : _consumer(std::move(consumer)), _seg(segment), _win_len(len), _in_eof(true), _e(e) {}
+    continuous_batch_parser(std::unique_ptr<batch_consumer> consumer, std::unique_ptr<input_stream> in,
+                            size_t readahead = default_readahead, rpgpu::engine& e = rpgpu::engine::local())
+      : _consumer(std::move(consumer)), _in(std::move(in)), _readahead(std::max<size_t>(readahead, 64)), _e(e) {}
     continuous_batch_parser(const continuous_batch_parser&) = delete;
     continuous_batch_parser& operator=(const continuous_batch_parser&) = delete;
 
     // continuous_batch_parser::consume (storage/parser.cc:218-254) over the
-    // GPU's verdicts.  The segment is validated on the first call; later
-    // calls resume where the previous one stopped.
+    // GPU's verdicts.  The segment (or the stream's first window) is
+    // validated on the first call; later calls resume where the previous one
+    // stopped.
     parse_result consume() {
         if (_err != parser_errc::none) return {0, _err};
-        if (!_scan) _scan = detail::scan_segment(_e, _seg, _len);
         for (;;) {
             const step s = consume_one();
             if (_eof) break;
@@ -567,22 +621,64 @@ private:
         bool stop = false;
     };
 
+    // The verdict of the chain's next batch (nullptr: the chain ended, see
+    // _term): from the current window's scan, refilled as the stream goes.
+    const rpgpu_batch_result* next_batch() {
+        for (;;) {
+            if (_scan && _i < _scan->batches.size()) return &_scan->batches[_i];
+            if (_scan && _final) return nullptr;
+            scan_window();
+        }
+    }
+
+    // Validate the window from the chain's position (the first batch not yet
+    // delivered); read more of the stream first when there is one.
+    void scan_window() {
+        if (_in) {
+            const size_t keep = _scan ? _keep_from : 0;
+            if (keep) {
+                std::memmove(_buf.data(), _buf.data() + keep, _win_len - keep);
+                _win_len -= keep;
+                _win_base += keep;
+            }
+            if (_buf.size() < _readahead) _buf.resize(_readahead);
+            if (_scan && keep == 0 && _win_len == _buf.size()) _buf.resize(_buf.size() * 2);  // a batch > the window
+            while (_win_len < _buf.size() && !_in_eof) {
+                const size_t k = _in->read(_buf.data() + _win_len, _buf.size() - _win_len);
+                if (k == 0) _in_eof = true;
+                _win_len += k;
+            }
+            _seg = _buf.data();
+        }
+        _scan = detail::scan_segment(_e, _seg, _win_len);
+        _i = 0;
+        const rpgpu_segment_summary& s = _scan->summary;
+        // the window ended, not the stream: the chain resumes at the stop
+        _final = !(s.terminal_eof && !_in_eof);
+        if (!_final) {
+            _keep_from = (size_t)s.terminal_pos;
+            // an incomplete last batch (its payload runs past the window) is
+            // read again with the next window
+            while (!_scan->batches.empty() && !(_scan->batches.back().flags & RPGPU_F_COMPLETE))
+                _scan->batches.pop_back();
+        }
+    }
+
     // consume_one (storage/parser.cc:178-190) = consume_header + consume_records
     step consume_one() {
-        const detail::segment_scan& sc = *_scan;
         for (;;) {
             if (!_pending) {
                 // read_header_impl (storage/parser.cc:139-176): the chain's
                 // next header, or the verdict that ended the chain.  A read
                 // past the end of the data is an empty read: end_of_stream.
-                if (_i >= sc.batches.size()) {
+                if (!next_batch()) {
                     if (_eof) return {parser_errc::end_of_stream, false};
-                    if (sc.summary.terminal_eof) _eof = true;
-                    return {(parser_errc)sc.summary.terminal_errc, false};
+                    if (_scan->summary.terminal_eof) _eof = true;
+                    return {(parser_errc)_scan->summary.terminal_errc, false};
                 }
                 _pending = true;
             }
-            const rpgpu_batch_result& r = sc.batches[_i];
+            const rpgpu_batch_result& r = *next_batch();
             const model::record_batch_header h = model::record_batch_header::from(r);
             const bool complete = (r.flags & RPGPU_F_COMPLETE) != 0;
             const size_t size = (size_t)(int64_t)h.size_bytes;
@@ -612,7 +708,7 @@ private:
                 _eof = true;
                 out.err = parser_errc::input_stream_not_enough_bytes;
             } else {
-                const uint8_t* payload = _seg + r.file_pos + RPGPU_HEADER_SIZE;
+                const uint8_t* payload = _seg + r.file_pos + RPGPU_HEADER_SIZE;  // window-relative
                 _consumer->consume_records(
                   rpgpu::iobuf(payload, (uint32_t)(r.size_bytes - (int32_t)RPGPU_HEADER_SIZE)));
                 out.stop = _consumer->consume_batch_end();
@@ -629,11 +725,18 @@ private:
     }
 
     std::unique_ptr<batch_consumer> _consumer;
-    const uint8_t* _seg;
-    size_t _len;
+    const uint8_t* _seg = nullptr;  // the window's bytes (the whole segment without a stream)
+    std::unique_ptr<input_stream> _in;
+    std::vector<uint8_t> _buf;      // the stream's window
+    size_t _win_len = 0;            // valid bytes at _seg
+    size_t _win_base = 0;           // stream position of _seg[0]
+    size_t _readahead = 0;
+    size_t _keep_from = 0;          // window position the chain resumes at (not final)
+    bool _in_eof = false;           // the stream returned 0 bytes
+    bool _final = false;            // the window scan's terminal verdict ends the chain
     rpgpu::engine& _e;
     std::optional<detail::segment_scan> _scan;
-    size_t _i = 0;         // chain ordinal of the next (or pending) header
+    size_t _i = 0;         // window chain ordinal of the next (or pending) header
     bool _pending = false; // _header is set
     bool _eof = false;     // _input.eof()
     parser_errc _err = parser_errc::none;

@@ -5,6 +5,7 @@
 //
 //   surfaces_test cpu <segment>                 host walk: model:: crc helpers
 //   surfaces_test parse <segment> M R S E       continuous_batch_parser replay
+//   surfaces_test parse_stream <segment> M R S E W   ... over a file stream, W-byte windows
 //   surfaces_test recover <segment>             log_replayer checkpoint
 //   surfaces_test recover_bench <reps> <seg>... log_replayer::recover timing (host path)
 //   surfaces_test index <segment> <base> <q>... log_replayer recovery + segment_index rebuild,
@@ -184,6 +185,19 @@ int main(int argc, char** argv) {
               seg.data(), seg.size());
             // a stop ends one consume(); the caller resumes, as the
             // reference's readers do after a stop_parser
+            for (int call = 0; call < 3; call++) {
+                print_result(p.consume());
+            }
+            p.close();
+            return 0;
+        }
+        if (mode == "parse_stream" && argc == 8) {
+            // the same replay over a file input stream read ahead in windows
+            // of argv[7] bytes
+            storage::continuous_batch_parser p(
+              std::make_unique<scripted_consumer>(std::atoi(argv[3]), std::atoi(argv[4]), std::atoi(argv[5]),
+                                                  std::atoi(argv[6])),
+              std::make_unique<storage::file_input_stream>(argv[2]), (size_t)std::atoll(argv[7]));
             for (int call = 0; call < 3; call++) {
                 print_result(p.consume());
             }

@@ -225,6 +225,24 @@ def test_continuous_batch_parser_replay(driver, rplib, oracle, engine, tmp_path)
 
 
 @pytest.mark.gpu
+def test_continuous_batch_parser_stream(driver, rplib, oracle, engine, tmp_path):
+    """The parser over an input stream (storage/parser.h:94-136 takes an
+    ss::input_stream; log_replayer.cc:95-114 reads the file from position 0)
+    read ahead in windows from 64 bytes (smaller than any batch: the window
+    doubles) to larger than the segment: the events are the reference's."""
+    for name, data in segment_cases(rplib):
+        path = write(tmp_path, name, data)
+        golden = name.startswith("golden_")
+        for w in ((64,) if golden else (64, 1000, 20000, 1 << 20)):
+            for sc in SCRIPTS[: 1 if golden else 3]:
+                got = run(driver, "parse_stream", path, *sc, w)
+                ref = RefParser(data, *sc, crc=oracle.crc32c)
+                for _ in range(3):
+                    ref.consume()
+                assert got == ref.ev, (name, sc, w)
+
+
+@pytest.mark.gpu
 def test_log_replayer_checkpoint(driver, rplib, oracle, engine, tmp_path):
     for name, data in segment_cases(rplib):
         (line,) = run(driver, "recover", write(tmp_path, name, data))
