@@ -113,6 +113,20 @@ def build_surfaces_test(force: bool = False) -> str:
     return SURFACES_BIN
 
 
+ZSHOST_SRC = os.path.join(ROOT, "tests", "cpp", "zstd_core_host.cpp")
+ZSHOST_LIB = os.path.join(ROOT, "tests", "cpp", "_bin", "libzshost.so")
+
+
+def build_zstd_host(force: bool = False) -> str:
+    """rp_zstd_core.h built for the host (test infrastructure: the GPU tests
+    compare the device decoder with the same logic on the host)."""
+    hdr = os.path.join(CSRC, "rp_zstd_core.h")
+    if force or _stale(ZSHOST_LIB, [ZSHOST_SRC, hdr]):
+        os.makedirs(os.path.dirname(ZSHOST_LIB), exist_ok=True)
+        _run(["g++", "-O2", "-std=c++17", "-shared", "-fPIC", "-o", ZSHOST_LIB, ZSHOST_SRC])
+    return ZSHOST_LIB
+
+
 if __name__ == "__main__":
     v = "checked" if "--checked" in sys.argv else "stamps" if "--stamps" in sys.argv else \
         "diag" if "--diag" in sys.argv else ""

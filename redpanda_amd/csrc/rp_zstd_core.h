@@ -23,10 +23,15 @@
 //     FSE_readNCount, ZSTD_buildFSETable, the sequence bit stream with
 //     BIT_DStream_t's exact reload / overflow behaviour, repeat offsets,
 //     sequence execution checks (capacity, literal overrun, reach).
-// Known divergence (corrupt streams only): a frame in the ring-buffer mode
-// (no content size, or larger than its window + 128 KiB) whose match reaches
-// further back than the window reads the true history here, where libzstd
-// reads whatever its ring holds at that address.
+// One documented divergence (corrupt streams only), pinned as a reject rule:
+// in the ring-buffer mode (no content size, or larger than its window + 128
+// KiB) a match reaching past the window into the part of the previous ring
+// segment that the current segment (or the 32-byte overcopy of its copies)
+// has already overwritten reads those newer bytes in libzstd; here the
+// payload is rejected (block(): kRingDirty).  Sources further up the
+// previous segment still hold the true history in libzstd too, and decode
+// the same (tests/test_zstd_core.py::test_ring_mode_far_matches,
+// tests/test_gpu_parity.py::test_zstd_ring_mode_reject_rule).
 #pragma once
 #include <stdint.h>
 
@@ -74,6 +79,7 @@ constexpr uint64_t kOutRoom = 64u << 10;  // stream_zstd's ZSTD_outBuffer (strea
 // ZSTD_estimateDStreamSize(8 MiB) - sizeof(ZSTD_DCtx): in + out buffers of the static DCtx
 constexpr uint64_t kStaticBuffers = 131072ull + (8388608ull + 131072ull + 64ull);
 constexpr uint64_t kMaxWindow = (1ull << 27) + 1;  // ZSTD_MAXWINDOWSIZE_DEFAULT
+constexpr uint64_t kRingDirty = 32;                // WILDCOPY_OVERLENGTH: ZSTD_wildcopy's reach past a copy
 
 ZS_CONST uint32_t kLLBase[36] = {0,  1,  2,  3,  4,  5,  6,  7,  8,   9,   10,  11,   12,   13,   14,   15,   16,    18,
                                  20, 22, 24, 28, 32, 40, 48, 64, 128, 256, 512, 1024, 2048, 4096, 8192, 16384, 32768, 65536};
@@ -796,6 +802,15 @@ ZS_FN int64_t block(E& e, Tabs* T, Frame& F, uint64_t bp, uint64_t bn, uint64_t 
             bo += ll;
             F.fo += ll;
             if (off > F.fo - F.seg0 + F.prevlen) return -1;  // beyond the prefix and the previous segment
+            // ring-buffer mode: the previous segment (libzstd's extDict) sits
+            // at the start of the DCtx's buffer, where this segment's output
+            // (and the up-to-32-byte overcopy of its last copies) has been
+            // written over it; a source there reads those newer bytes in
+            // libzstd.  Rejected here (a documented divergence on corrupt
+            // streams only: a conforming encoder never reaches past its
+            // window); sources further up the previous segment are the true
+            // history, as here.
+            if (off > F.fo - F.seg0 && F.prevlen - (off - (F.fo - F.seg0)) < F.fo - F.seg0 + kRingDirty) return -1;
             ZS_PROF(1, e.match(off, ml));
             bo += ml;
             F.fo += ml;

@@ -711,3 +711,31 @@ def test_zstd_members_corpus(engine, oracle):
     ok = (got.batches["flags"] & abi.F_CODEC_OK) != 0
     assert int(np.sum(ok)) > len(good)
     assert_same(got, ref, DFLAGS)
+
+
+def test_zstd_ring_mode_reject_rule(engine, oracle):
+    """The documented zstd divergence pinned on the device (rp_zstd_core.h,
+    kRingDirty; tests/test_zstd_core.py pins it on the host): a ring-buffer
+    mode match into the part of the previous ring segment that the current
+    segment has overwritten reads newer bytes in libzstd; the device rejects
+    the payload, exactly where the host build of the same decoder does.  Every
+    other payload -- far matches into the untouched previous segment included
+    -- decodes to libzstd's bytes, flags and decoded crcs."""
+    import random
+    from redpanda_amd import build as B
+    from tests import zstd_corpus as ZC
+    from tests.test_zstd_core import load_host
+    host = load_host(B.build_zstd_host())
+    pay = [f for _, f in ZC.ring_frames(random.Random(7), 120)]
+    div = np.array([host(p) is None and ZC.ref_decode(p) is not None for p in pay])
+    assert int(np.sum(div)) >= 10 and int(np.sum(~div)) >= 10
+    got, ref = run_both(engine, oracle, [_zstd_batches(pay, counts=[1] * len(pay))], flags=DFLAGS)
+    gb, rb = got.batches, ref.batches
+    assert len(gb) == len(rb) == len(pay)
+    assert np.all((gb["flags"][div] & abi.F_CODEC_OK) == 0) and np.all((rb["flags"][div] & abi.F_CODEC_OK) != 0)
+    for f in ("flags", "crc_computed", "header_crc_computed", "decoded_len", "decoded_crc", "decoded_header_crc",
+              "records_parsed", "parse_err", "walk_end"):
+        np.testing.assert_array_equal(gb[f][~div], rb[f][~div], err_msg=f)
+    for i in np.nonzero(~div & ((rb["flags"] & abi.F_CODEC_OK) != 0))[0]:
+        go, ro, n = int(gb["decoded_off"][i]), int(rb["decoded_off"][i]), int(rb["decoded_len"][i])
+        assert bytes(got.decoded[go:go + n]) == bytes(ref.decoded[ro:ro + n]), i

@@ -133,3 +133,28 @@ def ref_decode(b: bytes, cap: int = 1 << 24):
     from redpanda_amd import abi
     rc, out = O.uncompress(abi.CODEC_ZSTD, b, cap)
     return out if rc == 0 else None
+
+
+def ring_frames(rng: random.Random, count: int):
+    """Frames decoded in libzstd's ring-buffer mode (no content size, a 1-2
+    KiB window patched into a frame encoded with a 128 KiB window, blocks of at
+    most 900 bytes) whose matches reach past the window: some stay inside the
+    DCtx's previous ring segment (libzstd's extDict), some land where the
+    current segment has already written over it.  [(data, frame)]"""
+    out = []
+    for _ in range(count):
+        base = bytes(rng.getrandbits(8) for _ in range(rng.choice([200, 600, 1500, 3000])))
+        parts = []
+        for _k in range(rng.randint(8, 40)):
+            s = rng.randrange(len(base))
+            parts.append(base[s:s + rng.randint(20, 400)])
+            if rng.random() < 0.3:
+                parts.append(bytes(rng.getrandbits(8) for _ in range(rng.randint(1, 30))))
+        data = b"".join(parts)
+        step = rng.choice([300, 500, 700, 900])
+        f = bytearray(frame(data, level=rng.choice([1, 3, 9]), content_size=0, wlog=17,
+                            flushes=list(range(step, len(data), step)), pledged=False))
+        assert f[4] & 0x20 == 0 and f[4] >> 6 == 0  # window descriptor at byte 5, no content size
+        f[5] = rng.choice([0x00, 0x08])  # W = 1 KiB / 2 KiB
+        out.append((data, bytes(f)))
+    return out
