@@ -66,8 +66,6 @@ struct ChunkRec {
 };
 
 // Per-segment resolve output.
-constexpr uint32_t kPosStale = 0xFFFFFFFFu;
-
 struct SegTerm {
     uint64_t pos;
     int32_t errc;
@@ -143,9 +141,6 @@ struct DeviceJob {
     ChunkRec* chunks;
     uint64_t* chunk_count;        // total_chunks (+1) : resolved counts -> exclusive scan in place
     uint64_t* chunk_entry;        // total_chunks : resolved entry position
-    uint32_t* chunk_pos;          // total_chunks * emit_slots: k_chain's batch positions (chunk-relative),
-                                  // kPosStale in slot 0 once k_resolve re-walked the chunk
-    uint32_t emit_slots;          // positions kept per chunk (k_emit runs a batch per thread up to this)
     SegTerm* seg_term;
     rpgpu_batch_result* batches;
     uint64_t batch_capacity;

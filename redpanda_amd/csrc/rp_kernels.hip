@@ -290,15 +290,12 @@ __global__ __launch_bounds__(256) void k_discover(DeviceJob j) {
 // Follow the chain from p while headers start before ce, one chain per lane
 // (wave_walk's semantics with lane_header).
 DEV WalkOut lane_walk(uint32_t layout, const uint8_t* __restrict__ seg, uint64_t len, uint64_t p, uint64_t ce,
-                      const uint32_t* __restrict__ th, uint32_t c57, uint32_t* pos, uint32_t npos, uint64_t cs) {
+                      const uint32_t* __restrict__ th, uint32_t c57) {
     WalkOut w;
     w.count = 0;
     w.term = -1;
     w.tpos = 0;
     while (p < ce) {
-        // the position of each batch the chunk's chain holds (k_emit's
-        // batch-parallel path), the first npos of them
-        if (w.count < npos) pos[w.count] = (uint32_t)(p - cs);
         const LHdr h = lane_header(layout, seg, len, p, th, c57);
         if (h.status >= 0) { w.term = h.status | (h.eof << 8); w.tpos = p; break; }
         if (len - p - RPGPU_HEADER_SIZE < h.need) {
@@ -345,8 +342,7 @@ __global__ __launch_bounds__(256) void k_chain(DeviceJob j) {
         r.tpos = 0;
         if (p < ce) {
             // p >= cs: the first chain position at or after the chunk start
-            const WalkOut o = lane_walk(j.layout, j.data + off, len, p, ce, th, j.tables->c57,
-                                        j.chunk_pos + (g + k) * j.emit_slots, j.emit_slots, cs);
+            const WalkOut o = lane_walk(j.layout, j.data + off, len, p, ce, th, j.tables->c57);
             r.entry = p;
             r.exit = o.exit;
             r.count = o.count;
@@ -468,7 +464,6 @@ __global__ __launch_bounds__(256) void k_resolve(DeviceJob j) {
                 ChunkRec nr;
                 nr.entry = entry; nr.exit = o.exit; nr.count = o.count; nr.term = o.term; nr.tpos = o.tpos;
                 j.chunks[c0 + wf] = nr;
-                j.chunk_pos[(c0 + wf) * j.emit_slots] = kPosStale;  // k_chain's positions are not this chain's
                 j.chunk_count[c0 + wf] = o.count;
                 j.chunk_entry[c0 + wf] = entry;
                 atomicAdd(&j.counters[0], 1u);
@@ -496,115 +491,13 @@ __global__ __launch_bounds__(256) void k_resolve(DeviceJob j) {
 }
 
 // ---------------------------------------------------------------------------
-// Emit: the decoded header (storage/parser.cc:36-76) of every batch on the
-// resolved chain, its planned index slots / decode bytes and work lists.
-// One thread per batch: chunk g's batch k sits where k_chain's walk put it
-// (chunk_pos), valid because k_resolve confirmed that walk; a chunk k_resolve
-// re-walked, or holding more batches than positions were kept, is walked
-// again by its slot-0 thread.  (One lane per chunk walking its 16 C1 batches
-// in a dependent chain ran at 4 waves per CU: 111 us per 16 GiB.)
+// Emit: walk each chunk again from its resolved entry; write the decoded
+// header (storage/parser.cc:36-76) and plan index slots / decode bytes.
 // ---------------------------------------------------------------------------
-DEV bool emit_batch(const DeviceJob& j, const uint8_t* seg, uint64_t len, uint64_t off, uint32_t s, uint64_t p,
-                    uint64_t ord, const uint32_t* th, uint32_t c57, uint64_t& next) {
-    const bool wire = j.layout == RPGPU_LAYOUT_WIRE;
-    const LHdr h = lane_header(j.layout, seg, len, p, th, c57);  // known valid (resolved chain)
-    const bool complete = (len - p - RPGPU_HEADER_SIZE) >= h.need;
-    // prefix state of the batch crc: raw CRC contribution of the BE40
-    // prefix (init ~0 is added by k_validate)
-    const uint32_t praw = lane_prefix_raw(j.layout, h.w, th);
-    const uint32_t attrs = wire ? lbe16(h.w, 21) : l16(h.w, 21);
-    const int32_t rc = (int32_t)(wire ? lbe32(h.w, 57) : l32(h.w, 57));
-    const uint32_t codec = attrs & 7;
-    uint64_t slots = 0, cap = 0;
-    const bool decodable = (codec == RPGPU_CODEC_LZ4 || codec == RPGPU_CODEC_SNAPPY) && (j.flags & RPGPU_JOB_DECODE);
-    if (complete) {
-        if (codec == 0) {
-            if ((j.flags & RPGPU_JOB_PARSE) && rc > 0 && (uint64_t)rc <= h.need) slots = (uint64_t)rc;
-        } else if (decodable) {
-            cap = decode_capacity_dev((int)codec, seg + p + RPGPU_HEADER_SIZE, h.need);
-            if ((j.flags & RPGPU_JOB_PARSE) && rc > 0 && (uint64_t)rc <= cap) slots = (uint64_t)rc;
-        }
-    }
-    if (ord < j.batch_capacity) {
-        rpgpu_batch_result r;
-        r.file_pos = p;
-        uint32_t f = RPGPU_F_HEADER_OK;
-        if (wire) {
-            // kafka_batch_adapter::read_header (kafka_batch_adapter.cc:32-91)
-            r.base_offset = (int64_t)lbe64(h.w, 0);
-            r.first_timestamp = (int64_t)lbe64(h.w, 27);
-            r.max_timestamp = (int64_t)lbe64(h.w, 35);
-            r.producer_id = (int64_t)lbe64(h.w, 43);
-            r.last_offset_delta = (int32_t)lbe32(h.w, 23);
-            r.base_sequence = (int32_t)lbe32(h.w, 53);
-            r.header_crc = 0;
-            r.crc = lbe32(h.w, 17);
-            r.producer_epoch = (int16_t)lbe16(h.w, 51);
-            r.type = 1;  // record_batch_type::raft_data
-            if (lb(h.w, 16) == 2) f |= RPGPU_F_WIRE_V2;
-        } else {
-            // storage::header_from_iobuf (storage/parser.cc:36-76)
-            r.base_offset = (int64_t)l64(h.w, 8);
-            r.first_timestamp = (int64_t)l64(h.w, 27);
-            r.max_timestamp = (int64_t)l64(h.w, 35);
-            r.producer_id = (int64_t)l64(h.w, 43);
-            r.last_offset_delta = (int32_t)l32(h.w, 23);
-            r.base_sequence = (int32_t)l32(h.w, 53);
-            r.header_crc = h.hcrc;
-            r.crc = l32(h.w, 17);
-            r.producer_epoch = (int16_t)l16(h.w, 51);
-            r.type = (int8_t)lb(h.w, 16);
-        }
-        r.size_bytes = h.size;
-        r.record_count = rc;
-        r.crc_computed = 0;
-        r.header_crc_computed = h.computed;
-        if (complete) f |= RPGPU_F_COMPLETE;
-        if (codec) f |= RPGPU_F_COMPRESSED;
-        if (codec >= 5) f |= RPGPU_F_CODEC_INVALID;
-        const bool host_codec = (j.flags & RPGPU_JOB_DECODE) && (j.flags & RPGPU_JOB_HOST_CODECS);
-        if (complete && codec == RPGPU_CODEC_ZSTD && !(j.flags & RPGPU_JOB_DECODE)) f |= RPGPU_F_CODEC_UNSUPPORTED;
-        r.flags = f;
-        r.segment = s;
-        // scratch for k_validate: absolute payload start (overwritten with
-        // the record-index base there)
-        r.index_base = off + p + RPGPU_HEADER_SIZE;
-        r.decoded_off = 0;
-        r.records_parsed = 0;
-        r.decoded_len = (complete && codec == 0) ? (uint32_t)h.need : 0;
-        r.decoded_crc = 0;
-        r.decoded_header_crc = 0;
-        r.attrs = (int16_t)attrs;
-        r.parse_err = 0;
-        r.reserved0 = 0;
-        // scratch for k_validate: raw CRC contribution of the BE prefix
-        r.reserved1 = praw;
-        r.walk_end = 0;
-        j.batches[ord] = r;
-        j.slots[ord] = slots;
-        j.dcap[ord] = cap;
-        // decode work list for k_decode (order is irrelevant: every item
-        // writes only its own batch and its own reserved arena slot)
-        if (complete && decodable) j.decode_list[atomicAdd(&j.counters[2], 1u)] = (uint32_t)ord;
-        // gzip and zstd members: sized by k_members_first (dcap /
-        // slots above are 0 until then)
-        if (complete && (j.flags & RPGPU_JOB_DECODE) &&
-            (codec == RPGPU_CODEC_GZIP || (codec == RPGPU_CODEC_ZSTD && !host_codec)))
-            j.inf_list[atomicAdd(&j.counters[16], 1u)] = (uint32_t)ord;
-        // zstd members with RPGPU_JOB_HOST_CODECS: decoded by the host step
-        if (complete && codec == RPGPU_CODEC_ZSTD && host_codec)
-            j.host_list[atomicAdd(&j.counters[19], 1u)] = (uint32_t)ord;
-    }
-    next = p + RPGPU_HEADER_SIZE + h.need;
-    return complete;
-}
-
 __global__ __launch_bounds__(256) void k_emit(DeviceJob j) {
     extern __shared__ uint32_t th[];
     init_lds_hdr(th, j.tables);
-    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const uint64_t g = t / j.emit_slots;
-    const uint32_t k = (uint32_t)(t - g * j.emit_slots);
+    const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (g >= j.total_chunks) return;
     const uint64_t base_ord = j.chunk_count[g];
     const uint64_t cnt = j.chunk_count[g + 1] - base_ord;
@@ -613,14 +506,7 @@ __global__ __launch_bounds__(256) void k_emit(DeviceJob j) {
     const uint64_t off = j.seg_off[s], len = j.seg_off[s + 1] - off;
     const uint8_t* seg = j.data + off;
     const uint32_t c57 = j.tables->c57;
-    const uint32_t* pos = j.chunk_pos + g * j.emit_slots;
-    uint64_t next;
-    if (cnt <= j.emit_slots && pos[0] != kPosStale) {
-        if (k < cnt)
-            emit_batch(j, seg, len, off, s, (g - j.chunk_base[s]) * j.chunk_bytes + pos[k], base_ord + k, th, c57, next);
-        return;
-    }
-    if (k != 0) return;
+    const bool wire = j.layout == RPGPU_LAYOUT_WIRE;
     uint64_t p = j.chunk_entry[g];
     for (uint64_t i = 0; i < cnt; i++) {
 #ifdef RPGPU_CHECKED
@@ -630,8 +516,97 @@ __global__ __launch_bounds__(256) void k_emit(DeviceJob j) {
             break;
         }
 #endif
-        if (!emit_batch(j, seg, len, off, s, p, base_ord + i, th, c57, next)) break;
-        p = next;
+        const LHdr h = lane_header(j.layout, seg, len, p, th, c57);  // known valid (resolved chain)
+        const uint64_t ord = base_ord + i;
+        const bool complete = (len - p - RPGPU_HEADER_SIZE) >= h.need;
+        // prefix state of the batch crc: raw CRC contribution of the BE40
+        // prefix (init ~0 is added by k_validate)
+        const uint32_t praw = lane_prefix_raw(j.layout, h.w, th);
+        const uint32_t attrs = wire ? lbe16(h.w, 21) : l16(h.w, 21);
+        const int32_t rc = (int32_t)(wire ? lbe32(h.w, 57) : l32(h.w, 57));
+        const uint32_t codec = attrs & 7;
+        uint64_t slots = 0, cap = 0;
+        const bool decodable = (codec == RPGPU_CODEC_LZ4 || codec == RPGPU_CODEC_SNAPPY) && (j.flags & RPGPU_JOB_DECODE);
+        if (complete) {
+            if (codec == 0) {
+                if ((j.flags & RPGPU_JOB_PARSE) && rc > 0 && (uint64_t)rc <= h.need) slots = (uint64_t)rc;
+            } else if (decodable) {
+                cap = decode_capacity_dev((int)codec, seg + p + RPGPU_HEADER_SIZE, h.need);
+                if ((j.flags & RPGPU_JOB_PARSE) && rc > 0 && (uint64_t)rc <= cap) slots = (uint64_t)rc;
+            }
+        }
+        if (ord < j.batch_capacity) {
+            rpgpu_batch_result r;
+            r.file_pos = p;
+            uint32_t f = RPGPU_F_HEADER_OK;
+            if (wire) {
+                // kafka_batch_adapter::read_header (kafka_batch_adapter.cc:32-91)
+                r.base_offset = (int64_t)lbe64(h.w, 0);
+                r.first_timestamp = (int64_t)lbe64(h.w, 27);
+                r.max_timestamp = (int64_t)lbe64(h.w, 35);
+                r.producer_id = (int64_t)lbe64(h.w, 43);
+                r.last_offset_delta = (int32_t)lbe32(h.w, 23);
+                r.base_sequence = (int32_t)lbe32(h.w, 53);
+                r.header_crc = 0;
+                r.crc = lbe32(h.w, 17);
+                r.producer_epoch = (int16_t)lbe16(h.w, 51);
+                r.type = 1;  // record_batch_type::raft_data
+                if (lb(h.w, 16) == 2) f |= RPGPU_F_WIRE_V2;
+            } else {
+                // storage::header_from_iobuf (storage/parser.cc:36-76)
+                r.base_offset = (int64_t)l64(h.w, 8);
+                r.first_timestamp = (int64_t)l64(h.w, 27);
+                r.max_timestamp = (int64_t)l64(h.w, 35);
+                r.producer_id = (int64_t)l64(h.w, 43);
+                r.last_offset_delta = (int32_t)l32(h.w, 23);
+                r.base_sequence = (int32_t)l32(h.w, 53);
+                r.header_crc = h.hcrc;
+                r.crc = l32(h.w, 17);
+                r.producer_epoch = (int16_t)l16(h.w, 51);
+                r.type = (int8_t)lb(h.w, 16);
+            }
+            r.size_bytes = h.size;
+            r.record_count = rc;
+            r.crc_computed = 0;
+            r.header_crc_computed = h.computed;
+            if (complete) f |= RPGPU_F_COMPLETE;
+            if (codec) f |= RPGPU_F_COMPRESSED;
+            if (codec >= 5) f |= RPGPU_F_CODEC_INVALID;
+            const bool host_codec = (j.flags & RPGPU_JOB_DECODE) && (j.flags & RPGPU_JOB_HOST_CODECS);
+            if (complete && codec == RPGPU_CODEC_ZSTD && !(j.flags & RPGPU_JOB_DECODE)) f |= RPGPU_F_CODEC_UNSUPPORTED;
+            r.flags = f;
+            r.segment = s;
+            // scratch for k_validate: absolute payload start (overwritten with
+            // the record-index base there)
+            r.index_base = off + p + RPGPU_HEADER_SIZE;
+            r.decoded_off = 0;
+            r.records_parsed = 0;
+            r.decoded_len = (complete && codec == 0) ? (uint32_t)h.need : 0;
+            r.decoded_crc = 0;
+            r.decoded_header_crc = 0;
+            r.attrs = (int16_t)attrs;
+            r.parse_err = 0;
+            r.reserved0 = 0;
+            // scratch for k_validate: raw CRC contribution of the BE prefix
+            r.reserved1 = praw;
+            r.walk_end = 0;
+            j.batches[ord] = r;
+            j.slots[ord] = slots;
+            j.dcap[ord] = cap;
+            // decode work list for k_decode (order is irrelevant: every item
+            // writes only its own batch and its own reserved arena slot)
+            if (complete && decodable) j.decode_list[atomicAdd(&j.counters[2], 1u)] = (uint32_t)ord;
+            // gzip and zstd members: sized by k_members_first (dcap /
+            // slots above are 0 until then)
+            if (complete && (j.flags & RPGPU_JOB_DECODE) &&
+                (codec == RPGPU_CODEC_GZIP || (codec == RPGPU_CODEC_ZSTD && !host_codec)))
+                j.inf_list[atomicAdd(&j.counters[16], 1u)] = (uint32_t)ord;
+            // zstd members with RPGPU_JOB_HOST_CODECS: decoded by the host step
+            if (complete && codec == RPGPU_CODEC_ZSTD && host_codec)
+                j.host_list[atomicAdd(&j.counters[19], 1u)] = (uint32_t)ord;
+        }
+        if (!complete) break;
+        p += RPGPU_HEADER_SIZE + h.need;
     }
 }
 
@@ -958,8 +933,7 @@ hipError_t launch_resolve(const DeviceJob& j, hipStream_t s) {
     return hipGetLastError();
 }
 hipError_t launch_emit(const DeviceJob& j, hipStream_t s) {
-    const uint64_t threads = (uint64_t)j.total_chunks * j.emit_slots;
-    hipLaunchKernelGGL(k_emit, dim3((uint32_t)((threads + 255) / 256)), dim3(256), kLdsHdrBytes, s, j);
+    hipLaunchKernelGGL(k_emit, dim3((j.total_chunks + 255) / 256), dim3(256), kLdsHdrBytes, s, j);
     return hipGetLastError();
 }
 hipError_t launch_finalize(const DeviceJob& j, hipStream_t s) {

@@ -605,9 +605,6 @@ int submit_body(rpgpu_ctx* c, const rpgpu_job* job, hipStream_t s, int stop, Pla
     const size_t o_chunks = take(tc * sizeof(ChunkRec));
     const size_t o_ccount = take((tc + 1) * 8);
     const size_t o_centry = take(tc * 8);
-    // k_chain's batch positions per chunk, for the batch-parallel k_emit
-    const uint32_t emit_slots = std::min<uint32_t>(32u, std::max<uint32_t>(4u, cs / 4096u));
-    const size_t o_cpos = take(tc * emit_slots * 4);
     const size_t o_segterm = take(nseg * sizeof(SegTerm));
     const size_t o_slots = take((bcap + 1) * 8);
     const size_t o_dcap = take((bcap + 1) * 8);
@@ -687,8 +684,6 @@ int submit_body(rpgpu_ctx* c, const rpgpu_job* job, hipStream_t s, int stop, Pla
     j.chunks = (ChunkRec*)(ws + o_chunks);
     j.chunk_count = (uint64_t*)(ws + o_ccount);
     j.chunk_entry = (uint64_t*)(ws + o_centry);
-    j.chunk_pos = (uint32_t*)(ws + o_cpos);
-    j.emit_slots = emit_slots;
     j.seg_term = (SegTerm*)(ws + o_segterm);
     j.batches = job->d_batches;
     j.batch_capacity = bcap;
