@@ -1563,187 +1563,6 @@ __global__ __launch_bounds__(256) void k_walk(DeviceJob j) {
 }
 
 // ---------------------------------------------------------------------------
-// k_walk_pair: the lane walk two records per memory round trip.  A step of
-// k_walk loads C_k (around record k's guessed end) and parses record k; its
-// next step cannot start before C_k arrives, because record k + 1's end is
-// only known from its length varint.  Here a step also guesses record
-// k + 1's end as if it were as long as record k (same-sized records: one
-// producer's payloads) and loads that region C_{k+1} in the same round trip,
-// so record k + 1 is parsed in the same step when the guess held; when it did
-// not, its parse reads the bytes it needs with its own loads (exactly as a
-// missed guess in k_walk), so the records are the same either way.
-// Three region slots per wave rotate (H, X, Y) -> (Y, H, X): a walking lane's
-// next head is always in Y (copied there from X when record k + 1 ended
-// inside X), so the cooperative loads stay wave-uniform.
-// ---------------------------------------------------------------------------
-#ifndef RPGPU_WALK_PAIR
-#define RPGPU_WALK_PAIR 0
-#endif
-constexpr uint32_t kWalkPairLdsWave = 3u * kSlotBytes;
-
-// record w.start's guessed end (its length varint in H) and the guess's span
-// (length varint + length); 0xFFFFFFFF when unknown
-DEV uint32_t lane_guess_end(const LaneWalk& w, const uint8_t* H, uint32_t& span) {
-    const uint32_t n = w.n, mis = w.mis, start = w.start;
-    span = 0;
-    if (start >= n) return 0xFFFFFFFFu;
-    const uint32_t o = start + mis - w.h_base, k = o & ~3u, sh = o & 3u;
-    const uint32_t w0 = region_dw(H, k), w1 = region_dw(H, k + 4u), w2 = region_dw(H, k + 8u), w3 = region_dw(H, k + 12u);
-    uint32_t br;
-    const int64_t len = varint12(__builtin_amdgcn_alignbyte(w1, w0, sh), __builtin_amdgcn_alignbyte(w2, w1, sh),
-                                 __builtin_amdgcn_alignbyte(w3, w2, sh), n - start, br);
-    if (len < 0 || (uint64_t)len > n) return 0xFFFFFFFFu;
-    span = br + (uint32_t)len;
-    return start + span;
-}
-
-// grid offset of the region around a guessed end (48 bytes each side), not
-// below `floor`
-DEV uint32_t region_around(const LaneWalk& w, uint32_t guess, uint32_t floor) {
-    const uint32_t e16 = (guess + w.mis + 15u) & ~15u;
-    return (guess != 0xFFFFFFFFu && e16 >= floor + kRegionBefore) ? e16 - kRegionBefore : floor;
-}
-
-// one record from w.start over the reader's regions (a = where its head is,
-// t = the region after it, h = scratch for a read both miss); commits it
-DEV bool lane_parse_one(LaneWalk& w, WalkResult& wr, const uint8_t* a, uint32_t a_base, const uint8_t* t, uint32_t t_base,
-                        uint8_t* h, rpgpu_record_index& e, rpgpu_record_index*& dst) {
-    const uint32_t start = w.start;
-    LdsReader c;
-    c.p0 = w.p0;
-    c.mis = w.mis;
-    c.n = w.n;
-    c.pos = start;
-    c.a = a;
-    c.t = t;
-    c.h = h;
-    c.a_base = a_base;
-    c.t_base = t_base;
-    const Rec r = parse_fields(c);
-    if (r.err) {
-        wr.parsed = w.done;
-        wr.err = r.err;
-        wr.trailing = 0;
-        wr.end = start;
-        return true;
-    }
-    dst = nullptr;
-    if (w.done < w.cap) {
-        e = index_entry(start, r);
-        dst = w.out + w.done;
-    }
-    w.done++;
-    w.start = r.end;
-    if (w.done >= w.total) {
-        wr.parsed = w.done;
-        wr.err = 0;
-        wr.trailing = w.n - w.start;
-        wr.end = w.start;
-        return true;
-    }
-    return false;
-}
-
-__global__ __launch_bounds__(256) void k_walk_pair(DeviceJob j) {
-    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-    enum : uint32_t { kIdle = 0, kHead = 1, kWalk = 2, kFin = 3 };
-    uint8_t* wave = lds + (threadIdx.x >> 6) * kWalkPairLdsWave;
-    const uint32_t l = lane_v();
-    const uint64_t nb_total = j.chunk_count[j.total_chunks];
-    const uint64_t nb = nb_total < j.batch_capacity ? nb_total : j.batch_capacity;
-    const bool wire = j.layout == RPGPU_LAYOUT_WIRE;
-    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-    const WalkCtx c = walk_ctx(j);
-    uint64_t b = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    uint32_t st = kIdle;
-    bool first = true, idx_ok = false;
-    LaneWalk w;
-    uint32_t hs = 0, xs = 1, ys = 2;  // slot roles this step
-    const uint32_t mine = region_lane(l);
-    for (;;) {
-        uint8_t* H = wave + hs * kSlotBytes + mine;
-        uint8_t* X = wave + xs * kSlotBytes + mine;
-        uint8_t* Y = wave + ys * kSlotBytes + mine;
-        if (st == kIdle) {
-            if (!first) b += stride;
-            first = false;
-            if (b >= nb) st = kFin;
-            else if (!(wire && !(j.batches[b].flags & RPGPU_F_CRC_OK)) && lane_walk_setup(c, b, w, idx_ok)) {
-                if (w.total == 0) {
-                    WalkResult wr;
-                    wr.parsed = 0; wr.err = 0; wr.trailing = w.n; wr.end = 0;
-                    lane_walk_finish(c, b, wr, idx_ok, wire);
-                } else st = kHead;
-            }
-        }
-        // regions: a walking lane's C_k -> X and C_{k+1} -> Y; a lane about
-        // to walk its head -> Y
-        uint32_t xb = 0, yb = 0, xr = 0, yr = 0;
-        if (st == kWalk) {
-            uint32_t span;
-            const uint32_t g1 = lane_guess_end(w, H, span);
-            xb = region_around(w, g1, w.h_base);
-            xr = region_rows(w.n, w.mis, xb);
-            if (w.done + 1 < w.total && g1 != 0xFFFFFFFFu && span) {
-                yb = region_around(w, g1 + span, xb);
-                yr = yb != xb ? region_rows(w.n, w.mis, yb) : 0u;
-            }
-        } else if (st == kHead) {
-            yb = w.h_base;
-            yr = region_rows(w.n, w.mis, yb);
-        }
-        if (__ballot(st != kFin) == 0) break;
-        coop_load(wave + xs * kSlotBytes, w.p0 - w.mis + xb, xr);
-        coop_load(wave + ys * kSlotBytes, w.p0 - w.mis + yb, yr);
-        wait_vm();
-        rpgpu_record_index e1, e2;
-        rpgpu_record_index *d1 = nullptr, *d2 = nullptr;
-        if (st == kWalk) {
-            WalkResult wr;
-            bool fin = lane_parse_one(w, wr, H, w.h_base, X, xb, H, e1, d1);
-            bool fresh = false;
-            if (!fin) {
-                const uint32_t g = w.start + w.mis;
-                if (g - xb <= kRegionReach) {
-                    // record k + 1's head is in X: parse it now (its end
-                    // region guessed into Y; a miss reads into H, spent)
-                    fin = lane_parse_one(w, wr, X, xb, yr ? Y : X, yr ? yb : xb, H, e2, d2);
-                    if (!fin) {
-                        const uint32_t g2 = w.start + w.mis;
-                        if (yr && g2 - yb <= kRegionReach) {
-                            w.h_base = yb;
-                        } else if (g2 - xb <= kRegionReach) {
-                            // record k + 1 ended inside X: its region moves
-                            // to Y, the next head slot
-#pragma unroll
-                            for (uint32_t r = 0; r < kRegionRows; r++)
-                                *(uint4*)(Y + region_off(16u * r)) = *(const uint4*)(X + region_off(16u * r));
-                            w.h_base = xb;
-                        } else {
-                            fresh = true;
-                        }
-                    }
-                } else {
-                    fresh = true;
-                }
-                if (!fin && fresh) w.h_base = (w.start + w.mis) & ~15u;
-            }
-            if (fin) {
-                lane_walk_finish(c, b, wr, idx_ok, wire);
-                st = kIdle;
-            } else if (fresh) st = kHead;
-        } else if (st == kHead) st = kWalk;
-        // H is spent: its slot stages the entries (two halves of 3 KiB)
-        coop_store(wave + hs * kSlotBytes, e1, d1);
-        coop_store(wave + hs * kSlotBytes + 3072u, e2, d2);
-        const uint32_t t = hs;
-        hs = ys;
-        ys = xs;
-        xs = t;
-    }
-}
-
-// ---------------------------------------------------------------------------
 // Write side: stamp the headers of batches about to be
 // written, one wave per batch (claimed one at a time):
 //   * RPGPU_STAMP_OFFSETS — disk_log_appender::operator() (storage/
@@ -1911,16 +1730,7 @@ hipError_t launch_to_wire(const uint8_t* disk, uint8_t* wire, const rpgpu_batch_
 }
 
 hipError_t launch_walk(const DeviceJob& j, hipStream_t s, uint32_t grid) {
-    if (!(j.flags & RPGPU_JOB_PARSE)) return hipSuccess;
-    if (RPGPU_WALK_PAIR) {
-        static bool attr = false;
-        if (!attr) {
-            (void)hipFuncSetAttribute((const void*)k_walk_pair, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                      4 * kWalkPairLdsWave);
-            attr = true;
-        }
-        hipLaunchKernelGGL(k_walk_pair, dim3(grid), dim3(256), 4 * kWalkPairLdsWave, s, j);  // 72 KiB: 2 per CU
-    } else
+    if (j.flags & RPGPU_JOB_PARSE)
         hipLaunchKernelGGL(k_walk, dim3(grid), dim3(256), 4 * kWalkLdsWave, s, j);  // 48 KiB: 3 per CU
     return hipGetLastError();
 }
