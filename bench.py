@@ -632,10 +632,9 @@ def run_c1(args, plat, dist, eng, abi, world, rank):
                                 world, dist)
             if rank == 0:
                 b, r = gr["batches"], gr["records"]
-                rb = abi.record_batches(b, len(r))
                 ok = bool(len(r) == int(np.sum(b["records_parsed"].astype(np.int64)))
                           and np.all(np.diff(b["index_base"].astype(np.int64)) >= 0)
-                          and np.all(rb >= 0) and np.all(np.diff(rb) >= 0))
+                          and np.all(np.diff(r["batch"].astype(np.int64)) >= 0))
                 gathered = {"batches": int(len(b)), "records": int(len(r)), "consistent": ok}
         if rank == 0:
             gathered = dict(gathered or {}, bytes_per_step=int(sum(max(sz) * world for sz in sizes)),

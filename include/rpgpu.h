@@ -136,19 +136,16 @@ typedef struct rpgpu_batch_result {
     int8_t type;
     uint8_t parse_err;            /* rpgpu_parse_err */
     uint16_t reserved0;
-    uint32_t reserved1;
-    uint32_t walk_end;            /* payload offset after the last parsed record (0: none parsed) */
+    uint64_t reserved1;
 } rpgpu_batch_result;
 
 /* One entry per parsed record (model/record_utils.cc:94-181).  Positions are
- * byte offsets inside the batch's (decoded) payload.  48 bytes.
- * Record k of a batch sits in slot index_base + k (k < records_parsed), so
- * its batch is the result whose slot range holds it; it ends where record
- * k + 1 starts (rec_pos), the last parsed record at the batch's walk_end. */
+ * byte offsets inside the batch's (decoded) payload.  64 bytes. */
 typedef struct rpgpu_record_index {
+    uint32_t batch;               /* job-wide batch ordinal */
     uint32_t rec_pos;             /* offset of the record's length varint */
-    int32_t length;               /* record::size_bytes (length varint, int32) */
     int64_t ts_delta;             /* timestamp_delta */
+    int32_t length;               /* record::size_bytes (length varint, int32) */
     int32_t offset_delta;         /* static_cast<int32_t>(offset delta varint) */
     int32_t key_len;              /* key_length as stored by model::record (int32) */
     uint32_t key_pos;             /* first key byte */
@@ -156,8 +153,10 @@ typedef struct rpgpu_record_index {
     uint32_t val_pos;
     int32_t hdr_count;            /* number of record headers */
     uint32_t hdr_pos;             /* first byte after the header-count varint */
+    uint32_t end_pos;             /* first byte after this record */
     int8_t attrs;                 /* record attributes byte */
     uint8_t pad[3];
+    uint32_t reserved[2];
 } rpgpu_record_index;
 
 /* Per segment: where and why the parser chain stopped, and the

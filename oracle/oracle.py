@@ -60,9 +60,8 @@ def lib():
         L.rpo_decode_capacity.restype = C.c_uint64
         L.rpo_decode_capacity.argtypes = [C.c_int, C.c_void_p, C.c_size_t]
         L.rpo_walk_records.restype = C.c_uint32
-        L.rpo_walk_records.argtypes = [C.c_void_p, C.c_size_t, C.c_int32, C.c_void_p,
-                                       C.c_uint64, C.POINTER(C.c_uint8), C.POINTER(C.c_uint64),
-                                       C.POINTER(C.c_uint32)]
+        L.rpo_walk_records.argtypes = [C.c_void_p, C.c_size_t, C.c_int32, C.c_uint32, C.c_void_p,
+                                       C.c_uint64, C.POINTER(C.c_uint8), C.POINTER(C.c_uint64)]
         L.rpo_run_job.restype = C.c_int
         L.rpo_run_job.argtypes = [C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32, C.c_void_p,
                                   C.c_uint64, C.c_void_p, C.c_uint64, C.c_void_p, C.c_uint64,
@@ -212,24 +211,16 @@ def decode_capacity(codec: int, data: bytes) -> int:
     return lib().rpo_decode_capacity(codec, src.ctypes.data_as(C.c_void_p), len(data))
 
 
-def walk_records(payload: bytes, record_count: int, cap: int = None):
-    """(records parsed, parse_err, trailing bytes, index entries); the walk's
-    end offset is walk_records_end()."""
-    n, perr, trailing, idx, _ = walk_records_end(payload, record_count, cap)
-    return n, perr, trailing, idx
-
-
-def walk_records_end(payload: bytes, record_count: int, cap: int = None):
+def walk_records(payload: bytes, record_count: int, batch: int = 0, cap: int = None):
     src = np.frombuffer(bytes(payload) + b"\0" * 16, dtype=np.uint8)
     if cap is None:
         cap = max(record_count, 0)
     idx = np.zeros(max(cap, 1), dtype=abi.RECORD_INDEX)
     perr = C.c_uint8(0)
     trailing = C.c_uint64(0)
-    wend = C.c_uint32(0)
-    n = lib().rpo_walk_records(src.ctypes.data_as(C.c_void_p), len(payload), record_count,
-                               idx.ctypes.data_as(C.c_void_p), cap, C.byref(perr), C.byref(trailing), C.byref(wend))
-    return n, perr.value, trailing.value, idx[: min(n, cap)], wend.value
+    n = lib().rpo_walk_records(src.ctypes.data_as(C.c_void_p), len(payload), record_count, batch,
+                               idx.ctypes.data_as(C.c_void_p), cap, C.byref(perr), C.byref(trailing))
+    return n, perr.value, trailing.value, idx[: min(n, cap)]
 
 
 class JobResult:

@@ -307,17 +307,17 @@ static int copy_bytes(walk_cur* c, int64_t len) {
 }
 
 uint32_t rpo_walk_records(const uint8_t* payload, size_t n, int32_t record_count,
-                          rpgpu_record_index* index, uint64_t index_cap, uint8_t* parse_err,
-                          uint64_t* trailing, uint32_t* walk_end) {
+                          uint32_t batch_ordinal, rpgpu_record_index* index,
+                          uint64_t index_cap, uint8_t* parse_err, uint64_t* trailing) {
     walk_cur c = {payload, n, 0};
     uint32_t parsed = 0;
     *parse_err = RPGPU_PARSE_ERR_NONE;
     *trailing = 0;
-    *walk_end = 0;
     /* model/record.h:619: for (auto i = 0; i < record_count; i++) */
     for (int32_t i = 0; i < record_count; i++) {
         rpgpu_record_index e;
         memset(&e, 0, sizeof e);
+        e.batch = batch_ordinal;
         e.rec_pos = (uint32_t)c.pos;
         /* parse_record_meta_from_buffer (model/record_utils.cc:147-160) */
         int64_t record_size = rd_varlong(&c);
@@ -352,9 +352,9 @@ uint32_t rpo_walk_records(const uint8_t* payload, size_t n, int32_t record_count
         e.key_len = (int32_t)klen;
         e.val_len = (int32_t)vlen;
         e.hdr_count = (int32_t)hcount;
+        e.end_pos = (uint32_t)c.pos;
         if (index && (uint64_t)parsed < index_cap) index[parsed] = e;
         parsed++;
-        *walk_end = (uint32_t)c.pos;
     }
     *trailing = c.n - c.pos;
     return parsed;
@@ -1532,9 +1532,8 @@ int64_t rpo_scan_segment_layout(const uint8_t* seg, uint64_t len, uint32_t segme
         if (do_walk) {
             uint8_t perr;
             uint64_t trailing;
-            r->records_parsed = rpo_walk_records(walk, walk_len, h.record_count,
-                                                 idx_ok ? index + r->index_base : NULL, idx_ok ? slots : 0, &perr,
-                                                 &trailing, &r->walk_end);
+            r->records_parsed = rpo_walk_records(walk, walk_len, h.record_count, (uint32_t)(st->batch_base + nb),
+                                                 idx_ok ? index + r->index_base : NULL, idx_ok ? slots : 0, &perr, &trailing);
             r->flags |= RPGPU_F_PARSED;
             r->parse_err = perr;
             if (perr == RPGPU_PARSE_ERR_NONE) {
@@ -1662,8 +1661,7 @@ static void* base_worker(void* arg) {
             if (((uint16_t)h.attrs & 7) == 0) {
                 uint8_t perr;
                 uint64_t trailing;
-                uint32_t wend;
-                rpo_walk_records(payload, need, h.record_count, scratch, 65536, &perr, &trailing, &wend);
+                rpo_walk_records(payload, need, h.record_count, 0, scratch, 65536, &perr, &trailing);
             }
             t->batches++;
             t->bytes += RPGPU_HEADER_SIZE + need;

@@ -74,13 +74,12 @@ uint32_t rpo_crc_record_batch(const rpo_header* h, const uint8_t* payload, size_
 
 /* --- record walk: model/record.h:616-627 / :680-697 over
  *     model/record_utils.cc:94-181.  Returns records fully parsed; sets
- *     *parse_err (rpgpu_parse_err of the async walk), *trailing (bytes
- *     left after record_count records when no error) and *walk_end (the
- *     payload offset after the last parsed record, 0 when none).  Writes at
- *     most index_cap entries. */
+ *     *parse_err (rpgpu_parse_err of the async walk) and *trailing (bytes
+ *     left after record_count records when no error).  Writes at most
+ *     index_cap entries. */
 uint32_t rpo_walk_records(const uint8_t* payload, size_t n, int32_t record_count,
-                          rpgpu_record_index* index, uint64_t index_cap, uint8_t* parse_err,
-                          uint64_t* trailing, uint32_t* walk_end);
+                          uint32_t batch_ordinal, rpgpu_record_index* index,
+                          uint64_t index_cap, uint8_t* parse_err, uint64_t* trailing);
 
 /* --- compression::compressor::uncompress (compression/compression.cc:34-55)
  *     for lz4 (lz4_frame_compressor.cc:115-213) and snappy

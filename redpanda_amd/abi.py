@@ -60,16 +60,17 @@ BATCH_RESULT = np.dtype([
     ("index_base", "<u8"), ("decoded_off", "<u8"), ("records_parsed", "<u4"),
     ("decoded_len", "<u4"), ("decoded_crc", "<u4"), ("decoded_header_crc", "<u4"),
     ("attrs", "<i2"), ("producer_epoch", "<i2"), ("type", "i1"), ("parse_err", "u1"),
-    ("reserved0", "<u2"), ("reserved1", "<u4"), ("walk_end", "<u4"),
+    ("reserved0", "<u2"), ("reserved1", "<u8"),
 ])
 assert BATCH_RESULT.itemsize == 128
 
 RECORD_INDEX = np.dtype([
-    ("rec_pos", "<u4"), ("length", "<i4"), ("ts_delta", "<i8"), ("offset_delta", "<i4"),
-    ("key_len", "<i4"), ("key_pos", "<u4"), ("val_len", "<i4"), ("val_pos", "<u4"),
-    ("hdr_count", "<i4"), ("hdr_pos", "<u4"), ("attrs", "i1"), ("pad", "u1", (3,)),
+    ("batch", "<u4"), ("rec_pos", "<u4"), ("ts_delta", "<i8"), ("length", "<i4"),
+    ("offset_delta", "<i4"), ("key_len", "<i4"), ("key_pos", "<u4"), ("val_len", "<i4"),
+    ("val_pos", "<u4"), ("hdr_count", "<i4"), ("hdr_pos", "<u4"), ("end_pos", "<u4"),
+    ("attrs", "i1"), ("pad", "u1", (3,)), ("reserved", "<u4", (2,)),
 ])
-assert RECORD_INDEX.itemsize == 48
+assert RECORD_INDEX.itemsize == 64
 
 SEGMENT_SUMMARY = np.dtype([
     ("first_batch", "<u8"), ("n_batches", "<u8"), ("terminal_pos", "<u8"),
@@ -99,7 +100,7 @@ assert JOB_TOTALS.itemsize == 72
 # fields of rpgpu_batch_result that are outputs of the engine and compared
 # bit-exactly against the oracle (reserved fields excluded)
 BATCH_COMPARE_FIELDS = [n for n in BATCH_RESULT.names if not n.startswith("reserved")]
-RECORD_COMPARE_FIELDS = [n for n in RECORD_INDEX.names if n != "pad"]
+RECORD_COMPARE_FIELDS = [n for n in RECORD_INDEX.names if n not in ("pad", "reserved")]
 SUMMARY_COMPARE_FIELDS = [n for n in SEGMENT_SUMMARY.names if n != "reserved"]
 
 
@@ -125,16 +126,3 @@ def record_batches(batches: np.ndarray, n_records: int) -> np.ndarray:
     out[slot] = b
     return out
 
-
-def record_ends(batches: np.ndarray, records: np.ndarray) -> np.ndarray:
-    """Where each parsed record ends: the next record's rec_pos inside its
-    batch, the batch's walk_end for its last parsed record."""
-    n = len(records)
-    end = np.zeros(n, dtype=np.uint32)
-    slot, b, k = _record_slots(batches, n)
-    last = k == batches["records_parsed"].astype(np.int64)[b] - 1
-    end[slot[last]] = batches["walk_end"][b[last]]
-    nxt = slot[~last] + 1
-    ok = nxt < n
-    end[slot[~last][ok]] = records["rec_pos"][nxt[ok]]
-    return end

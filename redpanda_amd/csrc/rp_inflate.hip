@@ -267,28 +267,6 @@ DEV void inf_root(const InfCode& c, const uint16_t* syms, uint16_t* root) {
     }
 }
 
-// The root table held in four VGPRs (lane l: entries 64 k + l, two per
-// dword): the fast loop's lookups are four v_readlane and a select, where an
-// LDS read put its latency on every symbol of the serial chain (one wave per
-// member, one wave per SIMD: nothing else hides it)
-struct RootV {
-    uint32_t r[4];
-};
-DEV RootV root_v(const uint16_t* root) {
-    const uint32_t l = lane();
-    RootV t;
-#pragma unroll
-    for (uint32_t j = 0; j < 4; j++) t.r[j] = (uint32_t)root[128u * j + l] | ((uint32_t)root[128u * j + 64u + l] << 16);
-    return t;
-}
-DEV uint32_t root_at(const RootV& t, uint32_t idx) {
-    const int li = (int)(idx & 63u);
-    const uint32_t k = idx >> 6;
-    const uint32_t a = rl(t.r[0], li), b = rl(t.r[1], li), c = rl(t.r[2], li), d = rl(t.r[3], li);
-    const uint32_t w = k < 2 ? a : k < 4 ? b : k < 6 ? c : d;
-    return (k & 1) ? w >> 16 : w & 0xFFFFu;
-}
-
 // ---------------------------------------------------------------------------
 // Output (decode pass): ring in LDS, 1 KiB chunks flushed to the slot with
 // their CRC32 / Adler-32 folded into the running check.
@@ -594,7 +572,6 @@ DEV int inflate_member(InfIn& in, InfTabs* T, InfOut& o, const InfSymTabs& ST, u
             // root tables, longer ones by the limit compare.  It hands over to
             // the exact loop below near the end (and at the block end).
             if (kWrite) {
-                const RootV LR = root_v(T->lroot), DR = root_v(T->droot);
                 const uint64_t pb = bp + 8ull * in.mis;
                 uint64_t pq = (pb >> 5) << 2;                 // next dword to load (physical byte offset)
                 uint32_t sh = (uint32_t)(pb & 31);
@@ -621,7 +598,7 @@ DEV int inflate_member(InfIn& in, InfTabs* T, InfOut& o, const InfSymTabs& ST, u
                         bc += 32;
                         pq += 4;
                     }
-                    uint32_t e = root_at(LR, (uint32_t)bb & 511u);
+                    uint32_t e = uni32((uint32_t)T->lroot[(uint32_t)bb & 511u]);
                     if (e == 0) {  // a code longer than 9 bits
                         const int r = inf_decode((uint32_t)bb, 64, LC, T->lsym, sym, len);
                         if (r < 0) return -1;  // invalid literal/length code
@@ -649,7 +626,7 @@ DEV int inflate_member(InfIn& in, InfTabs* T, InfOut& o, const InfSymTabs& ST, u
                         bc += 32;
                         pq += 4;
                     }
-                    e = root_at(DR, (uint32_t)bb & 511u);
+                    e = uni32((uint32_t)T->droot[(uint32_t)bb & 511u]);
                     if (e == 0) {
                         const int r = inf_decode((uint32_t)bb, 64, DC, T->dsym, sym, len);
                         if (r < 0) return -1;  // invalid distance code

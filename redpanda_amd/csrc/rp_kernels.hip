@@ -589,7 +589,6 @@ __global__ __launch_bounds__(256) void k_emit(DeviceJob j) {
             r.reserved0 = 0;
             // scratch for k_validate: raw CRC contribution of the BE prefix
             r.reserved1 = praw;
-            r.walk_end = 0;
             j.batches[ord] = r;
             j.slots[ord] = slots;
             j.dcap[ord] = cap;

@@ -1523,6 +1523,7 @@ int rpgpu_validate_host(rpgpu_ctx* c, const rpgpu_host_job* job) {
             r.index_base += rec_base;
             r.decoded_off += dec_base;
         }
+        for (uint64_t i = 0; i < rtake; i++) job->records[rec_base + i].batch += (uint32_t)out_b;
         for (uint32_t i = 0; i < g.nseg; i++) job->summaries[g.seg0 + i].first_batch += out_b;
         if (ix)
             for (uint32_t i = 0; i < g.nseg; i++) job->index_states[g.seg0 + i].first_entry += out_b;

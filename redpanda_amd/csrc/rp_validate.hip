@@ -500,7 +500,6 @@ struct WalkResult {
     uint32_t parsed;
     uint32_t err;
     uint32_t trailing;
-    uint32_t end;  // payload offset after the last parsed record (the batch's walk_end)
 };
 
 // 12 bytes at payload offset q (wave-uniform) through the scalar cache: the
@@ -618,24 +617,6 @@ DEV uint32_t chain_starts_spec(const uint8_t* p0, uint32_t n, uint32_t start, ui
     }
 }
 
-// a parsed record's 48-byte index entry (rpgpu_record_index)
-DEV rpgpu_record_index index_entry(uint32_t start, const Rec& r) {
-    rpgpu_record_index e;
-    e.rec_pos = start;
-    e.length = r.length;
-    e.ts_delta = r.ts;
-    e.offset_delta = r.off;
-    e.key_len = r.klen;
-    e.key_pos = r.key_pos;
-    e.val_len = r.vlen;
-    e.val_pos = r.val_pos;
-    e.hdr_count = r.hcount;
-    e.hdr_pos = r.hdr_pos;
-    e.attrs = (int8_t)r.attr;
-    e.pad[0] = e.pad[1] = e.pad[2] = 0;
-    return e;
-}
-
 // Lanes [0, m) parse one record each from their speculative starts; the
 // prefix whose starts are confirmed by the previous record's exact end is
 // committed to the index.  Returns false when a record failed (wr filled).
@@ -655,12 +636,28 @@ DEV bool parse_group(const uint8_t* p0, uint32_t mis, uint32_t n, uint32_t m, ui
     const uint32_t exact = bad ? (uint32_t)__builtin_ctzll(bad) : m;  // lanes [0, exact) are exact
     const uint64_t errs = __ballot(act && l < exact && r.err != 0);
     const uint32_t nok = errs ? (uint32_t)__builtin_ctzll(errs) : exact;  // records parsed OK
-    if (l < nok && done + l < out_cap) out[done + l] = index_entry(my_start, r);
+    if (l < nok && done + l < out_cap) {
+        rpgpu_record_index e;
+        e.batch = batch_ord;
+        e.rec_pos = my_start;
+        e.ts_delta = r.ts;
+        e.length = r.length;
+        e.offset_delta = r.off;
+        e.key_len = r.klen;
+        e.key_pos = r.key_pos;
+        e.val_len = r.vlen;
+        e.val_pos = r.val_pos;
+        e.hdr_count = r.hcount;
+        e.hdr_pos = r.hdr_pos;
+        e.end_pos = r.end;
+        e.attrs = (int8_t)r.attr;
+        e.pad[0] = e.pad[1] = e.pad[2] = 0;
+        e.reserved[0] = e.reserved[1] = 0;
+        out[done + l] = e;
+    }
     if (errs) {
         wr.parsed = done + nok;
         wr.err = rl(r.err, (int)nok);
-        // the failing record starts where the last parsed one ended
-        wr.end = nok ? rl(my_start, (int)nok) : start;
         return false;
     }
     start = rl(r.end, (int)(exact - 1));
@@ -692,7 +689,6 @@ DEV WalkResult walk_records(const uint8_t* p0, uint32_t n, int32_t rc, uint32_t 
     wr.parsed = 0;
     wr.err = 0;
     wr.trailing = 0;
-    wr.end = 0;
     const uint32_t mis = (uint32_t)((uintptr_t)p0 & 15);
     const uint32_t total = (uint32_t)(rc > 0 ? rc : 0);
     uint32_t start = 0, done = 0;
@@ -718,7 +714,6 @@ DEV WalkResult walk_records(const uint8_t* p0, uint32_t n, int32_t rc, uint32_t 
     }
     wr.parsed = done;
     wr.trailing = n - start;
-    wr.end = start;
     return wr;
 }
 
@@ -971,36 +966,37 @@ DEV void coop_load(uint8_t* slot, const uint8_t* g, uint32_t rows) {
     }
 }
 
-// Wave-cooperative index store (all 64 lanes active): lane w's 48-byte entry
+// Wave-cooperative index store (all 64 lanes active): lane w's 64-byte entry
 // e goes to dst (null: nothing to write).  The entries are staged in LDS
-// (`stage`, 3 KiB, wave-uniform) and written as 3 wave-instructions of 64
-// lanes x 16 bytes, entry w's three quarters by three neighbouring lanes,
-// instead of one 16-byte piece of each of 64 scattered entries per
-// instruction (the index stores were a third of the walk's time).
+// (`stage`, 4 KiB, wave-uniform) and written 16 per wave-instruction, each
+// as 4 lanes x 16 contiguous bytes, instead of one 16-byte piece of each of
+// 64 scattered entries per instruction (the index stores were a third of
+// the walk's time).
 #ifndef RPGPU_NT_INDEX
 #define RPGPU_NT_INDEX 0  // index entries stored non-temporal (A/B knob)
 #endif
 DEV void coop_store(uint8_t* stage, const rpgpu_record_index& e, rpgpu_record_index* dst) {
-    static_assert(sizeof(rpgpu_record_index) == 48, "index entry is 3 x 16 bytes");
+    static_assert(sizeof(rpgpu_record_index) == 64, "index entry is 4 x 16 bytes");
     const uint32_t l = lane_v();
     const uint4* src = (const uint4*)&e;
-    uint4* mine = (uint4*)(stage + 48u * l);
+    uint4* mine = (uint4*)(stage + 64u * l);
     if (dst) {
         mine[0] = src[0];
         mine[1] = src[1];
         mine[2] = src[2];
+        mine[3] = src[3];
     }
     const uint64_t da = (uint64_t)(uintptr_t)dst;
     const int lo = (int)(uint32_t)da, hi = (int)(uint32_t)(da >> 32);
 #pragma unroll
-    for (uint32_t m = 0; m < 3u; m++) {
-        const uint32_t q = 64u * m + l, w = (q * 0xAABu) >> 13, part = q - 3u * w;  // q / 3 for q < 192
+    for (uint32_t m = 0; m < 4u; m++) {
+        const uint32_t w = 16u * m + (l >> 2), qtr = l & 3u;
         const int src_lane = (int)(w * 4u);
         const uint32_t wlo = (uint32_t)__builtin_amdgcn_ds_bpermute(src_lane, lo);
         const uint32_t whi = (uint32_t)__builtin_amdgcn_ds_bpermute(src_lane, hi);
         if (wlo | whi) {
-            const uint4 v = *(const uint4*)(stage + 16u * q);
-            uint4* d = (uint4*)((uint8_t*)(uintptr_t)(((uint64_t)whi << 32) | wlo) + 16u * part);
+            const uint4 v = *(const uint4*)(stage + 64u * w + 16u * qtr);
+            uint4* d = (uint4*)((uint8_t*)(uintptr_t)(((uint64_t)whi << 32) | wlo) + 16u * qtr);
             if (RPGPU_NT_INDEX) {
                 typedef uint32_t v4u __attribute__((ext_vector_type(4)));
                 v4u x;
@@ -1136,12 +1132,25 @@ DEV bool lane_record_step(LaneWalk& w, WalkResult& wr, uint8_t* H, const uint8_t
         wr.parsed = w.done;
         wr.err = r.err;
         wr.trailing = 0;
-        wr.end = start;  // where the last parsed record ended
         return true;
     }
     // the index entry is written by the wave's cooperative store (coop_store)
     if (w.done < w.cap) {
-        e = index_entry(start, r);
+        e.batch = w.ord;
+        e.rec_pos = start;
+        e.ts_delta = r.ts;
+        e.length = r.length;
+        e.offset_delta = r.off;
+        e.key_len = r.klen;
+        e.key_pos = r.key_pos;
+        e.val_len = r.vlen;
+        e.val_pos = r.val_pos;
+        e.hdr_count = r.hcount;
+        e.hdr_pos = r.hdr_pos;
+        e.end_pos = r.end;
+        e.attrs = (int8_t)r.attr;
+        e.pad[0] = e.pad[1] = e.pad[2] = 0;
+        e.reserved[0] = e.reserved[1] = 0;
         dst = w.out + w.done;
     }
     w.done++;
@@ -1150,7 +1159,6 @@ DEV bool lane_record_step(LaneWalk& w, WalkResult& wr, uint8_t* H, const uint8_t
         wr.parsed = w.done;
         wr.err = 0;
         wr.trailing = n - w.start;
-        wr.end = w.start;
         return true;
     }
     // the next record's head: in C_k when the guess held
@@ -1215,7 +1223,6 @@ DEV void lane_walk_finish(const WalkCtx& j, uint64_t b, const WalkResult& w, boo
     if (wire && !(f & RPGPU_F_PARSE_OK)) note_bad_lane(j, R->segment, b);
     atomicOr(&R->flags, f);
     R->records_parsed = w.parsed;
-    R->walk_end = w.end;
     R->parse_err = (uint8_t)perr;
 }
 
@@ -1267,7 +1274,7 @@ __global__ __launch_bounds__(1024) void k_validate(DeviceJob j) {
                 continue;
             }
             uint32_t f = d.flags;
-            uint32_t parsed = 0, perr = 0, wend = 0;
+            uint32_t parsed = 0, perr = 0;
             // uncompressed: the first record chain runs now, while the
             // window's lines are arriving in L2 (its scalar loads hit or merge
             // with them; after the CRC they would be evicted again)
@@ -1314,7 +1321,6 @@ __global__ __launch_bounds__(1024) void k_validate(DeviceJob j) {
                 const WalkResult w = walk_batch(j, d, p0, n, b, idx_ok, g0);
                 f |= walk_flags(j, w, idx_ok, perr);
                 parsed = w.parsed;
-                wend = w.end;
             }
             // wire: the first batch batch_reader::do_load_slice rejects
             // (kafka/protocol/batch_reader.cc:129-151): not v2 / bad crc, codec
@@ -1335,7 +1341,6 @@ __global__ __launch_bounds__(1024) void k_validate(DeviceJob j) {
                 R->decoded_off = d.doff;
                 if (walk) {
                     R->records_parsed = parsed;
-                    R->walk_end = wend;
                     R->parse_err = (uint8_t)perr;
                 }
                 // a decoded payload is finished by k_validate_decoded, which
@@ -1468,7 +1473,7 @@ __global__ __launch_bounds__(1024) void k_validate_decoded(DeviceJob j) {
         }
         const uint32_t dhcrc = decoded_header_crc(T, j.data + hdr, (uint32_t)(RPGPU_HEADER_SIZE + dl), dcrc,
                                                   j.layout == RPGPU_LAYOUT_WIRE);
-        uint32_t f = d.flags, perr = 0, parsed = 0, wend = 0;
+        uint32_t f = d.flags, perr = 0, parsed = 0;
         if ((j.flags & RPGPU_JOB_PARSE) && (j.layout != RPGPU_LAYOUT_WIRE || (d.flags & RPGPU_F_CRC_OK))) {
             bool idx_ok;
             Group g0;
@@ -1476,12 +1481,10 @@ __global__ __launch_bounds__(1024) void k_validate_decoded(DeviceJob j) {
             const WalkResult w = walk_batch(j, d, j.decoded + d.doff, (uint32_t)dl, b, idx_ok, g0);
             f |= walk_flags(j, w, idx_ok, perr);
             parsed = w.parsed;
-            wend = w.end;
         }
         if (l == 0) {
             R->flags = f;
             R->records_parsed = parsed;
-            R->walk_end = wend;
             R->parse_err = (uint8_t)perr;
             R->decoded_crc = dcrc;
             R->decoded_header_crc = dhcrc;
@@ -1528,7 +1531,7 @@ __global__ __launch_bounds__(256) void k_walk(DeviceJob j) {
             else if (!(wire && !(j.batches[b].flags & RPGPU_F_CRC_OK)) && lane_walk_setup(c, b, w, idx_ok)) {
                 if (w.total == 0) {
                     WalkResult wr;
-                    wr.parsed = 0; wr.err = 0; wr.trailing = w.n; wr.end = 0;
+                    wr.parsed = 0; wr.err = 0; wr.trailing = w.n;
                     lane_walk_finish(c, b, wr, idx_ok, wire);
                 } else st = kHead;
             }

@@ -115,10 +115,9 @@ def gather_records(batches, records, summaries, parts: Sequence[int], rank: int,
 
     On rank 0 the result is what a single-process job over all partitions
     (segment s = partition s) returns: batch `segment` = the partition id,
-    batch ordinals and `index_base` continue across partitions (a record's
-    batch is the result whose slot range holds it, abi.record_batches).
-    `decoded_off` stays rank-local (the decoded arena is not gathered).  None
-    on other ranks."""
+    batch ordinals and `index_base` continue across partitions, record
+    `batch` = the global batch ordinal.  `decoded_off` stays rank-local (the
+    decoded arena is not gathered).  None on other ranks."""
     import torch
     from . import abi
     meta = torch.tensor(list(parts), dtype=torch.int64, device=batches.device)
@@ -139,17 +138,18 @@ def gather_records(batches, records, summaries, parts: Sequence[int], rank: int,
             b0, nb, nrec = int(s["first_batch"]), int(s["n_batches"]), int(s["n_records"])
             if b0 + nb > len(rb) or rec0 + nrec > len(rr):
                 raise RuntimeError(f"rank {r} partition {p}: results shorter than its summary")
-            per_part[int(p)] = (rb[b0:b0 + nb], rr[rec0:rec0 + nrec], rec0)
+            per_part[int(p)] = (rb[b0:b0 + nb], rr[rec0:rec0 + nrec], b0, rec0)
             rec0 += nrec
     bs, rs_ = [], []
     gb = gr = 0
     for p in sorted(per_part):
-        b, rec, r0 = per_part[p]
+        b, rec, b0, r0 = per_part[p]
         b = b.copy()
         rec = rec.copy()
         b["segment"] = p
         # index_base: the record slot of the batch's first index entry
         b["index_base"] = b["index_base"] - np.uint64(r0) + np.uint64(gr)
+        rec["batch"] = (rec["batch"].astype(np.int64) - b0 + gb).astype(np.uint32)
         bs.append(b)
         rs_.append(rec)
         gb += len(b)

@@ -32,7 +32,7 @@ def test_struct_layouts_match_header():
 int main(void) {
   printf("%zu %zu %zu %zu %zu %zu %zu\n", sizeof(rpgpu_batch_result), sizeof(rpgpu_record_index),
          sizeof(rpgpu_segment_summary), sizeof(rpgpu_job_totals), offsetof(rpgpu_batch_result, flags),
-         offsetof(rpgpu_record_index, hdr_pos), offsetof(rpgpu_job, d_valid_bitmap));
+         offsetof(rpgpu_record_index, end_pos), offsetof(rpgpu_job, d_valid_bitmap));
   return 0;
 }'''
     exe = "/tmp/rpgpu_layout_check"
@@ -43,8 +43,7 @@ int main(void) {
     assert vals[:4] == [abi.BATCH_RESULT.itemsize, abi.RECORD_INDEX.itemsize, abi.SEGMENT_SUMMARY.itemsize,
                         abi.JOB_TOTALS.itemsize]
     assert vals[4] == abi.BATCH_RESULT.fields["flags"][1]
-    assert vals[5] == abi.RECORD_INDEX.fields["hdr_pos"][1]
-    assert abi.RECORD_INDEX.itemsize == 48  # 48 B per record
+    assert vals[5] == abi.RECORD_INDEX.fields["end_pos"][1]
     from redpanda_amd._lib import JobC
     assert vals[6] == JobC.d_valid_bitmap.offset
 
@@ -88,24 +87,3 @@ def test_generator_codec_mix_decodes(rplib, oracle):
     r = oracle.run_job(a, [0, a.size])
     f = r.batches["flags"]
     assert np.all(f & abi.F_COMPRESSED) and np.all(f & abi.F_CODEC_OK) and np.all(f & abi.F_PARSE_OK)
-
-
-def test_record_index_ends_and_batches(rplib, oracle):
-    """The 48-byte index drops the per-record batch ordinal and end position:
-    both follow from the batch results (abi.record_batches / record_ends)."""
-    a = np.zeros(3 << 20, dtype=np.uint8)
-    synth.gen_segment(a, 1, seed=0xC5, batch_bytes=0, min_batch=200, max_batch=200000, corrupt_payload_ppm=20000,
-                      weights=[3, 0, 1, 1, 0, 1])
-    r = oracle.run_job(a, [0, a.size], abi.JOB_CRC | abi.JOB_PARSE | abi.JOB_DECODE)
-    b, rec = r.batches, r.records
-    rb = abi.record_batches(b, len(rec))
-    ends = abi.record_ends(b, rec)
-    assert len(rec) > 1000 and np.all(rb >= 0) and np.all(np.diff(rb) >= 0)
-    first = np.r_[True, rb[1:] != rb[:-1]]
-    assert np.all(rec["rec_pos"][first] == 0)
-    assert np.all(ends > rec["rec_pos"]) and np.all(ends >= rec["hdr_pos"])
-    ok = (b["flags"] & abi.F_PARSE_OK) != 0
-    plen = np.where((b["flags"] & abi.F_COMPRESSED) != 0, b["decoded_len"], b["size_bytes"] - abi.HEADER_SIZE)
-    walked = ok & (b["records_parsed"] > 0)
-    assert np.any(walked) and np.all(b["walk_end"][walked] == plen[walked])
-    assert np.all(b["walk_end"][b["records_parsed"] == 0] == 0)

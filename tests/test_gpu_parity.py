@@ -734,7 +734,7 @@ def test_zstd_ring_mode_reject_rule(engine, oracle):
     assert len(gb) == len(rb) == len(pay)
     assert np.all((gb["flags"][div] & abi.F_CODEC_OK) == 0) and np.all((rb["flags"][div] & abi.F_CODEC_OK) != 0)
     for f in ("flags", "crc_computed", "header_crc_computed", "decoded_len", "decoded_crc", "decoded_header_crc",
-              "records_parsed", "parse_err", "walk_end"):
+              "records_parsed", "parse_err"):
         np.testing.assert_array_equal(gb[f][~div], rb[f][~div], err_msg=f)
     for i in np.nonzero(~div & ((rb["flags"] & abi.F_CODEC_OK) != 0))[0]:
         go, ro, n = int(gb["decoded_off"][i]), int(rb["decoded_off"][i]), int(rb["decoded_len"][i])

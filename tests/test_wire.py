@@ -166,10 +166,9 @@ def test_wire_equals_disk(oracle, rplib):
         np.testing.assert_array_equal(wb["flags"] & ~np.uint32(abi.F_WIRE_V2), want)
         np.testing.assert_array_equal(wb["records_parsed"][ok], db["records_parsed"][ok])
         np.testing.assert_array_equal(wb["index_base"], db["index_base"])
-        np.testing.assert_array_equal(wb["walk_end"][ok], db["walk_end"][ok])
         for i in np.nonzero(ok)[0]:
             lo, k = int(db["index_base"][i]), int(db["records_parsed"][i])
-            for f in ("rec_pos", "ts_delta", "length", "offset_delta", "key_len", "val_len", "hdr_count"):
+            for f in ("rec_pos", "ts_delta", "length", "offset_delta", "key_len", "val_len", "hdr_count", "end_pos"):
                 np.testing.assert_array_equal(w.records[f][lo:lo + k], d.records[f][lo:lo + k], err_msg=f)
         assert w.summaries[0]["first_bad"] == d.summaries[0]["first_bad"]
         assert w.summaries[0]["ckpt_last_offset"] == d.summaries[0]["ckpt_last_offset"]
