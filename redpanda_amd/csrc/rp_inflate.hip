@@ -346,8 +346,7 @@ DEV void inf_flush_upto(InfOut& o, uint64_t op) {
 DEV void inf_copy(InfOut& o, uint64_t op, uint32_t dist, uint32_t ml) {
     const uint32_t l = lane();
     const bool rep = dist < ml;
-    // (a 32-bit divide: the 64-bit one is a long software sequence per match)
-    const uint64_t mg = !rep ? 0ull : dist == 1 ? (1ull << 32) : (uint64_t)(0xFFFFFFFFu / dist) + 1ull;
+    const uint64_t mg = rep ? 0xFFFFFFFFull / dist + 1ull : 0ull;
     const uint32_t n = (ml + 63) >> 6;  // deflate: ml <= 258, at most 5 rows
     uint32_t b[5];
 #pragma unroll
@@ -1038,8 +1037,7 @@ struct ZDev {
         // byte x of a piece is x mod off into them (off < 256: a multiply by
         // the rounded-up reciprocal is exact for x < 256)
         const bool rep = off < 256 && off < ml;
-        const uint32_t off32 = (uint32_t)off;  // < 256 when rep
-        const uint64_t mg = !rep ? 0ull : off32 == 1 ? (1ull << 32) : (uint64_t)(0xFFFFFFFFu / off32) + 1ull;
+        const uint64_t mg = rep ? 0xFFFFFFFFull / off + 1ull : 0ull;  // 2^32 for off = 1
         for (uint64_t c = 0; c < ml; c += 256) {
             const uint32_t m = ml - c < 256 ? (uint32_t)(ml - c) : 256u;
             uint32_t v[4];

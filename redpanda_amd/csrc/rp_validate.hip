@@ -549,74 +549,6 @@ DEV uint32_t chain_starts(const Src& src, uint32_t n, uint32_t start, uint32_t w
     return m;
 }
 
-// The same starts and ends as chain_starts, found by speculation: lanes
-// [m, want) guess their record's start p + (lane - m) * stride (p exact) and
-// read its length varint with their own vector loads, all in one memory
-// round trip; the prefix whose guesses each equal the previous lane's end is
-// exact.  A round confirms at least one record (lane m starts at p), so it is
-// never slower than the serial chain in round trips, and a batch of
-// same-sized records (the common case: one producer's payloads) confirms 64
-// per round.  The stride starts at `hint` and then follows the last
-// confirmed record's size.  Used where the vector-memory queue is otherwise
-// idle (k_validate's first group keeps the scalar chain: there it runs while
-// the CRC window streams in).
-DEV uint32_t chain_starts_spec(const uint8_t* p0, uint32_t n, uint32_t start, uint32_t want, uint32_t hint,
-                               uint32_t& my_start, uint32_t& my_end) {
-    const uint32_t l = lane_v();
-    my_start = my_end = 0xFFFFFFFFu;
-    uint32_t p = start, m = 0, stride = hint;
-    for (;;) {
-        const bool in = l >= m && l < want;
-        const uint64_t q64 = (uint64_t)p + (uint64_t)(l - m) * stride;
-        // (a guess past 2^32 saturates and can only be wrong; lane m's is p)
-        const uint32_t q = q64 > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)q64;
-        bool term = false, valid = false;
-        uint32_t e = 0xFFFFFFFFu;
-        if (in) {
-            if (q >= n) {
-                term = true;
-            } else {
-                const uintptr_t a = (uintptr_t)(p0 + q);
-                uint4 w;
-                __builtin_memcpy(&w, (const void*)(a & ~(uintptr_t)3), 16);
-                const uint32_t sh = (uint32_t)(a & 3);
-                uint32_t br;
-                const int64_t len = varint12(__builtin_amdgcn_alignbyte(w.y, w.x, sh),
-                                             __builtin_amdgcn_alignbyte(w.z, w.y, sh),
-                                             __builtin_amdgcn_alignbyte(w.w, w.z, sh), n - q, br);
-                if (len < 0 || (uint64_t)len > n) term = true;
-                else {
-                    valid = true;
-                    e = q + br + (uint32_t)len;
-                }
-            }
-        }
-        // lane k > m is exact iff lane k - 1 is exact, ends and ends at q_k
-        const uint32_t pe = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)e, 0x138, 0xF, 0xF, false);
-        const uint32_t pv = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)valid, 0x138, 0xF, 0xF, false);
-        const bool link = l == m || (pv != 0u && pe == q);
-        const uint64_t bad = __ballot(in && !link);
-        const uint32_t c = bad ? (uint32_t)__builtin_ctzll(bad) : want;  // lanes [m, c) start exactly
-        const uint64_t tm = __ballot(in && l < c && term);
-        if (tm) {
-            // the serial chain stops at this record: its start, no end
-            const uint32_t t = (uint32_t)__builtin_ctzll(tm);
-            if (in && l <= t) my_start = q;
-            if (in && l < t) my_end = e;
-            return t + 1;
-        }
-        if (in && l < c) {
-            my_start = q;
-            my_end = e;
-        }
-        if (c >= want) return want;
-        const uint32_t qe = rl(q, (int)c - 1);
-        p = rl(e, (int)c - 1);
-        stride = p - qe;
-        m = c;
-    }
-}
-
 // Lanes [0, m) parse one record each from their speculative starts; the
 // prefix whose starts are confirmed by the previous record's exact end is
 // committed to the index.  Returns false when a record failed (wr filled).
@@ -696,11 +628,10 @@ DEV WalkResult walk_records(const uint8_t* p0, uint32_t n, int32_t rc, uint32_t 
         wr.trailing = n;
         return wr;
     }
-    // the stride guess of the speculative chain: the mean record size
-    const uint32_t hint = n / total;
+    const MemSrc mem{p0};
     if (!g.first) {
         STAMP(w0);
-        g.m = chain_starts_spec(p0, n, 0u, total < 64u ? total : 64u, hint, g.my_start, g.my_end);
+        g.m = chain_starts(mem, n, 0u, total < 64u ? total : 64u, g.my_start, g.my_end);
         record_regions(p0, mis, n, lane_v() < g.m, g.my_start, g.my_end, g.H, g.T);
         STAMP(w1);
         STAMP_ADD(6, w1 - w0);
@@ -709,7 +640,7 @@ DEV WalkResult walk_records(const uint8_t* p0, uint32_t n, int32_t rc, uint32_t 
         if (!parse_group(p0, mis, n, g.m, g.my_start, g.H, g.T, batch_ord, out, out_cap, done, start, wr)) return wr;
         if (done >= total) break;
         const uint32_t want = (total - done) < 64u ? (total - done) : 64u;
-        g.m = chain_starts_spec(p0, n, start, want, hint, g.my_start, g.my_end);
+        g.m = chain_starts(mem, n, start, want, g.my_start, g.my_end);
         record_regions(p0, mis, n, lane_v() < g.m, g.my_start, g.my_end, g.H, g.T);
     }
     wr.parsed = done;
@@ -1332,17 +1263,11 @@ __global__ __launch_bounds__(1024) void k_validate(DeviceJob j) {
             STAMP_ADD(1, tc - tb2);
             if (l == 0) {
                 R->crc_computed = crc;
-                // (plain stores: a device-scope atomic here put its memory
-                // round trip into the next batch's vmcnt waits, validate 2.9
-                // -> 5.3 ms on C1; the parse fields are written by whichever
-                // kernel walks the batch, k_emit zeroed them)
                 R->flags = f;
                 R->index_base = d.ib;
                 R->decoded_off = d.doff;
-                if (walk) {
-                    R->records_parsed = parsed;
-                    R->parse_err = (uint8_t)perr;
-                }
+                R->records_parsed = parsed;
+                R->parse_err = (uint8_t)perr;
                 // a decoded payload is finished by k_validate_decoded, which
                 // still needs the prefix contribution (so does k_crc_combine)
                 if (!(d.codec != 0 && (f & RPGPU_F_CODEC_OK)) && !split) R->reserved1 = 0;
