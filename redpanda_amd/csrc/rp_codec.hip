@@ -2517,6 +2517,59 @@ __global__ __launch_bounds__(64 * kExecWaves) void k_lz_exec(DeviceJob j) {
 }
 
 // ---------------------------------------------------------------------------
+// k_zexec: the zstd members the member pass parsed into records
+// (rp_inflate.hip zstd_fast_item, inf_state kZsFast), one wave each, claimed
+// in member-list order, through the same ring executor as LZ4 pieces: literals from the
+// member's literal buffer, matches from the ring or, further back, from the
+// slot itself (linked mode).  The decoded crc is k_validate_decoded's.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(64 * kExecWaves) void k_zexec(DeviceJob j) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t xlds[];
+    const uint32_t wi = threadIdx.x >> 6;
+    lds_u8* ring = (lds_u8*)(xlds + wi * kXRing);
+    uint32_t* ct_w = (uint32_t*)(xlds + kXCrcOff);
+    uint32_t* pat_w = (uint32_t*)(xlds + kXPatOff);
+    for (uint32_t i = threadIdx.x; i < 1024u; i += blockDim.x) {
+        ct_w[i] = j.tables->braid[i >> 8][i & 255u];
+        ct_w[1024u + i] = j.tables->hdr[3u - (i >> 8)][i & 255u];
+    }
+    for (uint32_t i = threadIdx.x; i < 128u; i += blockDim.x)
+        pat_w[i] = i < 64u ? (&kPat.a[0][0])[i] : (&kPat.b[0][0])[i - 64u];
+    __syncthreads();
+    const __attribute__((address_space(3))) uint32_t* pat = (const __attribute__((address_space(3))) uint32_t*)pat_w;
+    lds_cu32* ct = (lds_cu32*)ct_w;
+    const uint32_t count = j.counters[16];
+    for (;;) {
+        const uint32_t i = wave_fetch_add(&j.counters[21], 1u);
+        if (i >= count) break;
+        if (uni32(j.inf_state[i]) != kZsFast) continue;
+        const uint32_t b = uni32(j.inf_list[i]);
+        rpgpu_batch_result* R = &j.batches[b];
+        const uint64_t dst = uni64(j.dcap[b]), cap = uni64(j.dcap[b + 1]) - dst, total = uni64(j.inf_total[i]);
+        if (dst + cap > j.decoded_capacity) {
+            if (lane() == 0) R->flags = R->flags | RPGPU_F_DECODE_OVERFLOW;
+            continue;
+        }
+        const uint8_t* base = j.inf_scratch + uni64(j.inf_off[i]);
+        const ZsFastDesc* d = (const ZsFastDesc*)base;
+        const uint64_t nlit = uni64(d->nlit), nrec = uni64(d->nrec);
+        const uint8_t* lits = base + uni64(d->lit_off);
+        const SeqRec* recs = (const SeqRec*)(base + uni64(d->rec_off));
+        // the literal buffer has 16 spare bytes: 16-byte loads stay inside
+        const Src s{lits, (int64_t)nlit, (int64_t)nlit + 16};
+        XRing x;
+        xring_init(x, j, ring, dst, total > kXRing, false, pat, ct);
+        xrecords(x, s, recs, (uint32_t)nrec);
+        xflush(x, x.op);
+        if (lane() == 0) {
+            R->flags = R->flags | RPGPU_F_CODEC_OK;
+            R->decoded_len = (uint32_t)total;
+            R->reserved0 = 0;  // k_validate_decoded computes the decoded crc
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
 // k_decode_blocks: the sequential frames (what the planner did not split:
 // truncated or malformed frames, linked frames of more than 64 blocks,
 // unplannable snappy-java streams), one per lane through the lane engine,
@@ -2710,6 +2763,17 @@ hipError_t launch_lz_exec(const DeviceJob& j, hipStream_t s) {
 #ifdef RPGPU_DSTAMPS
     hipLaunchKernelGGL(k_print_dstamps, dim3(1), dim3(1), 0, s);
 #endif
+    return hipGetLastError();
+}
+
+hipError_t launch_zexec(const DeviceJob& j, hipStream_t s) {
+    static bool attr = false;
+    if (!attr) {
+        (void)hipFuncSetAttribute((const void*)k_zexec, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kXLds);
+        attr = true;
+    }
+    if (!j.exec_waves || !j.inf_scratch) return hipSuccess;
+    hipLaunchKernelGGL(k_zexec, dim3(j.exec_waves / kExecWaves), dim3(64 * kExecWaves), kXLds, s, j);
     return hipGetLastError();
 }
 

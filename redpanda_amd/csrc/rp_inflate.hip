@@ -1183,10 +1183,230 @@ DEV uint64_t zs_guess(InfIn& in) {
     return (g + 15) & ~15ull;
 }
 
+// ---------------------------------------------------------------------------
+// zstd parse / execute split (the first pass's fast path).  ZDev keeps the
+// decoder's state in SGPRs (readfirstlane on every value, spilled to VGPR
+// lanes) and pushes each literal and match through the LDS ring: ~1200
+// instructions per literal or sequence (profiles/r03_member_pass_sq.json).
+// ZLane runs the same decoder (zs::payload: the same acceptance rules) with
+// its state in VGPRs, every lane computing the same values, and produces no
+// output bytes: literals go to a literal buffer and each match becomes a
+// 16-byte record {literal start, literal count, match length, offset}.
+// k_zexec (rp_codec.hip) executes the records with the LZ4 engine's wave
+// executor straight into the arena slot once the plan is scanned.
+//   A member takes this path when zs_fast_size's header walk finds only
+// zstd frames without a content checksum, whole blocks and no skippable
+// frame, and the scratch pool holds its literal buffer and records (sized
+// exactly by that walk: literal section, raw and RLE bytes; sequence counts
+// + 1).  A payload the decoder rejects is rejected (state 1, as the wave
+// decoder would); one it accepts must deliver exactly the bytes its records
+// describe (state 3); anything else is decoded by ZDev as before.
+// ---------------------------------------------------------------------------
+struct ZLane {
+    const uint8_t* src;
+    uint64_t n;
+    uint8_t* lits;
+    SeqRec* recs;
+    uint64_t lcap, rcap;
+    uint64_t nlit, nrec, pend, mlsum;
+    bool bad;
+#ifdef RPGPU_ZSTAMPS
+    uint64_t prof[4];
+#endif
+    DEV uint32_t b(uint64_t i) { return i < n ? (uint32_t)src[i] : 0u; }
+    DEV uint64_t le(uint64_t i, uint32_t k) {
+        uint64_t v = 0;
+        for (uint32_t t = 0; t < k; t++) v |= (uint64_t)b(i + t) << (8 * t);
+        return v;
+    }
+    // 8 bytes at pos (pos + 8 <= n: the bit streams read inside the member)
+    DEV uint64_t lb(zs::Bits&, uint64_t pos) {
+        uint64_t v;
+        __builtin_memcpy(&v, (const __attribute__((address_space(1))) uint8_t*)(src + pos), 8);
+        return v;
+    }
+    DEV uint32_t U(uint32_t x) { return x; }
+    DEV zs::SeqSym sym(const zs::SeqSym& t) { return t; }
+    DEV void lit(uint32_t v) {
+        if (nlit >= lcap) bad = true;
+        else if (lane() == 0) lits[nlit] = (uint8_t)v;
+        nlit++;
+        pend++;
+    }
+    DEV void raw(uint64_t pos, uint64_t k) {
+        if (nlit + k > lcap) bad = true;
+        else
+            for (uint64_t c = lane(); c < k; c += 64) lits[nlit + c] = src[pos + c];
+        nlit += k;
+        pend += k;
+    }
+    DEV void fill(uint32_t v, uint64_t k) {
+        if (nlit + k > lcap) bad = true;
+        else
+            for (uint64_t c = lane(); c < k; c += 64) lits[nlit + c] = (uint8_t)v;
+        nlit += k;
+        pend += k;
+    }
+    DEV void match(uint64_t off, uint64_t ml) {
+        if (nrec >= rcap) bad = true;
+        else if (lane() == 0)
+            recs[nrec] = SeqRec{(uint32_t)(nlit - pend), (uint32_t)pend, (uint32_t)ml, (uint32_t)off};
+        nrec++;
+        pend = 0;
+        mlsum += ml;
+    }
+    DEV void frame_begin() {}
+    DEV int check(uint32_t) { return 2; }  // (never called: zs_fast_size admits no checksummed frame)
+};
+
+// The fast path's header walk: every frame a zstd frame without a content
+// checksum or dictionary, every block whole; sums the literal bytes the
+// decoder can emit and the sequences it can decode.  False sends the member to
+// the wave decoder (which also rules on anything malformed here).
+DEV bool zs_fast_size(const uint8_t* src, uint64_t n, uint64_t& nlit, uint64_t& nseq) {
+    auto b = [&](uint64_t i) -> uint32_t { return i < n ? (uint32_t)src[i] : 0u; };
+    nlit = nseq = 0;
+    uint64_t ip = 0;
+    if (n == 0) return false;
+    while (ip < n) {
+        if (n - ip < 6) return false;
+        const uint32_t magic = b(ip) | (b(ip + 1) << 8) | (b(ip + 2) << 16) | (b(ip + 3) << 24);
+        if (magic != 0xFD2FB528u) return false;
+        const uint32_t fhd = b(ip + 4);
+        const uint32_t single = (fhd >> 5) & 1, fcsid = fhd >> 6, did = fhd & 3, ck = (fhd >> 2) & 1;
+        if (ck || did || (fhd & 8)) return false;
+        const uint64_t hsize = 5 + (single ? 0 : 1) + (fcsid ? (fcsid == 1 ? 2 : fcsid == 2 ? 4 : 8) : 0) +
+                               ((single && !fcsid) ? 1 : 0);
+        if (n - ip < hsize) return false;
+        ip += hsize;
+        for (;;) {
+            if (n - ip < 3) return false;
+            const uint32_t bh = b(ip) | (b(ip + 1) << 8) | (b(ip + 2) << 16);
+            const uint32_t last = bh & 1, bt = (bh >> 1) & 3, bsz = bh >> 3;
+            ip += 3;
+            if (bt == 3) return false;
+            if (bt == 0) {
+                if (n - ip < bsz) return false;
+                nlit += bsz;
+                ip += bsz;
+            } else if (bt == 1) {
+                if (n - ip < 1) return false;
+                nlit += bsz;
+                ip += 1;
+            } else {
+                if (n - ip < bsz || bsz < 3) return false;
+                const uint32_t b0 = b(ip), lt = b0 & 3, lhl = (b0 >> 2) & 3;
+                uint64_t lsz, lcons;
+                if (lt < 2) {
+                    uint32_t lh;
+                    if (lhl == 1) {
+                        lh = 2;
+                        lsz = (b0 | (b(ip + 1) << 8)) >> 4;
+                    } else if (lhl == 3) {
+                        lh = 3;
+                        lsz = (b0 | (b(ip + 1) << 8) | (b(ip + 2) << 16)) >> 4;
+                    } else {
+                        lh = 1;
+                        lsz = b0 >> 3;
+                    }
+                    lcons = lt == 0 ? lh + lsz : lh + 1;
+                } else {
+                    if (bsz < 5) return false;
+                    const uint32_t lhc = b0 | (b(ip + 1) << 8) | (b(ip + 2) << 16) | (b(ip + 3) << 24);
+                    uint32_t lh;
+                    uint64_t lcs;
+                    if (lhl < 2) {
+                        lh = 3;
+                        lsz = (lhc >> 4) & 0x3FF;
+                        lcs = (lhc >> 14) & 0x3FF;
+                    } else if (lhl == 2) {
+                        lh = 4;
+                        lsz = (lhc >> 4) & 0x3FFF;
+                        lcs = lhc >> 18;
+                    } else {
+                        lh = 5;
+                        lsz = (lhc >> 4) & 0x3FFFF;
+                        lcs = (lhc >> 22) + ((uint64_t)b(ip + 4) << 10);
+                    }
+                    lcons = lh + lcs;
+                }
+                if (lsz > zs::kBlockMax || lcons >= bsz) return false;
+                nlit += lsz;
+                uint64_t sp = ip + lcons;
+                uint32_t ns = b(sp);
+                if (ns == 255) ns = (b(sp + 1) | (b(sp + 2) << 8)) + 0x7F00;
+                else if (ns >= 128) ns = ((ns - 128) << 8) + b(sp + 1);
+                nseq += ns;
+                ip += bsz;
+            }
+            if (last) break;
+        }
+    }
+    return ip == n;
+}
+
+// the fast path of zstd member i: 0 not taken (the wave decoder runs), else
+// the state set (1 rejected, kZsFast parsed)
+DEV uint32_t zstd_fast_item(const DeviceJob& j, uint8_t* lds, uint32_t i, uint32_t b, const rpgpu_batch_result* R) {
+    if (!j.inf_scratch) return 0;
+    const uint64_t S = uni64(j.seg_off[uni32(R->segment)]) + uni64(R->file_pos) + RPGPU_HEADER_SIZE;
+    const uint64_t n = (uint64_t)uni32((uint32_t)(R->size_bytes - (int32_t)RPGPU_HEADER_SIZE));
+    const uint8_t* src = j.data + S;
+    uint64_t nl = 0, nq = 0;
+    if (!zs_fast_size(src, n, nl, nq)) return 0;
+    const uint64_t lbytes = (nl + 16 + 15) & ~15ull, rcap = nq + 1;
+    const uint64_t need = kZsFastHdr + lbytes + rcap * sizeof(SeqRec);
+    const uint64_t soff =
+        uni64(atomicAdd((unsigned long long*)j.inf_scratch_used, lane() == 0 ? (unsigned long long)need : 0ull));
+    if (soff + need > j.inf_scratch_bytes) return 0;
+    uint8_t* base = j.inf_scratch + soff;
+    ZLane e;
+    e.src = src;
+    e.n = n;
+    e.lits = base + kZsFastHdr;
+    e.recs = (SeqRec*)(base + kZsFastHdr + lbytes);
+    e.lcap = nl;
+    e.rcap = rcap;
+    e.nlit = e.nrec = e.pend = e.mlsum = 0;
+    e.bad = false;
+#ifdef RPGPU_ZSTAMPS
+    e.prof[0] = e.prof[1] = e.prof[2] = e.prof[3] = 0;
+#endif
+    zs::Tabs* T = (zs::Tabs*)(lds + kInfRing);
+    uint64_t total = 0;
+    bool unsure = false;
+    const int rc = zs::payload(e, T, n, total, unsure);
+    if (rc != 0) {
+        if (lane() == 0) {
+            j.dcap[b] = 0;
+            j.slots[b] = 0;
+            j.inf_state[i] = 1;
+            j.inf_off[i] = 0;
+            j.inf_total[i] = 0;
+        }
+        return 1;
+    }
+    if (e.pend) e.match(0, 0);  // the literals after the last match
+    if (unsure || e.bad || e.nlit + e.mlsum != total || total >= (1ull << 31)) return 0;
+    const uint64_t cap = (total + 15) & ~15ull;
+    if (lane() == 0) {
+        ZsFastDesc d{e.nlit, e.nrec, kZsFastHdr, kZsFastHdr + lbytes};
+        *(ZsFastDesc*)base = d;
+        const int32_t rcount = R->record_count;
+        j.dcap[b] = cap;
+        j.slots[b] = ((j.flags & RPGPU_JOB_PARSE) && rcount > 0 && (uint64_t)rcount <= cap) ? (uint64_t)rcount : 0;
+        j.inf_state[i] = kZsFast;
+        j.inf_off[i] = soff;
+        j.inf_total[i] = total;
+    }
+    return kZsFast;
+}
+
 // first pass of zstd member i: the same plan / state rules as gzip's; a
 // payload whose content checksum could not be checked in the slot (it
 // outgrew it) is decoded again by the second pass
 DEV void zstd_first_item(const DeviceJob& j, uint8_t* lds, uint32_t i, uint32_t b, const rpgpu_batch_result* R) {
+    if (zstd_fast_item(j, lds, i, b, R)) return;
     zs::Tabs* T = (zs::Tabs*)(lds + kInfRing);
     InfIn in = inf_batch(j, R);
     uint64_t total = 0, soff = 0;

@@ -125,6 +125,15 @@ struct FramePlan {
     uint32_t csf;           // LZ4F: content size present
 };
 
+// zstd members parsed into records (rp_inflate.hip zstd_fast_item): inf_state
+// kZsFast, inf_off -> a ZsFastDesc in the scratch pool; k_zexec (rp_codec.hip)
+// executes them into their arena slots
+constexpr uint32_t kZsFast = 3;
+constexpr uint32_t kZsFastHdr = 64;  // descriptor bytes before the literal buffer
+struct ZsFastDesc {
+    uint64_t nlit, nrec, lit_off, rec_off;  // literal bytes, records; offsets from the descriptor
+};
+
 // job counters (DeviceJob::counters), zeroed per submit
 constexpr size_t kCounterBytes = 128;
 
@@ -161,7 +170,8 @@ struct DeviceJob {
                                   // [12] long-piece claim cursor, [13] k_validate_decoded claim cursor,
                                   // [14] k_decode_finish claim cursor, [15] k_crc_split claim cursor,
                                   // [16] gzip / zstd members (inf_list), [17] k_members_first / [18] k_members claim cursors,
-                                  // [19] host-decoded members (host_list), [20] k_members_first's second claim cursor
+                                  // [19] host-decoded members (host_list), [20] k_members_first's second claim cursor,
+                                  // [21] k_zexec claim cursor
     uint32_t* decode_list;        // batch_capacity: ordinals of batches to uncompress
     uint32_t* seq_list;           // batch_capacity: decode items decoded whole by one lane
     uint32_t* link_list;          // batch_capacity: decode items whose linked LZ4F blocks one wave decodes in order
@@ -184,7 +194,8 @@ struct DeviceJob {
     const uint64_t* seeds;        // optional chain seeds (index-seeded discovery), per segment ascending
     const uint64_t* seed_off;     // n_segments + 1
     uint32_t* inf_list;           // batch_capacity: ordinals of gzip / zstd batches (k_members_first / k_members)
-    uint32_t* inf_state;          // batch_capacity: 0 decoded into scratch, 1 rejected, 2 decode again (k_inflate)
+    uint32_t* inf_state;          // batch_capacity: 0 decoded into scratch, 1 rejected, 2 decode again (k_inflate),
+                                  // kZsFast parsed into records (k_zexec)
     uint64_t* inf_off;            // batch_capacity: scratch offset of each member's first-pass output
     uint64_t* inf_total;          // batch_capacity: decoded bytes of each member
     uint8_t* inf_scratch;         // first-pass output pool (context scratch)
@@ -227,6 +238,7 @@ hipError_t launch_decode_finish(const DeviceJob& j, hipStream_t s, uint32_t grid
 // scans, then the copy into the arena and the second pass where needed
 hipError_t launch_inflate_plan(const DeviceJob& j, hipStream_t s, uint32_t grid);
 hipError_t launch_inflate(const DeviceJob& j, hipStream_t s, uint32_t grid);
+hipError_t launch_zexec(const DeviceJob& j, hipStream_t s);  // rp_codec.hip
 // one payload, one wave (rpgpu_uncompress); res[0] = rc (0 / -1 / -2), res[1] = out_len
 hipError_t launch_uncompress_one(int codec, const uint8_t* src, uint64_t n, uint8_t* dst, uint64_t cap,
                                  int64_t* res, hipStream_t s);

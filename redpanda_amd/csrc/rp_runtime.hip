@@ -810,6 +810,7 @@ int submit_body(rpgpu_ctx* c, const rpgpu_job* job, hipStream_t s, int stop, Pla
         STAGE("lz_exec", launch_lz_exec(j, s));
         STAGE("decode_finish", launch_decode_finish(j, s, c->cu_count * 8));
         STAGE("inflate", launch_inflate(j, s, c->cu_count * 4));
+        STAGE("zexec", launch_zexec(j, s));
         if (c->hc_n) STAGE("host_scatter", launch_host_scatter(j, (const HostItem*)c->hc_items.p, c->hc_n,
                                                                (const uint8_t*)c->hc_out.p, s));
     }
