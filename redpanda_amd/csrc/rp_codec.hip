@@ -1227,10 +1227,10 @@ __global__ __launch_bounds__(256) void k_decode(DeviceJob j) {
 #define RPGPU_XRING_KIB 16
 #endif
 constexpr uint32_t kXRing = RPGPU_XRING_KIB * 1024u, kXM = kXRing - 1;
-static_assert((kXRing & kXM) == 0 && kXRing >= 8192, "ring: a power of two >= 8 KiB");
+static_assert((kXRing & kXM) == 0 && kXRing >= 16384, "ring: a power of two >= 16 KiB");
 // longer literals / matches run wave-cooperatively (a 64-record batch then
 // writes at most 128 kBig bytes)
-constexpr uint32_t kBig = kXRing >= 32768 ? 128 : kXRing >= 16384 ? 64 : 32;
+constexpr uint32_t kBig = kXRing >= 32768 ? 128 : 64;
 // ring stores are deferred: unflushed output stays below kFlushLag (+ the
 // 1 KiB flush granule + one batch), so most batches issue no global store
 // and the loads they wait on are counted exactly (gfx9's vmcnt also counts
@@ -1247,7 +1247,7 @@ static_assert(kXRing >= kFlushLag + 2048 + 128, "ring too small for xbig's far r
 // single copy) and the short-offset pattern selectors.  (One wave per
 // workgroup left no room for shared tables; 9 rings + 8.5 KiB fit 160 KiB,
 // as many waves per CU as the 10 one-wave workgroups that were resident.)
-constexpr uint32_t kExecWaves = (160u * 1024u - 8704u) / kXRing < 16u ? (160u * 1024u - 8704u) / kXRing : 16u;  // (1024 threads)
+constexpr uint32_t kExecWaves = (160u * 1024u - 8704u) / kXRing;
 constexpr uint32_t kXCrcOff = kExecWaves * kXRing;
 constexpr uint32_t kXPatOff = kXCrcOff + 8192u;
 constexpr uint32_t kXLds = kXPatOff + 512u;

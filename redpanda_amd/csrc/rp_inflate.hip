@@ -41,7 +41,7 @@
         stmt;                                   \
         e.prof[k] += wall_clock64() - t0_;      \
     }
-__device__ unsigned long long g_zst[8];
+__device__ unsigned long long g_zst[16];  // [0..7] the wave decoder, [8..15] the lane parse
 #endif
 #include "rp_zstd_core.h"
 
@@ -1220,10 +1220,49 @@ struct ZLane {
         return v;
     }
     // 8 bytes at pos (pos + 8 <= n: the bit streams read inside the member)
-    DEV uint64_t lb(zs::Bits&, uint64_t pos) {
-        uint64_t v;
-        __builtin_memcpy(&v, (const __attribute__((address_space(1))) uint8_t*)(src + pos), 8);
-        return v;
+    // for bit stream s from its LDS window: kZlWin bytes ending at or just past
+    // the read (the streams move down), loaded by the wave 16 bytes per lane
+    // when a read leaves it; each live stream has its own slot (round robin
+    // over kZlSlots at bits_init, more than the streams live at once: four
+    // literal streams and the sequence stream, or a weight stream)
+    inf_lds_u8* win;
+    uint32_t rr;
+    static constexpr uint32_t kZlWin = 4096, kZlSlots = 8;
+    DEV uint64_t lb(zs::Bits& s, uint64_t pos) {
+        if (s.wbase == zs::kUnknown) {
+            s.wreg = rr++ % kZlSlots;
+            s.wbase = zs::kUnknown - 1;
+        }
+        inf_lds_u8* w = win + s.wreg * kZlWin;
+        if (pos < s.wbase || pos + 8 > s.wbase + kZlWin) {
+            const uint64_t nb = (pos + 8 > kZlWin ? pos + 8 - kZlWin : 0) & ~15ull;
+            const uint32_t l = lane();
+#pragma unroll
+            for (uint32_t k = 0; k < kZlWin / 1024; k++) {
+                const uint64_t o = nb + 1024u * k + 16u * l;
+                uint4 v = make_uint4(0u, 0u, 0u, 0u);
+                if (o + 16 <= n) {
+                    __builtin_memcpy(&v, (const __attribute__((address_space(1))) uint8_t*)(src + o), 16);
+                } else if (o < n) {
+                    uint32_t t[4] = {0u, 0u, 0u, 0u};
+                    for (uint32_t q = 0; q < 16; q++)
+                        if (o + q < n) t[q >> 2] |= (uint32_t)src[o + q] << (8 * (q & 3));
+                    v = make_uint4(t[0], t[1], t[2], t[3]);
+                }
+                __attribute__((address_space(3))) uint32_t* q = (__attribute__((address_space(3))) uint32_t*)(w + 1024u * k + 16u * l);
+                q[0] = v.x;
+                q[1] = v.y;
+                q[2] = v.z;
+                q[3] = v.w;
+            }
+            s.wbase = nb;
+        }
+        const uint32_t o = (uint32_t)(pos - s.wbase), a = o & ~3u, sh = o & 3u;
+        typedef const __attribute__((address_space(3))) uint32_t lds_cu32_t;
+        const uint32_t d0 = *(lds_cu32_t*)(w + a), d1 = *(lds_cu32_t*)(w + a + 4);
+        const uint32_t d2 = a + 8 < kZlWin ? *(lds_cu32_t*)(w + a + 8) : 0u;
+        return (uint64_t)__builtin_amdgcn_alignbyte(d1, d0, sh) |
+               ((uint64_t)__builtin_amdgcn_alignbyte(d2, d1, sh) << 32);
     }
     DEV uint32_t U(uint32_t x) { return x; }
     DEV zs::SeqSym sym(const zs::SeqSym& t) { return t; }
@@ -1257,6 +1296,101 @@ struct ZLane {
     }
     DEV void frame_begin() {}
     DEV int check(uint32_t) { return 2; }  // (never called: zs_fast_size admits no checksummed frame)
+    // eager literals (zs::EagerLits): the block's Huffman literals are already
+    // in the buffer, in consumption order
+    DEV void take(uint64_t k) {
+        nlit += k;
+        pend += k;
+    }
+    DEV uint32_t hbits(const zs::Bits& s, uint32_t hlog) {
+        return (uint32_t)((s.c << (s.used & 63)) >> ((64 - hlog) & 63));
+    }
+    DEV void hstep(zs::Tabs* T, zs::Bits& s, uint32_t& open, bool x2, uint32_t hlog, uint64_t at) {
+        const uint32_t d = T->huf[hbits(s, hlog)];
+        const uint32_t l1 = d >> 8;
+        if (x2) open = (open && open + l1 <= 12) ? 0u : l1;
+        s.used += l1;
+        if (lane() == 0) lits[at] = (uint8_t)d;
+    }
+    // every symbol of the block's streams into the buffer at nlit (stream k's
+    // segment at k * seg): the four streams advance together, their table
+    // lookups issued back to back (one LDS latency per four symbols); each
+    // stream's last symbol (the X2 last-symbol rule) by zs::huf_one
+    DEV void huf_all(zs::Tabs* T, zs::Lits& L, uint32_t hlog) {
+#ifdef RPGPU_ZSTAMPS
+        const uint64_t t0 = wall_clock64();
+#endif
+        huf_all_(T, L, hlog);
+#ifdef RPGPU_ZSTAMPS
+        prof[2] += wall_clock64() - t0;
+#endif
+    }
+    DEV void huf_all_(zs::Tabs* T, zs::Lits& L, uint32_t hlog) {
+        const uint64_t at = nlit;
+        if (at + L.size > lcap) {
+            bad = true;
+            return;
+        }
+        const bool x2 = L.x2;
+        if (L.ns == 1) {
+            const uint32_t c = L.cnt[0];
+            for (uint32_t i = 0; i + 1 < c; i++) {
+                if (L.s[0].used > 64 - hlog) zs::bits_reload(*this, L.s[0]);
+                hstep(T, L.s[0], L.pend[0], x2, hlog, at + i);
+            }
+            if (c) {
+                const uint32_t v = zs::huf_one(*this, T, L.s[0], L.pend[0], 1, x2, hlog);
+                if (lane() == 0) lits[at + c - 1] = (uint8_t)v;
+            }
+        } else {
+            const uint32_t seg = L.seg, c3 = L.cnt[3];
+            for (uint32_t i = 0; i + 1 < seg; i++) {
+                const bool s3 = i + 1 < c3;
+                if (L.s[0].used > 64 - hlog) zs::bits_reload(*this, L.s[0]);
+                if (L.s[1].used > 64 - hlog) zs::bits_reload(*this, L.s[1]);
+                if (L.s[2].used > 64 - hlog) zs::bits_reload(*this, L.s[2]);
+                if (s3 && L.s[3].used > 64 - hlog) zs::bits_reload(*this, L.s[3]);
+                const uint32_t d0 = T->huf[hbits(L.s[0], hlog)], d1 = T->huf[hbits(L.s[1], hlog)],
+                               d2 = T->huf[hbits(L.s[2], hlog)], d3 = s3 ? (uint32_t)T->huf[hbits(L.s[3], hlog)] : 0u;
+                const uint32_t l0 = d0 >> 8, l1 = d1 >> 8, l2 = d2 >> 8, l3 = d3 >> 8;
+                if (x2) {
+                    L.pend[0] = (L.pend[0] && L.pend[0] + l0 <= 12) ? 0u : l0;
+                    L.pend[1] = (L.pend[1] && L.pend[1] + l1 <= 12) ? 0u : l1;
+                    L.pend[2] = (L.pend[2] && L.pend[2] + l2 <= 12) ? 0u : l2;
+                    if (s3) L.pend[3] = (L.pend[3] && L.pend[3] + l3 <= 12) ? 0u : l3;
+                }
+                L.s[0].used += l0;
+                L.s[1].used += l1;
+                L.s[2].used += l2;
+                if (s3) L.s[3].used += l3;
+                if (lane() == 0) {
+                    lits[at + i] = (uint8_t)d0;
+                    lits[at + seg + i] = (uint8_t)d1;
+                    lits[at + 2 * seg + i] = (uint8_t)d2;
+                    if (s3) lits[at + 3 * seg + i] = (uint8_t)d3;
+                }
+            }
+            // the last symbol of streams 0..2 and whatever stream 3 has left
+            // (c3 <= seg: one symbol at most)
+            for (uint32_t k = 0; k < 3; k++) {
+                const uint32_t v = zs::huf_one(*this, T, L.s[k], L.pend[k], 1, x2, hlog);
+                if (lane() == 0) lits[at + k * seg + seg - 1] = (uint8_t)v;
+            }
+            if (c3) {
+                const uint32_t v = zs::huf_one(*this, T, L.s[3], L.pend[3], 1, x2, hlog);
+                if (lane() == 0) lits[at + 3 * seg + c3 - 1] = (uint8_t)v;
+            }
+        }
+        L.dec[0] = L.cnt[0];
+        L.dec[1] = L.cnt[1];
+        L.dec[2] = L.cnt[2];
+        L.dec[3] = L.cnt[3];
+    }
+};
+static_assert(ZLane::kZlWin * ZLane::kZlSlots <= kInfRing, "ZLane's stream windows use the ring's LDS");
+template <>
+struct zs::EagerLits<ZLane> {
+    static constexpr bool value = true;
 };
 
 // The fast path's header walk: every frame a zstd frame without a content
@@ -1348,7 +1482,7 @@ DEV bool zs_fast_size(const uint8_t* src, uint64_t n, uint64_t& nlit, uint64_t& 
 // the fast path of zstd member i: 0 not taken (the wave decoder runs), else
 // the state set (1 rejected, kZsFast parsed)
 DEV uint32_t zstd_fast_item(const DeviceJob& j, uint8_t* lds, uint32_t i, uint32_t b, const rpgpu_batch_result* R) {
-    if (!j.inf_scratch) return 0;
+    if (!j.inf_scratch || !j.zs_fast) return 0;
     const uint64_t S = uni64(j.seg_off[uni32(R->segment)]) + uni64(R->file_pos) + RPGPU_HEADER_SIZE;
     const uint64_t n = (uint64_t)uni32((uint32_t)(R->size_bytes - (int32_t)RPGPU_HEADER_SIZE));
     const uint8_t* src = j.data + S;
@@ -1369,13 +1503,28 @@ DEV uint32_t zstd_fast_item(const DeviceJob& j, uint8_t* lds, uint32_t i, uint32
     e.rcap = rcap;
     e.nlit = e.nrec = e.pend = e.mlsum = 0;
     e.bad = false;
+    e.win = (inf_lds_u8*)lds;  // the ring's LDS (the wave decoder's, unused here)
+    e.rr = 0;
 #ifdef RPGPU_ZSTAMPS
     e.prof[0] = e.prof[1] = e.prof[2] = e.prof[3] = 0;
 #endif
     zs::Tabs* T = (zs::Tabs*)(lds + kInfRing);
     uint64_t total = 0;
     bool unsure = false;
+#ifdef RPGPU_ZSTAMPS
+    const uint64_t t0 = wall_clock64();
+#endif
     const int rc = zs::payload(e, T, n, total, unsure);
+#ifdef RPGPU_ZSTAMPS
+    if (lane() == 0) {
+        for (int k = 0; k < 4; k++) atomicAdd(&g_zst[8 + k], (unsigned long long)e.prof[k]);
+        atomicAdd(&g_zst[12], (unsigned long long)(wall_clock64() - t0));
+        atomicAdd(&g_zst[13], 1ull);
+        atomicAdd(&g_zst[14], (unsigned long long)(e.nrec + (e.nlit << 32)));
+        atomicMax(&g_zst[15], (unsigned long long)(wall_clock64() - t0));
+    }
+#endif
+    if (e.bad) return 0;  // (the header walk's sizes should always hold: the wave decoder then rules)
     if (rc != 0) {
         if (lane() == 0) {
             j.dcap[b] = 0;
@@ -1535,7 +1684,11 @@ __global__ void k_zstamps(int print) {
         printf("RPGPU_ZSTAMPS payloads=%llu out=%llu wall_ms(sum) lits=%.1f match=%.1f ends=%.1f blocks=%.1f total=%.1f max_payload_ms=%.2f\n",
                g_zst[5], g_zst[6], g_zst[0] * 1e-5, g_zst[1] * 1e-5, g_zst[2] * 1e-5, g_zst[3] * 1e-5,
                g_zst[4] * 1e-5, g_zst[7] * 1e-5);
-    for (int k = 0; k < 8; k++) g_zst[k] = 0;
+    if (print)
+        printf("RPGPU_ZSTAMPS lane-parse payloads=%llu recs=%llu lits=%llu wall_ms(sum) lits=%.1f match=%.1f ends=%.1f blocks=%.1f total=%.1f max_payload_ms=%.2f\n",
+               g_zst[13], g_zst[14] & 0xFFFFFFFFull, g_zst[14] >> 32, g_zst[8] * 1e-5, g_zst[9] * 1e-5,
+               g_zst[10] * 1e-5, g_zst[11] * 1e-5, g_zst[12] * 1e-5, g_zst[15] * 1e-5);
+    for (int k = 0; k < 16; k++) g_zst[k] = 0;
 }
 #endif
 

@@ -201,6 +201,7 @@ struct DeviceJob {
     uint8_t* inf_scratch;         // first-pass output pool (context scratch)
     uint64_t inf_scratch_bytes;
     uint64_t* inf_scratch_used;   // bump allocator of the pool (zeroed per job)
+    uint32_t zs_fast;             // zstd members may take the parse / execute split (kZsFast)
     uint32_t* host_list;          // batch_capacity: ordinals of host-decoded (zstd) batches (RPGPU_JOB_HOST_CODECS)
 };
 

@@ -740,6 +740,9 @@ int submit_body(rpgpu_ctx* c, const rpgpu_job* job, hipStream_t s, int stop, Pla
             j.inf_scratch_bytes = std::min<size_t>(c->gz_pool_bytes, want);
         }
     }
+    // RPGPU_ZS_FAST=0 (diagnostic build): every zstd member through the wave decoder (A/B)
+    static const uint32_t zs_fast = [] { const char* e = diag_env("RPGPU_ZS_FAST"); return e && *e == '0' ? 0u : 1u; }();
+    j.zs_fast = zs_fast;
     j.host_list = (uint32_t*)(ws + o_hlist);
     c->hc_n = 0;
     j.blocks = (BlockItem*)(ws + o_blocks);

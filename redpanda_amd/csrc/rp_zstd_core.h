@@ -516,30 +516,45 @@ ZS_FN bool huf_select_x2(uint32_t dsize, uint64_t csize) {
 // decoded values and the end check do not depend on when libzstd refills),
 // and always before a stream's last symbol (whose X2 clamp does).
 template <class E>
+ZS_FN uint32_t huf_one(E& e, Tabs* T, Bits& s, uint32_t& open, uint32_t left, bool x2, uint32_t hlog) {
+    if (left == 1 || s.used > 64 - hlog) bits_reload(e, s);
+    const uint32_t v = e.U((uint32_t)((s.c << (s.used & 63)) >> ((64 - hlog) & 63)));
+    const uint32_t d = e.U(T->huf[v]);
+    const uint32_t l1 = d >> 8;
+    if (x2) {
+        const bool paired = open && open + l1 <= 12;
+        if (left == 1 && !paired) {
+            const uint32_t w = e.U((uint32_t)((s.c << ((s.used + l1) & 63)) >> ((64 - hlog) & 63)));
+            const uint32_t l2 = e.U(T->huf[w]) >> 8;
+            if (l1 + l2 <= 12) {  // a double entry for the lone last symbol
+                if (s.used < 64) s.used = s.used + l1 + l2 > 64 ? 64u : s.used + l1 + l2;
+                return d & 0xFFu;
+            }
+        }
+        open = paired ? 0u : l1;
+    }
+    s.used += l1;
+    return d & 0xFFu;
+}
+template <class E>
 ZS_FN void huf_run(E& e, Tabs* T, Bits& s, uint32_t& open, uint32_t left, uint32_t n, bool x2, uint32_t hlog,
                    bool emit) {
     for (uint32_t i = 0; i < n; i++, left--) {
-        if (left == 1 || s.used > 64 - hlog) bits_reload(e, s);
-        const uint32_t v = e.U((uint32_t)((s.c << (s.used & 63)) >> ((64 - hlog) & 63)));
-        const uint32_t d = e.U(T->huf[v]);
-        const uint32_t l1 = d >> 8;
-        if (x2) {
-            const bool paired = open && open + l1 <= 12;
-            if (left == 1 && !paired) {
-                const uint32_t w = e.U((uint32_t)((s.c << ((s.used + l1) & 63)) >> ((64 - hlog) & 63)));
-                const uint32_t l2 = e.U(T->huf[w]) >> 8;
-                if (l1 + l2 <= 12) {  // a double entry for the lone last symbol
-                    if (s.used < 64) s.used = s.used + l1 + l2 > 64 ? 64u : s.used + l1 + l2;
-                    if (emit) e.lit(d & 0xFFu);
-                    continue;
-                }
-            }
-            open = paired ? 0u : l1;
-        }
-        s.used += l1;
-        if (emit) e.lit(d & 0xFFu);
+        const uint32_t sym = huf_one(e, T, s, open, left, x2, hlog);
+        if (emit) e.lit(sym);
     }
 }
+
+// An environment that keeps literals in a buffer of its own may decode a
+// block's Huffman literals eagerly, all streams at once (E::huf_all, as
+// HUF_decompress4X interleaves them); lits_emit then only takes them.  The
+// symbols, and the stream states lits_finish checks, are those of the lazy
+// consumption-order decode (no check happens between two symbols).
+template <class E>
+struct EagerLits {
+    static constexpr bool value = false;
+};
+
 // stream K (a constant: the per-stream state stays in registers on the device)
 #define ZS_RUN(K, N, EMIT) huf_run(e, T, L.s[K], L.pend[K], L.cnt[K] - L.dec[K], N, L.x2, hlog, EMIT)
 
@@ -550,6 +565,9 @@ ZS_FN void lits_emit(E& e, Tabs* T, Lits& L, uint32_t k, uint32_t hlog) {
         L.used += k;
     } else if (L.kind == 1) {
         e.fill(L.rle, k);
+        L.used += k;
+    } else if constexpr (EagerLits<E>::value) {
+        e.take(k);
         L.used += k;
     } else {
         while (k) {
@@ -716,6 +734,7 @@ ZS_FN int64_t block(E& e, Tabs* T, Frame& F, uint64_t bp, uint64_t bn, uint64_t 
         }
         F.lit_ok = true;
         lcons = lh + lcs;
+        if constexpr (EagerLits<E>::value) e.huf_all(T, L, F.hlog);
     }
     // sequences section header
     uint64_t sp = bp + lcons;

@@ -66,7 +66,48 @@ struct HostEnv {
     int check(uint32_t v) { return (uint32_t)xxh64(out.data() + fstart, out.size() - fstart) == v ? 1 : 0; }
 };
 
+// Eager literals (rp::zs::EagerLits, as the device's lane parser decodes
+// them): every Huffman literal of a block decoded before its sequences, taken
+// from a per-block buffer in consumption order
+struct EagerHostEnv : HostEnv {
+    std::vector<uint8_t> blk;
+    size_t took = 0;
+    void take(uint64_t k) {
+        out.insert(out.end(), blk.begin() + took, blk.begin() + took + k);
+        took += k;
+    }
+    void huf_all(rp::zs::Tabs* T, rp::zs::Lits& L, uint32_t hlog) {
+        blk.assign(L.size, 0);
+        took = 0;
+        for (uint32_t k = 0; k < L.ns; k++) {
+            for (uint32_t i = 0; i < L.cnt[k]; i++)
+                blk[(size_t)k * L.seg + i] =
+                    (uint8_t)rp::zs::huf_one(*this, T, L.s[k], L.pend[k], L.cnt[k] - i, L.x2, hlog);
+            L.dec[k] = L.cnt[k];
+        }
+    }
+};
+
 }  // namespace
+
+template <>
+struct rp::zs::EagerLits<EagerHostEnv> {
+    static constexpr bool value = true;
+};
+
+extern "C" int zs_host_decode_eager(const uint8_t* src, uint64_t n, uint8_t* dst, uint64_t cap, uint64_t* total) {
+    static rp::zs::Tabs T;
+    EagerHostEnv e;
+    e.src = src;
+    e.n = n;
+    uint64_t t = 0;
+    bool unsure = false;
+    const int rc = n == 0 ? -1 : rp::zs::payload(e, &T, n, t, unsure);
+    *total = rc == 0 ? t : 0;
+    if (rc == 0 && t > e.out.size()) return -9;
+    if (rc == 0) memcpy(dst, e.out.data(), t < cap ? t : cap);
+    return rc;
+}
 
 extern "C" int zs_host_decode(const uint8_t* src, uint64_t n, uint8_t* dst, uint64_t cap, uint64_t* total) {
     static rp::zs::Tabs T;

@@ -18,18 +18,21 @@ from tests import zstd_corpus as Z
 HERE = os.path.dirname(os.path.abspath(__file__))
 
 
-def load_host(path: str):
+def load_host(path: str, eager: bool = False):
     """decode(payload) -> bytes or None (rejected) through the host build of
-    rp_zstd_core.h (redpanda_amd.build.build_zstd_host)."""
+    rp_zstd_core.h (redpanda_amd.build.build_zstd_host); eager: with every
+    block's Huffman literals decoded before its sequences (zs::EagerLits, the
+    device lane parser's order)."""
     L = C.CDLL(path)
-    L.zs_host_decode.argtypes = [C.c_char_p, C.c_uint64, C.c_void_p, C.c_uint64, C.POINTER(C.c_uint64)]
+    fn = L.zs_host_decode_eager if eager else L.zs_host_decode
+    fn.argtypes = [C.c_char_p, C.c_uint64, C.c_void_p, C.c_uint64, C.POINTER(C.c_uint64)]
     L.zs_host_xxh64.argtypes = [C.c_char_p, C.c_uint64]
     L.zs_host_xxh64.restype = C.c_uint64
 
     def decode(b: bytes, cap: int = 1 << 24):
         dst = C.create_string_buffer(cap)
         t = C.c_uint64(0)
-        rc = L.zs_host_decode(b, len(b), dst, cap, C.byref(t))
+        rc = fn(b, len(b), dst, cap, C.byref(t))
         assert rc in (0, -1), rc
         return dst.raw[: t.value] if rc == 0 else None
     decode.xxh64 = lambda b: L.zs_host_xxh64(b, len(b))
@@ -118,3 +121,18 @@ def test_ring_mode_far_matches(host):
         assert got is None and ref is not None, f[:16].hex()
         rejected += 1
     assert same >= 40 and rejected >= 40, (same, rejected)
+
+
+@pytest.mark.parametrize("seed", [4, 5])
+def test_eager_literals_match_libzstd_loop(seed):
+    """zs::EagerLits (the device lane parser decodes every Huffman literal of a
+    block before its sequences): the same accept / reject and bytes as
+    libzstd's loop on valid frames and their mutations."""
+    from redpanda_amd import build as B
+    eager = load_host(B.build_zstd_host(), eager=True)
+    rng = random.Random(seed)
+    frames = Z.random_frames(rng, 40)
+    for data, f in frames:
+        assert eager(f) == Z.ref_decode(f)
+    bad = [c[:24].hex() for c in Z.mutations(rng, frames) if eager(c) != Z.ref_decode(c)]
+    assert not bad, (len(bad), bad[:4])
