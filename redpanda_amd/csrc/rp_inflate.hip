@@ -1235,7 +1235,8 @@ struct ZLane {
         }
         inf_lds_u8* w = win + s.wreg * kZlWin;
         if (pos < s.wbase || pos + 8 > s.wbase + kZlWin) {
-            const uint64_t nb = (pos + 8 > kZlWin ? pos + 8 - kZlWin : 0) & ~15ull;
+            // nb <= pos and nb + kZlWin >= pos + 8 (16-byte aligned start)
+            const uint64_t nb = (pos + 8 + 15 > kZlWin ? pos + 8 + 15 - kZlWin : 0) & ~15ull;
             const uint32_t l = lane();
 #pragma unroll
             for (uint32_t k = 0; k < kZlWin / 1024; k++) {
@@ -1273,9 +1274,19 @@ struct ZLane {
         pend++;
     }
     DEV void raw(uint64_t pos, uint64_t k) {
-        if (nlit + k > lcap) bad = true;
-        else
-            for (uint64_t c = lane(); c < k; c += 64) lits[nlit + c] = src[pos + c];
+        typedef __attribute__((address_space(1))) uint8_t g8;
+        if (nlit + k > lcap) {
+            bad = true;
+        } else {
+            // 16 bytes per lane, 1 KiB per step (any alignment); the tail bytewise
+            const uint64_t body = k & ~1023ull;
+            for (uint64_t c = 16u * lane(); c < body; c += 1024) {
+                uint4 v;
+                __builtin_memcpy(&v, (const g8*)(src + pos + c), 16);
+                __builtin_memcpy((g8*)(lits + nlit + c), &v, 16);
+            }
+            for (uint64_t c = body + lane(); c < k; c += 64) lits[nlit + c] = src[pos + c];
+        }
         nlit += k;
         pend += k;
     }
