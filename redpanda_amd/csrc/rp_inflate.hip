@@ -1202,6 +1202,35 @@ DEV uint64_t zs_guess(InfIn& in) {
 // decoder would); one it accepts must deliver exactly the bytes its records
 // describe (state 3); anything else is decoded by ZDev as before.
 // ---------------------------------------------------------------------------
+// a ZLane stream window: the 4 KiB of the member ending at or just past the
+// 8-byte read at pos, 16 bytes per lane; returns the window start (not
+// inlined: a refill is rare, and its code kept out of the literal loop)
+__device__ __noinline__ uint64_t zl_fill(const uint8_t* src, uint64_t n, inf_lds_u8* w, uint64_t pos) {
+    constexpr uint32_t kWin = 4096;
+    // nb <= pos and nb + kWin >= pos + 8 (16-byte aligned start)
+    const uint64_t nb = (pos + 8 + 15 > kWin ? pos + 8 + 15 - kWin : 0) & ~15ull;
+    const uint32_t l = lane();
+#pragma unroll
+    for (uint32_t k = 0; k < kWin / 1024; k++) {
+        const uint64_t o = nb + 1024u * k + 16u * l;
+        uint4 v = make_uint4(0u, 0u, 0u, 0u);
+        if (o + 16 <= n) {
+            __builtin_memcpy(&v, (const __attribute__((address_space(1))) uint8_t*)(src + o), 16);
+        } else if (o < n) {
+            uint32_t t[4] = {0u, 0u, 0u, 0u};
+            for (uint32_t q = 0; q < 16; q++)
+                if (o + q < n) t[q >> 2] |= (uint32_t)src[o + q] << (8 * (q & 3));
+            v = make_uint4(t[0], t[1], t[2], t[3]);
+        }
+        __attribute__((address_space(3))) uint32_t* q = (__attribute__((address_space(3))) uint32_t*)(w + 1024u * k + 16u * l);
+        q[0] = v.x;
+        q[1] = v.y;
+        q[2] = v.z;
+        q[3] = v.w;
+    }
+    return nb;
+}
+
 struct ZLane {
     const uint8_t* src;
     uint64_t n;
@@ -1234,30 +1263,7 @@ struct ZLane {
             s.wbase = zs::kUnknown - 1;
         }
         inf_lds_u8* w = win + s.wreg * kZlWin;
-        if (pos < s.wbase || pos + 8 > s.wbase + kZlWin) {
-            // nb <= pos and nb + kZlWin >= pos + 8 (16-byte aligned start)
-            const uint64_t nb = (pos + 8 + 15 > kZlWin ? pos + 8 + 15 - kZlWin : 0) & ~15ull;
-            const uint32_t l = lane();
-#pragma unroll
-            for (uint32_t k = 0; k < kZlWin / 1024; k++) {
-                const uint64_t o = nb + 1024u * k + 16u * l;
-                uint4 v = make_uint4(0u, 0u, 0u, 0u);
-                if (o + 16 <= n) {
-                    __builtin_memcpy(&v, (const __attribute__((address_space(1))) uint8_t*)(src + o), 16);
-                } else if (o < n) {
-                    uint32_t t[4] = {0u, 0u, 0u, 0u};
-                    for (uint32_t q = 0; q < 16; q++)
-                        if (o + q < n) t[q >> 2] |= (uint32_t)src[o + q] << (8 * (q & 3));
-                    v = make_uint4(t[0], t[1], t[2], t[3]);
-                }
-                __attribute__((address_space(3))) uint32_t* q = (__attribute__((address_space(3))) uint32_t*)(w + 1024u * k + 16u * l);
-                q[0] = v.x;
-                q[1] = v.y;
-                q[2] = v.z;
-                q[3] = v.w;
-            }
-            s.wbase = nb;
-        }
+        if (pos < s.wbase || pos + 8 > s.wbase + kZlWin) s.wbase = zl_fill(src, n, w, pos);
         const uint32_t o = (uint32_t)(pos - s.wbase), a = o & ~3u, sh = o & 3u;
         typedef const __attribute__((address_space(3))) uint32_t lds_cu32_t;
         const uint32_t d0 = *(lds_cu32_t*)(w + a), d1 = *(lds_cu32_t*)(w + a + 4);
@@ -1383,6 +1389,7 @@ struct ZLane {
             }
             // the last symbol of streams 0..2 and whatever stream 3 has left
             // (c3 <= seg: one symbol at most)
+#pragma unroll
             for (uint32_t k = 0; k < 3; k++) {
                 const uint32_t v = zs::huf_one(*this, T, L.s[k], L.pend[k], 1, x2, hlog);
                 if (lane() == 0) lits[at + k * seg + seg - 1] = (uint8_t)v;
@@ -1566,7 +1573,6 @@ DEV uint32_t zstd_fast_item(const DeviceJob& j, uint8_t* lds, uint32_t i, uint32
 // payload whose content checksum could not be checked in the slot (it
 // outgrew it) is decoded again by the second pass
 DEV void zstd_first_item(const DeviceJob& j, uint8_t* lds, uint32_t i, uint32_t b, const rpgpu_batch_result* R) {
-    if (zstd_fast_item(j, lds, i, b, R)) return;
     zs::Tabs* T = (zs::Tabs*)(lds + kInfRing);
     InfIn in = inf_batch(j, R);
     uint64_t total = 0, soff = 0;
@@ -1653,11 +1659,50 @@ __global__ __launch_bounds__(64) void k_members_first(DeviceJob j) {
                 if (!tab) inf_load_tab(T->crc_tab);
                 tab = true;
                 gzip_first_item(j, lds, T, W, i, b, R);
-            } else {
+            } else if (!j.zs_split) {
                 tab = false;
                 zstd_first_item(j, lds, i, b, R);
             }
         }
+    }
+}
+
+// j.zs_split: the zstd members' first pass leaves k_members_first.  k_zparse
+// (on a side stream, beside k_members_first's gzip members) runs the lane
+// parser on each, largest first as above, and marks the members it does not
+// take kZsPending; k_zfallback (after the join, before the slot scans) runs
+// the wave decoder on those.  (Separate kernels: the lane parser's VGPR state
+// and the wave decoder's SGPR state in one register allocation spilled.)
+constexpr uint32_t kZsPending = 4;
+
+__global__ __launch_bounds__(64) void k_zparse(DeviceJob j) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    const uint32_t count = j.counters[16];
+    for (uint32_t phase = 0; phase < 2; phase++) {
+        for (;;) {
+            const uint32_t i = wave_fetch_add(&j.counters[phase ? 23 : 22], 1u);
+            if (i >= count) break;
+            const uint32_t b = uni32(j.inf_list[i]);
+            const rpgpu_batch_result* R = &j.batches[b];
+            if ((uni32((uint32_t)(uint16_t)R->attrs) & 7u) == RPGPU_CODEC_GZIP) continue;
+            const bool big = uni32((uint32_t)R->size_bytes) >= (128u << 10);
+            if (big != (phase == 0)) continue;
+            if (!zstd_fast_item(j, lds, i, b, R) && lane() == 0) j.inf_state[i] = kZsPending;
+        }
+    }
+}
+
+__global__ __launch_bounds__(64) void k_zfallback(DeviceJob j) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    const uint32_t count = j.counters[16];
+    for (;;) {
+        const uint32_t i = wave_fetch_add(&j.counters[26], 1u);
+        if (i >= count) break;
+        const uint32_t b = uni32(j.inf_list[i]);
+        const rpgpu_batch_result* R = &j.batches[b];
+        if ((uni32((uint32_t)(uint16_t)R->attrs) & 7u) == RPGPU_CODEC_GZIP) continue;
+        if (uni32(j.inf_state[i]) != kZsPending) continue;
+        zstd_first_item(j, lds, i, b, R);
     }
 }
 
@@ -1703,19 +1748,43 @@ __global__ void k_zstamps(int print) {
 }
 #endif
 
+hipError_t launch_zstamps(hipStream_t s, int print) {
+#ifdef RPGPU_ZSTAMPS
+    hipLaunchKernelGGL(k_zstamps, dim3(1), dim3(1), 0, s, print);
+#else
+    (void)s;
+    (void)print;
+#endif
+    return hipGetLastError();
+}
+
 hipError_t launch_inflate_plan(const DeviceJob& j, hipStream_t s, uint32_t grid) {
     static bool attr = false;
     if (!attr) {
         (void)hipFuncSetAttribute((const void*)k_members_first, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kMemLds);
         attr = true;
     }
-#ifdef RPGPU_ZSTAMPS
-    hipLaunchKernelGGL(k_zstamps, dim3(1), dim3(1), 0, s, 0);
-#endif
     hipLaunchKernelGGL(k_members_first, dim3(grid), dim3(64), kMemLds, s, j);
-#ifdef RPGPU_ZSTAMPS
-    hipLaunchKernelGGL(k_zstamps, dim3(1), dim3(1), 0, s, 1);
-#endif
+    return hipGetLastError();
+}
+
+hipError_t launch_zparse(const DeviceJob& j, hipStream_t s, uint32_t grid) {
+    static bool attr = false;
+    if (!attr) {
+        (void)hipFuncSetAttribute((const void*)k_zparse, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kMemLds);
+        attr = true;
+    }
+    hipLaunchKernelGGL(k_zparse, dim3(grid), dim3(64), kMemLds, s, j);
+    return hipGetLastError();
+}
+
+hipError_t launch_zfallback(const DeviceJob& j, hipStream_t s, uint32_t grid) {
+    static bool attr = false;
+    if (!attr) {
+        (void)hipFuncSetAttribute((const void*)k_zfallback, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kMemLds);
+        attr = true;
+    }
+    hipLaunchKernelGGL(k_zfallback, dim3(grid), dim3(64), kMemLds, s, j);
     return hipGetLastError();
 }
 

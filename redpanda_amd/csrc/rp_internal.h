@@ -171,7 +171,7 @@ struct DeviceJob {
                                   // [14] k_decode_finish claim cursor, [15] k_crc_split claim cursor,
                                   // [16] gzip / zstd members (inf_list), [17] k_members_first / [18] k_members claim cursors,
                                   // [19] host-decoded members (host_list), [20] k_members_first's second claim cursor,
-                                  // [21] k_zexec claim cursor
+                                  // [21] k_zexec claim cursor, [22] / [23] k_zparse claim cursors, [26] k_zfallback claim cursor
     uint32_t* decode_list;        // batch_capacity: ordinals of batches to uncompress
     uint32_t* seq_list;           // batch_capacity: decode items decoded whole by one lane
     uint32_t* link_list;          // batch_capacity: decode items whose linked LZ4F blocks one wave decodes in order
@@ -195,13 +195,14 @@ struct DeviceJob {
     const uint64_t* seed_off;     // n_segments + 1
     uint32_t* inf_list;           // batch_capacity: ordinals of gzip / zstd batches (k_members_first / k_members)
     uint32_t* inf_state;          // batch_capacity: 0 decoded into scratch, 1 rejected, 2 decode again (k_inflate),
-                                  // kZsFast parsed into records (k_zexec)
+                                  // kZsFast parsed into records (k_zexec), 4 left by k_zparse to k_zfallback
     uint64_t* inf_off;            // batch_capacity: scratch offset of each member's first-pass output
     uint64_t* inf_total;          // batch_capacity: decoded bytes of each member
     uint8_t* inf_scratch;         // first-pass output pool (context scratch)
     uint64_t inf_scratch_bytes;
     uint64_t* inf_scratch_used;   // bump allocator of the pool (zeroed per job)
     uint32_t zs_fast;             // zstd members may take the parse / execute split (kZsFast)
+    uint32_t zs_split;            // k_zparse (side stream) owns the zstd members' first pass
     uint32_t* host_list;          // batch_capacity: ordinals of host-decoded (zstd) batches (RPGPU_JOB_HOST_CODECS)
 };
 
@@ -239,6 +240,9 @@ hipError_t launch_decode_finish(const DeviceJob& j, hipStream_t s, uint32_t grid
 // scans, then the copy into the arena and the second pass where needed
 hipError_t launch_inflate_plan(const DeviceJob& j, hipStream_t s, uint32_t grid);
 hipError_t launch_inflate(const DeviceJob& j, hipStream_t s, uint32_t grid);
+hipError_t launch_zparse(const DeviceJob& j, hipStream_t s, uint32_t grid);
+hipError_t launch_zfallback(const DeviceJob& j, hipStream_t s, uint32_t grid);
+hipError_t launch_zstamps(hipStream_t s, int print);  // RPGPU_ZSTAMPS builds: reset / print the decoder stamps
 hipError_t launch_zexec(const DeviceJob& j, hipStream_t s);  // rp_codec.hip
 // one payload, one wave (rpgpu_uncompress); res[0] = rc (0 / -1 / -2), res[1] = out_len
 hipError_t launch_uncompress_one(int codec, const uint8_t* src, uint64_t n, uint8_t* dst, uint64_t cap,

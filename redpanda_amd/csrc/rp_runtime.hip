@@ -151,6 +151,11 @@ struct rpgpu_ctx {
     // bytes in, per-batch results out), used alternately so the H2D copy of
     // group g + 1 runs while group g validates
     hipStream_t copy = nullptr;
+    // the zstd members' first pass (k_zparse) runs on a side stream beside
+    // k_members_first's gzip members: forked after k_emit, joined before the
+    // slot scans
+    hipStream_t side = nullptr;
+    hipEvent_t fork_ev = nullptr, join_ev = nullptr;
     struct HostSlot {
         uint8_t* d_data = nullptr;
         uint64_t data_bytes = 0;
@@ -307,6 +312,9 @@ int rpgpu_destroy(rpgpu_ctx* c) {
     for (auto* g : {&c->hc_items, &c->hc_items_h, &c->hc_in, &c->hc_in_h, &c->hc_out, &c->hc_out_h, &c->hc_small})
         if (g->p) (void)(g->pinned ? hipHostFree(g->p) : hipFree(g->p));
     if (c->ws_ev) { (void)hipEventSynchronize(c->ws_ev); (void)hipEventDestroy(c->ws_ev); }
+    if (c->side) { (void)hipStreamSynchronize(c->side); (void)hipStreamDestroy(c->side); }
+    if (c->fork_ev) (void)hipEventDestroy(c->fork_ev);
+    if (c->join_ev) (void)hipEventDestroy(c->join_ev);
     for (auto& set : c->ev_sets)
         for (auto& e : set) hipEventDestroy(e);
     if (c->stream) hipStreamDestroy(c->stream);
@@ -743,6 +751,7 @@ int submit_body(rpgpu_ctx* c, const rpgpu_job* job, hipStream_t s, int stop, Pla
     // RPGPU_ZS_FAST=0 (diagnostic build): every zstd member through the wave decoder (A/B)
     static const uint32_t zs_fast = [] { const char* e = diag_env("RPGPU_ZS_FAST"); return e && *e == '0' ? 0u : 1u; }();
     j.zs_fast = zs_fast;
+    j.zs_split = 0;
     j.host_list = (uint32_t*)(ws + o_hlist);
     c->hc_n = 0;
     j.blocks = (BlockItem*)(ws + o_blocks);
@@ -793,7 +802,28 @@ int submit_body(rpgpu_ctx* c, const rpgpu_job* job, hipStream_t s, int stop, Pla
     STAGE("emit", launch_emit(j, s));
     // gzip members: the first pass (their arena bytes, index slots and, when
     // they fit the pool, their output) before the scans
-    if (decode_job) STAGE("inflate_plan", launch_inflate_plan(j, s, c->cu_count * 4));
+    if (decode_job) {
+        // zstd members on the side stream when the lane parser can run (it
+        // needs the scratch pool), gzip members (and, otherwise, zstd ones) here
+        const bool split = j.inf_scratch && j.zs_fast;
+        STAGE("zstamps", launch_zstamps(s, 0));
+        if (split) {
+            if (!c->side) HIPCHK(c, hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking));
+            if (!c->fork_ev) HIPCHK(c, hipEventCreateWithFlags(&c->fork_ev, hipEventDisableTiming));
+            if (!c->join_ev) HIPCHK(c, hipEventCreateWithFlags(&c->join_ev, hipEventDisableTiming));
+            j.zs_split = 1;
+            HIPCHK(c, hipEventRecord(c->fork_ev, s));
+            HIPCHK(c, hipStreamWaitEvent(c->side, c->fork_ev, 0));
+            STAGE("zparse", launch_zparse(j, c->side, c->cu_count * 4));
+            HIPCHK(c, hipEventRecord(c->join_ev, c->side));
+        }
+        STAGE("inflate_plan", launch_inflate_plan(j, s, c->cu_count * 4));
+        if (split) {
+            HIPCHK(c, hipStreamWaitEvent(s, c->join_ev, 0));
+            STAGE("zfallback", launch_zfallback(j, s, c->cu_count * 4));
+        }
+        STAGE("zstamps", launch_zstamps(s, 1));
+    }
     // zstd members (RPGPU_JOB_HOST_CODECS): decoded on the host now, sized
     // before the scans like every other payload
     if (host_job)

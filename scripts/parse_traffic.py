@@ -45,15 +45,18 @@ def alg_bytes(w, st):
     """Algorithmic bytes per submit, per kernel (None = no fixed figure)."""
     if not st:
         return {}
+    sys.path.insert(0, root)
+    from redpanda_amd import abi
+    idx = abi.RECORD_INDEX.itemsize  # index entry bytes the walks write
     a = {
         # CRC of every stored payload, 128 B per batch result (read + write)
         "k_validate": st["stored_payload"] + 128 * st["batches"],
         "k_lz_walk": st["compressed_in"],
         "k_lz_exec": st["decoded"],
-        "k_validate_decoded": st["decoded"] + 48 * st["records"],
+        "k_validate_decoded": st["decoded"] + idx * st["records"],
     }
     if w == "c1":
-        a["k_walk"] = 48 * st["records"] + 128 * st["batches"]
+        a["k_walk"] = idx * st["records"] + 128 * st["batches"]
     return a
 
 
