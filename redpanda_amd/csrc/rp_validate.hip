@@ -691,13 +691,6 @@ DEV void note_bad(const DeviceJob& j, uint32_t seg, uint64_t b) {
 // batch by k_walk; k_validate walks the rest (and decoded payloads) with the
 // wave-parallel walk.
 constexpr int32_t kLaneWalkMax = 256;
-// decoded payloads: walked by k_walk (one lane each) rather than by
-// k_validate_decoded's wave walk (RPGPU_DEC_WAVE_WALK: the latter, for A/B)
-#ifdef RPGPU_DEC_WAVE_WALK
-constexpr bool kDecodedLaneWalk = false;
-#else
-constexpr bool kDecodedLaneWalk = true;
-#endif
 DEV bool lane_walked(uint32_t flags, uint32_t codec, int32_t rc) {
     return (flags & RPGPU_F_COMPLETE) && codec == 0 && rc <= kLaneWalkMax;
 }
@@ -1109,7 +1102,6 @@ DEV bool lane_record_step(LaneWalk& w, WalkResult& wr, uint8_t* H, const uint8_t
 // What a lane walk touches of the job
 struct WalkCtx {
     const uint8_t* data;
-    const uint8_t* decoded;       // the decoded arena (DECODE jobs), else null
     const uint64_t* seg_off;
     rpgpu_batch_result* batches;
     const uint64_t* slots;
@@ -1122,37 +1114,23 @@ struct WalkCtx {
 };
 
 DEV WalkCtx walk_ctx(const DeviceJob& j) {
-    return WalkCtx{j.data, (j.flags & RPGPU_JOB_DECODE) ? j.decoded : nullptr, j.seg_off, j.batches, j.slots,
-                   j.records, j.record_capacity, j.counters, j.chunk_count, j.chunk_base, j.seg_first_bad};
+    return WalkCtx{j.data, j.seg_off, j.batches, j.slots, j.records, j.record_capacity, j.counters,
+                   j.chunk_count, j.chunk_base, j.seg_first_bad};
 }
 
 // A lane-walked batch's descriptor, read by the walking lane itself: the
 // payload, its record count and index slots.  Returns false when the batch
-// is not lane-walked: incomplete, a stored payload of more than kLaneWalkMax
-// records (k_validate's wave walk takes it), or a compressed one that did not
-// decode.  Decoded payloads (k_lz_exec / k_zexec / the member passes wrote
-// them; k_validate_decoded has checksummed them) are walked here whatever
-// their record count: a wave per payload waited a memory latency per group
-// of 64 records on one chain, where a lane per payload runs all the chains
-// at once.
+// is not lane-walked (incomplete, compressed or > kLaneWalkMax records).
 DEV bool lane_walk_setup(const WalkCtx& j, uint64_t b, LaneWalk& w, bool& idx_ok) {
     const rpgpu_batch_result* R = &j.batches[b];
     const int32_t rc = R->record_count;
-    const uint32_t flags = R->flags, codec = (uint32_t)R->attrs & 7u;
-    const uint8_t* p0;
-    uint32_t n;
-    if (codec != 0 && kDecodedLaneWalk) {
-        if (!j.decoded || !(flags & RPGPU_F_COMPLETE) || !(flags & RPGPU_F_CODEC_OK)) return false;
-        p0 = j.decoded + R->decoded_off;
-        n = R->decoded_len;
-    } else {
-        if (!lane_walked(flags, codec, rc)) return false;
-        p0 = j.data + j.seg_off[R->segment] + R->file_pos + RPGPU_HEADER_SIZE;
-        n = (uint32_t)(R->size_bytes - (int32_t)RPGPU_HEADER_SIZE);
-    }
+    if (!lane_walked(R->flags, (uint32_t)R->attrs & 7u, rc)) return false;
+    const uint64_t S = j.seg_off[R->segment] + R->file_pos + RPGPU_HEADER_SIZE;
+    const uint32_t n = (uint32_t)(R->size_bytes - (int32_t)RPGPU_HEADER_SIZE);
     const uint64_t ib = j.slots[b], islots = j.slots[b + 1] - ib;
     idx_ok = ib + islots <= j.record_capacity;
-    lane_walk_begin(w, p0, n, rc, (uint32_t)b, idx_ok ? j.records + ib : nullptr, idx_ok ? (uint32_t)islots : 0u);
+    lane_walk_begin(w, j.data + S, n, rc, (uint32_t)b, idx_ok ? j.records + ib : nullptr,
+                    idx_ok ? (uint32_t)islots : 0u);
     return true;
 }
 
@@ -1421,8 +1399,7 @@ __global__ __launch_bounds__(1024) void k_validate_decoded(DeviceJob j) {
         const uint32_t dhcrc = decoded_header_crc(T, j.data + hdr, (uint32_t)(RPGPU_HEADER_SIZE + dl), dcrc,
                                                   j.layout == RPGPU_LAYOUT_WIRE);
         uint32_t f = d.flags, perr = 0, parsed = 0;
-        if (!kDecodedLaneWalk && (j.flags & RPGPU_JOB_PARSE) &&
-            (j.layout != RPGPU_LAYOUT_WIRE || (d.flags & RPGPU_F_CRC_OK))) {
+        if ((j.flags & RPGPU_JOB_PARSE) && (j.layout != RPGPU_LAYOUT_WIRE || (d.flags & RPGPU_F_CRC_OK))) {
             bool idx_ok;
             Group g0;
             group_init(g0);
