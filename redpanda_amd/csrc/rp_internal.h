@@ -171,8 +171,7 @@ struct DeviceJob {
                                   // [14] k_decode_finish claim cursor, [15] k_crc_split claim cursor,
                                   // [16] gzip / zstd members (inf_list), [17] k_members_first / [18] k_members claim cursors,
                                   // [19] host-decoded members (host_list), [20] k_members_first's second claim cursor,
-                                  // [21] k_zexec claim cursor, [22] / [23] k_zparse claim cursors, [26] k_zfallback claim cursor,
-                                  // [27] k_walk_decoded claim cursor
+                                  // [21] k_zexec claim cursor, [22] / [23] k_zparse claim cursors, [26] k_zfallback claim cursor
     uint32_t* decode_list;        // batch_capacity: ordinals of batches to uncompress
     uint32_t* seq_list;           // batch_capacity: decode items decoded whole by one lane
     uint32_t* link_list;          // batch_capacity: decode items whose linked LZ4F blocks one wave decodes in order

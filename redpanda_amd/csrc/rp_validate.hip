@@ -1398,45 +1398,23 @@ __global__ __launch_bounds__(1024) void k_validate_decoded(DeviceJob j) {
         }
         const uint32_t dhcrc = decoded_header_crc(T, j.data + hdr, (uint32_t)(RPGPU_HEADER_SIZE + dl), dcrc,
                                                   j.layout == RPGPU_LAYOUT_WIRE);
-        // (the record walk is k_walk_decoded's)
+        uint32_t f = d.flags, perr = 0, parsed = 0;
+        if ((j.flags & RPGPU_JOB_PARSE) && (j.layout != RPGPU_LAYOUT_WIRE || (d.flags & RPGPU_F_CRC_OK))) {
+            bool idx_ok;
+            Group g0;
+            group_init(g0);
+            const WalkResult w = walk_batch(j, d, j.decoded + d.doff, (uint32_t)dl, b, idx_ok, g0);
+            f |= walk_flags(j, w, idx_ok, perr);
+            parsed = w.parsed;
+        }
         if (l == 0) {
-            R->flags = d.flags;
-            R->records_parsed = 0;
-            R->parse_err = 0;
+            R->flags = f;
+            R->records_parsed = parsed;
+            R->parse_err = (uint8_t)perr;
             R->decoded_crc = dcrc;
             R->decoded_header_crc = dhcrc;
             R->reserved0 = 0;
             R->reserved1 = 0;
-        }
-    }
-}
-
-// k_walk_decoded: the record walk of every decoded payload, the wave-parallel
-// walk of k_validate (64 records per group), after k_validate_decoded wrote
-// the payload's checksums.  A kernel of its own: it needs no LDS, so twice
-// as many waves are resident as under the CRC kernels' 155 KiB table image,
-// and the walk waits on one record chain per wave.
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k_walk_decoded(DeviceJob j) {
-    const uint32_t nlz = j.counters[2], ngz = j.counters[16], count = nlz + ngz + j.counters[19];
-    const uint32_t l = lane_v();
-    for (;;) {
-        const uint32_t i = wave_fetch_add(&j.counters[27], 1u);
-        if (i >= count) break;
-        const uint64_t b = uni32(i < nlz ? j.decode_list[i] : i < nlz + ngz ? j.inf_list[i - nlz] : j.host_list[i - nlz - ngz]);
-        rpgpu_batch_result* R = &j.batches[b];
-        const Desc d = desc_of(load_desc_raw(j, b));
-        if (!(d.flags & RPGPU_F_CODEC_OK)) continue;
-        if (j.layout == RPGPU_LAYOUT_WIRE && !(d.flags & RPGPU_F_CRC_OK)) continue;
-        bool idx_ok;
-        Group g0;
-        group_init(g0);
-        const WalkResult w = walk_batch(j, d, j.decoded + d.doff, (uint32_t)d.dlen, b, idx_ok, g0);
-        uint32_t perr = 0;
-        const uint32_t f = d.flags | walk_flags(j, w, idx_ok, perr);
-        if (l == 0) {
-            R->flags = f;
-            R->records_parsed = w.parsed;
-            R->parse_err = (uint8_t)perr;
         }
     }
 }
@@ -1703,10 +1681,8 @@ hipError_t launch_validate(const DeviceJob& j, hipStream_t s, uint32_t grid) {
         hipLaunchKernelGGL(k_crc_split, dim3(grid), dim3(64 * kVWaves), kLdsValidateBytes, s, j);
         hipLaunchKernelGGL(k_crc_combine, dim3((j.split_capacity + 3) / 4), dim3(256), 0, s, j);
     }
-    if ((j.flags & RPGPU_JOB_DECODE) && j.decoded) {
+    if ((j.flags & RPGPU_JOB_DECODE) && j.decoded)
         hipLaunchKernelGGL(k_validate_decoded, dim3(grid), dim3(64 * kVWaves), kLdsValidateBytes, s, j);
-        if (j.flags & RPGPU_JOB_PARSE) hipLaunchKernelGGL(k_walk_decoded, dim3(grid * 8), dim3(256), 0, s, j);
-    }
     return hipGetLastError();
 }
 
