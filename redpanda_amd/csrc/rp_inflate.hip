@@ -1243,6 +1243,9 @@ struct ZLane {
     const uint8_t* src;
     uint64_t n;
     uint8_t* lits;
+    const ZsLitItem* items;  // the member's Huffman literal blocks k_zlits decoded ahead (k_zparse), in order
+    uint32_t nitems, hidx;
+    uint64_t lits_at;        // scratch offset of lits (matches ZsLitItem::lits)
     SeqRec* recs;
     uint64_t lcap, rcap;
     uint64_t nlit, nrec, pend, mlsum;
@@ -1354,12 +1357,32 @@ struct ZLane {
         prof[2] += wall_clock64() - t0;
 #endif
     }
+    // a block k_zlits decoded ahead: its bytes are in place; the streams are
+    // set to the end states lits_finish then reads (ended exactly, or
+    // overflowed: the verdict k_zlits found)
+    DEV bool take_planned(zs::Lits& L, uint32_t hlog) {
+        if (hidx >= nitems) return false;
+        const ZsLitItem* it = items + hidx++;
+        const uint32_t st = it->status;
+        bool same = st != 0 && it->lits == lits_at + nlit && it->lsz == L.size && it->ns == L.ns && it->hlog == hlog &&
+                    it->x2 == (uint32_t)L.x2;
+        for (uint32_t k = 0; k < 4; k++)
+            if (k < L.ns) same = same && it->s0[k] == L.s[k].start && it->cnt[k] == L.cnt[k];
+        if (!same) return false;
+        for (uint32_t k = 0; k < 4; k++) {
+            L.s[k].ptr = L.s[k].start;
+            L.s[k].used = st == 1 ? 64u : 65u;
+            L.dec[k] = L.cnt[k];
+        }
+        return true;
+    }
     DEV void huf_all_(zs::Tabs* T, zs::Lits& L, uint32_t hlog) {
         const uint64_t at = nlit;
         if (at + L.size > lcap) {
             bad = true;
             return;
         }
+        if (take_planned(L, hlog)) return;
         const bool x2 = L.x2;
         if (L.ns == 1) {
             const uint32_t c = L.cnt[0];
@@ -1427,9 +1450,10 @@ struct zs::EagerLits<ZLane> {
 // checksum or dictionary, every block whole; sums the literal bytes the
 // decoder can emit and the sequences it can decode.  False sends the member to
 // the wave decoder (which also rules on anything malformed here).
-DEV bool zs_fast_size(const uint8_t* src, uint64_t n, uint64_t& nlit, uint64_t& nseq) {
+DEV bool zs_fast_size(const uint8_t* src, uint64_t n, uint64_t& nlit, uint64_t& nseq, uint32_t& nhuf) {
     auto b = [&](uint64_t i) -> uint32_t { return i < n ? (uint32_t)src[i] : 0u; };
     nlit = nseq = 0;
+    nhuf = 0;
     uint64_t ip = 0;
     if (n == 0) return false;
     while (ip < n) {
@@ -1495,6 +1519,7 @@ DEV bool zs_fast_size(const uint8_t* src, uint64_t n, uint64_t& nlit, uint64_t& 
                     lcons = lh + lcs;
                 }
                 if (lsz > zs::kBlockMax || lcons >= bsz) return false;
+                if (lt >= 2) nhuf++;
                 nlit += lsz;
                 uint64_t sp = ip + lcons;
                 uint32_t ns = b(sp);
@@ -1509,28 +1534,144 @@ DEV bool zs_fast_size(const uint8_t* src, uint64_t n, uint64_t& nlit, uint64_t& 
     return ip == n;
 }
 
+// k_zplan's second walk over a member zs_fast_size admitted: each compressed
+// block with Huffman literals becomes a ZsLitItem (its stream bounds and
+// literal destination as block() will set them; its table built by the
+// decoder's own huf_table and snapshot for a new tree, the frame's last one
+// for a treeless block).  Stops at anything block() would reject there: the
+// blocks after it have no item and decode in place (or never: the member is
+// rejected at that block).  Returns the item count.
+DEV uint32_t zs_plan_items(ZLane& e, zs::Tabs* T, const DeviceJob& j, uint64_t src_off, uint64_t soff, ZsLitItem* items,
+                           uint32_t cap, uint64_t tabs_off) {
+    const uint64_t n = e.n;
+    uint64_t ip = 0, nlit = 0, tab = 0, ntab = 0;
+    uint32_t cnt = 0, hlog = 0, hx2 = 0;
+    bool have = false;
+    while (ip < n) {
+        if (n - ip < 6) return cnt;
+        const uint32_t fhd = e.b(ip + 4);
+        const uint32_t single = (fhd >> 5) & 1, fcsid = fhd >> 6;
+        ip += 5 + (single ? 0 : 1) + (fcsid ? (fcsid == 1 ? 2 : fcsid == 2 ? 4 : 8) : 0) + ((single && !fcsid) ? 1 : 0);
+        have = false;  // a frame's first Huffman block must carry its tree
+        for (;;) {
+            if (n - ip < 3) return cnt;
+            const uint32_t bh = (uint32_t)e.le(ip, 3);
+            const uint32_t last = bh & 1, bt = (bh >> 1) & 3, bsz = bh >> 3;
+            ip += 3;
+            const uint64_t adv = bt == 1 ? 1u : bsz;  // an RLE block occupies one byte
+            if (bt == 0 || bt == 1) {
+                nlit += bsz;
+            } else {
+                const uint64_t bp = ip;
+                const uint32_t b0 = e.b(bp), lt = b0 & 3, lhl = (b0 >> 2) & 3;
+                if (lt < 2) {
+                    nlit += lhl == 1 ? (e.le(bp, 2) >> 4) : lhl == 3 ? (e.le(bp, 3) >> 4) : (b0 >> 3);
+                } else {
+                    const uint32_t lhc = (uint32_t)e.le(bp, 4);
+                    uint32_t lh, lsz;
+                    uint64_t lcs;
+                    bool one = false;
+                    if (lhl < 2) {
+                        one = lhl == 0;
+                        lh = 3;
+                        lsz = (lhc >> 4) & 0x3FF;
+                        lcs = (lhc >> 14) & 0x3FF;
+                    } else if (lhl == 2) {
+                        lh = 4;
+                        lsz = (lhc >> 4) & 0x3FFF;
+                        lcs = lhc >> 18;
+                    } else {
+                        lh = 5;
+                        lsz = (lhc >> 4) & 0x3FFFF;
+                        lcs = (lhc >> 22) + ((uint64_t)e.b(bp + 4) << 10);
+                    }
+                    if (lcs + lh > bsz || cnt >= cap) return cnt;
+                    uint64_t hs = bp + lh, hn = lcs;
+                    if (lt == 2) {
+                        if (!one && (lsz == 0 || hn == 0)) return cnt;
+                        uint32_t hl = 0;
+                        const int64_t th = zs::huf_table(e, T, hs, hn, hl);
+                        if (th < 0 || (uint64_t)th >= hn) return cnt;
+                        hlog = hl;
+                        hx2 = !one && zs::huf_select_x2(lsz, lcs) ? 1u : 0u;
+                        hs += (uint64_t)th;
+                        hn -= (uint64_t)th;
+                        tab = tabs_off + 8192ull * ntab++;
+                        uint16_t* dst = (uint16_t*)(j.inf_scratch + tab);
+                        for (uint32_t u = lane(); u < (1u << hl); u += 64) dst[u] = T->huf[u];
+                        have = true;
+                    } else if (!have) {
+                        return cnt;  // treeless without a tree: block() rejects
+                    }
+                    ZsLitItem it;
+                    it.src = src_off;
+                    it.n = n;
+                    it.lits = soff + kZsFastHdr + nlit;
+                    it.tab = tab;
+                    it.lsz = lsz;
+                    it.hlog = hlog;
+                    it.status = 0;
+                    for (uint32_t k = 0; k < 4; k++) it.s0[k] = 0, it.sn[k] = 0, it.cnt[k] = 0;
+                    if (one) {
+                        it.ns = 1;
+                        it.seg = 1;
+                        it.x2 = 0;
+                        it.s0[0] = hs;
+                        it.sn[0] = (uint32_t)hn;
+                        it.cnt[0] = lsz;
+                    } else {
+                        if (hn < 10) return cnt;
+                        const uint64_t l1 = e.le(hs, 2), l2 = e.le(hs + 2, 2), l3 = e.le(hs + 4, 2);
+                        const uint64_t l4 = hn - (l1 + l2 + l3 + 6);
+                        if (l4 > hn) return cnt;
+                        it.ns = 4;
+                        it.x2 = hx2;
+                        it.seg = (lsz + 3) / 4;
+                        it.s0[0] = hs + 6;
+                        it.s0[1] = hs + 6 + l1;
+                        it.s0[2] = hs + 6 + l1 + l2;
+                        it.s0[3] = hs + 6 + l1 + l2 + l3;
+                        it.sn[0] = (uint32_t)l1;
+                        it.sn[1] = (uint32_t)l2;
+                        it.sn[2] = (uint32_t)l3;
+                        it.sn[3] = (uint32_t)l4;
+                        it.cnt[0] = it.cnt[1] = it.cnt[2] = it.seg;
+                        it.cnt[3] = lsz > 3 * it.seg ? lsz - 3 * it.seg : 0;
+                    }
+                    if (lane() == 0) items[cnt] = it;
+                    cnt++;
+                    nlit += lsz;
+                }
+            }
+            ip += adv;
+            if (last) break;
+        }
+    }
+    return cnt;
+}
+
 // the fast path of zstd member i: 0 not taken (the wave decoder runs), else
 // the state set (1 rejected, kZsFast parsed)
 DEV uint32_t zstd_fast_item(const DeviceJob& j, uint8_t* lds, uint32_t i, uint32_t b, const rpgpu_batch_result* R) {
-    if (!j.inf_scratch || !j.zs_fast) return 0;
+    // k_zplan sized the member's buffers (ZsFastDesc at inf_off[i]) and
+    // k_zlits decoded its Huffman literal blocks ahead
     const uint64_t S = uni64(j.seg_off[uni32(R->segment)]) + uni64(R->file_pos) + RPGPU_HEADER_SIZE;
     const uint64_t n = (uint64_t)uni32((uint32_t)(R->size_bytes - (int32_t)RPGPU_HEADER_SIZE));
     const uint8_t* src = j.data + S;
-    uint64_t nl = 0, nq = 0;
-    if (!zs_fast_size(src, n, nl, nq)) return 0;
-    const uint64_t lbytes = (nl + 16 + 15) & ~15ull, rcap = nq + 1;
-    const uint64_t need = kZsFastHdr + lbytes + rcap * sizeof(SeqRec);
-    const uint64_t soff =
-        uni64(atomicAdd((unsigned long long*)j.inf_scratch_used, lane() == 0 ? (unsigned long long)need : 0ull));
-    if (soff + need > j.inf_scratch_bytes) return 0;
+    const uint64_t soff = uni64(j.inf_off[i]);
     uint8_t* base = j.inf_scratch + soff;
+    ZsFastDesc* D = (ZsFastDesc*)base;
     ZLane e;
     e.src = src;
     e.n = n;
-    e.lits = base + kZsFastHdr;
-    e.recs = (SeqRec*)(base + kZsFastHdr + lbytes);
-    e.lcap = nl;
-    e.rcap = rcap;
+    e.lits = base + uni64(D->lit_off);
+    e.lits_at = soff + uni64(D->lit_off);
+    e.recs = (SeqRec*)(base + uni64(D->rec_off));
+    e.lcap = uni64(D->lcap);
+    e.rcap = uni64(D->rcap);
+    e.items = (const ZsLitItem*)(base + uni64(D->items));
+    e.nitems = uni32((uint32_t)D->nitems);
+    e.hidx = 0;
     e.nlit = e.nrec = e.pend = e.mlsum = 0;
     e.bad = false;
     e.win = (inf_lds_u8*)lds;  // the ring's LDS (the wave decoder's, unused here)
@@ -1569,8 +1710,8 @@ DEV uint32_t zstd_fast_item(const DeviceJob& j, uint8_t* lds, uint32_t i, uint32
     if (unsure || e.bad || e.nlit + e.mlsum != total || total >= (1ull << 31)) return 0;
     const uint64_t cap = (total + 15) & ~15ull;
     if (lane() == 0) {
-        ZsFastDesc d{e.nlit, e.nrec, kZsFastHdr, kZsFastHdr + lbytes};
-        *(ZsFastDesc*)base = d;
+        D->nlit = e.nlit;
+        D->nrec = e.nrec;
         const int32_t rcount = R->record_count;
         j.dcap[b] = cap;
         j.slots[b] = ((j.flags & RPGPU_JOB_PARSE) && rcount > 0 && (uint64_t)rcount <= cap) ? (uint64_t)rcount : 0;
@@ -1687,6 +1828,116 @@ __global__ __launch_bounds__(64) void k_members_first(DeviceJob j) {
 // and the wave decoder's SGPR state in one register allocation spilled.)
 constexpr uint32_t kZsPending = 4;
 
+// k_zplan: per zstd member, zs_fast_size's header walk, the scratch region
+// (descriptor, literal buffer, records, literal block items, table
+// snapshots) and the items (zs_plan_items), registered in zs_items for
+// k_zlits; kZsPlanned, or kZsPending for the wave decoder
+__global__ __launch_bounds__(64) void k_zplan(DeviceJob j) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    const uint32_t count = j.counters[16];
+    zs::Tabs* T = (zs::Tabs*)(lds + kInfRing);
+    for (;;) {
+        const uint32_t i = wave_fetch_add(&j.counters[30], 1u);
+        if (i >= count) break;
+        const uint32_t b = uni32(j.inf_list[i]);
+        const rpgpu_batch_result* R = &j.batches[b];
+        if ((uni32((uint32_t)(uint16_t)R->attrs) & 7u) == RPGPU_CODEC_GZIP) continue;
+        const uint64_t S = uni64(j.seg_off[uni32(R->segment)]) + uni64(R->file_pos) + RPGPU_HEADER_SIZE;
+        const uint64_t n = (uint64_t)uni32((uint32_t)(R->size_bytes - (int32_t)RPGPU_HEADER_SIZE));
+        uint64_t nl = 0, nq = 0;
+        uint32_t nh = 0;
+        uint32_t state = kZsPending;
+        uint64_t soff = 0;
+        if (j.zs_fast && zs_fast_size(j.data + S, n, nl, nq, nh)) {
+            const uint64_t lbytes = (nl + 16 + 15) & ~15ull, rcap = nq + 1;
+            const uint64_t ibytes = ((uint64_t)nh * sizeof(ZsLitItem) + 15) & ~15ull;
+            const uint64_t need = kZsFastHdr + lbytes + rcap * sizeof(SeqRec) + ibytes + 8192ull * nh;
+            soff = uni64(atomicAdd((unsigned long long*)j.inf_scratch_used, lane() == 0 ? (unsigned long long)need : 0ull));
+            if (soff + need <= j.inf_scratch_bytes) {
+                const uint64_t io = kZsFastHdr + lbytes + rcap * sizeof(SeqRec);
+                ZLane e;
+                e.src = j.data + S;
+                e.n = n;
+                e.win = (inf_lds_u8*)lds;
+                e.rr = 0;
+                const uint32_t ni = zs_plan_items(e, T, j, S, soff, (ZsLitItem*)(j.inf_scratch + soff + io), nh,
+                                                  soff + io + ibytes);
+                const uint32_t first = wave_fetch_add(&j.counters[28], ni);
+                if (lane() == 0) {
+                    for (uint32_t k = 0; k < ni && first + k < j.zs_items_cap; k++)
+                        j.zs_items[first + k] = soff + io + (uint64_t)k * sizeof(ZsLitItem);
+                    ZsFastDesc d{0, 0, kZsFastHdr, kZsFastHdr + lbytes, nl, rcap, io, ni};
+                    *(ZsFastDesc*)(j.inf_scratch + soff) = d;
+                }
+                state = kZsPlanned;
+            }
+        }
+        if (lane() == 0) {
+            j.inf_state[i] = state;
+            j.inf_off[i] = soff;
+        }
+    }
+}
+
+// k_zlits: one wave per planned literal block: the table snapshot into LDS,
+// the block's streams decoded into its place in the member's literal buffer
+// (ZLane::huf_all_, the four streams interleaved), then whether every stream
+// ended exactly (what lits_finish checks)
+__global__ __launch_bounds__(64) void k_zlits(DeviceJob j) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    zs::Tabs* T = (zs::Tabs*)(lds + kInfRing);
+    const uint32_t reg = j.counters[28];
+    const uint32_t count = reg < j.zs_items_cap ? reg : j.zs_items_cap;
+    for (;;) {
+        const uint32_t k = wave_fetch_add(&j.counters[29], 1u);
+        if (k >= count) break;
+        ZsLitItem* it = (ZsLitItem*)(j.inf_scratch + uni64(j.zs_items[k]));
+        const uint32_t hlog = uni32(it->hlog), ns = uni32(it->ns);
+        const uint16_t* tab = (const uint16_t*)(j.inf_scratch + uni64(it->tab));
+        for (uint32_t u = lane(); u < (1u << hlog); u += 64) T->huf[u] = tab[u];
+        ZLane e;
+        e.src = j.data + uni64(it->src);
+        e.n = uni64(it->n);
+        e.lits = j.inf_scratch + uni64(it->lits);
+        e.lcap = uni32(it->lsz);
+        e.nitems = 0;
+        e.hidx = 0;
+        e.nlit = 0;
+        e.bad = false;
+        e.win = (inf_lds_u8*)lds;
+        e.rr = 0;
+        zs::Lits L;
+        L.kind = 2;
+        L.size = uni32(it->lsz);
+        L.used = 0;
+        L.ns = ns;
+        L.seg = uni32(it->seg);
+        L.x2 = uni32(it->x2) != 0;
+        bool ok = true;
+        for (uint32_t q = 0; q < 4; q++) {
+            L.pend[q] = 0;
+            L.cnt[q] = uni32(it->cnt[q]);
+            L.dec[q] = 0;
+            if (q < ns) ok = ok && zs::bits_init(e, L.s[q], uni64(it->s0[q]), uni32(it->sn[q]));
+        }
+        uint32_t st = 2;
+        if (ok) {
+            e.huf_all_(T, L, hlog);
+            bool ends = !e.bad;
+            for (uint32_t q = 0; q < 4; q++)
+                if (q < ns) {
+                    zs::bits_reload(e, L.s[q]);
+                    ends = ends && zs::bits_end(L.s[q]);
+                }
+            st = ends ? 1u : 2u;
+            if (e.bad) st = 0;  // (never: the plan sized it) left to k_zparse
+        } else {
+            st = 0;
+        }
+        if (lane() == 0) it->status = st;
+    }
+}
+
 __global__ __launch_bounds__(64) void k_zparse(DeviceJob j) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     const uint32_t count = j.counters[16];
@@ -1694,9 +1945,9 @@ __global__ __launch_bounds__(64) void k_zparse(DeviceJob j) {
         for (;;) {
             const uint32_t i = wave_fetch_add(&j.counters[phase ? 23 : 22], 1u);
             if (i >= count) break;
+            if (uni32(j.inf_state[i]) != kZsPlanned) continue;
             const uint32_t b = uni32(j.inf_list[i]);
             const rpgpu_batch_result* R = &j.batches[b];
-            if ((uni32((uint32_t)(uint16_t)R->attrs) & 7u) == RPGPU_CODEC_GZIP) continue;
             const bool big = uni32((uint32_t)R->size_bytes) >= (128u << 10);
             if (big != (phase == 0)) continue;
             if (!zstd_fast_item(j, lds, i, b, R) && lane() == 0) j.inf_state[i] = kZsPending;
@@ -1780,12 +2031,24 @@ hipError_t launch_inflate_plan(const DeviceJob& j, hipStream_t s, uint32_t grid)
     return hipGetLastError();
 }
 
+hipError_t launch_zplan(const DeviceJob& j, hipStream_t s, uint32_t grid) {
+    static bool attr = false;
+    if (!attr) {
+        (void)hipFuncSetAttribute((const void*)k_zplan, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kMemLds);
+        attr = true;
+    }
+    hipLaunchKernelGGL(k_zplan, dim3(grid), dim3(64), kMemLds, s, j);
+    return hipGetLastError();
+}
+
 hipError_t launch_zparse(const DeviceJob& j, hipStream_t s, uint32_t grid) {
     static bool attr = false;
     if (!attr) {
+        (void)hipFuncSetAttribute((const void*)k_zlits, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kMemLds);
         (void)hipFuncSetAttribute((const void*)k_zparse, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kMemLds);
         attr = true;
     }
+    hipLaunchKernelGGL(k_zlits, dim3(grid), dim3(64), kMemLds, s, j);
     hipLaunchKernelGGL(k_zparse, dim3(grid), dim3(64), kMemLds, s, j);
     return hipGetLastError();
 }

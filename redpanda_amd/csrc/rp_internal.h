@@ -132,7 +132,24 @@ constexpr uint32_t kZsFast = 3;
 constexpr uint32_t kZsFastHdr = 64;  // descriptor bytes before the literal buffer
 struct ZsFastDesc {
     uint64_t nlit, nrec, lit_off, rec_off;  // literal bytes, records; offsets from the descriptor
+    uint64_t lcap, rcap;                    // literal buffer / record array capacities (k_zplan's header walk)
+    uint64_t items, nitems;                 // the member's Huffman literal blocks (ZsLitItem), offset from the descriptor
 };
+// One block's Huffman literal section, planned by k_zplan (table snapshot,
+// stream bounds, where its literals go) and decoded ahead by k_zlits, one
+// wave per block, while k_zparse later only takes the bytes
+struct ZsLitItem {
+    uint64_t src;      // member payload (offset in d_data)
+    uint64_t n;        // member bytes
+    uint64_t lits;     // scratch offset of the block's literals
+    uint64_t tab;      // scratch offset of the Huffman table snapshot (1 << hlog entries)
+    uint64_t s0[4];    // stream starts (member offsets)
+    uint32_t sn[4];    // stream bytes
+    uint32_t cnt[4];   // symbols per stream
+    uint32_t lsz, seg, ns, hlog, x2;
+    uint32_t status;   // 0 not decoded, 1 decoded and every stream ended exactly, 2 decoded, a stream did not
+};
+constexpr uint32_t kZsPlanned = 5;  // inf_state: k_zplan sized and planned the member for k_zparse
 
 // job counters (DeviceJob::counters), zeroed per submit
 constexpr size_t kCounterBytes = 128;
@@ -171,7 +188,8 @@ struct DeviceJob {
                                   // [14] k_decode_finish claim cursor, [15] k_crc_split claim cursor,
                                   // [16] gzip / zstd members (inf_list), [17] k_members_first / [18] k_members claim cursors,
                                   // [19] host-decoded members (host_list), [20] k_members_first's second claim cursor,
-                                  // [21] k_zexec claim cursor, [22] / [23] k_zparse claim cursors, [26] k_zfallback claim cursor
+                                  // [21] k_zexec claim cursor, [22] / [23] k_zparse claim cursors, [26] k_zfallback claim cursor,
+                                  // [28] planned literal blocks (zs_items), [29] k_zlits / [30] k_zplan claim cursors
     uint32_t* decode_list;        // batch_capacity: ordinals of batches to uncompress
     uint32_t* seq_list;           // batch_capacity: decode items decoded whole by one lane
     uint32_t* link_list;          // batch_capacity: decode items whose linked LZ4F blocks one wave decodes in order
@@ -203,6 +221,8 @@ struct DeviceJob {
     uint64_t* inf_scratch_used;   // bump allocator of the pool (zeroed per job)
     uint32_t zs_fast;             // zstd members may take the parse / execute split (kZsFast)
     uint32_t zs_split;            // k_zparse (side stream) owns the zstd members' first pass
+    uint64_t* zs_items;           // zs_items_cap: scratch offsets of the planned literal blocks (k_zplan -> k_zlits)
+    uint32_t zs_items_cap;
     uint32_t* host_list;          // batch_capacity: ordinals of host-decoded (zstd) batches (RPGPU_JOB_HOST_CODECS)
 };
 
@@ -241,6 +261,7 @@ hipError_t launch_decode_finish(const DeviceJob& j, hipStream_t s, uint32_t grid
 hipError_t launch_inflate_plan(const DeviceJob& j, hipStream_t s, uint32_t grid);
 hipError_t launch_inflate(const DeviceJob& j, hipStream_t s, uint32_t grid);
 hipError_t launch_zparse(const DeviceJob& j, hipStream_t s, uint32_t grid);
+hipError_t launch_zplan(const DeviceJob& j, hipStream_t s, uint32_t grid);
 hipError_t launch_zfallback(const DeviceJob& j, hipStream_t s, uint32_t grid);
 hipError_t launch_zstamps(hipStream_t s, int print);  // RPGPU_ZSTAMPS builds: reset / print the decoder stamps
 hipError_t launch_zexec(const DeviceJob& j, hipStream_t s);  // rp_codec.hip

@@ -628,6 +628,11 @@ int submit_body(rpgpu_ctx* c, const rpgpu_job* job, hipStream_t s, int stop, Pla
     const size_t o_itot = take(decode_job ? (bcap + 1) * 8 : 0);
     const bool host_job = decode_job && (job->flags & RPGPU_JOB_HOST_CODECS);
     const size_t o_hlist = take(host_job ? (bcap + 1) * 4 : 0);
+    // zstd literal blocks planned ahead (k_zplan -> k_zlits): a 128 KiB block
+    // each at most, so the job's bytes / 16 KiB + 8 per batch is ample (past
+    // it, blocks decode in place)
+    const uint64_t zcap64 = decode_job ? std::min<uint64_t>(job->h_seg_offsets[nseg] / 16384 + 8 * bcap + 64, 0x7FFFFFFFull) : 0;
+    const size_t o_zitems = take(zcap64 * 8);
     // block-parallel decode: one item per LZ4F block / snappy-java chunk
     const bool dec = (job->flags & RPGPU_JOB_DECODE) && job->d_decoded;
     const uint64_t data_len = job->h_seg_offsets[nseg];
@@ -752,6 +757,8 @@ int submit_body(rpgpu_ctx* c, const rpgpu_job* job, hipStream_t s, int stop, Pla
     static const uint32_t zs_fast = [] { const char* e = diag_env("RPGPU_ZS_FAST"); return e && *e == '0' ? 0u : 1u; }();
     j.zs_fast = zs_fast;
     j.zs_split = 0;
+    j.zs_items = (uint64_t*)(ws + o_zitems);
+    j.zs_items_cap = (uint32_t)zcap64;
     j.host_list = (uint32_t*)(ws + o_hlist);
     c->hc_n = 0;
     j.blocks = (BlockItem*)(ws + o_blocks);
@@ -814,6 +821,7 @@ int submit_body(rpgpu_ctx* c, const rpgpu_job* job, hipStream_t s, int stop, Pla
             j.zs_split = 1;
             HIPCHK(c, hipEventRecord(c->fork_ev, s));
             HIPCHK(c, hipStreamWaitEvent(c->side, c->fork_ev, 0));
+            STAGE("zplan", launch_zplan(j, c->side, c->cu_count * 4));
             STAGE("zparse", launch_zparse(j, c->side, c->cu_count * 4));
             HIPCHK(c, hipEventRecord(c->join_ev, c->side));
         }
