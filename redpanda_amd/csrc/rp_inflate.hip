@@ -1879,62 +1879,70 @@ __global__ __launch_bounds__(64) void k_zplan(DeviceJob j) {
     }
 }
 
-// k_zlits: one wave per planned literal block: the table snapshot into LDS,
-// the block's streams decoded into its place in the member's literal buffer
-// (ZLane::huf_all_, the four streams interleaved), then whether every stream
-// ended exactly (what lits_finish checks)
+// A per-lane bit-stream environment for k_zlits: each lane reads its own
+// stream straight from the payload (a stream moves down through L1-resident
+// lines; no wave-cooperative window, the lanes diverge)
+struct ZPer {
+    const uint8_t* src;
+    uint64_t n;
+    DEV uint32_t b(uint64_t i) { return i < n ? (uint32_t)src[i] : 0u; }
+    DEV uint64_t le(uint64_t i, uint32_t k) {
+        uint64_t v = 0;
+        for (uint32_t t = 0; t < k; t++) v |= (uint64_t)b(i + t) << (8 * t);
+        return v;
+    }
+    DEV uint64_t lb(zs::Bits&, uint64_t pos) {  // pos + 8 <= n
+        uint64_t v;
+        __builtin_memcpy(&v, (const __attribute__((address_space(1))) uint8_t*)(src + pos), 8);
+        return v;
+    }
+    DEV uint32_t U(uint32_t x) { return x; }
+};
+
+// k_zlits: one wave per planned literal block, one LANE per Huffman stream
+// (the four streams of a block are independent: lane q decodes stream q
+// into its segment of the member's literal buffer, all four through the
+// block's table snapshot in LDS, each lane's last symbol by zs::huf_one's
+// X2 rule); then whether every stream ended exactly (what lits_finish checks)
 __global__ __launch_bounds__(64) void k_zlits(DeviceJob j) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     zs::Tabs* T = (zs::Tabs*)(lds + kInfRing);
     const uint32_t reg = j.counters[28];
     const uint32_t count = reg < j.zs_items_cap ? reg : j.zs_items_cap;
+    const uint32_t l = lane();
     for (;;) {
         const uint32_t k = wave_fetch_add(&j.counters[29], 1u);
         if (k >= count) break;
         ZsLitItem* it = (ZsLitItem*)(j.inf_scratch + uni64(j.zs_items[k]));
         const uint32_t hlog = uni32(it->hlog), ns = uni32(it->ns);
         const uint16_t* tab = (const uint16_t*)(j.inf_scratch + uni64(it->tab));
-        for (uint32_t u = lane(); u < (1u << hlog); u += 64) T->huf[u] = tab[u];
-        ZLane e;
-        e.src = j.data + uni64(it->src);
-        e.n = uni64(it->n);
-        e.lits = j.inf_scratch + uni64(it->lits);
-        e.lcap = uni32(it->lsz);
-        e.nitems = 0;
-        e.hidx = 0;
-        e.nlit = 0;
-        e.bad = false;
-        e.win = (inf_lds_u8*)lds;
-        e.rr = 0;
-        zs::Lits L;
-        L.kind = 2;
-        L.size = uni32(it->lsz);
-        L.used = 0;
-        L.ns = ns;
-        L.seg = uni32(it->seg);
-        L.x2 = uni32(it->x2) != 0;
+        for (uint32_t u = l; u < (1u << hlog); u += 64) T->huf[u] = tab[u];
+        __builtin_amdgcn_s_waitcnt(0);  // (one wave: its LDS stores land before its loads)
         bool ok = true;
-        for (uint32_t q = 0; q < 4; q++) {
-            L.pend[q] = 0;
-            L.cnt[q] = uni32(it->cnt[q]);
-            L.dec[q] = 0;
-            if (q < ns) ok = ok && zs::bits_init(e, L.s[q], uni64(it->s0[q]), uni32(it->sn[q]));
-        }
-        uint32_t st = 2;
-        if (ok) {
-            e.huf_all_(T, L, hlog);
-            bool ends = !e.bad;
-            for (uint32_t q = 0; q < 4; q++)
-                if (q < ns) {
-                    zs::bits_reload(e, L.s[q]);
-                    ends = ends && zs::bits_end(L.s[q]);
+        if (l < ns) {
+            ZPer e{j.data + it->src, it->n};
+            const uint32_t cnt = it->cnt[l], seg = it->seg;
+            const bool x2 = it->x2 != 0;
+            uint8_t* dst = j.inf_scratch + it->lits + (uint64_t)l * seg;
+            zs::Bits s;
+            uint32_t open = 0;
+            ok = zs::bits_init(e, s, it->s0[l], it->sn[l]);
+            if (ok) {
+                for (uint32_t i = 0; i + 1 < cnt; i++) {
+                    if (s.used > 64 - hlog) zs::bits_reload(e, s);
+                    const uint32_t d = T->huf[(uint32_t)((s.c << (s.used & 63)) >> ((64 - hlog) & 63))];
+                    const uint32_t l1 = d >> 8;
+                    if (x2) open = (open && open + l1 <= 12) ? 0u : l1;
+                    s.used += l1;
+                    dst[i] = (uint8_t)d;
                 }
-            st = ends ? 1u : 2u;
-            if (e.bad) st = 0;  // (never: the plan sized it) left to k_zparse
-        } else {
-            st = 0;
+                if (cnt) dst[cnt - 1] = (uint8_t)zs::huf_one(e, T, s, open, 1, x2, hlog);
+                zs::bits_reload(e, s);
+                ok = zs::bits_end(s);
+            }
         }
-        if (lane() == 0) it->status = st;
+        const bool all = __ballot(!ok) == 0;
+        if (l == 0) it->status = all ? 1u : 2u;
     }
 }
 
