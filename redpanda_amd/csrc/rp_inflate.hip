@@ -1245,6 +1245,11 @@ struct ZLane {
     uint8_t* lits;
     const ZsLitItem* items;  // the member's Huffman literal blocks k_zlits decoded ahead (k_zparse), in order
     uint32_t nitems, hidx;
+    const ZsSeqItem* sitems;  // its sequence sections k_zlits decoded ahead, in order
+    uint32_t nsitems, sidx;
+    const zs::RawSeq* rseq;   // the taken section's raw sequences
+    uint32_t rpos, rok;
+    uint4 rbuf;               // 64 of them, lane k holding sequence 64 c + k
     uint64_t lits_at;        // scratch offset of lits (matches ZsLitItem::lits)
     SeqRec* recs;
     uint64_t lcap, rcap;
@@ -1376,6 +1381,31 @@ struct ZLane {
         }
         return true;
     }
+    // zs::EagerSeqs: the block's sequence section decoded ahead by k_zlits
+    // (same stream, same logs, all of it), read 64 at a time
+    DEV bool seqs_take(uint64_t sp, uint64_t sn, uint32_t nseq, uint32_t llog, uint32_t olog, uint32_t mlog) {
+        if (sidx >= nsitems) return false;
+        const ZsSeqItem* it = sitems + sidx++;
+        const uint32_t st = it->status;
+        if (st == 0 || it->sp != sp || it->sn != sn || it->nseq != nseq || it->llog != llog || it->olog != olog ||
+            it->mlog != mlog)
+            return false;
+        rseq = (const zs::RawSeq*)(scratch + it->seqs);
+        rpos = 0;
+        rok = st == 1;
+        return true;
+    }
+    uint8_t* scratch;
+    DEV void seq_next(zs::RawSeq& r) {
+        const uint32_t k = rpos & 63u;
+        if (k == 0) rbuf = *(const uint4*)(rseq + rpos + lane());  // (16 bytes past the section: inside the scratch region)
+        r.ll = (uint32_t)__builtin_amdgcn_readlane((int)rbuf.x, (int)k);
+        r.ml = (uint32_t)__builtin_amdgcn_readlane((int)rbuf.y, (int)k);
+        r.v = (uint32_t)__builtin_amdgcn_readlane((int)rbuf.z, (int)k);
+        r.kind = (uint32_t)__builtin_amdgcn_readlane((int)rbuf.w, (int)k);
+        rpos++;
+    }
+    DEV bool seqs_ok() { return rok != 0; }
     DEV void huf_all_(zs::Tabs* T, zs::Lits& L, uint32_t hlog) {
         const uint64_t at = nlit;
         if (at + L.size > lcap) {
@@ -1445,15 +1475,19 @@ template <>
 struct zs::EagerLits<ZLane> {
     static constexpr bool value = true;
 };
+template <>
+struct zs::EagerSeqs<ZLane> {
+    static constexpr bool value = true;
+};
 
 // The fast path's header walk: every frame a zstd frame without a content
 // checksum or dictionary, every block whole; sums the literal bytes the
 // decoder can emit and the sequences it can decode.  False sends the member to
 // the wave decoder (which also rules on anything malformed here).
-DEV bool zs_fast_size(const uint8_t* src, uint64_t n, uint64_t& nlit, uint64_t& nseq, uint32_t& nhuf) {
+DEV bool zs_fast_size(const uint8_t* src, uint64_t n, uint64_t& nlit, uint64_t& nseq, uint32_t& nhuf, uint32_t& nsb) {
     auto b = [&](uint64_t i) -> uint32_t { return i < n ? (uint32_t)src[i] : 0u; };
     nlit = nseq = 0;
-    nhuf = 0;
+    nhuf = nsb = 0;
     uint64_t ip = 0;
     if (n == 0) return false;
     while (ip < n) {
@@ -1526,6 +1560,7 @@ DEV bool zs_fast_size(const uint8_t* src, uint64_t n, uint64_t& nlit, uint64_t& 
                 if (ns == 255) ns = (b(sp + 1) | (b(sp + 2) << 8)) + 0x7F00;
                 else if (ns >= 128) ns = ((ns - 128) << 8) + b(sp + 1);
                 nseq += ns;
+                if (ns) nsb++;
                 ip += bsz;
             }
             if (last) break;
@@ -1534,27 +1569,37 @@ DEV bool zs_fast_size(const uint8_t* src, uint64_t n, uint64_t& nlit, uint64_t& 
     return ip == n;
 }
 
-// k_zplan's second walk over a member zs_fast_size admitted: each compressed
-// block with Huffman literals becomes a ZsLitItem (its stream bounds and
-// literal destination as block() will set them; its table built by the
-// decoder's own huf_table and snapshot for a new tree, the frame's last one
-// for a treeless block).  Stops at anything block() would reject there: the
-// blocks after it have no item and decode in place (or never: the member is
-// rejected at that block).  Returns the item count.
-DEV uint32_t zs_plan_items(ZLane& e, zs::Tabs* T, const DeviceJob& j, uint64_t src_off, uint64_t soff, ZsLitItem* items,
-                           uint32_t cap, uint64_t tabs_off) {
+// k_zplan's second walk over a member zs_fast_size admitted, block() step
+// by step without decoding a symbol: each compressed block's Huffman literal
+// section becomes a ZsLitItem (its stream bounds and literal destination;
+// its table built by the decoder's own huf_table and snapshot for a new
+// tree, the frame's last one for a treeless block) and its sequence section
+// a ZsSeqItem (its stream and the three FSE tables seq_table builds, the
+// repeat modes taking the frame's previous ones, snapshot).  It stops at
+// anything block() would reject there: the blocks after it have no items
+// and decode in place (or never: the member is rejected at that block).
+struct ZsPlan {
+    ZsLitItem* li;
+    uint32_t lcap, nl;
+    ZsSeqItem* si;
+    uint32_t scap, ns;
+    uint64_t tabs_off;   // scratch offset of the table snapshots (8 KiB Huffman, 10 KiB FSE each)
+    uint64_t seqs_off;   // scratch offset of the raw sequences
+};
+DEV void zs_plan_items(ZLane& e, zs::Tabs* T, const DeviceJob& j, uint64_t src_off, uint64_t soff, ZsPlan& P) {
     const uint64_t n = e.n;
-    uint64_t ip = 0, nlit = 0, tab = 0, ntab = 0;
-    uint32_t cnt = 0, hlog = 0, hx2 = 0;
-    bool have = false;
+    uint64_t ip = 0, nlit = 0, tab = 0, tabs = P.tabs_off, seqs = P.seqs_off;
+    uint32_t hlog = 0, hx2 = 0, llog = 0, olog = 0, mlog = 0;
+    bool have = false, fse_ok = false;
+    P.nl = P.ns = 0;
     while (ip < n) {
-        if (n - ip < 6) return cnt;
+        if (n - ip < 6) return;
         const uint32_t fhd = e.b(ip + 4);
         const uint32_t single = (fhd >> 5) & 1, fcsid = fhd >> 6;
         ip += 5 + (single ? 0 : 1) + (fcsid ? (fcsid == 1 ? 2 : fcsid == 2 ? 4 : 8) : 0) + ((single && !fcsid) ? 1 : 0);
-        have = false;  // a frame's first Huffman block must carry its tree
+        have = fse_ok = false;  // a frame's first blocks must carry their tables
         for (;;) {
-            if (n - ip < 3) return cnt;
+            if (n - ip < 3) return;
             const uint32_t bh = (uint32_t)e.le(ip, 3);
             const uint32_t last = bh & 1, bt = (bh >> 1) & 3, bsz = bh >> 3;
             ip += 3;
@@ -1562,10 +1607,16 @@ DEV uint32_t zs_plan_items(ZLane& e, zs::Tabs* T, const DeviceJob& j, uint64_t s
             if (bt == 0 || bt == 1) {
                 nlit += bsz;
             } else {
-                const uint64_t bp = ip;
+                const uint64_t bp = ip, end = ip + bsz;
                 const uint32_t b0 = e.b(bp), lt = b0 & 3, lhl = (b0 >> 2) & 3;
+                uint64_t lcons;
                 if (lt < 2) {
-                    nlit += lhl == 1 ? (e.le(bp, 2) >> 4) : lhl == 3 ? (e.le(bp, 3) >> 4) : (b0 >> 3);
+                    uint32_t lh, lsz;
+                    if (lhl == 1) lh = 2, lsz = (uint32_t)e.le(bp, 2) >> 4;
+                    else if (lhl == 3) lh = 3, lsz = (uint32_t)e.le(bp, 3) >> 4;
+                    else lh = 1, lsz = b0 >> 3;
+                    lcons = lt == 0 ? (uint64_t)lh + lsz : (uint64_t)lh + 1;
+                    nlit += lsz;
                 } else {
                     const uint32_t lhc = (uint32_t)e.le(bp, 4);
                     uint32_t lh, lsz;
@@ -1585,23 +1636,24 @@ DEV uint32_t zs_plan_items(ZLane& e, zs::Tabs* T, const DeviceJob& j, uint64_t s
                         lsz = (lhc >> 4) & 0x3FFFF;
                         lcs = (lhc >> 22) + ((uint64_t)e.b(bp + 4) << 10);
                     }
-                    if (lcs + lh > bsz || cnt >= cap) return cnt;
+                    if (lcs + lh > bsz || P.nl >= P.lcap) return;
                     uint64_t hs = bp + lh, hn = lcs;
                     if (lt == 2) {
-                        if (!one && (lsz == 0 || hn == 0)) return cnt;
+                        if (!one && (lsz == 0 || hn == 0)) return;
                         uint32_t hl = 0;
                         const int64_t th = zs::huf_table(e, T, hs, hn, hl);
-                        if (th < 0 || (uint64_t)th >= hn) return cnt;
+                        if (th < 0 || (uint64_t)th >= hn) return;
                         hlog = hl;
                         hx2 = !one && zs::huf_select_x2(lsz, lcs) ? 1u : 0u;
                         hs += (uint64_t)th;
                         hn -= (uint64_t)th;
-                        tab = tabs_off + 8192ull * ntab++;
+                        tab = tabs;
+                        tabs += 8192;
                         uint16_t* dst = (uint16_t*)(j.inf_scratch + tab);
                         for (uint32_t u = lane(); u < (1u << hl); u += 64) dst[u] = T->huf[u];
                         have = true;
                     } else if (!have) {
-                        return cnt;  // treeless without a tree: block() rejects
+                        return;  // treeless without a tree: block() rejects
                     }
                     ZsLitItem it;
                     it.src = src_off;
@@ -1620,10 +1672,10 @@ DEV uint32_t zs_plan_items(ZLane& e, zs::Tabs* T, const DeviceJob& j, uint64_t s
                         it.sn[0] = (uint32_t)hn;
                         it.cnt[0] = lsz;
                     } else {
-                        if (hn < 10) return cnt;
+                        if (hn < 10) return;
                         const uint64_t l1 = e.le(hs, 2), l2 = e.le(hs + 2, 2), l3 = e.le(hs + 4, 2);
                         const uint64_t l4 = hn - (l1 + l2 + l3 + 6);
-                        if (l4 > hn) return cnt;
+                        if (l4 > hn) return;
                         it.ns = 4;
                         it.x2 = hx2;
                         it.seg = (lsz + 3) / 4;
@@ -1638,16 +1690,67 @@ DEV uint32_t zs_plan_items(ZLane& e, zs::Tabs* T, const DeviceJob& j, uint64_t s
                         it.cnt[0] = it.cnt[1] = it.cnt[2] = it.seg;
                         it.cnt[3] = lsz > 3 * it.seg ? lsz - 3 * it.seg : 0;
                     }
-                    if (lane() == 0) items[cnt] = it;
-                    cnt++;
+                    if (lane() == 0) P.li[P.nl] = it;
+                    P.nl++;
                     nlit += lsz;
+                    lcons = lh + lcs;
+                }
+                // the sequences section header and tables (block() order)
+                uint64_t sp = bp + lcons;
+                if (sp >= end) return;
+                uint32_t nseq = e.b(sp++);
+                if (nseq == 255) {
+                    if (sp + 2 > end) return;
+                    nseq = (uint32_t)e.le(sp, 2) + 0x7F00;
+                    sp += 2;
+                } else if (nseq >= 128) {
+                    if (sp >= end) return;
+                    nseq = ((nseq - 128) << 8) + e.b(sp);
+                    sp++;
+                }
+                if (nseq) {
+                    if (sp + 1 > end || P.ns >= P.scap) return;
+                    const uint32_t modes = e.b(sp++);
+                    int64_t h = zs::seq_table(e, T, T->ll, llog, modes >> 6, 35, 9, sp, end - sp, zs::kLLBase,
+                                              zs::kLLBits, zs::kLLNorm, 35, 6, fse_ok);
+                    if (h < 0) return;
+                    sp += (uint64_t)h;
+                    h = zs::seq_table(e, T, T->of, olog, (modes >> 4) & 3, 31, 8, sp, end - sp, zs::kOFBase,
+                                      zs::kOFBits, zs::kOFNorm, 28, 5, fse_ok);
+                    if (h < 0) return;
+                    sp += (uint64_t)h;
+                    h = zs::seq_table(e, T, T->ml, mlog, (modes >> 2) & 3, 52, 9, sp, end - sp, zs::kMLBase,
+                                      zs::kMLBits, zs::kMLNorm, 52, 6, fse_ok);
+                    if (h < 0) return;
+                    sp += (uint64_t)h;
+                    fse_ok = true;
+                    // snapshot ll / of / ml (SeqSym, 8 bytes each) as dwords
+                    uint32_t* dst = (uint32_t*)(j.inf_scratch + tabs);
+                    const uint32_t* srct = (const uint32_t*)T->ll;
+                    for (uint32_t u = lane(); u < (uint32_t)(kZsSeqTab / 4); u += 64) dst[u] = srct[u];
+                    ZsSeqItem q;
+                    q.src = src_off;
+                    q.n = n;
+                    q.seqs = seqs;
+                    q.tab = tabs;
+                    q.sp = sp;
+                    q.sn = end - sp;
+                    q.nseq = nseq;
+                    q.llog = llog;
+                    q.olog = olog;
+                    q.mlog = mlog;
+                    q.status = 0;
+                    q.pad = 0;
+                    if (lane() == 0) P.si[P.ns] = q;
+                    P.ns++;
+                    tabs += kZsSeqTab;
+                    seqs += (uint64_t)nseq * sizeof(zs::RawSeq);
                 }
             }
             ip += adv;
             if (last) break;
         }
     }
-    return cnt;
 }
 
 // the fast path of zstd member i: 0 not taken (the wave decoder runs), else
@@ -1672,6 +1775,11 @@ DEV uint32_t zstd_fast_item(const DeviceJob& j, uint8_t* lds, uint32_t i, uint32
     e.items = (const ZsLitItem*)(base + uni64(D->items));
     e.nitems = uni32((uint32_t)D->nitems);
     e.hidx = 0;
+    e.sitems = (const ZsSeqItem*)(base + uni64(D->sitems));
+    e.nsitems = uni32((uint32_t)D->nsitems);
+    e.sidx = 0;
+    e.scratch = j.inf_scratch;
+    e.rpos = e.rok = 0;
     e.nlit = e.nrec = e.pend = e.mlsum = 0;
     e.bad = false;
     e.win = (inf_lds_u8*)lds;  // the ring's LDS (the wave decoder's, unused here)
@@ -1829,9 +1937,10 @@ __global__ __launch_bounds__(64) void k_members_first(DeviceJob j) {
 constexpr uint32_t kZsPending = 4;
 
 // k_zplan: per zstd member, zs_fast_size's header walk, the scratch region
-// (descriptor, literal buffer, records, literal block items, table
-// snapshots) and the items (zs_plan_items), registered in zs_items for
-// k_zlits; kZsPlanned, or kZsPending for the wave decoder
+// (descriptor, literal buffer, records, literal and sequence items, table
+// snapshots, raw sequences) and the items (zs_plan_items), registered in
+// zs_items for k_zlits (bit 63 marks a sequence item); kZsPlanned, or
+// kZsPending for the wave decoder
 __global__ __launch_bounds__(64) void k_zplan(DeviceJob j) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     const uint32_t count = j.counters[16];
@@ -1845,28 +1954,48 @@ __global__ __launch_bounds__(64) void k_zplan(DeviceJob j) {
         const uint64_t S = uni64(j.seg_off[uni32(R->segment)]) + uni64(R->file_pos) + RPGPU_HEADER_SIZE;
         const uint64_t n = (uint64_t)uni32((uint32_t)(R->size_bytes - (int32_t)RPGPU_HEADER_SIZE));
         uint64_t nl = 0, nq = 0;
-        uint32_t nh = 0;
+        uint32_t nh = 0, nsb = 0;
         uint32_t state = kZsPending;
         uint64_t soff = 0;
-        if (j.zs_fast && zs_fast_size(j.data + S, n, nl, nq, nh)) {
+        if (j.zs_fast && zs_fast_size(j.data + S, n, nl, nq, nh, nsb)) {
             const uint64_t lbytes = (nl + 16 + 15) & ~15ull, rcap = nq + 1;
-            const uint64_t ibytes = ((uint64_t)nh * sizeof(ZsLitItem) + 15) & ~15ull;
-            const uint64_t need = kZsFastHdr + lbytes + rcap * sizeof(SeqRec) + ibytes + 8192ull * nh;
+            const uint64_t o_rec = kZsFastHdr + lbytes;
+            const uint64_t o_li = o_rec + rcap * sizeof(SeqRec);
+            const uint64_t o_si = o_li + (((uint64_t)nh * sizeof(ZsLitItem) + 15) & ~15ull);
+            const uint64_t o_tab = o_si + (((uint64_t)nsb * sizeof(ZsSeqItem) + 15) & ~15ull);
+            const uint64_t o_seq = o_tab + 8192ull * nh + kZsSeqTab * nsb;
+            const uint64_t need = o_seq + nq * sizeof(zs::RawSeq) + 64 * sizeof(zs::RawSeq);
             soff = uni64(atomicAdd((unsigned long long*)j.inf_scratch_used, lane() == 0 ? (unsigned long long)need : 0ull));
             if (soff + need <= j.inf_scratch_bytes) {
-                const uint64_t io = kZsFastHdr + lbytes + rcap * sizeof(SeqRec);
                 ZLane e;
                 e.src = j.data + S;
                 e.n = n;
                 e.win = (inf_lds_u8*)lds;
                 e.rr = 0;
-                const uint32_t ni = zs_plan_items(e, T, j, S, soff, (ZsLitItem*)(j.inf_scratch + soff + io), nh,
-                                                  soff + io + ibytes);
-                const uint32_t first = wave_fetch_add(&j.counters[28], ni);
+                e.nitems = e.nsitems = 0;
+                ZsPlan P;
+                P.li = (ZsLitItem*)(j.inf_scratch + soff + o_li);
+                P.lcap = nh;
+                P.si = (ZsSeqItem*)(j.inf_scratch + soff + o_si);
+                P.scap = nsb;
+                P.tabs_off = soff + o_tab;
+                P.seqs_off = soff + o_seq;
+                zs_plan_items(e, T, j, S, soff, P);
+                const uint32_t first = wave_fetch_add(&j.counters[28], P.nl + P.ns);
                 if (lane() == 0) {
-                    for (uint32_t k = 0; k < ni && first + k < j.zs_items_cap; k++)
-                        j.zs_items[first + k] = soff + io + (uint64_t)k * sizeof(ZsLitItem);
-                    ZsFastDesc d{0, 0, kZsFastHdr, kZsFastHdr + lbytes, nl, rcap, io, ni};
+                    for (uint32_t k = 0; k < P.nl && first + k < j.zs_items_cap; k++)
+                        j.zs_items[first + k] = soff + o_li + (uint64_t)k * sizeof(ZsLitItem);
+                    for (uint32_t k = 0; k < P.ns && first + P.nl + k < j.zs_items_cap; k++)
+                        j.zs_items[first + P.nl + k] = (soff + o_si + (uint64_t)k * sizeof(ZsSeqItem)) | (1ull << 63);
+                    ZsFastDesc d{};
+                    d.lit_off = kZsFastHdr;
+                    d.rec_off = o_rec;
+                    d.lcap = nl;
+                    d.rcap = rcap;
+                    d.items = o_li;
+                    d.nitems = P.nl;
+                    d.sitems = o_si;
+                    d.nsitems = P.ns;
                     *(ZsFastDesc*)(j.inf_scratch + soff) = d;
                 }
                 state = kZsPlanned;
@@ -1897,7 +2026,35 @@ struct ZPer {
         return v;
     }
     DEV uint32_t U(uint32_t x) { return x; }
+    DEV zs::SeqSym sym(const zs::SeqSym& t) { return t; }
 };
+
+// a planned sequence section: its FSE tables into LDS, its stream decoded by
+// zs::seq_decode into raw sequences (every lane computes the same values,
+// lane 0 stores them), then whether the stream ended exactly
+DEV void zseq_item(const DeviceJob& j, zs::Tabs* T, ZsSeqItem* it) {
+    const uint32_t l = lane();
+    const uint32_t* tab = (const uint32_t*)(j.inf_scratch + uni64(it->tab));
+    uint32_t* dst = (uint32_t*)T->ll;
+    for (uint32_t u = l; u < (uint32_t)(kZsSeqTab / 4); u += 64) dst[u] = tab[u];
+    __builtin_amdgcn_s_waitcnt(0);
+    ZPer e{j.data + uni64(it->src), uni64(it->n)};
+    const uint32_t nseq = uni32(it->nseq);
+    zs::RawSeq* out = (zs::RawSeq*)(j.inf_scratch + uni64(it->seqs));
+    zs::Bits d;
+    uint32_t st = 0;
+    if (zs::bits_init(e, d, uni64(it->sp), uni64(it->sn))) {
+        zs::SeqState q;
+        zs::seq_begin(e, d, q, uni32(it->llog), uni32(it->olog), uni32(it->mlog));
+        for (uint32_t k = 0; k < nseq; k++) {
+            zs::RawSeq r;
+            zs::seq_decode(e, T, d, q, r);
+            if (l == 0) out[k] = r;
+        }
+        st = zs::bits_reload(e, d) >= zs::kCompleted ? 1u : 2u;
+    }
+    if (l == 0) it->status = st;
+}
 
 // k_zlits: one wave per planned literal block, one LANE per Huffman stream
 // (the four streams of a block are independent: lane q decodes stream q
@@ -1913,7 +2070,12 @@ __global__ __launch_bounds__(64) void k_zlits(DeviceJob j) {
     for (;;) {
         const uint32_t k = wave_fetch_add(&j.counters[29], 1u);
         if (k >= count) break;
-        ZsLitItem* it = (ZsLitItem*)(j.inf_scratch + uni64(j.zs_items[k]));
+        const uint64_t ref = uni64(j.zs_items[k]);
+        if (ref >> 63) {
+            zseq_item(j, T, (ZsSeqItem*)(j.inf_scratch + (ref & ~(1ull << 63))));
+            continue;
+        }
+        ZsLitItem* it = (ZsLitItem*)(j.inf_scratch + ref);
         const uint32_t hlog = uni32(it->hlog), ns = uni32(it->ns);
         const uint16_t* tab = (const uint16_t*)(j.inf_scratch + uni64(it->tab));
         for (uint32_t u = l; u < (1u << hlog); u += 64) T->huf[u] = tab[u];

@@ -129,12 +129,29 @@ struct FramePlan {
 // kZsFast, inf_off -> a ZsFastDesc in the scratch pool; k_zexec (rp_codec.hip)
 // executes them into their arena slots
 constexpr uint32_t kZsFast = 3;
-constexpr uint32_t kZsFastHdr = 64;  // descriptor bytes before the literal buffer
+constexpr uint32_t kZsFastHdr = 128;  // descriptor bytes before the literal buffer
 struct ZsFastDesc {
     uint64_t nlit, nrec, lit_off, rec_off;  // literal bytes, records; offsets from the descriptor
     uint64_t lcap, rcap;                    // literal buffer / record array capacities (k_zplan's header walk)
     uint64_t items, nitems;                 // the member's Huffman literal blocks (ZsLitItem), offset from the descriptor
+    uint64_t sitems, nsitems;               // its sequence sections (ZsSeqItem)
+    uint64_t pad[6];
 };
+static_assert(sizeof(ZsFastDesc) == kZsFastHdr, "descriptor size");
+// One block's sequence section, planned by k_zplan (its three FSE tables
+// snapshot, the stream) and decoded ahead by k_zlits into 16-byte raw
+// sequences (rp_zstd_core.h RawSeq: lengths and the offset code), which the
+// lane parser then only applies
+struct ZsSeqItem {
+    uint64_t src, n;   // member payload (offset in d_data), bytes
+    uint64_t seqs;     // scratch offset of its raw sequences
+    uint64_t tab;      // scratch offset of the ll / of / ml table snapshot
+    uint64_t sp, sn;   // stream start (member offset), bytes
+    uint32_t nseq, llog, olog, mlog;
+    uint32_t status;   // 0 not decoded, 1 decoded and the stream ended exactly, 2 decoded, it did not
+    uint32_t pad;
+};
+constexpr uint64_t kZsSeqTab = 10240;  // ll[512] + of[256] + ml[512] SeqSyms
 // One block's Huffman literal section, planned by k_zplan (table snapshot,
 // stream bounds, where its literals go) and decoded ahead by k_zlits, one
 // wave per block, while k_zparse later only takes the bytes

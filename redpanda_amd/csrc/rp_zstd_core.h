@@ -618,6 +618,65 @@ ZS_FN bool lits_finish(E& e, Tabs* T, Lits& L, uint32_t hlog) {
 #undef ZS_RUN
 
 // ---------------------------------------------------------------------------
+// One sequence off the bit stream (ZSTD_decodeSequence): the offset code as
+// its kind and value (the repeat offsets are applied by seq_apply), the
+// literal and match lengths; the three states advanced and the container
+// reloaded.  The bit reads are libzstd's, in its order.
+// ---------------------------------------------------------------------------
+struct RawSeq {
+    uint32_t ll, ml, v, kind;  // kind 0: new offset v; 1: repeat, no offset bit; 2: repeat code v (1..4)
+};
+struct SeqState {
+    uint32_t sll, sof, sml;
+};
+template <class E>
+ZS_FN void seq_decode(E& e, Tabs* T, Bits& d, SeqState& q, RawSeq& r) {
+    const SeqSym Ls = e.sym(T->ll[q.sll]), Ms = e.sym(T->ml[q.sml]), Os = e.sym(T->of[q.sof]);
+    const uint32_t tot = (uint32_t)Ls.nadd + Ms.nadd + Os.nadd;
+    if (Os.nadd > 1) {
+        r.kind = 0;
+        r.v = (uint32_t)(Os.base + bits_readf(d, Os.nadd));
+    } else if (Os.nadd == 0) {
+        r.kind = 1;
+        r.v = 0;
+    } else {
+        r.kind = 2;
+        r.v = Os.base + (Ls.base == 0 ? 1u : 0u) + (uint32_t)bits_readf(d, 1);
+    }
+    uint64_t ml = Ms.base;
+    if (Ms.nadd) ml += bits_readf(d, Ms.nadd);
+    if (tot >= 31) bits_reload(e, d);
+    uint64_t ll = Ls.base;
+    if (Ls.nadd) ll += bits_readf(d, Ls.nadd);
+    q.sll = Ls.next + (uint32_t)bits_read(d, Ls.nbits);
+    q.sml = Ms.next + (uint32_t)bits_read(d, Ms.nbits);
+    q.sof = Os.next + (uint32_t)bits_read(d, Os.nbits);
+    bits_reload(e, d);
+    r.ll = (uint32_t)ll;
+    r.ml = (uint32_t)ml;
+}
+// the stream's initial states (after bits_init)
+template <class E>
+ZS_FN void seq_begin(E& e, Bits& d, SeqState& q, uint32_t llog, uint32_t olog, uint32_t mlog) {
+    q.sll = (uint32_t)bits_read(d, llog);
+    bits_reload(e, d);
+    q.sof = (uint32_t)bits_read(d, olog);
+    bits_reload(e, d);
+    q.sml = (uint32_t)bits_read(d, mlog);
+    bits_reload(e, d);
+}
+
+// An environment may take a block's sequences decoded ahead (E::seqs_take:
+// the same seq_decode from the same tables and stream, all of them, and the
+// stream's end verdict): block() then only applies them (repeat offsets,
+// the reference's checks, literals, matches).  The verdict is unchanged:
+// every failure inside a block rejects the payload, whichever comes first.
+template <class E>
+struct EagerSeqs {
+    static constexpr bool value = false;
+};
+
+// ---------------------------------------------------------------------------
 // Frame state and one compressed block
 // ---------------------------------------------------------------------------
 struct Frame {
@@ -770,50 +829,44 @@ ZS_FN int64_t block(E& e, Tabs* T, Frame& F, uint64_t bp, uint64_t bn, uint64_t 
         // ZSTD_decompressSequences_body
         F.fse_ok = true;
         uint64_t r0 = F.rep[0], r1 = F.rep[1], r2 = F.rep[2];
+        bool pre = false;
+        if constexpr (EagerSeqs<E>::value) pre = e.seqs_take(sp, end - sp, nseq, F.llog, F.olog, F.mlog);
         Bits d;
-        if (!bits_init(e, d, sp, end - sp)) return -1;
-        uint32_t sll = (uint32_t)bits_read(d, F.llog);
-        bits_reload(e, d);
-        uint32_t sof = (uint32_t)bits_read(d, F.olog);
-        bits_reload(e, d);
-        uint32_t sml = (uint32_t)bits_read(d, F.mlog);
-        bits_reload(e, d);
+        SeqState q;
+        if (!pre) {
+            if (!bits_init(e, d, sp, end - sp)) return -1;
+            seq_begin(e, d, q, F.llog, F.olog, F.mlog);
+        }
         for (;;) {
-            const SeqSym Ls = e.sym(T->ll[sll]), Ms = e.sym(T->ml[sml]), Os = e.sym(T->of[sof]);
-            const uint32_t tot = (uint32_t)Ls.nadd + Ms.nadd + Os.nadd;
+            RawSeq rs;
+            if constexpr (EagerSeqs<E>::value) {
+                if (pre) e.seq_next(rs);
+                else seq_decode(e, T, d, q, rs);
+            } else {
+                seq_decode(e, T, d, q, rs);
+            }
             uint64_t off;
-            if (Os.nadd > 1) {
-                off = Os.base + bits_readf(d, Os.nadd);
+            if (rs.kind == 0) {
+                off = rs.v;
                 r2 = r1;
                 r1 = r0;
                 r0 = off;
-            } else {
-                const bool ll0 = Ls.base == 0;
-                if (Os.nadd == 0) {
-                    if (!ll0) {
-                        off = r0;
-                    } else {
-                        off = r1;
-                        r1 = r0;
-                        r0 = off;
-                    }
+            } else if (rs.kind == 1) {
+                if (rs.ll != 0) {
+                    off = r0;
                 } else {
-                    off = Os.base + (ll0 ? 1u : 0u) + bits_readf(d, 1);
-                    uint64_t t = off == 3 ? r0 - 1 : (off == 1 ? r1 : r2);
-                    t += !t;
-                    if (off != 1) r2 = r1;
+                    off = r1;
                     r1 = r0;
-                    r0 = off = t;
+                    r0 = off;
                 }
+            } else {
+                uint64_t t = rs.v == 3 ? r0 - 1 : (rs.v == 1 ? r1 : r2);
+                t += !t;
+                if (rs.v != 1) r2 = r1;
+                r1 = r0;
+                r0 = off = t;
             }
-            uint64_t ml = Ms.base;
-            if (Ms.nadd) ml += bits_readf(d, Ms.nadd);
-            if (tot >= 31) bits_reload(e, d);
-            uint64_t ll = Ls.base;
-            if (Ls.nadd) ll += bits_readf(d, Ls.nadd);
-            sll = Ls.next + (uint32_t)bits_read(d, Ls.nbits);
-            sml = Ms.next + (uint32_t)bits_read(d, Ms.nbits);
-            sof = Os.next + (uint32_t)bits_read(d, Os.nbits);
+            const uint64_t ll = rs.ll, ml = rs.ml;
             // ZSTD_execSequence's checks, then the copies
             if (ll + ml > capb - bo) return -1;
             if (ll > (uint64_t)(L.size - L.used)) return -1;
@@ -833,10 +886,13 @@ ZS_FN int64_t block(E& e, Tabs* T, Frame& F, uint64_t bp, uint64_t bn, uint64_t 
             ZS_PROF(1, e.match(off, ml));
             bo += ml;
             F.fo += ml;
-            bits_reload(e, d);
             if (--nseq == 0) break;
         }
-        if (bits_reload(e, d) < kCompleted) return -1;
+        if constexpr (EagerSeqs<E>::value) {
+            if (pre ? !e.seqs_ok() : bits_reload(e, d) < kCompleted) return -1;
+        } else {
+            if (bits_reload(e, d) < kCompleted) return -1;
+        }
         F.rep[0] = r0;
         F.rep[1] = r1;
         F.rep[2] = r2;

@@ -72,6 +72,25 @@ struct HostEnv {
 struct EagerHostEnv : HostEnv {
     std::vector<uint8_t> blk;
     size_t took = 0;
+    // eager sequences (rp::zs::EagerSeqs, as k_zlits decodes them ahead):
+    // the block's whole sequence stream decoded at once, then applied
+    rp::zs::Tabs* T = nullptr;
+    std::vector<rp::zs::RawSeq> seqs;
+    size_t next = 0;
+    bool ok = false;
+    bool seqs_take(uint64_t sp, uint64_t n, uint32_t nseq, uint32_t llog, uint32_t olog, uint32_t mlog) {
+        rp::zs::Bits d;
+        if (!rp::zs::bits_init(*this, d, sp, n)) return false;  // block() rejects in place
+        rp::zs::SeqState q;
+        rp::zs::seq_begin(*this, d, q, llog, olog, mlog);
+        seqs.resize(nseq);
+        for (uint32_t k = 0; k < nseq; k++) rp::zs::seq_decode(*this, T, d, q, seqs[k]);
+        ok = rp::zs::bits_reload(*this, d) >= rp::zs::kCompleted;
+        next = 0;
+        return true;
+    }
+    void seq_next(rp::zs::RawSeq& r) { r = seqs[next++]; }
+    bool seqs_ok() const { return ok; }
     void take(uint64_t k) {
         out.insert(out.end(), blk.begin() + took, blk.begin() + took + k);
         took += k;
@@ -94,12 +113,17 @@ template <>
 struct rp::zs::EagerLits<EagerHostEnv> {
     static constexpr bool value = true;
 };
+template <>
+struct rp::zs::EagerSeqs<EagerHostEnv> {
+    static constexpr bool value = true;
+};
 
 extern "C" int zs_host_decode_eager(const uint8_t* src, uint64_t n, uint8_t* dst, uint64_t cap, uint64_t* total) {
     static rp::zs::Tabs T;
     EagerHostEnv e;
     e.src = src;
     e.n = n;
+    e.T = &T;
     uint64_t t = 0;
     bool unsure = false;
     const int rc = n == 0 ? -1 : rp::zs::payload(e, &T, n, t, unsure);
