@@ -1339,6 +1339,28 @@ struct ZLane {
         nlit += k;
         pend += k;
     }
+    // a raw / RLE literal section in place at nlit, at once (16 bytes per lane)
+    DEV void raw_ahead(uint64_t pos, uint64_t k) {
+        typedef __attribute__((address_space(1))) uint8_t g8;
+        if (nlit + k > lcap) {
+            bad = true;
+            return;
+        }
+        const uint64_t body = k & ~1023ull;
+        for (uint64_t c = 16u * lane(); c < body; c += 1024) {
+            uint4 v;
+            __builtin_memcpy(&v, (const g8*)(src + pos + c), 16);
+            __builtin_memcpy((g8*)(lits + nlit + c), &v, 16);
+        }
+        for (uint64_t c = body + lane(); c < k; c += 64) lits[nlit + c] = src[pos + c];
+    }
+    DEV void fill_ahead(uint32_t v, uint64_t k) {
+        if (nlit + k > lcap) {
+            bad = true;
+            return;
+        }
+        for (uint64_t c = lane(); c < k; c += 64) lits[nlit + c] = (uint8_t)v;
+    }
     DEV uint32_t hbits(const zs::Bits& s, uint32_t hlog) {
         return (uint32_t)((s.c << (s.used & 63)) >> ((64 - hlog) & 63));
     }

@@ -545,9 +545,10 @@ ZS_FN void huf_run(E& e, Tabs* T, Bits& s, uint32_t& open, uint32_t left, uint32
     }
 }
 
-// An environment that keeps literals in a buffer of its own may decode a
-// block's Huffman literals eagerly, all streams at once (E::huf_all, as
-// HUF_decompress4X interleaves them); lits_emit then only takes them.  The
+// An environment that keeps literals in a buffer of its own may produce a
+// block's literals eagerly: Huffman ones all streams at once (E::huf_all, as
+// HUF_decompress4X interleaves them), raw and RLE ones in one copy or fill
+// (E::raw_ahead / E::fill_ahead); lits_emit then only takes them.  The
 // symbols, and the stream states lits_finish checks, are those of the lazy
 // consumption-order decode (no check happens between two symbols).
 template <class E>
@@ -560,14 +561,14 @@ struct EagerLits {
 
 template <class E>
 ZS_FN void lits_emit(E& e, Tabs* T, Lits& L, uint32_t k, uint32_t hlog) {
-    if (L.kind == 0) {
+    if constexpr (EagerLits<E>::value) {  // every kind already in place (raw_ahead, fill_ahead, huf_all)
+        e.take(k);
+        L.used += k;
+    } else if (L.kind == 0) {
         e.raw(L.pos + L.used, k);
         L.used += k;
     } else if (L.kind == 1) {
         e.fill(L.rle, k);
-        L.used += k;
-    } else if constexpr (EagerLits<E>::value) {
-        e.take(k);
         L.used += k;
     } else {
         while (k) {
@@ -729,6 +730,11 @@ ZS_FN int64_t block(E& e, Tabs* T, Frame& F, uint64_t bp, uint64_t bn, uint64_t 
             lcons = lh + 1u;
         }
         L.size = lsz;
+        // eager: the block's raw / RLE literals in place at once
+        if constexpr (EagerLits<E>::value) {
+            if (L.kind == 0) e.raw_ahead(L.pos, lsz);
+            else e.fill_ahead(L.rle, lsz);
+        }
     } else {
         if (lt == 3 && !F.lit_ok) return -1;
         if (bn < 5) return -1;

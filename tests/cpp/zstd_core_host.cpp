@@ -95,6 +95,14 @@ struct EagerHostEnv : HostEnv {
         out.insert(out.end(), blk.begin() + took, blk.begin() + took + k);
         took += k;
     }
+    void raw_ahead(uint64_t pos, uint64_t k) {
+        blk.assign(src + pos, src + pos + k);
+        took = 0;
+    }
+    void fill_ahead(uint32_t v, uint64_t k) {
+        blk.assign((size_t)k, (uint8_t)v);
+        took = 0;
+    }
     void huf_all(rp::zs::Tabs* T, rp::zs::Lits& L, uint32_t hlog) {
         blk.assign(L.size, 0);
         took = 0;
