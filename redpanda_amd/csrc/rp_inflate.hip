@@ -1258,7 +1258,11 @@ struct ZLane {
 #ifdef RPGPU_ZSTAMPS
     uint64_t prof[4];
 #endif
+#ifdef RPGPU_ZL_UNI  // (A/B: header bytes and table reads wave-uniform)
+    DEV uint32_t b(uint64_t i) { return uni32(i < n ? (uint32_t)src[i] : 0u); }
+#else
     DEV uint32_t b(uint64_t i) { return i < n ? (uint32_t)src[i] : 0u; }
+#endif
     DEV uint64_t le(uint64_t i, uint32_t k) {
         uint64_t v = 0;
         for (uint32_t t = 0; t < k; t++) v |= (uint64_t)b(i + t) << (8 * t);
@@ -1291,8 +1295,20 @@ struct ZLane {
     // (values stay in VGPRs: making the table reads wave-uniform, so that the
     // state moves to SGPRs and branches on SCC, measured 140 -> 159 ms per
     // 1 MiB member)
+#ifdef RPGPU_ZL_UNI
+    DEV uint32_t U(uint32_t x) { return uni32(x); }
+    DEV zs::SeqSym sym(const zs::SeqSym& t) {
+        uint64_t v;
+        __builtin_memcpy(&v, &t, 8);
+        v = uni64(v);
+        zs::SeqSym r;
+        __builtin_memcpy(&r, &v, 8);
+        return r;
+    }
+#else
     DEV uint32_t U(uint32_t x) { return x; }
     DEV zs::SeqSym sym(const zs::SeqSym& t) { return t; }
+#endif
     DEV void lit(uint32_t v) {
         if (nlit >= lcap) bad = true;
         else if (lane() == 0) lits[nlit] = (uint8_t)v;
