@@ -1444,6 +1444,91 @@ struct ZLane {
         rpos++;
     }
     DEV bool seqs_ok() { return rok != 0; }
+    // inclusive prefix sum over the wave (DPP row shifts, then the row
+    // broadcasts; as rp_codec.hip's wave_scan)
+    static DEV uint32_t scan(uint32_t v) {
+        v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xF, 0xF, true);
+        v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xF, 0xF, true);
+        v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xF, 0xF, true);
+        v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xF, 0xF, true);
+        v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xA, 0xF, false);
+        v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xC, 0xF, false);
+        return v;
+    }
+    // zs::EagerSeqs: block()'s loop over a taken section, 64 sequences per
+    // step, lane k holding sequence 64 c + k: the repeat offsets resolved in
+    // order (a scalar pass over the 64), the positions before each sequence
+    // by prefix sums of its lengths, every check of the loop per lane (any
+    // lane failing rejects, as the first failure in order would), then the
+    // 16-byte records written together
+    DEV bool seqs_apply(zs::Frame& F, zs::Lits& L, uint64_t& r0, uint64_t& r1, uint64_t& r2, uint64_t& bo,
+                        uint64_t capb, uint32_t nseq) {
+        const uint32_t l = lane();
+        for (uint32_t c = 0; c < nseq; c += 64) {
+            const uint32_t m = nseq - c < 64 ? nseq - c : 64u;
+            const bool on = l < m;
+            uint4 q = make_uint4(0u, 0u, 0u, 0u);
+            if (on) q = *(const uint4*)(rseq + c + l);
+            const uint32_t ll = q.x, ml = q.y;
+            // the repeat offsets, in order
+            uint64_t myoff = 0;
+            for (uint32_t k = 0; k < m; k++) {
+                const uint32_t kind = (uint32_t)__builtin_amdgcn_readlane((int)q.w, (int)k);
+                const uint32_t v = (uint32_t)__builtin_amdgcn_readlane((int)q.z, (int)k);
+                const uint32_t lk = (uint32_t)__builtin_amdgcn_readlane((int)q.x, (int)k);
+                uint64_t off;
+                if (kind == 0) {
+                    off = v;
+                    r2 = r1;
+                    r1 = r0;
+                    r0 = off;
+                } else if (kind == 1) {
+                    if (lk != 0) {
+                        off = r0;
+                    } else {
+                        off = r1;
+                        r1 = r0;
+                        r0 = off;
+                    }
+                } else {
+                    uint64_t t = v == 3 ? r0 - 1 : (v == 1 ? r1 : r2);
+                    t += !t;
+                    if (v != 1) r2 = r1;
+                    r1 = r0;
+                    r0 = off = t;
+                }
+                if (l == k) myoff = off;
+            }
+            // positions before this lane's sequence
+            const uint32_t lli = scan(ll), mli = scan(ml);
+            const uint64_t lle = lli - ll, mle = mli - ml;
+            const uint64_t bok = bo + lle + mle;
+            const uint64_t usedk = (uint64_t)L.used + lle;
+            const uint64_t fok = F.fo + lle + ll + mle;  // after this sequence's literals
+            bool fail = (uint64_t)ll + ml > capb - bok;
+            fail = fail || (uint64_t)ll > (uint64_t)L.size - usedk;
+            fail = fail || myoff > fok - F.seg0 + F.prevlen;
+            fail = fail || (myoff > fok - F.seg0 && F.prevlen - (myoff - (fok - F.seg0)) < fok - F.seg0 + zs::kRingDirty);
+            if (__ballot(on && fail)) return false;
+            if (nrec + m > rcap) {
+                bad = true;
+            } else if (on) {
+                const uint32_t lip = l == 0 ? (uint32_t)(nlit - pend) : (uint32_t)(nlit + lle);
+                const uint32_t lln = l == 0 ? (uint32_t)(pend + ll) : ll;
+                recs[nrec + l] = SeqRec{lip, lln, ml, (uint32_t)myoff};
+            }
+            const uint64_t lt = (uint32_t)__builtin_amdgcn_readlane((int)lli, (int)(m - 1));
+            const uint64_t mt = (uint32_t)__builtin_amdgcn_readlane((int)mli, (int)(m - 1));
+            bo += lt + mt;
+            F.fo += lt + mt;
+            L.used += (uint32_t)lt;
+            nlit += lt;
+            pend = 0;
+            nrec += m;
+            mlsum += mt;
+        }
+        return true;
+    }
     DEV void huf_all_(zs::Tabs* T, zs::Lits& L, uint32_t hlog) {
         const uint64_t at = nlit;
         if (at + L.size > lcap) {

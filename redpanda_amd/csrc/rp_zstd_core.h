@@ -843,7 +843,17 @@ ZS_FN int64_t block(E& e, Tabs* T, Frame& F, uint64_t bp, uint64_t bn, uint64_t 
             if (!bits_init(e, d, sp, end - sp)) return -1;
             seq_begin(e, d, q, F.llog, F.olog, F.mlog);
         }
-        for (;;) {
+        // a pre-decoded section is applied by the environment in one go
+        // (E::seqs_apply: the loop below, the same checks in the same
+        // arithmetic, any failure rejecting the payload)
+        bool applied = false;
+        if constexpr (EagerSeqs<E>::value) {
+            if (pre) {
+                if (!e.seqs_apply(F, L, r0, r1, r2, bo, capb, nseq)) return -1;
+                applied = true;
+            }
+        }
+        for (; !applied;) {
             RawSeq rs;
             if constexpr (EagerSeqs<E>::value) {
                 if (pre) e.seq_next(rs);

@@ -90,6 +90,38 @@ struct EagerHostEnv : HostEnv {
         return true;
     }
     void seq_next(rp::zs::RawSeq& r) { r = seqs[next++]; }
+    // the block() loop over the taken sequences (the device applies 64 at a
+    // time across lanes; here the plain restatement, pinning the hook)
+    bool seqs_apply(rp::zs::Frame& F, rp::zs::Lits& L, uint64_t& r0, uint64_t& r1, uint64_t& r2, uint64_t& bo,
+                    uint64_t capb, uint32_t nseq) {
+        for (uint32_t k = 0; k < nseq; k++) {
+            const rp::zs::RawSeq& s = seqs[k];
+            uint64_t off;
+            if (s.kind == 0) { off = s.v; r2 = r1; r1 = r0; r0 = off; }
+            else if (s.kind == 1) { if (s.ll != 0) off = r0; else { off = r1; r1 = r0; r0 = off; } }
+            else {
+                uint64_t t = s.v == 3 ? r0 - 1 : (s.v == 1 ? r1 : r2);
+                t += !t;
+                if (s.v != 1) r2 = r1;
+                r1 = r0;
+                r0 = off = t;
+            }
+            const uint64_t ll = s.ll, ml = s.ml;
+            if (ll + ml > capb - bo) return false;
+            if (ll > (uint64_t)(L.size - L.used)) return false;
+            take(ll);
+            L.used += (uint32_t)ll;
+            bo += ll;
+            F.fo += ll;
+            if (off > F.fo - F.seg0 + F.prevlen) return false;
+            if (off > F.fo - F.seg0 && F.prevlen - (off - (F.fo - F.seg0)) < F.fo - F.seg0 + rp::zs::kRingDirty)
+                return false;
+            match(off, ml);
+            bo += ml;
+            F.fo += ml;
+        }
+        return true;
+    }
     bool seqs_ok() const { return ok; }
     void take(uint64_t k) {
         out.insert(out.end(), blk.begin() + took, blk.begin() + took + k);
