@@ -1,17 +1,8 @@
-# round check: parity tests, smoke, the bench line (C1 headline + C2/C5
-# stanzas with CPU baselines), then a kernel trace of the compressed
-# workloads.  Every GPU step bounded, chained with &&; TAG names the outputs.
+# Round end on the final tree: PMC traffic + kernel trace of the bench
+# (scripts/gpu_traffic.sh TAG; then scripts/parse_traffic.py TAG here), the
+# GPU suite, smoke() and the driver's exact bench command (scripts/gpu_final.sh).
 set -e
 cd "$GRAFT_REPO_ROOT"
-export TMPDIR=/tmp
-TAG=${1:-r02}
-timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 240 --timeout-method thread > gpurun_out/pytest_gpu_$TAG.log 2>&1 || { tail -60 gpurun_out/pytest_gpu_$TAG.log; exit 1; }
-tail -3 gpurun_out/pytest_gpu_$TAG.log
-timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke_$TAG.log 2>&1 || { tail -20 gpurun_out/smoke_$TAG.log; exit 1; }
-tail -1 gpurun_out/smoke_$TAG.log
-timeout -k 10 600 python -u bench.py > gpurun_out/bench_$TAG.json 2> gpurun_out/bench_$TAG.err || { tail -30 gpurun_out/bench_$TAG.err; exit 1; }
-cat gpurun_out/bench_$TAG.json
-if [ "${2:-}" = "prof" ]; then
-timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$TAG -o $TAG --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-index > gpurun_out/prof_$TAG.log 2>&1
-echo "prof ok"
-fi
+TAG=${1:-r04}
+bash scripts/gpu_traffic.sh $TAG
+bash scripts/gpu_final.sh $TAG
