@@ -289,18 +289,17 @@ struct InfOut {
 // flush output bytes [o.flushed, o.flushed + len) (len <= 1024, the start
 // 1 KiB aligned) from the ring and fold them into the check
 DEV void inf_flush(InfOut& o, uint32_t len) {
-    if (o.over || o.flushed + len > o.cap) {  // the slot is full: count only
-        o.over = true;
-        o.flushed += len;
-        return;
-    }
+    // the slot is full: the bytes are no longer stored, but the check still
+    // folds them in (a member whose check then fails is rejected by this pass
+    // and needs no second one)
+    if (o.over || o.flushed + len > o.cap) o.over = true;
     const uint32_t l = lane();
     const uint32_t at = (uint32_t)(o.flushed & kInfMask) + 16u * l;
     const uint32_t t = 16u * l < len ? min(16u, len - 16u * l) : 0u;  // this lane's bytes
     uint4 v = make_uint4(0, 0, 0, 0);
     if (t) {
         v = *(const uint4*)(o.ring + at);
-        *(uint4*)(o.dst + o.flushed + 16u * l) = v;  // the slot is rounded up to 16: a whole piece fits
+        if (!o.over) *(uint4*)(o.dst + o.flushed + 16u * l) = v;  // the slot is rounded up to 16: a whole piece fits
     }
     const uint32_t w[4] = {v.x, v.y, v.z, v.w};
     if (o.gz) {
@@ -723,7 +722,9 @@ DEV int inflate_member(InfIn& in, InfTabs* T, InfOut& o, const InfSymTabs& ST, u
         NEED(32);
         if (op > o.flushed) inf_flush(o, (uint32_t)(op - o.flushed));
         total = op;
-        if (o.over) return 0;  // no bytes held to check: a second pass decides
+        // (an outgrown slot holds no bytes, but the check was folded: a
+        // failing one rejects here, a passing one leaves the member to the
+        // second pass, which writes its bytes into the arena)
         const uint32_t w = inf_peek(in, bp);
         if (gz) {
             if (w != ~o.crc) return -2;  // incorrect data check
