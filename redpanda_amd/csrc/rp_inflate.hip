@@ -893,6 +893,412 @@ DEV void gzip_item(const DeviceJob& j, uint8_t* lds, InfTabs* T, const InfWave& 
 }
 
 // ---------------------------------------------------------------------------
+// Split decode of large gzip members.  A member decodes serially on one wave
+// (above), so a job's member pass is as long as its largest member.  A gzip
+// member of >= kGzsMin stored bytes is cut instead into chunks of kGzsChunk
+// deflate bytes, one wave each:
+//   k_gzsplan    parses the gzip header (FHCRC members stay serial) and lists
+//                the member's chunks (GzsItem);
+//   k_gzsfind    finds the first dynamic-block header in each chunk k >= 1:
+//                lanes test 64 bit offsets at a time (block type, HLIT, HDIST
+//                and a complete code-length code), survivors are queued and
+//                each lane decodes one survivor's code lengths through its own
+//                7-bit table (complete literal/length and distance codes,
+//                end-of-block present: what a valid header satisfies);
+//   k_gzsdecode  decodes each chunk from its block start until the block
+//                boundary where the next chunk's start lies, into a 16-bit
+//                symbol region (a byte, or 256 + a position in the 32 KiB
+//                before the chunk: a match reaching before the chunk's start
+//                copies those placeholders -- the ring is primed with them);
+//   k_gzsresolve walks the chain from chunk 0 (each chunk must end where the
+//                next one begins, so a false start is never used), writes the
+//                bytes into a scratch slot with the placeholders replaced from
+//                the bytes before each chunk, computes the CRC32 in 256 pieces
+//                and sets the member's plan and state as gzip_first_item does.
+// The verdicts are those of inflate_member: a stream error in a chained chunk
+// (or a placeholder before the member's start: a distance too far back)
+// rejects; running out of input accepts what decoded; the CRC32 / ISIZE rules
+// of the CHECK section.  A member whose chain does not close (a false start, a
+// stored or fixed block at a chunk seam, a region outgrown) is left to
+// k_members_first, which decodes it serially as before.
+// ---------------------------------------------------------------------------
+typedef __attribute__((address_space(3))) uint16_t gzs_lds_u16;
+constexpr uint32_t kGzsLds = 2 * kInfRing + kInfTabBytes;
+
+struct GzsOut {
+    gzs_lds_u16* ring;  // 32 K symbols
+    uint16_t* dst;      // the chunk's region in the pool
+    uint64_t flushed, cap;
+    bool over;
+};
+
+// symbols [flushed, flushed + len) (len <= 1024, the start 1 K aligned) to
+// the region: 16 per lane (32 bytes)
+DEV void gzs_flush(GzsOut& o, uint32_t len) {
+    if (o.over || o.flushed + len > o.cap) {
+        o.over = true;
+    } else {
+        const uint32_t l = lane();
+        if (16u * l < len) {
+            const uint32_t at = (uint32_t)(o.flushed & kInfMask) + 16u * l;
+            const uint4 a = *(const uint4*)(o.ring + at), b = *(const uint4*)(o.ring + at + 8);
+            uint4* d = (uint4*)(o.dst + o.flushed + 16u * l);  // the region is a whole number of 1 K pieces
+            d[0] = a;
+            d[1] = b;
+        }
+    }
+    o.flushed += len;
+}
+DEV void gzs_flush_upto(GzsOut& o, uint64_t op) {
+    while ((op >> 10) > (o.flushed >> 10)) gzs_flush(o, 1024u);
+}
+// inf_copy over 16-bit symbols
+DEV void gzs_copy(gzs_lds_u16* ring, uint64_t op, uint32_t dist, uint32_t ml) {
+    const uint32_t l = lane();
+    const bool rep = dist < ml;
+    const uint64_t mg = rep ? 0xFFFFFFFFull / dist + 1ull : 0ull;
+    const uint32_t n = (ml + 63) >> 6;
+    uint32_t b[5];
+#pragma unroll
+    for (uint32_t i = 0; i < 5; i++) {
+        const uint32_t k = 64u * i + l;
+        const uint32_t x = rep ? k - (uint32_t)(((uint64_t)k * mg) >> 32) * dist : k;
+        b[i] = (i < n && k < ml) ? (uint32_t)ring[((uint32_t)(op - dist) + x) & kInfMask] : 0u;
+    }
+#pragma unroll
+    for (uint32_t i = 0; i < 5; i++) {
+        const uint32_t k = 64u * i + l;
+        if (i < n && k < ml) ring[(uint32_t)(op + k) & kInfMask] = (uint16_t)b[i];
+    }
+}
+
+// Decode blocks from bit bp (a block header) until a block boundary at
+// `stop`.  marks: matches may reach before the start (placeholders), else
+// such a distance is the stream error it is.  Returns 1 stopped at `stop`, 2
+// the final block ended (bp: its end), 3 the input ran out (inflate_member's
+// `done`), -1 a stream error, -3 the region was outgrown, -4 passed `stop`
+// (a false start); `total` = symbols decoded.
+DEV int gzs_run(InfIn& in, InfTabs* T, GzsOut& o, const InfSymTabs& ST, uint64_t& bp, uint64_t stop, bool marks,
+                uint64_t& total) {
+    const uint32_t l = lane();
+    const uint64_t nbits = in.n * 8;
+    uint64_t op = 0;
+    uint32_t v, sym, len;
+    InfCode LC, DC, CC;
+    int st = 0;
+#define GNEED(k)                          \
+    if (nbits - bp < (uint64_t)(k)) {     \
+        st = 3;                           \
+        goto out;                         \
+    }
+#define GFAIL  \
+    {          \
+        st = -1; \
+        goto out; \
+    }
+    for (;;) {
+        if (bp == stop) { st = 1; break; }
+        if (bp > stop) { st = -4; break; }
+        GNEED(3);
+        v = inf_peek(in, bp);
+        const uint32_t last = v & 1u, type = (v >> 1) & 3u;
+        bp += 3;
+        if (type == 0) {  // STORED
+            bp = (bp + 7) & ~7ull;
+            GNEED(32);
+            v = inf_peek(in, bp);
+            if ((v & 0xFFFFu) != ((v >> 16) ^ 0xFFFFu)) GFAIL;
+            bp += 32;
+            const uint64_t length = v & 0xFFFFu;
+            const uint64_t p = bp >> 3, have = in.n - p, copy = length < have ? length : have;
+            for (uint64_t c = 0; c < copy; c += 1024) {
+#pragma unroll
+                for (uint32_t k = 0; k < 16; k++) {
+                    const uint64_t i = c + 16u * l + k;
+                    if (i < copy) o.ring[(uint32_t)(op + i - c) & kInfMask] = (uint16_t)in.src[p + i];
+                }
+                op += copy - c < 1024 ? copy - c : 1024;
+                gzs_flush_upto(o, op);
+            }
+            bp += 8 * copy;
+            if (copy < length) { st = 3; goto out; }
+        } else if (type == 3) {
+            GFAIL;
+        } else {
+            inf_lds_u8* lens = (inf_lds_u8*)T->lens;
+            if (type == 1) {
+                for (uint32_t s = l; s < 288; s += 64) lens[s] = s < 144 ? 8 : s < 256 ? 9 : s < 280 ? 7 : 8;
+                inf_build(lens, 288, 1, T->lsym, LC);
+                if (l < 32) lens[l] = 5;
+                inf_build(lens, 32, 2, T->dsym, DC);
+            } else {
+                GNEED(14);
+                v = inf_peek(in, bp);
+                const uint32_t nlen = (v & 31u) + 257, ndist = ((v >> 5) & 31u) + 1, ncode = ((v >> 10) & 15u) + 4;
+                bp += 14;
+                if (nlen > 286 || ndist > 30) GFAIL;
+                const uint64_t need = 3ull * ncode;
+                const bool all = nbits - bp >= need;
+                const uint32_t got = all ? ncode : (uint32_t)((nbits - bp) / 3);
+                const uint64_t w57 = inf_peek64(in, bp);
+                const uint32_t cl = l < got ? (uint32_t)(w57 >> (3 * (l < 19 ? l : 0))) & 7u : 0u;
+                if (!all) { st = 3; goto out; }
+                bp += need;
+                if (l < 19) lens[kClenOrder[l]] = (uint8_t)(l < ncode ? cl : 0u);
+                if (inf_build(lens, 19, 0, T->csym, CC)) GFAIL;
+                uint32_t have = 0;
+                while (have < nlen + ndist) {
+                    v = inf_peek(in, bp);
+                    const int r = inf_decode(v, nbits - bp, CC, T->csym, sym, len);
+                    if (r == 0) { st = 3; goto out; }
+                    if (r < 0) { sym = 0; len = 1; }
+                    bp += len;
+                    if (sym < 16) {
+                        if (l == 0) lens[have] = (uint8_t)sym;
+                        have++;
+                        continue;
+                    }
+                    uint32_t rep = 0, cnt;
+                    v = inf_peek(in, bp);
+                    if (sym == 16) {
+                        GNEED(2);
+                        if (have == 0) GFAIL;
+                        rep = uni32((uint32_t)lens[have - 1]);
+                        cnt = 3 + (v & 3u);
+                        bp += 2;
+                    } else if (sym == 17) {
+                        GNEED(3);
+                        cnt = 3 + (v & 7u);
+                        bp += 3;
+                    } else {
+                        GNEED(7);
+                        cnt = 11 + (v & 127u);
+                        bp += 7;
+                    }
+                    if (have + cnt > nlen + ndist) GFAIL;
+                    if (l < cnt) lens[have + l] = (uint8_t)rep;
+                    if (l + 64 < cnt) lens[have + l + 64] = (uint8_t)rep;
+                    if (l + 128 < cnt) lens[have + l + 128] = (uint8_t)rep;
+                    have += cnt;
+                }
+                if (lens[256] == 0) GFAIL;
+                if (inf_build(lens, nlen, 1, T->lsym, LC)) GFAIL;
+                if (inf_build(lens + nlen, ndist, 2, T->dsym, DC)) GFAIL;
+            }
+            inf_root(LC, T->lsym, T->lroot);
+            inf_root(DC, T->dsym, T->droot);
+            // fast loop (inflate_member's, over 16-bit symbols)
+            {
+                const uint64_t pb = bp + 8ull * in.mis;
+                uint64_t pq = (pb >> 5) << 2;
+                uint32_t sh = (uint32_t)(pb & 31);
+                uint64_t bb = (uint64_t)(inf_dw(in, pq) >> sh);
+                uint32_t bc = 32 - sh;
+                pq += 4;
+                bool eob = false, bad = false;
+                uint32_t lb = 0, nl = 0;
+                auto spill = [&]() __attribute__((always_inline)) {
+                    if (nl) {
+                        if (l < nl) o.ring[(uint32_t)(op + l) & kInfMask] = (uint16_t)lb;
+                        op += nl;
+                        nl = 0;
+                        gzs_flush_upto(o, op);
+                    }
+                };
+                while (pq + 12 <= in.nphys) {
+                    while (bc <= 32) {
+                        bb |= (uint64_t)inf_dw(in, pq) << bc;
+                        bc += 32;
+                        pq += 4;
+                    }
+                    uint32_t e = uni32((uint32_t)T->lroot[(uint32_t)bb & 511u]);
+                    if (e == 0) {
+                        const int r = inf_decode((uint32_t)bb, 64, LC, T->lsym, sym, len);
+                        if (r < 0) { bad = true; break; }
+                        e = sym | (len << 9);
+                    }
+                    sym = e & 511u;
+                    len = e >> 9;
+                    bb >>= len;
+                    bc -= len;
+                    if (sym < 256) {
+                        lb = l == nl ? sym : lb;
+                        if (++nl == 64) spill();
+                        continue;
+                    }
+                    spill();
+                    if (sym == 256) { eob = true; break; }
+                    if (sym > 285) { bad = true; break; }
+                    const uint32_t lt = rl(ST.len, (int)(sym - 257));
+                    const uint32_t le = lt >> 16;
+                    const uint32_t ml = (lt & 0xFFFFu) + ((uint32_t)bb & ((1u << le) - 1u));
+                    bb >>= le;
+                    bc -= le;
+                    if (bc <= 32) {
+                        bb |= (uint64_t)inf_dw(in, pq) << bc;
+                        bc += 32;
+                        pq += 4;
+                    }
+                    e = uni32((uint32_t)T->droot[(uint32_t)bb & 511u]);
+                    if (e == 0) {
+                        const int r = inf_decode((uint32_t)bb, 64, DC, T->dsym, sym, len);
+                        if (r < 0) { bad = true; break; }
+                        e = sym | (len << 9);
+                    }
+                    sym = e & 511u;
+                    len = e >> 9;
+                    if (sym > 29) { bad = true; break; }
+                    bb >>= len;
+                    bc -= len;
+                    const uint32_t dt = rl(ST.dist, (int)sym);
+                    const uint32_t de = dt >> 16;
+                    const uint32_t dist = (dt & 0xFFFFu) + ((uint32_t)bb & ((1u << de) - 1u));
+                    bb >>= de;
+                    bc -= de;
+                    if (dist > op && !marks) { bad = true; break; }
+                    gzs_copy(o.ring, op, dist, ml);
+                    op += ml;
+                    gzs_flush_upto(o, op);
+                }
+                spill();
+                if (bad) GFAIL;
+                bp = 8 * (pq - in.mis) - bc;
+                if (eob) {
+                    if (last) { st = 2; break; }
+                    continue;
+                }
+            }
+            // exact loop near the end of the member
+            for (;;) {
+                v = inf_peek(in, bp);
+                int r = inf_decode(v, nbits - bp, LC, T->lsym, sym, len);
+                if (r == 0) { st = 3; goto out; }
+                if (r < 0 || sym > 285) GFAIL;
+                bp += len;
+                if (sym < 256) {
+                    if (l == 0) o.ring[(uint32_t)op & kInfMask] = (uint16_t)sym;
+                    op++;
+                    if ((op & 1023) == 0) gzs_flush(o, 1024u);
+                    continue;
+                }
+                if (sym == 256) break;
+                sym -= 257;
+                const uint32_t lt = rl(ST.len, (int)sym);
+                uint32_t ml = lt & 0xFFFFu;
+                const uint32_t le = lt >> 16;
+                v >>= len;
+                if (le) {
+                    GNEED(le);
+                    ml += v & ((1u << le) - 1u);
+                    bp += le;
+                }
+                v = inf_peek(in, bp);
+                r = inf_decode(v, nbits - bp, DC, T->dsym, sym, len);
+                if (r == 0) { st = 3; goto out; }
+                if (r < 0 || sym > 29) GFAIL;
+                bp += len;
+                const uint32_t dt = rl(ST.dist, (int)sym);
+                uint32_t dist = dt & 0xFFFFu;
+                const uint32_t de = dt >> 16;
+                if (de) {
+                    GNEED(de);
+                    dist += (v >> len) & ((1u << de) - 1u);
+                    bp += de;
+                }
+                if (dist > op && !marks) GFAIL;
+                gzs_copy(o.ring, op, dist, ml);
+                op += ml;
+                gzs_flush_upto(o, op);
+            }
+        }
+        if (last) { st = 2; break; }
+    }
+out:
+    if (op > o.flushed) gzs_flush(o, (uint32_t)(op - o.flushed));
+    total = op;
+    if (st > 0 && o.over) st = -3;
+    return st;
+#undef GNEED
+#undef GFAIL
+}
+
+// 32 stream bits from bit q, lane-private (bytes past the member: whatever
+// the member's last dword holds, or 0)
+DEV uint32_t gzs_bits(const InfIn& in, uint64_t q) {
+    const uint64_t pb = q + 8ull * in.mis, a = (pb >> 3) & ~3ull;
+    const uint32_t sh = (uint32_t)(pb - 8 * a);
+    const uint32_t d0 = inf_ld(in, a), d1 = inf_ld(in, a + 4);
+    return sh ? __builtin_amdgcn_alignbit(d1, d0, sh) : d0;
+}
+
+// stage 2 of the block-header search, one candidate per lane: decode the
+// code lengths at bit p through the lane's own table tb (128 entries: the
+// next 7 stream bits -> symbol | length << 5) and require what a valid
+// dynamic header has (inflate_member's TABLE checks)
+DEV bool gzs_check(const InfIn& in, uint64_t p, inf_lds_u8* tb, uint64_t nbits) {
+    constexpr uint8_t ord[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12, 3, 13, 2, 14, 1, 15};
+    const uint32_t a = gzs_bits(in, p), b = gzs_bits(in, p + 32), c = gzs_bits(in, p + 64);
+    const uint32_t nlen = ((a >> 3) & 31u) + 257, ndist = ((a >> 8) & 31u) + 1, ncode = ((a >> 13) & 15u) + 4;
+    const uint64_t x = (((uint64_t)b << 32 | a) >> 17) | ((uint64_t)c << 47);
+    uint64_t Ls = 0;
+#pragma unroll
+    for (uint32_t q = 0; q < 19; q++)
+        if (q < ncode) Ls |= ((x >> (3 * q)) & 7ull) << (3 * ord[q]);
+    uint32_t code = 0;
+    for (uint32_t L = 1; L <= 7; L++) {
+#pragma unroll
+        for (uint32_t s = 0; s < 19; s++) {
+            if (((uint32_t)(Ls >> (3 * s)) & 7u) == L) {
+                const uint32_t r = __builtin_bitreverse32(code) >> (32 - L);
+                for (uint32_t e = r; e < 128; e += 1u << L) tb[e] = (uint8_t)(s | (L << 5));
+                code++;
+            }
+        }
+        code <<= 1;
+    }
+    uint64_t q = p + 17 + 3 * ncode;
+    const uint32_t tot = nlen + ndist;
+    uint32_t have = 0, prev = 0, kl = 0, kd = 0, lmax = 0, dmax = 0;
+    bool ok = true, eob = false;
+    while (ok && have < tot) {
+        if (q + 32 > nbits) { ok = false; break; }
+        const uint32_t v = gzs_bits(in, q);
+        const uint32_t e = tb[v & 127u];
+        const uint32_t s = e & 31u, L = e >> 5;
+        uint32_t val = s, cnt = 1;
+        q += L;
+        if (s == 16) {
+            ok = have > 0;
+            val = prev;
+            cnt = 3 + ((v >> L) & 3u);
+            q += 2;
+        } else if (s == 17) {
+            val = 0;
+            cnt = 3 + ((v >> L) & 7u);
+            q += 3;
+        } else if (s == 18) {
+            val = 0;
+            cnt = 11 + ((v >> L) & 127u);
+            q += 7;
+        }
+        if (have + cnt > tot) ok = false;
+        if (ok && val) {
+            const uint32_t e1 = have + cnt;
+            const uint32_t nl = (e1 < nlen ? e1 : nlen) - (have < nlen ? have : nlen);
+            kl += nl * (32768u >> val);
+            kd += (cnt - nl) * (32768u >> val);
+            if (nl) lmax = lmax > val ? lmax : val;
+            if (cnt > nl) dmax = dmax > val ? dmax : val;
+            if (have <= 256 && 256 < e1) eob = true;
+        }
+        prev = val;
+        have += cnt;
+    }
+    return ok && eob && kl <= 32768u && kd <= 32768u && (kl == 32768u || lmax == 1) &&
+           (kd == 32768u || dmax <= 1);
+}
+
+// ---------------------------------------------------------------------------
 // zstd: the decoder of rp_zstd_core.h over a wave environment.  State is
 // wave-uniform (every lane runs the same scalar logic; table reads are made
 // uniform with readfirstlane); the input is read through the member's 512-byte
@@ -2040,6 +2446,7 @@ __global__ __launch_bounds__(64) void k_members_first(DeviceJob j) {
             const rpgpu_batch_result* R = &j.batches[b];
             const bool big = uni32((uint32_t)R->size_bytes) >= (128u << 10);
             if (big != (phase == 0)) continue;
+            if (j.gzs_mem && (uni32(j.gzs_mem[2 * i + 1]) >> 31)) continue;  // the split decode took it
             if ((uni32((uint32_t)(uint16_t)R->attrs) & 7u) == RPGPU_CODEC_GZIP) {
                 if (!tab) inf_load_tab(T->crc_tab);
                 tab = true;
@@ -2312,6 +2719,338 @@ hipError_t launch_zstamps(hipStream_t s, int print) {
     (void)s;
     (void)print;
 #endif
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// The split decode's kernels (see "Split decode of large gzip members").
+// ---------------------------------------------------------------------------
+DEV void gzs_null(DeviceJob& j, uint32_t from, uint32_t to) {
+    for (uint32_t t = from; t < to && t < j.gzs_items_cap; t++) j.gzs_items[t].member = ~0u;
+}
+
+// one thread per member: the gzip header, the chunks
+__global__ __launch_bounds__(256) void k_gzsplan(DeviceJob j) {
+    const uint32_t count = j.counters[16];
+    const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= count) return;
+    j.gzs_mem[2 * i] = 0;
+    j.gzs_mem[2 * i + 1] = 0;
+    const uint32_t b = j.inf_list[i];
+    const rpgpu_batch_result* R = &j.batches[b];
+    if (((uint32_t)(uint16_t)R->attrs & 7u) != RPGPU_CODEC_GZIP) return;
+    const uint64_t n = (uint64_t)(uint32_t)(R->size_bytes - (int32_t)RPGPU_HEADER_SIZE);
+    if (n < kGzsMin) return;
+    const uint8_t* p = j.data + j.seg_off[R->segment] + R->file_pos + RPGPU_HEADER_SIZE;
+    // RFC 1952 header: magic, CM 8, no reserved flags, no FHCRC
+    if (p[0] != 0x1fu || p[1] != 0x8bu || p[2] != 8u || (p[3] & 0xe2u)) return;
+    uint64_t h = 10;
+    if (p[3] & 4u) h = 12 + ((uint64_t)p[10] | ((uint64_t)p[11] << 8));
+    for (uint32_t f = 8; f <= 16; f <<= 1) {
+        if (!(p[3] & f)) continue;
+        while (h < n && p[h]) h++;
+        if (h >= n) return;
+        h++;
+    }
+    if (h + 2 * kGzsChunk > n) return;
+    const uint64_t isize = rd32h(p + n - 4);
+    uint64_t g = isize < 1032ull * n + 64 ? isize : 1032ull * n + 64;
+    const uint64_t nd = n - h;
+    uint32_t nk = (uint32_t)((nd + kGzsChunk - 1) / kGzsChunk);
+    nk = nk < kGzsMaxK ? nk : kGzsMaxK;
+    const uint64_t csz = (nd + nk - 1) / nk;
+    const uint32_t base = atomicAdd(&j.counters[32], nk);
+    if ((uint64_t)base + nk > j.gzs_items_cap) {
+        gzs_null(j, base, base + nk);
+        return;
+    }
+    for (uint32_t k = 0; k < nk; k++) {
+        GzsItem& it = j.gzs_items[base + k];
+        it.member = i;
+        it.k = k;
+        it.nk = nk;
+        it.status = 0;
+        it.begin = h + k * csz;
+        it.end = h + (k + 1) * csz < n ? h + (k + 1) * csz : n;
+        it.start = k == 0 ? 8 * h : ~0ull;
+        it.stop = 0;
+        it.out = 0;
+        it.len = 0;
+        it.guess = g;
+        it.cap = 0;
+    }
+    j.gzs_mem[2 * i] = base;
+    j.gzs_mem[2 * i + 1] = nk;
+}
+
+// the first dynamic-block header of each chunk k >= 1
+constexpr uint32_t kGzsFindLds = 64 * 128 + 128 * 8;
+__global__ __launch_bounds__(64) void k_gzsfind(DeviceJob j) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    const uint32_t l = lane();
+    inf_lds_u8* tb = (inf_lds_u8*)lds + 128 * l;
+    typedef __attribute__((address_space(3))) uint64_t lds_u64;
+    lds_u64* queue = (lds_u64*)(lds + 64 * 128);
+    const uint32_t nit = min(j.counters[32], j.gzs_items_cap);
+    for (;;) {
+        const uint32_t t = wave_fetch_add(&j.counters[33], 1u);
+        if (t >= nit) break;
+        GzsItem* it = &j.gzs_items[t];
+        if (uni32(it->member) == ~0u || uni32(it->k) == 0) continue;
+        const uint32_t b = uni32(j.inf_list[uni32(it->member)]);
+        const InfIn in = inf_batch(j, &j.batches[b]);
+        const uint64_t nbits = in.n * 8, pend = 8 * uni64(it->end);
+        uint64_t found = ~0ull;
+        uint32_t qn = 0;
+        for (uint64_t p0 = 8 * uni64(it->begin); p0 < pend && found == ~0ull; p0 += 64) {
+            const uint64_t p = p0 + l;
+            bool pass = false;
+            if (p < pend && p + 128 <= nbits) {
+                const uint32_t a = gzs_bits(in, p);
+                if (((a >> 1) & 3u) == 2u && ((a >> 3) & 31u) <= 29u && ((a >> 8) & 31u) <= 29u) {
+                    const uint32_t b2 = gzs_bits(in, p + 32), c = gzs_bits(in, p + 64);
+                    const uint32_t ncode = ((a >> 13) & 15u) + 4;
+                    const uint64_t x = (((uint64_t)b2 << 32 | a) >> 17) | ((uint64_t)c << 47);
+                    uint32_t kr = 0;
+#pragma unroll
+                    for (uint32_t q = 0; q < 19; q++) {
+                        const uint32_t L = (uint32_t)(x >> (3 * q)) & 7u;
+                        if (q < ncode && L) kr += 128u >> L;
+                    }
+                    pass = kr == 128u;
+                }
+            }
+            const uint64_t m = __ballot(pass);
+            if (pass) queue[qn + (uint32_t)__builtin_popcountll(m & ((1ull << l) - 1ull))] = p;
+            qn += (uint32_t)__builtin_popcountll(m);
+            const bool last = p0 + 64 >= pend;
+            while (qn >= 64 || (last && qn > 0)) {
+                const uint32_t take = qn < 64 ? qn : 64;
+                const bool ok = l < take ? gzs_check(in, queue[l], tb, nbits) : false;
+                const uint64_t mm = __ballot(ok);
+                if (mm) {
+                    found = uni64(queue[__builtin_ctzll(mm)]);
+                    qn = 0;
+                    break;
+                }
+                const uint32_t rest = qn - take;
+                const uint64_t mv = l < rest ? queue[take + l] : 0ull;
+                if (l < rest) queue[l] = mv;
+                qn = rest;
+            }
+        }
+        if (l == 0) it->start = found;
+    }
+}
+
+// each chunk from its block start to the next chunk's
+__global__ __launch_bounds__(64) void k_gzsdecode(DeviceJob j) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    gzs_lds_u16* ring = (gzs_lds_u16*)lds;
+    InfTabs* T = (InfTabs*)(lds + 2 * kInfRing);
+    const InfSymTabs ST = inf_sym_tabs();
+    const uint32_t nit = min(j.counters[32], j.gzs_items_cap);
+    unsigned long long* used = (unsigned long long*)(j.counters + 36);
+    for (;;) {
+        const uint32_t t = wave_fetch_add(&j.counters[34], 1u);
+        if (t >= nit) break;
+        GzsItem* it = &j.gzs_items[t];
+        if (uni32(it->member) == ~0u) continue;
+        const uint64_t start = uni64(it->start);
+        if (start == ~0ull) continue;
+        const uint32_t k = uni32(it->k), nk = uni32(it->nk);
+        uint64_t stop = ~0ull;
+        for (uint32_t u = t + 1; u < t + (nk - k); u++) {
+            const uint64_t s2 = uni64(j.gzs_items[u].start);
+            if (s2 != ~0ull) {
+                stop = s2;
+                break;
+            }
+        }
+        const uint32_t b = uni32(j.inf_list[uni32(it->member)]);
+        InfIn in = inf_batch(j, &j.batches[b]);
+        // the region: twice the member's output per deflate byte over the
+        // span, plus 16 K symbols, capped by the whole member's guess
+        const uint64_t h = uni64(j.gzs_items[t - k].begin), g = uni64(it->guess);
+        const uint64_t span = ((stop == ~0ull ? in.n * 8 : stop) - start) / 8 + 1;
+        const uint64_t ratio = (g + (in.n - h) - 1) / (in.n - h);
+        uint64_t want = 2 * ratio * span + 16384;
+        want = want < g + 2048 ? want : g + 2048;
+        want = (want + 1023) & ~1023ull;
+        want = want < 0xFFFFFC00ull ? want : 0xFFFFFC00ull;
+        const uint64_t off = uni64(atomicAdd(used, lane() == 0 ? (unsigned long long)want : 0ull));
+        int st = -3;
+        uint64_t bp = start, total = 0;
+        if (off + want <= j.gzs_pool_syms) {
+            for (uint32_t q = lane(); q < kInfRing; q += 64) ring[q] = (uint16_t)(256u + q);
+            GzsOut o;
+            o.ring = ring;
+            o.dst = j.gzs_pool + off;
+            o.flushed = 0;
+            o.cap = want;
+            o.over = false;
+            st = gzs_run(in, T, o, ST, bp, stop, k != 0, total);
+        }
+        if (lane() == 0) {
+            it->out = off;
+            it->cap = (uint32_t)want;
+            it->stop = bp;
+            it->len = total;
+            it->status = st;
+        }
+    }
+}
+
+// per member (256 threads): the chain, the bytes, the check, the plan
+__global__ __launch_bounds__(256) void k_gzsresolve(DeviceJob j) {
+    __shared__ uint32_t tab[256], raw[256], xp[256];
+    __shared__ uint32_t chain[kGzsMaxK];
+    __shared__ uint64_t coff[kGzsMaxK];
+    __shared__ uint32_t s_i, s_n, s_verdict, s_bad;
+    __shared__ uint64_t s_total, s_soff, s_end;
+    const uint32_t tid = threadIdx.x;
+    {
+        uint32_t c = tid;
+        for (int k = 0; k < 8; k++) c = (c & 1) ? (c >> 1) ^ 0xEDB88320u : c >> 1;
+        tab[tid] = c;
+    }
+    const uint32_t count = j.counters[16];
+    for (;;) {
+        __syncthreads();
+        if (tid == 0) s_i = atomicAdd(&j.counters[35], 1u);
+        __syncthreads();
+        const uint32_t i = s_i;
+        if (i >= count) break;
+        const uint32_t nk = j.gzs_mem[2 * i + 1];
+        if (nk == 0) continue;
+        const uint32_t b = j.inf_list[i];
+        rpgpu_batch_result* R = &j.batches[b];
+        const uint64_t S = j.seg_off[R->segment] + R->file_pos + RPGPU_HEADER_SIZE;
+        const uint64_t n = (uint64_t)(uint32_t)(R->size_bytes - (int32_t)RPGPU_HEADER_SIZE);
+        const uint8_t* src = j.data + S;
+        if (tid == 0) {
+            // verdict: 0 decoded to the end (s_end: the final block's end, ~0
+            // the input ran out), 1 a stream error (-1), 3 not closed: serial
+            const GzsItem* I = j.gzs_items + j.gzs_mem[2 * i];
+            uint32_t c = 0, nc = 0, v = 3;
+            uint64_t tot = 0, end = ~0ull;
+            for (;;) {
+                const GzsItem& it = I[c];
+                if (it.status == 1 || it.status == 2 || it.status == 3) {
+                    chain[nc] = c;
+                    coff[nc] = tot;
+                    nc++;
+                    tot += it.len;
+                    if (it.status == 2) { v = 0; end = it.stop; break; }
+                    if (it.status == 3) { v = 0; break; }
+                    uint32_t u = c + 1;
+                    while (u < nk && I[u].start == ~0ull) u++;
+                    if (u >= nk || I[u].start != it.stop) break;  // (cannot happen: the decode stopped there)
+                    c = u;
+                    continue;
+                }
+                if (it.status == -1) v = 1;
+                break;
+            }
+            uint64_t soff = 0;
+            if (v == 0) {
+                const uint64_t cap = (tot + 15) & ~15ull;
+                soff = atomicAdd((unsigned long long*)j.inf_scratch_used, (unsigned long long)cap);
+                if (soff + cap > j.inf_scratch_bytes) v = 3;
+            }
+            s_n = nc;
+            s_total = tot;
+            s_end = end;
+            s_soff = soff;
+            s_verdict = v;
+            s_bad = 0;
+        }
+        __syncthreads();
+        const uint32_t v0 = s_verdict;
+        if (v0 == 3) continue;
+        uint32_t rc = v0 == 1 ? 1u : 0u;  // 0 accept, 1 reject (-1), 2 reject (-2: the check)
+        const uint64_t total = s_total;
+        if (v0 == 0) {
+            uint8_t* dst = j.inf_scratch + s_soff;
+            const GzsItem* I = j.gzs_items + j.gzs_mem[2 * i];
+            for (uint32_t w = 0; w < s_n; w++) {
+                const GzsItem& it = I[chain[w]];
+                const uint16_t* sy = j.gzs_pool + it.out;
+                const uint64_t len = it.len, off = coff[w];
+                bool bad = false;
+                for (uint64_t e = 8ull * tid; e < len; e += 8ull * 256) {
+                    const uint4 q = *(const uint4*)(sy + e);
+                    const uint32_t wd[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+                    for (uint32_t k = 0; k < 8; k++) {
+                        if (e + k >= len) break;
+                        const uint32_t s = (wd[k >> 1] >> (16 * (k & 1))) & 0xFFFFu;
+                        uint8_t y = (uint8_t)s;
+                        if (s >= 256) {
+                            const int64_t g = (int64_t)off + (int64_t)(s - 256) - (int64_t)kInfRing;
+                            if (g < 0) bad = true;
+                            else y = dst[g];
+                        }
+                        dst[off + e + k] = y;
+                    }
+                }
+                if (bad) s_bad = 1;
+                __syncthreads();
+            }
+            if (s_bad) {
+                rc = 1;
+            } else if (s_end != ~0ull) {
+                // CHECK, LENGTH: inflate_member's rules on the trailer
+                const uint64_t bp = (s_end + 7) & ~7ull, nbits = n * 8;
+                if (nbits - bp >= 32) {
+                    const uint64_t seg = ((total + 255) / 256 + 15) & ~15ull;
+                    const uint64_t a = seg * tid, z = a + seg < total ? a + seg : total;
+                    uint32_t c = 0;
+                    for (uint64_t x = a; x < z; x++) c = tab[(c ^ dst[x]) & 0xFFu] ^ (c >> 8);
+                    raw[tid] = c;
+                    uint32_t pw = 1u << 31;
+                    const uint64_t ln = z > a ? z - a : 0;
+                    for (uint32_t k = 0; (ln >> k) != 0; k++)
+                        if ((ln >> k) & 1) pw = ieee_mulmod(kX2nIeee[(3 + k) & 31], pw);
+                    xp[tid] = z > a ? pw : 0u;
+                    __syncthreads();
+                    if (tid == 0) {
+                        uint32_t crc = 0xFFFFFFFFu;
+                        for (uint32_t t = 0; t < 256; t++)
+                            if (xp[t]) crc = ieee_mulmod(xp[t], crc) ^ raw[t];
+                        const uint8_t* tr = src + (bp >> 3);
+                        if (rd32h(tr) != ~crc) s_bad = 2;
+                        else if (nbits - bp >= 64 && rd32h(tr + 4) != (uint32_t)total) s_bad = 2;
+                    }
+                    __syncthreads();
+                    if (s_bad) rc = 2;
+                }
+            }
+        }
+        if (tid == 0) {
+            const uint64_t cap = rc == 1 ? 0 : (total + 15) & ~15ull;
+            const int32_t rcount = R->record_count;
+            j.dcap[b] = cap;
+            j.slots[b] = ((j.flags & RPGPU_JOB_PARSE) && rcount > 0 && (uint64_t)rcount <= cap) ? (uint64_t)rcount : 0;
+            j.inf_state[i] = rc != 0 ? 1u : 0u;
+            j.inf_off[i] = rc == 1 ? 0 : s_soff;
+            j.inf_total[i] = rc == 1 ? 0 : total;
+            j.gzs_mem[2 * i + 1] = nk | (1u << 31);
+        }
+    }
+}
+
+hipError_t launch_gzsplit(const DeviceJob& j, hipStream_t s, uint32_t grid) {
+    static bool attr = false;
+    if (!attr) {
+        (void)hipFuncSetAttribute((const void*)k_gzsdecode, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kGzsLds);
+        attr = true;
+    }
+    const uint32_t pg = (uint32_t)((j.batch_capacity + 255) / 256);
+    hipLaunchKernelGGL(k_gzsplan, dim3(pg ? pg : 1), dim3(256), 0, s, j);
+    hipLaunchKernelGGL(k_gzsfind, dim3(grid * 2), dim3(64), kGzsFindLds, s, j);
+    hipLaunchKernelGGL(k_gzsdecode, dim3(grid), dim3(64), kGzsLds, s, j);
+    hipLaunchKernelGGL(k_gzsresolve, dim3(grid), dim3(256), 0, s, j);
     return hipGetLastError();
 }
 

@@ -168,8 +168,26 @@ struct ZsLitItem {
 };
 constexpr uint32_t kZsPlanned = 5;  // inf_state: k_zplan sized and planned the member for k_zparse
 
+// one chunk of a large gzip member decoded on its own wave (rp_inflate.hip,
+// k_gzsplan / k_gzsfind / k_gzsdecode / k_gzsresolve)
+struct GzsItem {
+    uint32_t member;     // inf_list index (~0: unused)
+    uint32_t k, nk;      // chunk ordinal, chunks of the member
+    int32_t status;      // k_gzsdecode's verdict (0: not decoded)
+    uint64_t begin, end; // deflate bytes searched for the chunk's first block header
+    uint64_t start;      // bit offset of that block (~0: none found)
+    uint64_t stop;       // bit offset the decode ended at
+    uint64_t out;        // pool offset (symbols) of the decoded symbols
+    uint64_t len;        // symbols decoded
+    uint64_t guess;      // the member's output guess (sizes the region)
+    uint32_t cap, pad;   // region symbols
+};
+constexpr uint64_t kGzsMin = 32768;    // stored gzip payloads this large are split
+constexpr uint64_t kGzsChunk = 16384;  // deflate bytes per chunk
+constexpr uint32_t kGzsMaxK = 256;     // chunks per member at most
+
 // job counters (DeviceJob::counters), zeroed per submit
-constexpr size_t kCounterBytes = 128;
+constexpr size_t kCounterBytes = 192;
 
 struct DeviceJob {
     const uint8_t* data;
@@ -206,7 +224,9 @@ struct DeviceJob {
                                   // [16] gzip / zstd members (inf_list), [17] k_members_first / [18] k_members claim cursors,
                                   // [19] host-decoded members (host_list), [20] k_members_first's second claim cursor,
                                   // [21] k_zexec claim cursor, [22] / [23] k_zparse claim cursors, [26] k_zfallback claim cursor,
-                                  // [28] planned literal blocks (zs_items), [29] k_zlits / [30] k_zplan claim cursors
+                                  // [28] planned literal blocks (zs_items), [29] k_zlits / [30] k_zplan claim cursors,
+                                  // [32] gzip split items (gzs_items), [33] / [34] / [35] k_gzsfind / k_gzsdecode /
+                                  // k_gzsresolve claim cursors, [36..37] gzs_pool symbols used (u64)
     uint32_t* decode_list;        // batch_capacity: ordinals of batches to uncompress
     uint32_t* seq_list;           // batch_capacity: decode items decoded whole by one lane
     uint32_t* link_list;          // batch_capacity: decode items whose linked LZ4F blocks one wave decodes in order
@@ -241,6 +261,12 @@ struct DeviceJob {
     uint64_t* zs_items;           // zs_items_cap: scratch offsets of the planned literal blocks (k_zplan -> k_zlits)
     uint32_t zs_items_cap;
     uint32_t* host_list;          // batch_capacity: ordinals of host-decoded (zstd) batches (RPGPU_JOB_HOST_CODECS)
+    uint32_t* gzs_mem;            // 2 x batch_capacity, per member: first item, chunks | 1 << 31 once resolved
+                                  // (null: no split decode, k_members_first takes every gzip member)
+    GzsItem* gzs_items;           // gzs_items_cap
+    uint32_t gzs_items_cap;
+    uint16_t* gzs_pool;           // decoded symbols of the chunks (bytes, or 256 + a window position)
+    uint64_t gzs_pool_syms;
 };
 
 // one host-decoded batch (RPGPU_JOB_HOST_CODECS): its payload, the host's
@@ -279,6 +305,7 @@ hipError_t launch_inflate_plan(const DeviceJob& j, hipStream_t s, uint32_t grid)
 hipError_t launch_inflate(const DeviceJob& j, hipStream_t s, uint32_t grid);
 hipError_t launch_zparse(const DeviceJob& j, hipStream_t s, uint32_t grid);
 hipError_t launch_zplan(const DeviceJob& j, hipStream_t s, uint32_t grid);
+hipError_t launch_gzsplit(const DeviceJob& j, hipStream_t s, uint32_t grid);
 hipError_t launch_zfallback(const DeviceJob& j, hipStream_t s, uint32_t grid);
 hipError_t launch_zstamps(hipStream_t s, int print);  // RPGPU_ZSTAMPS builds: reset / print the decoder stamps
 hipError_t launch_zexec(const DeviceJob& j, hipStream_t s);  // rp_codec.hip

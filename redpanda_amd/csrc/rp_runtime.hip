@@ -198,6 +198,8 @@ struct rpgpu_ctx {
     // gzip / zstd first-pass output pool (k_members_first), grow-only
     void* gz_pool = nullptr;
     size_t gz_pool_bytes = 0;
+    void* gzs_pool = nullptr;  // the gzip split decode's chunk symbols
+    size_t gzs_pool_bytes = 0;
 };
 
 namespace {
@@ -309,6 +311,7 @@ int rpgpu_destroy(rpgpu_ctx* c) {
     if (c->std_) hipFree(c->std_);
     if (c->d_tables) hipFree(c->d_tables);
     if (c->gz_pool) hipFree(c->gz_pool);
+    if (c->gzs_pool) hipFree(c->gzs_pool);
     for (auto* g : {&c->hc_items, &c->hc_items_h, &c->hc_in, &c->hc_in_h, &c->hc_out, &c->hc_out_h, &c->hc_small})
         if (g->p) (void)(g->pinned ? hipHostFree(g->p) : hipFree(g->p));
     if (c->ws_ev) { (void)hipEventSynchronize(c->ws_ev); (void)hipEventDestroy(c->ws_ev); }
@@ -633,6 +636,11 @@ int submit_body(rpgpu_ctx* c, const rpgpu_job* job, hipStream_t s, int stop, Pla
     // it, blocks decode in place)
     const uint64_t zcap64 = decode_job ? std::min<uint64_t>(job->h_seg_offsets[nseg] / 16384 + 8 * bcap + 64, 0x7FFFFFFFull) : 0;
     const size_t o_zitems = take(zcap64 * 8);
+    // gzip split decode: per member its first item and chunk count; items:
+    // one per kGzsChunk deflate bytes of the split members, one more each
+    const size_t o_gzsmem = take(decode_job ? 2 * (bcap + 1) * 4 : 0);
+    const uint64_t gcap64 = decode_job ? std::min<uint64_t>(job->h_seg_offsets[nseg] / kGzsChunk + bcap + 64, 0x7FFFFFFFull) : 0;
+    const size_t o_gzsit = take(gcap64 * sizeof(GzsItem));
     // block-parallel decode: one item per LZ4F block / snappy-java chunk
     const bool dec = (job->flags & RPGPU_JOB_DECODE) && job->d_decoded;
     const uint64_t data_len = job->h_seg_offsets[nseg];
@@ -760,6 +768,28 @@ int submit_body(rpgpu_ctx* c, const rpgpu_job* job, hipStream_t s, int stop, Pla
     j.zs_items = (uint64_t*)(ws + o_zitems);
     j.zs_items_cap = (uint32_t)zcap64;
     j.host_list = (uint32_t*)(ws + o_hlist);
+    // the gzip split decode (with the scratch pool only: it writes the
+    // members' bytes there); RPGPU_GZS=0 (diagnostic build): every gzip member
+    // serial (A/B)
+    j.gzs_mem = nullptr;
+    j.gzs_items = (GzsItem*)(ws + o_gzsit);
+    j.gzs_items_cap = (uint32_t)gcap64;
+    j.gzs_pool = nullptr;
+    j.gzs_pool_syms = 0;
+#ifdef RPGPU_NO_GZS  // A/B variant (scripts/build_exp.py): every gzip member serial
+    static const bool gzs_on = false;
+#else
+    static const bool gzs_on = [] { const char* e = diag_env("RPGPU_GZS"); return !(e && *e == '0'); }();
+#endif
+    if (j.inf_scratch && gzs_on && gcap64) {
+        const size_t want = std::min<size_t>(std::max<size_t>(2 * data_len, 64ull << 20), 4ull << 30);
+        if (int rc = grow_pool(c, c->gzs_pool, c->gzs_pool_bytes, want, s)) return rc;
+        if (c->gzs_pool) {
+            j.gzs_mem = (uint32_t*)(ws + o_gzsmem);
+            j.gzs_pool = (uint16_t*)c->gzs_pool;
+            j.gzs_pool_syms = c->gzs_pool_bytes / 2;
+        }
+    }
     c->hc_n = 0;
     j.blocks = (BlockItem*)(ws + o_blocks);
     j.block_capacity = (uint32_t)bl_cap64;
@@ -825,6 +855,7 @@ int submit_body(rpgpu_ctx* c, const rpgpu_job* job, hipStream_t s, int stop, Pla
             STAGE("zparse", launch_zparse(j, c->side, c->cu_count * 4));
             HIPCHK(c, hipEventRecord(c->join_ev, c->side));
         }
+        if (j.gzs_mem) STAGE("gzsplit", launch_gzsplit(j, s, c->cu_count * 2));
         STAGE("inflate_plan", launch_inflate_plan(j, s, c->cu_count * 4));
         if (split) {
             HIPCHK(c, hipStreamWaitEvent(s, c->join_ev, 0));

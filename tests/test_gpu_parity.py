@@ -639,6 +639,46 @@ def test_gzip_members_corpus(engine, oracle):
     assert_same(got, ref, DFLAGS)
 
 
+def test_gzip_split_members(engine, oracle):
+    """gzip members of >= 32 KiB stored decode in 16 KiB chunks from
+    speculative block starts (rp_inflate.hip, k_gzsfind / k_gzsdecode /
+    k_gzsresolve), the chain closed from chunk 0: JSON-like, alphanumeric,
+    random (stored blocks), low-entropy and mixed payloads at levels 1 / 6 / 9,
+    and each one truncated, bit-flipped early / late, with its CRC32 or ISIZE
+    trailer damaged, cut inside the trailer and followed by trailing bytes.
+    Accept/reject, plan, decoded bytes, crc / header_crc and walk as the
+    oracle's (zlib 1.2.11's rules)."""
+    import random
+    from tests.gzip_corpus import _payload, gzip_member
+    rng = random.Random(0x6250)
+    plain = [_payload(rng, 400000, 2), _payload(rng, 300000, 1), rng.randbytes(200000), _payload(rng, 150000, 3),
+             _payload(rng, 120000, 2) + rng.randbytes(90000) + _payload(rng, 160000, 1) + _payload(rng, 90000, 2)]
+    good = [gzip_member(plain[0], 6), gzip_member(plain[1], 6), gzip_member(plain[2], 6), gzip_member(plain[3], 9),
+            gzip_member(plain[4], 6), gzip_member(plain[0], 1), gzip_member(plain[4], 9, flags=8),
+            gzip_member(plain[1], 6, flags=2)]
+    bad = []
+    for g in good:
+        n = len(g)
+        m = bytearray(g)
+        m[n // 2] ^= 0x10
+        bad.append(bytes(m))
+        m = bytearray(g)
+        m[n - 40] ^= 0x01
+        bad.append(bytes(m))
+        m = bytearray(g)
+        m[n - 6] ^= 0x80
+        bad.append(bytes(m))
+        m = bytearray(g)
+        m[n - 2] ^= 0x01
+        bad.append(bytes(m))
+        bad += [g[: rng.randrange(n // 3, n - 8)], g[: n - 2], g[: n - 6], g + b"trailing bytes"]
+    segs = [_gzip_batches(good), _gzip_batches(bad[: len(bad) // 2]), _gzip_batches(bad[len(bad) // 2:])]
+    got, ref = run_both(engine, oracle, segs, flags=DFLAGS)
+    ok = (ref.batches["flags"] & abi.F_CODEC_OK) != 0
+    assert int(np.sum(ok)) >= len(good) and int(np.sum(~ok)) >= len(good)
+    assert_same(got, ref, DFLAGS)
+
+
 @pytest.mark.parametrize("host", [False, True])
 def test_zstd_host_codec_job(engine, oracle, rplib, host):
     """zstd batches inside a job: decoded on the device (rp_zstd_core.h over
