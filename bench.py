@@ -59,8 +59,8 @@ CPU_C1_SAMPLE = 1 << 30
 IDX_BYTES_PER_RECORD = 48
 RESULT_BYTES_PER_BATCH = 64
 DECODE_KERNELS = ("k_decode", "k_decode_blocks", "k_lz_walk", "k_lz_exec", "k_decode_finish")
-MEMBER_KERNELS = ("k_members_first", "k_zplan", "k_zlits", "k_zparse", "k_zfallback", "k_zexec", "k_members",
-                  "k_inflate_copy")
+MEMBER_KERNELS = ("k_gzsplan", "k_gzsfind", "k_gzsdecode", "k_gzsresolve", "k_members_first", "k_zplan", "k_zlits",
+                  "k_zparse", "k_zfallback", "k_zexec", "k_members", "k_inflate_copy")
 # segment-summary fields that do not depend on where a partition sits in a job
 SUMMARY_JOB_FIELDS = ("n_batches", "terminal_pos", "bytes_consumed", "terminal_errc", "terminal_eof",
                       "has_checkpoint", "first_bad", "ckpt_last_offset", "ckpt_truncate_pos", "n_records")
@@ -402,9 +402,10 @@ def run_compressed(name, kw, n_parts, seg_bytes, args, plat, eng, abi, desc, ext
         # buffer_for_input does)
         gz_zs = sum(per_codec[c]["decoded_bytes"] for c in ("1", "4"))
         rp = tm["resolve_plan"]
-        st["member_pass"] = {"stage": "resolve_plan (gzip: k_members_first; zstd beside it on a side stream: k_zplan, "
-                                      "k_zlits, k_zparse, k_zfallback; their records execute in k_zexec, in the "
-                                      "decode stage)",
+        st["member_pass"] = {"stage": "resolve_plan (gzip: members >= 32 KiB in chunks from speculative block "
+                                      "starts, k_gzsplan / k_gzsfind / k_gzsdecode / k_gzsresolve, the rest serial "
+                                      "in k_members_first; zstd beside them on a side stream: k_zplan, k_zlits, "
+                                      "k_zparse, k_zfallback; their records execute in k_zexec, in the decode stage)",
                              "ms": round(rp, 3), "decoded_bytes": gz_zs,
                              "decoded_GBps": round(gz_zs / (rp * 1e-3) / 1e9, 3) if rp > 0 else None}
     del out, data, d_offs, cpu_host

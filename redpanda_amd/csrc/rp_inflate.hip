@@ -922,12 +922,20 @@ DEV void gzip_item(const DeviceJob& j, uint8_t* lds, InfTabs* T, const InfWave& 
 // stored or fixed block at a chunk seam, a region outgrown) is left to
 // k_members_first, which decodes it serially as before.
 // ---------------------------------------------------------------------------
+constexpr int kBufFlagsZs = 0x00020000;  // buffer resource word 3 (raw, 32-bit data format)
+DEV void zs_wait_vm() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+constexpr int kZsSc1 = 16;  // cache policy sc1: L2-coherent, bypasses the vector L1
 typedef __attribute__((address_space(3))) uint16_t gzs_lds_u16;
-constexpr uint32_t kGzsLds = 2 * kInfRing + kInfTabBytes;
+// the chunk's ring holds its last 8 K symbols (16 KiB of LDS, so eight waves
+// share a CU); a match from farther back reads the chunk's region in the pool
+// (its flushed symbols) or, before the chunk's start, is a placeholder
+constexpr uint32_t kGzsRing = 8192, kGzsMask = kGzsRing - 1;
+constexpr uint32_t kGzsLds = 2 * kGzsRing + kInfTabBytes;
 
 struct GzsOut {
-    gzs_lds_u16* ring;  // 32 K symbols
+    gzs_lds_u16* ring;  // kGzsRing symbols
     uint16_t* dst;      // the chunk's region in the pool
+    __amdgpu_buffer_rsrc_t rs;  // dst as a buffer (L2-coherent reads of flushed symbols)
     uint64_t flushed, cap;
     bool over;
 };
@@ -940,7 +948,7 @@ DEV void gzs_flush(GzsOut& o, uint32_t len) {
     } else {
         const uint32_t l = lane();
         if (16u * l < len) {
-            const uint32_t at = (uint32_t)(o.flushed & kInfMask) + 16u * l;
+            const uint32_t at = (uint32_t)(o.flushed & kGzsMask) + 16u * l;
             const uint4 a = *(const uint4*)(o.ring + at), b = *(const uint4*)(o.ring + at + 8);
             uint4* d = (uint4*)(o.dst + o.flushed + 16u * l);  // the region is a whole number of 1 K pieces
             d[0] = a;
@@ -952,23 +960,44 @@ DEV void gzs_flush(GzsOut& o, uint32_t len) {
 DEV void gzs_flush_upto(GzsOut& o, uint64_t op) {
     while ((op >> 10) > (o.flushed >> 10)) gzs_flush(o, 1024u);
 }
-// inf_copy over 16-bit symbols
-DEV void gzs_copy(gzs_lds_u16* ring, uint64_t op, uint32_t dist, uint32_t ml) {
+// inf_copy over 16-bit symbols; dist > kGzsRing: the source lies before the
+// ring (dist > ml, no overlap): the region's flushed symbols, or before the
+// chunk's start its placeholders (256 + 32768 + position)
+DEV void gzs_copy(GzsOut& o, uint64_t op, uint32_t dist, uint32_t ml) {
     const uint32_t l = lane();
-    const bool rep = dist < ml;
-    const uint64_t mg = rep ? 0xFFFFFFFFull / dist + 1ull : 0ull;
+    gzs_lds_u16* ring = o.ring;
     const uint32_t n = (ml + 63) >> 6;
     uint32_t b[5];
+    if (dist > kGzsRing) {
+        if (o.over) {
 #pragma unroll
-    for (uint32_t i = 0; i < 5; i++) {
-        const uint32_t k = 64u * i + l;
-        const uint32_t x = rep ? k - (uint32_t)(((uint64_t)k * mg) >> 32) * dist : k;
-        b[i] = (i < n && k < ml) ? (uint32_t)ring[((uint32_t)(op - dist) + x) & kInfMask] : 0u;
+            for (uint32_t i = 0; i < 5; i++) b[i] = 0;
+        } else {
+            zs_wait_vm();  // the symbols read below were stored by this wave's flushes
+#pragma unroll
+            for (uint32_t i = 0; i < 5; i++) {
+                const uint32_t k = 64u * i + l;
+                const int64_t src = (int64_t)op - (int64_t)dist + (int64_t)k;
+                b[i] = 0;
+                if (i < n && k < ml)
+                    b[i] = src < 0 ? (uint32_t)(256 + 32768 + src)
+                                   : (uint32_t)__builtin_amdgcn_raw_buffer_load_b16(o.rs, (int)(2 * src), 0, kZsSc1);
+            }
+        }
+    } else {
+        const bool rep = dist < ml;
+        const uint64_t mg = rep ? 0xFFFFFFFFull / dist + 1ull : 0ull;
+#pragma unroll
+        for (uint32_t i = 0; i < 5; i++) {
+            const uint32_t k = 64u * i + l;
+            const uint32_t x = rep ? k - (uint32_t)(((uint64_t)k * mg) >> 32) * dist : k;
+            b[i] = (i < n && k < ml) ? (uint32_t)ring[((uint32_t)(op - dist) + x) & kGzsMask] : 0u;
+        }
     }
 #pragma unroll
     for (uint32_t i = 0; i < 5; i++) {
         const uint32_t k = 64u * i + l;
-        if (i < n && k < ml) ring[(uint32_t)(op + k) & kInfMask] = (uint16_t)b[i];
+        if (i < n && k < ml) ring[(uint32_t)(op + k) & kGzsMask] = (uint16_t)b[i];
     }
 }
 
@@ -1015,7 +1044,7 @@ DEV int gzs_run(InfIn& in, InfTabs* T, GzsOut& o, const InfSymTabs& ST, uint64_t
 #pragma unroll
                 for (uint32_t k = 0; k < 16; k++) {
                     const uint64_t i = c + 16u * l + k;
-                    if (i < copy) o.ring[(uint32_t)(op + i - c) & kInfMask] = (uint16_t)in.src[p + i];
+                    if (i < copy) o.ring[(uint32_t)(op + i - c) & kGzsMask] = (uint16_t)in.src[p + i];
                 }
                 op += copy - c < 1024 ? copy - c : 1024;
                 gzs_flush_upto(o, op);
@@ -1099,7 +1128,7 @@ DEV int gzs_run(InfIn& in, InfTabs* T, GzsOut& o, const InfSymTabs& ST, uint64_t
                 uint32_t lb = 0, nl = 0;
                 auto spill = [&]() __attribute__((always_inline)) {
                     if (nl) {
-                        if (l < nl) o.ring[(uint32_t)(op + l) & kInfMask] = (uint16_t)lb;
+                        if (l < nl) o.ring[(uint32_t)(op + l) & kGzsMask] = (uint16_t)lb;
                         op += nl;
                         nl = 0;
                         gzs_flush_upto(o, op);
@@ -1156,7 +1185,7 @@ DEV int gzs_run(InfIn& in, InfTabs* T, GzsOut& o, const InfSymTabs& ST, uint64_t
                     bb >>= de;
                     bc -= de;
                     if (dist > op && !marks) { bad = true; break; }
-                    gzs_copy(o.ring, op, dist, ml);
+                    gzs_copy(o, op, dist, ml);
                     op += ml;
                     gzs_flush_upto(o, op);
                 }
@@ -1176,7 +1205,7 @@ DEV int gzs_run(InfIn& in, InfTabs* T, GzsOut& o, const InfSymTabs& ST, uint64_t
                 if (r < 0 || sym > 285) GFAIL;
                 bp += len;
                 if (sym < 256) {
-                    if (l == 0) o.ring[(uint32_t)op & kInfMask] = (uint16_t)sym;
+                    if (l == 0) o.ring[(uint32_t)op & kGzsMask] = (uint16_t)sym;
                     op++;
                     if ((op & 1023) == 0) gzs_flush(o, 1024u);
                     continue;
@@ -1206,7 +1235,7 @@ DEV int gzs_run(InfIn& in, InfTabs* T, GzsOut& o, const InfSymTabs& ST, uint64_t
                     bp += de;
                 }
                 if (dist > op && !marks) GFAIL;
-                gzs_copy(o.ring, op, dist, ml);
+                gzs_copy(o, op, dist, ml);
                 op += ml;
                 gzs_flush_upto(o, op);
             }
@@ -1223,11 +1252,21 @@ out:
 }
 
 // 32 stream bits from bit q, lane-private (bytes past the member: whatever
-// the member's last dword holds, or 0)
-DEV uint32_t gzs_bits(const InfIn& in, uint64_t q) {
+// the member's last dword holds, or 0): from the LDS copy of the chunk's
+// bytes (w: dwords from physical offset wa, kGzsWin bytes) when it holds them
+typedef __attribute__((address_space(3))) uint32_t gzs_lds_u32;
+constexpr uint32_t kGzsWin = 18432;
+DEV uint32_t gzs_bits(const InfIn& in, uint64_t q, const gzs_lds_u32* w, uint64_t wa) {
     const uint64_t pb = q + 8ull * in.mis, a = (pb >> 3) & ~3ull;
     const uint32_t sh = (uint32_t)(pb - 8 * a);
-    const uint32_t d0 = inf_ld(in, a), d1 = inf_ld(in, a + 4);
+    uint32_t d0, d1;
+    if (a >= wa && a + 8 <= wa + kGzsWin) {
+        d0 = w[(a - wa) >> 2];
+        d1 = w[((a - wa) >> 2) + 1];
+    } else {
+        d0 = inf_ld(in, a);
+        d1 = inf_ld(in, a + 4);
+    }
     return sh ? __builtin_amdgcn_alignbit(d1, d0, sh) : d0;
 }
 
@@ -1235,9 +1274,9 @@ DEV uint32_t gzs_bits(const InfIn& in, uint64_t q) {
 // code lengths at bit p through the lane's own table tb (128 entries: the
 // next 7 stream bits -> symbol | length << 5) and require what a valid
 // dynamic header has (inflate_member's TABLE checks)
-DEV bool gzs_check(const InfIn& in, uint64_t p, inf_lds_u8* tb, uint64_t nbits) {
+DEV bool gzs_check(const InfIn& in, uint64_t p, inf_lds_u8* tb, uint64_t nbits, const gzs_lds_u32* w, uint64_t wa) {
     constexpr uint8_t ord[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12, 3, 13, 2, 14, 1, 15};
-    const uint32_t a = gzs_bits(in, p), b = gzs_bits(in, p + 32), c = gzs_bits(in, p + 64);
+    const uint32_t a = gzs_bits(in, p, w, wa), b = gzs_bits(in, p + 32, w, wa), c = gzs_bits(in, p + 64, w, wa);
     const uint32_t nlen = ((a >> 3) & 31u) + 257, ndist = ((a >> 8) & 31u) + 1, ncode = ((a >> 13) & 15u) + 4;
     const uint64_t x = (((uint64_t)b << 32 | a) >> 17) | ((uint64_t)c << 47);
     uint64_t Ls = 0;
@@ -1262,7 +1301,7 @@ DEV bool gzs_check(const InfIn& in, uint64_t p, inf_lds_u8* tb, uint64_t nbits) 
     bool ok = true, eob = false;
     while (ok && have < tot) {
         if (q + 32 > nbits) { ok = false; break; }
-        const uint32_t v = gzs_bits(in, q);
+        const uint32_t v = gzs_bits(in, q, w, wa);
         const uint32_t e = tb[v & 127u];
         const uint32_t s = e & 31u, L = e >> 5;
         uint32_t val = s, cnt = 1;
@@ -1282,6 +1321,7 @@ DEV bool gzs_check(const InfIn& in, uint64_t p, inf_lds_u8* tb, uint64_t nbits) 
             q += 7;
         }
         if (have + cnt > tot) ok = false;
+        if (kl > 32768u || kd > 32768u) ok = false;  // over-subscribed already
         if (ok && val) {
             const uint32_t e1 = have + cnt;
             const uint32_t nl = (e1 < nlen ? e1 : nlen) - (have < nlen ? have : nlen);
@@ -1310,9 +1350,6 @@ DEV bool gzs_check(const InfIn& in, uint64_t p, inf_lds_u8* tb, uint64_t nbits) 
 // (L2-coherent loads once the flushes have completed).  A frame's XXH64
 // content checksum is computed by the wave over its bytes (slot + ring).
 // ---------------------------------------------------------------------------
-constexpr int kBufFlagsZs = 0x00020000;  // buffer resource word 3 (raw, 32-bit data format)
-DEV void zs_wait_vm() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
-constexpr int kZsSc1 = 16;  // cache policy sc1: L2-coherent, bypasses the vector L1
 constexpr uint32_t kZsTabBytes = (sizeof(zs::Tabs) + 15u) & ~15u;
 constexpr uint32_t kZsLds = kInfRing + kZsTabBytes;
 constexpr uint64_t kZsFarOff = kInfRing - 1024 - 256;  // offsets up to this read the ring
@@ -2446,7 +2483,7 @@ __global__ __launch_bounds__(64) void k_members_first(DeviceJob j) {
             const rpgpu_batch_result* R = &j.batches[b];
             const bool big = uni32((uint32_t)R->size_bytes) >= (128u << 10);
             if (big != (phase == 0)) continue;
-            if (j.gzs_mem && (uni32(j.gzs_mem[2 * i + 1]) >> 31)) continue;  // the split decode took it
+            if (j.gzs_mem && (uni32(j.gzs_mem[2 * i + 1]) >> 31)) continue;  // the split decode closed it
             if ((uni32((uint32_t)(uint16_t)R->attrs) & 7u) == RPGPU_CODEC_GZIP) {
                 if (!tab) inf_load_tab(T->crc_tab);
                 tab = true;
@@ -2784,13 +2821,14 @@ __global__ __launch_bounds__(256) void k_gzsplan(DeviceJob j) {
 }
 
 // the first dynamic-block header of each chunk k >= 1
-constexpr uint32_t kGzsFindLds = 64 * 128 + 128 * 8;
+constexpr uint32_t kGzsFindLds = 64 * 128 + 128 * 8 + kGzsWin;
 __global__ __launch_bounds__(64) void k_gzsfind(DeviceJob j) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     const uint32_t l = lane();
     inf_lds_u8* tb = (inf_lds_u8*)lds + 128 * l;
     typedef __attribute__((address_space(3))) uint64_t lds_u64;
     lds_u64* queue = (lds_u64*)(lds + 64 * 128);
+    gzs_lds_u32* w = (gzs_lds_u32*)(lds + 64 * 128 + 128 * 8);
     const uint32_t nit = min(j.counters[32], j.gzs_items_cap);
     for (;;) {
         const uint32_t t = wave_fetch_add(&j.counters[33], 1u);
@@ -2800,15 +2838,19 @@ __global__ __launch_bounds__(64) void k_gzsfind(DeviceJob j) {
         const uint32_t b = uni32(j.inf_list[uni32(it->member)]);
         const InfIn in = inf_batch(j, &j.batches[b]);
         const uint64_t nbits = in.n * 8, pend = 8 * uni64(it->end);
+        // the chunk's bytes (and 2 KiB past them) into LDS
+        const uint64_t wa = (uni64(it->begin) + in.mis) & ~3ull;
+        for (uint32_t d = l; d < kGzsWin / 4; d += 64) w[d] = inf_ld(in, wa + 4ull * d);
         uint64_t found = ~0ull;
         uint32_t qn = 0;
         for (uint64_t p0 = 8 * uni64(it->begin); p0 < pend && found == ~0ull; p0 += 64) {
             const uint64_t p = p0 + l;
             bool pass = false;
             if (p < pend && p + 128 <= nbits) {
-                const uint32_t a = gzs_bits(in, p);
-                if (((a >> 1) & 3u) == 2u && ((a >> 3) & 31u) <= 29u && ((a >> 8) & 31u) <= 29u) {
-                    const uint32_t b2 = gzs_bits(in, p + 32), c = gzs_bits(in, p + 64);
+                const uint32_t a = gzs_bits(in, p, w, wa);
+                // a final block is not looked for (the chunk before decodes on through it)
+                if ((a & 7u) == 4u && ((a >> 3) & 31u) <= 29u && ((a >> 8) & 31u) <= 29u) {
+                    const uint32_t b2 = gzs_bits(in, p + 32, w, wa), c = gzs_bits(in, p + 64, w, wa);
                     const uint32_t ncode = ((a >> 13) & 15u) + 4;
                     const uint64_t x = (((uint64_t)b2 << 32 | a) >> 17) | ((uint64_t)c << 47);
                     uint32_t kr = 0;
@@ -2826,7 +2868,7 @@ __global__ __launch_bounds__(64) void k_gzsfind(DeviceJob j) {
             const bool last = p0 + 64 >= pend;
             while (qn >= 64 || (last && qn > 0)) {
                 const uint32_t take = qn < 64 ? qn : 64;
-                const bool ok = l < take ? gzs_check(in, queue[l], tb, nbits) : false;
+                const bool ok = l < take ? gzs_check(in, queue[l], tb, nbits, w, wa) : false;
                 const uint64_t mm = __ballot(ok);
                 if (mm) {
                     found = uni64(queue[__builtin_ctzll(mm)]);
@@ -2847,7 +2889,7 @@ __global__ __launch_bounds__(64) void k_gzsfind(DeviceJob j) {
 __global__ __launch_bounds__(64) void k_gzsdecode(DeviceJob j) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     gzs_lds_u16* ring = (gzs_lds_u16*)lds;
-    InfTabs* T = (InfTabs*)(lds + 2 * kInfRing);
+    InfTabs* T = (InfTabs*)(lds + 2 * kGzsRing);
     const InfSymTabs ST = inf_sym_tabs();
     const uint32_t nit = min(j.counters[32], j.gzs_items_cap);
     unsigned long long* used = (unsigned long long*)(j.counters + 36);
@@ -2882,10 +2924,12 @@ __global__ __launch_bounds__(64) void k_gzsdecode(DeviceJob j) {
         int st = -3;
         uint64_t bp = start, total = 0;
         if (off + want <= j.gzs_pool_syms) {
-            for (uint32_t q = lane(); q < kInfRing; q += 64) ring[q] = (uint16_t)(256u + q);
+            // positions -8192 .. -1: their placeholders
+            for (uint32_t q = lane(); q < kGzsRing; q += 64) ring[q] = (uint16_t)(256u + 32768u - kGzsRing + q);
             GzsOut o;
             o.ring = ring;
             o.dst = j.gzs_pool + off;
+            o.rs = __builtin_amdgcn_make_buffer_rsrc(o.dst, 0, (int)(2 * want < 0x7FFFFFFFull ? 2 * want : 0x7FFFFFFFull), kBufFlagsZs);
             o.flushed = 0;
             o.cap = want;
             o.over = false;
@@ -3040,17 +3084,22 @@ __global__ __launch_bounds__(256) void k_gzsresolve(DeviceJob j) {
     }
 }
 
+hipError_t launch_gzsplan(const DeviceJob& j, hipStream_t s) {
+    const uint32_t pg = (uint32_t)((j.batch_capacity + 255) / 256);
+    hipLaunchKernelGGL(k_gzsplan, dim3(pg ? pg : 1), dim3(256), 0, s, j);
+    return hipGetLastError();
+}
+
 hipError_t launch_gzsplit(const DeviceJob& j, hipStream_t s, uint32_t grid) {
     static bool attr = false;
     if (!attr) {
         (void)hipFuncSetAttribute((const void*)k_gzsdecode, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kGzsLds);
+        (void)hipFuncSetAttribute((const void*)k_gzsfind, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kGzsFindLds);
         attr = true;
     }
-    const uint32_t pg = (uint32_t)((j.batch_capacity + 255) / 256);
-    hipLaunchKernelGGL(k_gzsplan, dim3(pg ? pg : 1), dim3(256), 0, s, j);
-    hipLaunchKernelGGL(k_gzsfind, dim3(grid * 2), dim3(64), kGzsFindLds, s, j);
-    hipLaunchKernelGGL(k_gzsdecode, dim3(grid), dim3(64), kGzsLds, s, j);
-    hipLaunchKernelGGL(k_gzsresolve, dim3(grid), dim3(256), 0, s, j);
+    hipLaunchKernelGGL(k_gzsfind, dim3(grid * 5), dim3(64), kGzsFindLds, s, j);
+    hipLaunchKernelGGL(k_gzsdecode, dim3(grid * 8), dim3(64), kGzsLds, s, j);
+    hipLaunchKernelGGL(k_gzsresolve, dim3(grid * 2), dim3(256), 0, s, j);
     return hipGetLastError();
 }
 

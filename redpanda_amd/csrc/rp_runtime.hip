@@ -855,7 +855,12 @@ int submit_body(rpgpu_ctx* c, const rpgpu_job* job, hipStream_t s, int stop, Pla
             STAGE("zparse", launch_zparse(j, c->side, c->cu_count * 4));
             HIPCHK(c, hipEventRecord(c->join_ev, c->side));
         }
-        if (j.gzs_mem) STAGE("gzsplit", launch_gzsplit(j, s, c->cu_count * 2));
+        // the split decode's members first, then the serial first pass over
+        // the rest and over the members the split decode did not close
+        if (j.gzs_mem) {
+            STAGE("gzsplan", launch_gzsplan(j, s));
+            STAGE("gzsplit", launch_gzsplit(j, s, c->cu_count));
+        }
         STAGE("inflate_plan", launch_inflate_plan(j, s, c->cu_count * 4));
         if (split) {
             HIPCHK(c, hipStreamWaitEvent(s, c->join_ev, 0));
