@@ -2631,7 +2631,7 @@ DEV void zseq_item(const DeviceJob& j, zs::Tabs* T, ZsSeqItem* it) {
 // X2 rule); then whether every stream ended exactly (what lits_finish checks)
 __global__ __launch_bounds__(64) void k_zlits(DeviceJob j) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-    zs::Tabs* T = (zs::Tabs*)(lds + kInfRing);
+    zs::Tabs* T = (zs::Tabs*)lds;  // the tables only (no ring): kZsTabBytes of LDS, more waves per CU
     const uint32_t reg = j.counters[28];
     const uint32_t count = reg < j.zs_items_cap ? reg : j.zs_items_cap;
     const uint32_t l = lane();
@@ -3126,11 +3126,11 @@ hipError_t launch_zplan(const DeviceJob& j, hipStream_t s, uint32_t grid) {
 hipError_t launch_zparse(const DeviceJob& j, hipStream_t s, uint32_t grid) {
     static bool attr = false;
     if (!attr) {
-        (void)hipFuncSetAttribute((const void*)k_zlits, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kMemLds);
+        (void)hipFuncSetAttribute((const void*)k_zlits, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kZsTabBytes);
         (void)hipFuncSetAttribute((const void*)k_zparse, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kMemLds);
         attr = true;
     }
-    hipLaunchKernelGGL(k_zlits, dim3(grid), dim3(64), kMemLds, s, j);
+    hipLaunchKernelGGL(k_zlits, dim3(grid * 2), dim3(64), kZsTabBytes, s, j);
     hipLaunchKernelGGL(k_zparse, dim3(grid), dim3(64), kMemLds, s, j);
     return hipGetLastError();
 }
