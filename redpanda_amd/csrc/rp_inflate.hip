@@ -2789,7 +2789,7 @@ __global__ __launch_bounds__(256) void k_gzsplan(DeviceJob j) {
         if (h >= n) return;
         h++;
     }
-    if (h + 2 * kGzsChunk > n) return;
+    if (h + kGzsChunk > n) return;
     const uint64_t isize = rd32h(p + n - 4);
     uint64_t g = isize < 1032ull * n + 64 ? isize : 1032ull * n + 64;
     const uint64_t nd = n - h;

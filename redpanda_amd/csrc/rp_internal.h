@@ -182,8 +182,14 @@ struct GzsItem {
     uint64_t guess;      // the member's output guess (sizes the region)
     uint32_t cap, pad;   // region symbols
 };
-constexpr uint64_t kGzsMin = 32768;    // stored gzip payloads this large are split
-constexpr uint64_t kGzsChunk = 16384;  // deflate bytes per chunk
+#ifndef RPGPU_GZS_MIN  // (A/B variants: scripts/build_exp.py -DRPGPU_GZS_MIN=... / -DRPGPU_GZS_CHUNK=...)
+#define RPGPU_GZS_MIN 32768
+#endif
+#ifndef RPGPU_GZS_CHUNK
+#define RPGPU_GZS_CHUNK 16384
+#endif
+constexpr uint64_t kGzsMin = RPGPU_GZS_MIN;      // stored gzip payloads this large are split
+constexpr uint64_t kGzsChunk = RPGPU_GZS_CHUNK;  // deflate bytes per chunk
 constexpr uint32_t kGzsMaxK = 256;     // chunks per member at most
 
 // job counters (DeviceJob::counters), zeroed per submit
