@@ -402,7 +402,7 @@ def run_compressed(name, kw, n_parts, seg_bytes, args, plat, eng, abi, desc, ext
         # buffer_for_input does)
         gz_zs = sum(per_codec[c]["decoded_bytes"] for c in ("1", "4"))
         rp = tm["resolve_plan"]
-        st["member_pass"] = {"stage": "resolve_plan (gzip: members >= 32 KiB in chunks from speculative block "
+        st["member_pass"] = {"stage": "resolve_plan (gzip: members >= 16 KiB in chunks from speculative block "
                                       "starts, k_gzsplan / k_gzsfind / k_gzsdecode / k_gzsresolve, the rest serial "
                                       "in k_members_first; zstd beside them on a side stream: k_zplan, k_zlits, "
                                       "k_zparse, k_zfallback; their records execute in k_zexec, in the decode stage)",

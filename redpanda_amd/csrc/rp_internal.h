@@ -183,12 +183,12 @@ struct GzsItem {
     uint32_t cap, pad;   // region symbols
 };
 #ifndef RPGPU_GZS_MIN  // (A/B variants: scripts/build_exp.py -DRPGPU_GZS_MIN=... / -DRPGPU_GZS_CHUNK=...)
-#define RPGPU_GZS_MIN 32768
+#define RPGPU_GZS_MIN 16384
 #endif
 #ifndef RPGPU_GZS_CHUNK
 #define RPGPU_GZS_CHUNK 16384
 #endif
-constexpr uint64_t kGzsMin = RPGPU_GZS_MIN;      // stored gzip payloads this large are split
+constexpr uint64_t kGzsMin = RPGPU_GZS_MIN;      // stored gzip payloads this large take the split decode
 constexpr uint64_t kGzsChunk = RPGPU_GZS_CHUNK;  // deflate bytes per chunk
 constexpr uint32_t kGzsMaxK = 256;     // chunks per member at most
 
