@@ -54,6 +54,8 @@ C5_PARTS, C5_SEG = 128, 64 << 20
 # batches take the reference's loops milliseconds each)
 C6_CPU_PARTS = 8
 CPU_C1_SAMPLE = 1 << 30
+# rpgpu_validate_host's staging group (group_kib 0): whole segments up to 256 MiB
+HOST_GROUP_BYTES = 256 << 20
 
 # index writes 48 B per record, result 64 B per batch
 IDX_BYTES_PER_RECORD = 48
@@ -102,6 +104,17 @@ class CudaPlatform:
         """Where collective tensors live: device memory for nccl (RCCL), the
         host for gloo."""
         return self.device if backend == "nccl" else self.torch.device("cpu")
+
+    def host_segments(self, data, seg_bytes: int, n: int):
+        """The job's n segments copied back into pinned host memory (the
+        host-resident input of the H2D stanza)."""
+        torch = self.torch
+        out = []
+        for i in range(n):
+            t = torch.empty(seg_bytes, dtype=torch.uint8, pin_memory=True)
+            t.copy_(data[i * seg_bytes:(i + 1) * seg_bytes])
+            out.append(t.numpy())
+        return out
 
     def time_on_side_stream(self, first, again, reps: int):
         """first(stream) once untimed, then `reps` x again(stream, prev)
@@ -363,6 +376,7 @@ def run_compressed(name, kw, n_parts, seg_bytes, args, plat, eng, abi, desc, ext
                              "decoded": decoded, "batches": n_batches,
                              "compressed_batches": parity["compressed"], "records": n_rec})
     st = {
+        "workload_id": name.upper(),
         "workload": desc,
         "partitions": n_parts,
         "segment_bytes": seg_bytes,
@@ -390,6 +404,7 @@ def run_compressed(name, kw, n_parts, seg_bytes, args, plat, eng, abi, desc, ext
             "alg_bytes_per_launch": dec_alg,
             "alg_def": "compressed payload read + decoded bytes written",
             "kernel_ms": round(dec_ms, 4),
+            "traffic_source": kernels_traffic.get("source") if kernels_traffic else None,
             "kernels_traffic": kernels_traffic,
         },
         "parity": parity,
@@ -402,15 +417,59 @@ def run_compressed(name, kw, n_parts, seg_bytes, args, plat, eng, abi, desc, ext
         # buffer_for_input does)
         gz_zs = sum(per_codec[c]["decoded_bytes"] for c in ("1", "4"))
         rp = tm["resolve_plan"]
+        # zstd members parsed in the member pass execute in k_zexec, inside
+        # the decode stage: the rate is taken over both stages (a lower
+        # bound: the decode stage also runs the lz4 / snappy pieces)
+        both = rp + dec_ms
         st["member_pass"] = {"stage": "resolve_plan (gzip: members >= 16 KiB in chunks from speculative block "
                                       "starts, k_gzsplan / k_gzsfind / k_gzsdecode / k_gzsresolve, the rest serial "
                                       "in k_members_first; zstd beside them on a side stream: k_zplan, k_zlits, "
-                                      "k_zparse, k_zfallback; their records execute in k_zexec, in the decode stage)",
+                                      "k_zparse, k_zfallback) + decode (k_zexec executes the parsed zstd members)",
                              "ms": round(rp, 3), "decoded_bytes": gz_zs,
-                             "decoded_GBps": round(gz_zs / (rp * 1e-3) / 1e9, 3) if rp > 0 else None}
+                             "gzip_decoded_bytes": per_codec["1"]["decoded_bytes"],
+                             "zstd_decoded_bytes": per_codec["4"]["decoded_bytes"],
+                             "decoded_GBps": round(gz_zs / (both * 1e-3) / 1e9, 3) if both > 0 else None,
+                             "decoded_GBps_def": "gzip + zstd decoded bytes / (resolve_plan + decode stage ms)"}
     del out, data, d_offs, cpu_host
     plat.empty_cache()
     return st
+
+
+def run_h2d(args, plat, eng, abi, data, seg_bytes, n_parts, flags, ref):
+    """H2D-inclusive rate (rpgpu_validate_host): the same C1 partitions,
+    host-resident in pinned memory, copied to the device in double-buffered
+    staging groups on a copy stream while the previous group validates, with
+    the batch results, record index and summaries returned to host arrays
+    (storage/log_replayer.cc:95-114 reads segments from the file into
+    memory).  Not `value` (device-resident); reported beside
+    it.  `ref` = the device job's (n_batches, n_records)."""
+    host = plat.host_segments(data, seg_bytes, n_parts)
+    total = seg_bytes * n_parts
+    r = eng.validate_host(host, flags)  # warm-up: staging slots allocated
+    b = r.batches
+    ok = bool(len(b) == ref[0] and len(r.records) == ref[1] and np.all(b["flags"] & abi.F_CRC_OK)
+              and np.all(b["flags"] & abi.F_PARSE_OK) and int(r.totals["overflow"]) == 0)
+    del r, b
+    reps = max(1, min(args.steps, 3))
+    times = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        r = eng.validate_host(host, flags)
+        times.append(time.perf_counter() - t0)
+        del r
+    del host
+    best, mean = min(times), sum(times) / len(times)
+    return {
+        "path": "rpgpu_validate_host (pinned host segments -> H2D on a copy stream, double-buffered groups, "
+                "results + record index back to host arrays)",
+        "group_bytes": max(HOST_GROUP_BYTES, seg_bytes),
+        "bytes": total,
+        "reps": reps,
+        "GBps": round(total / mean / 1e9, 2),
+        "GBps_best": round(total / best / 1e9, 2),
+        "ms_per_job": round(mean * 1e3, 2),
+        "parity": {"same_batches_records_as_device_job": ok},
+    }
 
 
 def run_stanza(name, *a, **kw):
@@ -420,6 +479,31 @@ def run_stanza(name, *a, **kw):
         return run_compressed(name, *a, **kw)
     except Exception as e:
         return failure(name, e)
+
+
+def _pick(d, keys):
+    return {k: d[k] for k in keys if d is not None and k in d}
+
+
+def compact_stanza(st):
+    """The fields of a stanza that ride on the JSON line.  The driver keeps
+    only the last 8 KB of stdout, so the per-kernel traffic tables, codec
+    splits and long descriptions go to --detail-out instead (the line names
+    the committed profile they come from)."""
+    if st is None or "error" in st:
+        return st
+    rf = st.get("roofline") or {}
+    out = _pick(st, ("workload_id", "ms_per_step", "stored_GBps", "decoded_GBps", "batches_per_s",
+                     "hbm_fraction_whole_pipeline", "stage_ms"))
+    out["roofline"] = _pick(rf, ("bound", "kernel", "achieved", "peak", "unit", "frac", "traffic", "kernel_ms",
+                                 "alg_bytes_per_launch", "traffic_source"))
+    p = st.get("parity") or {}
+    out["parity"] = _pick(p, ("batches", "codec_ok", "crc_ok", "parse_ok", "overflow", "all_valid",
+                              "records_eq_sum_parsed"))
+    out["cpu_baseline"] = _pick(st.get("cpu_baseline"), ("value", "unit", "decoded_GBs", "cores", "kind", "error"))
+    if "member_pass" in st:
+        out["member_pass"] = _pick(st["member_pass"], ("ms", "decoded_bytes", "decoded_GBps"))
+    return out
 
 
 STANZAS = {
@@ -461,9 +545,13 @@ def parse_args(argv=None):
                     help="size_bytes per batch (diagnostic; the headline workload is 16 KiB)")
     ap.add_argument("--stats-out", default="",
                     help="write each workload's byte counts (JSON) here, for scripts/parse_traffic.py")
-    ap.add_argument("--workloads", default="c1,c2,c5,c6",
-                    help="c1 is the headline; c2/c5/c6 stanzas run at N = 1 only; a run without c1 is a diagnostic "
-                         "(per-workload profiles)")
+    ap.add_argument("--workloads", default="c1,h2d,c2,c5,c6",
+                    help="c1 is the headline; h2d (the host path over c1's partitions) and the c2/c5/c6 stanzas run "
+                         "at N = 1 only; a run without c1 is a diagnostic (per-workload profiles)")
+    ap.add_argument("--no-h2d", action="store_true", help="skip the H2D-inclusive host-path stanza")
+    ap.add_argument("--detail-out", default="",
+                    help="write the full stanzas (per-kernel traffic tables, codec splits, descriptions) here; the "
+                         "JSON line carries the compact form")
     return ap.parse_args(argv)
 
 
@@ -498,6 +586,15 @@ def main(argv=None, platform=None):
                     extra[name] = run_stanza(name, kw(), parts, seg, args, plat, eng, abi, desc)
 
         if rank == 0:
+            if args.detail_out:
+                try:
+                    with open(args.detail_out, "w") as f:
+                        json.dump({"c1": c1, **extra}, f, indent=1, default=str)
+                except Exception as e:
+                    failure("detail-out", e)
+            roof = dict(c1["roofline"]) if c1 else None
+            if roof:
+                roof.pop("kernels_traffic", None)  # per-kernel tables: --detail-out / the committed profile
             line = {
                 "metric": "validated+decoded batch GB/s per GPU and whole node; % of HBM peak",
                 "value": c1["value"] if c1 else None,
@@ -512,11 +609,13 @@ def main(argv=None, platform=None):
                 "dtype": "u8",
                 "data": "synthetic (seeded mt19937_64, reference random_batch recipe), device-resident",
                 "config": {**(c1["config"] if c1 else {"workload": "diagnostic run without the headline (c1) workload"}),
-                           **extra},
-                "roofline": c1["roofline"] if c1 else None,
-                "cpu_baseline": c1["cpu_baseline"] if c1 else None,
+                           **({"h2d": c1["h2d"]} if c1 and c1.get("h2d") is not None else {}),
+                           **{k: compact_stanza(v) for k, v in extra.items()}},
+                "roofline": roof,
+                "cpu_baseline": _pick(c1["cpu_baseline"], ("value", "unit", "cores", "kind", "sample", "one_core_GBs",
+                                                           "host_logical_cpus", "error")) if c1 else None,
             }
-            print(json.dumps(line), flush=True)
+            print(json.dumps(line, separators=(",", ":")), flush=True)
     finally:
         if world > 1:
             dist.destroy_process_group()
@@ -736,18 +835,28 @@ def run_c1(args, plat, dist, eng, abi, world, rank):
             cpu = cpu_baseline_c1(host_first)
         except Exception as e:
             cpu = failure("c1 cpu baseline", e)
-    # release the C1 job before the compressed workloads
-    del out, data, d_offs, payload, index_res
+    # release the C1 job's outputs before the host path allocates its own
+    del out, d_offs, payload, index_res
+    plat.empty_cache()
+    h2d = None
+    if world == 1 and not args.no_h2d and "h2d" in args.workloads.split(","):
+        try:
+            h2d = run_h2d(args, plat, eng, abi, data, seg_bytes, len(parts), flags, (n_batches, n_records))
+        except Exception as e:
+            h2d = failure("h2d", e)
+    del data
     plat.empty_cache()
     gather_desc = {"bitmap": "bitmaps+summaries", "index": "bitmaps+summaries+batch results",
                    "records": "bitmaps+summaries+batch results+record index"}[args.gather]
     coll = "RCCL" if args.dist_backend == "nccl" else "gloo (host-staged)"
+    trace = committed_trace("k_validate")
     return {
         "value": round(value, 2),
         "ms_per_step": round(ms_per_step, 4),
+        "h2d": h2d,
         "config": {
             "workload": "C1/C3: per GPU 8 partitions x 2 GiB disk segments of uncompressed 16 KiB batches "
-                        "(seed 0xC1): chain discovery + header_crc + CRC32C + record walk/index + checkpoint",
+                        "(seed 0xC1): discovery + header_crc + CRC32C + record walk/index + checkpoint",
             "segment_bytes": seg_bytes,
             "partitions_per_gpu": len(parts),
             "batches_per_gpu": n_batches,
@@ -772,14 +881,33 @@ def run_c1(args, plat, dist, eng, abi, world, rank):
             "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
             "traffic": traffic,
+            "traffic_source": c1_traffic.get("source") if c1_traffic else None,
             "alg_bytes_per_launch": alg,
             "kernel_ms": round(v_ms, 4),
+            "kernel_ms_def": "validate stage between HIP events on the launch stream, mean over the timed steps",
+            # the committed rocprofv3 trace of the driver's command (same
+            # kernel, same steps): its mean and the fraction it implies
+            "trace": dict(trace, frac=round(alg / (trace["mean_ms"] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4))
+            if trace else None,
             "walk": {"kernel": "k_walk", "kernel_ms": round(w_ms, 4), "alg_bytes_per_launch": walk_alg,
                      "achieved": round(walk_alg / (w_ms * 1e-3) / 1e9, 1) if w_ms > 0 else None},
             "kernels_traffic": c1_traffic,
         },
         "cpu_baseline": cpu,
     }
+
+
+def committed_trace(kernel, fname="kernel_trace.json"):
+    """The committed rocprofv3 --kernel-trace summary of the driver's bench
+    command (scripts/trace_summary.py -> profiles/kernel_trace.json): the
+    mean duration of `kernel`'s C1 launches and the tag it was taken on."""
+    try:
+        with open(os.path.join(ROOT, "profiles", fname)) as f:
+            tj = json.load(f)
+        k = tj["c1"][kernel]
+        return {"tag": tj.get("tag"), "mean_ms": k["mean_ms"], "calls": k["calls"]}
+    except Exception:
+        return None
 
 
 if __name__ == "__main__":

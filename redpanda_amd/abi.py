@@ -102,27 +102,3 @@ assert JOB_TOTALS.itemsize == 72
 BATCH_COMPARE_FIELDS = [n for n in BATCH_RESULT.names if not n.startswith("reserved")]
 RECORD_COMPARE_FIELDS = [n for n in RECORD_INDEX.names if n not in ("pad", "reserved")]
 SUMMARY_COMPARE_FIELDS = [n for n in SEGMENT_SUMMARY.names if n != "reserved"]
-
-
-def _record_slots(batches: np.ndarray, n_records: int):
-    """(slot, batch ordinal, k-th record of its batch) of every record slot the
-    batches' parsed ranges [index_base, index_base + records_parsed) cover."""
-    rp = batches["records_parsed"].astype(np.int64)
-    sel = np.nonzero(rp > 0)[0]
-    cnt = rp[sel]
-    b = np.repeat(sel, cnt)
-    k = np.arange(int(cnt.sum()), dtype=np.int64) - np.repeat(np.cumsum(cnt) - cnt, cnt)
-    slot = batches["index_base"].astype(np.int64)[b] + k
-    ok = slot < n_records
-    return slot[ok], b[ok], k[ok]
-
-
-def record_batches(batches: np.ndarray, n_records: int) -> np.ndarray:
-    """The batch ordinal of each record-index slot [0, n_records): the result
-    whose parsed range [index_base, index_base + records_parsed) holds it
-    (-1 for a slot no batch parsed into)."""
-    out = np.full(n_records, -1, dtype=np.int64)
-    slot, b, _ = _record_slots(batches, n_records)
-    out[slot] = b
-    return out
-

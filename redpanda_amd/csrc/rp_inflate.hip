@@ -2074,6 +2074,10 @@ DEV bool zs_fast_size(const uint8_t* src, uint64_t n, uint64_t& nlit, uint64_t& 
             const uint32_t last = bh & 1, bt = (bh >> 1) & 3, bsz = bh >> 3;
             ip += 3;
             if (bt == 3) return false;
+            // a raw / RLE block larger than Block_Maximum_Size is corrupt
+            // (libzstd rejects it): the wave decoder rules on it, and its
+            // payload-controlled size never reserves scratch here
+            if (bt < 2 && bsz > zs::kBlockMax) return false;
             if (bt == 0) {
                 if (n - ip < bsz) return false;
                 nlit += bsz;
@@ -2533,8 +2537,13 @@ __global__ __launch_bounds__(64) void k_zplan(DeviceJob j) {
             const uint64_t o_tab = o_si + (((uint64_t)nsb * sizeof(ZsSeqItem) + 15) & ~15ull);
             const uint64_t o_seq = o_tab + 8192ull * nh + kZsSeqTab * nsb;
             const uint64_t need = o_seq + nq * sizeof(zs::RawSeq) + 64 * sizeof(zs::RawSeq);
-            soff = uni64(atomicAdd((unsigned long long*)j.inf_scratch_used, lane() == 0 ? (unsigned long long)need : 0ull));
-            if (soff + need <= j.inf_scratch_bytes) {
+            // at most 1/8 of the pool per member (as scratch_guess): one
+            // hostile header cannot starve the members claimed after it
+            const bool fits = need <= j.inf_scratch_bytes / 8;
+            soff = fits ? uni64(atomicAdd((unsigned long long*)j.inf_scratch_used, lane() == 0 ? (unsigned long long)need
+                                                                                                : 0ull))
+                        : 0;
+            if (fits && soff + need <= j.inf_scratch_bytes) {
                 ZLane e;
                 e.src = j.data + S;
                 e.n = n;
@@ -2918,6 +2927,9 @@ __global__ __launch_bounds__(64) void k_gzsdecode(DeviceJob j) {
         const uint64_t ratio = (g + (in.n - h) - 1) / (in.n - h);
         uint64_t want = 2 * ratio * span + 16384;
         want = want < g + 2048 ? want : g + 2048;
+        // a fixed share of the pool per chunk: one payload-controlled ISIZE
+        // cannot give each of a member's chunks the whole member's guess
+        want = want < j.gzs_pool_syms / 32 ? want : j.gzs_pool_syms / 32;
         want = (want + 1023) & ~1023ull;
         want = want < 0xFFFFFC00ull ? want : 0xFFFFFC00ull;
         const uint64_t off = uni64(atomicAdd(used, lane() == 0 ? (unsigned long long)want : 0ull));

@@ -807,6 +807,7 @@ int submit_body(rpgpu_ctx* c, const rpgpu_job* job, hipStream_t s, int stop, Pla
             fprintf(stderr, "[rpgpu] stage %s\n", name);                                   \
             fflush(stderr);                                                                \
             hipError_t _e = hipStreamSynchronize(s);                                       \
+            if (_e == hipSuccess && c->side) _e = hipStreamSynchronize(c->side);           \
             if (_e != hipSuccess) return fail(c, RPGPU_E_HIP, "stage " name " failed", _e); \
         }                                                                                  \
     } while (0)
@@ -844,6 +845,15 @@ int submit_body(rpgpu_ctx* c, const rpgpu_job* job, hipStream_t s, int stop, Pla
         // needs the scratch pool), gzip members (and, otherwise, zstd ones) here
         const bool split = j.inf_scratch && j.zs_fast;
         STAGE("zstamps", launch_zstamps(s, 0));
+        // an error return between the fork and the join still orders `s`
+        // after the side stream's kernels (the workspace is released on `s`)
+        struct SideJoin {
+            hipStream_t s = nullptr, side = nullptr;
+            hipEvent_t ev = nullptr;
+            ~SideJoin() {
+                if (side && hipEventRecord(ev, side) == hipSuccess) hipStreamWaitEvent(s, ev, 0);
+            }
+        } side_join;
         if (split) {
             if (!c->side) HIPCHK(c, hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking));
             if (!c->fork_ev) HIPCHK(c, hipEventCreateWithFlags(&c->fork_ev, hipEventDisableTiming));
@@ -851,6 +861,9 @@ int submit_body(rpgpu_ctx* c, const rpgpu_job* job, hipStream_t s, int stop, Pla
             j.zs_split = 1;
             HIPCHK(c, hipEventRecord(c->fork_ev, s));
             HIPCHK(c, hipStreamWaitEvent(c->side, c->fork_ev, 0));
+            side_join.s = s;
+            side_join.ev = c->join_ev;
+            side_join.side = c->side;
             STAGE("zplan", launch_zplan(j, c->side, c->cu_count * 4));
             STAGE("zparse", launch_zparse(j, c->side, c->cu_count * 4));
             HIPCHK(c, hipEventRecord(c->join_ev, c->side));
@@ -864,6 +877,7 @@ int submit_body(rpgpu_ctx* c, const rpgpu_job* job, hipStream_t s, int stop, Pla
         STAGE("inflate_plan", launch_inflate_plan(j, s, c->cu_count * 4));
         if (split) {
             HIPCHK(c, hipStreamWaitEvent(s, c->join_ev, 0));
+            side_join.side = nullptr;  // joined
             STAGE("zfallback", launch_zfallback(j, s, c->cu_count * 4));
         }
         STAGE("zstamps", launch_zstamps(s, 1));

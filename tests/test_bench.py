@@ -168,6 +168,18 @@ class OracleEngine:
         t = lambda a: torch.from_numpy(np.ascontiguousarray(a))  # noqa: E731
         return t(st.view(np.uint8)), t(ro.view(np.int32)), t(rt.view(np.int32)), t(ps.view(np.int64))
 
+    def validate_host(self, segments, flags):
+        """rpgpu_validate_host's result: one job over the host segments."""
+        from redpanda_amd import abi
+        from redpanda_amd.engine import HostResult
+        segs = [np.ascontiguousarray(x, dtype=np.uint8) for x in segments]
+        offs = np.cumsum([0] + [x.size for x in segs]).astype(np.uint64)
+        data = np.concatenate(segs)
+        total = int(offs[-1])
+        r = self.O.run_job(data, offs, flags, batch_cap=total // abi.HEADER_SIZE + len(segs) + 1,
+                           record_cap=max(total // 4, 64), decoded_cap=1)
+        return HostResult(r.batches, r.records, r.decoded[:0], r.summaries, r.totals, None)
+
     @staticmethod
     def index_to_host(states, rel_off, rel_time, pos, n_segments):
         from redpanda_amd import abi
@@ -195,6 +207,9 @@ class CpuPlatform:
 
     def comm_device(self, backend):
         return self.device
+
+    def host_segments(self, data, seg_bytes, n):
+        return [data[i * seg_bytes:(i + 1) * seg_bytes].numpy().copy() for i in range(n)]
 
     def time_on_side_stream(self, first, again, reps):
         t = time.perf_counter()
@@ -231,9 +246,12 @@ def env1(monkeypatch):
     monkeypatch.setenv("OMP_NUM_THREADS", "2")
 
 
-def test_bench_single_rank_all_stanzas(env1, rplib):
-    lines = _run_bench(["--steps", "1", "--warmup", "1", "--seg-gib", str(2 / 1024), "--partitions", "2"])
+def test_bench_single_rank_all_stanzas(env1, rplib, tmp_path):
+    lines = _run_bench(["--steps", "1", "--warmup", "1", "--seg-gib", str(2 / 1024), "--partitions", "2",
+                        "--detail-out", str(tmp_path / "detail.json")])
     assert len(lines) == 1
+    # the driver keeps the last 8 KB of stdout: the whole line must fit well inside
+    assert len(lines[0]) < 6000, len(lines[0])
     j = json.loads(lines[0])
     for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
               "vs_baseline", "dtype", "data", "config", "roofline", "cpu_baseline"):
@@ -246,10 +264,15 @@ def test_bench_single_rank_all_stanzas(env1, rplib):
     for name in ("c2", "c5", "c6"):
         st = j["config"][name]
         assert "error" not in st, (name, st)
-        assert st["batches"] > 0 and st["roofline"]["kernel_ms"] > 0
+        assert st["parity"]["batches"] > 0 and st["roofline"]["kernel_ms"] > 0
         assert st["cpu_baseline"] is not None
     assert j["config"]["c2"]["parity"]["all_valid"]
     assert j["config"]["c6"]["member_pass"]["decoded_bytes"] > 0
+    h = j["config"]["h2d"]
+    assert "error" not in h and h["GBps"] > 0 and h["parity"]["same_batches_records_as_device_job"], h
+    # the full stanzas (per-kernel tables) go to --detail-out
+    d = json.load(open(tmp_path / "detail.json"))
+    assert set(d) >= {"c1", "c2", "c5", "c6"} and "workload" in d["c2"]
 
 
 def test_bench_stanza_failure_keeps_headline(env1, rplib, monkeypatch):

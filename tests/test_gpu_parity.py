@@ -640,7 +640,7 @@ def test_gzip_members_corpus(engine, oracle):
 
 
 def test_gzip_split_members(engine, oracle):
-    """gzip members of >= 32 KiB stored decode in 16 KiB chunks from
+    """gzip members of >= 16 KiB stored decode in 16 KiB chunks from
     speculative block starts (rp_inflate.hip, k_gzsfind / k_gzsdecode /
     k_gzsresolve), the chain closed from chunk 0: JSON-like, alphanumeric,
     random (stored blocks), low-entropy and mixed payloads at levels 1 / 6 / 9,

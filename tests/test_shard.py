@@ -258,3 +258,64 @@ def test_gloo_world2_full_gather_gpu_outputs(rplib, oracle, tmp_path):
     out = str(tmp_path / "rank0_full.npz")
     mp.spawn(_full_gather_worker, args=(2, _free_port(), str(tmp_path), out), nprocs=2, join=True)
     _check_full_gather(out, oracle)
+
+
+@pytest.mark.gpu
+def test_rccl_world1_gather_device_tensors(rplib, oracle):
+    """bench.py's nccl branch (RCCL) on one GPU: a 1-rank nccl process group
+    opened with device_id, as `bench.py --gpus N` opens it, runs every gather
+    of §8(e) (sizes, bytes, verdicts, batch results + record index, segment
+    index) on the device tensors of a real HIP job; rank 0's picture must be
+    the local job's and the oracle's (storage/log_replayer.cc:62-79)."""
+    import torch
+    import torch.distributed as dist
+    from redpanda_amd.engine import Engine
+    from redpanda_amd.shard import as_bytes, gather_bytes, gather_job_verdicts, gather_records, gather_segment_index, \
+        gather_sizes
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    eng = Engine(0)
+    parts = list(range(N_PARTS))
+    segs = _segments(parts)
+    offs = np.cumsum([0] + [s.size for s in segs]).astype(np.uint64)
+    data = torch.from_numpy(np.concatenate(segs)).to(dev)
+    total = int(offs[-1])
+    out = eng.alloc_outputs(len(parts), total // abi.HEADER_SIZE + 16, total // 4, 1)
+    eng.submit(data, offs, out, abi.JOB_CRC | abi.JOB_PARSE)
+    torch.cuda.synchronize()
+    local = out.to_host()
+    nb, nr = len(local.batches), len(local.records)
+    ixo = eng.segment_index(out, [0] * len(parts), step=INDEX_STEP)
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{_free_port()}", rank=0, world_size=1,
+                            device_id=dev)
+    try:
+        assert dist.get_backend() == "nccl"
+        bm = as_bytes(out.bitmap)
+        sz = gather_sizes(bm, 1, dist)
+        assert sz == [bm.numel()]
+        g = gather_bytes(bm, 0, 1, dist, sizes=sz)
+        assert g[0].is_cuda and torch.equal(g[0], bm)
+        v = gather_job_verdicts(out.summaries, out.bitmap, nb, parts, 0, 1, dist)
+        rec = gather_records(out.batches[: nb * abi.BATCH_RESULT.itemsize],
+                             out.records[: nr * abi.RECORD_INDEX.itemsize], out.summaries, parts, 0, 1, dist)
+        ix = gather_segment_index(*ixo, parts, 0, 1, dist)
+        torch.cuda.synchronize()
+    finally:
+        dist.destroy_process_group()
+    ref = _oracle_job(segs)
+    for f in SUMMARY_FIELDS:
+        assert np.array_equal(v["summaries"][f], ref.summaries[f]), f
+        assert np.array_equal(v["summaries"][f], local.summaries[f]), f
+    bits = np.unpackbits(ref.bitmap.view(np.uint8), bitorder="little")[: len(ref.batches)]
+    assert np.array_equal(v["bitmaps"][tuple(parts)], bits) and not np.all(bits == 1)
+    assert len(rec["batches"]) == len(ref.batches) > 0 and len(rec["records"]) == len(ref.records) > 0
+    for f in abi.BATCH_COMPARE_FIELDS:
+        if f != "decoded_off":
+            assert np.array_equal(rec["batches"][f], ref.batches[f]), f"batches.{f}"
+    for f in abi.RECORD_COMPARE_FIELDS:
+        assert np.array_equal(rec["records"][f], ref.records[f]), f"records.{f}"
+    ixr = oracle.segment_index(ref.batches, ref.summaries, [0] * N_PARTS, step=INDEX_STEP)
+    for p, (s, ro, rt, ps) in enumerate(ixr):
+        assert int(ix[p][0]["n_entries"]) == int(s["n_entries"]) > 0
+        assert np.array_equal(ix[p][1], ro) and np.array_equal(ix[p][3], ps)
+    eng.close()
