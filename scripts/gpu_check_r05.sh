@@ -19,3 +19,6 @@ if [ -z "${NO_TRACE:-}" ]; then
 timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$TAG -o $TAG --output-format csv -- python3 bench.py --gpus 1 --steps 20 --warmup 5 > gpurun_out/prof_bench_$TAG.json 2> gpurun_out/prof_$TAG.log || { tail -30 gpurun_out/prof_$TAG.log; exit 1; }
 echo "trace ok"
 fi
+if [ -n "${AB:-}" ]; then
+W=c2,c5 bash scripts/gpu_ab.sh ${TAG}ab cur $AB cur $AB
+fi
