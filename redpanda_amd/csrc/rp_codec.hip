@@ -1037,7 +1037,7 @@ DEV bool plan_lz4f(const DeviceJob& j, In& in, int64_t n, uint64_t src_abs, uint
             it.kind = (raw ? kBlkRaw : 0u) | (bcs ? kBlkChecksum : 0u) | (linked ? kBlkLinked : 0u);
             it.out = -1;
             it.cap = raw ? (uint32_t)bsz : (uint32_t)bmax;
-            it.crc = it.pad = 0;
+            it.crc = it.fast = 0;
             j.blocks[first + k] = it;
             if (piece_is_long(it.kind, it.csize, it.cap)) lm |= 1ull << (k & 63);
             if ((k & 63) == 63 || k + 1 == nb) {
@@ -1103,7 +1103,7 @@ DEV bool plan_snappy_java(const DeviceJob& j, In& in, int64_t n, uint64_t src_ab
             it.kind = kBlkSnappy;
             it.out = -1;
             it.cap = ulen;
-            it.crc = it.pad = 0;
+            it.crc = it.fast = 0;
             j.blocks[first + k] = it;
             if (piece_is_long(it.kind, it.csize, it.cap)) lm |= 1ull << (k & 63);
             if ((k & 63) == 63 || k + 1 == nb) {
@@ -1138,7 +1138,7 @@ DEV bool plan_snappy_whole(const DeviceJob& j, int64_t n, uint64_t src_abs, uint
         it.kind = kBlkSnappy | kBlkWhole;
         it.out = -1;
         it.cap = (uint32_t)cap;
-        it.crc = it.pad = 0;
+        it.crc = it.fast = 0;
         j.blocks[first] = it;
         note_long(j, first);
     }
@@ -2155,7 +2155,7 @@ DEV void walk_long(const DeviceJob& j, uint32_t p, lds_u8* win) {
     it.kind = uni32(j.blocks[p].kind);
     it.out = -1;
     it.cap = uni32(j.blocks[p].cap);
-    it.crc = it.pad = 0;
+    it.crc = it.fast = 0;
     Piece pc;
     piece_begin(pc, j, it, win);  // (the window buffer hashes the block checksum first)
     PieceState out;
@@ -2261,6 +2261,7 @@ __global__ __launch_bounds__(256) void k_lz_walk(DeviceJob j) {
         const uint32_t k = wave_fetch_add(&j.counters[12], 1u);
         if (k >= nlong) break;
         const uint32_t p = uni32(j.long_list[k]);
+        if (uni32(j.blocks[p].fast) != kLzfNone) continue;  // the fast path has it
         if (!piece_wave_walked(uni32(j.blocks[p].kind), uni32(j.blocks[p].csize), uni32(j.blocks[p].cap), few))
             continue;  // a dense piece: the lane walk takes it
         walk_long(j, p, wl);
@@ -2280,6 +2281,7 @@ __global__ __launch_bounds__(256) void k_lz_walk(DeviceJob j) {
                 break;
             }
             const BlockItem it = j.blocks[p];
+            if (it.fast != kLzfNone) continue;                               // the fast path has it
             if (piece_wave_walked(it.kind, it.csize, it.cap, few)) continue;  // walked above
             piece_begin(pc, j, it);
             first_slab = 0xFFFFFFFFu;
@@ -2432,6 +2434,7 @@ DEV void exec_linked(const DeviceJob& j, lds_u8* ring, SeqRec* buf, uint32_t ite
 // one independent piece
 DEV void exec_one(const DeviceJob& j, lds_u8* ring, SeqRec* buf, uint32_t p, uint32_t kind,
                   const __attribute__((address_space(3))) uint32_t* pat, lds_cu32* ct) {
+    if (uni32(j.blocks[p].fast) != kLzfNone) return;  // k_lzf_parse / k_lzf_exec have it
     {
         const uint64_t dst = uni64(j.blocks[p].dst);
         XRing x;
@@ -2732,6 +2735,439 @@ __global__ void k_init_dstamps() {
 }
 #endif
 
+// ===========================================================================
+// Independent-block fast path: k_lzf_parse -> k_lzf_exec.
+//
+// The frames Redpanda writes are LZ4F with independent 64 KiB blocks
+// (compression/internal/lz4_frame_compressor.cc:70-76: LZ4F_blockIndependent,
+// default block size), decoded by LZ4F_decompress -> LZ4_decompress_safe per
+// block (lz4_frame_compressor.cc:123-200).  Such a block is one serial chain
+// of sequences (C2's JSON blocks: ~3200 of ~20 decoded bytes each); the lane
+// walk (k_lz_walk) parses it on one lane, ~3200 dependent steps.
+//
+// k_lzf_parse runs one WAVE per block and cuts the chain instead:
+//   * the block (<= kFIn bytes) is staged in LDS;
+//   * lane k parses its 1/64 of the input from a speculative start (a wrong
+//     start resynchronises with the true token chain after a few sequences:
+//     median 4, p99 40 on C2) and marks every position it visits in an LDS
+//     bitmap;
+//   * every lane then continues past its segment until it reaches a position
+//     a later lane visited: from there the two parses coincide (a parse is a
+//     function of its position), so the true chain from lane 0 runs through
+//     lane 0's parse, its exit into the lane that owns the exit, and so on
+//     (lanes it skips were never synchronised and are discarded);
+//   * the true lanes count their sequences and output bytes, a prefix sum
+//     places them, and a second parse writes 8-byte records
+//     {lip, ll | ml, off} to frecs, checking each sequence.
+// Verdicts follow LZ4_decompress_generic (liblz4 1.9.3, lz4_run above): a
+// sequence far from both ends (kFMarginIn input bytes, kFMarginOut output
+// bytes) is one the reference's fast loop takes, whose only failure is an
+// offset reaching before the block (H = 0 for an independent block); the
+// last lane runs lz4_run itself over the block's tail (safe loop, last
+// literals), from the exact state; anything else unusual (offset 0 mid-block,
+// an unsynchronised chain, no room in frecs) leaves the block to the walk /
+// exec kernels (BlockItem.fast stays kLzfNone).  k_lzf_exec then executes the
+// records with the ring executor (xbatch / xbig) into the block's arena slot,
+// taking the streaming decoded CRC on the way, as k_lz_exec does.
+// ===========================================================================
+#ifndef RPGPU_LZF_IN_KIB
+#define RPGPU_LZF_IN_KIB 20
+#endif
+constexpr uint32_t kFIn = RPGPU_LZF_IN_KIB * 1024u;  // largest block staged (compressed bytes)
+constexpr uint32_t kFPad = 64;                        // zero bytes after the staged block
+constexpr uint32_t kFWords = (kFIn + kFPad) / 32;     // visited-position bitmap
+constexpr uint32_t kFLds = kFIn + kFPad + 4 * kFWords;
+constexpr uint32_t kFSegMin = 256;                    // input bytes per lane at least
+constexpr uint32_t kFMarginIn = 64, kFMarginOut = 128;
+static_assert(kFIn % 16 == 0 && kFLds <= 64u * 1024u, "fast-path LDS image");
+
+typedef __attribute__((address_space(3))) uint32_t lds_u32;
+
+// one sequence at ip < n of the staged block, no checks: literal [lip, lip +
+// ll), match (off, ml; ml = 0: the stream ends in this literal run), next
+// token at nxt (> n when the lengths run past the block)
+struct FSeq {
+    uint32_t lip, ll, ml, off, nxt;
+};
+DEV FSeq fseq(const lds_u8* in, uint32_t ip, uint32_t n) {
+    FSeq q;
+    const uint32_t tok = in[ip];
+    uint32_t p = ip + 1, ll = tok >> 4;
+    if (ll == 15) {
+        uint32_t b;
+        do {
+            b = p < n ? (uint32_t)in[p] : 0u;
+            p++;
+            ll += b;
+        } while (b == 255);
+    }
+    q.lip = p;
+    q.ll = ll;
+    q.ml = 0;
+    q.off = 0;
+    if (p > n || ll > n - p || n - p - ll < 2) {  // the literals reach the end: the last sequence
+        q.nxt = p + ll;
+        return q;
+    }
+    p += ll;
+    q.off = (uint32_t)in[p] | ((uint32_t)in[p + 1] << 8);
+    p += 2;
+    uint32_t ml = tok & 15;
+    if (ml == 15) {
+        uint32_t b;
+        do {
+            b = p < n ? (uint32_t)in[p] : 0u;
+            p++;
+            ml += b;
+        } while (b == 255);
+    }
+    q.ml = ml + 4;
+    q.nxt = p;
+    return q;
+}
+
+// lz4_run's sink for the block's tail: 8-byte records
+struct FRecSink {
+    uint2* out;
+    uint32_t n, cap;
+    DEV bool seq(const uint4&, int32_t, int32_t lip, int32_t llen, int32_t, uint32_t off, int32_t ml) {
+        if (n < cap) out[n] = make_uint2((uint32_t)lip | ((uint32_t)llen << 16), (uint32_t)ml | (off << 16));
+        n++;
+        return true;
+    }
+};
+
+DEV uint32_t ex_scan(uint32_t v, uint32_t& total) {
+    const uint32_t incl = wave_scan(v);
+    total = rl(incl, 63);
+    return incl - v;
+}
+
+__global__ __launch_bounds__(64) void k_lzf_parse(DeviceJob j) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t flds[];
+    lds_u8* in = (lds_u8*)flds;
+    lds_u32* bits = (lds_u32*)(flds + kFIn + kFPad);
+    const uint32_t l = lane();
+    const uint32_t reserved = j.counters[4];
+    const uint32_t nblk = reserved < j.block_capacity ? reserved : j.block_capacity;
+    for (;;) {
+        const uint32_t p = wave_fetch_add(&j.counters[40], 1u);
+        if (p >= nblk) break;
+        const uint32_t kind = uni32(j.blocks[p].kind), n = uni32(j.blocks[p].csize), cap = uni32(j.blocks[p].cap);
+        // independent LZ4 blocks without a block checksum, staged whole, of
+        // at most 64 KiB out (the records' 16-bit fields)
+        if (kind != 0 || n < 16 || n > kFIn || cap > 65536u || cap < 256u) continue;
+        const uint64_t src = uni64(j.blocks[p].src);
+        const Src s{j.data + src, (int64_t)n, (int64_t)(j.data_len - src)};
+        for (uint32_t o = 16 * l; o < n + kFPad; o += 1024) {
+            uint4 v = make_uint4(0u, 0u, 0u, 0u);
+            if (o < n) {
+                v = ld16(s, o);
+                if (o + 16 > n) {  // bytes past the block read as zero
+                    const uint32_t k = n - o;
+                    uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+                    for (uint32_t d = 0; d < 4; d++) {
+                        const int32_t keep = (int32_t)k - 4 * (int32_t)d;
+                        w[d] = keep >= 4 ? w[d] : keep <= 0 ? 0u : (w[d] & ((1u << (8 * keep)) - 1u));
+                    }
+                    v = make_uint4(w[0], w[1], w[2], w[3]);
+                }
+            }
+            __builtin_memcpy(in + o, &v, 16);
+        }
+        for (uint32_t w = l; w < kFWords; w += 64) bits[w] = 0u;
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+        // lane segments
+        uint32_t nl = n / kFSegMin;
+        nl = nl < 1 ? 1 : nl > 64 ? 64 : nl;
+        const uint32_t seg = n / nl;
+        const bool act = l < nl;
+        const uint32_t S = l * seg, E = l == nl - 1 ? n : S + seg;
+        // pass 1: the speculative parse of the segment, positions marked
+        uint32_t ip = S;
+        if (act) {
+            while (ip < E) {
+                __hip_atomic_fetch_or(bits + (ip >> 5), 1u << (ip & 31), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                const FSeq q = fseq(in, ip, n);
+                if (q.ml == 0) {
+                    ip = n + 1;  // the last literal run: the parse ends
+                    break;
+                }
+                ip = q.nxt;
+            }
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        // pass 1b: on past the segment to the first position a later lane visited
+        if (act) {
+            while (ip < n && !((bits[ip >> 5] >> (ip & 31)) & 1u)) {
+                const FSeq q = fseq(in, ip, n);
+                if (q.ml == 0) {
+                    ip = n + 1;
+                    break;
+                }
+                ip = q.nxt;
+            }
+        }
+        const uint32_t exit_pos = ip;
+        // the true chain: lane 0, its exit into the lane owning it, ...
+        uint32_t entry = 0xFFFFFFFFu, last = 0, cur = 0, e = 0;
+        bool chained = true;
+        for (;;) {
+            entry = l == cur ? e : entry;
+            const uint32_t q = uni32(rl(exit_pos, (int)cur));
+            if (q >= n) {
+                last = cur;
+                break;
+            }
+            uint32_t o = q / seg;
+            o = o > nl - 1 ? nl - 1 : o;
+            if (o <= cur) {
+                chained = false;
+                break;
+            }
+            cur = o;
+            e = q;
+        }
+        if (!chained) continue;
+        const bool tl = entry != 0xFFFFFFFFu;
+        const bool is_last = l == last;
+        const uint32_t stop = is_last ? n : exit_pos;
+        // pass 2: count the true lanes' sequences and output bytes
+        uint32_t cnt = 0, out = 0;
+        if (tl) {
+            uint32_t q_ip = entry;
+            while (q_ip < stop) {
+                const FSeq q = fseq(in, q_ip, n);
+                cnt++;
+                out += q.ll + q.ml;
+                if (q.ml == 0) break;
+                q_ip = q.nxt;
+            }
+        }
+        uint32_t total_cnt = 0, total_out = 0;
+        const uint32_t rec0 = ex_scan(cnt, total_cnt);
+        const uint32_t op0 = ex_scan(out, total_out);
+        if (total_out > cap || total_cnt == 0) continue;  // not a block the fast path takes: the walk decides
+        uint64_t base = 0;
+        if (l == 0) base = atomicAdd((unsigned long long*)(j.counters + 42), (unsigned long long)total_cnt);
+        base = uni64(rl64(base, 0));
+        if (base + total_cnt > j.frec_cap) continue;
+        // pass 3: the records, every sequence checked (0 ok, 1 reject, 2 fall back)
+        uint32_t verdict = 0;
+        if (tl) {
+            uint32_t q_ip = entry, op = op0, r = rec0;
+            bool tail = false;
+            while (q_ip < stop) {
+                const FSeq q = fseq(in, q_ip, n);
+                const uint32_t opl = op + q.ll, ope = opl + q.ml;
+                const bool ord = q.ml != 0 && q.nxt + kFMarginIn <= n && ope + kFMarginOut <= cap && q.off != 0;
+                if (!ord) {
+                    if (is_last) tail = true;
+                    else verdict = 2;
+                    break;
+                }
+                if (q.off > opl) {  // before the block (LZ4_decompress_safe: offset outside buffers)
+                    verdict = 1;
+                    break;
+                }
+                j.frecs[base + r] = make_uint2(q.lip | (q.ll << 16), q.ml | (q.off << 16));
+                r++;
+                op = ope;
+                q_ip = q.nxt;
+            }
+            if (tail) {
+                // the reference's loops from this sequence on (its fast-loop
+                // state: every earlier sequence was an ordinary one)
+                PState ps;
+                ps.ip = (int32_t)q_ip;
+                ps.op = (int32_t)op;
+                ps.need = 0;
+                ps.st = 0;
+                ps.ulen = 0;
+                ps.safe = cap < (uint32_t)kFastSafeDistance;
+                Src ws = s;
+                ws.win = in;
+                ws.wlo = 0;
+                ws.whi = (int64_t)(n + kFPad);
+                FRecSink fs{j.frecs + base, r, total_cnt};
+                lz4_run(ws, (int32_t)cap, 0, ps, fs);
+                if (ps.st != 1) verdict = 1;
+                else if ((uint32_t)ps.op != total_out || fs.n != total_cnt) verdict = 2;
+            }
+        }
+        const uint64_t fb = __ballot(verdict == 2), rj = __ballot(verdict == 1);
+        if (fb) continue;
+        if (l == 0) {
+            if (rj) {
+                j.blocks[p].out = -1;
+                j.blocks[p].crc = 0u;
+                j.blocks[p].fast = kLzfReject;
+            } else {
+                PieceState ps;
+                ps.ip = 0;
+                ps.op = (int32_t)total_out;
+                ps.need = 0;
+                ps.st = 1;
+                ps.ulen = 0;
+                ps.safe = 0;
+                ps.nrec = total_cnt;
+                ps.first_slab = (uint32_t)base;
+                j.pstate[p] = ps;
+                j.blocks[p].fast = kLzfReady;
+                j.fast_list[atomicAdd(&j.counters[44], 1u)] = p;
+            }
+        }
+    }
+}
+
+DEV SeqRec frec_at(const uint2* recs, uint32_t k, uint32_t cnt) {
+    SeqRec r{0u, 0u, 0u, 0u};
+    if (k < cnt) {
+        const uint2 v = recs[k];
+        r.lip = v.x & 0xFFFFu;
+        r.ll = v.x >> 16;
+        r.ml = v.y & 0xFFFFu;
+        r.off = v.y >> 16;
+    }
+    return r;
+}
+
+// xbatch for k_lzf_exec: every chunk of every far source (a match reaching
+// further back than the ring, C2: ~8 % of matches, nearly every batch has
+// one) is loaded from the arena at the start of the batch, all in flight
+// together, and written from registers in the match rounds; xbatch loads
+// them inside the rounds, one dependent load per 16-byte chunk.
+DEV void fbatch(XRing& x, const Src& s, const SeqRec& r, uint32_t lo, uint32_t hi_lane, const Lit& lit) {
+    const uint32_t l = lane();
+    const bool v = l >= lo && l < hi_lane;
+    const uint32_t len = v ? r.ll + r.ml : 0u;
+    const uint32_t incl = wave_scan(len);
+    const uint32_t o = x.op + incl - len;
+    const uint32_t hi = x.op + rl(incl, (int)hi_lane - 1);
+    const uint32_t d = o + r.ll, src = d - r.off;
+    bool pend = v && r.ml > 0;
+    // sources before (batch end - ring): their ring slots may be rewritten by this batch
+    const bool far = x.linked && pend && hi > kXRing && src < hi - kXRing;
+    if (__ballot(far && src + r.ml > x.safe) && x.fpend) {
+        wait_vm();
+        x.fpend = false;
+        x.safe = x.flushed;
+    }
+    uint4 F[kBig / 16];
+#pragma unroll
+    for (uint32_t k = 0; k < kBig / 16; k++) {
+        F[k] = make_uint4(0u, 0u, 0u, 0u);
+        if (far && r.ml > 16 * k) {
+            const auto t = __builtin_amdgcn_raw_buffer_load_b128(x.rs, src + 16 * k, 0, kSc1);
+            F[k] = make_uint4(t[0], t[1], t[2], t[3]);
+        }
+    }
+    if (v && r.ll) {
+#pragma unroll
+        for (uint32_t k = 0; k < kBig / 16; k++)
+            if (r.ll > 16 * k) xst(x.r, o + 16 * k, lit.v[k], r.ll - 16 * k < 16 ? r.ll - 16 * k : 16);
+    }
+    for (;;) {
+        const uint64_t pm = __ballot(pend);
+        if (!pm) break;
+        const int first = __builtin_ctzll(pm);
+        const uint32_t f = rl(d, first);
+        const bool ready = pend && (src + r.ml <= f || l == (uint32_t)first);
+        if (ready) {
+            if (far) {
+#pragma unroll
+                for (uint32_t k = 0; k < kBig / 16; k++)
+                    if (r.ml > 16 * k) xst(x.r, d + 16 * k, F[k], r.ml - 16 * k < 16 ? r.ml - 16 * k : 16);
+            } else {
+                xmatch(x, d, r.off, r.ml, false);
+            }
+        }
+        pend = pend && !ready;
+    }
+    x.op = hi;
+    if (x.op - x.flushed > kFlushLag) xflush_chunks(x);
+}
+
+#ifndef RPGPU_LZF_XBATCH
+#define RPGPU_LZF_XBATCH 0  // 1: k_lzf_exec through xbatch (A/B)
+#endif
+
+// xrecords over 8-byte records
+DEV void frecords(XRing& x, const Src& s, const uint2* recs, uint32_t cnt) {
+    const uint32_t l = lane();
+    SeqRec r0 = frec_at(recs, l, cnt), r1 = frec_at(recs, 64 + l, cnt);
+    Lit lit0 = lit_load(s, r0);
+    uint32_t fh0 = x.safe, fh1 = x.safe;
+    for (uint32_t b = 0; b < cnt; b += 64) {
+        x.safe = fh1 > x.safe ? fh1 : x.safe;
+        fh1 = fh0;
+        fh0 = x.flushed;
+        const SeqRec r2 = frec_at(recs, b + 128 + l, cnt);
+        const Lit lit1 = lit_load(s, r1);
+        const uint32_t nb = cnt - b < 64 ? cnt - b : 64;
+        const uint64_t bigm = __ballot(l < nb && (r0.ll > kBig || r0.ml > kBig));
+        uint32_t lo = 0;
+        for (;;) {
+            const uint64_t bm = bigm & (~0ull << lo);
+            const uint32_t e = bm ? (uint32_t)__builtin_ctzll(bm) : nb;
+            if (e > lo) {
+                if (RPGPU_LZF_XBATCH) xbatch(x, s, r0, lo, e, lit0);
+                else fbatch(x, s, r0, lo, e, lit0);
+            }
+            if (!bm) break;
+            xbig(x, s, rl(r0.lip, (int)e), rl(r0.ll, (int)e), rl(r0.ml, (int)e), rl(r0.off, (int)e));
+            lo = e + 1;
+            if (lo >= nb) break;
+        }
+        r0 = r1;
+        r1 = r2;
+        lit0 = lit1;
+    }
+}
+
+// k_lzf_exec: the blocks k_lzf_parse made ready, one wave each (the
+// k_lz_exec workgroup layout with one ring fewer: fbatch keeps the far
+// sources in registers, and at 8 waves per workgroup the register budget is
+// 256 per lane (9 waves: 168, and fbatch spilled))
+constexpr uint32_t kFExecWaves = kExecWaves - 1;
+constexpr uint32_t kFXCrcOff = kFExecWaves * kXRing, kFXPatOff = kFXCrcOff + 8192u, kFXLds = kFXPatOff + 512u;
+__global__ __launch_bounds__(64 * kFExecWaves) void k_lzf_exec(DeviceJob j) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t xlds[];
+    const uint32_t wi = threadIdx.x >> 6;
+    lds_u8* ring = (lds_u8*)(xlds + wi * kXRing);
+    uint32_t* ct_w = (uint32_t*)(xlds + kFXCrcOff);
+    uint32_t* pat_w = (uint32_t*)(xlds + kFXPatOff);
+    for (uint32_t i = threadIdx.x; i < 1024u; i += blockDim.x) {
+        ct_w[i] = j.tables->braid[i >> 8][i & 255u];
+        ct_w[1024u + i] = j.tables->hdr[3u - (i >> 8)][i & 255u];
+    }
+    for (uint32_t i = threadIdx.x; i < 128u; i += blockDim.x)
+        pat_w[i] = i < 64u ? (&kPat.a[0][0])[i] : (&kPat.b[0][0])[i - 64u];
+    __syncthreads();
+    const __attribute__((address_space(3))) uint32_t* pat = (const __attribute__((address_space(3))) uint32_t*)pat_w;
+    lds_cu32* ct = (lds_cu32*)ct_w;
+    const uint32_t count = j.counters[44];
+    for (;;) {
+        const uint32_t u = wave_fetch_add(&j.counters[41], 1u);
+        if (u >= count) break;
+        const uint32_t p = uni32(j.fast_list[u]);
+        const uint64_t src = uni64(j.blocks[p].src), dst = uni64(j.blocks[p].dst);
+        const uint32_t n = uni32(j.blocks[p].csize), cap = uni32(j.blocks[p].cap);
+        const uint32_t nrec = uni32(j.pstate[p].nrec), base = uni32(j.pstate[p].first_slab);
+        const Src s{j.data + src, (int64_t)n, (int64_t)(j.data_len - src)};
+        XRing x;
+        xring_init(x, j, ring, dst, cap > kXRing, false, pat, ct);
+        frecords(x, s, j.frecs + base, nrec);
+        xflush(x, x.op);
+        const uint32_t crc = crc_finish(x, j.tables, x.op);
+        if (lane() == 0) {
+            j.blocks[p].out = (int32_t)x.op;
+            j.blocks[p].crc = crc;
+        }
+    }
+}
+
 uint32_t lz_exec_wgs_per_cu() { return kExecWaves; }
 
 hipError_t launch_decode(const DeviceJob& j, hipStream_t s, uint32_t grid) {
@@ -2763,6 +3199,29 @@ hipError_t launch_lz_exec(const DeviceJob& j, hipStream_t s) {
 #ifdef RPGPU_DSTAMPS
     hipLaunchKernelGGL(k_print_dstamps, dim3(1), dim3(1), 0, s);
 #endif
+    return hipGetLastError();
+}
+
+hipError_t launch_lzf_parse(const DeviceJob& j, hipStream_t s, uint32_t cus) {
+    static bool attr = false;
+    if (!attr) {
+        (void)hipFuncSetAttribute((const void*)k_lzf_parse, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kFLds);
+        attr = true;
+    }
+    if (!j.frecs || !j.fast_list) return hipSuccess;
+    // one wave per workgroup, as many as the LDS image allows per CU
+    hipLaunchKernelGGL(k_lzf_parse, dim3(cus * (160u * 1024u / kFLds)), dim3(64), kFLds, s, j);
+    return hipGetLastError();
+}
+
+hipError_t launch_lzf_exec(const DeviceJob& j, hipStream_t s) {
+    static bool attr = false;
+    if (!attr) {
+        (void)hipFuncSetAttribute((const void*)k_lzf_exec, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kFXLds);
+        attr = true;
+    }
+    if (!j.exec_waves || !j.frecs || !j.fast_list) return hipSuccess;
+    hipLaunchKernelGGL(k_lzf_exec, dim3(j.exec_waves / kExecWaves), dim3(64 * kFExecWaves), kFXLds, s, j);
     return hipGetLastError();
 }
 

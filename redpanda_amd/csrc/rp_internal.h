@@ -85,8 +85,12 @@ struct BlockItem {
     uint32_t cap;    // bytes reserved at dst (LZ4: the block maximum = the decoder's output bound)
     uint32_t crc;    // linear CRC32C (zero state, no final xor) of the decoded bytes, from k_lz_exec's
                      // flush; a linked frame's whole output on its first block
-    uint32_t pad;
+    uint32_t fast;   // kLzf*: taken by the independent-block fast path (k_lzf_parse / k_lzf_exec)
 };
+// BlockItem.fast: 0 the walk / exec kernels decode it; kLzfReady parsed into
+// frecs by k_lzf_parse (k_lzf_exec executes it); kLzfReject rejected there
+// (out = -1 written)
+constexpr uint32_t kLzfNone = 0, kLzfReady = 1, kLzfReject = 2;
 // kBlkWhole: a raw (non-xerial) snappy payload, snappy_standard_compressor
 // semantics (length 0 is an empty result whatever follows)
 constexpr uint32_t kBlkRaw = 1, kBlkChecksum = 2, kBlkSnappy = 4, kBlkLinked = 8, kBlkWhole = 16;
@@ -232,7 +236,8 @@ struct DeviceJob {
                                   // [21] k_zexec claim cursor, [22] / [23] k_zparse claim cursors, [26] k_zfallback claim cursor,
                                   // [28] planned literal blocks (zs_items), [29] k_zlits / [30] k_zplan claim cursors,
                                   // [32] gzip split items (gzs_items), [33] / [34] / [35] k_gzsfind / k_gzsdecode /
-                                  // k_gzsresolve claim cursors, [36..37] gzs_pool symbols used (u64)
+                                  // k_gzsresolve claim cursors, [36..37] gzs_pool symbols used (u64),
+                                  // [40] / [41] k_lzf_parse / k_lzf_exec claim cursors, [42..43] frecs used (u64), [44] fast_list count
     uint32_t* decode_list;        // batch_capacity: ordinals of batches to uncompress
     uint32_t* seq_list;           // batch_capacity: decode items decoded whole by one lane
     uint32_t* link_list;          // batch_capacity: decode items whose linked LZ4F blocks one wave decodes in order
@@ -248,6 +253,9 @@ struct DeviceJob {
     SeqRec* pool;                 // record slabs
     uint32_t* slab_next;          // pool_slabs: next slab of the same piece
     uint32_t pool_slabs;
+    uint2* frecs;                 // fast-path LZ4 sequence records (k_lzf_parse -> k_lzf_exec), 8 B each
+    uint64_t frec_cap;            // records frecs holds
+    uint32_t* fast_list;          // block_capacity: pieces k_lzf_parse made ready ([44] count)
     BlockItem* blocks;            // block work list ([4] items reserved, [5] claim cursor)
     uint32_t block_capacity;
     FramePlan* plans;             // one per decode item
@@ -304,6 +312,8 @@ hipError_t launch_decode(const DeviceJob& j, hipStream_t s, uint32_t grid);    /
 hipError_t launch_decode_blocks(const DeviceJob& j, hipStream_t s, uint32_t grid);
 hipError_t launch_lz_walk(const DeviceJob& j, hipStream_t s, uint32_t grid);
 hipError_t launch_lz_exec(const DeviceJob& j, hipStream_t s);
+hipError_t launch_lzf_parse(const DeviceJob& j, hipStream_t s, uint32_t cus);
+hipError_t launch_lzf_exec(const DeviceJob& j, hipStream_t s);
 hipError_t launch_decode_finish(const DeviceJob& j, hipStream_t s, uint32_t grid);
 // gzip members (rp_inflate.hip): first pass (into scratch) before the slot
 // scans, then the copy into the arena and the second pass where needed

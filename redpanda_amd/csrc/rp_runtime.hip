@@ -139,6 +139,10 @@ struct rpgpu_ctx {
     // k_lz_walk record pool (slabs) and its chain links, grow-only
     void* pool = nullptr;
     size_t pool_bytes = 0;
+    // k_lzf_parse's 8-byte records (independent-block fast path); without it
+    // every piece takes the walk / exec kernels
+    void* fpool = nullptr;
+    size_t fpool_bytes = 0;
     std::string err;
     // Context scratch (ws, pool, seqs, sws, iws) is shared by every job on
     // the context, whichever stream it is launched on: each async entry
@@ -306,6 +310,7 @@ int rpgpu_destroy(rpgpu_ctx* c) {
     if (c->bh) hipHostFree(c->bh);
     if (c->seqs) hipFree(c->seqs);
     if (c->pool) hipFree(c->pool);
+    if (c->fpool) hipFree(c->fpool);
     if (c->pin) hipHostFree(c->pin);
     if (c->sth) hipHostFree(c->sth);
     if (c->std_) hipFree(c->std_);
@@ -649,6 +654,7 @@ int submit_body(rpgpu_ctx* c, const rpgpu_job* job, hipStream_t s, int stop, Pla
     const size_t o_plans = take(dec ? (bcap + 1) * sizeof(FramePlan) : 0);
     const size_t o_pstate = take(bl_cap64 * sizeof(PieceState));
     const size_t o_longl = take(bl_cap64 * 4);
+    const size_t o_fastl = take(bl_cap64 * 4);
     uint64_t split_min = std::max<uint64_t>(kSplitMin, 2 * data_len / ((uint64_t)c->cu_count * kVWaves));
     // RPGPU_SPLIT_MIN_KIB (diagnostic build): override (scripts/bench_skew.py A/B)
     if (const char* e = diag_env("RPGPU_SPLIT_MIN_KIB")) split_min = std::max<uint64_t>(strtoull(e, nullptr, 10) << 10, 64);
@@ -736,6 +742,21 @@ int submit_body(rpgpu_ctx* c, const rpgpu_job* job, hipStream_t s, int stop, Pla
     if (const char* e = diag_env("RPGPU_POOL_SLABS")) j.pool_slabs = std::min<uint32_t>(j.pool_slabs, (uint32_t)atoi(e));
     j.pool = (SeqRec*)c->pool;
     j.slab_next = (uint32_t*)((uint8_t*)c->pool + (size_t)j.pool_slabs * kSlabRecs * sizeof(SeqRec));
+    // fast-path records: half the job's bytes (C2: 0.17 of them), 64 MiB ..
+    // 8 GiB; a block that finds no room takes the walk / exec kernels.
+    // RPGPU_LZF=0 (diagnostic build): every piece through the walk / exec (A/B)
+    j.frecs = nullptr;
+    j.frec_cap = 0;
+    j.fast_list = (uint32_t*)(ws + o_fastl);
+    static const bool lzf_on = [] { const char* e = diag_env("RPGPU_LZF"); return !(e && *e == '0'); }();
+    if (dec && lzf_on && stop == kRunAll) {
+        const size_t want = std::min<size_t>(std::max<size_t>(data_len / 2, 64ull << 20), 8ull << 30);
+        if (int rc = grow_pool(c, c->fpool, c->fpool_bytes, want, s)) return rc;
+        if (c->fpool) {
+            j.frecs = (uint2*)c->fpool;
+            j.frec_cap = c->fpool_bytes / sizeof(uint2);
+        }
+    }
     j.seg_first_bad = (uint32_t*)(ws + o_fbad);
     j.seeds = (job->d_seeds && job->d_seed_offsets) ? job->d_seeds : nullptr;
     j.seed_off = j.seeds ? job->d_seed_offsets : nullptr;
@@ -897,8 +918,10 @@ int submit_body(rpgpu_ctx* c, const rpgpu_job* job, hipStream_t s, int stop, Pla
     if ((job->flags & RPGPU_JOB_DECODE) && j.decoded) {
         STAGE("decode", launch_decode(j, s, c->cu_count * 8));
         STAGE("decode_blocks", launch_decode_blocks(j, s, c->cu_count * 8));
+        STAGE("lzf_parse", launch_lzf_parse(j, s, c->cu_count));
         STAGE("lz_walk", launch_lz_walk(j, s, c->cu_count * 16));
         STAGE("lz_exec", launch_lz_exec(j, s));
+        STAGE("lzf_exec", launch_lzf_exec(j, s));
         STAGE("decode_finish", launch_decode_finish(j, s, c->cu_count * 8));
         STAGE("inflate", launch_inflate(j, s, c->cu_count * 4));
         STAGE("zexec", launch_zexec(j, s));
