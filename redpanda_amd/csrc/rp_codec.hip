@@ -961,16 +961,84 @@ DEV bool piece_wave_walked(uint32_t kind, uint32_t csize, uint32_t cap, bool few
 }
 
 // long pieces base + i for the set bits i of m (lane 0): one atomic per 64
-// blocks of a frame (one per piece cost the planner ~1 ms on C2's dense blocks)
-DEV void note_longs(const DeviceJob& j, uint32_t base, uint64_t m) {
-    if (!m) return;
-    uint32_t at = atomicAdd(&j.counters[11], (uint32_t)__builtin_popcountll(m));
-    for (; m; m &= m - 1) j.long_list[at++] = base + (uint32_t)__builtin_ctzll(m);
+// blocks of a frame (one per piece cost the planner ~1 ms on C2's dense
+// blocks).  k_lz_exec runs every long piece alone (long_list); k_lz_walk
+// walks those of w (wlong_list: not the ones k_lzf_walk takes, which it
+// would claim one wave-wide atomic apiece only to skip)
+DEV void note_longs(const DeviceJob& j, uint32_t base, uint64_t m, uint64_t w) {
+    if (m) {
+        uint32_t at = atomicAdd(&j.counters[11], (uint32_t)__builtin_popcountll(m));
+        for (; m; m &= m - 1) j.long_list[at++] = base + (uint32_t)__builtin_ctzll(m);
+    }
+    if (w) {
+        uint32_t at = atomicAdd(&j.counters[38], (uint32_t)__builtin_popcountll(w));
+        for (; w; w &= w - 1) j.wlong_list[at++] = base + (uint32_t)__builtin_ctzll(w);
+    }
 }
+// k_lzf_walk's per-lane window (design note at k_lzf_walk)
+#ifndef RPGPU_LZF_WIN
+#define RPGPU_LZF_WIN 256
+#endif
+constexpr uint32_t kFWin = RPGPU_LZF_WIN;  // sequence starts walked per staged window
+constexpr uint32_t kFSlot = kFWin + 32;    // + a 16-byte read at the last start, or the offset bytes after it
+constexpr uint32_t kFMarginIn = 64, kFMarginOut = 128;
+static_assert(kFWin % 16 == 0 && kFWin >= 64, "lane window");
+// a planned LZ4 block k_lzf_walk takes: no raw block, no block checksum
+// (independent or linked), at most 64 KiB in and out (the records' 16-bit
+// fields)
+DEV bool lzf_eligible(bool raw, bool bcs, int64_t bsz, int64_t bmax) {
+    return !raw && !bcs && bsz >= 16 && bsz <= 65536 && bmax >= 256 && bmax <= 65536;
+}
+// the records an LZ4 block of csize bytes parses into at most (every
+// sequence but the last takes >= 3 input bytes)
+DEV uint32_t lzf_reserve(uint32_t csize) { return csize / 3 + 2; }
+// eligible blocks base + i for the set bits i of m (lane 0), one atomic per
+// 64 for the list and one for their frecs: each block's first_slab (pstate)
+// holds its offset in the group, `res` records in all; a group frecs cannot
+// hold stays with k_lz_walk.  Returns the blocks listed.
+DEV uint64_t note_fast(const DeviceJob& j, uint32_t base, uint64_t m, uint32_t res) {
+    if (!m || !j.lzf_list || !j.frecs) return 0;
+    const uint64_t fb = atomicAdd((unsigned long long*)(j.counters + 42), (unsigned long long)res);
+    if (fb + res > j.frec_cap) return 0;
+    const uint64_t listed = m;
+    uint32_t at = atomicAdd(&j.counters[45], (uint32_t)__builtin_popcountll(m));
+    for (; m; m &= m - 1) {
+        const uint32_t p = base + (uint32_t)__builtin_ctzll(m);
+        j.lzf_list[at++] = p;
+        j.pstate[p].first_slab += (uint32_t)fb;
+        j.blocks[p].fast = kLzfListed;
+    }
+    return listed;
+}
+
+// blocks base + i for the set bits i of m (lane 0) that k_lz_walk's lane
+// loop considers (every block but k_lzf_walk's and k_raw_copy's: C2 leaves
+// it none, where its lanes had scanned all 277 K items)
+DEV void note_lane(const DeviceJob& j, uint32_t base, uint64_t m) {
+    if (!m) return;
+    uint32_t at = atomicAdd(&j.counters[41], (uint32_t)__builtin_popcountll(m));
+    for (; m; m &= m - 1) j.lane_list[at++] = base + (uint32_t)__builtin_ctzll(m);
+}
+// the blocks [0, (k & 63) + 1) of a group of 64
+DEV uint64_t group_mask(uint32_t k) { return (k & 63) == 63 ? ~0ull : (1ull << ((k & 63) + 1)) - 1; }
+// independent raw blocks without a block checksum base + i for the set bits
+// i of m (lane 0): k_raw_copy copies them (BlockItem.fast = kLzfRaw)
+DEV void note_raw(const DeviceJob& j, uint32_t base, uint64_t m) {
+    if (!m) return;
+    uint32_t at = atomicAdd(&j.counters[40], (uint32_t)__builtin_popcountll(m));
+    for (; m; m &= m - 1) {
+        const uint32_t p = base + (uint32_t)__builtin_ctzll(m);
+        j.raw_list[at++] = p;
+        j.blocks[p].fast = kLzfRaw;
+    }
+}
+
 // a long piece (walked by a wave in k_lz_walk): lane 0 appends it
 DEV void note_long(const DeviceJob& j, uint32_t idx) {
     const uint32_t at = atomicAdd(&j.counters[11], 1u);
     j.long_list[at] = idx;
+    const uint32_t aw = atomicAdd(&j.counters[38], 1u);
+    j.wlong_list[aw] = idx;
 }
 
 // reserve `nb` items (wave-uniform); UINT32_MAX when the list is full
@@ -1024,7 +1092,8 @@ DEV bool plan_lz4f(const DeviceJob& j, In& in, int64_t n, uint64_t src_abs, uint
     const uint32_t first = reserve_blocks(j, nb);
     if (first == 0xFFFFFFFFu) return false;
     pos = hsize;
-    uint64_t plan = 0, lm = 0;
+    uint64_t plan = 0, lm = 0, fm = 0, rm = 0;
+    uint32_t fres = 0;
     for (uint32_t k = 0; k < nb; k++) {
         const uint32_t bh = in_le32(in, pos);
         const int64_t bsz = bh & 0x7FFFFFFFu;
@@ -1040,9 +1109,21 @@ DEV bool plan_lz4f(const DeviceJob& j, In& in, int64_t n, uint64_t src_abs, uint
             it.crc = it.fast = 0;
             j.blocks[first + k] = it;
             if (piece_is_long(it.kind, it.csize, it.cap)) lm |= 1ull << (k & 63);
+            if (raw && !bcs && !linked && j.raw_list) rm |= 1ull << (k & 63);
+            if (lzf_eligible(raw, bcs, bsz, bmax) && j.frecs) {
+                fm |= 1ull << (k & 63);
+                j.pstate[first + k].first_slab = fres;
+                fres += lzf_reserve((uint32_t)bsz);
+            }
             if ((k & 63) == 63 || k + 1 == nb) {
-                note_longs(j, first + (k & ~63u), lm);
+                const uint64_t listed = note_fast(j, first + (k & ~63u), fm, fres);
+                note_longs(j, first + (k & ~63u), lm, lm & ~listed);
+                note_raw(j, first + (k & ~63u), rm);
+                note_lane(j, first + (k & ~63u), group_mask(k) & ~listed & ~rm);
                 lm = 0;
+                fm = 0;
+                rm = 0;
+                fres = 0;
             }
         }
         plan += raw ? (uint64_t)bsz : (uint64_t)bmax;
@@ -1088,7 +1169,7 @@ DEV bool plan_snappy_java(const DeviceJob& j, In& in, int64_t n, uint64_t src_ab
     const uint32_t first = reserve_blocks(j, nb);
     if (first == 0xFFFFFFFFu) return false;
     pos = 16;
-    uint64_t plan = 0, lm = 0;
+    uint64_t plan = 0, lm = 0, fm = 0;
     for (uint32_t k = 0; k < nb; k++) {
         const int32_t clen = (int32_t)((in_byte(in, pos) << 24) | (in_byte(in, pos + 1) << 16) |
                                        (in_byte(in, pos + 2) << 8) | in_byte(in, pos + 3));
@@ -1107,7 +1188,8 @@ DEV bool plan_snappy_java(const DeviceJob& j, In& in, int64_t n, uint64_t src_ab
             j.blocks[first + k] = it;
             if (piece_is_long(it.kind, it.csize, it.cap)) lm |= 1ull << (k & 63);
             if ((k & 63) == 63 || k + 1 == nb) {
-                note_longs(j, first + (k & ~63u), lm);
+                note_longs(j, first + (k & ~63u), lm, lm);
+                note_lane(j, first + (k & ~63u), group_mask(k));
                 lm = 0;
             }
         }
@@ -1141,6 +1223,7 @@ DEV bool plan_snappy_whole(const DeviceJob& j, int64_t n, uint64_t src_abs, uint
         it.crc = it.fast = 0;
         j.blocks[first] = it;
         note_long(j, first);
+        note_lane(j, first, 1ull);
     }
     fp.mode = 2;
     fp.first = first;
@@ -1312,6 +1395,9 @@ DEV void crc_init(CrcState& c) {
 }
 // the next 1 KiB row of the output (this lane's 16 bytes; zero past the end)
 DEV void crc_row(CrcState& c, lds_cu32* ct, const uint4& v) {
+#if defined(RPGPU_XABL) && RPGPU_XABL == 3
+    return;  // ablation (diagnostic build only): no streaming CRC
+#endif
     if (c.hp) {
         xbraid(c, ct, 0, c.pend.x);
         xbraid(c, ct, 1, c.pend.y);
@@ -1491,7 +1577,14 @@ DEV void xbatch(XRing& x, const Src& s, const SeqRec& r, uint32_t lo, uint32_t h
     uint32_t rounds = 0;
 #endif
     // sources before (batch end - 64 KiB): their ring slots may be rewritten by this batch
+#if defined(RPGPU_XABL) && RPGPU_XABL == 2
+    const bool far = false;  // ablation (diagnostic build only): far sources read the ring
+#else
     const bool far = x.linked && pend && hi > kXRing && src < hi - kXRing;
+#endif
+#if defined(RPGPU_XABL) && RPGPU_XABL == 1
+    pend = false;  // ablation (diagnostic build only): no match copies
+#endif
     // a far source was stored by an earlier flush: wait only while a flush
     // may still be in flight (a wait drains every earlier memory op)
     if (__ballot(far && src + r.ml > x.safe) && x.fpend) {
@@ -1619,24 +1712,65 @@ DEV void xrecords(XRing& x, const Src& s, const SeqRec* recs, uint32_t cnt) {
     }
 }
 
+// k_lzf_walk's 8-byte records {lip | ll << 16, ml | off << 16}
+DEV SeqRec frec_at(const uint2* recs, uint32_t k, uint32_t cnt) {
+    SeqRec r{0u, 0u, 0u, 0u};
+    if (k < cnt) {
+        const uint2 v = recs[k];
+        r.lip = v.x & 0xFFFFu;
+        r.ll = v.x >> 16;
+        r.ml = v.y & 0xFFFFu;
+        r.off = v.y >> 16;
+    }
+    return r;
+}
+
+// xrecords over 8-byte records
+DEV void frecords(XRing& x, const Src& s, const uint2* recs, uint32_t cnt) {
+    const uint32_t l = lane();
+    SeqRec r0 = frec_at(recs, l, cnt), r1 = frec_at(recs, 64 + l, cnt);
+    Lit lit0 = lit_load(s, r0);
+    uint32_t fh0 = x.safe, fh1 = x.safe;
+    for (uint32_t b = 0; b < cnt; b += 64) {
+        x.safe = fh1 > x.safe ? fh1 : x.safe;
+        fh1 = fh0;
+        fh0 = x.flushed;
+        const SeqRec r2 = frec_at(recs, b + 128 + l, cnt);
+        const Lit lit1 = lit_load(s, r1);
+        const uint32_t nb = cnt - b < 64 ? cnt - b : 64;
+        const uint64_t bigm = __ballot(l < nb && (r0.ll > kBig || r0.ml > kBig));
+        uint32_t lo = 0;
+        for (;;) {
+            const uint64_t bm = bigm & (~0ull << lo);
+            const uint32_t e = bm ? (uint32_t)__builtin_ctzll(bm) : nb;
+            if (e > lo) xbatch(x, s, r0, lo, e, lit0);
+            if (!bm) break;
+            xbig(x, s, rl(r0.lip, (int)e), rl(r0.ll, (int)e), rl(r0.ml, (int)e), rl(r0.off, (int)e));
+            lo = e + 1;
+            if (lo >= nb) break;
+        }
+        r0 = r1;
+        r1 = r2;
+        lit0 = lit1;
+    }
+}
+
 // raw bytes straight from the stream to the arena (an independent raw
-// block): 16 bytes per lane, 4 KiB per step
-// (the rows also feed the streaming CRC).  Not inlined: inlined into
-// k_lz_exec, its unrolled rows of CRC table loads pushed the kernel past the
-// 168 VGPRs its 9-wave workgroups allow; a call per raw piece is cheap.
-__device__ __noinline__ CrcState raw_copy(uint8_t* dst, const uint8_t* src, int64_t rl, uint32_t len, lds_cu32* ct,
-                                          CrcState c) {
+// block): 16 bytes per lane, U KiB per step (U loads in flight per lane)
+// (the rows also feed the streaming CRC)
+template <int U>
+DEV CrcState raw_copy_rows(uint8_t* dst, const uint8_t* src, int64_t rl, uint32_t len, lds_cu32* ct, CrcState c) {
     const Src s{src, (int64_t)len, rl};
     const uint32_t l = lane();
     uint32_t k = 0;
-    for (; k + 4096 <= len; k += 4096) {
-        uint4 v[4];
+    for (; k + 1024 * U <= len; k += 1024 * U) {
+        uint4 v[U];
 #pragma unroll
-        for (int u = 0; u < 4; u++) v[u] = ld16(s, (int64_t)k + 1024 * u + 16 * l);
+        for (int u = 0; u < U; u++) v[u] = ld16(s, (int64_t)k + 1024 * u + 16 * l);
 #pragma unroll
-        for (int u = 0; u < 4; u++) gst16(dst + k + 1024 * u + 16 * l, v[u]);
+        for (int u = 0; u < U; u++) gst16(dst + k + 1024 * u + 16 * l, v[u]);
 #pragma unroll
-        for (int u = 0; u < 4; u++) crc_row(c, ct, v[u]);
+        for (int u = 0; u < U; u++) crc_row(c, ct, v[u]);
     }
     for (; k < len; k += 1024) {
         const uint32_t q = k + 16 * l;
@@ -1656,6 +1790,14 @@ __device__ __noinline__ CrcState raw_copy(uint8_t* dst, const uint8_t* src, int6
         crc_row(c, ct, v);
     }
     return c;
+}
+// k_lz_exec's copy (raw blocks of linked frames' neighbours, checksummed
+// ones).  Not inlined: inlined into k_lz_exec, its unrolled rows of CRC
+// table loads pushed the kernel past the 168 VGPRs its 9-wave workgroups
+// allow; a call per raw piece is cheap.
+__device__ __noinline__ CrcState raw_copy(uint8_t* dst, const uint8_t* src, int64_t rl, uint32_t len, lds_cu32* ct,
+                                          CrcState c) {
+    return raw_copy_rows<4>(dst, src, rl, len, ct, c);
 }
 DEV void xcopy_raw(XRing& x, const Src& s, uint32_t len) { x.cs = raw_copy(x.dst, s.p, s.rl, len, x.ct, x.cs); }
 
@@ -2252,15 +2394,16 @@ __global__ __launch_bounds__(256) void k_lz_walk(DeviceJob j) {
     __shared__ __attribute__((aligned(16))) uint8_t wwin[4][kWaveLds];
     const uint32_t reserved = j.counters[4];
     const uint32_t nblk = reserved < j.block_capacity ? reserved : j.block_capacity;
-    const uint32_t nlong = j.counters[11];
+    const uint32_t nlong = j.counters[38];
+    const uint32_t nlane = j.counters[41] < j.block_capacity ? j.counters[41] : j.block_capacity;
     // few pieces: fewer than 512 per CU (the grid is 16 workgroups per CU, 2
     // resident: 512 lanes)
     const bool few = nblk < gridDim.x * 32u;
     lds_u8* wl = (lds_u8*)wwin[threadIdx.x >> 6];
     for (;;) {
-        const uint32_t k = wave_fetch_add(&j.counters[12], 1u);
+        const uint32_t k = wave_fetch_add(&j.counters[39], 1u);
         if (k >= nlong) break;
-        const uint32_t p = uni32(j.long_list[k]);
+        const uint32_t p = uni32(j.wlong_list[k]);
         if (uni32(j.blocks[p].fast) != kLzfNone) continue;  // the fast path has it
         if (!piece_wave_walked(uni32(j.blocks[p].kind), uni32(j.blocks[p].csize), uni32(j.blocks[p].cap), few))
             continue;  // a dense piece: the lane walk takes it
@@ -2272,14 +2415,24 @@ __global__ __launch_bounds__(256) void k_lz_walk(DeviceJob j) {
     Piece pc;
     SlabSink sink{j.pool, j.slab_next, &j.counters[9], j.pool_slabs, 0, 0, 0, 0, {}, {}, {}};
     for (;;) {
-        // lanes without a piece take the next one (pieces that end at their
-        // begin, raw ones or a failed block checksum, are written at once)
-        while (!active && !drained) {
-            p = atomicAdd(&j.counters[10], 1u);
-            if (p >= nblk) {
+        // lanes without a piece take the next ones, one claim per wave (a
+        // claim per lane serialised ~277K atomics on C2: 1.5 ms); pieces that
+        // end at their begin, raw ones or a failed block checksum, are
+        // written at once
+        for (;;) {
+            const bool want = !active && !drained;
+            const uint64_t wm = __ballot(want);
+            if (!wm) break;
+            const int lead = __builtin_ctzll(wm);
+            uint32_t u0 = 0;
+            if (lane() == (uint32_t)lead) u0 = atomicAdd(&j.counters[10], (uint32_t)__builtin_popcountll(wm));
+            const uint32_t u = rl(u0, lead) + (uint32_t)__builtin_popcountll(wm & ((1ull << lane()) - 1));
+            if (!want) continue;
+            if (u >= nlane) {
                 drained = true;
-                break;
+                continue;
             }
+            p = j.lane_list[u];
             const BlockItem it = j.blocks[p];
             if (it.fast != kLzfNone) continue;                               // the fast path has it
             if (piece_wave_walked(it.kind, it.csize, it.cap, few)) continue;  // walked above
@@ -2292,7 +2445,7 @@ __global__ __launch_bounds__(256) void k_lz_walk(DeviceJob j) {
                     sink.slab = fs;
                     sink.pos = sink.n = sink.cut = 0;
                     active = true;
-                    break;
+                    continue;
                 }
             }
             put_pstate(j, p, pc.ps, 0, first_slab);
@@ -2333,9 +2486,19 @@ DEV int32_t exec_piece(XRing& x, const DeviceJob& j, uint32_t p, uint32_t hist, 
     const uint64_t src = uni64(itr.src);
     const uint32_t csize = uni32(itr.csize), kind = uni32(itr.kind), cap = uni32(itr.cap);
     const PieceState& psr = j.pstate[p];
+    const uint32_t fast = uni32(itr.fast);
+    if (fast == kLzfReject) return -1;
     int32_t st = (int32_t)uni32((uint32_t)psr.st);
     if (st < 0) return -1;
     const Src s{j.data + src, (int64_t)csize, (int64_t)(j.data_len - src)};
+    if (fast == kLzfReady) {
+        // walked by k_lzf_walk: its 8-byte records; a linked block's matches
+        // reach at most `need` before it (checked against the real history)
+        const uint32_t start = x.op;
+        frecords(x, s, j.frecs + uni32(psr.first_slab), uni32(psr.nrec));
+        if ((int32_t)uni32((uint32_t)psr.need) > (int32_t)hist) return -1;
+        return (int32_t)(x.op - start);
+    }
     if (kind & kBlkRaw) {
         if (x.hist) xbig(x, s, 0, csize, 0, 0);
         else {
@@ -2434,7 +2597,12 @@ DEV void exec_linked(const DeviceJob& j, lds_u8* ring, SeqRec* buf, uint32_t ite
 // one independent piece
 DEV void exec_one(const DeviceJob& j, lds_u8* ring, SeqRec* buf, uint32_t p, uint32_t kind,
                   const __attribute__((address_space(3))) uint32_t* pat, lds_cu32* ct) {
-    if (uni32(j.blocks[p].fast) != kLzfNone) return;  // k_lzf_parse / k_lzf_exec have it
+    const uint32_t fast = uni32(j.blocks[p].fast);
+    if (fast == kLzfRaw) return;  // k_raw_copy did it
+    if (fast == kLzfReject) {
+        if (lane() == 0) j.blocks[p].out = -1;  // (k_lzf_walk wrote it; kept here for clarity)
+        return;
+    }
     {
         const uint64_t dst = uni64(j.blocks[p].dst);
         XRing x;
@@ -2515,6 +2683,40 @@ __global__ __launch_bounds__(64 * kExecWaves) void k_lz_exec(DeviceJob j) {
             if (!(kind & kBlkLinked)) exec_one(j, ring, buf, p, kind, pat, ct);
         } else {
             exec_chunk(j, ring, buf, (u - nlink - nlong) * 64, nblk, pat, ct);
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// k_raw_copy: the independent raw LZ4F blocks without a block checksum
+// (note_raw; C2: 183 K of its 277 K blocks, 12 GB), copied to their arena
+// slots with their streaming CRC exactly as exec_one would (raw_copy,
+// crc_finish), a static stride of waves, 16 waves per CU.  It runs while
+// k_lzf_walk (latency-bound, on the side stream) parses the LZ4 blocks, so
+// the copy's HBM traffic hides behind the parse instead of holding k_lz_exec's
+// ring waves through 16 dependent load rounds per block.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(1024) void k_raw_copy(DeviceJob j) {
+    __shared__ uint32_t ct_w[2048];
+    for (uint32_t i = threadIdx.x; i < 1024u; i += blockDim.x) {
+        ct_w[i] = j.tables->braid[i >> 8][i & 255u];
+        ct_w[1024u + i] = j.tables->hdr[3u - (i >> 8)][i & 255u];
+    }
+    __syncthreads();
+    lds_cu32* ct = (lds_cu32*)ct_w;
+    const uint32_t nraw = j.counters[40];
+    const uint32_t waves = gridDim.x * (blockDim.x >> 6);
+    for (uint32_t u = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); u < nraw; u += waves) {
+        const uint32_t p = uni32(j.raw_list[u]);
+        const uint64_t src = uni64(j.blocks[p].src), dst = uni64(j.blocks[p].dst);
+        const uint32_t n = uni32(j.blocks[p].csize);
+        XRing x;
+        xring_init(x, j, nullptr, dst, false, false, nullptr, ct);
+        x.cs = raw_copy_rows<8>(x.dst, j.data + src, (int64_t)(j.data_len - src), n, ct, x.cs);
+        const uint32_t pcrc = crc_finish(x, j.tables, n);
+        if (lane() == 0) {
+            j.blocks[p].out = (int32_t)n;
+            j.blocks[p].crc = pcrc;
         }
     }
 }
@@ -2727,106 +2929,114 @@ __global__ void k_print_dstamps() {
     printf("RPGPU_DSTAMPS snappy-long iterations=%llu hops=%llu | per iteration clk: decode=%.0f hops=%.0f rest=%.0f\n",
            g[40], g[41], (double)g[42] / (g[40] ? g[40] : 1), (double)g[43] / (g[40] ? g[40] : 1),
            (double)g[44] / (g[40] ? g[40] : 1));
+    printf("RPGPU_DSTAMPS lzf walk rounds=%llu wave-steps=%llu | tails=%llu tail records=%llu\n", g[48], g[49], g[50],
+           g[51]);
     for (int i = 0; i < 64; i++) g_dst[i] = 0;
 }
 __global__ void k_init_dstamps() {
-    for (int i = 0; i < 64; i++) g_dst[i] = 0;
+    for (int i = 0; i < 46; i++) g_dst[i] = 0;  // [46, 64): k_lzf_walk / k_lzf_tail, which run before it
     g_dst[35] = ~0ull;
 }
 #endif
 
 // ===========================================================================
-// Independent-block fast path: k_lzf_parse -> k_lzf_exec.
+// LZ4 block walk for k_lz_exec: k_lzf_walk + k_lzf_tail.
 //
 // The frames Redpanda writes are LZ4F with independent 64 KiB blocks
 // (compression/internal/lz4_frame_compressor.cc:70-76: LZ4F_blockIndependent,
 // default block size), decoded by LZ4F_decompress -> LZ4_decompress_safe per
-// block (lz4_frame_compressor.cc:123-200).  Such a block is one serial chain
-// of sequences (C2's JSON blocks: ~3200 of ~20 decoded bytes each); the lane
-// walk (k_lz_walk) parses it on one lane, ~3200 dependent steps.
+// block (lz4_frame_compressor.cc:123-200).  A block is one serial chain of
+// sequences (C2's JSON blocks: ~3200 of ~20 decoded bytes each).
 //
-// k_lzf_parse runs one WAVE per block and cuts the chain instead:
-//   * the block (<= kFIn bytes) is staged in LDS;
-//   * lane k parses its 1/64 of the input from a speculative start (a wrong
-//     start resynchronises with the true token chain after a few sequences:
-//     median 4, p99 40 on C2) and marks every position it visits in an LDS
-//     bitmap;
-//   * every lane then continues past its segment until it reaches a position
-//     a later lane visited: from there the two parses coincide (a parse is a
-//     function of its position), so the true chain from lane 0 runs through
-//     lane 0's parse, its exit into the lane that owns the exit, and so on
-//     (lanes it skips were never synchronised and are discarded);
-//   * the true lanes count their sequences and output bytes, a prefix sum
-//     places them, and a second parse writes 8-byte records
-//     {lip, ll | ml, off} to frecs, checking each sequence.
+// k_lzf_walk walks one block per LANE, 64 blocks per wave, from the
+// planner's list (k_decode_blocks, lzf_eligible).  Every round each lane
+// stages the kFSlot stream bytes at its parse position in its own LDS slot
+// (all lanes' 16-byte loads in flight together: one memory latency per
+// round for the wave) and walks the sequences that start in the first kFWin
+// of them with a straight-line step (fseq_w: one unaligned 16-byte LDS read,
+// ~60 instructions, no per-sequence branches), writing each as an 8-byte
+// record {lip | ll << 16, ml | off << 16} to frecs (a block reserves
+// csize / 3 + 2 records: every sequence but the last takes >= 3 input bytes).
 // Verdicts follow LZ4_decompress_generic (liblz4 1.9.3, lz4_run above): a
 // sequence far from both ends (kFMarginIn input bytes, kFMarginOut output
 // bytes) is one the reference's fast loop takes, whose only failure is an
-// offset reaching before the block (H = 0 for an independent block); the
-// last lane runs lz4_run itself over the block's tail (safe loop, last
-// literals), from the exact state; anything else unusual (offset 0 mid-block,
-// an unsynchronised chain, no room in frecs) leaves the block to the walk /
-// exec kernels (BlockItem.fast stays kLzfNone).  k_lzf_exec then executes the
-// records with the ring executor (xbatch / xbig) into the block's arena slot,
-// taking the streaming decoded CRC on the way, as k_lz_exec does.
+// offset reaching before the block (H = 0 for an independent block; a
+// linked block's reach is kept as `need` and checked against its real
+// history when its frame executes).  At the first sequence that is not such
+// an ordinary one (the block's last ones, offset 0, a length of more than
+// one extension byte) the lane files the block for k_lzf_tail, which runs
+// lz4_run itself from that exact state to the block's end, one lane per
+// block, all tails in lock step; then takes its next block.  A block with no
+// room in frecs stays with k_lz_walk (BlockItem.fast stays kLzfNone).
+// k_lz_exec executes the records (exec_piece -> frecords) like the walk's.
+//
+// (Round 5 first tried one WAVE per block: the block staged whole in LDS,
+// lanes parsing 1/64 of it each from speculative starts that resynchronise
+// with the true chain, a visited-position bitmap to chain them.  Four
+// passes over every lane's segment plus the resynchronisation wait cost
+// ~160 us per block, 9.2 ms on C2, against ~2 wave-steps per sequence here.)
 // ===========================================================================
-#ifndef RPGPU_LZF_IN_KIB
-#define RPGPU_LZF_IN_KIB 20
-#endif
-constexpr uint32_t kFIn = RPGPU_LZF_IN_KIB * 1024u;  // largest block staged (compressed bytes)
-constexpr uint32_t kFPad = 64;                        // zero bytes after the staged block
-constexpr uint32_t kFWords = (kFIn + kFPad) / 32;     // visited-position bitmap
-constexpr uint32_t kFLds = kFIn + kFPad + 4 * kFWords;
-constexpr uint32_t kFSegMin = 256;                    // input bytes per lane at least
-constexpr uint32_t kFMarginIn = 64, kFMarginOut = 128;
-static_assert(kFIn % 16 == 0 && kFLds <= 64u * 1024u, "fast-path LDS image");
 
 typedef __attribute__((address_space(3))) uint32_t lds_u32;
 
-// one sequence at ip < n of the staged block, no checks: literal [lip, lip +
-// ll), match (off, ml; ml = 0: the stream ends in this literal run), next
-// token at nxt (> n when the lengths run past the block)
+// one sequence at ip: literal [lip, lip + ll), match (off, ml; ml = 0: the
+// stream ends in this literal run), next token at nxt (> n when the lengths
+// run past the block)
 struct FSeq {
     uint32_t lip, ll, ml, off, nxt;
 };
-DEV FSeq fseq(const lds_u8* in, uint32_t ip, uint32_t n) {
+// fseq_w: the sequence at ip of a lane window: slot holds stream bytes
+// [wb, wb + kFSlot), zero past the block's n bytes; ip - wb < kFWin.  Three
+// aligned 8-byte LDS reads (24 bytes from ip rounded down to 8) funnel-shifted
+// to the 16 bytes at ip cover the token, a literal-length byte, literals up
+// to 11 bytes, the offset and a match-length byte (C2: 98 % of sequences);
+// otherwise two aligned dwords at the literals' end.  (Unaligned LDS reads
+// stalled the LDS pipe: SQ_LDS_UNALIGNED_STALL was 87 % of its active
+// cycles.)  st: 0 parsed; 1 a length needs more than one extension byte; 2
+// the offset bytes lie too close to the window's end.  (Byte for byte the
+// parse of LZ4_decompress_generic's length reads; checked against a
+// byte-wise parse on adversarial streams.)
+DEV FSeq fseq_w(const lds_u8* slot, uint32_t wb, uint32_t ip, uint32_t n, uint32_t& st) {
+    typedef const __attribute__((address_space(3))) uint64_t lds_cu64;
+    typedef const __attribute__((address_space(3))) uint32_t lds_cu32w;
+    const uint32_t rel = ip - wb, a = rel >> 3, sh = 8 * (rel & 7);
+    const uint64_t w0 = ((lds_cu64*)slot)[a], w1 = ((lds_cu64*)slot)[a + 1], w2 = ((lds_cu64*)slot)[a + 2];
+    const uint64_t lo = sh ? (w0 >> sh) | (w1 << (64 - sh)) : w0;
+    const uint64_t hi = sh ? (w1 >> sh) | (w2 << (64 - sh)) : w1;
+    const uint32_t tok = (uint32_t)lo & 0xFFu, b1 = ((uint32_t)lo >> 8) & 0xFFu;
+    const uint32_t l4 = tok >> 4, m4 = tok & 15u;
+    const bool e = l4 == 15;
+    const uint32_t ll = l4 + (e ? b1 : 0u);
+    const uint32_t lip = ip + (e ? 2u : 1u);
+    const uint32_t pe = lip + ll;
+    // the literals reach the end (ll > n - lip || n - lip - ll < 2): the last sequence
+    const bool last = pe + 2 > n;
+    const uint32_t k = pe - ip;
+    // bytes [k, k + 4) of the 16 for k <= 12 (a per-lane dword select
+    // compiles to branches)
+    const uint32_t fs = 8 * (k & 7);
+    const uint64_t fa = (k & 8) ? hi : lo, fb = (k & 8) ? 0ull : hi;
+    uint32_t t = (uint32_t)(fa >> fs) | (uint32_t)((fb << 1) << (63 - fs));
+    const uint32_t rp = pe - wb;
+    const bool rd = k > 12 && !last;
+    const bool past = rd && rp + 8 > kFSlot;
+    if (rd && !past) {
+        const uint32_t d0 = ((lds_cu32w*)slot)[rp >> 2], d1 = ((lds_cu32w*)slot)[(rp >> 2) + 1];
+        t = __builtin_amdgcn_alignbyte(d1, d0, rp & 3);
+    }
+    const bool me = m4 == 15;
+    const uint32_t b2 = (t >> 16) & 0xFFu;
     FSeq q;
-    const uint32_t tok = in[ip];
-    uint32_t p = ip + 1, ll = tok >> 4;
-    if (ll == 15) {
-        uint32_t b;
-        do {
-            b = p < n ? (uint32_t)in[p] : 0u;
-            p++;
-            ll += b;
-        } while (b == 255);
-    }
-    q.lip = p;
+    q.lip = lip;
     q.ll = ll;
-    q.ml = 0;
-    q.off = 0;
-    if (p > n || ll > n - p || n - p - ll < 2) {  // the literals reach the end: the last sequence
-        q.nxt = p + ll;
-        return q;
-    }
-    p += ll;
-    q.off = (uint32_t)in[p] | ((uint32_t)in[p + 1] << 8);
-    p += 2;
-    uint32_t ml = tok & 15;
-    if (ml == 15) {
-        uint32_t b;
-        do {
-            b = p < n ? (uint32_t)in[p] : 0u;
-            p++;
-            ml += b;
-        } while (b == 255);
-    }
-    q.ml = ml + 4;
-    q.nxt = p;
+    q.off = last ? 0u : t & 0xFFFFu;
+    q.ml = last ? 0u : m4 + (me ? b2 : 0u) + 4;
+    q.nxt = last ? pe : pe + (me ? 3u : 2u);
+    st = (e && b1 == 255) ? 1u : past ? 2u : (!last && me && b2 == 255) ? 1u : 0u;
     return q;
 }
 
-// lz4_run's sink for the block's tail: 8-byte records
+// lz4_run's sink for a block's tail: 8-byte records
 struct FRecSink {
     uint2* out;
     uint32_t n, cap;
@@ -2837,334 +3047,175 @@ struct FRecSink {
     }
 };
 
-DEV uint32_t ex_scan(uint32_t v, uint32_t& total) {
-    const uint32_t incl = wave_scan(v);
-    total = rl(incl, 63);
-    return incl - v;
-}
+constexpr uint32_t kFLaneWgs = (160u * 1024u) / (256u * kFSlot);  // resident 256-lane workgroups per CU
+static_assert(kFLaneWgs >= 1, "lane windows");
 
-__global__ __launch_bounds__(64) void k_lzf_parse(DeviceJob j) {
-    extern __shared__ __attribute__((aligned(16))) uint8_t flds[];
-    lds_u8* in = (lds_u8*)flds;
-    lds_u32* bits = (lds_u32*)(flds + kFIn + kFPad);
-    const uint32_t l = lane();
-    const uint32_t reserved = j.counters[4];
-    const uint32_t nblk = reserved < j.block_capacity ? reserved : j.block_capacity;
+__global__ __launch_bounds__(256) void k_lzf_walk(DeviceJob j) {
+    __shared__ __attribute__((aligned(16))) uint8_t fwin[256 * kFSlot];
+    lds_u8* slot = (lds_u8*)fwin + kFSlot * threadIdx.x;
+    const uint32_t cnt_list = j.counters[45];
+    const uint32_t nlist = cnt_list < j.block_capacity ? cnt_list : j.block_capacity;
+    bool active = false, drained = false;
+    uint32_t p = 0, n = 0, cap = 0, ip = 0, op = 0, r = 0, resv = 0, base = 0;
+    int32_t need = 0;
+    bool linked = false;
+    Src s{nullptr, 0, 0};
+#ifdef RPGPU_DSTAMPS
+    uint64_t d_rounds = 0, d_steps = 0;
+#endif
     for (;;) {
-        const uint32_t p = wave_fetch_add(&j.counters[40], 1u);
-        if (p >= nblk) break;
-        const uint32_t kind = uni32(j.blocks[p].kind), n = uni32(j.blocks[p].csize), cap = uni32(j.blocks[p].cap);
-        // independent LZ4 blocks without a block checksum, staged whole, of
-        // at most 64 KiB out (the records' 16-bit fields)
-        if (kind != 0 || n < 16 || n > kFIn || cap > 65536u || cap < 256u) continue;
-        const uint64_t src = uni64(j.blocks[p].src);
-        const Src s{j.data + src, (int64_t)n, (int64_t)(j.data_len - src)};
-        for (uint32_t o = 16 * l; o < n + kFPad; o += 1024) {
-            uint4 v = make_uint4(0u, 0u, 0u, 0u);
-            if (o < n) {
-                v = ld16(s, o);
-                if (o + 16 > n) {  // bytes past the block read as zero
-                    const uint32_t k = n - o;
-                    uint32_t w[4] = {v.x, v.y, v.z, v.w};
+        // lanes without a block take the next ones: one claim per wave
+        for (;;) {
+            const bool want = !active && !drained;
+            const uint64_t wm = __ballot(want);
+            if (!wm) break;
+            const int lead = __builtin_ctzll(wm);
+            uint32_t u0 = 0;
+            if (lane() == (uint32_t)lead) u0 = atomicAdd(&j.counters[46], (uint32_t)__builtin_popcountll(wm));
+            const uint32_t u = rl(u0, lead) + (uint32_t)__builtin_popcountll(wm & ((1ull << lane()) - 1));
+            if (!want) continue;
+            if (u >= nlist) {
+                drained = true;
+                continue;
+            }
+            p = j.lzf_list[u];
+            const BlockItem it = j.blocks[p];
+            resv = lzf_reserve(it.csize);
+            base = j.pstate[p].first_slab;  // reserved by the planner (note_fast)
+            n = it.csize;
+            cap = it.cap;
+            linked = (it.kind & kBlkLinked) != 0;
+            s = Src{j.data + it.src, (int64_t)n, (int64_t)(j.data_len - it.src)};
+            ip = op = r = 0;
+            need = 0;
+            active = true;
+        }
+        if (!__ballot(active)) break;
+        // stage stream bytes [wb, wb + kFSlot), zero past the block
+        const uint32_t wb = ip;
+        if (active) {
+            uint4 v[kFSlot / 16];
+#pragma unroll
+            for (uint32_t c = 0; c < kFSlot / 16; c++) v[c] = ld16(s, (int64_t)wb + 16 * c);
+#pragma unroll
+            for (uint32_t c = 0; c < kFSlot / 16; c++) {
+                const int32_t keep = (int32_t)n - (int32_t)(wb + 16 * c);  // bytes of this chunk inside the block
+                if (keep < 16) {
+                    uint32_t w[4] = {v[c].x, v[c].y, v[c].z, v[c].w};
 #pragma unroll
                     for (uint32_t d = 0; d < 4; d++) {
-                        const int32_t keep = (int32_t)k - 4 * (int32_t)d;
-                        w[d] = keep >= 4 ? w[d] : keep <= 0 ? 0u : (w[d] & ((1u << (8 * keep)) - 1u));
+                        const int32_t kd = keep - 4 * (int32_t)d;
+                        w[d] = kd >= 4 ? w[d] : kd <= 0 ? 0u : (w[d] & ((1u << (8 * kd)) - 1u));
                     }
-                    v = make_uint4(w[0], w[1], w[2], w[3]);
+                    v[c] = make_uint4(w[0], w[1], w[2], w[3]);
                 }
-            }
-            __builtin_memcpy(in + o, &v, 16);
-        }
-        for (uint32_t w = l; w < kFWords; w += 64) bits[w] = 0u;
-        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-        // lane segments
-        uint32_t nl = n / kFSegMin;
-        nl = nl < 1 ? 1 : nl > 64 ? 64 : nl;
-        const uint32_t seg = n / nl;
-        const bool act = l < nl;
-        const uint32_t S = l * seg, E = l == nl - 1 ? n : S + seg;
-        // pass 1: the speculative parse of the segment, positions marked
-        uint32_t ip = S;
-        if (act) {
-            while (ip < E) {
-                __hip_atomic_fetch_or(bits + (ip >> 5), 1u << (ip & 31), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                const FSeq q = fseq(in, ip, n);
-                if (q.ml == 0) {
-                    ip = n + 1;  // the last literal run: the parse ends
-                    break;
-                }
-                ip = q.nxt;
+                __builtin_memcpy(slot + 16 * c, &v[c], 16);
             }
         }
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        // pass 1b: on past the segment to the first position a later lane visited
-        if (act) {
-            while (ip < n && !((bits[ip >> 5] >> (ip & 31)) & 1u)) {
-                const FSeq q = fseq(in, ip, n);
-                if (q.ml == 0) {
-                    ip = n + 1;
-                    break;
-                }
-                ip = q.nxt;
-            }
-        }
-        const uint32_t exit_pos = ip;
-        // the true chain: lane 0, its exit into the lane owning it, ...
-        uint32_t entry = 0xFFFFFFFFu, last = 0, cur = 0, e = 0;
-        bool chained = true;
-        for (;;) {
-            entry = l == cur ? e : entry;
-            const uint32_t q = uni32(rl(exit_pos, (int)cur));
-            if (q >= n) {
-                last = cur;
-                break;
-            }
-            uint32_t o = q / seg;
-            o = o > nl - 1 ? nl - 1 : o;
-            if (o <= cur) {
-                chained = false;
-                break;
-            }
-            cur = o;
-            e = q;
-        }
-        if (!chained) continue;
-        const bool tl = entry != 0xFFFFFFFFu;
-        const bool is_last = l == last;
-        const uint32_t stop = is_last ? n : exit_pos;
-        // pass 2: count the true lanes' sequences and output bytes
-        uint32_t cnt = 0, out = 0;
-        if (tl) {
-            uint32_t q_ip = entry;
-            while (q_ip < stop) {
-                const FSeq q = fseq(in, q_ip, n);
-                cnt++;
-                out += q.ll + q.ml;
-                if (q.ml == 0) break;
-                q_ip = q.nxt;
-            }
-        }
-        uint32_t total_cnt = 0, total_out = 0;
-        const uint32_t rec0 = ex_scan(cnt, total_cnt);
-        const uint32_t op0 = ex_scan(out, total_out);
-        if (total_out > cap || total_cnt == 0) continue;  // not a block the fast path takes: the walk decides
-        uint64_t base = 0;
-        if (l == 0) base = atomicAdd((unsigned long long*)(j.counters + 42), (unsigned long long)total_cnt);
-        base = uni64(rl64(base, 0));
-        if (base + total_cnt > j.frec_cap) continue;
-        // pass 3: the records, every sequence checked (0 ok, 1 reject, 2 fall back)
-        uint32_t verdict = 0;
-        if (tl) {
-            uint32_t q_ip = entry, op = op0, r = rec0;
-            bool tail = false;
-            while (q_ip < stop) {
-                const FSeq q = fseq(in, q_ip, n);
-                const uint32_t opl = op + q.ll, ope = opl + q.ml;
-                const bool ord = q.ml != 0 && q.nxt + kFMarginIn <= n && ope + kFMarginOut <= cap && q.off != 0;
-                if (!ord) {
-                    if (is_last) tail = true;
-                    else verdict = 2;
-                    break;
-                }
-                if (q.off > opl) {  // before the block (LZ4_decompress_safe: offset outside buffers)
-                    verdict = 1;
-                    break;
-                }
-                j.frecs[base + r] = make_uint2(q.lip | (q.ll << 16), q.ml | (q.off << 16));
-                r++;
-                op = ope;
-                q_ip = q.nxt;
-            }
-            if (tail) {
-                // the reference's loops from this sequence on (its fast-loop
-                // state: every earlier sequence was an ordinary one)
-                PState ps;
-                ps.ip = (int32_t)q_ip;
-                ps.op = (int32_t)op;
-                ps.need = 0;
-                ps.st = 0;
-                ps.ulen = 0;
-                ps.safe = cap < (uint32_t)kFastSafeDistance;
-                Src ws = s;
-                ws.win = in;
-                ws.wlo = 0;
-                ws.whi = (int64_t)(n + kFPad);
-                FRecSink fs{j.frecs + base, r, total_cnt};
-                lz4_run(ws, (int32_t)cap, 0, ps, fs);
-                if (ps.st != 1) verdict = 1;
-                else if ((uint32_t)ps.op != total_out || fs.n != total_cnt) verdict = 2;
-            }
-        }
-        const uint64_t fb = __ballot(verdict == 2), rj = __ballot(verdict == 1);
-        if (fb) continue;
-        if (l == 0) {
-            if (rj) {
-                j.blocks[p].out = -1;
-                j.blocks[p].crc = 0u;
-                j.blocks[p].fast = kLzfReject;
-            } else {
-                PieceState ps;
-                ps.ip = 0;
-                ps.op = (int32_t)total_out;
-                ps.need = 0;
-                ps.st = 1;
-                ps.ulen = 0;
-                ps.safe = 0;
-                ps.nrec = total_cnt;
-                ps.first_slab = (uint32_t)base;
-                j.pstate[p] = ps;
-                j.blocks[p].fast = kLzfReady;
-                j.fast_list[atomicAdd(&j.counters[44], 1u)] = p;
-            }
-        }
-    }
-}
-
-DEV SeqRec frec_at(const uint2* recs, uint32_t k, uint32_t cnt) {
-    SeqRec r{0u, 0u, 0u, 0u};
-    if (k < cnt) {
-        const uint2 v = recs[k];
-        r.lip = v.x & 0xFFFFu;
-        r.ll = v.x >> 16;
-        r.ml = v.y & 0xFFFFu;
-        r.off = v.y >> 16;
-    }
-    return r;
-}
-
-// xbatch for k_lzf_exec: every chunk of every far source (a match reaching
-// further back than the ring, C2: ~8 % of matches, nearly every batch has
-// one) is loaded from the arena at the start of the batch, all in flight
-// together, and written from registers in the match rounds; xbatch loads
-// them inside the rounds, one dependent load per 16-byte chunk.
-DEV void fbatch(XRing& x, const Src& s, const SeqRec& r, uint32_t lo, uint32_t hi_lane, const Lit& lit) {
-    const uint32_t l = lane();
-    const bool v = l >= lo && l < hi_lane;
-    const uint32_t len = v ? r.ll + r.ml : 0u;
-    const uint32_t incl = wave_scan(len);
-    const uint32_t o = x.op + incl - len;
-    const uint32_t hi = x.op + rl(incl, (int)hi_lane - 1);
-    const uint32_t d = o + r.ll, src = d - r.off;
-    bool pend = v && r.ml > 0;
-    // sources before (batch end - ring): their ring slots may be rewritten by this batch
-    const bool far = x.linked && pend && hi > kXRing && src < hi - kXRing;
-    if (__ballot(far && src + r.ml > x.safe) && x.fpend) {
-        wait_vm();
-        x.fpend = false;
-        x.safe = x.flushed;
-    }
-    uint4 F[kBig / 16];
-#pragma unroll
-    for (uint32_t k = 0; k < kBig / 16; k++) {
-        F[k] = make_uint4(0u, 0u, 0u, 0u);
-        if (far && r.ml > 16 * k) {
-            const auto t = __builtin_amdgcn_raw_buffer_load_b128(x.rs, src + 16 * k, 0, kSc1);
-            F[k] = make_uint4(t[0], t[1], t[2], t[3]);
-        }
-    }
-    if (v && r.ll) {
-#pragma unroll
-        for (uint32_t k = 0; k < kBig / 16; k++)
-            if (r.ll > 16 * k) xst(x.r, o + 16 * k, lit.v[k], r.ll - 16 * k < 16 ? r.ll - 16 * k : 16);
-    }
-    for (;;) {
-        const uint64_t pm = __ballot(pend);
-        if (!pm) break;
-        const int first = __builtin_ctzll(pm);
-        const uint32_t f = rl(d, first);
-        const bool ready = pend && (src + r.ml <= f || l == (uint32_t)first);
-        if (ready) {
-            if (far) {
-#pragma unroll
-                for (uint32_t k = 0; k < kBig / 16; k++)
-                    if (r.ml > 16 * k) xst(x.r, d + 16 * k, F[k], r.ml - 16 * k < 16 ? r.ml - 16 * k : 16);
-            } else {
-                xmatch(x, d, r.off, r.ml, false);
-            }
-        }
-        pend = pend && !ready;
-    }
-    x.op = hi;
-    if (x.op - x.flushed > kFlushLag) xflush_chunks(x);
-}
-
-#ifndef RPGPU_LZF_XBATCH
-#define RPGPU_LZF_XBATCH 0  // 1: k_lzf_exec through xbatch (A/B)
+        // walk the window: 0 on, 1 the tail, 2 reject, 3 restage
+        bool go = active;
+        uint32_t outcome = 0;
+#ifdef RPGPU_DSTAMPS
+        d_rounds++;
 #endif
-
-// xrecords over 8-byte records
-DEV void frecords(XRing& x, const Src& s, const uint2* recs, uint32_t cnt) {
-    const uint32_t l = lane();
-    SeqRec r0 = frec_at(recs, l, cnt), r1 = frec_at(recs, 64 + l, cnt);
-    Lit lit0 = lit_load(s, r0);
-    uint32_t fh0 = x.safe, fh1 = x.safe;
-    for (uint32_t b = 0; b < cnt; b += 64) {
-        x.safe = fh1 > x.safe ? fh1 : x.safe;
-        fh1 = fh0;
-        fh0 = x.flushed;
-        const SeqRec r2 = frec_at(recs, b + 128 + l, cnt);
-        const Lit lit1 = lit_load(s, r1);
-        const uint32_t nb = cnt - b < 64 ? cnt - b : 64;
-        const uint64_t bigm = __ballot(l < nb && (r0.ll > kBig || r0.ml > kBig));
-        uint32_t lo = 0;
-        for (;;) {
-            const uint64_t bm = bigm & (~0ull << lo);
-            const uint32_t e = bm ? (uint32_t)__builtin_ctzll(bm) : nb;
-            if (e > lo) {
-                if (RPGPU_LZF_XBATCH) xbatch(x, s, r0, lo, e, lit0);
-                else fbatch(x, s, r0, lo, e, lit0);
+        while (__ballot(go)) {
+#ifdef RPGPU_DSTAMPS
+            d_steps++;
+#endif
+            uint32_t st;
+            const FSeq q = fseq_w(slot, wb, go ? ip : wb, n, st);
+            const uint32_t opl = op + q.ll, ope = opl + q.ml;
+            const bool ord = st == 0 && q.ml != 0 && q.nxt + kFMarginIn <= n && ope + kFMarginOut <= cap && q.off != 0;
+            // before the block (LZ4_decompress_safe: offset outside buffers)
+            const bool rej = ord && !linked && q.off > opl;
+            if (go && ord && linked) {
+                const int32_t d = (int32_t)q.off - (int32_t)opl;
+                need = d > need ? d : need;
             }
-            if (!bm) break;
-            xbig(x, s, rl(r0.lip, (int)e), rl(r0.ll, (int)e), rl(r0.ml, (int)e), rl(r0.off, (int)e));
-            lo = e + 1;
-            if (lo >= nb) break;
+            const bool ok = go && ord && !rej;
+            if (ok) j.frecs[(size_t)base + r] = make_uint2(q.lip | (q.ll << 16), q.ml | (q.off << 16));
+            if (go && !ok) outcome = (st == 2 && ip > wb) ? 3u : rej ? 2u : 1u;
+            r += ok ? 1u : 0u;
+            op = ok ? ope : op;
+            ip = ok ? q.nxt : ip;
+            go = ok && ip < wb + kFWin;
         }
-        r0 = r1;
-        r1 = r2;
-        lit0 = lit1;
+        if (active && outcome == 1) {
+            // the rest is the reference loop's: k_lzf_tail
+            const uint32_t t = atomicAdd(&j.counters[47], 1u);
+            j.lzf_tail[t] = p;
+            PieceState ps;
+            ps.ip = (int32_t)ip;
+            ps.op = (int32_t)op;
+            ps.need = need;
+            ps.st = 0;
+            ps.ulen = (int32_t)resv;  // (the reservation, for k_lzf_tail)
+            ps.safe = 0;
+            ps.nrec = r;
+            ps.first_slab = base;
+            j.pstate[p] = ps;
+            active = false;
+        } else if (active && outcome == 2) {
+            j.blocks[p].out = -1;
+            j.blocks[p].crc = 0u;
+            j.blocks[p].fast = kLzfReject;
+            active = false;
+        }
     }
+#ifdef RPGPU_DSTAMPS
+    if (lane() == 0) {
+        atomicAdd(&g_dst[48], d_rounds);
+        atomicAdd(&g_dst[49], d_steps);
+    }
+#endif
 }
 
-// k_lzf_exec: the blocks k_lzf_parse made ready, one wave each (the
-// k_lz_exec workgroup layout with one ring fewer: fbatch keeps the far
-// sources in registers, and at 8 waves per workgroup the register budget is
-// 256 per lane (9 waves: 168, and fbatch spilled))
-constexpr uint32_t kFExecWaves = kExecWaves - 1;
-constexpr uint32_t kFXCrcOff = kFExecWaves * kXRing, kFXPatOff = kFXCrcOff + 8192u, kFXLds = kFXPatOff + 512u;
-__global__ __launch_bounds__(64 * kFExecWaves) void k_lzf_exec(DeviceJob j) {
-    extern __shared__ __attribute__((aligned(16))) uint8_t xlds[];
-    const uint32_t wi = threadIdx.x >> 6;
-    lds_u8* ring = (lds_u8*)(xlds + wi * kXRing);
-    uint32_t* ct_w = (uint32_t*)(xlds + kFXCrcOff);
-    uint32_t* pat_w = (uint32_t*)(xlds + kFXPatOff);
-    for (uint32_t i = threadIdx.x; i < 1024u; i += blockDim.x) {
-        ct_w[i] = j.tables->braid[i >> 8][i & 255u];
-        ct_w[1024u + i] = j.tables->hdr[3u - (i >> 8)][i & 255u];
-    }
-    for (uint32_t i = threadIdx.x; i < 128u; i += blockDim.x)
-        pat_w[i] = i < 64u ? (&kPat.a[0][0])[i] : (&kPat.b[0][0])[i - 64u];
-    __syncthreads();
-    const __attribute__((address_space(3))) uint32_t* pat = (const __attribute__((address_space(3))) uint32_t*)pat_w;
-    lds_cu32* ct = (lds_cu32*)ct_w;
-    const uint32_t count = j.counters[44];
-    for (;;) {
-        const uint32_t u = wave_fetch_add(&j.counters[41], 1u);
-        if (u >= count) break;
-        const uint32_t p = uni32(j.fast_list[u]);
-        const uint64_t src = uni64(j.blocks[p].src), dst = uni64(j.blocks[p].dst);
-        const uint32_t n = uni32(j.blocks[p].csize), cap = uni32(j.blocks[p].cap);
-        const uint32_t nrec = uni32(j.pstate[p].nrec), base = uni32(j.pstate[p].first_slab);
-        const Src s{j.data + src, (int64_t)n, (int64_t)(j.data_len - src)};
-        XRing x;
-        xring_init(x, j, ring, dst, cap > kXRing, false, pat, ct);
-        frecords(x, s, j.frecs + base, nrec);
-        xflush(x, x.op);
-        const uint32_t crc = crc_finish(x, j.tables, x.op);
-        if (lane() == 0) {
-            j.blocks[p].out = (int32_t)x.op;
-            j.blocks[p].crc = crc;
+// the tails k_lzf_walk filed: lz4_run from the first sequence that is not an
+// ordinary one (the reference's fast loop, every earlier sequence having been
+// one) to the block's end, one lane per block
+__global__ __launch_bounds__(256) void k_lzf_tail(DeviceJob j) {
+    const uint32_t nt = j.counters[47];
+    for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < nt; t += gridDim.x * blockDim.x) {
+        const uint32_t p = j.lzf_tail[t];
+        const BlockItem it = j.blocks[p];
+        PieceState pst = j.pstate[p];
+        const bool linked = (it.kind & kBlkLinked) != 0;
+        const Src s{j.data + it.src, (int64_t)it.csize, (int64_t)(j.data_len - it.src)};
+        PState ps;
+        ps.ip = pst.ip;
+        ps.op = pst.op;
+        ps.need = 0;
+        ps.st = 0;
+        ps.ulen = 0;
+        ps.safe = it.cap < (uint32_t)kFastSafeDistance;
+        const uint32_t resv = (uint32_t)pst.ulen;
+        FRecSink fs{j.frecs + pst.first_slab, pst.nrec, resv};
+        lz4_run(s, (int32_t)it.cap, linked ? 65536 : 0, ps, fs);
+#ifdef RPGPU_DSTAMPS
+        atomicAdd(&g_dst[50], 1ull);
+        atomicAdd(&g_dst[51], (unsigned long long)(fs.n - pst.nrec));
+#endif
+        if (ps.st != 1) {
+            j.blocks[p].out = -1;
+            j.blocks[p].crc = 0u;
+            j.blocks[p].fast = kLzfReject;
+            continue;
         }
+        if (fs.n > resv) {  // (cannot happen: the reservation bounds any parse)
+            j.blocks[p].out = -1;
+            j.blocks[p].fast = kLzfReject;
+            continue;
+        }
+        const int32_t need = ps.need > pst.need ? ps.need : pst.need;
+        pst.ip = 0;
+        pst.op = ps.op;
+        pst.need = need > 0 ? need : 0;
+        pst.st = 1;
+        pst.ulen = 0;
+        pst.safe = 0;
+        pst.nrec = fs.n;
+        j.pstate[p] = pst;
+        j.blocks[p].fast = kLzfReady;
     }
 }
 
@@ -3188,6 +3239,14 @@ hipError_t launch_lz_walk(const DeviceJob& j, hipStream_t s, uint32_t grid) {
     return hipGetLastError();
 }
 
+hipError_t launch_raw_copy(const DeviceJob& j, hipStream_t s, uint32_t cus) {
+    if (!j.raw_list) return hipSuccess;
+    // one 16-wave workgroup per CU (one 8 KiB CRC table copy: k_lzf_walk's
+    // two 74 KiB workgroups per CU still fit beside it)
+    hipLaunchKernelGGL(k_raw_copy, dim3(cus), dim3(1024), 0, s, j);
+    return hipGetLastError();
+}
+
 hipError_t launch_lz_exec(const DeviceJob& j, hipStream_t s) {
     static bool attr = false;
     if (!attr) {
@@ -3202,26 +3261,11 @@ hipError_t launch_lz_exec(const DeviceJob& j, hipStream_t s) {
     return hipGetLastError();
 }
 
-hipError_t launch_lzf_parse(const DeviceJob& j, hipStream_t s, uint32_t cus) {
-    static bool attr = false;
-    if (!attr) {
-        (void)hipFuncSetAttribute((const void*)k_lzf_parse, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kFLds);
-        attr = true;
-    }
-    if (!j.frecs || !j.fast_list) return hipSuccess;
-    // one wave per workgroup, as many as the LDS image allows per CU
-    hipLaunchKernelGGL(k_lzf_parse, dim3(cus * (160u * 1024u / kFLds)), dim3(64), kFLds, s, j);
-    return hipGetLastError();
-}
-
-hipError_t launch_lzf_exec(const DeviceJob& j, hipStream_t s) {
-    static bool attr = false;
-    if (!attr) {
-        (void)hipFuncSetAttribute((const void*)k_lzf_exec, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kFXLds);
-        attr = true;
-    }
-    if (!j.exec_waves || !j.frecs || !j.fast_list) return hipSuccess;
-    hipLaunchKernelGGL(k_lzf_exec, dim3(j.exec_waves / kExecWaves), dim3(64 * kFExecWaves), kFXLds, s, j);
+hipError_t launch_lzf_walk(const DeviceJob& j, hipStream_t s, uint32_t cus) {
+    if (!j.frecs || !j.lzf_list || !j.lzf_tail) return hipSuccess;
+    // persistent lane walkers, as many as the windows allow per CU; then the tails
+    hipLaunchKernelGGL(k_lzf_walk, dim3(cus * kFLaneWgs), dim3(256), 0, s, j);
+    hipLaunchKernelGGL(k_lzf_tail, dim3(cus * 2), dim3(256), 0, s, j);
     return hipGetLastError();
 }
 

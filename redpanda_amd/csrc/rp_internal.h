@@ -85,12 +85,14 @@ struct BlockItem {
     uint32_t cap;    // bytes reserved at dst (LZ4: the block maximum = the decoder's output bound)
     uint32_t crc;    // linear CRC32C (zero state, no final xor) of the decoded bytes, from k_lz_exec's
                      // flush; a linked frame's whole output on its first block
-    uint32_t fast;   // kLzf*: taken by the independent-block fast path (k_lzf_parse / k_lzf_exec)
+    uint32_t fast;   // kLzf*: walked by k_lzf_walk (executed from its records by k_lz_exec)
 };
-// BlockItem.fast: 0 the walk / exec kernels decode it; kLzfReady parsed into
-// frecs by k_lzf_parse (k_lzf_exec executes it); kLzfReject rejected there
-// (out = -1 written)
-constexpr uint32_t kLzfNone = 0, kLzfReady = 1, kLzfReject = 2;
+// BlockItem.fast: 0 k_lz_walk walks it; kLzfListed the planner gave it to
+// k_lzf_walk (frecs reserved: PieceState.first_slab); kLzfReady walked into
+// frecs by k_lzf_walk + k_lzf_tail (k_lz_exec executes those records);
+// kLzfReject rejected there (out = -1 written)
+// kLzfRaw: an independent raw block k_raw_copy copies (out / crc written there)
+constexpr uint32_t kLzfNone = 0, kLzfReady = 1, kLzfReject = 2, kLzfListed = 3, kLzfRaw = 4;
 // kBlkWhole: a raw (non-xerial) snappy payload, snappy_standard_compressor
 // semantics (length 0 is an empty result whatever follows)
 constexpr uint32_t kBlkRaw = 1, kBlkChecksum = 2, kBlkSnappy = 4, kBlkLinked = 8, kBlkWhole = 16;
@@ -228,8 +230,8 @@ struct DeviceJob {
     uint32_t* counters;           // [0] rewalks, [1] overflow bits, [2] decode items, [3] split batches,
                                   // [4] block items reserved, [5] sequential-frame claim cursor,
                                   // [6] sequential frames, [7] linked frames, [8] k_lz_exec claim cursor,
-                                  // [9] slab pool cursor, [10] k_lz_walk claim cursor, [11] long pieces,
-                                  // [12] long-piece claim cursor, [13] k_validate_decoded claim cursor,
+                                  // [9] slab pool cursor, [10] k_lz_walk lane_list cursor, [11] long pieces,
+                                  // [12] (unused), [13] k_validate_decoded claim cursor,
                                   // [14] k_decode_finish claim cursor, [15] k_crc_split claim cursor,
                                   // [16] gzip / zstd members (inf_list), [17] k_members_first / [18] k_members claim cursors,
                                   // [19] host-decoded members (host_list), [20] k_members_first's second claim cursor,
@@ -237,11 +239,15 @@ struct DeviceJob {
                                   // [28] planned literal blocks (zs_items), [29] k_zlits / [30] k_zplan claim cursors,
                                   // [32] gzip split items (gzs_items), [33] / [34] / [35] k_gzsfind / k_gzsdecode /
                                   // k_gzsresolve claim cursors, [36..37] gzs_pool symbols used (u64),
-                                  // [40] / [41] k_lzf_parse / k_lzf_exec claim cursors, [42..43] frecs used (u64), [44] fast_list count
+                                  // [38] / [39] wlong_list count / cursor, [40] raw_list count, [41] lane_list count,
+                                  // [42..43] frecs used (u64), [45] lzf_list count, [46] k_lzf_walk claim cursor,
+                                  // [47] lzf_tail count
     uint32_t* decode_list;        // batch_capacity: ordinals of batches to uncompress
     uint32_t* seq_list;           // batch_capacity: decode items decoded whole by one lane
     uint32_t* link_list;          // batch_capacity: decode items whose linked LZ4F blocks one wave decodes in order
-    uint32_t* long_list;          // block_capacity: pieces k_lz_walk walks one wave each ([11] count, [12] cursor)
+    uint32_t* long_list;          // block_capacity: pieces k_lz_exec runs alone ([11] count)
+    uint32_t* wlong_list;         // block_capacity: the long pieces k_lz_walk may walk one wave each (not
+                                  // k_lzf_walk's; [38] count, [39] cursor)
     uint32_t* split_list;         // split_capacity: stored payloads >= kSplitMin whose CRC runs in kSplitParts
                                   // chunks on separate waves ([3] count)
     uint32_t* split_part;         // split_capacity * kSplitParts: the chunks' linear CRCs
@@ -253,9 +259,12 @@ struct DeviceJob {
     SeqRec* pool;                 // record slabs
     uint32_t* slab_next;          // pool_slabs: next slab of the same piece
     uint32_t pool_slabs;
-    uint2* frecs;                 // fast-path LZ4 sequence records (k_lzf_parse -> k_lzf_exec), 8 B each
+    uint2* frecs;                 // LZ4 sequence records of k_lzf_walk (executed by k_lz_exec), 8 B each
     uint64_t frec_cap;            // records frecs holds
-    uint32_t* fast_list;          // block_capacity: pieces k_lzf_parse made ready ([44] count)
+    uint32_t* lzf_list;           // block_capacity: blocks k_lzf_walk takes (planner-listed, [45] count)
+    uint32_t* lane_list;          // block_capacity: the blocks k_lz_walk's lane loop considers ([41] count, [10] cursor)
+    uint32_t* raw_list;           // block_capacity: independent raw blocks k_raw_copy copies ([40] count)
+    uint32_t* lzf_tail;           // block_capacity: blocks whose tails k_lzf_tail runs ([47] count)
     BlockItem* blocks;            // block work list ([4] items reserved, [5] claim cursor)
     uint32_t block_capacity;
     FramePlan* plans;             // one per decode item
@@ -312,8 +321,8 @@ hipError_t launch_decode(const DeviceJob& j, hipStream_t s, uint32_t grid);    /
 hipError_t launch_decode_blocks(const DeviceJob& j, hipStream_t s, uint32_t grid);
 hipError_t launch_lz_walk(const DeviceJob& j, hipStream_t s, uint32_t grid);
 hipError_t launch_lz_exec(const DeviceJob& j, hipStream_t s);
-hipError_t launch_lzf_parse(const DeviceJob& j, hipStream_t s, uint32_t cus);
-hipError_t launch_lzf_exec(const DeviceJob& j, hipStream_t s);
+hipError_t launch_raw_copy(const DeviceJob& j, hipStream_t s, uint32_t cus);
+hipError_t launch_lzf_walk(const DeviceJob& j, hipStream_t s, uint32_t cus);
 hipError_t launch_decode_finish(const DeviceJob& j, hipStream_t s, uint32_t grid);
 // gzip members (rp_inflate.hip): first pass (into scratch) before the slot
 // scans, then the copy into the arena and the second pass where needed

@@ -139,7 +139,7 @@ struct rpgpu_ctx {
     // k_lz_walk record pool (slabs) and its chain links, grow-only
     void* pool = nullptr;
     size_t pool_bytes = 0;
-    // k_lzf_parse's 8-byte records (independent-block fast path); without it
+    // k_lzf_walk's 8-byte records (independent-block fast path); without it
     // every piece takes the walk / exec kernels
     void* fpool = nullptr;
     size_t fpool_bytes = 0;
@@ -654,7 +654,11 @@ int submit_body(rpgpu_ctx* c, const rpgpu_job* job, hipStream_t s, int stop, Pla
     const size_t o_plans = take(dec ? (bcap + 1) * sizeof(FramePlan) : 0);
     const size_t o_pstate = take(bl_cap64 * sizeof(PieceState));
     const size_t o_longl = take(bl_cap64 * 4);
-    const size_t o_fastl = take(bl_cap64 * 4);
+    const size_t o_wlong = take(bl_cap64 * 4);
+    const size_t o_rawl = take(bl_cap64 * 4);
+    const size_t o_lanel = take(bl_cap64 * 4);
+    const size_t o_lzfl = take(bl_cap64 * 4);
+    const size_t o_lzft = take(bl_cap64 * 4);
     uint64_t split_min = std::max<uint64_t>(kSplitMin, 2 * data_len / ((uint64_t)c->cu_count * kVWaves));
     // RPGPU_SPLIT_MIN_KIB (diagnostic build): override (scripts/bench_skew.py A/B)
     if (const char* e = diag_env("RPGPU_SPLIT_MIN_KIB")) split_min = std::max<uint64_t>(strtoull(e, nullptr, 10) << 10, 64);
@@ -729,6 +733,9 @@ int submit_body(rpgpu_ctx* c, const rpgpu_job* job, hipStream_t s, int stop, Pla
     j.seq_list = (uint32_t*)(ws + o_slist);
     j.link_list = (uint32_t*)(ws + o_llist);
     j.long_list = (uint32_t*)(ws + o_longl);
+    j.wlong_list = (uint32_t*)(ws + o_wlong);
+    j.raw_list = (dec && stop == kRunAll) ? (uint32_t*)(ws + o_rawl) : nullptr;
+    j.lane_list = (uint32_t*)(ws + o_lanel);
     j.split_list = (uint32_t*)(ws + o_split);
     j.split_part = (uint32_t*)(ws + o_spart);
     j.split_capacity = (uint32_t)split_cap;
@@ -742,19 +749,24 @@ int submit_body(rpgpu_ctx* c, const rpgpu_job* job, hipStream_t s, int stop, Pla
     if (const char* e = diag_env("RPGPU_POOL_SLABS")) j.pool_slabs = std::min<uint32_t>(j.pool_slabs, (uint32_t)atoi(e));
     j.pool = (SeqRec*)c->pool;
     j.slab_next = (uint32_t*)((uint8_t*)c->pool + (size_t)j.pool_slabs * kSlabRecs * sizeof(SeqRec));
-    // fast-path records: half the job's bytes (C2: 0.17 of them), 64 MiB ..
-    // 8 GiB; a block that finds no room takes the walk / exec kernels.
+    // fast-path records: the planner reserves csize / 3 + 2 per listed LZ4
+    // block (2.7 bytes per compressed byte; C2 uses 0.3 of the job's bytes),
+    // 1.5x the job's bytes, 64 MiB .. 16 GiB; a group of blocks that finds no
+    // room takes the walk / exec kernels.
     // RPGPU_LZF=0 (diagnostic build): every piece through the walk / exec (A/B)
     j.frecs = nullptr;
     j.frec_cap = 0;
-    j.fast_list = (uint32_t*)(ws + o_fastl);
+    j.lzf_list = nullptr;
+    j.lzf_tail = nullptr;
     static const bool lzf_on = [] { const char* e = diag_env("RPGPU_LZF"); return !(e && *e == '0'); }();
     if (dec && lzf_on && stop == kRunAll) {
-        const size_t want = std::min<size_t>(std::max<size_t>(data_len / 2, 64ull << 20), 8ull << 30);
+        const size_t want = std::min<size_t>(std::max<size_t>(data_len / 2 * 3, 64ull << 20), 16ull << 30);
         if (int rc = grow_pool(c, c->fpool, c->fpool_bytes, want, s)) return rc;
         if (c->fpool) {
             j.frecs = (uint2*)c->fpool;
             j.frec_cap = c->fpool_bytes / sizeof(uint2);
+            j.lzf_list = (uint32_t*)(ws + o_lzfl);
+            j.lzf_tail = (uint32_t*)(ws + o_lzft);
         }
     }
     j.seg_first_bad = (uint32_t*)(ws + o_fbad);
@@ -918,10 +930,38 @@ int submit_body(rpgpu_ctx* c, const rpgpu_job* job, hipStream_t s, int stop, Pla
     if ((job->flags & RPGPU_JOB_DECODE) && j.decoded) {
         STAGE("decode", launch_decode(j, s, c->cu_count * 8));
         STAGE("decode_blocks", launch_decode_blocks(j, s, c->cu_count * 8));
-        STAGE("lzf_parse", launch_lzf_parse(j, s, c->cu_count));
-        STAGE("lz_walk", launch_lz_walk(j, s, c->cu_count * 16));
+        {
+            // the listed LZ4 blocks (k_lzf_walk + k_lzf_tail) on the side
+            // stream, every other piece (k_lz_walk) here: the planner fixed
+            // the two sets (BlockItem.fast), so they run side by side
+            struct LzfJoin {
+                hipStream_t s = nullptr, side = nullptr;
+                hipEvent_t ev = nullptr;
+                ~LzfJoin() {
+                    if (side && hipEventRecord(ev, side) == hipSuccess) hipStreamWaitEvent(s, ev, 0);
+                }
+            } lzf_join;
+            const bool lzf = j.lzf_list != nullptr;
+            if (lzf) {
+                if (!c->side) HIPCHK(c, hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking));
+                if (!c->fork_ev) HIPCHK(c, hipEventCreateWithFlags(&c->fork_ev, hipEventDisableTiming));
+                if (!c->join_ev) HIPCHK(c, hipEventCreateWithFlags(&c->join_ev, hipEventDisableTiming));
+                HIPCHK(c, hipEventRecord(c->fork_ev, s));
+                HIPCHK(c, hipStreamWaitEvent(c->side, c->fork_ev, 0));
+                lzf_join.s = s;
+                lzf_join.ev = c->join_ev;
+                lzf_join.side = c->side;
+                STAGE("lzf_walk", launch_lzf_walk(j, c->side, c->cu_count));
+                HIPCHK(c, hipEventRecord(c->join_ev, c->side));
+            }
+            STAGE("raw_copy", launch_raw_copy(j, s, c->cu_count));
+            STAGE("lz_walk", launch_lz_walk(j, s, c->cu_count * 16));
+            if (lzf) {
+                HIPCHK(c, hipStreamWaitEvent(s, c->join_ev, 0));
+                lzf_join.side = nullptr;  // joined
+            }
+        }
         STAGE("lz_exec", launch_lz_exec(j, s));
-        STAGE("lzf_exec", launch_lzf_exec(j, s));
         STAGE("decode_finish", launch_decode_finish(j, s, c->cu_count * 8));
         STAGE("inflate", launch_inflate(j, s, c->cu_count * 4));
         STAGE("zexec", launch_zexec(j, s));

@@ -1,8 +1,11 @@
-# decode-engine cycle stamps (RPGPU_DSTAMPS build, diagnostics only) on C2 and C5
+# Decode-kernel wall-clock stamps (diag builds librpgpu_<variant>.so, never the
+# product): one C2 (or $W) bench stanza per variant in $VARS, the RPGPU_DSTAMPS lines
 set -e
 cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
-RPGPU_VARIANT=dstamps timeout -k 10 300 python -u bench.py --workloads c2 --steps 1 --warmup 0 --no-cpu-baseline > gpurun_out/dstamps_c2.out 2> gpurun_out/dstamps_c2.err
-grep RPGPU_DSTAMPS gpurun_out/dstamps_c2.out | tail -4
-RPGPU_VARIANT=dstamps timeout -k 10 300 python -u bench.py --workloads c5 --steps 1 --warmup 0 --no-cpu-baseline > gpurun_out/dstamps_c5.out 2> gpurun_out/dstamps_c5.err
-grep RPGPU_DSTAMPS gpurun_out/dstamps_c5.out | tail -4
+TAG=${1:-dst}
+for V in ${VARS:-dstamps}; do
+RPGPU_VARIANT=$V timeout -k 10 300 python -u bench.py --workloads ${W:-c2} --no-cpu-baseline --no-index --steps 2 --warmup 1 > gpurun_out/dst_${TAG}_$V.json 2> gpurun_out/dst_${TAG}_$V.err || { tail -30 gpurun_out/dst_${TAG}_$V.err; exit 1; }
+echo "== $V"
+grep -h "RPGPU_DSTAMPS" gpurun_out/dst_${TAG}_$V.err gpurun_out/dst_${TAG}_$V.json | tail -2 || true
+done

@@ -13,4 +13,4 @@ timeout -s KILL 180 rocprofv3 --pmc SQ_INSTS_LDS SQ_INSTS_SMEM SQ_INSTS_VMEM_RD 
 echo "pass b ok"
 timeout -s KILL 180 rocprofv3 --pmc SQ_LDS_BANK_CONFLICT SQ_LDS_ADDR_CONFLICT SQ_LDS_UNALIGNED_STALL SQ_LDS_IDX_ACTIVE SQ_INSTS_FLAT SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_MISC SQ_INST_CYCLES_SALU -d gpurun_out/${TAG}_c -o c --output-format csv -- $J > gpurun_out/${TAG}_c.log 2>&1
 echo "pass c ok"
-for k in k_lz_walk k_lz_exec k_validate_decoded; do echo "== $k"; python3 scripts/sq_summary.py $TAG $k; done
+for k in ${KS:-k_lz_walk k_lz_exec k_validate_decoded}; do echo "== $k"; python3 scripts/sq_summary.py $TAG $k; done
