@@ -60,7 +60,8 @@ HOST_GROUP_BYTES = 256 << 20
 # index writes 48 B per record, result 64 B per batch
 IDX_BYTES_PER_RECORD = 48
 RESULT_BYTES_PER_BATCH = 64
-DECODE_KERNELS = ("k_decode", "k_decode_blocks", "k_lz_walk", "k_lz_exec", "k_decode_finish")
+DECODE_KERNELS = ("k_decode", "k_decode_blocks", "k_lzf_walk", "k_lzf_tail", "k_raw_copy", "k_lz_walk", "k_lz_exec",
+                  "k_decode_finish")
 MEMBER_KERNELS = ("k_gzsplan", "k_gzsfind", "k_gzsdecode", "k_gzsresolve", "k_members_first", "k_zplan", "k_zlits",
                   "k_zparse", "k_zfallback", "k_zexec", "k_members", "k_inflate_copy")
 # segment-summary fields that do not depend on where a partition sits in a job

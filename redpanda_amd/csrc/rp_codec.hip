@@ -1330,7 +1330,11 @@ static_assert(kXRing >= kFlushLag + 2048 + 128, "ring too small for xbig's far r
 // single copy) and the short-offset pattern selectors.  (One wave per
 // workgroup left no room for shared tables; 9 rings + 8.5 KiB fit 160 KiB,
 // as many waves per CU as the 10 one-wave workgroups that were resident.)
+#ifdef RPGPU_EXEC_WAVES
+constexpr uint32_t kExecWaves = RPGPU_EXEC_WAVES;  // (experiment builds)
+#else
 constexpr uint32_t kExecWaves = (160u * 1024u - 8704u) / kXRing;
+#endif
 constexpr uint32_t kXCrcOff = kExecWaves * kXRing;
 constexpr uint32_t kXPatOff = kXCrcOff + 8192u;
 constexpr uint32_t kXLds = kXPatOff + 512u;
@@ -2696,7 +2700,10 @@ __global__ __launch_bounds__(64 * kExecWaves) void k_lz_exec(DeviceJob j) {
 // the copy's HBM traffic hides behind the parse instead of holding k_lz_exec's
 // ring waves through 16 dependent load rounds per block.
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(1024) void k_raw_copy(DeviceJob j) {
+#ifndef RPGPU_RAW_THREADS
+#define RPGPU_RAW_THREADS 1024
+#endif
+__global__ __launch_bounds__(RPGPU_RAW_THREADS) void k_raw_copy(DeviceJob j) {
     __shared__ uint32_t ct_w[2048];
     for (uint32_t i = threadIdx.x; i < 1024u; i += blockDim.x) {
         ct_w[i] = j.tables->braid[i >> 8][i & 255u];
@@ -3243,7 +3250,7 @@ hipError_t launch_raw_copy(const DeviceJob& j, hipStream_t s, uint32_t cus) {
     if (!j.raw_list) return hipSuccess;
     // one 16-wave workgroup per CU (one 8 KiB CRC table copy: k_lzf_walk's
     // two 74 KiB workgroups per CU still fit beside it)
-    hipLaunchKernelGGL(k_raw_copy, dim3(cus), dim3(1024), 0, s, j);
+    hipLaunchKernelGGL(k_raw_copy, dim3(cus), dim3(RPGPU_RAW_THREADS), 0, s, j);
     return hipGetLastError();
 }
 

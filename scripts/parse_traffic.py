@@ -51,7 +51,8 @@ def alg_bytes(w, st):
     a = {
         # CRC of every stored payload, 128 B per batch result (read + write)
         "k_validate": st["stored_payload"] + 128 * st["batches"],
-        "k_lz_walk": st["compressed_in"],
+        "k_lz_walk": None,  # (round 5: only the pieces k_lzf_walk does not take)
+        "k_lzf_walk": st["compressed_in"],
         "k_lz_exec": st["decoded"],
         "k_validate_decoded": st["decoded"] + idx * st["records"],
     }
