@@ -1270,6 +1270,11 @@ DEV uint32_t gzs_bits(const InfIn& in, uint64_t q, const gzs_lds_u32* w, uint64_
     return sh ? __builtin_amdgcn_alignbit(d1, d0, sh) : d0;
 }
 
+// the dword at 4-aligned physical byte a: from the LDS window when it holds it
+DEV uint32_t gzs_dw(const InfIn& in, uint64_t a, const gzs_lds_u32* w, uint64_t wa) {
+    return (a >= wa && a + 4 <= wa + kGzsWin) ? w[(a - wa) >> 2] : inf_ld(in, a);
+}
+
 // stage 2 of the block-header search, one candidate per lane: decode the
 // code lengths at bit p through the lane's own table tb (128 entries: the
 // next 7 stream bits -> symbol | length << 5) and require what a valid
@@ -2586,36 +2591,85 @@ __global__ __launch_bounds__(64) void k_zplan(DeviceJob j) {
 }
 
 // A per-lane bit-stream environment for k_zlits: each lane reads its own
-// stream straight from the payload (a stream moves down through L1-resident
-// lines; no wave-cooperative window, the lanes diverge)
+// stream through its own LDS window (kW bytes ending just past the read: the
+// streams move down), refilled with kW / 16 independent 16-byte loads issued
+// together when a read leaves it.  (Reading each reload's 8 bytes straight
+// from the payload put one global-memory latency on the chain every ~7
+// literals: k_zlits was 27 ms of C6's member pass.)  uni: the whole wave
+// reads one stream (a sequence section), its window filled 16 bytes per lane.
 struct ZPer {
     const uint8_t* src;
     uint64_t n;
+    inf_lds_u8* win;  // this stream's window: kW + 16 bytes, 16-aligned
+    bool uni;
+    static constexpr uint32_t kW = 256, kWU = 1024;
+    DEV uint64_t fill(uint64_t pos) {
+        const uint32_t W = uni ? kWU : kW;
+        // [nb, nb + W) holds [pos, pos + 8) at its top (16-aligned base)
+        const uint64_t nb = pos + 8 + 15 > W ? (pos + 8 + 15 - W) & ~15ull : 0;
+        auto chunk = [&](uint64_t a) {
+            uint4 v = make_uint4(0u, 0u, 0u, 0u);
+            if (a + 16 <= n) {
+                __builtin_memcpy(&v, (const __attribute__((address_space(1))) uint8_t*)(src + a), 16);
+            } else {
+                uint32_t w4[4] = {0u, 0u, 0u, 0u};
+                for (uint32_t k = 0; k < 16; k++)
+                    if (a + k < n) w4[k >> 2] |= (uint32_t)src[a + k] << (8 * (k & 3));
+                v = make_uint4(w4[0], w4[1], w4[2], w4[3]);
+            }
+            return v;
+        };
+        if (uni) {
+            const uint32_t l = lane();
+            const uint4 v = chunk(nb + 16u * l);
+            __builtin_memcpy(win + 16u * l, &v, 16);
+            if (l == 0) {
+                const uint4 t = chunk(nb + kWU);
+                __builtin_memcpy(win + kWU, &t, 16);
+            }
+        } else {
+            uint4 v[kW / 16 + 1];
+#pragma unroll
+            for (uint32_t c = 0; c <= kW / 16; c++) v[c] = chunk(nb + 16u * c);
+#pragma unroll
+            for (uint32_t c = 0; c <= kW / 16; c++) __builtin_memcpy(win + 16u * c, &v[c], 16);
+        }
+        __builtin_amdgcn_s_waitcnt(0);  // (the wave's LDS stores land before its reads)
+        return nb;
+    }
     DEV uint32_t b(uint64_t i) { return i < n ? (uint32_t)src[i] : 0u; }
     DEV uint64_t le(uint64_t i, uint32_t k) {
         uint64_t v = 0;
         for (uint32_t t = 0; t < k; t++) v |= (uint64_t)b(i + t) << (8 * t);
         return v;
     }
-    DEV uint64_t lb(zs::Bits&, uint64_t pos) {  // pos + 8 <= n
-        uint64_t v;
-        __builtin_memcpy(&v, (const __attribute__((address_space(1))) uint8_t*)(src + pos), 8);
-        return v;
+    DEV uint64_t lb(zs::Bits& s, uint64_t pos) {  // pos + 8 <= n
+        const uint32_t W = uni ? kWU : kW;
+        if (pos < s.wbase || pos + 8 > s.wbase + W) s.wbase = fill(pos);
+        const uint32_t o = (uint32_t)(pos - s.wbase), a = o & ~3u, sh = o & 3u;
+        typedef const __attribute__((address_space(3))) uint32_t lds_cu32_t;
+        const uint32_t d0 = *(lds_cu32_t*)(win + a), d1 = *(lds_cu32_t*)(win + a + 4), d2 = *(lds_cu32_t*)(win + a + 8);
+        return (uint64_t)__builtin_amdgcn_alignbyte(d1, d0, sh) | ((uint64_t)__builtin_amdgcn_alignbyte(d2, d1, sh) << 32);
     }
     DEV uint32_t U(uint32_t x) { return x; }
     DEV zs::SeqSym sym(const zs::SeqSym& t) { return t; }
 };
+// k_zlits' LDS: the tables, then the sequence stream's window, then the four
+// literal streams' windows
+constexpr uint32_t kZlitsWinU = kZsTabBytes;
+constexpr uint32_t kZlitsWinL = kZlitsWinU + ZPer::kWU + 16;
+constexpr uint32_t kZlitsLds = kZlitsWinL + 4 * (ZPer::kW + 16);
 
 // a planned sequence section: its FSE tables into LDS, its stream decoded by
 // zs::seq_decode into raw sequences (every lane computes the same values,
 // lane 0 stores them), then whether the stream ended exactly
-DEV void zseq_item(const DeviceJob& j, zs::Tabs* T, ZsSeqItem* it) {
+DEV void zseq_item(const DeviceJob& j, zs::Tabs* T, ZsSeqItem* it, inf_lds_u8* win) {
     const uint32_t l = lane();
     const uint32_t* tab = (const uint32_t*)(j.inf_scratch + uni64(it->tab));
     uint32_t* dst = (uint32_t*)T->ll;
     for (uint32_t u = l; u < (uint32_t)(kZsSeqTab / 4); u += 64) dst[u] = tab[u];
     __builtin_amdgcn_s_waitcnt(0);
-    ZPer e{j.data + uni64(it->src), uni64(it->n)};
+    ZPer e{j.data + uni64(it->src), uni64(it->n), win, true};
     const uint32_t nseq = uni32(it->nseq);
     zs::RawSeq* out = (zs::RawSeq*)(j.inf_scratch + uni64(it->seqs));
     zs::Bits d;
@@ -2649,7 +2703,7 @@ __global__ __launch_bounds__(64) void k_zlits(DeviceJob j) {
         if (k >= count) break;
         const uint64_t ref = uni64(j.zs_items[k]);
         if (ref >> 63) {
-            zseq_item(j, T, (ZsSeqItem*)(j.inf_scratch + (ref & ~(1ull << 63))));
+            zseq_item(j, T, (ZsSeqItem*)(j.inf_scratch + (ref & ~(1ull << 63))), (inf_lds_u8*)(lds + kZlitsWinU));
             continue;
         }
         ZsLitItem* it = (ZsLitItem*)(j.inf_scratch + ref);
@@ -2659,7 +2713,7 @@ __global__ __launch_bounds__(64) void k_zlits(DeviceJob j) {
         __builtin_amdgcn_s_waitcnt(0);  // (one wave: its LDS stores land before its loads)
         bool ok = true;
         if (l < ns) {
-            ZPer e{j.data + it->src, it->n};
+            ZPer e{j.data + it->src, it->n, (inf_lds_u8*)(lds + kZlitsWinL + (ZPer::kW + 16) * l), false};
             const uint32_t cnt = it->cnt[l], seg = it->seg;
             const bool x2 = it->x2 != 0;
             uint8_t* dst = j.inf_scratch + it->lits + (uint64_t)l * seg;
@@ -2830,14 +2884,12 @@ __global__ __launch_bounds__(256) void k_gzsplan(DeviceJob j) {
 }
 
 // the first dynamic-block header of each chunk k >= 1
-constexpr uint32_t kGzsFindLds = 64 * 128 + 128 * 8 + kGzsWin;
+constexpr uint32_t kGzsFindLds = 64 * 128 + kGzsWin;
 __global__ __launch_bounds__(64) void k_gzsfind(DeviceJob j) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     const uint32_t l = lane();
     inf_lds_u8* tb = (inf_lds_u8*)lds + 128 * l;
-    typedef __attribute__((address_space(3))) uint64_t lds_u64;
-    lds_u64* queue = (lds_u64*)(lds + 64 * 128);
-    gzs_lds_u32* w = (gzs_lds_u32*)(lds + 64 * 128 + 128 * 8);
+    gzs_lds_u32* w = (gzs_lds_u32*)(lds + 64 * 128);
     const uint32_t nit = min(j.counters[32], j.gzs_items_cap);
     for (;;) {
         const uint32_t t = wave_fetch_add(&j.counters[33], 1u);
@@ -2850,45 +2902,76 @@ __global__ __launch_bounds__(64) void k_gzsfind(DeviceJob j) {
         // the chunk's bytes (and 2 KiB past them) into LDS
         const uint64_t wa = (uni64(it->begin) + in.mis) & ~3ull;
         for (uint32_t d = l; d < kGzsWin / 4; d += 64) w[d] = inf_ld(in, wa + 4ull * d);
+        // 64 bit positions per lane, 4096 per step: the fixed header bits
+        // (BFINAL 0, BTYPE 2, HLIT <= 29, HDIST <= 29) of all 64 at once from
+        // the lane's 160 stream bits (word shifts), the code-length code's
+        // Kraft sum per survivor (~9 % of positions), then the full header
+        // check (gzs_check) lane-parallel on the Kraft survivors in position
+        // order.  (One position per lane per step spent ~100 instructions a
+        // position: 26 ms of C6's member pass.)
+        const uint64_t q_lo = 8 * uni64(it->begin);
+        const uint64_t q_hi = pend < (nbits >= 128 ? nbits - 127 : 0) ? pend : (nbits >= 128 ? nbits - 127 : 0);
+        const uint64_t pb0 = (q_lo + 8ull * in.mis) & ~63ull;  // physical bit, 64-aligned
         uint64_t found = ~0ull;
-        uint32_t qn = 0;
-        for (uint64_t p0 = 8 * uni64(it->begin); p0 < pend && found == ~0ull; p0 += 64) {
-            const uint64_t p = p0 + l;
-            bool pass = false;
-            if (p < pend && p + 128 <= nbits) {
-                const uint32_t a = gzs_bits(in, p, w, wa);
-                // a final block is not looked for (the chunk before decodes on through it)
-                if ((a & 7u) == 4u && ((a >> 3) & 31u) <= 29u && ((a >> 8) & 31u) <= 29u) {
-                    const uint32_t b2 = gzs_bits(in, p + 32, w, wa), c = gzs_bits(in, p + 64, w, wa);
-                    const uint32_t ncode = ((a >> 13) & 15u) + 4;
-                    const uint64_t x = (((uint64_t)b2 << 32 | a) >> 17) | ((uint64_t)c << 47);
-                    uint32_t kr = 0;
+        for (uint64_t pb = pb0; found == ~0ull; pb += 4096) {
+            const uint64_t plane = pb + 64ull * l;     // this lane's first physical bit
+            const uint64_t ql = plane - 8ull * in.mis;  // ... as a stream bit position
+            if (uni64(pb - 8ull * in.mis) >= q_hi) break;
+            // valid positions ql + i: q_lo <= . < q_hi
+            uint64_t vm = 0;
+            if (ql + 64 > q_lo && ql < q_hi) {
+                const uint32_t i0 = q_lo > ql ? (uint32_t)(q_lo - ql) : 0u;
+                const uint32_t i1 = q_hi - ql < 64 ? (uint32_t)(q_hi - ql) : 64u;
+                vm = (i1 >= 64 ? ~0ull : ((1ull << i1) - 1)) & ~((1ull << i0) - 1);
+            }
+            const uint64_t a = plane >> 3;
+            const uint32_t d0 = gzs_dw(in, a, w, wa), d1 = gzs_dw(in, a + 4, w, wa), d2 = gzs_dw(in, a + 8, w, wa),
+                           d3 = gzs_dw(in, a + 12, w, wa), d4 = gzs_dw(in, a + 16, w, wa);
+            const uint64_t lo = (uint64_t)d1 << 32 | d0, hi = (uint64_t)d3 << 32 | d2;
+#define GZS_SH(k) ((lo >> (k)) | (hi << (64 - (k))))
+            uint64_t m = vm & ~lo & ~GZS_SH(1) & GZS_SH(2);
+            m &= ~(GZS_SH(4) & GZS_SH(5) & GZS_SH(6) & GZS_SH(7));
+            m &= ~(GZS_SH(9) & GZS_SH(10) & GZS_SH(11) & GZS_SH(12));
+#undef GZS_SH
+            // the code-length code of each survivor: HCLEN at i + 13, 19 x 3 bits after
+            uint64_t km = 0;
+            for (uint64_t mm = m; mm; mm &= mm - 1) {
+                const uint32_t i = (uint32_t)__builtin_ctzll(mm), o = i + 13;
+                const uint32_t k = o >= 64 ? o - 64 : 0u;
+                const uint64_t v = o < 64 ? (lo >> o) | (hi << (64 - o))
+                                          : (hi >> k) | (k ? (uint64_t)d4 << (64 - k) : 0ull);
+                const uint32_t ncode = (uint32_t)(v & 15u) + 4;
+                const uint64_t x = v >> 4;
+                uint32_t kr = 0;
 #pragma unroll
-                    for (uint32_t q = 0; q < 19; q++) {
-                        const uint32_t L = (uint32_t)(x >> (3 * q)) & 7u;
-                        if (q < ncode && L) kr += 128u >> L;
-                    }
-                    pass = kr == 128u;
+                for (uint32_t q = 0; q < 19; q++) {
+                    const uint32_t L = (uint32_t)(x >> (3 * q)) & 7u;
+                    if (q < ncode && L) kr += 128u >> L;
                 }
+                if (kr == 128u) km |= 1ull << i;
             }
-            const uint64_t m = __ballot(pass);
-            if (pass) queue[qn + (uint32_t)__builtin_popcountll(m & ((1ull << l) - 1ull))] = p;
-            qn += (uint32_t)__builtin_popcountll(m);
-            const bool last = p0 + 64 >= pend;
-            while (qn >= 64 || (last && qn > 0)) {
-                const uint32_t take = qn < 64 ? qn : 64;
-                const bool ok = l < take ? gzs_check(in, queue[l], tb, nbits, w, wa) : false;
-                const uint64_t mm = __ballot(ok);
-                if (mm) {
-                    found = uni64(queue[__builtin_ctzll(mm)]);
-                    qn = 0;
-                    break;
+            // the full check, each lane on its survivors in order; the answer
+            // is the lowest position that passes once every lower survivor
+            // (lower lanes' included) has failed
+            uint64_t best = ~0ull;
+            for (;;) {
+                const uint64_t mine = km ? ql + (uint64_t)__builtin_ctzll(km) : ~0ull;
+                const bool go = mine < best;
+                if (!__ballot(go)) break;
+                bool ok = false;
+                if (go) {
+                    ok = gzs_check(in, mine, tb, nbits, w, wa);
+                    km &= km - 1;
                 }
-                const uint32_t rest = qn - take;
-                const uint64_t mv = l < rest ? queue[take + l] : 0ull;
-                if (l < rest) queue[l] = mv;
-                qn = rest;
+                uint64_t cand = ok ? mine : ~0ull;
+#pragma unroll
+                for (int sh = 32; sh > 0; sh >>= 1) {
+                    const uint64_t o2 = __shfl_xor(cand, sh, 64);
+                    cand = o2 < cand ? o2 : cand;
+                }
+                best = cand < best ? cand : best;
             }
+            found = uni64(best);
         }
         if (l == 0) it->start = found;
     }
@@ -3138,11 +3221,11 @@ hipError_t launch_zplan(const DeviceJob& j, hipStream_t s, uint32_t grid) {
 hipError_t launch_zparse(const DeviceJob& j, hipStream_t s, uint32_t grid) {
     static bool attr = false;
     if (!attr) {
-        (void)hipFuncSetAttribute((const void*)k_zlits, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kZsTabBytes);
+        (void)hipFuncSetAttribute((const void*)k_zlits, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kZlitsLds);
         (void)hipFuncSetAttribute((const void*)k_zparse, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kMemLds);
         attr = true;
     }
-    hipLaunchKernelGGL(k_zlits, dim3(grid * 2), dim3(64), kZsTabBytes, s, j);
+    hipLaunchKernelGGL(k_zlits, dim3(grid * 2), dim3(64), kZlitsLds, s, j);
     hipLaunchKernelGGL(k_zparse, dim3(grid), dim3(64), kMemLds, s, j);
     return hipGetLastError();
 }
