@@ -982,7 +982,7 @@ DEV void note_longs(const DeviceJob& j, uint32_t base, uint64_t m, uint64_t w) {
 constexpr uint32_t kFWin = RPGPU_LZF_WIN;  // sequence starts walked per staged window
 constexpr uint32_t kFSlot = kFWin + 32;    // + a 16-byte read at the last start, or the offset bytes after it
 constexpr uint32_t kFMarginIn = 64, kFMarginOut = 128;
-static_assert(kFWin % 16 == 0 && kFWin >= 64, "lane window");
+static_assert(kFWin % 32 == 0 && kFWin >= 64, "lane window");
 // a planned LZ4 block k_lzf_walk takes: no raw block, no block checksum
 // (independent or linked), at most 64 KiB in and out (the records' 16-bit
 // fields)
@@ -1428,7 +1428,10 @@ DEV uint32_t crc_finish(const XRing& x, const Tables* __restrict__ T, uint32_t n
     return multmodp(uni32(T->inv_shift[(c.crow - n) & 1023u]), uni32(acc));
 }
 
-// 16 ring bytes at position p (wrapping)
+// 16 ring bytes at position p (wrapping).  (Three aligned 8-byte reads
+// funnel-shifted instead of one unaligned 16-byte read: C2 decode 26.1 ->
+// 27.8 ms, the extra instructions cost more than the LDS pipe's unaligned
+// stalls saved.)
 DEV uint4 xld16(const lds_u8* r, uint32_t p) {
     const uint32_t sl = p & kXM;
     if (sl <= kXRing - 16) {
@@ -3100,23 +3103,29 @@ __global__ __launch_bounds__(256) void k_lzf_walk(DeviceJob j) {
         if (!__ballot(active)) break;
         // stage stream bytes [wb, wb + kFSlot), zero past the block
         const uint32_t wb = ip;
+        // (in two halves: 9 loads in flight per lane, ~36 fewer VGPRs, so two
+        // workgroups per CU stay resident beside k_raw_copy's)
+#pragma unroll
+        for (uint32_t h = 0; h < 2; h++)
         if (active) {
-            uint4 v[kFSlot / 16];
+            constexpr uint32_t kH = kFSlot / 32;
+            uint4 v[kH];
 #pragma unroll
-            for (uint32_t c = 0; c < kFSlot / 16; c++) v[c] = ld16(s, (int64_t)wb + 16 * c);
+            for (uint32_t c0 = 0; c0 < kH; c0++) v[c0] = ld16(s, (int64_t)wb + 16 * (h * kH + c0));
 #pragma unroll
-            for (uint32_t c = 0; c < kFSlot / 16; c++) {
+            for (uint32_t c0 = 0; c0 < kH; c0++) {
+                const uint32_t c = h * kH + c0;
                 const int32_t keep = (int32_t)n - (int32_t)(wb + 16 * c);  // bytes of this chunk inside the block
                 if (keep < 16) {
-                    uint32_t w[4] = {v[c].x, v[c].y, v[c].z, v[c].w};
+                    uint32_t w[4] = {v[c0].x, v[c0].y, v[c0].z, v[c0].w};
 #pragma unroll
                     for (uint32_t d = 0; d < 4; d++) {
                         const int32_t kd = keep - 4 * (int32_t)d;
                         w[d] = kd >= 4 ? w[d] : kd <= 0 ? 0u : (w[d] & ((1u << (8 * kd)) - 1u));
                     }
-                    v[c] = make_uint4(w[0], w[1], w[2], w[3]);
+                    v[c0] = make_uint4(w[0], w[1], w[2], w[3]);
                 }
-                __builtin_memcpy(slot + 16 * c, &v[c], 16);
+                __builtin_memcpy(slot + 16 * c, &v[c0], 16);
             }
         }
         // walk the window: 0 on, 1 the tail, 2 reject, 3 restage

@@ -690,7 +690,10 @@ DEV void note_bad(const DeviceJob& j, uint32_t seg, uint64_t b) {
 // Stored payloads with at most kLaneWalkMax records are walked one lane per
 // batch by k_walk; k_validate walks the rest (and decoded payloads) with the
 // wave-parallel walk.
-constexpr int32_t kLaneWalkMax = 256;
+#ifndef RPGPU_LANE_WALK_MAX
+#define RPGPU_LANE_WALK_MAX 256
+#endif
+constexpr int32_t kLaneWalkMax = RPGPU_LANE_WALK_MAX;
 DEV bool lane_walked(uint32_t flags, uint32_t codec, int32_t rc) {
     return (flags & RPGPU_F_COMPLETE) && codec == 0 && rc <= kLaneWalkMax;
 }
