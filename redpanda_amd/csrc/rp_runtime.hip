@@ -254,6 +254,22 @@ const char* diag_env(const char* name) { return getenv(name); }
 const char* diag_env(const char*) { return nullptr; }
 #endif
 
+// The side stream of a job (the zstd member pass beside the gzip one, the LZ4
+// lane walk beside the raw copies and the other pieces' walk): created at the
+// device's highest stream priority.  HIP spreads a process's streams over
+// GPU_MAX_HW_QUEUES hardware queues (4 here) round robin, and a side stream
+// that lands on the caller's queue runs after it instead of beside it (C6's
+// member pass measured 64 ms alone, 77 ms after the bench's H2D stanza had
+// created its copy streams); a priority of its own gives it a queue of its own.
+// RPGPU_SIDE_PRIO=0 (diagnostic build): the default priority (A/B).
+hipError_t side_stream_create(rpgpu_ctx* c) {
+    static const bool prio = [] { const char* e = diag_env("RPGPU_SIDE_PRIO"); return !(e && *e == '0'); }();
+    int least = 0, greatest = 0;
+    if (prio && hipDeviceGetStreamPriorityRange(&least, &greatest) == hipSuccess && greatest != least)
+        return hipStreamCreateWithPriority(&c->side, hipStreamNonBlocking, greatest);
+    return hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking);
+}
+
 // gzip / zstd: the CPU fallback behind compressor::uncompress (rp_hostcodec.cpp)
 int host_codec(rpgpu_ctx* c, int codec, const void* in, size_t n, void* out, size_t cap, size_t* out_len) {
     const int rc = host_uncompress(codec, (const uint8_t*)in, n, (uint8_t*)out, cap, out_len);
@@ -888,7 +904,7 @@ int submit_body(rpgpu_ctx* c, const rpgpu_job* job, hipStream_t s, int stop, Pla
             }
         } side_join;
         if (split) {
-            if (!c->side) HIPCHK(c, hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking));
+            if (!c->side) HIPCHK(c, side_stream_create(c));
             if (!c->fork_ev) HIPCHK(c, hipEventCreateWithFlags(&c->fork_ev, hipEventDisableTiming));
             if (!c->join_ev) HIPCHK(c, hipEventCreateWithFlags(&c->join_ev, hipEventDisableTiming));
             j.zs_split = 1;
@@ -943,7 +959,7 @@ int submit_body(rpgpu_ctx* c, const rpgpu_job* job, hipStream_t s, int stop, Pla
             } lzf_join;
             const bool lzf = j.lzf_list != nullptr;
             if (lzf) {
-                if (!c->side) HIPCHK(c, hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking));
+                if (!c->side) HIPCHK(c, side_stream_create(c));
                 if (!c->fork_ev) HIPCHK(c, hipEventCreateWithFlags(&c->fork_ev, hipEventDisableTiming));
                 if (!c->join_ev) HIPCHK(c, hipEventCreateWithFlags(&c->join_ev, hipEventDisableTiming));
                 HIPCHK(c, hipEventRecord(c->fork_ev, s));
