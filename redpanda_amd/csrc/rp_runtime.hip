@@ -970,12 +970,15 @@ int submit_body(rpgpu_ctx* c, const rpgpu_job* job, hipStream_t s, int stop, Pla
                 STAGE("lzf_walk", launch_lzf_walk(j, c->side, c->cu_count));
                 HIPCHK(c, hipEventRecord(c->join_ev, c->side));
             }
-            STAGE("raw_copy", launch_raw_copy(j, s, c->cu_count));
+            // RPGPU_RAW_SERIAL=1 (diagnostic build): the raw copies after the join (A/B of the overlap)
+            static const bool raw_serial = [] { const char* e = diag_env("RPGPU_RAW_SERIAL"); return e && *e == '1'; }();
+            if (!raw_serial) STAGE("raw_copy", launch_raw_copy(j, s, c->cu_count));
             STAGE("lz_walk", launch_lz_walk(j, s, c->cu_count * 16));
             if (lzf) {
                 HIPCHK(c, hipStreamWaitEvent(s, c->join_ev, 0));
                 lzf_join.side = nullptr;  // joined
             }
+            if (raw_serial) STAGE("raw_copy", launch_raw_copy(j, s, c->cu_count));
         }
         STAGE("lz_exec", launch_lz_exec(j, s));
         STAGE("decode_finish", launch_decode_finish(j, s, c->cu_count * 8));
