@@ -1908,6 +1908,9 @@ struct SlabSink {
 // block checksum, then the walk.  High occupancy: the lane walk is a chain
 // of dependent loads per lane.
 // ---------------------------------------------------------------------------
+#ifndef RPGPU_WALK_PRIO
+#define RPGPU_WALK_PRIO 0  // s_setprio of a wave walking a long piece (experiment builds)
+#endif
 constexpr uint32_t kWalkWin = 4096;  // staged stream bytes per wave (long pieces)
 
 
@@ -1923,22 +1926,58 @@ DEV uint64_t shfl_up64(uint64_t v, int d) {
 }  // namespace
 
 // The walk of one long raw snappy stream by a whole wave, window-parallel:
-// with the stream staged in LDS, lane l decodes the tag that WOULD start at
-// ip + l (one 8-byte LDS read: its type, lengths, offset and the position
-// of the tag after it).  The true tags among those 64 are found by hopping
-// from ip through the lanes' "next" positions (one readlane per tag, scalar
-// work); the output positions of the tags on that chain are a prefix sum,
-// which is all the op-dependent checks need; their records are stored by
-// the lanes in chain order.  The checks are DecompressAllTags' over the
-// stream, SnappyArrayWriter's limits and AppendFromSelf's offset rule, in
-// tag order (the first failing tag on the chain fails the stream).  A lane
-// walking the stream alone took ~1 us per tag (62 K tags: 65 ms on C5).
+// with the stream staged in LDS, lane l decodes the tags that WOULD start at
+// ip + l and at ip + 64 + l (one 8-byte LDS read each: type, lengths, offset
+// and the position of the tag after it).  The true tags among those 128 are
+// found by pointer doubling in each 64-position half at once (two
+// independent chains of shuffles: the second costs no latency), the first
+// half's chain from ip, the second's from where the first leaves its half;
+// the output positions of the chain tags are a prefix sum, which is all the
+// op-dependent checks need; their records are stored by the lanes in chain
+// order.  The checks are DecompressAllTags' over the stream,
+// SnappyArrayWriter's limits and AppendFromSelf's offset rule, in tag order
+// (the first failing tag on the chain fails the stream).  A lane walking
+// the stream alone took ~1 us per tag (62 K tags: 65 ms on C5); one 64-position
+// window per round ~19.5 tags per ~2.7 K cycles (the round's latency chain),
+// two windows ~39.
+struct SnapCand {
+    uint32_t nxt, lip, t;  // next tag position (0xFFFFFFFF: none), literal position, tag type
+    uint64_t out, off;     // output bytes, copy offset
+    bool bad;              // cut short by the stream's end, or offset 0
+};
+DEV SnapCand snappy_cand(const __attribute__((address_space(3))) uint32_t* w32, int64_t w0, uint32_t p, uint32_t n) {
+    SnapCand r{0xFFFFFFFFu, 0u, 0u, 0u, 0u, false};
+    if (p >= n) return r;
+    const uint32_t o = (uint32_t)((int64_t)p - w0);
+    const uint64_t q = (((uint64_t)w32[(o >> 2) + 1] << 32) | w32[o >> 2]) >> (8 * (o & 3));
+    const uint32_t c = (uint32_t)q & 0xFFu, x = (uint32_t)(q >> 8);
+    r.t = c & 3;
+    const uint32_t extra = r.t == 0 ? (((c >> 2) >= 60) ? (c >> 2) - 59 : 0u) : r.t == 1 ? 1u : r.t == 2 ? 2u : 4u;
+    if (n - p < 1 + extra) {
+        r.bad = true;
+    } else if (r.t == 0) {
+        uint64_t lit = (uint64_t)(c >> 2) + 1;
+        if (lit >= 61) lit = (uint64_t)(extra == 4 ? x : x & ((1u << (8 * extra)) - 1u)) + 1;
+        r.lip = p + 1 + extra;
+        if ((uint64_t)(n - r.lip) < lit) r.bad = true;
+        else {
+            r.out = lit;
+            r.nxt = r.lip + (uint32_t)lit;
+        }
+    } else {
+        r.out = r.t == 1 ? 4 + ((c >> 2) & 7) : (c >> 2) + 1;
+        r.off = r.t == 1 ? (((c >> 5) << 8) | (x & 0xFFu)) : r.t == 2 ? (x & 0xFFFFu) : x;
+        r.nxt = p + 1 + extra;
+        if (r.off == 0) r.bad = true;
+    }
+    return r;
+}
+
 DEV void walk_snappy_long(const DeviceJob& j, Piece& pc, SlabSink& sink, lds_u8* win) {
     typedef __attribute__((address_space(3))) const uint32_t lds_cu32;
     const uint32_t l = lane();
     // the walk state is wave-uniform: kept in SGPRs (readfirstlane), or the
-    // compiler runs the hop loop below as a divergent VGPR loop (~250 cycles
-    // per hop measured, against a few SALU instructions)
+    // compiler runs the loop as a divergent VGPR loop
     const uint32_t n = uni32((uint32_t)pc.s.n);
     const uint64_t ulen = uni32(pc.ps.ulen);
     uint32_t ip = uni32((uint32_t)pc.ps.ip);
@@ -1948,6 +1987,7 @@ DEV void walk_snappy_long(const DeviceJob& j, Piece& pc, SlabSink& sink, lds_u8*
     bool cut = false;
     int64_t w0 = -1;
     lds_cu32* w32 = (lds_cu32*)win;
+    const uint64_t below = (1ull << l) - 1;
 #ifdef RPGPU_DSTAMPS
     uint64_t ds_it = 0, ds_hops = 0, ds_c0 = 0, ds_c1 = 0, ds_c2 = 0;
 #endif
@@ -1962,7 +2002,7 @@ DEV void walk_snappy_long(const DeviceJob& j, Piece& pc, SlabSink& sink, lds_u8*
             st = op == ulen ? 1 : -1;
             break;
         }
-        if (w0 < 0 || (int64_t)ip + 72 > w0 + kWalkWin) {
+        if (w0 < 0 || (int64_t)ip + 136 > w0 + kWalkWin) {
             w0 = (int64_t)ip & ~15ll;
 #pragma unroll
             for (uint32_t k = 0; k < kWalkWin / 1024; k++) {
@@ -1971,82 +2011,66 @@ DEV void walk_snappy_long(const DeviceJob& j, Piece& pc, SlabSink& sink, lds_u8*
             }
             asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
         }
-        // the tag that would start at ip + l
-        const uint32_t p = ip + l;
-        uint32_t nxt = 0xFFFFFFFFu, lip = 0, t = 0;
-        uint64_t out = 0, off = 0;
-        bool bad = false;
-        if (p < n) {
-            const uint32_t o = (uint32_t)((int64_t)p - w0);
-            const uint64_t q = (((uint64_t)w32[(o >> 2) + 1] << 32) | w32[o >> 2]) >> (8 * (o & 3));
-            const uint32_t c = (uint32_t)q & 0xFFu, x = (uint32_t)(q >> 8);
-            t = c & 3;
-            const uint32_t extra = t == 0 ? (((c >> 2) >= 60) ? (c >> 2) - 59 : 0u) : t == 1 ? 1u : t == 2 ? 2u : 4u;
-            if (n - p < 1 + extra) {
-                bad = true;
-            } else if (t == 0) {
-                uint64_t lit = (uint64_t)(c >> 2) + 1;
-                if (lit >= 61) lit = (uint64_t)(extra == 4 ? x : x & ((1u << (8 * extra)) - 1u)) + 1;
-                lip = p + 1 + extra;
-                if ((uint64_t)(n - lip) < lit) bad = true;
-                else {
-                    out = lit;
-                    nxt = lip + (uint32_t)lit;
-                }
-            } else {
-                out = t == 1 ? 4 + ((c >> 2) & 7) : (c >> 2) + 1;
-                off = t == 1 ? (((c >> 5) << 8) | (x & 0xFFu)) : t == 2 ? (x & 0xFFFFu) : x;
-                nxt = p + 1 + extra;
-                if (off == 0) bad = true;
-            }
-        }
+        // the tags that would start at ip + l (a) and ip + 64 + l (b)
+        const uint32_t ib = ip + 64;
+        const SnapCand a = snappy_cand(w32, w0, ip + l, n);
+        const SnapCand b = snappy_cand(w32, w0, ib + l, n);
 #ifdef RPGPU_DSTAMPS
         const uint64_t q1 = __builtin_amdgcn_s_memtime();
 #endif
-        // the true tags among the 64, by pointer doubling: J = the lane of
-        // the next tag (itself where the chain leaves the window, ends the
-        // stream or meets a bad tag), F = the lanes visited from here; after
-        // six rounds (F, J) <- (F | F[J], J[J]) lane 0's F is the chain.  (A
-        // scalar hop per tag, readlane -> SALU -> branch, cost ~130 cycles
-        // each.)
-        uint32_t J = l;
-        if (!bad && nxt != 0xFFFFFFFFu && nxt - ip < 64u && nxt < n) J = nxt - ip;
-        uint64_t F = 1ull << l;
+        // the true tags of each half by pointer doubling: J = the lane of the
+        // next tag in the half (itself where the chain leaves the half, ends
+        // the stream or meets a bad tag), F = the lanes visited from here;
+        // after six rounds (F, J) <- (F | F[J], J[J]) lane e's F is the chain
+        // from e.  (A scalar hop per tag, readlane -> SALU -> branch, cost
+        // ~130 cycles each.)
+        uint32_t Ja = l, Jb = l;
+        if (!a.bad && a.nxt != 0xFFFFFFFFu && a.nxt - ip < 64u && a.nxt < n) Ja = a.nxt - ip;
+        if (!b.bad && b.nxt != 0xFFFFFFFFu && b.nxt - ib < 64u && b.nxt < n) Jb = b.nxt - ib;
+        uint64_t Fa = 1ull << l, Fb = 1ull << l;
 #pragma unroll
-        for (int t = 0; t < 6; t++) {
-            const uint32_t Jo = (uint32_t)__shfl((int)J, (int)J, 64);
-            const uint32_t flo = (uint32_t)__shfl((int)(uint32_t)F, (int)J, 64);
-            const uint32_t fhi = (uint32_t)__shfl((int)(uint32_t)(F >> 32), (int)J, 64);
-            F |= (uint64_t)flo | ((uint64_t)fhi << 32);
-            J = Jo;
+        for (int r = 0; r < 6; r++) {
+            const uint32_t Jao = (uint32_t)__shfl((int)Ja, (int)Ja, 64);
+            const uint32_t Jbo = (uint32_t)__shfl((int)Jb, (int)Jb, 64);
+            const uint32_t alo = (uint32_t)__shfl((int)(uint32_t)Fa, (int)Ja, 64);
+            const uint32_t blo = (uint32_t)__shfl((int)(uint32_t)Fb, (int)Jb, 64);
+            const uint32_t ahi = (uint32_t)__shfl((int)(uint32_t)(Fa >> 32), (int)Ja, 64);
+            const uint32_t bhi = (uint32_t)__shfl((int)(uint32_t)(Fb >> 32), (int)Jb, 64);
+            Fa |= (uint64_t)alo | ((uint64_t)ahi << 32);
+            Fb |= (uint64_t)blo | ((uint64_t)bhi << 32);
+            Ja = Jao;
+            Jb = Jbo;
         }
-        const uint64_t chain = (uint64_t)uni32((uint32_t)rl((uint32_t)F, 0)) |
-                               ((uint64_t)uni32(rl((uint32_t)(F >> 32), 0)) << 32);
-        // where the next iteration starts: the last chain tag's successor
-        const int last = 63 - __builtin_clzll(chain);
-        const uint32_t qn = uni32(rl(nxt, last));
+        const uint64_t ca = (uint64_t)uni32(rl((uint32_t)Fa, 0)) | ((uint64_t)uni32(rl((uint32_t)(Fa >> 32), 0)) << 32);
+        // where the first half's chain leaves it: the second half's entry
+        const uint32_t qa = uni32(rl(a.nxt, 63 - __builtin_clzll(ca)));
+        const uint32_t e = qa - ib;  // (a good chain tag's successor is >= ib or the stream's end)
+        uint64_t cb = 0;
+        if (qa < n && e < 64u)
+            cb = (uint64_t)uni32(rl((uint32_t)Fb, (int)e)) | ((uint64_t)uni32(rl((uint32_t)(Fb >> 32), (int)e)) << 32);
+        const uint32_t qn = cb ? uni32(rl(b.nxt, 63 - __builtin_clzll(cb))) : qa;
 #ifdef RPGPU_DSTAMPS
-        ds_hops += (uint64_t)__builtin_popcountll(chain);
-#endif
-#ifdef RPGPU_DSTAMPS
+        ds_hops += (uint64_t)(__builtin_popcountll(ca) + __builtin_popcountll(cb));
         const uint64_t q2 = __builtin_amdgcn_s_memtime();
         ds_c0 += q1 - q0;
         ds_c1 += q2 - q1;
 #endif
-        const bool on = (chain >> l) & 1;
-        // output before each chain tag: a 32-bit DPP scan (a good chain tag's
+        const bool ona = (ca >> l) & 1, onb = (cb >> l) & 1;
+        // output before each chain tag: 32-bit DPP scans (a good chain tag's
         // output is a literal inside the stream or a copy of <= 64 bytes)
-        const uint32_t o32 = on ? (uint32_t)out : 0u;
-        const uint32_t incl = wave_scan(o32);
-        const uint64_t opt = op + (incl - o32);
-        const bool fail = on && (bad || (int64_t)(ulen - opt) < (int64_t)out || (t != 0 && opt < off));
+        const uint32_t oa = ona ? (uint32_t)a.out : 0u, ob = onb ? (uint32_t)b.out : 0u;
+        const uint32_t ia = wave_scan(oa), ibn = wave_scan(ob);
+        const uint32_t ta = uni32(rl(ia, 63));
+        const uint64_t opa = op + (ia - oa), opb = op + ta + (ibn - ob);
+        const bool fail = (ona && (a.bad || (int64_t)(ulen - opa) < (int64_t)a.out || (a.t != 0 && opa < a.off))) ||
+                          (onb && (b.bad || (int64_t)(ulen - opb) < (int64_t)b.out || (b.t != 0 && opb < b.off)));
         if (__ballot(fail)) {
             st = -1;
             break;
         }
-        // records in chain order
-        const uint32_t cnt = (uint32_t)__builtin_popcountll(chain);
-        const uint32_t rank = (uint32_t)__builtin_popcountll(chain & ((1ull << l) - 1));
+        // records in chain order: the first half's, then the second's
+        const uint32_t na = (uint32_t)__builtin_popcountll(ca);
+        const uint32_t cnt = na + (uint32_t)__builtin_popcountll(cb);
         const uint32_t room = kSlabRecs - pos;
         uint32_t ns = 0xFFFFFFFFu, emit = cnt;
         if (cnt >= room) {
@@ -2058,10 +2082,17 @@ DEV void walk_snappy_long(const DeviceJob& j, Piece& pc, SlabSink& sink, lds_u8*
                 j.slab_next[slab] = ns;
             }
         }
-        if (on && rank < emit) {
-            const SeqRec r = t == 0 ? SeqRec{lip, (uint32_t)out, 0u, 0u} : SeqRec{0u, 0u, (uint32_t)out, (uint32_t)off};
-            if (rank < room) j.pool[(size_t)slab * kSlabRecs + pos + rank] = r;
-            else j.pool[(size_t)ns * kSlabRecs + (rank - room)] = r;
+#pragma unroll
+        for (int h = 0; h < 2; h++) {
+            const bool on = h ? onb : ona;
+            const SnapCand& c = h ? b : a;
+            const uint32_t rank = h ? na + (uint32_t)__builtin_popcountll(cb & below)
+                                    : (uint32_t)__builtin_popcountll(ca & below);
+            if (on && rank < emit) {
+                const SeqRec r = c.t == 0 ? SeqRec{c.lip, (uint32_t)c.out, 0u, 0u} : SeqRec{0u, 0u, (uint32_t)c.out, (uint32_t)c.off};
+                if (rank < room) j.pool[(size_t)slab * kSlabRecs + pos + rank] = r;
+                else j.pool[(size_t)ns * kSlabRecs + (rank - room)] = r;
+            }
         }
         nrec += emit;
         if (cnt >= room && !cut) {
@@ -2071,18 +2102,20 @@ DEV void walk_snappy_long(const DeviceJob& j, Piece& pc, SlabSink& sink, lds_u8*
             pos += emit;
         }
         if (emit < cnt) {
-            // resume after the last stored record
+            // resume after the last stored record (the emit-th chain tag)
+            const bool inb = emit > na;
+            uint64_t m = inb ? cb : ca;
+            const uint32_t k = inb ? emit - na : emit;
             uint32_t kk = 0;
-            uint64_t m = chain;
-            for (uint32_t e = 0; e < emit; e++) {
+            for (uint32_t x = 0; x < k; x++) {
                 kk = (uint32_t)__builtin_ctzll(m);
                 m &= m - 1;
             }
-            ip = rl(nxt, (int)kk);
-            op = op + rl(incl, (int)kk);
+            ip = inb ? rl(b.nxt, (int)kk) : rl(a.nxt, (int)kk);
+            op = inb ? op + ta + rl(ibn, (int)kk) : op + rl(ia, (int)kk);
             break;
         }
-        op += rl(incl, 63);
+        op += ta + rl(ibn, 63);
         ip = qn;
 #ifdef RPGPU_DSTAMPS
         ds_c2 += __builtin_amdgcn_s_memtime() - q2;
@@ -2414,7 +2447,13 @@ __global__ __launch_bounds__(256) void k_lz_walk(DeviceJob j) {
         if (uni32(j.blocks[p].fast) != kLzfNone) continue;  // the fast path has it
         if (!piece_wave_walked(uni32(j.blocks[p].kind), uni32(j.blocks[p].csize), uni32(j.blocks[p].cap), few))
             continue;  // a dense piece: the lane walk takes it
+#if RPGPU_WALK_PRIO
+        __builtin_amdgcn_s_setprio(RPGPU_WALK_PRIO);
+#endif
         walk_long(j, p, wl);
+#if RPGPU_WALK_PRIO
+        __builtin_amdgcn_s_setprio(0);
+#endif
     }
     lds_u8* slot = wl + kLaneSlot * lane();
     bool active = false, drained = false;

@@ -160,6 +160,8 @@ struct rpgpu_ctx {
     // slot scans
     hipStream_t side = nullptr;
     hipEvent_t fork_ev = nullptr, join_ev = nullptr;
+    hipStream_t side2 = nullptr;  // k_raw_copy beside k_lzf_walk and k_lz_walk
+    hipEvent_t join2_ev = nullptr;
     struct HostSlot {
         uint8_t* d_data = nullptr;
         uint64_t data_bytes = 0;
@@ -262,12 +264,12 @@ const char* diag_env(const char*) { return nullptr; }
 // member pass measured 64 ms alone, 77 ms after the bench's H2D stanza had
 // created its copy streams); a priority of its own gives it a queue of its own.
 // RPGPU_SIDE_PRIO=0 (diagnostic build): the default priority (A/B).
-hipError_t side_stream_create(rpgpu_ctx* c) {
+hipError_t side_stream_create(hipStream_t* out) {
     static const bool prio = [] { const char* e = diag_env("RPGPU_SIDE_PRIO"); return !(e && *e == '0'); }();
     int least = 0, greatest = 0;
     if (prio && hipDeviceGetStreamPriorityRange(&least, &greatest) == hipSuccess && greatest != least)
-        return hipStreamCreateWithPriority(&c->side, hipStreamNonBlocking, greatest);
-    return hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking);
+        return hipStreamCreateWithPriority(out, hipStreamNonBlocking, greatest);
+    return hipStreamCreateWithFlags(out, hipStreamNonBlocking);
 }
 
 // gzip / zstd: the CPU fallback behind compressor::uncompress (rp_hostcodec.cpp)
@@ -339,6 +341,8 @@ int rpgpu_destroy(rpgpu_ctx* c) {
     if (c->side) { (void)hipStreamSynchronize(c->side); (void)hipStreamDestroy(c->side); }
     if (c->fork_ev) (void)hipEventDestroy(c->fork_ev);
     if (c->join_ev) (void)hipEventDestroy(c->join_ev);
+    if (c->side2) { (void)hipStreamSynchronize(c->side2); (void)hipStreamDestroy(c->side2); }
+    if (c->join2_ev) (void)hipEventDestroy(c->join2_ev);
     for (auto& set : c->ev_sets)
         for (auto& e : set) hipEventDestroy(e);
     if (c->stream) hipStreamDestroy(c->stream);
@@ -857,6 +861,7 @@ int submit_body(rpgpu_ctx* c, const rpgpu_job* job, hipStream_t s, int stop, Pla
             fflush(stderr);                                                                \
             hipError_t _e = hipStreamSynchronize(s);                                       \
             if (_e == hipSuccess && c->side) _e = hipStreamSynchronize(c->side);           \
+            if (_e == hipSuccess && c->side2) _e = hipStreamSynchronize(c->side2);         \
             if (_e != hipSuccess) return fail(c, RPGPU_E_HIP, "stage " name " failed", _e); \
         }                                                                                  \
     } while (0)
@@ -904,7 +909,7 @@ int submit_body(rpgpu_ctx* c, const rpgpu_job* job, hipStream_t s, int stop, Pla
             }
         } side_join;
         if (split) {
-            if (!c->side) HIPCHK(c, side_stream_create(c));
+            if (!c->side) HIPCHK(c, side_stream_create(&c->side));
             if (!c->fork_ev) HIPCHK(c, hipEventCreateWithFlags(&c->fork_ev, hipEventDisableTiming));
             if (!c->join_ev) HIPCHK(c, hipEventCreateWithFlags(&c->join_ev, hipEventDisableTiming));
             j.zs_split = 1;
@@ -956,27 +961,55 @@ int submit_body(rpgpu_ctx* c, const rpgpu_job* job, hipStream_t s, int stop, Pla
                 ~LzfJoin() {
                     if (side && hipEventRecord(ev, side) == hipSuccess) hipStreamWaitEvent(s, ev, 0);
                 }
-            } lzf_join;
+            } lzf_join, raw_join;
             const bool lzf = j.lzf_list != nullptr;
+            // RPGPU_WALK_FIRST=1 (diagnostic build): k_lz_walk submitted before
+            // the side streams' kernels (dispatch-order A/B)
+            static const bool walk_first = [] { const char* e = diag_env("RPGPU_WALK_FIRST"); return e && *e == '1'; }();
+            bool walked = false;
             if (lzf) {
-                if (!c->side) HIPCHK(c, side_stream_create(c));
+                if (!c->side) HIPCHK(c, side_stream_create(&c->side));
                 if (!c->fork_ev) HIPCHK(c, hipEventCreateWithFlags(&c->fork_ev, hipEventDisableTiming));
                 if (!c->join_ev) HIPCHK(c, hipEventCreateWithFlags(&c->join_ev, hipEventDisableTiming));
                 HIPCHK(c, hipEventRecord(c->fork_ev, s));
                 HIPCHK(c, hipStreamWaitEvent(c->side, c->fork_ev, 0));
+                if (walk_first) {
+                    STAGE("lz_walk", launch_lz_walk(j, s, c->cu_count * 16));
+                    walked = true;
+                }
                 lzf_join.s = s;
                 lzf_join.ev = c->join_ev;
                 lzf_join.side = c->side;
                 STAGE("lzf_walk", launch_lzf_walk(j, c->side, c->cu_count));
                 HIPCHK(c, hipEventRecord(c->join_ev, c->side));
             }
-            // RPGPU_RAW_SERIAL=1 (diagnostic build): the raw copies after the join (A/B of the overlap)
+            // the raw copies on a stream of their own, so that neither walk
+            // waits for them (C5: the longest raw snappy walk, ~3.7 ms, began
+            // after ~0.45 ms of copies).  RPGPU_RAW_SERIAL=1 (diagnostic
+            // build): after the join (A/B of the overlap); RPGPU_RAW_STREAM=0:
+            // before k_lz_walk on the job's stream (round-5 order)
             static const bool raw_serial = [] { const char* e = diag_env("RPGPU_RAW_SERIAL"); return e && *e == '1'; }();
-            if (!raw_serial) STAGE("raw_copy", launch_raw_copy(j, s, c->cu_count));
-            STAGE("lz_walk", launch_lz_walk(j, s, c->cu_count * 16));
+            static const bool raw_own = [] { const char* e = diag_env("RPGPU_RAW_STREAM"); return !(e && *e == '0'); }();
+            if (!raw_serial && lzf && raw_own && j.raw_list) {
+                if (!c->side2) HIPCHK(c, side_stream_create(&c->side2));
+                if (!c->join2_ev) HIPCHK(c, hipEventCreateWithFlags(&c->join2_ev, hipEventDisableTiming));
+                HIPCHK(c, hipStreamWaitEvent(c->side2, c->fork_ev, 0));
+                raw_join.s = s;
+                raw_join.ev = c->join2_ev;
+                raw_join.side = c->side2;
+                STAGE("raw_copy", launch_raw_copy(j, c->side2, c->cu_count));
+                HIPCHK(c, hipEventRecord(c->join2_ev, c->side2));
+            } else if (!raw_serial) {
+                STAGE("raw_copy", launch_raw_copy(j, s, c->cu_count));
+            }
+            if (!walked) STAGE("lz_walk", launch_lz_walk(j, s, c->cu_count * 16));
             if (lzf) {
                 HIPCHK(c, hipStreamWaitEvent(s, c->join_ev, 0));
                 lzf_join.side = nullptr;  // joined
+            }
+            if (raw_join.side) {
+                HIPCHK(c, hipStreamWaitEvent(s, c->join2_ev, 0));
+                raw_join.side = nullptr;
             }
             if (raw_serial) STAGE("raw_copy", launch_raw_copy(j, s, c->cu_count));
         }
