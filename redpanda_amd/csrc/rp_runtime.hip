@@ -991,7 +991,9 @@ int submit_body(rpgpu_ctx* c, const rpgpu_job* job, hipStream_t s, int stop, Pla
             static const bool raw_serial = [] { const char* e = diag_env("RPGPU_RAW_SERIAL"); return e && *e == '1'; }();
             static const bool raw_own = [] { const char* e = diag_env("RPGPU_RAW_STREAM"); return !(e && *e == '0'); }();
             if (!raw_serial && lzf && raw_own && j.raw_list) {
-                if (!c->side2) HIPCHK(c, side_stream_create(&c->side2));
+                // RPGPU_RAW_PRIO=0 (diagnostic build): the raw-copy stream at the default priority (A/B)
+                static const bool raw_prio = [] { const char* e = diag_env("RPGPU_RAW_PRIO"); return !(e && *e == '0'); }();
+                if (!c->side2) HIPCHK(c, raw_prio ? side_stream_create(&c->side2) : hipStreamCreateWithFlags(&c->side2, hipStreamNonBlocking));
                 if (!c->join2_ev) HIPCHK(c, hipEventCreateWithFlags(&c->join2_ev, hipEventDisableTiming));
                 HIPCHK(c, hipStreamWaitEvent(c->side2, c->fork_ev, 0));
                 raw_join.s = s;
