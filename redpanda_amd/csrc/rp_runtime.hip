@@ -967,6 +967,9 @@ int submit_body(rpgpu_ctx* c, const rpgpu_job* job, hipStream_t s, int stop, Pla
             // the side streams' kernels (dispatch-order A/B)
             static const bool walk_first = [] { const char* e = diag_env("RPGPU_WALK_FIRST"); return e && *e == '1'; }();
             bool walked = false;
+            // RPGPU_LZWALK_WGS (diagnostic build): k_lz_walk's grid (workgroups)
+            static const uint32_t lzw_env = [] { const char* e = diag_env("RPGPU_LZWALK_WGS"); return e ? (uint32_t)atoi(e) : 0u; }();
+            const uint32_t lzw_grid = lzw_env ? lzw_env : c->cu_count * 16;
             if (lzf) {
                 if (!c->side) HIPCHK(c, side_stream_create(&c->side));
                 if (!c->fork_ev) HIPCHK(c, hipEventCreateWithFlags(&c->fork_ev, hipEventDisableTiming));
@@ -974,7 +977,7 @@ int submit_body(rpgpu_ctx* c, const rpgpu_job* job, hipStream_t s, int stop, Pla
                 HIPCHK(c, hipEventRecord(c->fork_ev, s));
                 HIPCHK(c, hipStreamWaitEvent(c->side, c->fork_ev, 0));
                 if (walk_first) {
-                    STAGE("lz_walk", launch_lz_walk(j, s, c->cu_count * 16));
+                    STAGE("lz_walk", launch_lz_walk(j, s, lzw_grid));
                     walked = true;
                 }
                 lzf_join.s = s;
@@ -1004,7 +1007,7 @@ int submit_body(rpgpu_ctx* c, const rpgpu_job* job, hipStream_t s, int stop, Pla
             } else if (!raw_serial) {
                 STAGE("raw_copy", launch_raw_copy(j, s, c->cu_count));
             }
-            if (!walked) STAGE("lz_walk", launch_lz_walk(j, s, c->cu_count * 16));
+            if (!walked) STAGE("lz_walk", launch_lz_walk(j, s, lzw_grid));
             if (lzf) {
                 HIPCHK(c, hipStreamWaitEvent(s, c->join_ev, 0));
                 lzf_join.side = nullptr;  // joined
