@@ -1371,6 +1371,9 @@ struct XRing {
     const __attribute__((address_space(3))) uint32_t* pat;  // kPat.a then kPat.b in LDS (a constant-memory
                                                           // load per short-offset match waited on HBM latency)
     __amdgpu_buffer_rsrc_t rs;  // dst window for far read-backs (linked)
+#ifdef RPGPU_DSTAMPS
+    uint64_t ds[10];            // per-piece phase cycles / counts (diagnostic build), see ds_flush
+#endif
 };
 
 DEV void wait_vm() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
@@ -1515,8 +1518,50 @@ DEV uint32_t wave_scan(uint32_t v) {
 
 // one lane's match: ml bytes at d from d - off (every source byte final or
 // this match's own earlier output)
+// RPGPU_XMATCH_BATCH (experiment builds): 1 = a non-overlapping match's
+// source loaded whole before its stores (1632 VGPR spills: C2 decode 26 ->
+// 47 ms); 2 = far sources two 16-byte loads at a time
+#ifndef RPGPU_XMATCH_BATCH
+#define RPGPU_XMATCH_BATCH 0
+#endif
 DEV void xmatch(XRing& x, uint32_t d, uint32_t off, uint32_t ml, bool far) {
     const uint32_t s = d - off;
+#if RPGPU_XMATCH_BATCH == 2
+    if (far) {
+        for (uint32_t c = 0; c < ml; c += 32) {
+            const auto t0 = __builtin_amdgcn_raw_buffer_load_b128(x.rs, s + c, 0, kSc1);
+            const auto t1 = __builtin_amdgcn_raw_buffer_load_b128(x.rs, s + c + 16, 0, kSc1);
+            xst(x.r, d + c, make_uint4(t0[0], t0[1], t0[2], t0[3]), ml - c < 16 ? ml - c : 16);
+            if (c + 16 < ml) xst(x.r, d + c + 16, make_uint4(t1[0], t1[1], t1[2], t1[3]), ml - c - 16 < 16 ? ml - c - 16 : 16);
+        }
+        return;
+    }
+#endif
+#if RPGPU_XMATCH_BATCH == 1
+    // ml <= kBig here (xbatch).  A source that does not overlap the
+    // destination (every far one: off > ring - 1 KiB) is read whole before
+    // anything is stored: one load latency per match instead of one per 16
+    // bytes
+    if (far || off >= ml) {
+        uint4 t[kBig / 16];
+#pragma unroll
+        for (uint32_t k = 0; k < kBig / 16; k++) {
+            t[k] = make_uint4(0u, 0u, 0u, 0u);
+            if (16 * k < ml) {
+                if (far) {
+                    const auto v = __builtin_amdgcn_raw_buffer_load_b128(x.rs, s + 16 * k, 0, kSc1);
+                    t[k] = make_uint4(v[0], v[1], v[2], v[3]);
+                } else {
+                    t[k] = xld16(x.r, s + 16 * k);
+                }
+            }
+        }
+#pragma unroll
+        for (uint32_t k = 0; k < kBig / 16; k++)
+            if (16 * k < ml) xst(x.r, d + 16 * k, t[k], ml - 16 * k < 16 ? ml - 16 * k : 16);
+        return;
+    }
+#endif
     if (far) {
         for (uint32_t c = 0; c < ml; c += 16) {
             const auto t = __builtin_amdgcn_raw_buffer_load_b128(x.rs, s + c, 0, kSc1);
@@ -1594,7 +1639,16 @@ DEV void xbatch(XRing& x, const Src& s, const SeqRec& r, uint32_t lo, uint32_t h
 #endif
     // a far source was stored by an earlier flush: wait only while a flush
     // may still be in flight (a wait drains every earlier memory op)
+#ifdef RPGPU_DSTAMPS
+    const uint64_t farm = __ballot(far), mm = __ballot(pend);
+    x.ds[6] += farm ? 1u : 0u;
+    x.ds[7] += (uint64_t)__builtin_popcountll(farm);
+    x.ds[9] += (uint64_t)__builtin_popcountll(mm);
+#endif
     if (__ballot(far && src + r.ml > x.safe) && x.fpend) {
+#ifdef RPGPU_DSTAMPS
+        if (l == 0) atomicAdd(&g_dst[54], 1ull);
+#endif
         wait_vm();
         x.fpend = false;
         x.safe = x.flushed;
@@ -1618,16 +1672,25 @@ DEV void xbatch(XRing& x, const Src& s, const SeqRec& r, uint32_t lo, uint32_t h
     if (x.op - x.flushed > kFlushLag) xflush_chunks(x);
 #ifdef RPGPU_DSTAMPS
     const uint64_t c4 = __builtin_amdgcn_s_memtime();
-    if (l == 0) {
-        atomicAdd(&g_dst[16], c1 - c0);   // scan
-        atomicAdd(&g_dst[17], c2 - c1);   // literals
-        atomicAdd(&g_dst[18], c3 - c2);   // rounds
-        atomicAdd(&g_dst[19], c4 - c3);   // flush
-        atomicAdd(&g_dst[20], 1ull);      // batches
-        atomicAdd(&g_dst[21], (unsigned long long)rounds);
-    }
+    // accumulated per piece, added to g_dst once per piece (ds_flush): an
+    // atomic per batch from every wave perturbed the kernel it measured
+    x.ds[0] += c1 - c0;  // scan (waits for the batch's records / literals)
+    x.ds[1] += c2 - c1;  // literals
+    x.ds[2] += c3 - c2;  // rounds
+    x.ds[3] += c4 - c3;  // flush
+    x.ds[4] += 1u;       // batches
+    x.ds[5] += rounds;
+    x.ds[8] += farm ? c3 - c2 : 0u;  // rounds of batches with far lanes
 #endif
 }
+
+#ifdef RPGPU_DSTAMPS
+DEV void ds_flush(const XRing& x) {
+    if (lane() != 0) return;
+    const int slot[10] = {16, 17, 18, 19, 20, 21, 52, 53, 56, 55};
+    for (int i = 0; i < 10; i++) atomicAdd(&g_dst[slot[i]], (unsigned long long)x.ds[i]);
+}
+#endif
 
 // one long record, wave-cooperatively
 DEV void xbig(XRing& x, const Src& s, uint32_t lip, uint32_t ll, uint32_t ml, uint32_t off) {
@@ -2609,6 +2672,9 @@ DEV void xring_init(XRing& x, const DeviceJob& j, lds_u8* ring, uint64_t dst, bo
     x.safe = 0;
     const uint64_t room = j.decoded_capacity - dst;
     x.rs = __builtin_amdgcn_make_buffer_rsrc(x.dst, 0, (int)(room < 0x7FFFFFFFull ? room : 0x7FFFFFFFull), kBufFlags);
+#ifdef RPGPU_DSTAMPS
+    for (int i = 0; i < 10; i++) x.ds[i] = 0;
+#endif
 }
 
 // the blocks of one linked LZ4F frame, in order, one position space
@@ -2637,6 +2703,7 @@ DEV void exec_linked(const DeviceJob& j, lds_u8* ring, SeqRec* buf, uint32_t ite
     if (lane() == 0) j.blocks[first].crc = fcrc;
 #ifdef RPGPU_DSTAMPS
     if (lane() == 0) { atomicAdd(&g_dst[10], wall_clock64() - t1); atomicAdd(&g_dst[9], 1ull); }
+    ds_flush(x);
 #endif
 }
 
@@ -2672,6 +2739,7 @@ DEV void exec_one(const DeviceJob& j, lds_u8* ring, SeqRec* buf, uint32_t p, uin
             atomicAdd(&g_dst[11], (unsigned long long)j.pstate[p].nrec);
             if (j.pstate[p].st == 0) atomicAdd(&g_dst[12], 1ull);
         }
+        ds_flush(x);
 #endif
     }
 }
@@ -2980,6 +3048,9 @@ __global__ void k_print_dstamps() {
            (double)g[44] / (g[40] ? g[40] : 1));
     printf("RPGPU_DSTAMPS lzf walk rounds=%llu wave-steps=%llu | tails=%llu tail records=%llu\n", g[48], g[49], g[50],
            g[51]);
+    printf("RPGPU_DSTAMPS exec batches with far lanes=%llu far lanes=%llu far drains=%llu match lanes=%llu | rounds clk "
+           "in batches with far lanes=%.0f per batch (all batches %.0f)\n", g[52], g[53], g[54], g[55],
+           (double)g[56] / (g[52] ? g[52] : 1), (double)g[18] / (g[20] ? g[20] : 1));
     for (int i = 0; i < 64; i++) g_dst[i] = 0;
 }
 __global__ void k_init_dstamps() {

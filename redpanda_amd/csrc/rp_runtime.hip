@@ -771,20 +771,24 @@ int submit_body(rpgpu_ctx* c, const rpgpu_job* job, hipStream_t s, int stop, Pla
     j.slab_next = (uint32_t*)((uint8_t*)c->pool + (size_t)j.pool_slabs * kSlabRecs * sizeof(SeqRec));
     // fast-path records: the planner reserves csize / 3 + 2 per listed LZ4
     // block (2.7 bytes per compressed byte; C2 uses 0.3 of the job's bytes),
-    // 1.5x the job's bytes, 64 MiB .. 16 GiB; a group of blocks that finds no
-    // room takes the walk / exec kernels.
-    // RPGPU_LZF=0 (diagnostic build): every piece through the walk / exec (A/B)
+    // 3x the job's bytes (a job of nothing but LZ4 blocks fits whole), 64 MiB
+    // .. 16 GiB; a group of blocks that finds no room (and every group after
+    // it) takes the walk / exec kernels, with the same results.
+    // RPGPU_LZF=0 (diagnostic build): every piece through the walk / exec (A/B);
+    // RPGPU_FREC_CAP=n (diagnostic build): at most n records (mixes listed
+    // groups with walked ones in small jobs; tests/test_gpu_diag.py)
     j.frecs = nullptr;
     j.frec_cap = 0;
     j.lzf_list = nullptr;
     j.lzf_tail = nullptr;
     static const bool lzf_on = [] { const char* e = diag_env("RPGPU_LZF"); return !(e && *e == '0'); }();
     if (dec && lzf_on && stop == kRunAll) {
-        const size_t want = std::min<size_t>(std::max<size_t>(data_len / 2 * 3, 64ull << 20), 16ull << 30);
+        const size_t want = std::min<size_t>(std::max<size_t>(data_len * 3, 64ull << 20), 16ull << 30);
         if (int rc = grow_pool(c, c->fpool, c->fpool_bytes, want, s)) return rc;
         if (c->fpool) {
             j.frecs = (uint2*)c->fpool;
             j.frec_cap = c->fpool_bytes / sizeof(uint2);
+            if (const char* e = diag_env("RPGPU_FREC_CAP")) j.frec_cap = std::min<uint64_t>(j.frec_cap, strtoull(e, nullptr, 10));
             j.lzf_list = (uint32_t*)(ws + o_lzfl);
             j.lzf_tail = (uint32_t*)(ws + o_lzft);
         }

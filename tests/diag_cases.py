@@ -85,7 +85,45 @@ def case_host_codec_missing():
     print("host_codec_missing ok")
 
 
-CASES = {"small_pool": case_small_pool, "host_codec_missing": case_host_codec_missing}
+def case_small_frec():
+    """RPGPU_FREC_CAP=n: the fast-path record pool holds n records, so the
+    planner lists the first groups of LZ4 blocks for k_lzf_walk and leaves
+    every later group (note_fast: no room) to k_lz_walk / k_lz_exec; frames
+    mix listed blocks with walked ones.  Every field is still the oracle's
+    (rp_codec.hip note_fast)."""
+    import random
+    import synth
+    from oracle import oracle as O
+    from redpanda_amd.engine import Engine
+    from tests import test_gpu_lz4_walk as W
+    from tests.test_gpu_parity import assert_same, gen, run_both
+    assert os.environ.get("RPGPU_FREC_CAP"), "run with RPGPU_FREC_CAP"
+    O.build()
+    eng = Engine(0)
+    rnd = random.Random(11)
+    frames = []
+    for kind in ("mixed", "text", "long_lits", "long_match"):
+        for _ in range(3):
+            blk, _ = W.valid_block(rnd, kind)
+            frames.append(W.frame([blk]))
+    for _ in range(3):  # several blocks per frame, so a frame's blocks can land on both sides of the cut
+        blks = [W.valid_block(rnd, "text") for _ in range(4)]
+        frames.append(W.frame([b for b, _ in blks]))
+        frames.append(W.frame([b for b, _ in blks], content=b"".join(o for _, o in blks)))
+    frames += W.raw_block_frames(rnd)
+    frames += [W.frame([b]) for b in W.bad_blocks(rnd)]
+    rnd.shuffle(frames)
+    segs = [W.segment(frames[i::2]) for i in range(2)]
+    kw = dict(synth.C2, lz4_linked_ppm=200000, lz4_content_checksum_ppm=200000, lz4_block_checksum_ppm=50000)
+    segs += [gen(None, 6 << 20, i, **kw) for i in range(2)]
+    got, ref = run_both(eng, O, segs, flags=DFLAGS)
+    ok = (ref.batches["flags"] & abi.F_CODEC_OK) != 0
+    assert int(np.sum(ok)) > len(frames) // 2
+    assert_same(got, ref, DFLAGS)
+    print(f"small_frec ok: {len(got.batches)} batches, {int(np.sum(ok))} decoded")
+
+
+CASES = {"small_pool": case_small_pool, "host_codec_missing": case_host_codec_missing, "small_frec": case_small_frec}
 
 if __name__ == "__main__":
     CASES[sys.argv[1]]()

@@ -1,6 +1,7 @@
 """GPU cases run on the diagnostic library variant in a child process
 (tests/diag_cases.py): the gzip / zstd first-pass pool exhausted by hostile
-ISIZE trailers, and RPGPU_JOB_HOST_CODECS without a loadable libzstd."""
+ISIZE trailers, RPGPU_JOB_HOST_CODECS without a loadable libzstd, and the
+LZ4 fast-path record pool cut so that listed and walked blocks mix."""
 import os
 import subprocess
 import sys
@@ -27,3 +28,10 @@ def test_member_pool_exhausted_hostile_isize():
 
 def test_host_codec_missing_is_unsupported():
     assert "host_codec_missing ok" in _run("host_codec_missing", RPGPU_HOST_CODEC_MISSING="1")
+
+
+@pytest.mark.parametrize("cap", ["0", "30000", "400000"])
+def test_lz4_fast_pool_exhausted(cap):
+    """a fast-path record pool too small for the job's
+    LZ4 blocks (none / a few groups / most of them listed)."""
+    assert "small_frec ok" in _run("small_frec", RPGPU_FREC_CAP=cap)

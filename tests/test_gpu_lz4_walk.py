@@ -59,16 +59,23 @@ def seq(lit: bytes, off: int = 0, ml: int = 0) -> bytes:
     return bytes(out)
 
 
-def frame(blocks, linked=False, raw=()) -> bytes:
-    """LZ4F frame, 64 KiB blocks, no checksums."""
+def frame(blocks, linked=False, raw=(), bcs=False, content=None) -> bytes:
+    """LZ4F frame, 64 KiB blocks; blocks whose index is in `raw` are stored
+    (uncompressed, size word bit 31); bcs = a block checksum after every
+    block; content = the decoded bytes, whose XXH32 then follows the end mark
+    (the content-checksum flag)."""
     import xxhash
-    flg = 0x40 | (0 if linked else 0x20)
+    flg = 0x40 | (0 if linked else 0x20) | (0x10 if bcs else 0) | (0x04 if content is not None else 0)
     bd = 0x40
     hc = (xxhash.xxh32(bytes([flg, bd]), seed=0).intdigest() >> 8) & 0xFF
     out = bytearray(b"\x04\x22\x4d\x18" + bytes([flg, bd, hc]))
     for i, b in enumerate(blocks):
         out += (len(b) | (0x80000000 if i in raw else 0)).to_bytes(4, "little") + b
+        if bcs:
+            out += xxhash.xxh32(b, seed=0).intdigest().to_bytes(4, "little")
     out += b"\x00\x00\x00\x00"
+    if content is not None:
+        out += xxhash.xxh32(content, seed=0).intdigest().to_bytes(4, "little")
     return bytes(out)
 
 
@@ -208,4 +215,55 @@ def test_lz4_walk_compressed_records(engine, oracle):
     got, ref = run_both(engine, oracle, [seg], flags=DFLAGS)
     f = ref.batches["flags"]
     assert np.all(f & abi.F_CODEC_OK) and np.all(f & abi.F_PARSE_OK)
+    assert_same(got, ref, DFLAGS)
+
+
+def raw_block_frames(rnd):
+    """Frames mixing stored (raw) blocks with compressed ones: independent raw
+    blocks without a block checksum go to k_raw_copy (BlockItem.fast =
+    kLzfRaw, its streaming crc combined into the frame's), the compressed ones
+    to k_lzf_walk; a raw block under a block checksum, and every block of a
+    linked frame, stay on the lane walk / exec."""
+    def rawb(n):
+        return text(rnd, n) if rnd.random() < 0.5 else bytes(rnd.getrandbits(8) for _ in range(n))
+    frames = []
+    for _ in range(3):
+        b0, o0 = valid_block(rnd, "mixed")
+        b2, o2 = valid_block(rnd, "text")
+        r1, r3 = rawb(65536), rawb(rnd.randint(1, 65536))
+        # a raw block between / after compressed ones, with and without a content checksum
+        frames.append(frame([b0, r1, b2], raw=(1,)))
+        frames.append(frame([b0, r1, b2, r3], raw=(1, 3), content=o0 + r1 + o2 + r3))
+        # raw blocks first and last
+        frames.append(frame([r1, b0, r3], raw=(0, 2)))
+        frames.append(frame([r1, b2, r3], raw=(0, 2), content=r1 + o2 + r3))
+        # every block raw, with a content checksum; a damaged content checksum
+        frames.append(frame([r1, r3], raw=(0, 1), content=r1 + r3))
+        bad = bytearray(frame([r3, b0], raw=(0,), content=r3 + o0))
+        bad[-1] ^= 0x40
+        frames.append(bytes(bad))
+        # raw blocks under a block checksum (the lane walk's), one damaged
+        frames.append(frame([b0, r1, r3], raw=(1, 2), bcs=True))
+        frames.append(frame([r3, b2], raw=(0,), bcs=True, content=r3 + o2))
+        bad = bytearray(frame([b0, r3], raw=(1,), bcs=True))
+        bad[-6] ^= 0x01  # the raw block's checksum
+        frames.append(bytes(bad))
+        # a linked frame whose compressed block copies from the raw block before it
+        lk = seq(b"R" * 7, len(r1) - 10, 200) + seq(text(rnd, 30), 40000, 70) + seq(b"tail-bytes-12")
+        frames.append(frame([r1, lk], linked=True, raw=(0,)))
+        frames.append(frame([b0, r1, lk], linked=True, raw=(1,)))
+    return frames
+
+
+@pytest.mark.parametrize("seed", [3, 4])
+def test_lz4_walk_raw_blocks(engine, oracle, seed):
+    """stored blocks beside walked ones, content and block
+    checksums, raw blocks in linked frames."""
+    rnd = random.Random(seed)
+    frames = raw_block_frames(rnd)
+    rnd.shuffle(frames)
+    segs = [segment(frames[i::2]) for i in range(2)]
+    got, ref = run_both(engine, oracle, segs, flags=DFLAGS)
+    f = ref.batches["flags"]
+    assert np.sum((f & abi.F_CODEC_OK) != 0) >= len(frames) - 8 and not np.all(f & abi.F_CODEC_OK)
     assert_same(got, ref, DFLAGS)
