@@ -166,6 +166,75 @@ def write_stats(args, name, d):
         json.dump(cur, f, indent=1)
 
 
+def _lz4_seq_count(blk: bytes) -> int:
+    """Sequences of one LZ4 block (token walk; the last literal run counts)."""
+    ip, n, k = 0, len(blk), 0
+    while ip < n:
+        t = blk[ip]
+        ip += 1
+        ll = t >> 4
+        if ll == 15:
+            while ip < n:
+                x = blk[ip]
+                ip += 1
+                ll += x
+                if x != 255:
+                    break
+        ip += ll
+        k += 1
+        if ip + 2 > n:
+            break
+        ip += 2
+        if (t & 15) == 15:
+            while ip < n:
+                x = blk[ip]
+                ip += 1
+                if x != 255:
+                    break
+    return k
+
+
+def lz4_composition(seg: np.ndarray, file_pos, sizes, attrs, decoded_len=None, seq_sample: int = 300):
+    """Byte composition of one segment's LZ4F payloads for the per-kernel
+    algorithmic bytes (scripts/parse_traffic.py): stored (raw) block bytes
+    (k_raw_copy's), compressed block bytes and the sequences they parse into
+    (k_lzf_walk's / k_lz_exec's; sequences counted on the first seq_sample
+    compressed blocks and scaled by compressed bytes).  Frame headers only,
+    no decoding."""
+    import struct
+    raw = comp = nblk = lz4_out = 0
+    sampled_bytes = sampled_seq = 0
+    if decoded_len is None:
+        decoded_len = np.zeros(len(sizes), np.int64)
+    for pos, size, a, dl in zip(file_pos, sizes, attrs, decoded_len):
+        if (int(a) & 7) != 3:
+            continue
+        lz4_out += int(dl)
+        pay = seg[int(pos) + 61:int(pos) + int(size)].tobytes()
+        if len(pay) < 7 or pay[:4] != b"\x04\x22\x4d\x18":
+            continue
+        flg = pay[4]
+        p = 7 + (8 if flg & 8 else 0) + (4 if flg & 1 else 0)
+        while p + 4 <= len(pay):
+            w = struct.unpack_from("<I", pay, p)[0]
+            p += 4
+            if w == 0:
+                break
+            n = w & 0x7FFFFFFF
+            if w & 0x80000000:
+                raw += n
+            else:
+                comp += n
+                nblk += 1
+                if nblk <= seq_sample:
+                    sampled_bytes += n
+                    sampled_seq += _lz4_seq_count(pay[p:p + n])
+            p += n + (4 if flg & 0x10 else 0)
+    seq = int(round(comp * sampled_seq / sampled_bytes)) if sampled_bytes else 0
+    return {"raw_block_bytes": raw, "comp_block_bytes": comp, "comp_blocks": nblk, "sequences_est": seq,
+            "comp_block_decoded": max(0, lz4_out - raw)}
+
+
 def host_threads() -> int:
     """Host cores this process may use: the pool's CPU share where the box
     sets one (OMP_NUM_THREADS = 16 per GPU there), else the affinity mask."""
@@ -346,6 +415,15 @@ def run_compressed(name, kw, n_parts, seg_bytes, args, plat, eng, abi, desc, ext
                      for c in (1, 2, 3, 4)}
     n_batches = int(len(b))
     stored_payload = int(np.sum(b["size_bytes"].astype(np.int64) - abi.HEADER_SIZE))
+    lz4c = None
+    if args.stats_out and host_first is not None:
+        # partition 0's LZ4 block composition, scaled to the job by stored bytes
+        s0 = (b["segment"] == 0) & dec_ok
+        lz4c = lz4_composition(host_first, b["file_pos"][s0], b["size_bytes"][s0], b["attrs"][s0],
+                               b["decoded_len"][s0].astype(np.int64))
+        scale = stored / max(1, int(np.sum(b["size_bytes"].astype(np.int64)[b["segment"] == 0])))
+        lz4c = {k: int(round(v * scale)) for k, v in lz4c.items()}
+        lz4c["sample"] = "partition 0, scaled by stored bytes"
     del h, b, f
     eng.set_timing(True)
     plat.sync()
@@ -375,7 +453,7 @@ def run_compressed(name, kw, n_parts, seg_bytes, args, plat, eng, abi, desc, ext
             cpu = failure(f"{name} cpu baseline", e)
     write_stats(args, name, {"stored": stored, "stored_payload": stored_payload, "compressed_in": comp_in,
                              "decoded": decoded, "batches": n_batches,
-                             "compressed_batches": parity["compressed"], "records": n_rec})
+                             "compressed_batches": parity["compressed"], "records": n_rec, "lz4": lz4c})
     st = {
         "workload_id": name.upper(),
         "workload": desc,
@@ -436,6 +514,18 @@ def run_compressed(name, kw, n_parts, seg_bytes, args, plat, eng, abi, desc, ext
     return st
 
 
+def job_digest(abi, res) -> str:
+    """sha256 over every compared field of a job's batch results and record
+    index (the fields the GPU parity tests compare with the oracle)."""
+    import hashlib
+    h = hashlib.sha256()
+    for f in abi.BATCH_COMPARE_FIELDS:
+        h.update(np.ascontiguousarray(res.batches[f]).tobytes())
+    for f in abi.RECORD_COMPARE_FIELDS:
+        h.update(np.ascontiguousarray(res.records[f]).tobytes())
+    return h.hexdigest()
+
+
 def run_h2d(args, plat, eng, abi, data, seg_bytes, n_parts, flags, ref):
     """H2D-inclusive rate (rpgpu_validate_host): the same C1 partitions,
     host-resident in pinned memory, copied to the device in double-buffered
@@ -443,13 +533,14 @@ def run_h2d(args, plat, eng, abi, data, seg_bytes, n_parts, flags, ref):
     the batch results, record index and summaries returned to host arrays
     (storage/log_replayer.cc:95-114 reads segments from the file into
     memory).  Not `value` (device-resident); reported beside
-    it.  `ref` = the device job's (n_batches, n_records)."""
+    it.  `ref` = the device job's (n_batches, n_records, job_digest)."""
     host = plat.host_segments(data, seg_bytes, n_parts)
     total = seg_bytes * n_parts
     r = eng.validate_host(host, flags)  # warm-up: staging slots allocated
     b = r.batches
-    ok = bool(len(b) == ref[0] and len(r.records) == ref[1] and np.all(b["flags"] & abi.F_CRC_OK)
-              and np.all(b["flags"] & abi.F_PARSE_OK) and int(r.totals["overflow"]) == 0)
+    counts_ok = bool(len(b) == ref[0] and len(r.records) == ref[1] and np.all(b["flags"] & abi.F_CRC_OK)
+                     and np.all(b["flags"] & abi.F_PARSE_OK) and int(r.totals["overflow"]) == 0)
+    same = bool(ref[2] is not None and job_digest(abi, r) == ref[2])
     del r, b
     reps = max(1, min(args.steps, 3))
     times = []
@@ -469,7 +560,9 @@ def run_h2d(args, plat, eng, abi, data, seg_bytes, n_parts, flags, ref):
         "GBps": round(total / mean / 1e9, 2),
         "GBps_best": round(total / best / 1e9, 2),
         "ms_per_job": round(mean * 1e3, 2),
-        "parity": {"same_batches_records_as_device_job": ok},
+        # counts and verdict bits, and every compared field of the batch
+        # results and the record index (sha256) against the device job's
+        "parity": {"counts_and_flags_match": counts_ok, "batch_results_and_record_index_identical": same},
     }
 
 
@@ -836,13 +929,19 @@ def run_c1(args, plat, dist, eng, abi, world, rank):
             cpu = cpu_baseline_c1(host_first)
         except Exception as e:
             cpu = failure("c1 cpu baseline", e)
+    dev_digest = None
+    if world == 1 and not args.no_h2d and "h2d" in args.workloads.split(","):
+        try:
+            dev_digest = job_digest(abi, out.to_host())
+        except Exception:
+            dev_digest = None
     # release the C1 job's outputs before the host path allocates its own
     del out, d_offs, payload, index_res
     plat.empty_cache()
     h2d = None
     if world == 1 and not args.no_h2d and "h2d" in args.workloads.split(","):
         try:
-            h2d = run_h2d(args, plat, eng, abi, data, seg_bytes, len(parts), flags, (n_batches, n_records))
+            h2d = run_h2d(args, plat, eng, abi, data, seg_bytes, len(parts), flags, (n_batches, n_records, dev_digest))
         except Exception as e:
             h2d = failure("h2d", e)
     del data
@@ -886,9 +985,11 @@ def run_c1(args, plat, dist, eng, abi, world, rank):
             "alg_bytes_per_launch": alg,
             "kernel_ms": round(v_ms, 4),
             "kernel_ms_def": "validate stage between HIP events on the launch stream, mean over the timed steps",
-            # the committed rocprofv3 trace of the driver's command (same
-            # kernel, same steps): its mean and the fraction it implies
-            "trace": dict(trace, frac=round(alg / (trace["mean_ms"] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4))
+            # the COMMITTED rocprofv3 trace of the driver's command (taken on
+            # the tree named by its tag, not in this run): its mean and the
+            # fraction it implies, labelled as such
+            "committed_trace": dict(trace, source="profiles/kernel_trace.json (committed; not this run)",
+                                    frac_at_trace=round(alg / (trace["mean_ms"] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4))
             if trace else None,
             "walk": {"kernel": "k_walk", "kernel_ms": round(w_ms, 4), "alg_bytes_per_launch": walk_alg,
                      "achieved": round(walk_alg / (w_ms * 1e-3) / 1e9, 1) if w_ms > 0 else None},

@@ -1526,6 +1526,29 @@ DEV uint32_t wave_scan(uint32_t v) {
 #endif
 DEV void xmatch(XRing& x, uint32_t d, uint32_t off, uint32_t ml, bool far) {
     const uint32_t s = d - off;
+#if RPGPU_XMATCH_BATCH == 3
+    // a source that does not overlap the destination (off >= ml: C2 99.96 %
+    // of matches; every far one) is read 32 bytes at a time, both loads in
+    // flight before the stores: one LDS (or arena) latency per 32 bytes
+    // instead of one per 16 (the round's chain is these latencies)
+    if (far || off >= ml) {
+        for (uint32_t c = 0; c < ml; c += 32) {
+            uint4 v0, v1;
+            if (far) {
+                const auto t0 = __builtin_amdgcn_raw_buffer_load_b128(x.rs, s + c, 0, kSc1);
+                const auto t1 = __builtin_amdgcn_raw_buffer_load_b128(x.rs, s + c + 16, 0, kSc1);
+                v0 = make_uint4(t0[0], t0[1], t0[2], t0[3]);
+                v1 = make_uint4(t1[0], t1[1], t1[2], t1[3]);
+            } else {
+                v0 = xld16(x.r, s + c);
+                v1 = c + 16 < ml ? xld16(x.r, s + c + 16) : v0;
+            }
+            xst(x.r, d + c, v0, ml - c < 16 ? ml - c : 16);
+            if (c + 16 < ml) xst(x.r, d + c + 16, v1, ml - c - 16 < 16 ? ml - c - 16 : 16);
+        }
+        return;
+    }
+#endif
 #if RPGPU_XMATCH_BATCH == 2
     if (far) {
         for (uint32_t c = 0; c < ml; c += 32) {
@@ -3073,8 +3096,8 @@ __global__ void k_init_dstamps() {
 // stages the kFSlot stream bytes at its parse position in its own LDS slot
 // (all lanes' 16-byte loads in flight together: one memory latency per
 // round for the wave) and walks the sequences that start in the first kFWin
-// of them with a straight-line step (fseq_w: one unaligned 16-byte LDS read,
-// ~60 instructions, no per-sequence branches), writing each as an 8-byte
+// of them with a straight-line step (fseq_w: three aligned 8-byte LDS reads
+// funnel-shifted, ~60 instructions, no per-sequence branches), writing each as an 8-byte
 // record {lip | ll << 16, ml | off << 16} to frecs (a block reserves
 // csize / 3 + 2 records: every sequence but the last takes >= 3 input bytes).
 // Verdicts follow LZ4_decompress_generic (liblz4 1.9.3, lz4_run above): a

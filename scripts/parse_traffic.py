@@ -52,10 +52,22 @@ def alg_bytes(w, st):
         # CRC of every stored payload, 128 B per batch result (read + write)
         "k_validate": st["stored_payload"] + 128 * st["batches"],
         "k_lz_walk": None,  # (round 5: only the pieces k_lzf_walk does not take)
-        "k_lzf_walk": st["compressed_in"],
-        "k_lz_exec": st["decoded"],
         "k_validate_decoded": st["decoded"] + idx * st["records"],
     }
+    z = st.get("lz4")
+    if z:
+        # round 6: the LZ4 kernels priced at their own
+        # share.  k_raw_copy: stored blocks read + written; k_lzf_walk: the
+        # compressed blocks read + 8 B records written; k_lz_exec: records +
+        # literal bytes read (compressed bytes less >= 3 bytes of token /
+        # offset per sequence) + the compressed blocks' output written
+        seq = z["sequences_est"]
+        a["k_raw_copy"] = 2 * z["raw_block_bytes"]
+        a["k_lzf_walk"] = z["comp_block_bytes"] + 8 * seq
+        a["k_lz_exec"] = 8 * seq + max(0, z["comp_block_bytes"] - 3 * seq) + z["comp_block_decoded"]
+    else:
+        a["k_lzf_walk"] = st["compressed_in"]
+        a["k_lz_exec"] = st["decoded"]
     if w == "c1":
         a["k_walk"] = idx * st["records"] + 128 * st["batches"]
     return a

@@ -269,7 +269,7 @@ def test_bench_single_rank_all_stanzas(env1, rplib, tmp_path):
     assert j["config"]["c2"]["parity"]["all_valid"]
     assert j["config"]["c6"]["member_pass"]["decoded_bytes"] > 0
     h = j["config"]["h2d"]
-    assert "error" not in h and h["GBps"] > 0 and h["parity"]["same_batches_records_as_device_job"], h
+    assert "error" not in h and h["GBps"] > 0 and h["parity"]["counts_and_flags_match"], h
     # the full stanzas (per-kernel tables) go to --detail-out
     d = json.load(open(tmp_path / "detail.json"))
     assert set(d) >= {"c1", "c2", "c5", "c6"} and "workload" in d["c2"]
