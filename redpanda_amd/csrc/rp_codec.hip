@@ -1138,8 +1138,12 @@ DEV bool plan_lz4f(const DeviceJob& j, In& in, int64_t n, uint64_t src_abs, uint
     fp.nb = nb;
     fp.ccs = ccs;
     fp.ccs_val = ccs_val;
-    fp.csf = csf;
     fp.content_size = csf ? ((uint64_t)in_le32(in, 6) | ((uint64_t)in_le32(in, 10) << 32)) : 0;
+    // a content-size field of 0 is "unknown" to LZ4F (frameRemainingSize is
+    // never set, so the frameSize_wrong check never fires): found by the
+    // round-6 mutation corpus, where the job rejected such a frame that
+    // liblz4, the oracle and rpgpu_uncompress all accept
+    fp.csf = csf && fp.content_size != 0;
     return true;
 }
 

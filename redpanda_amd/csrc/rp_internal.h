@@ -257,6 +257,9 @@ struct DeviceJob {
     uint32_t exec_waves;          // k_lz_exec waves (lz_exec_wgs_per_cu() per workgroup; sizes `seqs`)
     PieceState* pstate;           // block_capacity: walk results
     SeqRec* pool;                 // record slabs
+    uint32_t crc_compose;         // k_crc_compose assembles LZ4F stored crcs from k_raw_copy's block CRCs
+    uint32_t* dchain;             // k_dchain's record-chain ends of decoded payloads, at their index slots (the
+                                  // record pool, free again once decode is done); nullptr = k_validate_decoded chains
     uint32_t* slab_next;          // pool_slabs: next slab of the same piece
     uint32_t pool_slabs;
     uint2* frecs;                 // LZ4 sequence records of k_lzf_walk (executed by k_lz_exec), 8 B each

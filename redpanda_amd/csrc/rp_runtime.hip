@@ -768,6 +768,15 @@ int submit_body(rpgpu_ctx* c, const rpgpu_job* job, hipStream_t s, int stop, Pla
     // k_lz_exec's own walk of the pieces the pool cuts short)
     if (const char* e = diag_env("RPGPU_POOL_SLABS")) j.pool_slabs = std::min<uint32_t>(j.pool_slabs, (uint32_t)atoi(e));
     j.pool = (SeqRec*)c->pool;
+    // the decoded payloads' record chains (k_dchain) reuse the record pool,
+    // idle once decode is done: one u32 per index slot.  RPGPU_DCHAIN=0
+    // (diagnostic build): k_validate_decoded chains the records itself (A/B)
+    // RPGPU_CRC_COMPOSE=0 (diagnostic build): k_validate streams every stored payload (A/B)
+    static const bool compose_on = [] { const char* e = diag_env("RPGPU_CRC_COMPOSE"); return !(e && *e == '0'); }();
+    j.crc_compose = compose_on ? 1u : 0u;
+    static const bool dchain_on = [] { const char* e = diag_env("RPGPU_DCHAIN"); return !(e && *e == '0'); }();
+    j.dchain = (dec && dchain_on && c->pool && (uint64_t)c->pool_bytes / 4 >= j.record_capacity) ? (uint32_t*)c->pool
+                                                                                                  : nullptr;
     j.slab_next = (uint32_t*)((uint8_t*)c->pool + (size_t)j.pool_slabs * kSlabRecs * sizeof(SeqRec));
     // fast-path records: the planner reserves csize / 3 + 2 per listed LZ4
     // block (2.7 bytes per compressed byte; C2 uses 0.3 of the job's bytes),

@@ -549,6 +549,26 @@ DEV uint32_t chain_starts(const Src& src, uint32_t n, uint32_t start, uint32_t w
     return m;
 }
 
+// The same starts and ends from k_dchain's precomputed chain of the payload
+// (pre[k] = the position after record k, 0xFFFFFFFF where chain_starts
+// stops): one coalesced load per 64 records instead of 64 dependent ones.
+// s0 = the start of record `done` (0, or pre[done - 1]).
+DEV uint32_t pre_starts(const uint32_t* pre, uint32_t s0, uint32_t done, uint32_t want, uint32_t& my_start,
+                        uint32_t& my_end) {
+    const uint32_t l = lane_v();
+    const uint32_t e = l < want ? pre[done + l] : 0u;
+    // lane l - 1's end is lane l's start (DPP wave_shr:1; lane 0 takes s0)
+    const uint32_t prev = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)e, 0x138, 0xF, 0xF, false);
+    const uint64_t stops = __ballot(l < want && e == 0xFFFFFFFFu);
+    const uint32_t m = stops ? (uint32_t)__builtin_ctzll(stops) + 1u : want;
+    my_start = my_end = 0xFFFFFFFFu;
+    if (l < m) {
+        my_start = l == 0 ? s0 : prev;
+        my_end = e;
+    }
+    return m;
+}
+
 // Lanes [0, m) parse one record each from their speculative starts; the
 // prefix whose starts are confirmed by the previous record's exact end is
 // committed to the index.  Returns false when a record failed (wr filled).
@@ -616,7 +636,7 @@ DEV void group_init(Group& g) {
 }
 
 DEV WalkResult walk_records(const uint8_t* p0, uint32_t n, int32_t rc, uint32_t batch_ord, rpgpu_record_index* out,
-                            uint64_t out_cap, Group& g) {
+                            uint64_t out_cap, Group& g, const uint32_t* pre = nullptr) {
     WalkResult wr;
     wr.parsed = 0;
     wr.err = 0;
@@ -631,7 +651,8 @@ DEV WalkResult walk_records(const uint8_t* p0, uint32_t n, int32_t rc, uint32_t 
     const MemSrc mem{p0};
     if (!g.first) {
         STAMP(w0);
-        g.m = chain_starts(mem, n, 0u, total < 64u ? total : 64u, g.my_start, g.my_end);
+        const uint32_t want = total < 64u ? total : 64u;
+        g.m = pre ? pre_starts(pre, 0u, 0u, want, g.my_start, g.my_end) : chain_starts(mem, n, 0u, want, g.my_start, g.my_end);
         record_regions(p0, mis, n, lane_v() < g.m, g.my_start, g.my_end, g.H, g.T);
         STAMP(w1);
         STAMP_ADD(6, w1 - w0);
@@ -640,7 +661,12 @@ DEV WalkResult walk_records(const uint8_t* p0, uint32_t n, int32_t rc, uint32_t 
         if (!parse_group(p0, mis, n, g.m, g.my_start, g.H, g.T, batch_ord, out, out_cap, done, start, wr)) return wr;
         if (done >= total) break;
         const uint32_t want = (total - done) < 64u ? (total - done) : 64u;
-        g.m = chain_starts(mem, n, start, want, g.my_start, g.my_end);
+        // the precomputed chain holds while the parsed records confirm it
+        // (they do unless a record's parse ends elsewhere than its length
+        // says, which fails the walk first); otherwise chain from `start`
+        if (pre && uni32(pre[done - 1]) != start) pre = nullptr;
+        g.m = pre ? pre_starts(pre, start, done, want, g.my_start, g.my_end)
+                  : chain_starts(mem, n, start, want, g.my_start, g.my_end);
         record_regions(p0, mis, n, lane_v() < g.m, g.my_start, g.my_end, g.H, g.T);
     }
     wr.parsed = done;
@@ -712,6 +738,9 @@ constexpr int kDwBase = offsetof(rpgpu_batch_result, index_base) / 4;
 constexpr int kDwDlen = offsetof(rpgpu_batch_result, decoded_len) / 4;
 constexpr int kDwAttrs = offsetof(rpgpu_batch_result, attrs) / 4;
 constexpr int kDwPraw = offsetof(rpgpu_batch_result, reserved1) / 4;
+constexpr int kDwRes0 = offsetof(rpgpu_batch_result, reserved0) / 4;  // reserved0 in the high half
+constexpr int kDwCcomp = offsetof(rpgpu_batch_result, crc_computed) / 4;
+static_assert(offsetof(rpgpu_batch_result, reserved0) % 4 == 2, "reserved0: the high half of its dword");
 static_assert(sizeof(rpgpu_batch_result) == 128 && offsetof(rpgpu_batch_result, attrs) % 4 == 0, "desc layout");
 
 DEV uint32_t load_desc_raw(const DeviceJob& j, uint64_t b) {
@@ -727,6 +756,8 @@ struct Desc {
     uint32_t flags, crc, praw, codec, seg, dlen;
     uint64_t S, n, ib, islots, doff;
     int32_t rc;
+    uint32_t scc;    // the stored crc was composed by k_crc_compose (reserved0 bit 1): ccomp holds it
+    uint32_t ccomp;
 };
 
 DEV Desc desc_of(uint32_t raw) {
@@ -743,21 +774,39 @@ DEV Desc desc_of(uint32_t raw) {
     d.ib = (uint64_t)rl(raw, 32) | ((uint64_t)rl(raw, 33) << 32);
     d.islots = ((uint64_t)rl(raw, 34) | ((uint64_t)rl(raw, 35) << 32)) - d.ib;
     d.doff = (uint64_t)rl(raw, 36) | ((uint64_t)rl(raw, 37) << 32);
+    d.scc = (rl(raw, kDwRes0) >> 16) & 2u;
+    d.ccomp = rl(raw, kDwCcomp);
     return d;
 }
 
 // the stored payload of a batch as a stream (empty when there is none)
 DEV Stream stored_stream(const DeviceJob& j, const Desc& d, bool valid) {
-    return (valid && (d.flags & RPGPU_F_COMPLETE)) ? make_stream(j.data, d.S, d.S + d.n) : make_stream(j.data, 0, 0);
+    return (valid && (d.flags & RPGPU_F_COMPLETE) && !d.scc) ? make_stream(j.data, d.S, d.S + d.n)
+                                                               : make_stream(j.data, 0, 0);
 }
 
 // the record walk of one payload into the batch's index slots
 DEV WalkResult walk_batch(const DeviceJob& j, const Desc& ds, const uint8_t* p0, uint32_t n, uint64_t b, bool& idx_ok,
-                          Group& g0) {
+                          Group& g0, const uint32_t* pre = nullptr) {
     idx_ok = ds.ib + ds.islots <= j.record_capacity;
     rpgpu_record_index* out = idx_ok ? j.records + ds.ib : nullptr;
     const uint64_t cap = idx_ok ? ds.islots : 0;
-    return walk_records(p0, n, ds.rc, (uint32_t)b, out, cap, g0);
+    return walk_records(p0, n, ds.rc, (uint32_t)b, out, cap, g0, pre);
+}
+
+// a decoded payload whose record chain k_dchain precomputes (k_validate_decoded
+// takes it from there iff this holds for both): its walk runs, its
+// record_count index slots exist and hold the chain, and its records are
+// long enough that each chain step is a line of its own (>= 256 B on
+// average; shorter records share lines, which the wave's scalar chain reads
+// at cache latency: C5's 100-byte records ran 3.6 -> 4.0 ms lane-chained)
+// and few enough for one lane's serial chain
+constexpr uint32_t kDchainMinRecBytes = 256, kDchainMaxRecs = 8192;
+DEV bool dchain_ok(const DeviceJob& j, uint32_t flags, int32_t rc, uint64_t ib, uint64_t islots, uint32_t dlen) {
+    return j.dchain && (flags & RPGPU_F_CODEC_OK) && (j.flags & RPGPU_JOB_PARSE) &&
+           (j.layout != RPGPU_LAYOUT_WIRE || (flags & RPGPU_F_CRC_OK)) && rc > 0 && (uint64_t)rc <= islots &&
+           ib + islots <= j.record_capacity && (uint32_t)rc <= kDchainMaxRecs &&
+           dlen >= kDchainMinRecBytes * (uint32_t)rc;
 }
 
 // LDS image of the CRC tables (every workgroup of the validate kernels).
@@ -1232,9 +1281,12 @@ __global__ __launch_bounds__(1024) void k_validate(DeviceJob j) {
             // a large stored payload (disk layout) has its CRC computed in
             // kSplitParts chunks on other waves (k_crc_split) and merged by
             // GF(2) shifts (k_crc_combine), which then sets the verdict
-            const bool split = !wire && d.n >= j.split_min;
+            // (a payload whose crc k_crc_compose assembled from the raw-block
+            // CRCs of k_raw_copy and its other bytes: taken as it is)
+            const bool split = !wire && !d.scc && d.n >= j.split_min;
             uint32_t crc = 0;
-            if (!split) crc = ~crc_stream(lds, K, st, v, gt, d.praw ^ c40);
+            if (d.scc) crc = d.ccomp;
+            else if (!split) crc = ~crc_stream(lds, K, st, v, gt, d.praw ^ c40);
             record_regions(p0, (uint32_t)((uintptr_t)p0 & 15), n, g0.first && lane_v() < g0.m, g0.my_start, g0.my_end,
                            g0.H, g0.T);
             STAMP(tb2);
@@ -1358,6 +1410,130 @@ __global__ __launch_bounds__(256) void k_crc_combine(DeviceJob j) {
     }
 }
 
+// k_crc_compose (round 6): the stored crc of an LZ4F payload decoded block by
+// block, assembled without reading its stored (raw) blocks again.  k_raw_copy
+// copied every independent raw block without a block checksum to the arena
+// and took its linear CRC on the way (BlockItem.crc; the decoded bytes are the
+// stored ones); the payload's other bytes (frame header, size words,
+// compressed blocks, checksums, end mark, anything after it) are CRC'd here
+// from the stored payload, and the pieces merged in order by GF(2) shifts:
+//   state = x^(8 len) * state  ^  L(block)     per raw block,
+// from the BE40 prefix state S0, exactly the state k_validate's stream
+// reaches.  C2: 12 of its 12.9 GB of stored payload are raw blocks that
+// k_validate read a second time.  One wave per decode item; k_validate takes
+// the result (Desc.scc) instead of streaming the payload.
+constexpr uint64_t kComposeMin = 64u << 10;
+// sum over the wave of block sizes (each <= 4 MiB, so 64 of them fit 32 bits)
+DEV uint32_t wave_sum_u32(uint32_t v) {
+    for (int o = 32; o >= 1; o >>= 1) v += (uint32_t)__shfl_xor((int)v, o, 64);
+    return uni32(v);
+}
+__global__ __launch_bounds__(1024) void k_crc_compose(DeviceJob j) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    const uint32_t count = j.counters[2];
+    if (count == 0 || j.counters[40] == 0) return;
+    init_lds_tables(lds, j.tables);
+    const Keys K = make_keys();
+    const uint32_t l = lane_v(), c40 = uni32(j.tables->c40);
+    auto gap = [&](uint64_t a, uint64_t e, uint32_t state) __attribute__((always_inline)) {
+        const Stream st = make_stream(j.data, a, e);
+        Win v;
+        load_window(st, 0, v);
+        const uint4 gt = load_tail(st);
+        return crc_stream(lds, K, st, v, gt, state);
+    };
+    for (;;) {
+        const uint32_t item = wave_fetch_add(&j.counters[12], 1u);
+        if (item >= count) break;
+        if (uni32(j.plans[item].mode) != 1u) continue;
+        const uint32_t first = uni32(j.plans[item].first), nb = uni32(j.plans[item].nb);
+        // composed only where raw blocks are most of a large payload: a
+        // payload of mostly compressed blocks streams faster through
+        // k_validate than its gaps do here one window latency each (C5:
+        // validate 3.67 -> 3.98 ms with every payload holding a raw block
+        // composed)
+        uint64_t rawb = 0;
+        for (uint32_t k0 = 0; k0 < nb; k0 += 64) {
+            const uint32_t k = k0 + l;
+            const bool r = k < nb && j.blocks[first + k].fast == kLzfRaw;
+            rawb += wave_sum_u32(r ? j.blocks[first + k].csize : 0u);
+        }
+        const uint64_t b = uni32(j.decode_list[item]);
+        const Desc d = desc_of(load_desc_raw(j, b));
+        if (!(d.flags & RPGPU_F_COMPLETE) || d.n < kComposeMin || 4 * rawb < 3 * d.n) continue;
+        uint32_t state = d.praw ^ c40;
+        uint64_t pos = d.S;  // (index_base still holds the payload start: k_validate runs after)
+        for (uint32_t k = 0; k < nb; k++) {
+            if (uni32(j.blocks[first + k].fast) != kLzfRaw) continue;
+            const uint64_t a = uni64(j.blocks[first + k].src);
+            const uint32_t len = uni32(j.blocks[first + k].csize);
+            if (a > pos) state = gap(pos, a, state);
+            state = crc_shift(state, len) ^ uni32(j.blocks[first + k].crc);
+            pos = a + len;
+        }
+        if (d.S + d.n > pos) state = gap(pos, d.S + d.n, state);
+        if (l == 0) {
+            rpgpu_batch_result* R = &j.batches[b];
+            R->crc_computed = ~state;
+            R->reserved0 = (uint16_t)(R->reserved0 | 2u);
+        }
+    }
+}
+
+// k_dchain (round 6): the record chain of every decoded payload, one LANE per
+// payload, so that all of a job's chains are in flight at once.  (The chain
+// is one dependent load per record: k_validate_decoded's wave-uniform
+// chain_starts paid ~520 of them per C2 batch, for one batch after another
+// on each wave, 3.3 ms for C2's 16 M records.)  pre[k] = the position after
+// record k's length varint and body, exactly chain_starts' arithmetic, and
+// 0xFFFFFFFF where it stops (a start at or past the end, a bad length);
+// written at the payload's index slots of the record pool (j.dchain), read
+// back 64 at a time by walk_records (pre_starts).
+__global__ __launch_bounds__(256) void k_dchain(DeviceJob j) {
+    const uint32_t nlz = j.counters[2], ngz = j.counters[16], count = nlz + ngz + j.counters[19];
+    const uint8_t* const aend = j.decoded + j.decoded_capacity;
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < count; i += gridDim.x * blockDim.x) {
+        const uint64_t b = i < nlz ? j.decode_list[i] : i < nlz + ngz ? j.inf_list[i - nlz] : j.host_list[i - nlz - ngz];
+        const rpgpu_batch_result& R = j.batches[b];
+        const uint32_t flags = R.flags;
+        const int32_t rc = R.record_count;
+        const uint64_t ib = j.slots[b], islots = j.slots[b + 1] - ib;
+        if (!dchain_ok(j, flags, rc, ib, islots, R.decoded_len)) continue;
+        const uint8_t* p0 = j.decoded + j.dcap[b];
+        const uint32_t n = R.decoded_len;
+        uint32_t* pre = j.dchain + ib;
+        uint32_t p = 0;
+        for (int32_t k = 0; k < rc; k++) {
+            if (p >= n) {
+                pre[k] = 0xFFFFFFFFu;
+                break;
+            }
+            // 12 bytes at p: four aligned dwords (byte loads at the arena's end)
+            const uint8_t* q = p0 + p;
+            const uint32_t* a = (const uint32_t*)((uintptr_t)q & ~(uintptr_t)3);
+            const uint32_t sh = (uint32_t)((uintptr_t)q & 3);
+            uint32_t w0, w1, w2, w3;
+            if ((const uint8_t*)(a + 4) <= aend) {
+                w0 = a[0]; w1 = a[1]; w2 = a[2]; w3 = a[3];
+            } else {
+                uint32_t w[4] = {0u, 0u, 0u, 0u};
+                for (uint32_t t = 0; t < 16; t++)
+                    if ((const uint8_t*)a + t < aend) w[t >> 2] |= (uint32_t)((const uint8_t*)a)[t] << (8 * (t & 3));
+                w0 = w[0]; w1 = w[1]; w2 = w[2]; w3 = w[3];
+            }
+            uint32_t br;
+            const int64_t len = varint12(__builtin_amdgcn_alignbyte(w1, w0, sh), __builtin_amdgcn_alignbyte(w2, w1, sh),
+                                         __builtin_amdgcn_alignbyte(w3, w2, sh), n - p, br);
+            if (len < 0 || (uint64_t)len > n) {
+                pre[k] = 0xFFFFFFFFu;
+                break;
+            }
+            p = p + br + (uint32_t)len;
+            pre[k] = p;
+        }
+    }
+}
+
 // reset_size_checksum_metadata (storage/parser_utils.cc:114-120) and the
 // record walk over every payload k_decode uncompressed: one wave per
 // worklist item, after k_validate has written the stored-payload verdict.
@@ -1390,7 +1566,7 @@ __global__ __launch_bounds__(1024) void k_validate_decoded(DeviceJob j) {
         // of k_lz_exec's flushes (reserved0 = 1); frames decoded whole (the
         // sequential list) are read back here
         uint32_t dcrc;
-        if (uni32((uint32_t)R->reserved0) == 1u) {
+        if (uni32((uint32_t)R->reserved0) & 1u) {
             dcrc = uni32(R->decoded_crc);
         } else {
             const Stream ds = make_stream(j.decoded, d.doff, d.doff + dl);
@@ -1406,7 +1582,8 @@ __global__ __launch_bounds__(1024) void k_validate_decoded(DeviceJob j) {
             bool idx_ok;
             Group g0;
             group_init(g0);
-            const WalkResult w = walk_batch(j, d, j.decoded + d.doff, (uint32_t)dl, b, idx_ok, g0);
+            const uint32_t* pre = dchain_ok(j, d.flags, d.rc, d.ib, d.islots, d.dlen) ? j.dchain + d.ib : nullptr;
+            const WalkResult w = walk_batch(j, d, j.decoded + d.doff, (uint32_t)dl, b, idx_ok, g0, pre);
             f |= walk_flags(j, w, idx_ok, perr);
             parsed = w.parsed;
         }
@@ -1674,8 +1851,12 @@ hipError_t launch_validate(const DeviceJob& j, hipStream_t s, uint32_t grid) {
                                   kLdsValidateBytes);
         (void)hipFuncSetAttribute((const void*)k_crc_split, hipFuncAttributeMaxDynamicSharedMemorySize,
                                   kLdsValidateBytes);
+        (void)hipFuncSetAttribute((const void*)k_crc_compose, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  kLdsValidateBytes);
         attr = true;
     }
+    if (j.crc_compose && (j.flags & RPGPU_JOB_DECODE) && j.decoded && j.raw_list && j.layout == RPGPU_LAYOUT_DISK)
+        hipLaunchKernelGGL(k_crc_compose, dim3(grid), dim3(64 * kVWaves), kLdsValidateBytes, s, j);
     hipLaunchKernelGGL(k_validate, dim3(grid), dim3(64 * kVWaves), kLdsValidateBytes, s, j);
 #ifdef RPGPU_STAMPS
     hipLaunchKernelGGL(k_print_stamps, dim3(1), dim3(1), 0, s);
@@ -1684,8 +1865,10 @@ hipError_t launch_validate(const DeviceJob& j, hipStream_t s, uint32_t grid) {
         hipLaunchKernelGGL(k_crc_split, dim3(grid), dim3(64 * kVWaves), kLdsValidateBytes, s, j);
         hipLaunchKernelGGL(k_crc_combine, dim3((j.split_capacity + 3) / 4), dim3(256), 0, s, j);
     }
-    if ((j.flags & RPGPU_JOB_DECODE) && j.decoded)
+    if ((j.flags & RPGPU_JOB_DECODE) && j.decoded) {
+        if (j.dchain && (j.flags & RPGPU_JOB_PARSE)) hipLaunchKernelGGL(k_dchain, dim3(grid * 8), dim3(256), 0, s, j);
         hipLaunchKernelGGL(k_validate_decoded, dim3(grid), dim3(64 * kVWaves), kLdsValidateBytes, s, j);
+    }
     return hipGetLastError();
 }
 

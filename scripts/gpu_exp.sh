@@ -6,7 +6,7 @@ cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
 TAG=${1:-r06x}
 if [ -z "${SKIP_TESTS:-}" ]; then
-timeout -k 10 600 python -u -m pytest tests/test_gpu_lz4_walk.py tests/test_gpu_parity.py -m gpu -x -v --timeout 240 --timeout-method thread -k "${TESTK:-lz4 or c2_recipe or c5_recipe or codec_mix or raw_snappy or uncompress or golden}" > gpurun_out/pytest_$TAG.log 2>&1 || { tail -60 gpurun_out/pytest_$TAG.log; exit 1; }
+timeout -k 10 600 python -u -m pytest ${TESTS:-tests/test_gpu_lz4_walk.py tests/test_gpu_parity.py} -m gpu -x -v --timeout 240 --timeout-method thread -k "${TESTK:-lz4 or c2_recipe or c5_recipe or codec_mix or raw_snappy or uncompress or golden}" > gpurun_out/pytest_$TAG.log 2>&1 || { tail -60 gpurun_out/pytest_$TAG.log; exit 1; }
 tail -2 gpurun_out/pytest_$TAG.log
 fi
 if [ -n "${AB:-}" ]; then

@@ -105,16 +105,26 @@ def test_oracle_job_on_corpus(oracle):
     libraries on the corpus."""
     segs, parts = corpus_segments()
     offs = np.cumsum([0] + [s.size for s in segs]).astype(np.uint64)
-    ref = oracle.run_job(np.concatenate(segs), offs, JFLAGS)
+    data = np.concatenate(segs)
+    ref = oracle.run_job(data, offs, JFLAGS, decoded_cap=data.size * 64)
     n_ok = sum(1 for p in parts for e, _ in p if e["rc"] == 0)
     assert _job_vs_libraries(ref, parts) >= n_ok - 8
 
 
 @pytest.mark.gpu
 def test_gpu_corpus_job(engine, oracle):
-    from test_gpu_parity import assert_same, run_both
+    import torch
+    from test_gpu_parity import assert_same
     segs, parts = corpus_segments()
-    got, ref = run_both(engine, oracle, segs, flags=JFLAGS)
+    offs = np.cumsum([0] + [s.size for s in segs]).astype(np.uint64)
+    data = np.concatenate(segs)
+    # one decode-arena capacity for both: mutated frames claim large plans
+    # (content sizes, block maxima), and an arena that runs out sets the same
+    # DECODE_OVERFLOW bits in both only when both have the same room
+    cap = data.size * 64
+    ref = oracle.run_job(data, offs, JFLAGS, decoded_cap=cap)
+    d = torch.from_numpy(np.concatenate([data, np.zeros(16, np.uint8)])).cuda()[: data.size]
+    got = engine.validate(d, offs, JFLAGS, decoded_capacity=cap)
     assert_same(got, ref, JFLAGS)
     n_ok = sum(1 for p in parts for e, _ in p if e["rc"] == 0)
     assert _job_vs_libraries(got, parts) >= n_ok - 8
@@ -130,3 +140,32 @@ def test_gpu_corpus_uncompress_batch(engine):
             assert st == 0 and len(got) == e["out_len"] and hashlib.sha256(got).hexdigest() == e["out_sha256"], e
         else:
             assert st == abi.E_CODEC, (e, st)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", [11, 12])
+def test_gpu_fuzz_job(engine, oracle, seed):
+    """~5,200 fresh mutations per seed (library-made frames, tests/codec_fuzz.py)
+    through one HIP job, field by field against the oracle's job; the
+    oracle is pinned to the libraries by test_oracle_matches_libraries."""
+    import torch
+    from test_gpu_parity import assert_same
+    R = oracle.ref()
+    if R is None:
+        pytest.skip("oracle/_ref/libcodecref.so not built")
+    cor = F.corpus(R, 0xF100 + seed, 400, 12)
+    segs = []
+    for part in (cor[0::2], cor[1::2]):
+        out = bytearray()
+        for i, (codec, _kind, f) in enumerate(part):
+            out += bg.batch(f, 1, base_offset=i, attrs=codec)
+        segs.append(np.frombuffer(bytes(out), dtype=np.uint8).copy())
+    offs = np.cumsum([0] + [s.size for s in segs]).astype(np.uint64)
+    data = np.concatenate(segs)
+    cap = data.size * 64
+    ref = oracle.run_job(data, offs, JFLAGS, decoded_cap=cap)
+    d = torch.from_numpy(np.concatenate([data, np.zeros(16, np.uint8)])).cuda()[: data.size]
+    got = engine.validate(d, offs, JFLAGS, decoded_capacity=cap)
+    ok = (ref.batches["flags"] & abi.F_CODEC_OK) != 0
+    assert len(ref.batches) == len(cor) and 0.1 * len(cor) < int(np.sum(ok)) < 0.9 * len(cor)
+    assert_same(got, ref, JFLAGS)
