@@ -2861,6 +2861,7 @@ __global__ __launch_bounds__(RPGPU_RAW_THREADS) void k_raw_copy(DeviceJob j) {
         if (lane() == 0) {
             j.blocks[p].out = (int32_t)n;
             j.blocks[p].crc = pcrc;
+            atomicAdd((unsigned long long*)(j.counters + 24), (unsigned long long)n);  // k_crc_compose's gate
         }
     }
 }
@@ -2955,12 +2956,19 @@ __global__ __launch_bounds__(256) void k_decode_finish(DeviceJob j) {
     lds_u8* xbuf = (lds_u8*)xb[threadIdx.x >> 6];
     const uint32_t count = j.counters[2];
     const uint32_t l = lane();
-    // frames claimed one at a time (counters[14]): the content checksums are
-    // long serial chains and only some frames carry one
+    // frames claimed one at a time: the content checksums are long serial
+    // chains (~1 ms per MiB: XXH32's four accumulators, one lane each) and
+    // only some frames carry one, so those are claimed first (counters[44])
+    // and all start at once; the rest after them (counters[14]).  (In item
+    // order a wave could meet two 1 MiB checksummed frames in a row: C2's
+    // k_decode_finish 2.5-3.1 ms.)
+    for (uint32_t phase = 0; phase < 2; phase++)
     for (;;) {
-        const uint32_t item = wave_fetch_add(&j.counters[14], 1u);
+        const uint32_t item = wave_fetch_add(&j.counters[phase == 0 ? 44 : 14], 1u);
         if (item >= count) break;
         const uint32_t mode = uni32(j.plans[item].mode);
+        const bool xxh_first = mode == 1 && uni32(j.plans[item].ccs) != 0;
+        if (xxh_first != (phase == 0)) continue;
         const uint32_t b = uni32(j.decode_list[item]);
         rpgpu_batch_result* R = &j.batches[b];
         if (mode == 3) {

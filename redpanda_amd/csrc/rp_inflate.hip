@@ -1366,6 +1366,8 @@ DEV uint64_t xround(uint64_t acc, uint64_t in) { return xrotl(acc + in * kXP2, 3
 
 struct ZDev {
     InfIn in;
+    bool dirty;  // a match reached into the overwritten previous ring segment (zs::RingDirtyHook)
+    DEV void ring_dirty() { dirty = true; }
     inf_lds_u8* ring;
     uint8_t* dst;
     // output positions are 32-bit (SALU compares; the slot is < 2 GiB, and
@@ -1601,9 +1603,15 @@ struct ZDev {
     }
 };
 
+template <>
+struct zs::RingDirtyHook<ZDev> {
+    static constexpr bool value = true;
+};
+
 DEV ZDev zdev(const InfIn& in, uint8_t* lds, uint8_t* dst, uint64_t cap) {
     ZDev e;
     e.in = in;
+    e.dirty = false;
     e.ring = (inf_lds_u8*)lds;
     e.dst = dst;
     e.cap = cap < (1ull << 31) ? (uint32_t)cap : 0u;  // a slot past 2 GiB: count only (never one real batch)
@@ -1621,23 +1629,25 @@ DEV ZDev zdev(const InfIn& in, uint8_t* lds, uint8_t* dst, uint64_t cap) {
 
 // the scratch slot of the first pass: the first frame's content size when
 // its header carries one (exact for a one-frame payload), else 8 x the input
-DEV uint64_t zs_guess(InfIn& in) {
-    const uint64_t n = in.n;
+template <class Rd>
+DEV uint64_t zs_guess_at(uint64_t n, Rd byte) {
     uint64_t g = 8 * n + 4096;
-    if (n >= 6 && (inf_byte(in, 0) | (inf_byte(in, 1) << 8) | (inf_byte(in, 2) << 16) | (inf_byte(in, 3) << 24)) ==
-                      0xFD2FB528u) {
-        const uint32_t fhd = inf_byte(in, 4);
+    if (n >= 6 && (byte(0) | (byte(1) << 8) | (byte(2) << 16) | (byte(3) << 24)) == 0xFD2FB528u) {
+        const uint32_t fhd = byte(4);
         const uint32_t single = (fhd >> 5) & 1, fcsid = fhd >> 6, did = fhd & 3;
         const uint64_t at = 5 + (single ? 0 : 1) + (did == 3 ? 4 : did);
         const uint32_t sz = fcsid == 0 ? (single ? 1 : 0) : fcsid == 1 ? 2 : fcsid == 2 ? 4 : 8;
         if (sz && at + sz <= n) {
             uint64_t f = 0;
-            for (uint32_t k = 0; k < sz; k++) f |= (uint64_t)inf_byte(in, at + k) << (8 * k);
+            for (uint32_t k = 0; k < sz; k++) f |= (uint64_t)byte(at + k) << (8 * k);
             if (fcsid == 1) f += 256;
             if (f < (1ull << 32)) g = f + 64;
         }
     }
     return (g + 15) & ~15ull;
+}
+DEV uint64_t zs_guess(InfIn& in) {
+    return zs_guess_at(in.n, [&](uint64_t i) { return inf_byte(in, i); });
 }
 
 // ---------------------------------------------------------------------------
@@ -1691,6 +1701,7 @@ __device__ __noinline__ uint64_t zl_fill(const uint8_t* src, uint64_t n, inf_lds
 struct ZLane {
     const uint8_t* src;
     uint64_t n;
+    DEV void ring_dirty();  // (defined after `bad`: the wave decoder takes the member)
     uint8_t* lits;
     const ZsLitItem* items;  // the member's Huffman literal blocks k_zlits decoded ahead (k_zparse), in order
     uint32_t nitems, hidx;
@@ -1957,8 +1968,13 @@ struct ZLane {
             bool fail = (uint64_t)ll + ml > capb - bok;
             fail = fail || (uint64_t)ll > (uint64_t)L.size - usedk;
             fail = fail || myoff > fok - F.seg0 + F.prevlen;
-            fail = fail || (myoff > fok - F.seg0 && F.prevlen - (myoff - (fok - F.seg0)) < fok - F.seg0 + zs::kRingDirty);
-            if (__ballot(on && fail)) return false;
+            // a reach into the overwritten previous ring segment: the wave
+            // decoder (then the exact path) takes the member
+            const bool dirty = myoff > fok - F.seg0 && F.prevlen - (myoff - (fok - F.seg0)) < fok - F.seg0 + zs::kRingDirty;
+            if (__ballot(on && (fail || dirty))) {
+                if (__ballot(on && dirty)) bad = true;
+                return false;
+            }
             if (nrec + m > rcap) {
                 bad = true;
             } else if (on) {
@@ -2043,8 +2059,13 @@ struct ZLane {
     }
 };
 static_assert(ZLane::kZlWin * ZLane::kZlSlots <= kInfRing, "ZLane's stream windows use the ring's LDS");
+DEV void ZLane::ring_dirty() { bad = true; }
 template <>
 struct zs::EagerLits<ZLane> {
+    static constexpr bool value = true;
+};
+template <>
+struct zs::RingDirtyHook<ZLane> {
     static constexpr bool value = true;
 };
 template <>
@@ -2414,7 +2435,7 @@ DEV void zstd_first_item(const DeviceJob& j, uint8_t* lds, uint32_t i, uint32_t 
     InfIn in = inf_batch(j, R);
     uint64_t total = 0, soff = 0;
     int rc = -1;  // compressor::uncompress throws on an empty payload (compression/compression.cc:34-55)
-    bool again = true;
+    bool again = true, dirty = false;
     if (in.n) {
         const uint64_t guess = scratch_guess(j, zs_guess(in), in.n);
         soff = uni64(atomicAdd((unsigned long long*)j.inf_scratch_used, lane() == 0 ? (unsigned long long)guess : 0ull));
@@ -2427,6 +2448,7 @@ DEV void zstd_first_item(const DeviceJob& j, uint8_t* lds, uint32_t i, uint32_t 
         rc = zs::payload(e, T, in.n, total, unsure);
         e.flush_all();
         again = unsure || e.stored < total;
+        dirty = e.dirty;
 #ifdef RPGPU_ZSTAMPS
         if (lane() == 0) {
             for (int k = 0; k < 4; k++) atomicAdd(&g_zst[k], (unsigned long long)e.prof[k]);
@@ -2442,7 +2464,8 @@ DEV void zstd_first_item(const DeviceJob& j, uint8_t* lds, uint32_t i, uint32_t 
         const int32_t rcount = R->record_count;
         j.dcap[b] = cap;
         j.slots[b] = ((j.flags & RPGPU_JOB_PARSE) && rcount > 0 && (uint64_t)rcount <= cap) ? (uint64_t)rcount : 0;
-        j.inf_state[i] = rc != 0 ? 1u : again ? 2u : 0u;
+        j.inf_state[i] = dirty ? kZsExact : rc != 0 ? 1u : again ? 2u : 0u;
+        if (dirty) atomicAdd(&j.counters[27], 1u);
         j.inf_off[i] = soff;
         j.inf_total[i] = total;
     }
@@ -2461,6 +2484,380 @@ DEV void zstd_item(const DeviceJob& j, uint8_t* lds, rpgpu_batch_result* R, uint
         R->flags = R->flags | RPGPU_F_CODEC_OK;
         R->decoded_len = (uint32_t)total;
         R->reserved0 = 0;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// The exact path (round 6).  In libzstd's ring-buffer
+// mode a corrupt stream's match can reach past the window into the part of
+// the previous ring segment (the DCtx's extDict) that the current segment,
+// or the up-to-32-byte overcopy of its copies, has already written, and then
+// reads those newer bytes.  The fast decoders report such a member
+// (zs::RingDirtyHook: ZLane hands it to ZDev, ZDev marks it kZsExact) and
+// k_zexact decodes it again over ZExact: the same decoder (zs::payload, the
+// same acceptance rules) on one lane, with the DCtx's output buffer emulated
+// byte for byte in scratch memory -- every ZSTD_execSequence write as
+// libzstd 1.4.x performs it on x86-64 (ZSTD_copy16 of the literals and the
+// x86 ZSTD_wildcopy: one COPY16, then two per turn; ZSTD_overlapCopy8; the
+// extDict memmove; ZSTD_execSequenceEnd's safecopy within 32 bytes of the
+// buffer end; the literal buffer's padding: zeros, the RLE byte, or the
+// block's own bytes for raw literals read in place) -- so that such a match
+// reads what libzstd reads.  The emulation is pinned against libzstd on the
+// host by tests/test_zstd_core.py (tests/cpp/zstd_core_host.cpp ExactHostEnv,
+// the same writes).  Corrupt streams only: one wave takes these members one
+// after another.
+// ---------------------------------------------------------------------------
+constexpr uint64_t kZxBuf = zs::kStaticBuffers + 512;  // the DCtx's outBuff (its largest), + overcopy room
+constexpr uint64_t kZxBlk = zs::kBlockMax + 128;       // a block's literal buffer + its padding
+
+struct ZExact {
+    const uint8_t* src;
+    uint64_t n;
+    uint8_t* dst;                 // the member's output slot
+    uint64_t cap, out, fstart;    // slot bytes, output so far, the frame's first output byte
+    bool over;                    // the output outgrew the slot (counted on)
+    uint8_t* buf;                 // the emulated DCtx output buffer
+    uint64_t op, oend, prevlen;   // write position, buffer end, previous segment's length (extDict)
+    uint8_t* blk;                 // the block's literals, then the bytes a wildcopy reads past them
+    uint64_t blkn, took;
+
+    DEV uint32_t b(uint64_t i) { return i < n ? (uint32_t)src[i] : 0u; }
+    DEV uint64_t le(uint64_t i, uint32_t k) {
+        uint64_t v = 0;
+        for (uint32_t q = 0; q < k; q++) v |= (uint64_t)b(i + q) << (8 * q);
+        return v;
+    }
+    DEV uint64_t lb(zs::Bits&, uint64_t i) { return le(i, 8); }
+    DEV uint32_t U(uint32_t x) { return x; }
+    DEV zs::SeqSym sym(const zs::SeqSym& t) { return t; }
+    DEV void frame_begin() { fstart = out; }
+    // final bytes [a, a + k) of the buffer to the output
+    DEV void emit(uint64_t a, uint64_t k) {
+        for (uint64_t q = 0; q < k; q++)
+            if (out + q < cap) dst[out + q] = buf[a + q];
+        out += k;
+        if (out > cap) over = true;
+    }
+    // exact writes: raw / RLE blocks, the literals after the last sequence
+    DEV void raw(uint64_t pos, uint64_t k) {
+        for (uint64_t q = 0; q < k; q++) buf[op + q] = (uint8_t)b(pos + q);
+        emit(op, k);
+        op += k;
+    }
+    DEV void fill(uint32_t v, uint64_t k) {
+        for (uint64_t q = 0; q < k; q++) buf[op + q] = (uint8_t)v;
+        emit(op, k);
+        op += k;
+    }
+    DEV void lit(uint32_t v) { fill(v, 1); }
+    DEV void match(uint64_t, uint64_t) {}  // (ExactRing: exec_seq does the sequence's copies)
+    DEV void take(uint64_t k) {
+        for (uint64_t q = 0; q < k; q++) buf[op + q] = blk[took + q];
+        emit(op, k);
+        op += k;
+        took += k;
+    }
+    // zs::EagerLits: the block's literals in place before its sequences
+    DEV void raw_ahead(uint64_t pos, uint64_t k) {
+        for (uint64_t q = 0; q < k; q++) blk[q] = (uint8_t)b(pos + q);
+        blkn = k;
+        took = 0;
+    }
+    DEV void fill_ahead(uint32_t v, uint64_t k) {
+        for (uint64_t q = 0; q < k; q++) blk[q] = (uint8_t)v;
+        blkn = k;
+        took = 0;
+    }
+    DEV void huf_all(zs::Tabs* T, zs::Lits& L, uint32_t hlog) {
+        for (uint32_t k = 0; k < L.ns; k++) {
+            for (uint32_t i = 0; i < L.cnt[k]; i++)
+                blk[(uint64_t)k * L.seg + i] = (uint8_t)zs::huf_one(*this, T, L.s[k], L.pend[k], L.cnt[k] - i, L.x2, hlog);
+            L.dec[k] = L.cnt[k];
+        }
+        blkn = L.size;
+        took = 0;
+    }
+    // zs::ExactRing
+    DEV void ring_begin(uint64_t size) {
+        oend = size;
+        op = 0;
+        prevlen = 0;
+    }
+    DEV void ring_wrap() {
+        prevlen = op;
+        op = 0;
+    }
+    DEV void lit_pad(int mode, uint64_t pos, uint32_t rle) {
+        for (uint32_t q = 0; q < 64; q++) blk[blkn + q] = mode == 1 ? (uint8_t)b(pos + q) : mode == 2 ? (uint8_t)rle : 0;
+    }
+    // COPY16 / COPY8 (an SSE / 8-byte load, then the store)
+    DEV void copy_n(uint64_t d, uint64_t s, uint32_t k) {
+        uint8_t t[16];
+        for (uint32_t i = 0; i < k; i++) t[i] = buf[s + i];
+        for (uint32_t i = 0; i < k; i++) buf[d + i] = t[i];
+    }
+    DEV void wild_buf(uint64_t d, uint64_t s, int64_t length, bool overlap) {
+        const uint64_t e = d + (uint64_t)length;
+        if (overlap && d - s < 16) {
+            do { copy_n(d, s, 8); d += 8; s += 8; } while (d < e);
+            return;
+        }
+        copy_n(d, s, 16);
+        if (16 >= length) return;
+        d += 16;
+        s += 16;
+        do {
+            copy_n(d, s, 16); d += 16; s += 16;
+            copy_n(d, s, 16); d += 16; s += 16;
+        } while (d < e);
+    }
+    DEV void wild_lit(uint64_t d, uint64_t s, int64_t length) {
+        const uint64_t e = d + (uint64_t)length;
+        for (uint32_t i = 0; i < 16; i++) buf[d + i] = blk[s + i];
+        if (16 >= length) return;
+        d += 16;
+        s += 16;
+        do {
+            for (uint32_t i = 0; i < 32; i++) buf[d + i] = blk[s + i];
+            d += 32;
+            s += 32;
+        } while (d < e);
+    }
+    DEV void overlap8(uint64_t& d, uint64_t& s, uint64_t offset) {
+        if (offset < 8) {
+            const uint32_t dec32 = (0x44441210u >> (4 * offset)) & 15u;   // {0, 1, 2, 1, 4, 4, 4, 4}
+            const int32_t sub2 = (int32_t)((0xBA987888u >> (4 * offset)) & 15u);  // {8, 8, 8, 7, 8, 9, 10, 11}
+            buf[d] = buf[s];
+            buf[d + 1] = buf[s + 1];
+            buf[d + 2] = buf[s + 2];
+            buf[d + 3] = buf[s + 3];
+            s += dec32;
+            copy_n(d + 4, s, 4);
+            s -= (uint64_t)sub2;
+        } else {
+            copy_n(d, s, 8);
+        }
+        s += 8;
+        d += 8;
+    }
+    DEV void memmove_buf(uint64_t d, uint64_t s, uint64_t k) {
+        if (d <= s)
+            for (uint64_t q = 0; q < k; q++) buf[d + q] = buf[s + q];
+        else
+            for (uint64_t q = k; q-- > 0;) buf[d + q] = buf[s + q];
+    }
+    DEV void safecopy_buf(uint64_t d, uint64_t oend_w, uint64_t s, int64_t length) {
+        const uint64_t e = d + (uint64_t)length;
+        if (length < 8) {
+            while (d < e) buf[d++] = buf[s++];
+            return;
+        }
+        overlap8(d, s, d - s);
+        if (e <= oend_w) {
+            wild_buf(d, s, length, true);
+            return;
+        }
+        if (d <= oend_w) {
+            wild_buf(d, s, (int64_t)(oend_w - d), true);
+            s += oend_w - d;
+            d = oend_w;
+        }
+        while (d < e) buf[d++] = buf[s++];
+    }
+    DEV void safecopy_lit(uint64_t d, uint64_t oend_w, uint64_t s, int64_t length) {
+        const uint64_t e = d + (uint64_t)length;
+        if (length < 8) {
+            while (d < e) buf[d++] = blk[s++];
+            return;
+        }
+        if (e <= oend_w) {
+            wild_lit(d, s, length);
+            return;
+        }
+        if (d <= oend_w) {
+            wild_lit(d, s, (int64_t)(oend_w - d));
+            s += oend_w - d;
+            d = oend_w;
+        }
+        while (d < e) buf[d++] = blk[s++];
+    }
+    // ZSTD_execSequence / ZSTD_execSequenceEnd on the buffer (prefixStart 0,
+    // the extDict the previous segment's [0, prevlen) of the same buffer)
+    DEV void exec_seq(uint64_t ll, uint64_t off, uint64_t ml) {
+        const uint64_t o0 = op, oLitEnd = op + ll, oMatchEnd = oLitEnd + ml, oend_w = oend - 32;
+        const bool end_path = oMatchEnd > oend_w;
+        if (end_path) {
+            safecopy_lit(op, oend_w, took, (int64_t)ll);
+        } else {
+            for (uint32_t i = 0; i < 16; i++) buf[op + i] = blk[took + i];
+            if (ll > 16) wild_lit(op + 16, took + 16, (int64_t)ll - 16);
+        }
+        took += ll;
+        uint64_t d = oLitEnd, m = oLitEnd - off, rem = ml;
+        if (off > oLitEnd) {
+            m = prevlen - (off - oLitEnd);
+            if (m + ml <= prevlen) {
+                memmove_buf(oLitEnd, m, ml);
+                op = oMatchEnd;
+                emit(o0, ll + ml);
+                return;
+            }
+            const uint64_t len1 = prevlen - m;
+            memmove_buf(oLitEnd, m, len1);
+            d = oLitEnd + len1;
+            rem = ml - len1;
+            m = 0;
+        }
+        if (end_path) {
+            safecopy_buf(d, oend_w, m, (int64_t)rem);
+        } else if (off >= 16) {
+            wild_buf(d, m, (int64_t)rem, false);
+        } else {
+            overlap8(d, m, off);
+            if (rem > 8) wild_buf(d, m, (int64_t)rem - 8, true);
+        }
+        op = oMatchEnd;
+        emit(o0, ll + ml);
+    }
+    // the frame's XXH64 content checksum over its output (2: the output
+    // outgrew the slot, not checkable here)
+    DEV int check(uint32_t want) {
+        if (over) return 2;
+        const uint64_t len = out - fstart;
+        const uint8_t* p = dst + fstart;
+        uint64_t h, q = 0;
+        if (len >= 32) {
+            uint64_t v1 = kXP1 + kXP2, v2 = kXP2, v3 = 0, v4 = 0 - kXP1;
+            for (; q + 32 <= len; q += 32) {
+                uint64_t w[4];
+                for (int k = 0; k < 4; k++) {
+                    w[k] = 0;
+                    for (int t = 0; t < 8; t++) w[k] |= (uint64_t)p[q + 8 * k + t] << (8 * t);
+                }
+                v1 = xround(v1, w[0]);
+                v2 = xround(v2, w[1]);
+                v3 = xround(v3, w[2]);
+                v4 = xround(v4, w[3]);
+            }
+            h = xrotl(v1, 1) + xrotl(v2, 7) + xrotl(v3, 12) + xrotl(v4, 18);
+            h = (h ^ xround(0, v1)) * kXP1 + kXP4;
+            h = (h ^ xround(0, v2)) * kXP1 + kXP4;
+            h = (h ^ xround(0, v3)) * kXP1 + kXP4;
+            h = (h ^ xround(0, v4)) * kXP1 + kXP4;
+        } else {
+            h = kXP5;
+        }
+        h += len;
+        for (; q + 8 <= len; q += 8) {
+            uint64_t k = 0;
+            for (int t = 0; t < 8; t++) k |= (uint64_t)p[q + t] << (8 * t);
+            h ^= xround(0, k);
+            h = xrotl(h, 27) * kXP1 + kXP4;
+        }
+        if (q + 4 <= len) {
+            uint64_t k = 0;
+            for (int t = 0; t < 4; t++) k |= (uint64_t)p[q + t] << (8 * t);
+            h ^= k * kXP1;
+            h = xrotl(h, 23) * kXP2 + kXP3;
+            q += 4;
+        }
+        for (; q < len; q++) {
+            h ^= (uint64_t)p[q] * kXP5;
+            h = xrotl(h, 11) * kXP1;
+        }
+        h ^= h >> 33;
+        h *= kXP2;
+        h ^= h >> 29;
+        h *= kXP3;
+        h ^= h >> 32;
+        return (uint32_t)h == want ? 1 : 0;
+    }
+};
+template <>
+struct zs::EagerLits<ZExact> {
+    static constexpr bool value = true;
+};
+template <>
+struct zs::ExactRing<ZExact> {
+    static constexpr bool value = true;
+};
+
+// k_zexact: pass 0 (after the first pass, before the slot scans) decodes the
+// kZsExact members into scratch slots and sets their plan and state as
+// zstd_first_item does (kZsExactAgain instead of 2); pass 1 (after
+// k_members) decodes the kZsExactAgain ones into their arena slots.  One
+// wave, lane 0; the buffer and the literal buffer from the scratch pool.
+__global__ __launch_bounds__(64) void k_zexact(DeviceJob j, int pass) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t zlds[];
+    if (threadIdx.x != 0 || !j.inf_scratch || j.counters[27] == 0) return;
+    const uint32_t count = j.counters[16];
+    zs::Tabs* T = (zs::Tabs*)zlds;
+    uint8_t* work = nullptr;
+    for (uint32_t i = 0; i < count; i++) {
+        const uint32_t st = j.inf_state[i];
+        if (st != (pass == 0 ? kZsExact : kZsExactAgain)) continue;
+        const uint32_t b = j.inf_list[i];
+        rpgpu_batch_result* R = &j.batches[b];
+        const uint64_t S = j.seg_off[R->segment] + R->file_pos + RPGPU_HEADER_SIZE;
+        const uint64_t n = (uint64_t)(uint32_t)(R->size_bytes - (int32_t)RPGPU_HEADER_SIZE);
+        // the buffers: taken from the pool by the first pass, kept for the
+        // second ([31]: offset / 16 + 1, 0 while none)
+        if (!work && j.counters[31]) work = j.inf_scratch + 16ull * (j.counters[31] - 1);
+        if (!work && pass == 0) {
+            const uint64_t w = atomicAdd((unsigned long long*)j.inf_scratch_used, (unsigned long long)(kZxBuf + kZxBlk));
+            if (w + kZxBuf + kZxBlk <= j.inf_scratch_bytes) {
+                work = j.inf_scratch + w;
+                j.counters[31] = (uint32_t)(w >> 4) + 1;
+            }
+        }
+        ZExact e;
+        e.src = j.data + S;
+        e.n = n;
+        e.dst = nullptr;
+        e.out = e.fstart = 0;
+        e.over = false;
+        e.op = e.oend = e.prevlen = 0;
+        e.blkn = e.took = 0;
+        uint64_t soff = 0, cap = 0;
+        if (pass == 0) {
+            const uint64_t guess = scratch_guess(j, zs_guess_at(n, [&](uint64_t q) { return e.b(q); }), n);
+            soff = atomicAdd((unsigned long long*)j.inf_scratch_used, (unsigned long long)guess);
+            cap = soff + guess <= j.inf_scratch_bytes ? guess : 0;
+            e.dst = j.inf_scratch + soff;
+        } else {
+            const uint64_t dst = j.dcap[b];
+            cap = j.dcap[b + 1] - dst;
+            if (dst + cap > j.decoded_capacity) {
+                R->flags = R->flags | RPGPU_F_DECODE_OVERFLOW;
+                continue;
+            }
+            e.dst = j.decoded + dst;
+        }
+        e.cap = cap;
+        uint64_t total = 0;
+        bool unsure = false;
+        int rc = -1;
+        if (work && n) {
+            e.buf = work;
+            e.blk = work + kZxBuf;
+            rc = zs::payload(e, T, n, total, unsure);
+        }
+        // no scratch for the buffer (a pool too small for it): the member
+        // stays turned down, as the fast decoders left it
+        if (pass == 0) {
+            const bool again = unsure || e.over;
+            const uint64_t dcap = rc != 0 ? 0 : (total + 15) & ~15ull;
+            const int32_t rcount = R->record_count;
+            j.dcap[b] = dcap;
+            j.slots[b] = ((j.flags & RPGPU_JOB_PARSE) && rcount > 0 && (uint64_t)rcount <= dcap) ? (uint64_t)rcount : 0;
+            j.inf_state[i] = rc != 0 ? 1u : again ? kZsExactAgain : 0u;
+            j.inf_off[i] = soff;
+            j.inf_total[i] = total;
+        } else if (rc == 0 && !unsure && !e.over) {
+            R->flags = R->flags | RPGPU_F_CODEC_OK;
+            R->decoded_len = (uint32_t)total;
+            R->reserved0 = 0;
+        }
     }
 }
 
@@ -3237,6 +3634,16 @@ hipError_t launch_zfallback(const DeviceJob& j, hipStream_t s, uint32_t grid) {
         attr = true;
     }
     hipLaunchKernelGGL(k_zfallback, dim3(grid), dim3(64), kMemLds, s, j);
+    return hipGetLastError();
+}
+
+hipError_t launch_zexact(const DeviceJob& j, hipStream_t s, int pass) {
+    static bool attr = false;
+    if (!attr) {
+        (void)hipFuncSetAttribute((const void*)k_zexact, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kZsTabBytes);
+        attr = true;
+    }
+    hipLaunchKernelGGL(k_zexact, dim3(1), dim3(64), kZsTabBytes, s, j, pass);
     return hipGetLastError();
 }
 

@@ -173,6 +173,11 @@ struct ZsLitItem {
     uint32_t status;   // 0 not decoded, 1 decoded and every stream ended exactly, 2 decoded, a stream did not
 };
 constexpr uint32_t kZsPlanned = 5;  // inf_state: k_zplan sized and planned the member for k_zparse
+// inf_state: a zstd member whose decode reached into the overwritten part of
+// the previous ring segment (zs::RingDirtyHook): k_zexact decodes it over the
+// exact DCtx-buffer environment (first pass), and again into its arena slot
+// when it outgrew the scratch slot (kZsExactAgain)
+constexpr uint32_t kZsExact = 6, kZsExactAgain = 7;
 
 // one chunk of a large gzip member decoded on its own wave (rp_inflate.hip,
 // k_gzsplan / k_gzsfind / k_gzsdecode / k_gzsresolve)
@@ -241,7 +246,9 @@ struct DeviceJob {
                                   // k_gzsresolve claim cursors, [36..37] gzs_pool symbols used (u64),
                                   // [38] / [39] wlong_list count / cursor, [40] raw_list count, [41] lane_list count,
                                   // [42..43] frecs used (u64), [45] lzf_list count, [46] k_lzf_walk claim cursor,
-                                  // [47] lzf_tail count
+                                  // [47] lzf_tail count; [12] k_crc_compose claim cursor, [24..25] bytes
+                                  // k_raw_copy copied (u64), [44] k_decode_finish's checksummed-frame claim cursor,
+                                  // [27] zstd members for k_zexact, [31] k_zexact's buffers (pool offset / 16 + 1)
     uint32_t* decode_list;        // batch_capacity: ordinals of batches to uncompress
     uint32_t* seq_list;           // batch_capacity: decode items decoded whole by one lane
     uint32_t* link_list;          // batch_capacity: decode items whose linked LZ4F blocks one wave decodes in order
@@ -319,6 +326,9 @@ hipError_t launch_discover(const DeviceJob& j, hipStream_t s);
 hipError_t launch_resolve(const DeviceJob& j, hipStream_t s);
 hipError_t launch_emit(const DeviceJob& j, hipStream_t s);
 hipError_t launch_validate(const DeviceJob& j, hipStream_t s, uint32_t grid);  // rp_validate.hip
+bool dchain_wanted(const DeviceJob& j);                                         // rp_validate.hip
+hipError_t launch_dchain(const DeviceJob& j, hipStream_t s, uint32_t grid);
+hipError_t launch_validate_decoded(const DeviceJob& j, hipStream_t s, uint32_t grid);
 hipError_t launch_walk(const DeviceJob& j, hipStream_t s, uint32_t grid);
 hipError_t launch_decode(const DeviceJob& j, hipStream_t s, uint32_t grid);    // rp_codec.hip
 hipError_t launch_decode_blocks(const DeviceJob& j, hipStream_t s, uint32_t grid);
@@ -336,6 +346,7 @@ hipError_t launch_zplan(const DeviceJob& j, hipStream_t s, uint32_t grid);
 hipError_t launch_gzsplan(const DeviceJob& j, hipStream_t s);
 hipError_t launch_gzsplit(const DeviceJob& j, hipStream_t s, uint32_t grid);
 hipError_t launch_zfallback(const DeviceJob& j, hipStream_t s, uint32_t grid);
+hipError_t launch_zexact(const DeviceJob& j, hipStream_t s, int pass);  // rp_inflate.hip
 hipError_t launch_zstamps(hipStream_t s, int print);  // RPGPU_ZSTAMPS builds: reset / print the decoder stamps
 hipError_t launch_zexec(const DeviceJob& j, hipStream_t s);  // rp_codec.hip
 // one payload, one wave (rpgpu_uncompress); res[0] = rc (0 / -1 / -2), res[1] = out_len

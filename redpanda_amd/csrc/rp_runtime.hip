@@ -947,6 +947,9 @@ int submit_body(rpgpu_ctx* c, const rpgpu_job* job, hipStream_t s, int stop, Pla
             side_join.side = nullptr;  // joined
             STAGE("zfallback", launch_zfallback(j, s, c->cu_count * 4));
         }
+        // zstd members whose corrupt stream reads ring bytes the current
+        // segment has overwritten: decoded again over libzstd's exact buffer
+        STAGE("zexact", launch_zexact(j, s, 0));
         STAGE("zstamps", launch_zstamps(s, 1));
     }
     // zstd members (RPGPU_JOB_HOST_CODECS): decoded on the host now, sized
@@ -1035,6 +1038,7 @@ int submit_body(rpgpu_ctx* c, const rpgpu_job* job, hipStream_t s, int stop, Pla
         STAGE("decode_finish", launch_decode_finish(j, s, c->cu_count * 8));
         STAGE("inflate", launch_inflate(j, s, c->cu_count * 4));
         STAGE("zexec", launch_zexec(j, s));
+        STAGE("zexact", launch_zexact(j, s, 1));
         if (c->hc_n) STAGE("host_scatter", launch_host_scatter(j, (const HostItem*)c->hc_items.p, c->hc_n,
                                                                (const uint8_t*)c->hc_out.p, s));
     }
@@ -1042,6 +1046,12 @@ int submit_body(rpgpu_ctx* c, const rpgpu_job* job, hipStream_t s, int stop, Pla
     static const uint32_t walk_wgs = [] { const char* e = diag_env("RPGPU_WALK_WGS"); return e ? (uint32_t)atoi(e) : 8u; }();
     if (tm) HIPCHK(c, hipEventRecord(ev[3], s));
     STAGE("validate", launch_validate(j, s, c->cu_count));
+    // the decoded payloads' record chains, then their walk.  (k_dchain on the
+    // side stream beside k_crc_compose / k_validate measured slower than here:
+    // C2 validate stage 4.36 against 3.72 ms, the chains' serial loads
+    // queueing behind the two streams' HBM traffic)
+    STAGE("dchain", launch_dchain(j, s, c->cu_count));
+    STAGE("validate_decoded", launch_validate_decoded(j, s, c->cu_count));
     if (tm) HIPCHK(c, hipEventRecord(ev[4], s));
     STAGE("walk", launch_walk(j, s, c->cu_count * walk_wgs));
     if (tm) HIPCHK(c, hipEventRecord(ev[5], s));

@@ -801,10 +801,12 @@ DEV WalkResult walk_batch(const DeviceJob& j, const Desc& ds, const uint8_t* p0,
 // average; shorter records share lines, which the wave's scalar chain reads
 // at cache latency: C5's 100-byte records ran 3.6 -> 4.0 ms lane-chained)
 // and few enough for one lane's serial chain
-constexpr uint32_t kDchainMinRecBytes = 256, kDchainMaxRecs = 8192;
+constexpr uint32_t kDchainMinRecBytes = 256, kDchainMaxRecs = 1024;
 DEV bool dchain_ok(const DeviceJob& j, uint32_t flags, int32_t rc, uint64_t ib, uint64_t islots, uint32_t dlen) {
+    // (disk layout only: k_dchain runs beside k_validate, which sets the
+    // CRC_OK bit the wire layout's walk depends on)
     return j.dchain && (flags & RPGPU_F_CODEC_OK) && (j.flags & RPGPU_JOB_PARSE) &&
-           (j.layout != RPGPU_LAYOUT_WIRE || (flags & RPGPU_F_CRC_OK)) && rc > 0 && (uint64_t)rc <= islots &&
+           j.layout == RPGPU_LAYOUT_DISK && rc > 0 && (uint64_t)rc <= islots &&
            ib + islots <= j.record_capacity && (uint32_t)rc <= kDchainMaxRecs &&
            dlen >= kDchainMinRecBytes * (uint32_t)rc;
 }
@@ -1431,11 +1433,29 @@ DEV uint32_t wave_sum_u32(uint32_t v) {
 __global__ __launch_bounds__(1024) void k_crc_compose(DeviceJob j) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     const uint32_t count = j.counters[2];
-    if (count == 0 || j.counters[40] == 0) return;
+    // worth it only when raw blocks are most of the job's stored bytes (C2:
+    // 12 of 12.9 GB); otherwise k_validate streams every payload as before
+    // (C5, a few raw blocks among snappy and compressed LZ4: the kernel's
+    // pass over the decode list cost more than it saved)
+    const uint64_t raw_bytes = *(const volatile uint64_t*)(j.counters + 24);
+    if (count == 0 || j.counters[40] == 0 || 2 * raw_bytes < j.data_len) return;
     init_lds_tables(lds, j.tables);
     const Keys K = make_keys();
     const uint32_t l = lane_v(), c40 = uni32(j.tables->c40);
     auto gap = [&](uint64_t a, uint64_t e, uint32_t state) __attribute__((always_inline)) {
+        if (e - a <= 64) {
+            // a short gap (size words, checksums, the frame header): lane k
+            // holds byte k, folded in with uniform word / byte steps (a
+            // window here cost a load round trip and 16 rows of braids)
+            const uint32_t nb = (uint32_t)(e - a);
+            const uint32_t by = l < nb ? (uint32_t)j.data[a + l] : 0u;
+            uint32_t k = 0;
+            for (; k + 4 <= nb; k += 4)
+                state = uni32(word_step(lds, state, rl(by, (int)k) | (rl(by, (int)k + 1) << 8) |
+                                                        (rl(by, (int)k + 2) << 16) | (rl(by, (int)k + 3) << 24)));
+            for (; k < nb; k++) state = uni32(byte_step(lds, state, rl(by, (int)k)));
+            return state;
+        }
         const Stream st = make_stream(j.data, a, e);
         Win v;
         load_window(st, 0, v);
@@ -1865,10 +1885,23 @@ hipError_t launch_validate(const DeviceJob& j, hipStream_t s, uint32_t grid) {
         hipLaunchKernelGGL(k_crc_split, dim3(grid), dim3(64 * kVWaves), kLdsValidateBytes, s, j);
         hipLaunchKernelGGL(k_crc_combine, dim3((j.split_capacity + 3) / 4), dim3(256), 0, s, j);
     }
-    if ((j.flags & RPGPU_JOB_DECODE) && j.decoded) {
-        if (j.dchain && (j.flags & RPGPU_JOB_PARSE)) hipLaunchKernelGGL(k_dchain, dim3(grid * 8), dim3(256), 0, s, j);
+    return hipGetLastError();
+}
+
+// k_dchain: lanes with no payload exit at once; a grid of 2 workgroups per CU
+// covers C2's 31 K payloads in one pass
+bool dchain_wanted(const DeviceJob& j) {
+    return (j.flags & RPGPU_JOB_DECODE) && (j.flags & RPGPU_JOB_PARSE) && j.decoded && j.dchain &&
+           j.layout == RPGPU_LAYOUT_DISK;
+}
+hipError_t launch_dchain(const DeviceJob& j, hipStream_t s, uint32_t grid) {
+    if (dchain_wanted(j)) hipLaunchKernelGGL(k_dchain, dim3(grid * 2), dim3(256), 0, s, j);  // 8 waves per CU beside k_validate's 16
+    return hipGetLastError();
+}
+
+hipError_t launch_validate_decoded(const DeviceJob& j, hipStream_t s, uint32_t grid) {
+    if ((j.flags & RPGPU_JOB_DECODE) && j.decoded)
         hipLaunchKernelGGL(k_validate_decoded, dim3(grid), dim3(64 * kVWaves), kLdsValidateBytes, s, j);
-    }
     return hipGetLastError();
 }
 

@@ -23,15 +23,16 @@
 //     FSE_readNCount, ZSTD_buildFSETable, the sequence bit stream with
 //     BIT_DStream_t's exact reload / overflow behaviour, repeat offsets,
 //     sequence execution checks (capacity, literal overrun, reach).
-// One documented divergence (corrupt streams only), pinned as a reject rule:
-// in the ring-buffer mode (no content size, or larger than its window + 128
-// KiB) a match reaching past the window into the part of the previous ring
-// segment that the current segment (or the 32-byte overcopy of its copies)
-// has already overwritten reads those newer bytes in libzstd; here the
-// payload is rejected (block(): kRingDirty).  Sources further up the
-// previous segment still hold the true history in libzstd too, and decode
-// the same (tests/test_zstd_core.py::test_ring_mode_far_matches,
-// tests/test_gpu_parity.py::test_zstd_ring_mode_reject_rule).
+// Ring-buffer mode (no content size, or larger than its window + 128 KiB),
+// corrupt streams only: a match reaching past the window into the part of
+// the previous ring segment that the current segment (or the up-to-32-byte
+// overcopy of its copies) has already overwritten reads those newer bytes in
+// libzstd.  The fast environments report it (RingDirtyHook) and turn the
+// payload down; an ExactRing environment, which emulates the DCtx buffer
+// write for write (ZSTD_execSequence's copies as libzstd performs them),
+// decodes it as libzstd does (round 6; tests/test_zstd_core.py
+// ::test_ring_mode_far_matches, tests/test_gpu_parity.py
+// ::test_zstd_ring_mode_exact).  Until round 5 such payloads were rejected.
 #pragma once
 #include <stdint.h>
 
@@ -677,6 +678,29 @@ struct EagerSeqs {
     static constexpr bool value = false;
 };
 
+// An environment may emulate the DCtx's output buffer byte for byte (round
+// 6): every ZSTD_execSequence write as libzstd 1.4.x
+// performs it on x86-64 (literal copy16 / wildcopy with their overcopy,
+// the match's wildcopy / overlapCopy8 / extDict memmove, ZSTD_execSequenceEnd's
+// safecopy near the buffer end), so that a match reaching into the
+// previous ring segment where the current one has written (or overcopied)
+// reads what libzstd reads.  block() then hands each sequence to
+// E::exec_seq after the reference's checks (no ring rule), and payload()
+// tells the environment the buffer geometry (ring_begin, ring_wrap) and
+// each literal section's padding (lit_pad).
+template <class E>
+struct ExactRing {
+    static constexpr bool value = false;
+};
+// An environment that is told (E::ring_dirty) when a match of a
+// non-ExactRing decode reaches into the overwritten part of the previous ring
+// segment, just before the payload is turned down: the device then decodes
+// that payload again over an ExactRing environment (rp_inflate.hip k_zexact).
+template <class E>
+struct RingDirtyHook {
+    static constexpr bool value = false;
+};
+
 // ---------------------------------------------------------------------------
 // Frame state and one compressed block
 // ---------------------------------------------------------------------------
@@ -734,6 +758,14 @@ ZS_FN int64_t block(E& e, Tabs* T, Frame& F, uint64_t bp, uint64_t bn, uint64_t 
         if constexpr (EagerLits<E>::value) {
             if (L.kind == 0) e.raw_ahead(L.pos, lsz);
             else e.fill_ahead(L.rle, lsz);
+        }
+        // what a wildcopy reads past the literals (ZSTD_decodeLiteralsBlock):
+        // raw literals are read in place from the block unless they end
+        // within WILDCOPY_OVERLENGTH of it (then copied, zero padded); RLE
+        // literals are memset 32 bytes long
+        if constexpr (ExactRing<E>::value) {
+            if (L.kind == 0) e.lit_pad(lh + (uint64_t)lsz + kRingDirty > bn ? 0 : 1, L.pos + lsz, 0u);
+            else e.lit_pad(2, 0, L.rle);
         }
     } else {
         if (lt == 3 && !F.lit_ok) return -1;
@@ -800,6 +832,7 @@ ZS_FN int64_t block(E& e, Tabs* T, Frame& F, uint64_t bp, uint64_t bn, uint64_t 
         F.lit_ok = true;
         lcons = lh + lcs;
         if constexpr (EagerLits<E>::value) e.huf_all(T, L, F.hlog);
+        if constexpr (ExactRing<E>::value) e.lit_pad(0, 0, 0u);  // Huffman literals: zero padded
     }
     // sequences section header
     uint64_t sp = bp + lcons;
@@ -886,6 +919,17 @@ ZS_FN int64_t block(E& e, Tabs* T, Frame& F, uint64_t bp, uint64_t bn, uint64_t 
             // ZSTD_execSequence's checks, then the copies
             if (ll + ml > capb - bo) return -1;
             if (ll > (uint64_t)(L.size - L.used)) return -1;
+            if constexpr (ExactRing<E>::value) {
+                // the copies on the emulated buffer (reads past the window
+                // into the previous segment see what libzstd sees)
+                if (off > F.fo + ll - F.seg0 + F.prevlen) return -1;
+                e.exec_seq(ll, off, ml);
+                L.used += (uint32_t)ll;
+                bo += ll + ml;
+                F.fo += ll + ml;
+                if (--nseq == 0) break;
+                continue;
+            }
             if (ll) ZS_PROF(0, lits_emit(e, T, L, (uint32_t)ll, F.hlog));
             bo += ll;
             F.fo += ll;
@@ -898,7 +942,10 @@ ZS_FN int64_t block(E& e, Tabs* T, Frame& F, uint64_t bp, uint64_t bn, uint64_t 
             // streams only: a conforming encoder never reaches past its
             // window); sources further up the previous segment are the true
             // history, as here.
-            if (off > F.fo - F.seg0 && F.prevlen - (off - (F.fo - F.seg0)) < F.fo - F.seg0 + kRingDirty) return -1;
+            if (off > F.fo - F.seg0 && F.prevlen - (off - (F.fo - F.seg0)) < F.fo - F.seg0 + kRingDirty) {
+                if constexpr (RingDirtyHook<E>::value) e.ring_dirty();
+                return -1;
+            }
             ZS_PROF(1, e.match(off, ml));
             bo += ml;
             F.fo += ml;
@@ -1058,6 +1105,9 @@ ZS_FN int payload(E& e, Tabs* T, uint64_t n, uint64_t& total, bool& unsure) {
         F.llog = F.olog = F.mlog = F.hlog = 0;
         F.lit_ok = F.fse_ok = F.hx2 = false;
         e.frame_begin();
+        // the buffer the frame's blocks decode into: the caller's output room
+        // (single pass) or the DCtx's outBuff of `outbuf` bytes (streaming)
+        if constexpr (ExactRing<E>::value) e.ring_begin(sp ? room : outbuf);
         uint64_t ostart = 0;  // streaming: outStart in the DCtx's buffer
         bool empty_end = false;
         ip += hsize;
@@ -1124,6 +1174,7 @@ ZS_FN int payload(E& e, Tabs* T, uint64_t n, uint64_t& total, bool& unsure) {
                     ostart = 0;
                     F.prevlen = F.fo - F.seg0;
                     F.seg0 = F.fo;
+                    if constexpr (ExactRing<E>::value) e.ring_wrap();
                 }
             }
             if (last) break;

@@ -147,7 +147,190 @@ struct EagerHostEnv : HostEnv {
     }
 };
 
+// The DCtx's output buffer emulated byte for byte (rp::zs::ExactRing): what
+// libzstd's ZSTD_execSequence (x86-64, SSE2 COPY16) writes, overcopies
+// included, so that a match reaching into the previous ring segment where
+// the current one has written reads libzstd's bytes.  WILDCOPY_PAIRS selects
+// the x86 ZSTD_wildcopy loop shape (one COPY16, then two per iteration).
+#ifndef WILDCOPY_PAIRS
+#define WILDCOPY_PAIRS 1
+#endif
+struct ExactHostEnv : EagerHostEnv {
+    std::vector<uint8_t> buf;  // the DCtx's outBuff (or the caller's output room: single pass)
+    uint64_t op = 0, oend = 0;
+    std::vector<uint8_t> pad;  // bytes a wildcopy reads past the block's literals
+    uint8_t L(size_t i) const { return i < blk.size() ? blk[i] : pad[i - blk.size()]; }
+    void ring_begin(uint64_t size) {
+        oend = size;
+        if (buf.size() < size + 256) buf.resize(size + 256, 0);
+        op = 0;
+        prevlen = 0;
+    }
+    void ring_wrap() {
+        prevlen = op;
+        op = 0;
+    }
+    void lit_pad(int mode, uint64_t pos, uint32_t rle) {
+        pad.assign(64, 0);
+        if (mode == 1)
+            for (int i = 0; i < 64; i++) pad[i] = (pos + i < n) ? src[pos + i] : 0;
+        else if (mode == 2)
+            for (int i = 0; i < 64; i++) pad[i] = (uint8_t)rle;
+    }
+    void emit(uint64_t a, uint64_t k) { out.insert(out.end(), buf.begin() + a, buf.begin() + a + k); }
+    // exact writes (raw / RLE blocks, the last literals): memcpy / memset
+    void raw(uint64_t pos, uint64_t k) {
+        memcpy(&buf[op], src + pos, k);
+        emit(op, k);
+        op += k;
+    }
+    void fill(uint32_t v, uint64_t k) {
+        memset(&buf[op], (int)v, k);
+        emit(op, k);
+        op += k;
+    }
+    void take(uint64_t k) {
+        for (uint64_t i = 0; i < k; i++) buf[op + i] = L(took + i);
+        emit(op, k);
+        op += k;
+        took += k;
+    }
+    // COPY16 / COPY8: the whole source loaded, then stored
+    void copy_n(uint64_t d, uint64_t s, int k) {
+        uint8_t t[16];
+        for (int i = 0; i < k; i++) t[i] = buf[s + i];
+        for (int i = 0; i < k; i++) buf[d + i] = t[i];
+    }
+    // ZSTD_wildcopy from the output buffer (src_before_dst: overlap allowed)
+    void wild_buf(uint64_t d, uint64_t s, int64_t length, bool overlap) {
+        const uint64_t e = d + (uint64_t)length;
+        if (overlap && d - s < 16) {
+            do { copy_n(d, s, 8); d += 8; s += 8; } while (d < e);
+            return;
+        }
+#if WILDCOPY_PAIRS
+        copy_n(d, s, 16);
+        if (16 >= length) return;
+        d += 16; s += 16;
+        do { copy_n(d, s, 16); d += 16; s += 16; copy_n(d, s, 16); d += 16; s += 16; } while (d < e);
+#else
+        do { copy_n(d, s, 16); d += 16; s += 16; } while (d < e);
+#endif
+    }
+    // ZSTD_wildcopy from the literal buffer (no overlap)
+    void wild_lit(uint64_t d, size_t s, int64_t length) {
+        const uint64_t e = d + (uint64_t)length;
+#if WILDCOPY_PAIRS
+        for (int i = 0; i < 16; i++) buf[d + i] = L(s + i);
+        if (16 >= length) return;
+        d += 16; s += 16;
+        do {
+            for (int i = 0; i < 32; i++) buf[d + i] = L(s + i);
+            d += 32; s += 32;
+        } while (d < e);
+#else
+        do { for (int i = 0; i < 16; i++) buf[d + i] = L(s + i); d += 16; s += 16; } while (d < e);
+#endif
+    }
+    // ZSTD_overlapCopy8
+    void overlap8(uint64_t& d, uint64_t& s, uint64_t offset) {
+        if (offset < 8) {
+            static const uint32_t dec32[] = {0, 1, 2, 1, 4, 4, 4, 4};
+            static const int dec64[] = {8, 8, 8, 7, 8, 9, 10, 11};
+            const int sub2 = dec64[offset];
+            buf[d] = buf[s]; buf[d + 1] = buf[s + 1]; buf[d + 2] = buf[s + 2]; buf[d + 3] = buf[s + 3];
+            s += dec32[offset];
+            copy_n(d + 4, s, 4);
+            s -= sub2;
+        } else {
+            copy_n(d, s, 8);
+        }
+        s += 8;
+        d += 8;
+    }
+    void memmove_buf(uint64_t d, uint64_t s, uint64_t k) {
+        std::vector<uint8_t> t(buf.begin() + s, buf.begin() + s + k);
+        memcpy(&buf[d], t.data(), k);
+    }
+    // ZSTD_safecopy (near the buffer end)
+    void safecopy_buf(uint64_t d, uint64_t oend_w, uint64_t s, int64_t length) {
+        const uint64_t e = d + (uint64_t)length;
+        if (length < 8) { while (d < e) buf[d++] = buf[s++]; return; }
+        overlap8(d, s, d - s);
+        if (e <= oend_w) { wild_buf(d, s, length, true); return; }
+        if (d <= oend_w) { wild_buf(d, s, (int64_t)(oend_w - d), true); s += oend_w - d; d = oend_w; }
+        while (d < e) buf[d++] = buf[s++];
+    }
+    void safecopy_lit(uint64_t d, uint64_t oend_w, size_t s, int64_t length) {
+        const uint64_t e = d + (uint64_t)length;
+        if (length < 8) { while (d < e) buf[d++] = L(s++); return; }
+        if (e <= oend_w) { wild_lit(d, s, length); return; }
+        if (d <= oend_w) { wild_lit(d, s, (int64_t)(oend_w - d)); s += oend_w - d; d = oend_w; }
+        while (d < e) buf[d++] = L(s++);
+    }
+    // ZSTD_execSequence / ZSTD_execSequenceEnd; prefixStart = 0, the
+    // previous segment (extDict) = [0, prevlen) of the same buffer
+    uint64_t prevlen = 0;
+    void exec_seq(uint64_t ll, uint64_t off, uint64_t ml) {
+        const uint64_t o0 = op, oLitEnd = op + ll, oMatchEnd = oLitEnd + ml, oend_w = oend - 32;
+        const bool end_path = oMatchEnd > oend_w;
+        if (end_path) safecopy_lit(op, oend_w, took, (int64_t)ll);
+        else {
+            for (int i = 0; i < 16; i++) buf[op + i] = L(took + i);
+            if (ll > 16) wild_lit(op + 16, took + 16, (int64_t)ll - 16);
+        }
+        took += ll;
+        uint64_t d = oLitEnd, m = oLitEnd - off, rem = ml;
+        if (off > oLitEnd) {  // extDict: the previous segment's place in the buffer
+            m = prevlen - (off - oLitEnd);
+            if (m + ml <= prevlen) {
+                memmove_buf(oLitEnd, m, ml);
+                op = oMatchEnd;
+                emit(o0, ll + ml);
+                return;
+            }
+            const uint64_t len1 = prevlen - m;
+            memmove_buf(oLitEnd, m, len1);
+            d = oLitEnd + len1;
+            rem = ml - len1;
+            m = 0;
+        }
+        if (end_path) safecopy_buf(d, oend_w, m, (int64_t)rem);
+        else if (off >= 16) wild_buf(d, m, (int64_t)rem, false);
+        else {
+            overlap8(d, m, off);
+            if (rem > 8) wild_buf(d, m, (int64_t)rem - 8, true);
+        }
+        op = oMatchEnd;
+        emit(o0, ll + ml);
+    }
+};
+
 }  // namespace
+
+template <>
+struct rp::zs::EagerLits<ExactHostEnv> {
+    static constexpr bool value = true;
+};
+template <>
+struct rp::zs::ExactRing<ExactHostEnv> {
+    static constexpr bool value = true;
+};
+
+extern "C" int zs_host_decode_exact(const uint8_t* src, uint64_t n, uint8_t* dst, uint64_t cap, uint64_t* total) {
+    static rp::zs::Tabs T;
+    ExactHostEnv e;
+    e.src = src;
+    e.n = n;
+    e.T = &T;
+    uint64_t t = 0;
+    bool unsure = false;
+    const int rc = n == 0 ? -1 : rp::zs::payload(e, &T, n, t, unsure);
+    *total = rc == 0 ? t : 0;
+    if (rc == 0 && t > e.out.size()) return -9;
+    if (rc == 0) memcpy(dst, e.out.data(), t < cap ? t : cap);
+    return rc;
+}
 
 template <>
 struct rp::zs::EagerLits<EagerHostEnv> {

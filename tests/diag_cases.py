@@ -123,7 +123,30 @@ def case_small_frec():
     print(f"small_frec ok: {len(got.batches)} batches, {int(np.sum(ok))} decoded")
 
 
-CASES = {"small_pool": case_small_pool, "host_codec_missing": case_host_codec_missing, "small_frec": case_small_frec}
+def case_zstd_ring_wave():
+    """RPGPU_ZS_FAST=0: every zstd member through the wave decoder (ZDev, no
+    lane parser), so the ring-mode members it turns down reach k_zexact from
+    k_members_first rather than from k_zfallback; libzstd's bytes either way."""
+    import random
+    from oracle import oracle as O
+    from redpanda_amd.engine import Engine
+    from tests import zstd_corpus as ZC
+    from tests.test_gpu_parity import _zstd_batches, assert_same, run_both
+    assert os.environ.get("RPGPU_ZS_FAST") == "0"
+    O.build()
+    eng = Engine(0)
+    rng = random.Random(7)
+    frames = ZC.ring_frames(rng, 80)
+    pay = [f for _, f in frames] + ZC.mutations(rng, frames[:10], per=3)
+    got, ref = run_both(eng, O, [_zstd_batches(pay, counts=[1] * len(pay))], flags=DFLAGS)
+    ok = (ref.batches["flags"] & abi.F_CODEC_OK) != 0
+    assert int(np.sum(ok)) >= 40, int(np.sum(ok))
+    assert_same(got, ref, DFLAGS)
+    print(f"zstd_ring_wave ok: {len(got.batches)} batches, {int(np.sum(ok))} decoded")
+
+
+CASES = {"small_pool": case_small_pool, "host_codec_missing": case_host_codec_missing, "small_frec": case_small_frec,
+         "zstd_ring_wave": case_zstd_ring_wave}
 
 if __name__ == "__main__":
     CASES[sys.argv[1]]()

@@ -1,7 +1,8 @@
 """GPU cases run on the diagnostic library variant in a child process
 (tests/diag_cases.py): the gzip / zstd first-pass pool exhausted by hostile
 ISIZE trailers, RPGPU_JOB_HOST_CODECS without a loadable libzstd, and the
-LZ4 fast-path record pool cut so that listed and walked blocks mix."""
+LZ4 fast-path record pool cut so that listed and walked blocks mix, zstd
+ring-mode members through the wave decoder alone."""
 import os
 import subprocess
 import sys
@@ -35,3 +36,7 @@ def test_lz4_fast_pool_exhausted(cap):
     """a fast-path record pool too small for the job's
     LZ4 blocks (none / a few groups / most of them listed)."""
     assert "small_frec ok" in _run("small_frec", RPGPU_FREC_CAP=cap)
+
+
+def test_zstd_ring_exact_wave_decoder():
+    assert "zstd_ring_wave ok" in _run("zstd_ring_wave", RPGPU_ZS_FAST="0")

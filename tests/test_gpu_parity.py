@@ -753,29 +753,28 @@ def test_zstd_members_corpus(engine, oracle):
     assert_same(got, ref, DFLAGS)
 
 
-def test_zstd_ring_mode_reject_rule(engine, oracle):
-    """The documented zstd divergence pinned on the device (rp_zstd_core.h,
-    kRingDirty; tests/test_zstd_core.py pins it on the host): a ring-buffer
-    mode match into the part of the previous ring segment that the current
-    segment has overwritten reads newer bytes in libzstd; the device rejects
-    the payload, exactly where the host build of the same decoder does.  Every
-    other payload -- far matches into the untouched previous segment included
-    -- decodes to libzstd's bytes, flags and decoded crcs."""
+def test_zstd_ring_mode_exact(engine, oracle):
+    """zstd's ring-buffer mode on the device, libzstd's bytes everywhere: a
+    match into the part of the previous ring segment that the current
+    segment (or the overcopy of its copies) has overwritten reads those newer
+    bytes in libzstd; the fast decoders hand such a member to k_zexact, which
+    decodes it again over libzstd's output buffer emulated byte for byte
+    (rp_inflate.hip ZExact; tests/test_zstd_core.py pins the same emulation on
+    the host).  Ring frames that take that path and ones that do not, plus
+    their mutations: flags, decoded bytes and crcs, index and walk as the
+    oracle's."""
     import random
     from redpanda_amd import build as B
     from tests import zstd_corpus as ZC
     from tests.test_zstd_core import load_host
     host = load_host(B.build_zstd_host())
-    pay = [f for _, f in ZC.ring_frames(random.Random(7), 120)]
+    rng = random.Random(7)
+    frames = ZC.ring_frames(rng, 120)
+    pay = [f for _, f in frames]
     div = np.array([host(p) is None and ZC.ref_decode(p) is not None for p in pay])
     assert int(np.sum(div)) >= 10 and int(np.sum(~div)) >= 10
-    got, ref = run_both(engine, oracle, [_zstd_batches(pay, counts=[1] * len(pay))], flags=DFLAGS)
-    gb, rb = got.batches, ref.batches
-    assert len(gb) == len(rb) == len(pay)
-    assert np.all((gb["flags"][div] & abi.F_CODEC_OK) == 0) and np.all((rb["flags"][div] & abi.F_CODEC_OK) != 0)
-    for f in ("flags", "crc_computed", "header_crc_computed", "decoded_len", "decoded_crc", "decoded_header_crc",
-              "records_parsed", "parse_err"):
-        np.testing.assert_array_equal(gb[f][~div], rb[f][~div], err_msg=f)
-    for i in np.nonzero(~div & ((rb["flags"] & abi.F_CODEC_OK) != 0))[0]:
-        go, ro, n = int(gb["decoded_off"][i]), int(rb["decoded_off"][i]), int(rb["decoded_len"][i])
-        assert bytes(got.decoded[go:go + n]) == bytes(ref.decoded[ro:ro + n]), i
+    mutated = ZC.mutations(rng, frames[:30], per=3)
+    got, ref = run_both(engine, oracle, [_zstd_batches(pay, counts=[1] * len(pay)),
+                                         _zstd_batches(mutated, counts=[1] * len(mutated))], flags=DFLAGS)
+    assert np.all((got.batches["flags"][: len(pay)][div] & abi.F_CODEC_OK) != 0)
+    assert_same(got, ref, DFLAGS)

@@ -18,13 +18,14 @@ from tests import zstd_corpus as Z
 HERE = os.path.dirname(os.path.abspath(__file__))
 
 
-def load_host(path: str, eager: bool = False):
+def load_host(path: str, eager: bool = False, exact: bool = False):
     """decode(payload) -> bytes or None (rejected) through the host build of
     rp_zstd_core.h (redpanda_amd.build.build_zstd_host); eager: with every
     block's Huffman literals decoded before its sequences (zs::EagerLits, the
-    device lane parser's order)."""
+    device lane parser's order); exact: over the emulated DCtx output buffer
+    (zs::ExactRing, the device's k_zexact)."""
     L = C.CDLL(path)
-    fn = L.zs_host_decode_eager if eager else L.zs_host_decode
+    fn = L.zs_host_decode_exact if exact else L.zs_host_decode_eager if eager else L.zs_host_decode
     fn.argtypes = [C.c_char_p, C.c_uint64, C.c_void_p, C.c_uint64, C.POINTER(C.c_uint64)]
     L.zs_host_xxh64.argtypes = [C.c_char_p, C.c_uint64]
     L.zs_host_xxh64.restype = C.c_uint64
@@ -103,13 +104,13 @@ def test_core_edge_frames(host):
 
 
 def test_ring_mode_far_matches(host):
-    """The one documented divergence from libzstd, pinned as a reject rule
-    (rp_zstd_core.h, kRingDirty): in the ring-buffer mode a match reaching
-    into the previous ring segment where the current segment (or the 32-byte
-    overcopy of its copies) has already written reads those newer bytes in
-    libzstd; the engine rejects such a frame.  Everywhere else the output is
-    libzstd's, far matches into the untouched part of the previous segment
-    included."""
+    """The fast decoders' hand-off rule (rp_zstd_core.h, kRingDirty): in the
+    ring-buffer mode a match reaching into the previous ring segment where the
+    current segment (or the 32-byte overcopy of its copies) has already
+    written reads those newer bytes in libzstd; the plain environment turns
+    such a frame down (the device then decodes it again over the exact buffer,
+    test_ring_mode_exact).  Everywhere else the output is libzstd's, far
+    matches into the untouched part of the previous segment included."""
     rng = random.Random(7)
     same = rejected = 0
     for data, f in Z.ring_frames(rng, 300):
@@ -136,3 +137,38 @@ def test_eager_literals_match_libzstd_loop(seed):
         assert eager(f) == Z.ref_decode(f)
     bad = [c[:24].hex() for c in Z.mutations(rng, frames) if eager(c) != Z.ref_decode(c)]
     assert not bad, (len(bad), bad[:4])
+
+
+@pytest.fixture(scope="module")
+def exact():
+    from redpanda_amd import build as B
+    return load_host(B.build_zstd_host(), exact=True)
+
+
+def test_ring_mode_exact(exact):
+    """zs::ExactRing (the device's k_zexact): the DCtx's output buffer emulated
+    byte for byte, libzstd 1.4.x's x86-64 execSequence writes and overcopies
+    included, so that the far matches the plain environment turns down read
+    what libzstd reads: libzstd's accept / reject and bytes on every frame."""
+    rng = random.Random(7)
+    frames = Z.ring_frames(rng, 300)
+    accepted = 0
+    for data, f in frames:
+        ref = Z.ref_decode(f)
+        assert exact(f) == ref, f[:16].hex()
+        accepted += ref is not None
+    assert accepted >= 80, accepted
+
+
+@pytest.mark.parametrize("seed", [8, 9])
+def test_exact_matches_libzstd_loop(exact, seed):
+    """The exact environment on the ordinary frames and their mutations (raw,
+    RLE and Huffman literals, single-pass and streaming frames, the end-of-
+    buffer safecopy path): the same accept / reject and bytes as libzstd."""
+    rng = random.Random(seed)
+    frames = Z.random_frames(rng, 40)
+    for data, f in frames:
+        assert exact(f) == Z.ref_decode(f)
+    cases = Z.mutations(rng, frames) + [m for data, f in Z.ring_frames(rng, 20) for m in Z.mutations(rng, [(data, f)])]
+    bad = [c[:24].hex() for c in cases if exact(c) != Z.ref_decode(c)]
+    assert not bad, (len(bad), len(cases), bad[:4])
