@@ -1323,6 +1323,7 @@ constexpr uint32_t kBig = kXRing >= 32768 ? 128 : 64;
 // and the loads they wait on are counted exactly (gfx9's vmcnt also counts
 // stores)
 constexpr uint32_t kFlushLag = kXRing >= 65536 ? (24u << 10) : kXRing / 4;
+
 // a batch overwrites ring slots up to 128 kBig bytes behind the front, and
 // its far matches read up to kBig bytes past (front - ring): both must lie
 // below the flushed position; xbig's far reads need ring >= lag + 2 KiB + 64
@@ -1522,11 +1523,13 @@ DEV uint32_t wave_scan(uint32_t v) {
 
 // one lane's match: ml bytes at d from d - off (every source byte final or
 // this match's own earlier output)
-// RPGPU_XMATCH_BATCH (experiment builds): 1 = a non-overlapping match's
-// source loaded whole before its stores (1632 VGPR spills: C2 decode 26 ->
-// 47 ms); 2 = far sources two 16-byte loads at a time
+// RPGPU_XMATCH_BATCH: 3 (default) = a source that does not overlap its
+// destination read 32 bytes at a time, both reads before the stores (C2
+// decode 24.4 -> 23.9 ms); 0 = 16 bytes at a time; experiment builds: 1 = a
+// non-overlapping match's source loaded whole before its stores (1632 VGPR
+// spills: C2 decode 26 -> 47 ms); 2 = far sources two 16-byte loads at a time
 #ifndef RPGPU_XMATCH_BATCH
-#define RPGPU_XMATCH_BATCH 0
+#define RPGPU_XMATCH_BATCH 3
 #endif
 DEV void xmatch(XRing& x, uint32_t d, uint32_t off, uint32_t ml, bool far) {
     const uint32_t s = d - off;
@@ -1617,16 +1620,49 @@ DEV void xmatch(XRing& x, uint32_t d, uint32_t off, uint32_t ml, bool far) {
 }
 
 // a lane's literal bytes (up to kBig), loaded a window ahead of its batch:
-// every load of a batch is then in flight before the batch starts
+// every load of a batch is then in flight before the batch starts.
+// The loads are unconditional and land straight in the registers the batch
+// reads (no select or copy after them: a value moved or masked right after
+// its load makes the compiler wait for that load there, which drained the
+// prefetch).  A chunk that would read past the job's data (the stream's
+// last 16 bytes) is loaded from 16 bytes before that end instead and
+// shifted into place once it has arrived (lit_fix): sh packs each chunk's
+// shift, 4 bits per chunk.  Reads start at most 16 bytes before the stream
+// (s.p - 16 lies inside the job's data: a payload follows its 61-byte
+// header).
 struct Lit {
     uint4 v[kBig / 16];
+    uint32_t sh;
 };
 DEV Lit lit_load(const Src& s, const SeqRec& r) {
     Lit L;
+    L.sh = 0;
+    const int64_t top = s.rl - 16;
 #pragma unroll
-    for (uint32_t k = 0; k < kBig / 16; k++)
-        L.v[k] = (r.ll > 16 * k && r.ll <= kBig) ? ld16(s, (int64_t)r.lip + 16 * k) : make_uint4(0, 0, 0, 0);
+    for (uint32_t k = 0; k < kBig / 16; k++) {
+        const bool want = r.ll > 16 * k && r.ll <= kBig;
+        const int64_t q = (int64_t)r.lip + 16 * k;
+        const int64_t a = want ? (q < top ? q : top) : (top < 0 ? top : 0);
+        L.sh |= (uint32_t)(want ? q - a : 0) << (4 * k);
+        L.v[k] = gld16(s.p + a);
+    }
     return L;
+}
+// bytes [sh, 16) of v to [0, 16 - sh)
+DEV uint4 shr16(const uint4& v, uint32_t sh) {
+    const uint32_t d = sh >> 2, b = sh & 3;
+    return make_uint4(__builtin_amdgcn_alignbyte(dw(v, d + 1), dw(v, d), b),
+                      __builtin_amdgcn_alignbyte(dw(v, d + 2), dw(v, d + 1), b),
+                      __builtin_amdgcn_alignbyte(dw(v, d + 3), dw(v, d + 2), b),
+                      __builtin_amdgcn_alignbyte(dw(v, d + 4), dw(v, d + 3), b));
+}
+DEV void lit_fix(Lit& L) {
+    if (!__ballot(L.sh != 0)) return;
+#pragma unroll
+    for (uint32_t k = 0; k < kBig / 16; k++) {
+        const uint32_t sh = (L.sh >> (4 * k)) & 15u;
+        if (sh) L.v[k] = shr16(L.v[k], sh);
+    }
 }
 
 // the records of lanes [lo, hi) (none longer than kBig); lit = each lane's
@@ -1688,7 +1724,11 @@ DEV void xbatch(XRing& x, const Src& s, const SeqRec& r, uint32_t lo, uint32_t h
 #endif
         const int first = __builtin_ctzll(pm);
         const uint32_t f = rl(d, first);
+#if defined(RPGPU_XABL) && RPGPU_XABL == 4
+        const bool ready = pend;  // ablation (diagnostic build only): every match in one round, no dependencies
+#else
         const bool ready = pend && (src + r.ml <= f || l == (uint32_t)first);
+#endif
         if (ready) xmatch(x, d, r.off, r.ml, far);
         pend = pend && !ready;
     }
@@ -1696,7 +1736,6 @@ DEV void xbatch(XRing& x, const Src& s, const SeqRec& r, uint32_t lo, uint32_t h
     const uint64_t c3 = __builtin_amdgcn_s_memtime();
 #endif
     x.op = hi;
-    if (x.op - x.flushed > kFlushLag) xflush_chunks(x);
 #ifdef RPGPU_DSTAMPS
     const uint64_t c4 = __builtin_amdgcn_s_memtime();
     // accumulated per piece, added to g_dst once per piece (ds_flush): an
@@ -1767,19 +1806,43 @@ DEV void xbig(XRing& x, const Src& s, uint32_t lip, uint32_t ll, uint32_t ml, ui
     if (x.op - x.flushed > kFlushLag) xflush_chunks(x);
 }
 
-DEV SeqRec rec_at(const SeqRec* recs, uint32_t k, uint32_t cnt) {
-    SeqRec r{0, 0, 0, 0};
-    if (k < cnt) r = recs[k];
-    return r;
-}
+// Record sources of the window pipeline: load(k) reads record k (an index
+// past the end reads record 0: unconditional, see Lit) and unpack() makes
+// it a SeqRec once it has arrived (zero for an index past the end).
+struct SeqRecs {  // k_lz_walk's 16-byte records
+    const SeqRec* recs;
+    typedef SeqRec Raw;
+    DEV Raw load(uint32_t k, uint32_t cnt) const { return recs[k < cnt ? k : 0u]; }
+    DEV SeqRec unpack(const Raw& v, bool ok) const {
+        return ok ? v : SeqRec{0u, 0u, 0u, 0u};
+    }
+};
+struct FRecs {  // k_lzf_walk's 8-byte records {lip | ll << 16, ml | off << 16}
+    const uint2* recs;
+    typedef uint2 Raw;
+    DEV Raw load(uint32_t k, uint32_t cnt) const { return recs[k < cnt ? k : 0u]; }
+    DEV SeqRec unpack(const Raw& v, bool ok) const {
+        return ok ? SeqRec{v.x & 0xFFFFu, v.x >> 16, v.y & 0xFFFFu, v.y >> 16} : SeqRec{0u, 0u, 0u, 0u};
+    }
+};
 
 // records [0, cnt) in windows of 64 (lane k = record 64 w + k): records are
 // loaded two windows ahead and literal heads one window ahead, so the
 // global-load latency hides behind the previous window's LDS work; a record
-// longer than kBig splits its window and runs alone
-DEV void xrecords(XRing& x, const Src& s, const SeqRec* recs, uint32_t cnt) {
+// longer than kBig splits its window and runs alone.  The window's deferred
+// flush is issued at its top, before its prefetch loads: the waits the
+// register rotation needs at the window's end then find the stores and the
+// loads a window old.
+#ifndef RPGPU_XSPLIT
+#define RPGPU_XSPLIT 1
+#endif
+template <class RS>
+DEV void xwindows(XRing& x, const Src& s, const RS& rs, uint32_t cnt) {
+    if (cnt == 0) return;
     const uint32_t l = lane();
-    SeqRec r0 = rec_at(recs, l, cnt), r1 = rec_at(recs, 64 + l, cnt);
+    typename RS::Raw q0 = rs.load(l, cnt), q1 = rs.load(64 + l, cnt);
+    SeqRec r1 = rs.unpack(q1, 64 + l < cnt);
+    SeqRec r0 = rs.unpack(q0, l < cnt);
     Lit lit0 = lit_load(s, r0);
     // vmcnt drains in issue order: once a batch has waited for its records
     // (loaded two windows back), every flush issued before that load is
@@ -1788,69 +1851,34 @@ DEV void xrecords(XRing& x, const Src& s, const SeqRec* recs, uint32_t cnt) {
     for (uint32_t b = 0; b < cnt; b += 64) {
         x.safe = fh1 > x.safe ? fh1 : x.safe;
         fh1 = fh0;
-        fh0 = x.flushed;
-        const SeqRec r2 = rec_at(recs, b + 128 + l, cnt);
+        if (x.op - x.flushed > kFlushLag) xflush_chunks(x);
+        fh0 = x.flushed;  // (stores issued before this window's record loads)
+        const typename RS::Raw q2 = rs.load(b + 128 + l, cnt);
         const Lit lit1 = lit_load(s, r1);
-        const uint32_t n = cnt - b < 64 ? cnt - b : 64;
-        const uint64_t bigm = __ballot(l < n && (r0.ll > kBig || r0.ml > kBig));
-        uint32_t lo = 0;
-        for (;;) {
-            const uint64_t bm = bigm & (~0ull << lo);
-            const uint32_t e = bm ? (uint32_t)__builtin_ctzll(bm) : n;
-            if (e > lo) xbatch(x, s, r0, lo, e, lit0);
-            if (!bm) break;
-            xbig(x, s, rl(r0.lip, (int)e), rl(r0.ll, (int)e), rl(r0.ml, (int)e), rl(r0.off, (int)e));
-            lo = e + 1;
-            if (lo >= n) break;
-        }
-        r0 = r1;
-        r1 = r2;
-        lit0 = lit1;
-    }
-}
-
-// k_lzf_walk's 8-byte records {lip | ll << 16, ml | off << 16}
-DEV SeqRec frec_at(const uint2* recs, uint32_t k, uint32_t cnt) {
-    SeqRec r{0u, 0u, 0u, 0u};
-    if (k < cnt) {
-        const uint2 v = recs[k];
-        r.lip = v.x & 0xFFFFu;
-        r.ll = v.x >> 16;
-        r.ml = v.y & 0xFFFFu;
-        r.off = v.y >> 16;
-    }
-    return r;
-}
-
-// xrecords over 8-byte records
-DEV void frecords(XRing& x, const Src& s, const uint2* recs, uint32_t cnt) {
-    const uint32_t l = lane();
-    SeqRec r0 = frec_at(recs, l, cnt), r1 = frec_at(recs, 64 + l, cnt);
-    Lit lit0 = lit_load(s, r0);
-    uint32_t fh0 = x.safe, fh1 = x.safe;
-    for (uint32_t b = 0; b < cnt; b += 64) {
-        x.safe = fh1 > x.safe ? fh1 : x.safe;
-        fh1 = fh0;
-        fh0 = x.flushed;
-        const SeqRec r2 = frec_at(recs, b + 128 + l, cnt);
-        const Lit lit1 = lit_load(s, r1);
+        lit_fix(lit0);
         const uint32_t nb = cnt - b < 64 ? cnt - b : 64;
         const uint64_t bigm = __ballot(l < nb && (r0.ll > kBig || r0.ml > kBig));
-        uint32_t lo = 0;
-        for (;;) {
-            const uint64_t bm = bigm & (~0ull << lo);
-            const uint32_t e = bm ? (uint32_t)__builtin_ctzll(bm) : nb;
-            if (e > lo) xbatch(x, s, r0, lo, e, lit0);
-            if (!bm) break;
-            xbig(x, s, rl(r0.lip, (int)e), rl(r0.ll, (int)e), rl(r0.ml, (int)e), rl(r0.off, (int)e));
-            lo = e + 1;
-            if (lo >= nb) break;
+        if (RPGPU_XSPLIT && !bigm) {
+            xbatch(x, s, r0, 0, nb, lit0);
+        } else {
+            uint32_t lo = 0;
+            for (;;) {
+                const uint64_t bm = bigm & (~0ull << lo);
+                const uint32_t e = bm ? (uint32_t)__builtin_ctzll(bm) : nb;
+                if (e > lo) xbatch(x, s, r0, lo, e, lit0);
+                if (!bm) break;
+                xbig(x, s, rl(r0.lip, (int)e), rl(r0.ll, (int)e), rl(r0.ml, (int)e), rl(r0.off, (int)e));
+                lo = e + 1;
+                if (lo >= nb) break;
+            }
         }
         r0 = r1;
-        r1 = r2;
+        r1 = rs.unpack(q2, b + 128 + l < cnt);
         lit0 = lit1;
     }
 }
+DEV void xrecords(XRing& x, const Src& s, const SeqRec* recs, uint32_t cnt) { xwindows(x, s, SeqRecs{recs}, cnt); }
+DEV void frecords(XRing& x, const Src& s, const uint2* recs, uint32_t cnt) { xwindows(x, s, FRecs{recs}, cnt); }
 
 // raw bytes straight from the stream to the arena (an independent raw
 // block): 16 bytes per lane, U KiB per step (U loads in flight per lane)
