@@ -271,11 +271,14 @@ DEV uint32_t xxh32_wave(const uint8_t* p, uint64_t n, uint32_t seed, lds_u8* buf
     uint32_t h;
     if (ns) {
         uint32_t acc = l == 0 ? seed + P1 + P2 : l == 1 ? seed + P2 : l == 2 ? seed : seed - P1;
-        uint4 q = l < ns ? gld16(p + 16 * (uint64_t)l) : make_uint4(0, 0, 0, 0);
+        // the row loads are unconditional (a lane past the end reads stripe
+        // 0 again, unused): a select right after a load made the compiler
+        // wait for it there, so the next row was never in flight
+        uint4 q = gld16(p + 16 * (uint64_t)(l < ns ? l : 0u));
         lds_u32* w = (lds_u32*)buf;
         for (uint64_t r = 0; r < ns; r += 64) {
             const uint64_t k = r + 64 + l;
-            const uint4 nq = k < ns ? gld16(p + 16 * k) : make_uint4(0, 0, 0, 0);
+            const uint4 nq = gld16(p + 16 * (k < ns ? k : 0ull));
             w[4 * l] = q.x;
             w[4 * l + 1] = q.y;
             w[4 * l + 2] = q.z;

@@ -189,8 +189,13 @@ DEV uint32_t scan_step(uint32_t layout, const uint8_t* __restrict__ seg, const S
 // runs of tens of spent chunks between two entries (up to ~150 at 16 KiB),
 // each carried by one k_chain lane at ~0.6 header hops per chunk.  (32 KiB:
 // C2 discover 3.0 ms, a 32-chunk carry limit made k_resolve re-walk the
-// rest of the longer runs serially, 0.86 ms.)
-constexpr uint64_t kScanBudget = 16u << 10;
+// rest of the longer runs serially, 0.86 ms.  Round 6, 16 -> 8 KiB: C2
+// discover 1.79 -> 1.28 ms, C5 0.90 -> 0.77 ms, C1 unchanged; 4 KiB: C2 1.17,
+// C5 0.82 ms.)
+#ifndef RPGPU_SCAN_BUDGET_KIB
+#define RPGPU_SCAN_BUDGET_KIB 8
+#endif
+constexpr uint64_t kScanBudget = (uint64_t)RPGPU_SCAN_BUDGET_KIB << 10;
 constexpr uint64_t kExhausted = kNone - 1;
 // chunks one k_chain lane carries its chain through: unbounded in practice
 // (a run is as long as the gap between two entries); the serial cost is the
