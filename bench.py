@@ -460,6 +460,11 @@ def run_compressed(name, kw, n_parts, seg_bytes, args, plat, eng, abi, desc, ext
         "partitions": n_parts,
         "segment_bytes": seg_bytes,
         "stored_bytes": stored,
+        "generated_bytes": int(offs[-1]),
+        "generated_batches": int(sum(counts)),
+        "reachable_note": "stored_bytes / batches count the batches the parser chain reaches; a chain ends at an "
+                          "injected header fault (storage/parser.cc semantics), so generated bytes past it are "
+                          "not batches" if int(sum(counts)) != n_batches else "every generated batch is reached",
         "decoded_bytes": decoded,
         "batches": n_batches,
         "records": n_rec,

@@ -2520,6 +2520,9 @@ struct ZExact {
     uint64_t op, oend, prevlen;   // write position, buffer end, previous segment's length (extDict)
     uint8_t* blk;                 // the block's literals, then the bytes a wildcopy reads past them
     uint64_t blkn, took;
+#ifdef RPGPU_ZSTAMPS
+    uint64_t prof[4];
+#endif
 
     DEV uint32_t b(uint64_t i) { return i < n ? (uint32_t)src[i] : 0u; }
     DEV uint64_t le(uint64_t i, uint32_t k) {
