@@ -929,7 +929,14 @@ typedef __attribute__((address_space(3))) uint16_t gzs_lds_u16;
 // the chunk's ring holds its last 8 K symbols (16 KiB of LDS, so eight waves
 // share a CU); a match from farther back reads the chunk's region in the pool
 // (its flushed symbols) or, before the chunk's start, is a placeholder
-constexpr uint32_t kGzsRing = 8192, kGzsMask = kGzsRing - 1;
+#ifndef RPGPU_GZS_RING
+#define RPGPU_GZS_RING 8192
+#endif
+#ifndef RPGPU_GZS_WGS
+#define RPGPU_GZS_WGS 8  // k_gzsdecode workgroups (one wave) per CU
+#endif
+constexpr uint32_t kGzsRing = RPGPU_GZS_RING, kGzsMask = kGzsRing - 1;
+static_assert((kGzsRing & kGzsMask) == 0 && kGzsRing >= 2048, "split-decode ring: a power of two >= 2 K symbols");
 constexpr uint32_t kGzsLds = 2 * kGzsRing + kInfTabBytes;
 
 struct GzsOut {
@@ -3593,7 +3600,7 @@ hipError_t launch_gzsplit(const DeviceJob& j, hipStream_t s, uint32_t grid) {
         attr = true;
     }
     hipLaunchKernelGGL(k_gzsfind, dim3(grid * 5), dim3(64), kGzsFindLds, s, j);
-    hipLaunchKernelGGL(k_gzsdecode, dim3(grid * 8), dim3(64), kGzsLds, s, j);
+    hipLaunchKernelGGL(k_gzsdecode, dim3(grid * RPGPU_GZS_WGS), dim3(64), kGzsLds, s, j);
     hipLaunchKernelGGL(k_gzsresolve, dim3(grid * 2), dim3(256), 0, s, j);
     return hipGetLastError();
 }
