@@ -926,11 +926,13 @@ constexpr int kBufFlagsZs = 0x00020000;  // buffer resource word 3 (raw, 32-bit 
 DEV void zs_wait_vm() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 constexpr int kZsSc1 = 16;  // cache policy sc1: L2-coherent, bypasses the vector L1
 typedef __attribute__((address_space(3))) uint16_t gzs_lds_u16;
-// the chunk's ring holds its last 8 K symbols (16 KiB of LDS, so eight waves
-// share a CU); a match from farther back reads the chunk's region in the pool
-// (its flushed symbols) or, before the chunk's start, is a placeholder
+// the chunk's ring holds its last 4 K symbols (8 KiB of LDS: eight 12 KiB
+// workgroups leave a CU ~64 KiB for the zstd kernels beside them; an 8 K
+// ring filled the CU, C6 resolve+plan 64.4 -> 60.3 ms); a match from farther
+// back reads the chunk's region in the pool (its flushed symbols) or, before
+// the chunk's start, is a placeholder
 #ifndef RPGPU_GZS_RING
-#define RPGPU_GZS_RING 8192
+#define RPGPU_GZS_RING 4096
 #endif
 #ifndef RPGPU_GZS_WGS
 #define RPGPU_GZS_WGS 8  // k_gzsdecode workgroups (one wave) per CU
