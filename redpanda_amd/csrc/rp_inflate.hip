@@ -2885,7 +2885,11 @@ __global__ __launch_bounds__(64) void k_zexact(DeviceJob j, int pass) {
 // ---------------------------------------------------------------------------
 constexpr uint32_t kMemLds = kZsLds > kInfLdsDecode ? kZsLds : kInfLdsDecode;
 
-__global__ __launch_bounds__(64) void k_members_first(DeviceJob j) {
+// pass 0: every member the split decode did not close (after it); with the
+// split decode, pass 1 takes the members it never planned (small, FHCRC)
+// beside it on another stream, and pass 2 after it the planned ones whose
+// chain did not close
+__global__ __launch_bounds__(64) void k_members_first(DeviceJob j, int pass) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     InfTabs* T = (InfTabs*)(lds + kInfRing);
     const InfWave W = inf_wave();
@@ -2895,13 +2899,16 @@ __global__ __launch_bounds__(64) void k_members_first(DeviceJob j) {
     // would set the pass's tail): members of >= 128 KiB stored, then the rest
     for (uint32_t phase = 0; phase < 2; phase++) {
         for (;;) {
-            const uint32_t i = wave_fetch_add(&j.counters[phase ? 20 : 17], 1u);
+            const uint32_t i = wave_fetch_add(&j.counters[pass == 2 ? (phase ? 49 : 48) : (phase ? 20 : 17)], 1u);
             if (i >= count) break;
             const uint32_t b = uni32(j.inf_list[i]);
             const rpgpu_batch_result* R = &j.batches[b];
             const bool big = uni32((uint32_t)R->size_bytes) >= (128u << 10);
             if (big != (phase == 0)) continue;
-            if (j.gzs_mem && (uni32(j.gzs_mem[2 * i + 1]) >> 31)) continue;  // the split decode closed it
+            const uint32_t gm = j.gzs_mem ? uni32(j.gzs_mem[2 * i + 1]) : 0u;
+            if (gm >> 31) continue;  // the split decode closed it
+            if (pass == 1 && gm != 0) continue;  // planned: after the split decode
+            if (pass == 2 && gm == 0) continue;  // done by pass 1
             if ((uni32((uint32_t)(uint16_t)R->attrs) & 7u) == RPGPU_CODEC_GZIP) {
                 if (!tab) inf_load_tab(T->crc_tab);
                 tab = true;
@@ -3607,13 +3614,13 @@ hipError_t launch_gzsplit(const DeviceJob& j, hipStream_t s, uint32_t grid) {
     return hipGetLastError();
 }
 
-hipError_t launch_inflate_plan(const DeviceJob& j, hipStream_t s, uint32_t grid) {
+hipError_t launch_inflate_plan(const DeviceJob& j, hipStream_t s, uint32_t grid, int pass) {
     static bool attr = false;
     if (!attr) {
         (void)hipFuncSetAttribute((const void*)k_members_first, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kMemLds);
         attr = true;
     }
-    hipLaunchKernelGGL(k_members_first, dim3(grid), dim3(64), kMemLds, s, j);
+    hipLaunchKernelGGL(k_members_first, dim3(grid), dim3(64), kMemLds, s, j, pass);
     return hipGetLastError();
 }
 

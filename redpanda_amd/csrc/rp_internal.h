@@ -204,7 +204,7 @@ constexpr uint64_t kGzsChunk = RPGPU_GZS_CHUNK;  // deflate bytes per chunk
 constexpr uint32_t kGzsMaxK = 256;     // chunks per member at most
 
 // job counters (DeviceJob::counters), zeroed per submit
-constexpr size_t kCounterBytes = 192;
+constexpr size_t kCounterBytes = 256;
 
 struct DeviceJob {
     const uint8_t* data;
@@ -248,7 +248,8 @@ struct DeviceJob {
                                   // [42..43] frecs used (u64), [45] lzf_list count, [46] k_lzf_walk claim cursor,
                                   // [47] lzf_tail count; [12] k_crc_compose claim cursor, [24..25] bytes
                                   // k_raw_copy copied (u64), [44] k_decode_finish's checksummed-frame claim cursor,
-                                  // [27] zstd members for k_zexact, [31] k_zexact's buffers (pool offset / 16 + 1)
+                                  // [27] zstd members for k_zexact, [31] k_zexact's buffers (pool offset / 16 + 1),
+                                  // [48] / [49] k_members_first's claim cursors of its pass 2
     uint32_t* decode_list;        // batch_capacity: ordinals of batches to uncompress
     uint32_t* seq_list;           // batch_capacity: decode items decoded whole by one lane
     uint32_t* link_list;          // batch_capacity: decode items whose linked LZ4F blocks one wave decodes in order
@@ -339,7 +340,7 @@ hipError_t launch_lzf_walk(const DeviceJob& j, hipStream_t s, uint32_t cus);
 hipError_t launch_decode_finish(const DeviceJob& j, hipStream_t s, uint32_t grid);
 // gzip members (rp_inflate.hip): first pass (into scratch) before the slot
 // scans, then the copy into the arena and the second pass where needed
-hipError_t launch_inflate_plan(const DeviceJob& j, hipStream_t s, uint32_t grid);
+hipError_t launch_inflate_plan(const DeviceJob& j, hipStream_t s, uint32_t grid, int pass = 0);
 hipError_t launch_inflate(const DeviceJob& j, hipStream_t s, uint32_t grid);
 hipError_t launch_zparse(const DeviceJob& j, hipStream_t s, uint32_t grid);
 hipError_t launch_zplan(const DeviceJob& j, hipStream_t s, uint32_t grid);

@@ -160,8 +160,9 @@ struct rpgpu_ctx {
     // slot scans
     hipStream_t side = nullptr;
     hipEvent_t fork_ev = nullptr, join_ev = nullptr;
-    hipStream_t side2 = nullptr;  // k_raw_copy beside k_lzf_walk and k_lz_walk
-    hipEvent_t join2_ev = nullptr;
+    hipStream_t side2 = nullptr;  // k_raw_copy beside k_lzf_walk and k_lz_walk; the gzip members
+                                  // the split decode does not plan, beside it
+    hipEvent_t join2_ev = nullptr, mfork_ev = nullptr, mjoin_ev = nullptr;
     struct HostSlot {
         uint8_t* d_data = nullptr;
         uint64_t data_bytes = 0;
@@ -343,6 +344,8 @@ int rpgpu_destroy(rpgpu_ctx* c) {
     if (c->join_ev) (void)hipEventDestroy(c->join_ev);
     if (c->side2) { (void)hipStreamSynchronize(c->side2); (void)hipStreamDestroy(c->side2); }
     if (c->join2_ev) (void)hipEventDestroy(c->join2_ev);
+    if (c->mfork_ev) (void)hipEventDestroy(c->mfork_ev);
+    if (c->mjoin_ev) (void)hipEventDestroy(c->mjoin_ev);
     for (auto& set : c->ev_sets)
         for (auto& e : set) hipEventDestroy(e);
     if (c->stream) hipStreamDestroy(c->stream);
@@ -939,9 +942,39 @@ int submit_body(rpgpu_ctx* c, const rpgpu_job* job, hipStream_t s, int stop, Pla
         // the rest and over the members the split decode did not close
         if (j.gzs_mem) {
             STAGE("gzsplan", launch_gzsplan(j, s));
+            // the members it did not plan (below 16 KiB stored, FHCRC: one
+            // wave each) beside the split decode, on the raw-copy stream
+            // (idle until the decode stage), the rest after it.  RPGPU_MEM_SIDE=0
+            // (diagnostic build): all after it (A/B)
+            static const bool mem_side = [] { const char* e = diag_env("RPGPU_MEM_SIDE"); return !(e && *e == '0'); }();
+            struct MemJoin {
+                hipStream_t s = nullptr, side = nullptr;
+                hipEvent_t ev = nullptr;
+                ~MemJoin() {
+                    if (side && hipEventRecord(ev, side) == hipSuccess) hipStreamWaitEvent(s, ev, 0);
+                }
+            } mem_join;
+            if (mem_side) {
+                if (!c->side2) HIPCHK(c, side_stream_create(&c->side2));
+                if (!c->mfork_ev) HIPCHK(c, hipEventCreateWithFlags(&c->mfork_ev, hipEventDisableTiming));
+                if (!c->mjoin_ev) HIPCHK(c, hipEventCreateWithFlags(&c->mjoin_ev, hipEventDisableTiming));
+                HIPCHK(c, hipEventRecord(c->mfork_ev, s));
+                HIPCHK(c, hipStreamWaitEvent(c->side2, c->mfork_ev, 0));
+                mem_join.s = s;
+                mem_join.ev = c->mjoin_ev;
+                mem_join.side = c->side2;
+                STAGE("inflate_plan", launch_inflate_plan(j, c->side2, c->cu_count * 4, 1));
+                HIPCHK(c, hipEventRecord(c->mjoin_ev, c->side2));
+            }
             STAGE("gzsplit", launch_gzsplit(j, s, c->cu_count));
+            STAGE("inflate_plan", launch_inflate_plan(j, s, c->cu_count * 4, mem_side ? 2 : 0));
+            if (mem_side) {
+                HIPCHK(c, hipStreamWaitEvent(s, c->mjoin_ev, 0));
+                mem_join.side = nullptr;  // joined
+            }
+        } else {
+            STAGE("inflate_plan", launch_inflate_plan(j, s, c->cu_count * 4));
         }
-        STAGE("inflate_plan", launch_inflate_plan(j, s, c->cu_count * 4));
         if (split) {
             HIPCHK(c, hipStreamWaitEvent(s, c->join_ev, 0));
             side_join.side = nullptr;  // joined
