@@ -279,10 +279,13 @@ DEV uint32_t xxh32_wave(const uint8_t* p, uint64_t n, uint32_t seed, lds_u8* buf
         for (uint64_t r = 0; r < ns; r += 64) {
             const uint64_t k = r + 64 + l;
             const uint4 nq = gld16(p + 16 * (k < ns ? k : 0ull));
-            w[4 * l] = q.x;
-            w[4 * l + 1] = q.y;
-            w[4 * l + 2] = q.z;
-            w[4 * l + 3] = q.w;
+            // each stripe word's product with P2 by its own lane (a wave
+            // instruction for 64 stripes): the four serial chains below are
+            // then add, rotate and one multiply per stripe
+            w[4 * l] = q.x * P2;
+            w[4 * l + 1] = q.y * P2;
+            w[4 * l + 2] = q.z * P2;
+            w[4 * l + 3] = q.w * P2;
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
             const uint32_t cnt = ns - r < 64 ? (uint32_t)(ns - r) : 64u;
             if (l < 4) {
@@ -292,9 +295,9 @@ DEV uint32_t xxh32_wave(const uint8_t* p, uint64_t n, uint32_t seed, lds_u8* buf
 #pragma unroll
                     for (int u = 0; u < 8; u++) x[u] = w[4 * (i + u) + l];
 #pragma unroll
-                    for (int u = 0; u < 8; u++) acc = rotl32(acc + x[u] * P2, 13) * P1;
+                    for (int u = 0; u < 8; u++) acc = rotl32(acc + x[u], 13) * P1;
                 }
-                for (; i < cnt; i++) acc = rotl32(acc + w[4 * i + l] * P2, 13) * P1;
+                for (; i < cnt; i++) acc = rotl32(acc + w[4 * i + l], 13) * P1;
             }
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
             q = nq;
