@@ -3601,16 +3601,18 @@ hipError_t launch_gzsplan(const DeviceJob& j, hipStream_t s) {
     return hipGetLastError();
 }
 
-hipError_t launch_gzsplit(const DeviceJob& j, hipStream_t s, uint32_t grid) {
+hipError_t launch_gzsplit(const DeviceJob& j, hipStream_t s, uint32_t grid, int part) {
     static bool attr = false;
     if (!attr) {
         (void)hipFuncSetAttribute((const void*)k_gzsdecode, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kGzsLds);
         (void)hipFuncSetAttribute((const void*)k_gzsfind, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kGzsFindLds);
         attr = true;
     }
-    hipLaunchKernelGGL(k_gzsfind, dim3(grid * 5), dim3(64), kGzsFindLds, s, j);
-    hipLaunchKernelGGL(k_gzsdecode, dim3(grid * RPGPU_GZS_WGS), dim3(64), kGzsLds, s, j);
-    hipLaunchKernelGGL(k_gzsresolve, dim3(grid * 2), dim3(256), 0, s, j);
+    if (part != 2) hipLaunchKernelGGL(k_gzsfind, dim3(grid * 5), dim3(64), kGzsFindLds, s, j);
+    if (part != 1) {
+        hipLaunchKernelGGL(k_gzsdecode, dim3(grid * RPGPU_GZS_WGS), dim3(64), kGzsLds, s, j);
+        hipLaunchKernelGGL(k_gzsresolve, dim3(grid * 2), dim3(256), 0, s, j);
+    }
     return hipGetLastError();
 }
 

@@ -345,7 +345,7 @@ hipError_t launch_inflate(const DeviceJob& j, hipStream_t s, uint32_t grid);
 hipError_t launch_zparse(const DeviceJob& j, hipStream_t s, uint32_t grid);
 hipError_t launch_zplan(const DeviceJob& j, hipStream_t s, uint32_t grid);
 hipError_t launch_gzsplan(const DeviceJob& j, hipStream_t s);
-hipError_t launch_gzsplit(const DeviceJob& j, hipStream_t s, uint32_t grid);
+hipError_t launch_gzsplit(const DeviceJob& j, hipStream_t s, uint32_t grid, int part = 0);  // part 1: find, 2: decode + resolve, 0: all
 hipError_t launch_zfallback(const DeviceJob& j, hipStream_t s, uint32_t grid);
 hipError_t launch_zexact(const DeviceJob& j, hipStream_t s, int pass);  // rp_inflate.hip
 hipError_t launch_zstamps(hipStream_t s, int print);  // RPGPU_ZSTAMPS builds: reset / print the decoder stamps

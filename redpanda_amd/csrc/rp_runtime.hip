@@ -943,10 +943,13 @@ int submit_body(rpgpu_ctx* c, const rpgpu_job* job, hipStream_t s, int stop, Pla
         if (j.gzs_mem) {
             STAGE("gzsplan", launch_gzsplan(j, s));
             // the members it did not plan (below 16 KiB stored, FHCRC: one
-            // wave each) beside the split decode, on the raw-copy stream
-            // (idle until the decode stage), the rest after it.  RPGPU_MEM_SIDE=0
-            // (diagnostic build): all after it (A/B)
-            static const bool mem_side = [] { const char* e = diag_env("RPGPU_MEM_SIDE"); return !(e && *e == '0'); }();
+            // wave each) beside the split decode's k_gzsdecode, on the
+            // raw-copy stream (idle until the decode stage), the rest after
+            // it.  (Forked before k_gzsfind instead, they slowed it 14.3 ->
+            // 19.9 ms: C6 resolve+plan 58.9 against 56.7 ms.)  Diagnostic build:
+            // RPGPU_MEM_SIDE=0 all after the split decode, 1 forked before k_gzsfind
+            static const int mem_side = [] { const char* e = diag_env("RPGPU_MEM_SIDE"); return e ? atoi(e) : 2; }();
+            if (mem_side == 2) STAGE("gzsfind", launch_gzsplit(j, s, c->cu_count, 1));
             struct MemJoin {
                 hipStream_t s = nullptr, side = nullptr;
                 hipEvent_t ev = nullptr;
@@ -966,7 +969,7 @@ int submit_body(rpgpu_ctx* c, const rpgpu_job* job, hipStream_t s, int stop, Pla
                 STAGE("inflate_plan", launch_inflate_plan(j, c->side2, c->cu_count * 4, 1));
                 HIPCHK(c, hipEventRecord(c->mjoin_ev, c->side2));
             }
-            STAGE("gzsplit", launch_gzsplit(j, s, c->cu_count));
+            STAGE("gzsplit", launch_gzsplit(j, s, c->cu_count, mem_side == 2 ? 2 : 0));
             STAGE("inflate_plan", launch_inflate_plan(j, s, c->cu_count * 4, mem_side ? 2 : 0));
             if (mem_side) {
                 HIPCHK(c, hipStreamWaitEvent(s, c->mjoin_ev, 0));
