@@ -1264,7 +1264,7 @@ __global__ __launch_bounds__(256) void k_decode(DeviceJob j) {
         const uint64_t cap = uni64(j.dcap[b + 1]) - doff;
         FramePlan fp;
         fp.mode = 0;
-        fp.first = fp.nb = fp.ccs = fp.ccs_val = fp.csf = 0;
+        fp.first = fp.nb = fp.ccs = fp.ccs_val = fp.csf = fp.xxh = fp.pad = 0;
         fp.content_size = 0;
         if (doff + cap > j.decoded_capacity) {
             fp.mode = 3;  // no room: DECODE_OVERFLOW
@@ -2985,7 +2985,12 @@ __global__ __launch_bounds__(256) void k_decode_blocks(DeviceJob j) {
 // when an earlier one came out short (ascending 1 KiB steps, each loaded
 // whole before it is stored: safe for any gap), content size / checksum
 // checked
-__global__ __launch_bounds__(256) void k_decode_finish(DeviceJob j) {
+// defer (round 6): the content checksum of a frame whose pieces all came out
+// where the planner put them (no move) is k_content_xxh's, which runs beside
+// this kernel from k_lz_exec's end; such a frame gets its verdict here as if
+// it matched, and k_content_apply takes it back after the join if it did not.
+// A frame whose pieces move is hashed here, after its move, as without defer.
+__global__ __launch_bounds__(256) void k_decode_finish(DeviceJob j, int defer) {
     __shared__ __attribute__((aligned(16))) uint8_t xb[4][1024];
     lds_u8* xbuf = (lds_u8*)xb[threadIdx.x >> 6];
     const uint32_t count = j.counters[2];
@@ -2996,13 +3001,13 @@ __global__ __launch_bounds__(256) void k_decode_finish(DeviceJob j) {
     // and all start at once; the rest after them (counters[14]).  (In item
     // order a wave could meet two 1 MiB checksummed frames in a row: C2's
     // k_decode_finish 2.5-3.1 ms.)
-    for (uint32_t phase = 0; phase < 2; phase++)
+    for (uint32_t phase = defer ? 1u : 0u; phase < 2; phase++)
     for (;;) {
         const uint32_t item = wave_fetch_add(&j.counters[phase == 0 ? 44 : 14], 1u);
         if (item >= count) break;
         const uint32_t mode = uni32(j.plans[item].mode);
         const bool xxh_first = mode == 1 && uni32(j.plans[item].ccs) != 0;
-        if (xxh_first != (phase == 0)) continue;
+        if (!defer && xxh_first != (phase == 0)) continue;
         const uint32_t b = uni32(j.decode_list[item]);
         rpgpu_batch_result* R = &j.batches[b];
         if (mode == 3) {
@@ -3012,7 +3017,7 @@ __global__ __launch_bounds__(256) void k_decode_finish(DeviceJob j) {
         if (mode == 0) continue;
         const uint32_t first = uni32(j.plans[item].first), nb = uni32(j.plans[item].nb);
         const uint64_t d0 = uni64(j.dcap[b]);
-        bool ok = true;
+        bool ok = true, moved = false;
         uint64_t run = d0;  // where the next piece belongs
         for (uint32_t k = 0; k < nb; k++) {
             const int32_t out = (int32_t)uni32((uint32_t)j.blocks[first + k].out);
@@ -3020,6 +3025,7 @@ __global__ __launch_bounds__(256) void k_decode_finish(DeviceJob j) {
             const uint64_t at = uni64(j.blocks[first + k].dst);
             if (at < run) { ok = false; break; }  // a piece longer than planned (cannot happen: out <= cap)
             if (at != run) {
+                moved = true;
                 uint8_t* dd = j.decoded;
                 for (uint32_t o = 0; o < (uint32_t)out; o += 1024) {
                     const uint32_t c = o + 16 * l;
@@ -3039,7 +3045,8 @@ __global__ __launch_bounds__(256) void k_decode_finish(DeviceJob j) {
         const uint64_t total = run - d0;
         if (ok && mode == 1) {
             if (uni32(j.plans[item].csf) && total != uni64(j.plans[item].content_size)) ok = false;  // frameSize_wrong
-            if (ok && uni32(j.plans[item].ccs) && xxh32_wave(j.decoded + d0, total, 0, xbuf) != uni32(j.plans[item].ccs_val))
+            if (ok && !(defer && !moved) && uni32(j.plans[item].ccs) &&
+                xxh32_wave(j.decoded + d0, total, 0, xbuf) != uni32(j.plans[item].ccs_val))
                 ok = false;
         }
         uint32_t dcrc = 0;
@@ -3070,8 +3077,71 @@ __global__ __launch_bounds__(256) void k_decode_finish(DeviceJob j) {
             R->flags = R->flags | RPGPU_F_CODEC_OK;
             R->decoded_len = (uint32_t)total;
             R->decoded_crc = dcrc;
-            R->reserved0 = 1;  // decoded crc done (k_validate_decoded skips its CRC pass)
+            // decoded crc done (k_validate_decoded skips its CRC pass); OR'd:
+            // with defer, k_crc_compose ran before and set bit 1
+            R->reserved0 = (uint16_t)(R->reserved0 | 1u);
         }
+    }
+}
+
+// the content checksums k_decode_finish(defer) leaves: one wave per
+// checksummed frame whose pieces need no move (the same test as the
+// finish's: every piece decoded, each where the previous one ended), from
+// k_lz_exec's end, beside the rest of the decode stage.  The verdict goes to
+// FramePlan.xxh only (k_decode_finish writes the result beside it);
+// k_content_apply applies it after the join.  One wave per workgroup (1 KiB
+// of LDS): the few waves hashing a long frame hold their CUs for ~2 ms, and
+// k_crc_compose's 156 KiB workgroups and k_zexec's still fit beside one.
+#ifndef RPGPU_XXH_PRIO
+#define RPGPU_XXH_PRIO 1
+#endif
+__global__ __launch_bounds__(64) void k_content_xxh(DeviceJob j) {
+    __shared__ __attribute__((aligned(16))) uint8_t xb[1024];
+    lds_u8* xbuf = (lds_u8*)xb;
+    const uint32_t count = j.counters[2];
+    const uint32_t l = lane();
+    // first in issue on a shared SIMD (k_dchain, which waits on memory, is
+    // above it): beside k_decode_finish's waves at equal priority the chains
+    // ran ~1.4x their time alone
+    __builtin_amdgcn_s_setprio(RPGPU_XXH_PRIO);
+    for (;;) {
+        const uint32_t item = wave_fetch_add(&j.counters[44], 1u);
+        if (item >= count) break;
+        if (uni32(j.plans[item].mode) != 1u || uni32(j.plans[item].ccs) == 0u) continue;
+        const uint32_t b = uni32(j.decode_list[item]);
+        const uint32_t first = uni32(j.plans[item].first), nb = uni32(j.plans[item].nb);
+        const uint64_t d0 = uni64(j.dcap[b]);
+        uint64_t carry = 0;
+        uint32_t bad = 0;
+        for (uint32_t b0 = 0; b0 < nb; b0 += 64) {
+            const uint32_t k = b0 + l;
+            const int32_t out = k < nb ? (int32_t)j.blocks[first + k].out : 0;
+            const uint32_t o = out > 0 ? (uint32_t)out : 0u;
+            const uint32_t incl = wave_scan(o);
+            if (k < nb && (out < 0 || j.blocks[first + k].dst != d0 + carry + (incl - o))) bad = 1;
+            carry += rl(incl, 63);
+        }
+        if (wave_or(bad)) continue;  // moved (or failed): k_decode_finish's
+        if (uni32(j.plans[item].csf) && carry != uni64(j.plans[item].content_size)) continue;  // fails there
+        const uint32_t v = xxh32_wave(j.decoded + d0, carry, 0, xbuf) == uni32(j.plans[item].ccs_val) ? 1u : 2u;
+        if (l == 0) j.plans[item].xxh = v;
+    }
+}
+
+// after the join: a mismatched checksum restores what k_emit left in the
+// result (no CODEC_OK, decoded_len / decoded_crc 0, reserved0 bit 0 clear),
+// which is what k_decode_finish writes for such a frame without defer.
+// (k_dchain may have chained the frame's payload meanwhile: never read, its
+// verdict now fails dchain_ok.)
+__global__ __launch_bounds__(256) void k_content_apply(DeviceJob j) {
+    const uint32_t count = j.counters[2];
+    for (uint32_t item = blockIdx.x * blockDim.x + threadIdx.x; item < count; item += gridDim.x * blockDim.x) {
+        if (j.plans[item].xxh != 2u) continue;
+        rpgpu_batch_result* R = &j.batches[j.decode_list[item]];
+        R->flags = R->flags & ~(uint32_t)RPGPU_F_CODEC_OK;
+        R->decoded_len = 0;
+        R->decoded_crc = 0;
+        atomicAnd(reserved0_word(R), ~(1u << 16));
     }
 }
 
@@ -3475,8 +3545,16 @@ hipError_t launch_zexec(const DeviceJob& j, hipStream_t s) {
     return hipGetLastError();
 }
 
-hipError_t launch_decode_finish(const DeviceJob& j, hipStream_t s, uint32_t grid) {
-    hipLaunchKernelGGL(k_decode_finish, dim3(grid), dim3(256), 0, s, j);
+hipError_t launch_decode_finish(const DeviceJob& j, hipStream_t s, uint32_t grid, bool defer) {
+    hipLaunchKernelGGL(k_decode_finish, dim3(grid), dim3(256), 0, s, j, defer ? 1 : 0);
+    return hipGetLastError();
+}
+hipError_t launch_content_xxh(const DeviceJob& j, hipStream_t s, uint32_t grid) {
+    hipLaunchKernelGGL(k_content_xxh, dim3(grid), dim3(64), 0, s, j);
+    return hipGetLastError();
+}
+hipError_t launch_content_apply(const DeviceJob& j, hipStream_t s, uint32_t grid) {
+    hipLaunchKernelGGL(k_content_apply, dim3(grid), dim3(256), 0, s, j);
     return hipGetLastError();
 }
 

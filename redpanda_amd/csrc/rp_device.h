@@ -27,6 +27,13 @@ DEV uint32_t uni32(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane
 DEV uint64_t uni64(uint64_t v) {
     return (uint64_t)uni32((uint32_t)v) | ((uint64_t)uni32((uint32_t)(v >> 32)) << 32);
 }
+// the dword holding rpgpu_batch_result.reserved0 (its high half), for the
+// atomic bit updates of kernels that run side by side (k_crc_compose,
+// k_content_xxh)
+static_assert(offsetof(rpgpu_batch_result, reserved0) % 4 == 2, "reserved0 is the high half of a dword");
+DEV uint32_t* reserved0_word(rpgpu_batch_result* R) {
+    return (uint32_t*)((uint8_t*)R + offsetof(rpgpu_batch_result, reserved0) - 2);
+}
 
 // byte k (0..60) of a header whose bytes are spread one per lane
 DEV uint32_t hb(uint32_t b, int k) { return rl(b, k); }

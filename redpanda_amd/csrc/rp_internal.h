@@ -129,6 +129,8 @@ struct FramePlan {
     uint64_t content_size;  // LZ4F: content size (0 = absent)
     uint32_t ccs_val;       // LZ4F: stored content checksum
     uint32_t csf;           // LZ4F: content size present
+    uint32_t xxh;           // k_content_xxh's verdict: 0 not taken, 1 match, 2 mismatch
+    uint32_t pad;
 };
 
 // zstd members parsed into records (rp_inflate.hip zstd_fast_item): inf_state
@@ -326,7 +328,8 @@ hipError_t launch_chunk_base(const DeviceJob& j, hipStream_t s);
 hipError_t launch_discover(const DeviceJob& j, hipStream_t s);
 hipError_t launch_resolve(const DeviceJob& j, hipStream_t s);
 hipError_t launch_emit(const DeviceJob& j, hipStream_t s);
-hipError_t launch_validate(const DeviceJob& j, hipStream_t s, uint32_t grid);  // rp_validate.hip
+hipError_t launch_validate(const DeviceJob& j, hipStream_t s, uint32_t grid, bool compose = true);  // rp_validate.hip
+hipError_t launch_crc_compose(const DeviceJob& j, hipStream_t s, uint32_t grid);
 bool dchain_wanted(const DeviceJob& j);                                         // rp_validate.hip
 hipError_t launch_dchain(const DeviceJob& j, hipStream_t s, uint32_t grid);
 hipError_t launch_validate_decoded(const DeviceJob& j, hipStream_t s, uint32_t grid);
@@ -337,7 +340,9 @@ hipError_t launch_lz_walk(const DeviceJob& j, hipStream_t s, uint32_t grid);
 hipError_t launch_lz_exec(const DeviceJob& j, hipStream_t s);
 hipError_t launch_raw_copy(const DeviceJob& j, hipStream_t s, uint32_t cus);
 hipError_t launch_lzf_walk(const DeviceJob& j, hipStream_t s, uint32_t cus);
-hipError_t launch_decode_finish(const DeviceJob& j, hipStream_t s, uint32_t grid);
+hipError_t launch_decode_finish(const DeviceJob& j, hipStream_t s, uint32_t grid, bool defer = false);
+hipError_t launch_content_xxh(const DeviceJob& j, hipStream_t s, uint32_t grid);  // k_decode_finish(defer)'s checksums
+hipError_t launch_content_apply(const DeviceJob& j, hipStream_t s, uint32_t grid);  // their mismatches, after the join
 // gzip members (rp_inflate.hip): first pass (into scratch) before the slot
 // scans, then the copy into the arena and the second pass where needed
 hipError_t launch_inflate_plan(const DeviceJob& j, hipStream_t s, uint32_t grid, int pass = 0);

@@ -999,6 +999,15 @@ int submit_body(rpgpu_ctx* c, const rpgpu_job* job, hipStream_t s, int stop, Pla
     if (job->flags & RPGPU_JOB_DECODE) STAGE("scan_dcap", scan_exclusive_u64_devn(j.dcap, d_nb, bcap, scan_tmp, s));
     if (stop == kStopAfterPlan) return RPGPU_OK;
     if (tm) HIPCHK(c, hipEventRecord(ev[2], s));
+    // k_content_xxh's side stream (below) joins s on every return, error paths too
+    struct SideJoin {
+        hipStream_t s = nullptr, side = nullptr;
+        hipEvent_t ev = nullptr;
+        ~SideJoin() {
+            if (side && hipEventRecord(ev, side) == hipSuccess) hipStreamWaitEvent(s, ev, 0);
+        }
+    } xjoin;
+    bool xside = false;
     // decode first: k_validate checksums and walks the decoded payloads
     if ((job->flags & RPGPU_JOB_DECODE) && j.decoded) {
         STAGE("decode", launch_decode(j, s, c->cu_count * 8));
@@ -1071,22 +1080,54 @@ int submit_body(rpgpu_ctx* c, const rpgpu_job* job, hipStream_t s, int stop, Pla
             if (raw_serial) STAGE("raw_copy", launch_raw_copy(j, s, c->cu_count));
         }
         STAGE("lz_exec", launch_lz_exec(j, s));
-        STAGE("decode_finish", launch_decode_finish(j, s, c->cu_count * 8));
+        // RPGPU_XXH_SIDE=0 (diagnostic build): the content checksums inside
+        // k_decode_finish, k_crc_compose and k_dchain in the validate stage (A/B)
+        static const bool xxh_side = [] { const char* e = diag_env("RPGPU_XXH_SIDE"); return !(e && *e == '0'); }();
+        xside = xxh_side;
+        // the gzip / zstd members first: k_zexec's workgroups take a CU's
+        // registers each and did not fit beside k_content_xxh's waves
         STAGE("inflate", launch_inflate(j, s, c->cu_count * 4));
         STAGE("zexec", launch_zexec(j, s));
         STAGE("zexact", launch_zexact(j, s, 1));
         if (c->hc_n) STAGE("host_scatter", launch_host_scatter(j, (const HostItem*)c->hc_items.p, c->hc_n,
                                                                (const uint8_t*)c->hc_out.p, s));
+        if (xside) {
+            // k_crc_compose (no dependence on the decoded bytes) before the
+            // fork, for the same reason.  Then the LZ4F content checksums
+            // (serial XXH32 chains, ~1 ms per MiB on one wave each: the rest
+            // of the chip idles) on the side stream beside k_decode_finish
+            // and the decoded payloads' record chains, which do not depend on
+            // them (k_decode_finish gives a checksummed frame its verdict as
+            // if it matched; k_content_apply takes it back after the join)
+            STAGE("crc_compose", launch_crc_compose(j, s, c->cu_count));
+            if (!c->side) HIPCHK(c, side_stream_create(&c->side));
+            if (!c->fork_ev) HIPCHK(c, hipEventCreateWithFlags(&c->fork_ev, hipEventDisableTiming));
+            if (!c->join_ev) HIPCHK(c, hipEventCreateWithFlags(&c->join_ev, hipEventDisableTiming));
+            HIPCHK(c, hipEventRecord(c->fork_ev, s));
+            HIPCHK(c, hipStreamWaitEvent(c->side, c->fork_ev, 0));
+            xjoin.s = s;
+            xjoin.ev = c->join_ev;
+            xjoin.side = c->side;
+            STAGE("content_xxh", launch_content_xxh(j, c->side, c->cu_count * 4));
+        }
+        STAGE("decode_finish", launch_decode_finish(j, s, c->cu_count * 8, xside));
+        if (xside) {
+            STAGE("dchain", launch_dchain(j, s, c->cu_count));
+            HIPCHK(c, hipEventRecord(c->join_ev, c->side));
+            HIPCHK(c, hipStreamWaitEvent(s, c->join_ev, 0));
+            xjoin.side = nullptr;  // joined
+            STAGE("content_apply", launch_content_apply(j, s, c->cu_count));
+        }
     }
     // RPGPU_WALK_WGS (diagnostic build): k_walk's grid (workgroups per CU)
     static const uint32_t walk_wgs = [] { const char* e = diag_env("RPGPU_WALK_WGS"); return e ? (uint32_t)atoi(e) : 8u; }();
     if (tm) HIPCHK(c, hipEventRecord(ev[3], s));
-    STAGE("validate", launch_validate(j, s, c->cu_count));
+    STAGE("validate", launch_validate(j, s, c->cu_count, !xside));
     // the decoded payloads' record chains, then their walk.  (k_dchain on the
     // side stream beside k_crc_compose / k_validate measured slower than here:
     // C2 validate stage 4.36 against 3.72 ms, the chains' serial loads
     // queueing behind the two streams' HBM traffic)
-    STAGE("dchain", launch_dchain(j, s, c->cu_count));
+    if (!xside) STAGE("dchain", launch_dchain(j, s, c->cu_count));
     STAGE("validate_decoded", launch_validate_decoded(j, s, c->cu_count));
     if (tm) HIPCHK(c, hipEventRecord(ev[4], s));
     STAGE("walk", launch_walk(j, s, c->cu_count * walk_wgs));

@@ -1509,7 +1509,14 @@ __global__ __launch_bounds__(1024) void k_crc_compose(DeviceJob j) {
 // 0xFFFFFFFF where it stops (a start at or past the end, a bad length);
 // written at the payload's index slots of the record pool (j.dchain), read
 // back 64 at a time by walk_records (pre_starts).
+#ifndef RPGPU_DCHAIN_PRIO
+#define RPGPU_DCHAIN_PRIO 2
+#endif
 __global__ __launch_bounds__(256) void k_dchain(DeviceJob j) {
+    // above k_content_xxh's waves on a shared SIMD: an XXH32 chain keeps the
+    // SIMD's VALU busy back to back (its quarter-rate multiply per stripe), and
+    // a chain lane waiting behind it held k_dchain's end with it (0.9 -> 1.9 ms)
+    __builtin_amdgcn_s_setprio(RPGPU_DCHAIN_PRIO);
     const uint32_t nlz = j.counters[2], ngz = j.counters[16], count = nlz + ngz + j.counters[19];
     const uint8_t* const aend = j.decoded + j.decoded_capacity;
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < count; i += gridDim.x * blockDim.x) {
@@ -1863,7 +1870,14 @@ hipError_t launch_walk(const DeviceJob& j, hipStream_t s, uint32_t grid) {
     return hipGetLastError();
 }
 
-hipError_t launch_validate(const DeviceJob& j, hipStream_t s, uint32_t grid) {
+hipError_t launch_crc_compose(const DeviceJob& j, hipStream_t s, uint32_t grid) {
+    (void)hipFuncSetAttribute((const void*)k_crc_compose, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsValidateBytes);
+    if (j.crc_compose && (j.flags & RPGPU_JOB_DECODE) && j.decoded && j.raw_list && j.layout == RPGPU_LAYOUT_DISK)
+        hipLaunchKernelGGL(k_crc_compose, dim3(grid), dim3(64 * kVWaves), kLdsValidateBytes, s, j);
+    return hipGetLastError();
+}
+
+hipError_t launch_validate(const DeviceJob& j, hipStream_t s, uint32_t grid, bool compose) {
     static bool attr = false;
     if (!attr) {
         (void)hipFuncSetAttribute((const void*)k_validate, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsValidateBytes);
@@ -1875,7 +1889,7 @@ hipError_t launch_validate(const DeviceJob& j, hipStream_t s, uint32_t grid) {
                                   kLdsValidateBytes);
         attr = true;
     }
-    if (j.crc_compose && (j.flags & RPGPU_JOB_DECODE) && j.decoded && j.raw_list && j.layout == RPGPU_LAYOUT_DISK)
+    if (compose && j.crc_compose && (j.flags & RPGPU_JOB_DECODE) && j.decoded && j.raw_list && j.layout == RPGPU_LAYOUT_DISK)
         hipLaunchKernelGGL(k_crc_compose, dim3(grid), dim3(64 * kVWaves), kLdsValidateBytes, s, j);
     hipLaunchKernelGGL(k_validate, dim3(grid), dim3(64 * kVWaves), kLdsValidateBytes, s, j);
 #ifdef RPGPU_STAMPS
