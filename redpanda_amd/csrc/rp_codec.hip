@@ -3089,15 +3089,15 @@ __global__ __launch_bounds__(256) void k_decode_finish(DeviceJob j, int defer) {
 // finish's: every piece decoded, each where the previous one ended), from
 // k_lz_exec's end, beside the rest of the decode stage.  The verdict goes to
 // FramePlan.xxh only (k_decode_finish writes the result beside it);
-// k_content_apply applies it after the join.  One wave per workgroup (1 KiB
-// of LDS): the few waves hashing a long frame hold their CUs for ~2 ms, and
-// k_crc_compose's 156 KiB workgroups and k_zexec's still fit beside one.
+// k_content_apply applies it after the join.  Four waves per workgroup, one
+// per SIMD: with one-wave workgroups two hashing waves could share a SIMD,
+// each at half speed (the longest hash 2.0 -> 2.95 ms).
 #ifndef RPGPU_XXH_PRIO
 #define RPGPU_XXH_PRIO 1
 #endif
-__global__ __launch_bounds__(64) void k_content_xxh(DeviceJob j) {
-    __shared__ __attribute__((aligned(16))) uint8_t xb[1024];
-    lds_u8* xbuf = (lds_u8*)xb;
+__global__ __launch_bounds__(256) void k_content_xxh(DeviceJob j) {
+    __shared__ __attribute__((aligned(16))) uint8_t xb[4][1024];
+    lds_u8* xbuf = (lds_u8*)xb[threadIdx.x >> 6];
     const uint32_t count = j.counters[2];
     const uint32_t l = lane();
     // first in issue on a shared SIMD (k_dchain, which waits on memory, is
@@ -3550,7 +3550,7 @@ hipError_t launch_decode_finish(const DeviceJob& j, hipStream_t s, uint32_t grid
     return hipGetLastError();
 }
 hipError_t launch_content_xxh(const DeviceJob& j, hipStream_t s, uint32_t grid) {
-    hipLaunchKernelGGL(k_content_xxh, dim3(grid), dim3(64), 0, s, j);
+    hipLaunchKernelGGL(k_content_xxh, dim3(grid), dim3(256), 0, s, j);
     return hipGetLastError();
 }
 hipError_t launch_content_apply(const DeviceJob& j, hipStream_t s, uint32_t grid) {

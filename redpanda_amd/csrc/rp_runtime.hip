@@ -1108,7 +1108,7 @@ int submit_body(rpgpu_ctx* c, const rpgpu_job* job, hipStream_t s, int stop, Pla
             xjoin.s = s;
             xjoin.ev = c->join_ev;
             xjoin.side = c->side;
-            STAGE("content_xxh", launch_content_xxh(j, c->side, c->cu_count * 4));
+            STAGE("content_xxh", launch_content_xxh(j, c->side, c->cu_count * 2));
         }
         STAGE("decode_finish", launch_decode_finish(j, s, c->cu_count * 8, xside));
         if (xside) {
