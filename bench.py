@@ -60,8 +60,10 @@ HOST_GROUP_BYTES = 256 << 20
 # index writes 48 B per record, result 64 B per batch
 IDX_BYTES_PER_RECORD = 48
 RESULT_BYTES_PER_BATCH = 64
+# (since round 6 the decode stage also holds k_crc_compose, the side-stream
+# content checksums and k_dchain, which ran in the validate stage before)
 DECODE_KERNELS = ("k_decode", "k_decode_blocks", "k_lzf_walk", "k_lzf_tail", "k_raw_copy", "k_lz_walk", "k_lz_exec",
-                  "k_decode_finish")
+                  "k_decode_finish", "k_crc_compose", "k_content_xxh", "k_dchain", "k_content_apply")
 MEMBER_KERNELS = ("k_gzsplan", "k_gzsfind", "k_gzsdecode", "k_gzsresolve", "k_members_first", "k_zplan", "k_zlits",
                   "k_zparse", "k_zfallback", "k_zexec", "k_members", "k_inflate_copy")
 # segment-summary fields that do not depend on where a partition sits in a job
@@ -435,7 +437,7 @@ def run_compressed(name, kw, n_parts, seg_bytes, args, plat, eng, abi, desc, ext
     tm = eng.last_timings()
     eng.set_timing(False)
     dec_ms = tm["decode"]
-    # decode stage (k_decode .. k_decode_finish): compressed payload read
+    # decode stage (k_decode .. k_content_apply): compressed payload read
     # once + decoded bytes written once
     dec_alg = comp_in + decoded
     # whole pipeline, SURVEY §8(d) C2/C5 bytes per unit: every stored byte
@@ -479,7 +481,7 @@ def run_compressed(name, kw, n_parts, seg_bytes, args, plat, eng, abi, desc, ext
         "stage_ms": {k: round(v, 4) for k, v in tm.items()},
         "roofline": {
             "bound": "hbm",
-            "kernel": "decode stage (k_decode .. k_decode_finish)",
+            "kernel": "decode stage (k_decode .. k_content_apply)",
             "achieved": round(dec_alg / (dec_ms * 1e-3) / 1e9, 1) if dec_ms > 0 else None,
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
