@@ -329,7 +329,7 @@ hipError_t launch_discover(const DeviceJob& j, hipStream_t s);
 hipError_t launch_resolve(const DeviceJob& j, hipStream_t s);
 hipError_t launch_emit(const DeviceJob& j, hipStream_t s);
 hipError_t launch_validate(const DeviceJob& j, hipStream_t s, uint32_t grid, bool compose = true);  // rp_validate.hip
-hipError_t launch_crc_compose(const DeviceJob& j, hipStream_t s, uint32_t grid);
+hipError_t launch_crc_compose(const DeviceJob& j, hipStream_t s, uint32_t grid, uint32_t waves = 16);
 bool dchain_wanted(const DeviceJob& j);                                         // rp_validate.hip
 hipError_t launch_dchain(const DeviceJob& j, hipStream_t s, uint32_t grid);
 hipError_t launch_validate_decoded(const DeviceJob& j, hipStream_t s, uint32_t grid);

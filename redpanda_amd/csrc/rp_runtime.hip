@@ -1099,7 +1099,10 @@ int submit_body(rpgpu_ctx* c, const rpgpu_job* job, hipStream_t s, int stop, Pla
             // and the decoded payloads' record chains, which do not depend on
             // them (k_decode_finish gives a checksummed frame its verdict as
             // if it matched; k_content_apply takes it back after the join)
-            STAGE("crc_compose", launch_crc_compose(j, s, c->cu_count));
+            // RPGPU_COMPOSE_BESIDE=1 (diagnostic build): k_crc_compose after the
+            // fork, 8 waves per workgroup (room for a hashing wave per SIMD) (A/B)
+            static const bool compose_beside = [] { const char* e = diag_env("RPGPU_COMPOSE_BESIDE"); return e && *e == '1'; }();
+            if (!compose_beside) STAGE("crc_compose", launch_crc_compose(j, s, c->cu_count));
             if (!c->side) HIPCHK(c, side_stream_create(&c->side));
             if (!c->fork_ev) HIPCHK(c, hipEventCreateWithFlags(&c->fork_ev, hipEventDisableTiming));
             if (!c->join_ev) HIPCHK(c, hipEventCreateWithFlags(&c->join_ev, hipEventDisableTiming));
@@ -1109,6 +1112,7 @@ int submit_body(rpgpu_ctx* c, const rpgpu_job* job, hipStream_t s, int stop, Pla
             xjoin.ev = c->join_ev;
             xjoin.side = c->side;
             STAGE("content_xxh", launch_content_xxh(j, c->side, c->cu_count * 2));
+            if (compose_beside) STAGE("crc_compose", launch_crc_compose(j, s, c->cu_count, 8));
         }
         STAGE("decode_finish", launch_decode_finish(j, s, c->cu_count * 8, xside));
         if (xside) {

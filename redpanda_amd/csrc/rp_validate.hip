@@ -1870,10 +1870,10 @@ hipError_t launch_walk(const DeviceJob& j, hipStream_t s, uint32_t grid) {
     return hipGetLastError();
 }
 
-hipError_t launch_crc_compose(const DeviceJob& j, hipStream_t s, uint32_t grid) {
+hipError_t launch_crc_compose(const DeviceJob& j, hipStream_t s, uint32_t grid, uint32_t waves) {
     (void)hipFuncSetAttribute((const void*)k_crc_compose, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsValidateBytes);
     if (j.crc_compose && (j.flags & RPGPU_JOB_DECODE) && j.decoded && j.raw_list && j.layout == RPGPU_LAYOUT_DISK)
-        hipLaunchKernelGGL(k_crc_compose, dim3(grid), dim3(64 * kVWaves), kLdsValidateBytes, s, j);
+        hipLaunchKernelGGL(k_crc_compose, dim3(grid), dim3(64 * waves), kLdsValidateBytes, s, j);
     return hipGetLastError();
 }
 
